@@ -1,0 +1,63 @@
+"""Synthetic verify workloads (BASELINE.json configs C1-C5), repo-owned.
+
+The validity mix follows SURVEY.md 8(d) (config 2): per signature a seeded
+roll picks one of
+  10% single random bit flip in the 512-bit signature
+   2% S += L                      (S >= L, rejected by fd_curve25519_scalar_validate)
+   2% A = one of the 8 small-order encodings   (fd_curve25519.h:91-98)
+   2% R = one of the 8 small-order encodings
+   2% non-canonical A: y in [p, p+18], sign bit kept
+   2% non-canonical R: y in [p, p+18], sign bit kept
+   1% public-key bit flip
+  79% untouched (valid)
+"""
+import numpy as np
+
+P_INT = 2**255 - 19
+L_INT = 2**252 + 27742317777372353535851937790883648493
+
+SMALL_ORDER_ENCODINGS = [bytes.fromhex(h) for h in (
+    "0100000000000000000000000000000000000000000000000000000000000000",
+    "ecffffffffffffffffffffffffffffffffffffffffffffffffffffffffffff7f",
+    "0000000000000000000000000000000000000000000000000000000000000000",
+    "0000000000000000000000000000000000000000000000000000000000000080",
+    "26e8958fc2b227b045c3f489f2ef98f0d5dfac05d3c63339b13802886d53fc05",
+    "26e8958fc2b227b045c3f489f2ef98f0d5dfac05d3c63339b13802886d53fc85",
+    "c7176a703d4dd84fba3c0b760d10670f2a2053fa2c39ccc64ec7fd7792ac037a",
+    "c7176a703d4dd84fba3c0b760d10670f2a2053fa2c39ccc64ec7fd7792ac03fa",
+)]
+
+KIND_VALID, KIND_SIGFLIP, KIND_S_GE_L, KIND_A_SMALL, KIND_R_SMALL, KIND_A_NONCANON, KIND_R_NONCANON, KIND_PUBFLIP = range(8)
+_EDGES = np.array([0.10, 0.12, 0.14, 0.16, 0.18, 0.20, 0.21])
+_KIND_OF_BIN = np.array([KIND_SIGFLIP, KIND_S_GE_L, KIND_A_SMALL, KIND_R_SMALL, KIND_A_NONCANON,
+                         KIND_R_NONCANON, KIND_PUBFLIP, KIND_VALID], np.uint8)
+
+
+def _noncanon(orig32, k):
+    y = P_INT + int(k)                                   # in [p, p+18] < 2^255
+    b = bytearray(y.to_bytes(32, "little"))
+    b[31] |= orig32[31] & 0x80                            # keep the sign bit
+    return np.frombuffer(bytes(b), np.uint8)
+
+
+def c2_mutate(sigs, pubs, rng):
+    """Mutate (n,64) sigs and (n,32) pubs in place; return the per-record kind."""
+    n = sigs.shape[0]
+    kinds = _KIND_OF_BIN[np.searchsorted(_EDGES, rng.random(n), side="right")]
+    idx = np.nonzero(kinds == KIND_SIGFLIP)[0]
+    bits = rng.integers(0, 512, size=idx.size)
+    sigs[idx, bits >> 3] ^= (1 << (bits & 7)).astype(np.uint8)
+    for i in np.nonzero(kinds == KIND_S_GE_L)[0]:
+        s = int.from_bytes(sigs[i, 32:].tobytes(), "little") + L_INT
+        sigs[i, 32:] = np.frombuffer(s.to_bytes(32, "little"), np.uint8)
+    so = np.frombuffer(b"".join(SMALL_ORDER_ENCODINGS), np.uint8).reshape(8, 32)
+    idx = np.nonzero(kinds == KIND_A_SMALL)[0]; pubs[idx] = so[rng.integers(0, 8, idx.size)]
+    idx = np.nonzero(kinds == KIND_R_SMALL)[0]; sigs[idx, :32] = so[rng.integers(0, 8, idx.size)]
+    for i in np.nonzero(kinds == KIND_A_NONCANON)[0]:
+        pubs[i] = _noncanon(pubs[i], rng.integers(0, 19))
+    for i in np.nonzero(kinds == KIND_R_NONCANON)[0]:
+        sigs[i, :32] = _noncanon(sigs[i, :32], rng.integers(0, 19))
+    idx = np.nonzero(kinds == KIND_PUBFLIP)[0]
+    bits = rng.integers(0, 256, size=idx.size)
+    pubs[idx, bits >> 3] ^= (1 << (bits & 7)).astype(np.uint8)
+    return kinds
