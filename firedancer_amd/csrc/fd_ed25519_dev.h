@@ -1,0 +1,447 @@
+/* fd_ed25519_dev.h -- device-side building blocks of the gfx950 ed25519
+   verify engine: GF(2^255-19) helpers on top of the generated fe25519_asm.h,
+   extended-coordinate group law, point decode, SHA-512 and scalar mod L.
+
+   Every function restates the semantics of the reference verify path
+   (anoushk1234/firedancer src/ballet/ed25519/, cited per function); the
+   arithmetic is organised for one signature per 64-wide-wave lane with
+   8x32-bit limbs (see gen_fe_asm.py for the limb/bound conventions:
+   "loose" < 2^256, "tight" < 2^255 + 2^43). */
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include "fe25519_asm.h"
+
+typedef uint32_t u32;
+typedef uint64_t u64;
+typedef uint8_t  u8;
+
+#define DEV __device__ __forceinline__
+
+/**********************************************************************/
+/* Field elements                                                      */
+
+struct fe { u32 v[8]; };
+
+DEV void fe_set( fe & r, u32 c0, u32 c1, u32 c2, u32 c3, u32 c4, u32 c5, u32 c6, u32 c7 ) {
+  r.v[0]=c0; r.v[1]=c1; r.v[2]=c2; r.v[3]=c3; r.v[4]=c4; r.v[5]=c5; r.v[6]=c6; r.v[7]=c7;
+}
+DEV void fe_0( fe & r ) { fe_set( r, 0,0,0,0,0,0,0,0 ); }
+DEV void fe_1( fe & r ) { fe_set( r, 1,0,0,0,0,0,0,0 ); }
+/* d = -121665/121666, 2d, sqrt(-1): fd_f25519_table_ref.c:28-47 */
+DEV void fe_d( fe & r )      { fe_set( r, 0x135978a3u,0x75eb4dcau,0x4141d8abu,0x00700a4du,0x7779e898u,0x8cc74079u,0x2b6ffe73u,0x52036ceeu ); }
+DEV void fe_d2( fe & r )     { fe_set( r, 0x26b2f159u,0xebd69b94u,0x8283b156u,0x00e0149au,0xeef3d130u,0x198e80f2u,0x56dffce7u,0x2406d9dcu ); }
+DEV void fe_sqrtm1( fe & r ) { fe_set( r, 0x4a0ea0b0u,0xc4ee1b27u,0xad2fe478u,0x2f431806u,0x3dfbd7a7u,0x2b4d0099u,0x4fc1df0bu,0x2b832480u ); }
+
+DEV void fe_mul( fe & r, fe const & a, fe const & b ) { fe_mul( r.v, a.v, b.v ); }
+DEV void fe_sq ( fe & r, fe const & a )               { fe_mul( r.v, a.v, a.v ); }
+DEV void fe_add( fe & r, fe const & a, fe const & b ) { fe_add( r.v, a.v, b.v ); }
+DEV void fe_sub( fe & r, fe const & a, fe const & b ) { fe_sub( r.v, a.v, b.v ); }
+
+DEV void fe_sqn( fe & r, fe const & a, int n ) {
+  fe_sq( r, a );
+  #pragma unroll 1
+  for( int i=1; i<n; i++ ) fe_sq( r, r );
+}
+
+/* loose (< 2^256) -> canonical [0,p).  Fold bit 255 with 19, then subtract
+   p once if needed (t = v+19 >= 2^255  <=>  v >= p). */
+DEV void fe_canon( fe & r, fe const & a ) {
+  u32 top = a.v[7] >> 31;
+  u64 c = (u64)a.v[0] + 19u*top;
+  u32 v[8];
+  v[0] = (u32)c; c >>= 32;
+  #pragma unroll
+  for( int i=1; i<7; i++ ) { c += a.v[i]; v[i] = (u32)c; c >>= 32; }
+  v[7] = (u32)(c + (a.v[7] & 0x7fffffffu));
+  /* now v < 2^255 + 19; t = v + 19 */
+  u32 t[8]; c = (u64)v[0] + 19u;
+  t[0] = (u32)c; c >>= 32;
+  #pragma unroll
+  for( int i=1; i<8; i++ ) { c += v[i]; t[i] = (u32)c; c >>= 32; }
+  u32 ge = t[7] >> 31;                      /* v >= p */
+  u32 m = 0u - ge;
+  t[7] &= 0x7fffffffu;
+  #pragma unroll
+  for( int i=0; i<8; i++ ) r.v[i] = (t[i] & m) | (v[i] & ~m);
+}
+
+DEV bool fe_is_zero_c( fe const & c ) {   /* c canonical */
+  return (c.v[0]|c.v[1]|c.v[2]|c.v[3]|c.v[4]|c.v[5]|c.v[6]|c.v[7]) == 0u;
+}
+DEV bool fe_eq_c( fe const & a, fe const & b ) {   /* both canonical */
+  return ((a.v[0]^b.v[0])|(a.v[1]^b.v[1])|(a.v[2]^b.v[2])|(a.v[3]^b.v[3])|
+          (a.v[4]^b.v[4])|(a.v[5]^b.v[5])|(a.v[6]^b.v[6])|(a.v[7]^b.v[7])) == 0u;
+}
+DEV bool fe_is_zero( fe const & a ) { fe c; fe_canon( c, a ); return fe_is_zero_c( c ); }
+
+/* r = -a for tight a (result loose) */
+DEV void fe_neg( fe & r, fe const & a ) { fe z; fe_0( z ); fe_sub( r, z, a ); }
+
+/* conditional swap (mask is 0 or ~0 per lane) */
+DEV void fe_cswap( fe & a, fe & b, u32 mask ) {
+  #pragma unroll
+  for( int i=0; i<8; i++ ) { u32 t = (a.v[i] ^ b.v[i]) & mask; a.v[i] ^= t; b.v[i] ^= t; }
+}
+DEV void fe_cmov( fe & r, fe const & a, u32 mask ) {   /* r = mask ? a : r */
+  #pragma unroll
+  for( int i=0; i<8; i++ ) r.v[i] ^= (r.v[i] ^ a.v[i]) & mask;
+}
+
+/* z^(2^252-3): fd_f25519.c:25-74 (same exponent; this addition chain) */
+DEV void fe_pow22523( fe & out, fe const & z ) {
+  fe z2, z9, z11, a, b, c, t;
+  fe_sq( z2, z );                         /* 2 */
+  fe_sqn( t, z2, 2 ); fe_mul( z9, t, z ); /* 9 */
+  fe_mul( z11, z9, z2 );                  /* 11 */
+  fe_sq( t, z11 ); fe_mul( a, t, z9 );    /* a = z^(2^5-1) */
+  fe_sqn( t, a, 5 );   fe_mul( b, t, a ); /* 2^10-1 */
+  fe_sqn( t, b, 10 );  fe_mul( c, t, b ); /* 2^20-1 */
+  fe_sqn( t, c, 20 );  fe_mul( t, t, c ); /* 2^40-1 */
+  fe_sqn( t, t, 10 );  fe_mul( b, t, b ); /* b = 2^50-1 */
+  fe_sqn( t, b, 50 );  fe_mul( c, t, b ); /* c = 2^100-1 */
+  fe_sqn( t, c, 100 ); fe_mul( t, t, c ); /* 2^200-1 */
+  fe_sqn( t, t, 50 );  fe_mul( t, t, b ); /* 2^250-1 */
+  fe_sqn( t, t, 2 );   fe_mul( out, t, z );  /* 2^252-3 */
+}
+
+/* z^(p-2) = (z^(2^252-3))^8 * z^3 */
+DEV void fe_invert( fe & out, fe const & z ) {
+  fe a, z3;
+  fe_pow22523( a, z ); fe_sqn( a, a, 3 );
+  fe_sq( z3, z ); fe_mul( z3, z3, z );
+  fe_mul( out, a, z3 );
+}
+
+/* 32 little-endian bytes (as 8 LE u32 words) -> fe, masking bit 255
+   (fd_f25519.h frombytes accepts non-canonical y in [p, 2^255)) */
+DEV void fe_from_words( fe & r, u32 const w[8] ) {
+  #pragma unroll
+  for( int i=0; i<7; i++ ) r.v[i] = w[i];
+  r.v[7] = w[7] & 0x7fffffffu;
+}
+
+/**********************************************************************/
+/* Group: twisted Edwards a=-1, extended coordinates, HWCD'08 formulas
+   (ref/fd_curve25519.c:25-92 add, ref/fd_curve25519.h:190-211 dbl).     */
+
+struct ge_p3     { fe X, Y, Z, T; };
+struct ge_cached { fe YmX, YpX, T2d, Z2; };   /* (Y-X, Y+X, 2d*T, 2*Z) */
+struct ge_affc   { fe YmX, YpX, T2d; };       /* Z == 1 */
+
+DEV void ge_identity( ge_p3 & r ) { fe_0( r.X ); fe_1( r.Y ); fe_1( r.Z ); fe_0( r.T ); }
+
+/* r = 2p.  partial_dbl + final mul; T produced only when asked. */
+DEV void ge_dbl( ge_p3 & r, ge_p3 const & p, bool needT ) {
+  fe A, B, C, S, Tp, Zp, Yp, Xp;
+  fe_add( S, p.X, p.Y );
+  fe_sq( A, p.X ); fe_sq( B, p.Y ); fe_sq( C, p.Z ); fe_sq( S, S );
+  fe_add( C, C, C );          /* 2Z^2            tight */
+  fe_add( Tp, A, B );         /* A+B             tight */
+  fe_sub( Zp, A, B );         /* A-B             loose */
+  fe_add( Yp, C, Zp );        /* 2Z^2+A-B        tight */
+  fe_sub( Xp, Tp, S );        /* A+B-(X+Y)^2     loose */
+  fe_mul( r.X, Xp, Yp );
+  fe_mul( r.Y, Zp, Tp );
+  fe_mul( r.Z, Yp, Zp );
+  if( needT ) fe_mul( r.T, Xp, Tp );
+}
+
+/* r = p +/- q (q in cached form).  neg is a per-lane mask (0 or ~0). */
+DEV void ge_add_cached( ge_p3 & r, ge_p3 const & p, ge_cached q, u32 neg, bool needT ) {
+  fe a, b, A, B, C, D, E, F, G, H;
+  fe_cswap( q.YmX, q.YpX, neg );           /* -q: swap Y-X / Y+X ... */
+  fe_sub( a, p.Y, p.X ); fe_add( b, p.Y, p.X );
+  fe_mul( A, a, q.YmX ); fe_mul( B, b, q.YpX );
+  fe_mul( C, p.T, q.T2d ); fe_mul( D, p.Z, q.Z2 );
+  fe_sub( E, B, A ); fe_add( H, B, A );
+  fe_sub( F, D, C ); fe_add( G, D, C );
+  fe_cswap( F, G, neg );                   /* ... and negate 2dT: C -> -C swaps F and G */
+  fe_mul( r.X, E, F ); fe_mul( r.Y, G, H ); fe_mul( r.Z, F, G );
+  if( needT ) fe_mul( r.T, E, H );
+}
+
+/* r = p +/- q with q affine (Z == 1): D = 2*Z1 */
+DEV void ge_add_affc( ge_p3 & r, ge_p3 const & p, ge_affc q, u32 neg, bool needT ) {
+  fe a, b, A, B, C, D, E, F, G, H;
+  fe_cswap( q.YmX, q.YpX, neg );
+  fe_sub( a, p.Y, p.X ); fe_add( b, p.Y, p.X );
+  fe_mul( A, a, q.YmX ); fe_mul( B, b, q.YpX );
+  fe_mul( C, p.T, q.T2d ); fe_add( D, p.Z, p.Z );
+  fe_sub( E, B, A ); fe_add( H, B, A );
+  fe_sub( F, D, C ); fe_add( G, D, C );
+  fe_cswap( F, G, neg );
+  fe_mul( r.X, E, F ); fe_mul( r.Y, G, H ); fe_mul( r.Z, F, G );
+  if( needT ) fe_mul( r.T, E, H );
+}
+
+/* fd_curve25519_into_precomputed (ref/fd_curve25519.h:141-151) with Z doubled */
+DEV void ge_to_cached( ge_cached & c, ge_p3 const & p ) {
+  fe d2; fe_d2( d2 );
+  fe_sub( c.YmX, p.Y, p.X ); fe_add( c.YpX, p.Y, p.X );
+  fe_mul( c.T2d, p.T, d2 );  fe_add( c.Z2, p.Z, p.Z );
+}
+
+/* Point decompression: fd_curve25519.c:34-61 + fd_f25519.c:122-158, with the
+   AVX-512 backend's failure split (avx512/fd_r43x6_ge.c:163-254).
+   Returns bit0 = not on curve (u/v not a square), bit1 = x==0 with sign bit
+   set (AVX-512 rejects in decode; the ref backend keeps x=0 and rejects it
+   as small order).  On success r = (x, y, 1, xy) with x, y canonical. */
+DEV u32 ge_decode( ge_p3 & r, u32 const w[8] ) {
+  fe y, y2, u, v, v3, v7, t, x, chk, one, d;
+  u32 sign = w[7] >> 31;
+  fe_from_words( y, w );
+  fe_1( one ); fe_d( d );
+  fe_sq( y2, y );
+  fe_sub( u, y2, one );                 /* u = y^2 - 1 */
+  fe_mul( v, y2, d ); fe_add( v, v, one ); /* v = d y^2 + 1 */
+  fe_sq( v3, v ); fe_mul( v3, v3, v );  /* v^3 */
+  fe_sq( v7, v3 ); fe_mul( v7, v7, v ); /* v^7 */
+  fe_mul( t, u, v7 ); fe_pow22523( t, t );
+  fe_mul( x, u, v3 ); fe_mul( x, x, t ); /* x = u v^3 (u v^7)^((p-5)/8) */
+  fe_sq( chk, x ); fe_mul( chk, chk, v ); /* v x^2 */
+  fe cu, cc, nu;
+  fe_canon( cu, u ); fe_canon( cc, chk );
+  fe_neg( nu, cu ); fe_canon( nu, nu );
+  bool ok1 = fe_eq_c( cc, cu );
+  bool ok2 = fe_eq_c( cc, nu );
+  fe xs, sq; fe_sqrtm1( sq ); fe_mul( xs, x, sq );
+  fe_cmov( x, xs, ok1 ? 0u : ~0u );     /* v x^2 == -u: x *= sqrt(-1) */
+  fe_canon( x, x );
+  u32 xz = fe_is_zero_c( x ) ? 1u : 0u;
+  u32 flags = ((ok1 || ok2) ? 0u : 1u) | ((xz & sign) << 1);
+  /* choose the root with parity == sign (neg(0) stays 0) */
+  fe nx; fe_neg( nx, x ); fe_canon( nx, nx );
+  fe_cmov( x, nx, ((x.v[0] & 1u) != sign) ? ~0u : 0u );
+  fe_canon( r.Y, y );
+  r.X = x; fe_1( r.Z ); fe_mul( r.T, x, y );
+  return flags;
+}
+
+/* fd_curve25519.h:88-118: x==0 | y==0 | y==y0 | y==y1 (affine, canonical x,y) */
+DEV bool ge_affine_is_small_order( ge_p3 const & p ) {
+  fe y0, y1;
+  fe_set( y0, 0x8f95e826u,0xb027b2c2u,0x89f4c345u,0xf098eff2u,0x05acdfd5u,0x3933c6d3u,0x880238b1u,0x05fc536du );
+  fe_set( y1, 0x706a17c7u,0x4fd84d3du,0x760b3cbau,0x0f67100du,0xfa53202au,0xc6cc392cu,0x77fdc74eu,0x7a03ac92u );
+  return fe_is_zero_c( p.X ) | fe_is_zero_c( p.Y ) | fe_eq_c( p.Y, y0 ) | fe_eq_c( p.Y, y1 );
+}
+
+/**********************************************************************/
+/* Scalars mod L (fd_curve25519_scalar.h / .c)                         */
+
+/* S <= L-1 (fd_curve25519_scalar.h:57-73) */
+DEV bool sc_is_canonical( u32 const s[8] ) {
+  const u32 L[8] = { 0x5cf5d3edu,0x5812631au,0xa2f79cd6u,0x14def9deu,0u,0u,0u,0x10000000u };
+  /* s < L  <=>  s - L borrows */
+  u64 bw = 0;
+  #pragma unroll
+  for( int i=0; i<8; i++ ) { u64 d = (u64)s[i] - L[i] - bw; bw = (d >> 63) & 1u; }
+  return bw != 0;
+}
+
+/* 512-bit little-endian x (16 limbs) mod L, Barrett (HAC 14.42, b=2^32, k=8,
+   mu = floor(2^512/L)).  Restates fd_curve25519_scalar_reduce
+   (fd_curve25519_scalar.c:3-110) as a different algorithm with the same
+   result. */
+DEV void sc_reduce512( u32 r[8], u32 const x[16] ) {
+  const u32 MU[9] = { 0x0a2c131bu,0xed9ce5a3u,0x086329a7u,0x2106215du,0xffffffebu,0xffffffffu,0xffffffffu,0xffffffffu,0x0000000fu };
+  const u32 L[8]  = { 0x5cf5d3edu,0x5812631au,0xa2f79cd6u,0x14def9deu,0u,0u,0u,0x10000000u };
+  /* q3 = floor( floor(x / b^7) * mu / b^9 ) : columns 9..17 of q1*mu (q1 = x[7..15]) */
+  u32 q3[9];
+  u64 lo = 0, hi = 0;   /* 128-bit column accumulator (lo, hi) */
+  #pragma unroll
+  for( int k=0; k<18; k++ ) {
+    #pragma unroll
+    for( int i=0; i<9; i++ ) {
+      int j = k - i;
+      if( j < 0 || j > 8 ) continue;
+      u64 p = (u64)x[7+i] * MU[j];
+      lo += p; hi += (lo < p) ? 1u : 0u;
+    }
+    if( k >= 9 ) q3[k-9] = (u32)lo;
+    lo = (lo >> 32) | (hi << 32); hi >>= 32;
+  }
+  /* r2 = q3 * L mod b^9 ; r = x mod b^9 - r2 (mod b^9) */
+  u32 r2[9];
+  lo = 0; hi = 0;
+  #pragma unroll
+  for( int k=0; k<9; k++ ) {
+    #pragma unroll
+    for( int i=0; i<9; i++ ) {
+      int j = k - i;
+      if( j < 0 || j > 7 ) continue;
+      if( j >= 4 && j < 7 ) continue;     /* L limbs 4..6 are zero */
+      u64 p = (u64)q3[i] * L[j];
+      lo += p; hi += (lo < p) ? 1u : 0u;
+    }
+    r2[k] = (u32)lo;
+    lo = (lo >> 32) | (hi << 32); hi >>= 32;
+  }
+  u32 t[9]; u64 bw = 0;
+  #pragma unroll
+  for( int i=0; i<9; i++ ) { u64 d = (u64)x[i] - r2[i] - bw; t[i] = (u32)d; bw = (d >> 63) & 1u; }
+  /* t < 3L: subtract L at most twice */
+  #pragma unroll
+  for( int rep=0; rep<2; rep++ ) {
+    u32 s[9]; bw = 0;
+    #pragma unroll
+    for( int i=0; i<9; i++ ) { u64 d = (u64)t[i] - (i<8 ? L[i] : 0u) - bw; s[i] = (u32)d; bw = (d >> 63) & 1u; }
+    u32 m = bw ? 0u : ~0u;                 /* no borrow: t >= L, take s */
+    #pragma unroll
+    for( int i=0; i<9; i++ ) t[i] = (s[i] & m) | (t[i] & ~m);
+  }
+  #pragma unroll
+  for( int i=0; i<8; i++ ) r[i] = t[i];
+}
+
+/* Signed radix-16 digits of k < 2^253 packed (biased by 8) 8 per u32:
+   nibble i of out[i/8] = d_i + 8, d_i in [-8,7] except d_63 in [0,2]. */
+DEV void sc_recode16( u32 out[8], u32 const k[8] ) {
+  u32 carry = 0;
+  #pragma unroll
+  for( int w=0; w<8; w++ ) {
+    u32 o = 0;
+    #pragma unroll
+    for( int n=0; n<8; n++ ) {
+      u32 d = ((k[w] >> (4*n)) & 15u) + carry;
+      carry = (d + 8u) >> 4;
+      d = d + 8u - (carry << 4);          /* biased digit in [0,15] (d_63 may be 10) */
+      o |= d << (4*n);
+    }
+    out[w] = o;
+  }
+}
+
+/* Signed radix-256 digits of s < 2^253 packed (biased by 128) 4 per u32 */
+DEV void sc_recode256( u32 out[8], u32 const s[8] ) {
+  u32 carry = 0;
+  #pragma unroll
+  for( int w=0; w<8; w++ ) {
+    u32 o = 0;
+    #pragma unroll
+    for( int n=0; n<4; n++ ) {
+      u32 d = ((s[w] >> (8*n)) & 255u) + carry;
+      carry = (d + 128u) >> 8;
+      d = d + 128u - (carry << 8);
+      o |= d << (8*n);
+    }
+    out[w] = o;
+  }
+}
+
+/**********************************************************************/
+/* SHA-512 (fd_sha512.c:264-399 semantics), one message per lane.      */
+
+DEV u64 ror64( u64 x, int n ) { return (x >> n) | (x << (64 - n)); }
+
+DEV void sha512_block( u64 st[8], u64 W[16] ) {
+  const u64 K[80] = {
+    0x428a2f98d728ae22ULL,0x7137449123ef65cdULL,0xb5c0fbcfec4d3b2fULL,0xe9b5dba58189dbbcULL,
+    0x3956c25bf348b538ULL,0x59f111f1b605d019ULL,0x923f82a4af194f9bULL,0xab1c5ed5da6d8118ULL,
+    0xd807aa98a3030242ULL,0x12835b0145706fbeULL,0x243185be4ee4b28cULL,0x550c7dc3d5ffb4e2ULL,
+    0x72be5d74f27b896fULL,0x80deb1fe3b1696b1ULL,0x9bdc06a725c71235ULL,0xc19bf174cf692694ULL,
+    0xe49b69c19ef14ad2ULL,0xefbe4786384f25e3ULL,0x0fc19dc68b8cd5b5ULL,0x240ca1cc77ac9c65ULL,
+    0x2de92c6f592b0275ULL,0x4a7484aa6ea6e483ULL,0x5cb0a9dcbd41fbd4ULL,0x76f988da831153b5ULL,
+    0x983e5152ee66dfabULL,0xa831c66d2db43210ULL,0xb00327c898fb213fULL,0xbf597fc7beef0ee4ULL,
+    0xc6e00bf33da88fc2ULL,0xd5a79147930aa725ULL,0x06ca6351e003826fULL,0x142929670a0e6e70ULL,
+    0x27b70a8546d22ffcULL,0x2e1b21385c26c926ULL,0x4d2c6dfc5ac42aedULL,0x53380d139d95b3dfULL,
+    0x650a73548baf63deULL,0x766a0abb3c77b2a8ULL,0x81c2c92e47edaee6ULL,0x92722c851482353bULL,
+    0xa2bfe8a14cf10364ULL,0xa81a664bbc423001ULL,0xc24b8b70d0f89791ULL,0xc76c51a30654be30ULL,
+    0xd192e819d6ef5218ULL,0xd69906245565a910ULL,0xf40e35855771202aULL,0x106aa07032bbd1b8ULL,
+    0x19a4c116b8d2d0c8ULL,0x1e376c085141ab53ULL,0x2748774cdf8eeb99ULL,0x34b0bcb5e19b48a8ULL,
+    0x391c0cb3c5c95a63ULL,0x4ed8aa4ae3418acbULL,0x5b9cca4f7763e373ULL,0x682e6ff3d6b2b8a3ULL,
+    0x748f82ee5defb2fcULL,0x78a5636f43172f60ULL,0x84c87814a1f0ab72ULL,0x8cc702081a6439ecULL,
+    0x90befffa23631e28ULL,0xa4506cebde82bde9ULL,0xbef9a3f7b2c67915ULL,0xc67178f2e372532bULL,
+    0xca273eceea26619cULL,0xd186b8c721c0c207ULL,0xeada7dd6cde0eb1eULL,0xf57d4f7fee6ed178ULL,
+    0x06f067aa72176fbaULL,0x0a637dc5a2c898a6ULL,0x113f9804bef90daeULL,0x1b710b35131c471bULL,
+    0x28db77f523047d84ULL,0x32caab7b40c72493ULL,0x3c9ebe0a15c9bebcULL,0x431d67c49c100d4cULL,
+    0x4cc5d4becb3e42b6ULL,0x597f299cfc657e2aULL,0x5fcb6fab3ad6faecULL,0x6c44198c4a475817ULL };
+  u64 a=st[0],b=st[1],c=st[2],d=st[3],e=st[4],f=st[5],g=st[6],h=st[7];
+  #pragma unroll
+  for( int t=0; t<80; t++ ) {
+    if( t >= 16 ) {
+      u64 w15 = W[(t-15)&15], w2 = W[(t-2)&15];
+      u64 s0 = ror64( w15, 1 ) ^ ror64( w15, 8 ) ^ (w15 >> 7);
+      u64 s1 = ror64( w2, 19 ) ^ ror64( w2, 61 ) ^ (w2 >> 6);
+      W[t&15] += s0 + W[(t-7)&15] + s1;
+    }
+    u64 S1 = ror64( e, 14 ) ^ ror64( e, 18 ) ^ ror64( e, 41 );
+    u64 ch = (e & f) ^ (~e & g);
+    u64 t1 = h + S1 + ch + K[t] + W[t&15];
+    u64 S0 = ror64( a, 28 ) ^ ror64( a, 34 ) ^ ror64( a, 39 );
+    u64 mj = (a & b) ^ (a & c) ^ (b & c);
+    h = g; g = f; f = e; e = d + t1; d = c; c = b; b = a; a = t1 + S0 + mj;
+  }
+  st[0]+=a; st[1]+=b; st[2]+=c; st[3]+=d; st[4]+=e; st[5]+=f; st[6]+=g; st[7]+=h;
+}
+
+DEV u32 bswap32( u32 x ) { return __builtin_bswap32( x ); }
+DEV u64 be64_of_le_words( u32 lo, u32 hi ) {   /* bytes b0..b7 (lo = b0..b3 LE) -> big-endian word */
+  return ((u64)bswap32( lo ) << 32) | (u64)bswap32( hi );
+}
+
+/* 8 message bytes starting at message offset m (m a multiple of 8, m < msz),
+   as two little-endian words, zero-masked past msz and with the 0x80 pad
+   byte at msz if it falls inside.  The pool must be readable up to
+   msg + msz + 12 (the host pads every pool by 16 bytes). */
+DEV void msg_load8( u32 & lo, u32 & hi, u8 const * msg, u32 msz, u32 m ) {
+  u32 c = msz - m; if( c > 8u ) c = 8u;               /* valid bytes, >= 1 */
+  uintptr_t a = (uintptr_t)(msg + m);
+  u32 const * p = (u32 const *)(a & ~(uintptr_t)3);
+  u32 sh = (u32)(a & 3u) * 8u;
+  u32 w0 = p[0], w1 = p[1], w2 = p[2];
+  lo = __builtin_amdgcn_alignbit( w1, w0, sh );
+  hi = __builtin_amdgcn_alignbit( w2, w1, sh );
+  if( c < 8u ) {
+    u32 pad_lo = 0, pad_hi = 0;
+    if( c < 4u ) { lo &= (1u << (8u*c)) - 1u; pad_lo = 0x80u << (8u*c); hi = 0; }
+    else         { hi &= (c == 4u) ? 0u : ((1u << (8u*(c-4u))) - 1u); pad_hi = 0x80u << (8u*(c-4u)); }
+    lo |= pad_lo; hi |= pad_hi;
+  }
+}
+
+/* SHA-512( pre || M ) where pre is 32 or 64 bytes given as LE words and
+   M = msg[0..msz); the 64-byte digest is returned reinterpreted as a 512-bit
+   little-endian integer (16 LE limbs), the form fd_curve25519_scalar_reduce
+   consumes. */
+DEV void sha512_prefixed( u32 x[16], u32 const pre[16], u32 plen, u8 const * msg, u32 msz ) {
+  u64 st[8] = { 0x6a09e667f3bcc908ULL,0xbb67ae8584caa73bULL,0x3c6ef372fe94f82bULL,0xa54ff53a5f1d36f1ULL,
+                0x510e527fade682d1ULL,0x9b05688c2b3e6c1fULL,0x1f83d9abfb41bd6bULL,0x5be0cd19137e2179ULL };
+  u32 tot = plen + msz;
+  u32 nb = (tot + 17u + 127u) >> 7;           /* ceil((plen + msz + 1 + 16) / 128) */
+  u64 bitlen = (u64)tot << 3;
+  #pragma unroll 1
+  for( u32 b=0; b<nb; b++ ) {
+    u64 W[16];
+    bool last = (b + 1u == nb);
+    #pragma unroll
+    for( int t=0; t<16; t++ ) {
+      u32 g = b*128u + 8u*(u32)t;             /* byte offset in pre||M||pad */
+      u64 w;
+      if( t < 8 && b == 0u && 8u*(u32)t < plen ) {   /* prefix words: static index (no scratch) */
+        w = be64_of_le_words( pre[(2*t)&15], pre[(2*t+1)&15] );
+      } else {
+        u32 m = g - plen;
+        u32 lo = 0, hi = 0;
+        if( m < msz )       msg_load8( lo, hi, msg, msz, m );
+        else if( m == msz ) lo = 0x80u;
+        w = be64_of_le_words( lo, hi );
+      }
+      if( last && t == 14 ) w = 0;
+      if( last && t == 15 ) w = bitlen;
+      W[t] = w;
+    }
+    sha512_block( st, W );
+  }
+  #pragma unroll
+  for( int j=0; j<8; j++ ) { x[2*j] = bswap32( (u32)(st[j] >> 32) ); x[2*j+1] = bswap32( (u32)st[j] ); }
+}
+
+/* k = SHA512( R || A || M ) mod L as 8 LE limbs (fd_ed25519_user.c:205-207). */
+DEV void hram_mod_l( u32 kout[8], u32 const R[8], u32 const A[8], u8 const * msg, u32 msz ) {
+  u32 pre[16], x[16];
+  #pragma unroll
+  for( int i=0; i<8; i++ ) { pre[i] = R[i]; pre[8+i] = A[i]; }
+  sha512_prefixed( x, pre, 64u, msg, msz );
+  sc_reduce512( kout, x );
+}

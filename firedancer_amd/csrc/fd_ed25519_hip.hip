@@ -1,0 +1,601 @@
+/* fd_ed25519_hip.hip -- gfx950 ed25519 batch verify engine: kernels and the
+   C ABI declared in include/fd_ed25519_hip.h.
+
+   Pipeline per chunk of up to ctx->chunk signatures (one signature per lane,
+   256-thread workgroups = 4 wave64):
+
+     k_verify_prep  S<L check, decode A and R (sqrt chains), small-order
+                    checks, k = SHA-512(R||A||M) mod L  -> 128-B state record
+     k_verify_dsm   base-point table -> LDS; table [0..8](-A) -> per-lane HBM
+                    scratch; [k](-A) + [S]B by fixed signed windows (radix 16
+                    for A, radix 256 for B: every lane adds at the same
+                    positions, so the wave never diverges on digits);
+                    projective compare with R; int8 code + verdict bitmap
+     k_group_reduce batch_single_msg / per-txn semantics over sig codes
+
+   Reference semantics: fd_ed25519_user.c:135-310 (see fd_ed25519_dev.h for
+   the per-function citations). */
+
+#include "fd_ed25519_dev.h"
+#include "../../include/fd_ed25519_hip.h"
+
+#include <hip/hip_runtime.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <mutex>
+
+#define FD_CHECK( x ) do {                                                            \
+    hipError_t e_ = (x);                                                               \
+    if( e_ != hipSuccess ) {                                                           \
+      fprintf( stderr, "fd_ed25519_hip: %s failed at %s:%d: %s\n", #x, __FILE__,     \
+               __LINE__, hipGetErrorString( e_ ) );                                    \
+      abort();                                                                         \
+    }                                                                                  \
+  } while( 0 )
+
+/* flags in the state record */
+#define F_S_BAD      (1u<<0)
+#define F_A_NOTSQ    (1u<<1)
+#define F_A_ZX       (1u<<2)
+#define F_R_NOTSQ    (1u<<3)
+#define F_R_ZX       (1u<<4)
+#define F_A_SMALL    (1u<<5)
+#define F_R_SMALL    (1u<<6)
+
+#define BTAB_N      129            /* 0..128 multiples of B */
+#define BTAB_WORDS  (BTAB_N*24)    /* affine cached: YmX, YpX, T2d */
+#define ATAB_WORDS  (9*32)         /* per lane: [0..8](-A) cached: YmX, YpX, T2d, Z2 */
+
+/* state record: 32 u32 words per field group, laid out SoA per chunk for
+   coalescing: word w of signature i lives at st[ w*chunk + i ]. */
+#define ST_K     0
+#define ST_S     8
+#define ST_AX   16
+#define ST_AY   24
+#define ST_RX   32
+#define ST_RY   40
+#define ST_FLAG 48
+#define ST_WORDS 49
+
+struct fd_ed25519_hip_ctx {
+  int          device;
+  hipStream_t  stream;
+  ulong        chunk;       /* signatures per launch */
+  u32 *        d_btab;      /* BTAB_WORDS */
+  u32 *        d_state;     /* ST_WORDS * chunk */
+  u32 *        d_atab;      /* ATAB_WORDS * chunk */
+  int          errmode;
+  /* staging for the host-memory entry points (grown on demand) */
+  ulong        h_cap_n, h_cap_pool, h_cap_groups;
+  uchar *      d_sigs; uchar * d_pubs; uchar * d_pool; uint * d_moff; uint * d_msz;
+  signed char * d_codes; ulong * d_bitmap;
+  uint *       d_gfirst; uchar * d_gcnt; signed char * d_gcodes;
+};
+
+/**********************************************************************/
+/* Kernels                                                             */
+
+DEV void load_words( u32 * w, uchar const * p, int nw ) {   /* 16-byte aligned p */
+  uint4 const * q = (uint4 const *)p;
+  #pragma unroll
+  for( int i=0; i<nw/4; i++ ) { uint4 v = q[i]; w[4*i]=v.x; w[4*i+1]=v.y; w[4*i+2]=v.z; w[4*i+3]=v.w; }
+}
+
+/* Base point B (encoding 0x58666...66, fd_curve25519_table_ref.c:7-14) */
+DEV void ge_base( ge_p3 & B ) {
+  u32 w[8];
+  #pragma unroll
+  for( int i=0; i<8; i++ ) w[i] = 0x66666666u;
+  w[0] = 0x66666658u;
+  ge_decode( B, w );
+}
+
+DEV void ge_to_affc_canon( ge_affc & a, ge_p3 const & p ) {
+  fe zi, x, y, t, d2;
+  fe_invert( zi, p.Z ); fe_mul( x, p.X, zi ); fe_mul( y, p.Y, zi );
+  fe_d2( d2 ); fe_mul( t, x, y ); fe_mul( t, t, d2 );
+  fe_sub( a.YmX, y, x ); fe_add( a.YpX, y, x );
+  fe_canon( a.YmX, a.YmX ); fe_canon( a.YpX, a.YpX ); fe_canon( a.T2d, t );
+}
+
+/* j*B for j in [0,128] in affine cached form (the reference's verify uses a
+   128-entry odd-multiple B table, fd_curve25519_table_ref.c:32; ours holds
+   all multiples 0..128 for signed radix-256 windows). */
+__global__ void k_btab_init( u32 * btab ) {
+  int j = blockIdx.x * blockDim.x + threadIdx.x;
+  if( j >= BTAB_N ) return;
+  ge_p3 B, P; ge_base( B ); ge_identity( P );
+  ge_cached Bc; ge_to_cached( Bc, B );
+  for( int bit=7; bit>=0; bit-- ) {
+    ge_dbl( P, P, true );
+    if( (j >> bit) & 1 ) ge_add_cached( P, P, Bc, 0u, true );
+  }
+  ge_affc a; ge_to_affc_canon( a, P );
+  #pragma unroll
+  for( int i=0; i<8; i++ ) { btab[j*24+i] = a.YmX.v[i]; btab[j*24+8+i] = a.YpX.v[i]; btab[j*24+16+i] = a.T2d.v[i]; }
+}
+
+__global__ __launch_bounds__(256)
+void k_verify_prep( ulong n, ulong chunk, uchar const * __restrict__ sigs, uchar const * __restrict__ pubs,
+                    uchar const * __restrict__ pool, uint const * __restrict__ moff, uint const * __restrict__ msz,
+                    u32 * __restrict__ st ) {
+  ulong i = (ulong)blockIdx.x * blockDim.x + threadIdx.x;
+  if( i >= n ) return;
+  u32 sig[16], pub[8];
+  load_words( sig, sigs + 64*i, 16 );
+  load_words( pub, pubs + 32*i, 8 );
+  u32 flags = sc_is_canonical( sig + 8 ) ? 0u : F_S_BAD;                 /* user.c:159-161 */
+  ge_p3 A, R;
+  u32 fa = ge_decode( A, pub );                                            /* user.c:165 */
+  u32 fr = ge_decode( R, sig );
+  flags |= ((fa & 1u) ? F_A_NOTSQ : 0u) | ((fa & 2u) ? F_A_ZX : 0u)
+        |  ((fr & 1u) ? F_R_NOTSQ : 0u) | ((fr & 2u) ? F_R_ZX : 0u);
+  if( !(fa & 1u) && ge_affine_is_small_order( A ) ) flags |= F_A_SMALL;   /* user.c:194-199 */
+  if( !(fr & 1u) && ge_affine_is_small_order( R ) ) flags |= F_R_SMALL;
+  u32 k[8];
+  hram_mod_l( k, sig, pub, pool + moff[i], msz[i] );                       /* user.c:205-207 */
+  u32 * s = st + i;
+  #pragma unroll
+  for( int w=0; w<8; w++ ) {
+    s[(ST_K +w)*chunk] = k[w];
+    s[(ST_S +w)*chunk] = sig[8+w];
+    s[(ST_AX+w)*chunk] = A.X.v[w];
+    s[(ST_AY+w)*chunk] = A.Y.v[w];
+    s[(ST_RX+w)*chunk] = R.X.v[w];
+    s[(ST_RY+w)*chunk] = R.Y.v[w];
+  }
+  s[ST_FLAG*chunk] = flags;
+}
+
+DEV int code_of( u32 f, int errmode, bool eq ) {
+  if( errmode == FD_ED25519_HIP_ERRMODE_AVX512 ) {
+    if( f & F_S_BAD ) return FD_ED25519_ERR_SIG;
+    if( f & (F_A_NOTSQ|F_A_ZX|F_R_NOTSQ|F_R_ZX) ) return FD_ED25519_ERR_SIG;  /* decode2 -> -1/-2 -> ERR_SIG */
+    if( f & F_A_SMALL ) return FD_ED25519_ERR_PUBKEY;
+    if( f & F_R_SMALL ) return FD_ED25519_ERR_SIG;
+  } else {
+    if( f & F_S_BAD ) return FD_ED25519_ERR_SIG;
+    if( f & F_A_NOTSQ ) return FD_ED25519_ERR_PUBKEY;                          /* frombytes_2x -> 1 */
+    if( f & F_R_NOTSQ ) return FD_ED25519_ERR_SIG;                             /*             -> 2 */
+    if( f & (F_A_SMALL|F_A_ZX) ) return FD_ED25519_ERR_PUBKEY;
+    if( f & (F_R_SMALL|F_R_ZX) ) return FD_ED25519_ERR_SIG;
+  }
+  return eq ? FD_ED25519_SUCCESS : FD_ED25519_ERR_MSG;
+}
+
+DEV void store_cached( u32 * t, ge_cached const & c ) {   /* 32 words, 16-byte aligned */
+  uint4 * q = (uint4 *)t;
+  q[0] = make_uint4( c.YmX.v[0], c.YmX.v[1], c.YmX.v[2], c.YmX.v[3] );
+  q[1] = make_uint4( c.YmX.v[4], c.YmX.v[5], c.YmX.v[6], c.YmX.v[7] );
+  q[2] = make_uint4( c.YpX.v[0], c.YpX.v[1], c.YpX.v[2], c.YpX.v[3] );
+  q[3] = make_uint4( c.YpX.v[4], c.YpX.v[5], c.YpX.v[6], c.YpX.v[7] );
+  q[4] = make_uint4( c.T2d.v[0], c.T2d.v[1], c.T2d.v[2], c.T2d.v[3] );
+  q[5] = make_uint4( c.T2d.v[4], c.T2d.v[5], c.T2d.v[6], c.T2d.v[7] );
+  q[6] = make_uint4( c.Z2.v[0],  c.Z2.v[1],  c.Z2.v[2],  c.Z2.v[3] );
+  q[7] = make_uint4( c.Z2.v[4],  c.Z2.v[5],  c.Z2.v[6],  c.Z2.v[7] );
+}
+DEV void load_cached( ge_cached & c, u32 const * t ) {
+  uint4 const * q = (uint4 const *)t;
+  uint4 v;
+  v = q[0]; fe_set( c.YmX, v.x, v.y, v.z, v.w, 0,0,0,0 ); v = q[1]; c.YmX.v[4]=v.x; c.YmX.v[5]=v.y; c.YmX.v[6]=v.z; c.YmX.v[7]=v.w;
+  v = q[2]; fe_set( c.YpX, v.x, v.y, v.z, v.w, 0,0,0,0 ); v = q[3]; c.YpX.v[4]=v.x; c.YpX.v[5]=v.y; c.YpX.v[6]=v.z; c.YpX.v[7]=v.w;
+  v = q[4]; fe_set( c.T2d, v.x, v.y, v.z, v.w, 0,0,0,0 ); v = q[5]; c.T2d.v[4]=v.x; c.T2d.v[5]=v.y; c.T2d.v[6]=v.z; c.T2d.v[7]=v.w;
+  v = q[6]; fe_set( c.Z2,  v.x, v.y, v.z, v.w, 0,0,0,0 ); v = q[7]; c.Z2.v[4]=v.x;  c.Z2.v[5]=v.y;  c.Z2.v[6]=v.z;  c.Z2.v[7]=v.w;
+}
+
+/* shift a packed 256-bit digit vector left by `bits` (4 or 8) */
+DEV void digits_shl( u32 d[8], u32 bits ) {
+  #pragma unroll
+  for( int i=7; i>0; i-- ) d[i] = __builtin_amdgcn_alignbit( d[i], d[i-1], 32u - bits );
+  d[0] <<= bits;
+}
+
+__global__ __launch_bounds__(256)
+void k_verify_dsm( ulong n, ulong chunk, u32 const * __restrict__ st, u32 const * __restrict__ btab,
+                   u32 * __restrict__ atab, int errmode, signed char * __restrict__ codes,
+                   ulong * __restrict__ bitmap ) {
+  __shared__ __attribute__((aligned(16))) u32 lds_btab[BTAB_WORDS];
+  for( int t = threadIdx.x; t < BTAB_WORDS/4; t += blockDim.x )
+    ((uint4 *)lds_btab)[t] = ((uint4 const *)btab)[t];
+  __syncthreads();
+
+  ulong i = (ulong)blockIdx.x * blockDim.x + threadIdx.x;
+  bool active = i < n;
+  ulong ii = active ? i : 0;
+  u32 const * s = st + ii;
+  u32 flags = s[ST_FLAG*chunk];
+  bool eq = false;
+  if( active && code_of( flags, FD_ED25519_HIP_ERRMODE_AVX512, true ) == FD_ED25519_SUCCESS ) {
+    /* ---- recode scalars (fixed signed windows) ---- */
+    u32 k[8], S[8], kd[8], sd[8];
+    #pragma unroll
+    for( int w=0; w<8; w++ ) { k[w] = s[(ST_K+w)*chunk]; S[w] = s[(ST_S+w)*chunk]; }
+    sc_recode16( kd, k );
+    sc_recode256( sd, S );
+
+    /* ---- table [0..8]Q, Q = -A (user.c:216; fd_curve25519.c:130-143) ---- */
+    u32 * tab = atab + ii * ATAB_WORDS;
+    {
+      ge_p3 Q;
+      fe ax;
+      #pragma unroll
+      for( int w=0; w<8; w++ ) { ax.v[w] = s[(ST_AX+w)*chunk]; Q.Y.v[w] = s[(ST_AY+w)*chunk]; }
+      fe_neg( Q.X, ax ); fe_1( Q.Z ); fe_mul( Q.T, Q.X, Q.Y );
+      ge_cached c;
+      fe_1( c.YmX ); fe_1( c.YpX ); fe_0( c.T2d ); fe_set( c.Z2, 2,0,0,0,0,0,0,0 );
+      store_cached( tab + 0*32, c );                                  /* identity */
+      ge_cached c1; ge_to_cached( c1, Q ); store_cached( tab + 1*32, c1 );
+      ge_p3 P2, P3, P4, P5, P6, P7, P8;
+      ge_dbl( P2, Q, true );            ge_to_cached( c, P2 ); store_cached( tab + 2*32, c );
+      ge_add_cached( P3, P2, c1, 0u, true ); ge_to_cached( c, P3 ); store_cached( tab + 3*32, c );
+      ge_dbl( P4, P2, true );           ge_to_cached( c, P4 ); store_cached( tab + 4*32, c );
+      ge_add_cached( P5, P4, c1, 0u, true ); ge_to_cached( c, P5 ); store_cached( tab + 5*32, c );
+      ge_dbl( P6, P3, true );           ge_to_cached( c, P6 ); store_cached( tab + 6*32, c );
+      ge_add_cached( P7, P6, c1, 0u, true ); ge_to_cached( c, P7 ); store_cached( tab + 7*32, c );
+      ge_dbl( P8, P4, true );           ge_to_cached( c, P8 ); store_cached( tab + 8*32, c );
+    }
+
+    /* ---- [k]Q + [S]B (user.c:217; fd_curve25519.c:121-165) ---- */
+    ge_p3 P; ge_identity( P );
+    #pragma unroll 1
+    for( int w=63; w>=0; w-- ) {
+      u32 da = kd[7] >> 28; digits_shl( kd, 4u );
+      int sa = (int)da - 8;
+      u32 nega = sa < 0 ? ~0u : 0u;
+      u32 ia = (u32)(sa < 0 ? -sa : sa);
+      ge_cached e; load_cached( e, tab + ia*32 );
+      if( w != 63 ) {
+        #pragma unroll 1
+        for( int j=0; j<3; j++ ) ge_dbl( P, P, false );
+        ge_dbl( P, P, true );
+      }
+      bool even = (w & 1) == 0;
+      ge_add_cached( P, P, e, nega, even );
+      if( even ) {
+        u32 db = sd[7] >> 24; digits_shl( sd, 8u );
+        int sb = (int)db - 128;
+        u32 negb = sb < 0 ? ~0u : 0u;
+        u32 ib = (u32)(sb < 0 ? -sb : sb);
+        ge_affc b;
+        u32 const * bt = lds_btab + ib*24;
+        #pragma unroll
+        for( int q=0; q<8; q++ ) { b.YmX.v[q] = bt[q]; b.YpX.v[q] = bt[8+q]; b.T2d.v[q] = bt[16+q]; }
+        ge_add_affc( P, P, b, negb, false );
+      }
+    }
+
+    /* ---- projective compare with R (user.c:226; fd_r43x6_ge.h:52-82) ---- */
+    fe rx, ry, t, cx, cy;
+    #pragma unroll
+    for( int w=0; w<8; w++ ) { rx.v[w] = s[(ST_RX+w)*chunk]; ry.v[w] = s[(ST_RY+w)*chunk]; }
+    fe_mul( t, rx, P.Z ); fe_canon( t, t ); fe_canon( cx, P.X );
+    bool ex = fe_eq_c( t, cx );
+    fe_mul( t, ry, P.Z ); fe_canon( t, t ); fe_canon( cy, P.Y );
+    eq = ex && fe_eq_c( t, cy );
+  }
+  int code = code_of( flags, errmode, eq );
+  if( active ) codes[i] = (signed char)code;
+  unsigned long long ball = __ballot( active && code == FD_ED25519_SUCCESS );
+  if( bitmap && (threadIdx.x & 63) == 0 && active ) bitmap[i >> 6] = ball;
+}
+
+/* fd_ed25519_verify_batch_single_msg (user.c:232-310) over per-sig codes */
+__global__ void k_group_reduce( ulong ng, uint const * first, uchar const * cnt, signed char const * sc,
+                                signed char * gc ) {
+  ulong g = (ulong)blockIdx.x * blockDim.x + threadIdx.x;
+  if( g >= ng ) return;
+  uint f = first[g], c = cnt[g];
+  int r;
+  if( c == 0u || c > 16u ) r = FD_ED25519_ERR_SIG;
+  else {
+    r = FD_ED25519_SUCCESS;
+    int msg_fail = 0;
+    for( uint j=0; j<c; j++ ) {
+      int x = sc[f+j];
+      if( x == FD_ED25519_ERR_SIG || x == FD_ED25519_ERR_PUBKEY ) { r = x; break; }
+      if( x == FD_ED25519_ERR_MSG ) msg_fail = 1;
+    }
+    if( r == FD_ED25519_SUCCESS && msg_fail ) r = FD_ED25519_ERR_MSG;
+  }
+  gc[g] = (signed char)r;
+}
+
+/* [s]B for s < 2^253 with the radix-256 B table (signing) */
+DEV void ge_scalarmult_base( ge_p3 & P, u32 const s[8], u32 const * lds_btab ) {
+  u32 sd[8]; sc_recode256( sd, s );
+  ge_identity( P );
+  #pragma unroll 1
+  for( int j=31; j>=0; j-- ) {
+    if( j != 31 ) {
+      #pragma unroll 1
+      for( int q=0; q<7; q++ ) ge_dbl( P, P, false );
+      ge_dbl( P, P, true );
+    }
+    u32 db = sd[7] >> 24; digits_shl( sd, 8u );
+    int sb = (int)db - 128;
+    u32 negb = sb < 0 ? ~0u : 0u;
+    u32 ib = (u32)(sb < 0 ? -sb : sb);
+    ge_affc b;
+    u32 const * bt = lds_btab + ib*24;
+    #pragma unroll
+    for( int q=0; q<8; q++ ) { b.YmX.v[q] = bt[q]; b.YpX.v[q] = bt[8+q]; b.T2d.v[q] = bt[16+q]; }
+    ge_add_affc( P, P, b, negb, true );
+  }
+}
+
+/* fd_ed25519_point_tobytes (fd_curve25519.c:63-74) as 8 LE words */
+DEV void ge_encode( u32 out[8], ge_p3 const & P ) {
+  fe zi, x, y;
+  fe_invert( zi, P.Z ); fe_mul( x, P.X, zi ); fe_mul( y, P.Y, zi );
+  fe_canon( x, x ); fe_canon( y, y );
+  #pragma unroll
+  for( int i=0; i<8; i++ ) out[i] = y.v[i];
+  out[7] |= (x.v[0] & 1u) << 31;
+}
+
+/* keygen + sign: fd_ed25519_user.c:4-133 */
+__global__ __launch_bounds__(256)
+void k_sign( ulong n, uchar const * __restrict__ prvs, uchar const * __restrict__ pool,
+             uint const * __restrict__ moff, uint const * __restrict__ msz, u32 const * __restrict__ btab,
+             uchar * __restrict__ pubs, uchar * __restrict__ sigs ) {
+  __shared__ __attribute__((aligned(16))) u32 lds_btab[BTAB_WORDS];
+  for( int t = threadIdx.x; t < BTAB_WORDS/4; t += blockDim.x )
+    ((uint4 *)lds_btab)[t] = ((uint4 const *)btab)[t];
+  __syncthreads();
+  ulong i = (ulong)blockIdx.x * blockDim.x + threadIdx.x;
+  if( i >= n ) return;
+  u32 pre[16], h[16];
+  load_words( pre, prvs + 32*i, 8 );
+  #pragma unroll
+  for( int q=8; q<16; q++ ) pre[q] = 0;
+  sha512_prefixed( h, pre, 32u, pool, 0u );                     /* h = SHA512(prv) */
+  u32 s[8];
+  #pragma unroll
+  for( int q=0; q<8; q++ ) s[q] = h[q];
+  s[0] &= 0xfffffff8u; s[7] &= 0x7fffffffu; s[7] |= 0x40000000u;   /* clamp (user.c:30-32) */
+  /* [s]B == [s mod L]B (B has order L); the reduced scalar is < 2^253 so its
+     top radix-256 digit cannot carry out of the table range */
+  u32 sx[16], sr[8];
+  #pragma unroll
+  for( int q=0; q<16; q++ ) sx[q] = q < 8 ? s[q] : 0u;
+  sc_reduce512( sr, sx );
+  ge_p3 P; u32 A[8], R[8];
+  ge_scalarmult_base( P, sr, lds_btab ); ge_encode( A, P );
+  uchar const * msg = pool + moff[i]; u32 mlen = msz[i];
+  #pragma unroll
+  for( int q=0; q<8; q++ ) pre[q] = h[8+q];
+  u32 x[16], r[8];
+  sha512_prefixed( x, pre, 32u, msg, mlen ); sc_reduce512( r, x );   /* r = H(prefix||M) mod L */
+  ge_scalarmult_base( P, r, lds_btab ); ge_encode( R, P );
+  u32 k[8]; hram_mod_l( k, R, A, msg, mlen );
+  /* S = (r + k*s) mod L */
+  u32 prod[16];
+  {
+    u64 lo = 0, hi = 0;
+    #pragma unroll
+    for( int c=0; c<16; c++ ) {
+      #pragma unroll
+      for( int a=0; a<8; a++ ) {
+        int b = c - a; if( b < 0 || b > 7 ) continue;
+        u64 p = (u64)k[a] * s[b]; lo += p; hi += (lo < p) ? 1u : 0u;
+      }
+      if( c < 8 ) { u64 q = lo + r[c]; hi += (q < lo) ? 1u : 0u; lo = q; }
+      prod[c] = (u32)lo; lo = (lo >> 32) | (hi << 32); hi >>= 32;
+    }
+  }
+  u32 S[8]; sc_reduce512( S, prod );
+  uint4 * o = (uint4 *)(sigs + 64*i);
+  o[0] = make_uint4( R[0],R[1],R[2],R[3] ); o[1] = make_uint4( R[4],R[5],R[6],R[7] );
+  o[2] = make_uint4( S[0],S[1],S[2],S[3] ); o[3] = make_uint4( S[4],S[5],S[6],S[7] );
+  uint4 * pa = (uint4 *)(pubs + 32*i);
+  pa[0] = make_uint4( A[0],A[1],A[2],A[3] ); pa[1] = make_uint4( A[4],A[5],A[6],A[7] );
+}
+
+/**********************************************************************/
+/* Host side                                                           */
+
+extern "C" {
+
+fd_ed25519_hip_ctx_t *
+fd_ed25519_hip_ctx_new( int device, ulong chunk_sigs ) {
+  if( !chunk_sigs ) chunk_sigs = 1UL << 20;
+  chunk_sigs = (chunk_sigs + 255UL) & ~255UL;
+  fd_ed25519_hip_ctx_t * ctx = (fd_ed25519_hip_ctx_t *)calloc( 1, sizeof(*ctx) );
+  if( !ctx ) { fprintf( stderr, "fd_ed25519_hip: out of host memory\n" ); abort(); }
+  ctx->device = device;
+  ctx->chunk  = chunk_sigs;
+  FD_CHECK( hipSetDevice( device ) );
+  FD_CHECK( hipStreamCreateWithFlags( &ctx->stream, hipStreamNonBlocking ) );
+  FD_CHECK( hipMalloc( (void **)&ctx->d_btab,  BTAB_WORDS * sizeof(u32) ) );
+  FD_CHECK( hipMalloc( (void **)&ctx->d_state, (size_t)ST_WORDS * chunk_sigs * sizeof(u32) ) );
+  FD_CHECK( hipMalloc( (void **)&ctx->d_atab,  (size_t)ATAB_WORDS * chunk_sigs * sizeof(u32) ) );
+  hipLaunchKernelGGL( k_btab_init, dim3( (BTAB_N + 63)/64 ), dim3( 64 ), 0, ctx->stream, ctx->d_btab );
+  FD_CHECK( hipGetLastError() );
+  FD_CHECK( hipStreamSynchronize( ctx->stream ) );
+  return ctx;
+}
+
+static void free_staging( fd_ed25519_hip_ctx_t * ctx ) {
+  (void)hipFree( ctx->d_sigs ); (void)hipFree( ctx->d_pubs ); (void)hipFree( ctx->d_pool ); (void)hipFree( ctx->d_moff );
+  (void)hipFree( ctx->d_msz ); (void)hipFree( ctx->d_codes ); (void)hipFree( ctx->d_bitmap );
+  (void)hipFree( ctx->d_gfirst ); (void)hipFree( ctx->d_gcnt ); (void)hipFree( ctx->d_gcodes );
+}
+
+void
+fd_ed25519_hip_ctx_delete( fd_ed25519_hip_ctx_t * ctx ) {
+  if( !ctx ) return;
+  (void)hipSetDevice( ctx->device );
+  (void)hipStreamSynchronize( ctx->stream );
+  (void)hipFree( ctx->d_btab ); (void)hipFree( ctx->d_state ); (void)hipFree( ctx->d_atab );
+  free_staging( ctx );
+  (void)hipStreamDestroy( ctx->stream );
+  free( ctx );
+}
+
+int   fd_ed25519_hip_ctx_device( fd_ed25519_hip_ctx_t const * ctx ) { return ctx->device; }
+void *fd_ed25519_hip_ctx_stream( fd_ed25519_hip_ctx_t const * ctx ) { return (void *)ctx->stream; }
+void  fd_ed25519_hip_set_errmode( fd_ed25519_hip_ctx_t * ctx, int m ) { ctx->errmode = m; }
+
+int
+fd_ed25519_hip_verify_dev( fd_ed25519_hip_ctx_t * ctx, ulong n, uchar const * d_sigs, uchar const * d_pubs,
+                           uchar const * d_pool, uint const * d_msg_off, uint const * d_msg_sz,
+                           signed char * d_codes, ulong * d_bitmap, void * stream ) {
+  hipStream_t s = stream ? (hipStream_t)stream : ctx->stream;
+  FD_CHECK( hipSetDevice( ctx->device ) );
+  for( ulong off = 0; off < n; off += ctx->chunk ) {
+    ulong m = n - off < ctx->chunk ? n - off : ctx->chunk;
+    dim3 grid( (unsigned)((m + 255) / 256) ), blk( 256 );
+    hipLaunchKernelGGL( k_verify_prep, grid, blk, 0, s, m, ctx->chunk, d_sigs + 64*off, d_pubs + 32*off,
+                        d_pool, d_msg_off + off, d_msg_sz + off, ctx->d_state );
+    FD_CHECK( hipGetLastError() );
+    hipLaunchKernelGGL( k_verify_dsm, grid, blk, 0, s, m, ctx->chunk, ctx->d_state, ctx->d_btab, ctx->d_atab,
+                        ctx->errmode, d_codes + off, d_bitmap ? d_bitmap + off/64 : (ulong *)NULL );
+    FD_CHECK( hipGetLastError() );
+  }
+  return 0;
+}
+
+int
+fd_ed25519_hip_group_reduce_dev( fd_ed25519_hip_ctx_t * ctx, ulong ng, uint const * d_first, uchar const * d_cnt,
+                                 signed char const * d_sig_codes, signed char * d_group_codes, void * stream ) {
+  hipStream_t s = stream ? (hipStream_t)stream : ctx->stream;
+  FD_CHECK( hipSetDevice( ctx->device ) );
+  if( !ng ) return 0;
+  hipLaunchKernelGGL( k_group_reduce, dim3( (unsigned)((ng + 255)/256) ), dim3( 256 ), 0, s,
+                      ng, d_first, d_cnt, d_sig_codes, d_group_codes );
+  FD_CHECK( hipGetLastError() );
+  return 0;
+}
+
+int
+fd_ed25519_hip_sign_dev( fd_ed25519_hip_ctx_t * ctx, ulong n, uchar const * d_prvs, uchar const * d_pool,
+                         uint const * d_msg_off, uint const * d_msg_sz, uchar * d_pubs, uchar * d_sigs,
+                         void * stream ) {
+  hipStream_t s = stream ? (hipStream_t)stream : ctx->stream;
+  FD_CHECK( hipSetDevice( ctx->device ) );
+  if( !n ) return 0;
+  hipLaunchKernelGGL( k_sign, dim3( (unsigned)((n + 255)/256) ), dim3( 256 ), 0, s,
+                      n, d_prvs, d_pool, d_msg_off, d_msg_sz, ctx->d_btab, d_pubs, d_sigs );
+  FD_CHECK( hipGetLastError() );
+  return 0;
+}
+
+int
+fd_ed25519_hip_sync( fd_ed25519_hip_ctx_t * ctx ) {
+  FD_CHECK( hipSetDevice( ctx->device ) );
+  FD_CHECK( hipStreamSynchronize( ctx->stream ) );
+  return 0;
+}
+
+static void ensure_staging( fd_ed25519_hip_ctx_t * ctx, ulong n, ulong pool_sz, ulong ng ) {
+  if( n > ctx->h_cap_n ) {
+    ulong c = n < 4096 ? 4096 : n;
+    (void)hipFree( ctx->d_sigs ); (void)hipFree( ctx->d_pubs ); (void)hipFree( ctx->d_moff ); (void)hipFree( ctx->d_msz );
+    (void)hipFree( ctx->d_codes ); (void)hipFree( ctx->d_bitmap );
+    FD_CHECK( hipMalloc( (void **)&ctx->d_sigs, 64*c ) );
+    FD_CHECK( hipMalloc( (void **)&ctx->d_pubs, 32*c ) );
+    FD_CHECK( hipMalloc( (void **)&ctx->d_moff, 4*c ) );
+    FD_CHECK( hipMalloc( (void **)&ctx->d_msz, 4*c ) );
+    FD_CHECK( hipMalloc( (void **)&ctx->d_codes, c ) );
+    FD_CHECK( hipMalloc( (void **)&ctx->d_bitmap, 8*((c+63)/64) ) );
+    ctx->h_cap_n = c;
+  }
+  if( pool_sz + 16 > ctx->h_cap_pool ) {
+    ulong c = pool_sz + 16 < 65536 ? 65536 : pool_sz + 16;
+    (void)hipFree( ctx->d_pool );
+    FD_CHECK( hipMalloc( (void **)&ctx->d_pool, c ) );
+    FD_CHECK( hipMemset( ctx->d_pool, 0, c ) );
+    ctx->h_cap_pool = c;
+  }
+  if( ng > ctx->h_cap_groups ) {
+    ulong c = ng < 4096 ? 4096 : ng;
+    (void)hipFree( ctx->d_gfirst ); (void)hipFree( ctx->d_gcnt ); (void)hipFree( ctx->d_gcodes );
+    FD_CHECK( hipMalloc( (void **)&ctx->d_gfirst, 4*c ) );
+    FD_CHECK( hipMalloc( (void **)&ctx->d_gcnt, c ) );
+    FD_CHECK( hipMalloc( (void **)&ctx->d_gcodes, c ) );
+    ctx->h_cap_groups = c;
+  }
+}
+
+int
+fd_ed25519_hip_verify_host( fd_ed25519_hip_ctx_t * ctx, ulong n, uchar const * sigs, uchar const * pubs,
+                            uchar const * pool, ulong pool_sz, uint const * msg_off, uint const * msg_sz,
+                            signed char * codes, ulong * bitmap ) {
+  if( !n ) return 0;
+  FD_CHECK( hipSetDevice( ctx->device ) );
+  ensure_staging( ctx, n, pool_sz, 0 );
+  hipStream_t s = ctx->stream;
+  FD_CHECK( hipMemcpyAsync( ctx->d_sigs, sigs, 64*n, hipMemcpyHostToDevice, s ) );
+  FD_CHECK( hipMemcpyAsync( ctx->d_pubs, pubs, 32*n, hipMemcpyHostToDevice, s ) );
+  if( pool_sz ) FD_CHECK( hipMemcpyAsync( ctx->d_pool, pool, pool_sz, hipMemcpyHostToDevice, s ) );
+  FD_CHECK( hipMemcpyAsync( ctx->d_moff, msg_off, 4*n, hipMemcpyHostToDevice, s ) );
+  FD_CHECK( hipMemcpyAsync( ctx->d_msz, msg_sz, 4*n, hipMemcpyHostToDevice, s ) );
+  fd_ed25519_hip_verify_dev( ctx, n, ctx->d_sigs, ctx->d_pubs, ctx->d_pool, ctx->d_moff, ctx->d_msz,
+                             ctx->d_codes, ctx->d_bitmap, s );
+  FD_CHECK( hipMemcpyAsync( codes, ctx->d_codes, n, hipMemcpyDeviceToHost, s ) );
+  if( bitmap ) FD_CHECK( hipMemcpyAsync( bitmap, ctx->d_bitmap, 8*((n+63)/64), hipMemcpyDeviceToHost, s ) );
+  FD_CHECK( hipStreamSynchronize( s ) );
+  return 0;
+}
+
+/* ---- reference API on a lazily created process-wide context ---------- */
+
+static fd_ed25519_hip_ctx_t * g_ctx;
+static std::mutex             g_lock;
+
+static fd_ed25519_hip_ctx_t * default_ctx( void ) {
+  if( !g_ctx ) {
+    char const * e = getenv( "FD_ED25519_HIP_DEVICE" );
+    g_ctx = fd_ed25519_hip_ctx_new( e ? atoi( e ) : 0, 4096 );
+    char const * m = getenv( "FD_ED25519_HIP_ERRMODE" );
+    if( m && !strcmp( m, "ref" ) ) g_ctx->errmode = FD_ED25519_HIP_ERRMODE_REF;
+  }
+  return g_ctx;
+}
+
+int
+fd_ed25519_verify( uchar const msg[], ulong msg_sz, uchar const sig[64], uchar const public_key[32],
+                   struct fd_sha512_private * sha ) {
+  (void)sha;
+  std::lock_guard<std::mutex> lk( g_lock );
+  fd_ed25519_hip_ctx_t * ctx = default_ctx();
+  uint off = 0, sz = (uint)msg_sz;
+  signed char code;
+  fd_ed25519_hip_verify_host( ctx, 1, sig, public_key, msg_sz ? msg : (uchar const *)"", msg_sz, &off, &sz, &code, NULL );
+  return (int)code;
+}
+
+int
+fd_ed25519_verify_batch_single_msg( uchar const msg[], ulong const msg_sz, uchar const signatures[64],
+                                    uchar const pubkeys[32], struct fd_sha512_private * shas[1],
+                                    uchar const batch_sz ) {
+  (void)shas;
+  if( batch_sz == 0 || batch_sz > 16 ) return FD_ED25519_ERR_SIG;         /* user.c:238-241 */
+  std::lock_guard<std::mutex> lk( g_lock );
+  fd_ed25519_hip_ctx_t * ctx = default_ctx();
+  uint off[16], sz[16]; signed char codes[16];
+  for( int j=0; j<batch_sz; j++ ) { off[j] = 0; sz[j] = (uint)msg_sz; }
+  fd_ed25519_hip_verify_host( ctx, batch_sz, signatures, pubkeys, msg_sz ? msg : (uchar const *)"", msg_sz,
+                              off, sz, codes, NULL );
+  int msg_fail = 0;
+  for( int j=0; j<batch_sz; j++ ) {                                        /* pass-1 order, then pass 2 */
+    if( codes[j] == FD_ED25519_ERR_SIG || codes[j] == FD_ED25519_ERR_PUBKEY ) return codes[j];
+    if( codes[j] == FD_ED25519_ERR_MSG ) msg_fail = 1;
+  }
+  return msg_fail ? FD_ED25519_ERR_MSG : FD_ED25519_SUCCESS;
+}
+
+char const *
+fd_ed25519_strerror( int err ) {
+  switch( err ) {
+  case FD_ED25519_SUCCESS:    return "success";
+  case FD_ED25519_ERR_SIG:    return "bad signature";
+  case FD_ED25519_ERR_PUBKEY: return "bad public key";
+  case FD_ED25519_ERR_MSG:    return "bad message";
+  default: break;
+  }
+  return "unknown";
+}
+
+} /* extern "C" */

@@ -1,0 +1,164 @@
+"""Host-side mirror of the reference's ed25519 verify interface, backed by the
+gfx950 engine (firedancer_amd/libfd_ed25519_hip.so, C ABI in
+include/fd_ed25519_hip.h).
+
+Names, argument meaning and result codes follow src/ballet/ed25519/fd_ed25519.h
+(fd_ed25519_verify :96-101, fd_ed25519_verify_batch_single_msg :124-130,
+fd_ed25519_strerror :137-138).  There is no CPU fallback: if the HIP library is
+missing or no GPU is present, every entry point raises.
+"""
+import ctypes
+import os
+
+import numpy as np
+
+from .build import LIB
+
+FD_ED25519_SUCCESS = 0
+FD_ED25519_ERR_SIG = -1
+FD_ED25519_ERR_PUBKEY = -2
+FD_ED25519_ERR_MSG = -3
+
+ERRMODE_AVX512 = 0
+ERRMODE_REF = 1
+
+# Every symbol include/fd_ed25519_hip.h declares (checked by tests/test_abi.py).
+EXPORTS = (
+    "fd_ed25519_verify", "fd_ed25519_verify_batch_single_msg", "fd_ed25519_strerror",
+    "fd_ed25519_hip_ctx_new", "fd_ed25519_hip_ctx_delete", "fd_ed25519_hip_ctx_device",
+    "fd_ed25519_hip_ctx_stream", "fd_ed25519_hip_set_errmode", "fd_ed25519_hip_verify_dev",
+    "fd_ed25519_hip_verify_host", "fd_ed25519_hip_group_reduce_dev", "fd_ed25519_hip_sign_dev",
+    "fd_ed25519_hip_sync",
+)
+
+_lib = None
+
+
+def lib():
+    """Load the engine library (raises if it was not built)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB):
+            raise RuntimeError(f"{LIB} missing: run __graft_entry__.build() (no CPU fallback exists)")
+        L = ctypes.CDLL(LIB)
+        c = ctypes
+        vp, u64 = c.c_void_p, c.c_ulong
+        L.fd_ed25519_verify.restype = c.c_int
+        L.fd_ed25519_verify.argtypes = [c.c_char_p, u64, c.c_char_p, c.c_char_p, vp]
+        L.fd_ed25519_verify_batch_single_msg.restype = c.c_int
+        L.fd_ed25519_verify_batch_single_msg.argtypes = [c.c_char_p, u64, c.c_char_p, c.c_char_p, vp, c.c_ubyte]
+        L.fd_ed25519_strerror.restype = c.c_char_p
+        L.fd_ed25519_strerror.argtypes = [c.c_int]
+        L.fd_ed25519_hip_ctx_new.restype = vp
+        L.fd_ed25519_hip_ctx_new.argtypes = [c.c_int, u64]
+        L.fd_ed25519_hip_ctx_delete.argtypes = [vp]
+        L.fd_ed25519_hip_ctx_device.restype = c.c_int
+        L.fd_ed25519_hip_ctx_device.argtypes = [vp]
+        L.fd_ed25519_hip_ctx_stream.restype = vp
+        L.fd_ed25519_hip_ctx_stream.argtypes = [vp]
+        L.fd_ed25519_hip_set_errmode.argtypes = [vp, c.c_int]
+        L.fd_ed25519_hip_verify_dev.restype = c.c_int
+        L.fd_ed25519_hip_verify_dev.argtypes = [vp, u64, vp, vp, vp, vp, vp, vp, vp, vp]
+        L.fd_ed25519_hip_verify_host.restype = c.c_int
+        L.fd_ed25519_hip_verify_host.argtypes = [vp, u64, vp, vp, vp, u64, vp, vp, vp, vp]
+        L.fd_ed25519_hip_group_reduce_dev.restype = c.c_int
+        L.fd_ed25519_hip_group_reduce_dev.argtypes = [vp, u64, vp, vp, vp, vp, vp]
+        L.fd_ed25519_hip_sign_dev.restype = c.c_int
+        L.fd_ed25519_hip_sign_dev.argtypes = [vp, u64, vp, vp, vp, vp, vp, vp, vp]
+        L.fd_ed25519_hip_sync.restype = c.c_int
+        L.fd_ed25519_hip_sync.argtypes = [vp]
+        _lib = L
+    return _lib
+
+
+def fd_ed25519_verify(msg, sig, public_key, sha=None):
+    """fd_ed25519_user.c:135-230 semantics; returns an FD_ED25519_* code."""
+    assert len(sig) == 64 and len(public_key) == 32
+    return lib().fd_ed25519_verify(bytes(msg), len(msg), bytes(sig), bytes(public_key), None)
+
+
+def fd_ed25519_verify_batch_single_msg(msg, signatures, pubkeys, batch_sz, shas=None):
+    """fd_ed25519_user.c:232-310 semantics (batch_sz 0 or > 16 -> ERR_SIG)."""
+    n = int(batch_sz)
+    sigs = bytes(signatures) if n else b"\0" * 64
+    pubs = bytes(pubkeys) if n else b"\0" * 32
+    assert n > 16 or n == 0 or (len(sigs) >= 64 * n and len(pubs) >= 32 * n)
+    return lib().fd_ed25519_verify_batch_single_msg(bytes(msg), len(msg), sigs, pubs, None, n & 0xff if n <= 255 else 255)
+
+
+def fd_ed25519_strerror(err):
+    return lib().fd_ed25519_strerror(int(err)).decode()
+
+
+def _ptr(a):
+    if a is None:
+        return None
+    if isinstance(a, np.ndarray):
+        return a.ctypes.data
+    return a.data_ptr()   # torch tensor on the device
+
+
+class Verifier:
+    """One GPU context (device, stream, base-point table, chunk scratch)."""
+
+    def __init__(self, device=0, chunk_sigs=1 << 20, errmode=ERRMODE_AVX512):
+        self._lib = lib()
+        self.ctx = self._lib.fd_ed25519_hip_ctx_new(int(device), int(chunk_sigs))
+        if not self.ctx:
+            raise RuntimeError("fd_ed25519_hip_ctx_new failed")
+        self.device = int(device)
+        self.set_errmode(errmode)
+
+    def set_errmode(self, errmode):
+        self._lib.fd_ed25519_hip_set_errmode(self.ctx, int(errmode))
+
+    @property
+    def stream(self):
+        return self._lib.fd_ed25519_hip_ctx_stream(self.ctx)
+
+    def close(self):
+        if self.ctx:
+            self._lib.fd_ed25519_hip_ctx_delete(self.ctx)
+            self.ctx = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # ---- host memory -------------------------------------------------------
+    def verify_host(self, sigs, pubs, pool, msg_off, msg_sz):
+        sigs = np.ascontiguousarray(sigs, np.uint8).reshape(-1, 64)
+        n = sigs.shape[0]
+        pubs = np.ascontiguousarray(pubs, np.uint8).reshape(n, 32)
+        pool = np.ascontiguousarray(pool, np.uint8).reshape(-1)
+        if pool.size == 0:
+            pool = np.zeros(1, np.uint8)
+        msg_off = np.ascontiguousarray(msg_off, np.uint32).reshape(n)
+        msg_sz = np.ascontiguousarray(msg_sz, np.uint32).reshape(n)
+        if n and int((msg_off.astype(np.uint64) + msg_sz).max()) > pool.size:
+            raise ValueError("message outside the pool")
+        codes = np.zeros(n, np.int8)
+        bitmap = np.zeros((n + 63) // 64, np.uint64)
+        if n:
+            self._lib.fd_ed25519_hip_verify_host(self.ctx, n, sigs.ctypes.data, pubs.ctypes.data, pool.ctypes.data,
+                                                 pool.size, msg_off.ctypes.data, msg_sz.ctypes.data,
+                                                 codes.ctypes.data, bitmap.ctypes.data)
+        return codes, bitmap
+
+    # ---- device memory (torch tensors or raw pointers) ---------------------
+    def verify_dev(self, n, sigs, pubs, pool, msg_off, msg_sz, codes, bitmap=None, stream=None):
+        return self._lib.fd_ed25519_hip_verify_dev(self.ctx, int(n), _ptr(sigs), _ptr(pubs), _ptr(pool), _ptr(msg_off),
+                                                   _ptr(msg_sz), _ptr(codes), _ptr(bitmap), stream)
+
+    def group_reduce_dev(self, n_groups, first, cnt, sig_codes, group_codes, stream=None):
+        return self._lib.fd_ed25519_hip_group_reduce_dev(self.ctx, int(n_groups), _ptr(first), _ptr(cnt),
+                                                         _ptr(sig_codes), _ptr(group_codes), stream)
+
+    def sign_dev(self, n, prvs, pool, msg_off, msg_sz, pubs, sigs, stream=None):
+        return self._lib.fd_ed25519_hip_sign_dev(self.ctx, int(n), _ptr(prvs), _ptr(pool), _ptr(msg_off),
+                                                 _ptr(msg_sz), _ptr(pubs), _ptr(sigs), stream)
+
+    def sync(self):
+        self._lib.fd_ed25519_hip_sync(self.ctx)

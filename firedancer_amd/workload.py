@@ -61,3 +61,46 @@ def c2_mutate(sigs, pubs, rng):
     bits = rng.integers(0, 256, size=idx.size)
     pubs[idx, bits >> 3] ^= (1 << (bits & 7)).astype(np.uint8)
     return kinds
+
+
+class Batch:
+    """A verify batch resident in HBM (torch tensors on one device)."""
+
+    def __init__(self, dev, sigs, pubs, pool, msg_off, msg_sz, kinds=None):
+        self.dev, self.sigs, self.pubs, self.pool = dev, sigs, pubs, pool
+        self.msg_off, self.msg_sz, self.kinds = msg_off, msg_sz, kinds
+
+    @property
+    def n(self):
+        return self.sigs.shape[0]
+
+
+def make_batch_gpu(verifier, n, msg_sz=64, seed=0x5eed0001, mix="c1", shared_msg=False):
+    """Config-1 style batch: n random keypairs, one random msg_sz-byte message
+    per signature (or one shared message: config 3), signed on the GPU by the
+    engine's own signer (fd_ed25519_hip_sign_dev).  mix="c2" applies the C2
+    mutation model on the host afterwards."""
+    import torch
+    dev = torch.device("cuda", verifier.device)
+    rng = np.random.default_rng(seed)
+    prvs = rng.integers(0, 256, size=(n, 32), dtype=np.uint8)
+    if shared_msg:
+        pool = np.concatenate([rng.integers(0, 256, size=msg_sz, dtype=np.uint8), np.zeros(16, np.uint8)])
+        moff = np.zeros(n, np.uint32)
+    else:
+        pool = np.concatenate([rng.integers(0, 256, size=n * msg_sz, dtype=np.uint8), np.zeros(16, np.uint8)])
+        moff = (np.arange(n, dtype=np.uint64) * msg_sz).astype(np.uint32)
+    msz = np.full(n, msg_sz, np.uint32)
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+    d_prv, d_pool = t(prvs), t(pool)
+    d_off, d_sz = t(moff.view(np.int32)), t(msz.view(np.int32))
+    d_pub = torch.empty((n, 32), dtype=torch.uint8, device=dev)
+    d_sig = torch.empty((n, 64), dtype=torch.uint8, device=dev)
+    verifier.sign_dev(n, d_prv, d_pool, d_off, d_sz, d_pub, d_sig)
+    verifier.sync()
+    kinds = None
+    if mix == "c2":
+        sigs = d_sig.cpu().numpy(); pubs = d_pub.cpu().numpy()
+        kinds = c2_mutate(sigs, pubs, np.random.default_rng(seed ^ 0xc2))
+        d_sig.copy_(torch.from_numpy(sigs)); d_pub.copy_(torch.from_numpy(pubs))
+    return Batch(dev, d_sig, d_pub, d_pool, d_off, d_sz, kinds)

@@ -1,0 +1,161 @@
+#ifndef HEADER_fd_ed25519_hip_h
+#define HEADER_fd_ed25519_hip_h
+
+/* fd_ed25519_hip.h -- C ABI of the MI355X (gfx950) ed25519 verify engine.
+
+   Drop-in boundary for the reference's verify path
+   (anoushk1234/firedancer, src/ballet/ed25519/fd_ed25519.h).  Part 1 is
+   link-compatible with the reference declarations it replaces; part 2 is the
+   GPU-native bulk interface the verify tile's batches go through (the
+   reference has no such entry; the precedent is the async wiredancer offload,
+   src/wiredancer/c/wd_f1.h:71-112).  No torch or HIP types appear in any
+   signature: plain pointers and sizes only.
+
+   Library: firedancer_amd/libfd_ed25519_hip.so (built by __graft_entry__.build()).
+   The reference-side bindings a maintainer would add are in INTEGRATION.md. */
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef unsigned char uchar;
+typedef unsigned long ulong;
+typedef unsigned int  uint;
+
+/* Result codes: fd_ed25519.h:11-14 */
+#define FD_ED25519_SUCCESS    ( 0)
+#define FD_ED25519_ERR_SIG    (-1)
+#define FD_ED25519_ERR_PUBKEY (-2)
+#define FD_ED25519_ERR_MSG    (-3)
+
+/* ---- Part 1: reference API (link-compatible) ----------------------------
+
+   fd_sha512_t is opaque here (footprint 256, align 128: fd_sha512.h:56-77);
+   the GPU engine takes no interest in it (the reference uses it as scratch).
+   Semantics, including the order of the checks and the error code of every
+   reject, are those of the reference's AVX-512 build (fd_ed25519_user.c with
+   avx512/fd_r43x6_ge.c decode); fd_ed25519_hip_set_errmode() switches the
+   error codes to the portable build's (the accept/reject bit is the same). */
+
+struct fd_sha512_private;
+
+/* replaces fd_ed25519_verify, fd_ed25519.h:96-101 (fd_ed25519_user.c:135-230) */
+int
+fd_ed25519_verify( uchar const                msg[], /* msg_sz */
+                   ulong                      msg_sz,
+                   uchar const                sig[ 64 ],
+                   uchar const                public_key[ 32 ],
+                   struct fd_sha512_private * sha );
+
+/* replaces fd_ed25519_verify_batch_single_msg, fd_ed25519.h:124-130
+   (fd_ed25519_user.c:232-310): batch_sz 0 or >16 -> ERR_SIG; otherwise the
+   first pre-check failure in signature order, else ERR_MSG if any equation
+   fails, else SUCCESS. */
+int
+fd_ed25519_verify_batch_single_msg( uchar const                msg[], /* msg_sz */
+                                    ulong const                msg_sz,
+                                    uchar const                signatures[ 64 ], /* 64*batch_sz */
+                                    uchar const                pubkeys[ 32 ],    /* 32*batch_sz */
+                                    struct fd_sha512_private * shas[ 1 ],        /* batch_sz, ignored */
+                                    uchar const                batch_sz );
+
+/* replaces fd_ed25519_strerror, fd_ed25519.h:137-138 (fd_ed25519_user.c:312-322) */
+char const *
+fd_ed25519_strerror( int err );
+
+/* ---- Part 2: GPU-native bulk interface -----------------------------------
+
+   A context owns one HIP device, one stream, the LDS-staged base-point table
+   and the scratch for up to chunk_sigs signatures in flight per launch
+   (larger requests are processed in chunks of chunk_sigs).  Contexts are not
+   thread-safe; use one per host thread (one per verify tile).
+
+   Record layout (all pointers are device pointers for *_dev, host pointers
+   otherwise):
+     sigs     64*n bytes   sig i = R||S  (fd_ed25519_sig_t, fd_ed25519.h:17-20)
+     pubs     32*n bytes
+     pool     message bytes; message i = pool[ msg_off[i], msg_off[i]+msg_sz[i] )
+              (several signatures may share one message, as in a txn)
+     codes    n int8 results (FD_ED25519_* codes, fd_ed25519_verify semantics)
+     bitmap   ceil(n/64) ulong: bit i%64 of word i/64 set iff codes[i]==0
+   Device buffers for *_dev must be 16-byte aligned and the pool must stay
+   readable 16 bytes past its last message byte.
+
+   Any HIP failure aborts the process with a message on stderr (the tile
+   restarts) -- a device error is never reported as a rejected signature. */
+
+typedef struct fd_ed25519_hip_ctx fd_ed25519_hip_ctx_t;
+
+#define FD_ED25519_HIP_ERRMODE_AVX512 0   /* error codes of the AVX-512 build (default) */
+#define FD_ED25519_HIP_ERRMODE_REF    1   /* error codes of the portable build */
+
+fd_ed25519_hip_ctx_t * fd_ed25519_hip_ctx_new   ( int device, ulong chunk_sigs );
+void                   fd_ed25519_hip_ctx_delete( fd_ed25519_hip_ctx_t * ctx );
+int                    fd_ed25519_hip_ctx_device( fd_ed25519_hip_ctx_t const * ctx );
+void *                 fd_ed25519_hip_ctx_stream( fd_ed25519_hip_ctx_t const * ctx ); /* hipStream_t */
+void                   fd_ed25519_hip_set_errmode( fd_ed25519_hip_ctx_t * ctx, int errmode );
+
+/* Per-signature verify, inputs resident in HBM, asynchronous on `stream`
+   (NULL: the context's stream).  bitmap may be NULL.  Returns 0. */
+int
+fd_ed25519_hip_verify_dev( fd_ed25519_hip_ctx_t * ctx,
+                           ulong                  n,
+                           uchar const *          d_sigs,
+                           uchar const *          d_pubs,
+                           uchar const *          d_pool,
+                           uint const *           d_msg_off,
+                           uint const *           d_msg_sz,
+                           signed char *          d_codes,
+                           ulong *                d_bitmap,
+                           void *                 stream );
+
+/* Same from host memory, synchronous (copies in/out over PCIe). */
+int
+fd_ed25519_hip_verify_host( fd_ed25519_hip_ctx_t * ctx,
+                            ulong                  n,
+                            uchar const *          sigs,
+                            uchar const *          pubs,
+                            uchar const *          pool,
+                            ulong                  pool_sz,
+                            uint const *           msg_off,
+                            uint const *           msg_sz,
+                            signed char *          codes,
+                            ulong *                bitmap );
+
+/* Group reduction with fd_ed25519_verify_batch_single_msg semantics: group g
+   covers signatures [first[g], first[g]+cnt[g]) of a preceding verify; its
+   code is ERR_SIG if cnt is 0 or >16, else the first ERR_SIG/ERR_PUBKEY in
+   order, else ERR_MSG if any signature failed its equation, else SUCCESS.
+   Device pointers, asynchronous on `stream`. */
+int
+fd_ed25519_hip_group_reduce_dev( fd_ed25519_hip_ctx_t * ctx,
+                                 ulong                  n_groups,
+                                 uint const *           d_first,
+                                 uchar const *          d_cnt,
+                                 signed char const *    d_sig_codes,
+                                 signed char *          d_group_codes,
+                                 void *                 stream );
+
+/* Key generation + signing on the GPU (synthetic workloads, fd_ed25519_user.c
+   :4-133 semantics; NOT hardened against side channels: do not use with
+   secrets you care about).  prvs 32*n, writes pubs 32*n and sigs 64*n.
+   Device pointers, asynchronous on `stream`. */
+int
+fd_ed25519_hip_sign_dev( fd_ed25519_hip_ctx_t * ctx,
+                         ulong                  n,
+                         uchar const *          d_prvs,
+                         uchar const *          d_pool,
+                         uint const *           d_msg_off,
+                         uint const *           d_msg_sz,
+                         uchar *                d_pubs,
+                         uchar *                d_sigs,
+                         void *                 stream );
+
+/* Blocks until all work queued on the context's stream is done. */
+int fd_ed25519_hip_sync( fd_ed25519_hip_ctx_t * ctx );
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* HEADER_fd_ed25519_hip_h */

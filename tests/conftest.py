@@ -1,0 +1,38 @@
+import json
+import os
+import sys
+
+import numpy as np
+import pytest
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(HERE)
+sys.path.insert(0, REPO)
+sys.path.insert(0, HERE)
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs an MI355X (run on the GPU box)")
+
+
+@pytest.fixture(scope="session")
+def kat():
+    with open(os.path.join(HERE, "golden", "kat_vectors.json")) as f:
+        return json.load(f)
+
+
+@pytest.fixture(scope="session")
+def c2mix():
+    d = np.load(os.path.join(HERE, "golden", "c2_mix_4096.npz"))   # allow_pickle=False (default)
+    return {k: d[k] for k in d.files}
+
+
+@pytest.fixture(scope="session")
+def verifier():
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from firedancer_amd import Verifier
+    v = Verifier(device=0, chunk_sigs=1 << 18)
+    yield v
+    v.close()

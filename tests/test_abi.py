@@ -1,0 +1,50 @@
+"""CPU: the C-ABI library loads and exports every symbol include/*.h declares
+(no compute calls without a GPU)."""
+import ctypes
+import os
+import re
+import subprocess
+
+from firedancer_amd import ed25519
+from firedancer_amd.build import LIB, build
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def declared_functions():
+    hdr = open(os.path.join(REPO, "include", "fd_ed25519_hip.h")).read()
+    hdr = re.sub(r"/\*.*?\*/", "", hdr, flags=re.S)
+    names = set(re.findall(r"\b(fd_ed25519\w*)\s*\(", hdr))
+    return names
+
+
+def test_build_and_exports():
+    build()
+    assert os.path.exists(LIB)
+    names = declared_functions()
+    assert names == set(ed25519.EXPORTS)
+    out = subprocess.check_output(["nm", "-D", "--defined-only", LIB]).decode()
+    exported = set(re.findall(r" T (\w+)", out))
+    assert names <= exported, names - exported
+    lib = ctypes.CDLL(LIB)
+    for n in names:
+        assert getattr(lib, n)
+
+
+def test_strerror_matches_reference():
+    # fd_ed25519_user.c:312-322 (no GPU needed: pure host function)
+    assert ed25519.fd_ed25519_strerror(0) == "success"
+    assert ed25519.fd_ed25519_strerror(-1) == "bad signature"
+    assert ed25519.fd_ed25519_strerror(-2) == "bad public key"
+    assert ed25519.fd_ed25519_strerror(-3) == "bad message"
+    assert ed25519.fd_ed25519_strerror(7) == "unknown"
+
+
+def test_no_reference_or_oracle_in_product():
+    """The product package must not load the oracle or read /root/reference."""
+    pkg = os.path.join(REPO, "firedancer_amd")
+    for root, _, files in os.walk(pkg):
+        for f in files:
+            if f.endswith((".py", ".hip", ".h")):
+                s = open(os.path.join(root, f)).read()
+                assert "liboracle" not in s and "oracle_lib" not in s and "/root/reference" not in s, f
