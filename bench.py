@@ -1,0 +1,215 @@
+#!/usr/bin/env python3
+"""bench.py -- ed25519 verifies/s on MI355X (BASELINE.json metric), one JSON line.
+
+A step is one verify pass (k_verify_prep + k_verify_dsm) over one batch of
+2^20 signatures resident in HBM: BASELINE config 2 ("same 1M-sig batch on one
+MI355X with 10% corrupted sigs plus non-canonical R/A, S>=L and small-order
+points"), 64-byte messages, keys/signatures generated on the GPU by the
+engine's own signer, mutated with the C2 model (firedancer_amd/workload.py).
+
+Multi-GPU (python -m torch.distributed.run --nproc-per-node N bench.py --gpus N):
+one process per GPU, each verifies its own 2^20-signature shard (weak scaling,
+no data-path collective: signatures are independent); RCCL is used only for
+the barrier and the max-over-ranks time.
+
+Roofline: INT32 VALU.  Algorithmic work per verify
+W = 304*N_M + 200*N_S + 4900*N_blk 32-bit-op equivalents (N_M = 1378.6,
+N_S = 1518.1 field mul/sqr of the reference algorithm, N_blk SHA-512 blocks);
+W = 7.33e5 at 64 B.  The dominant kernel, k_verify_dsm, carries the
+double-scalar multiplication part: W_dsm = 304*(1378.6-42) + 200*(1518.1-510)
+= 6.08e5 per signature that reaches it (the two point decodes -- 42 M + 510 S
+-- and SHA-512 run in k_verify_prep).  Peak: 256 CU x 4 SIMD x 16 lanes x
+2.4 GHz = 39.3e12 32-bit lane-ops/s (VOP3 integer issue rate, measured at
+36-38e12 for v_mad_u64_u32 / v_addc_co_u32 in profiles/r01_valu_rates_*.txt).
+The kernel duration is measured live with HIP events on the launch stream.
+
+cpu_baseline (rank 0, N=1): the reference's own fd_ed25519_verify (AVX-512
+IFMA build, compiled from the reference sources into oracle/_ref/) on a
+bounded 65536-record sample of the same batch, one pinned thread per core.
+"""
+import argparse
+import json
+import os
+import subprocess
+import sys
+import tempfile
+import time
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+METRIC = "ed25519 verifies/sec (1/2/4/8 MI355X) + % of INT32 VALU peak"
+N_M, N_S = 1378.6, 1518.1
+N_M_DECODE, N_S_DECODE = 42.0, 510.0
+PEAK_OPS = 256 * 4 * 16 * 2.4e9          # 39.3e12 int32 lane-ops/s
+
+
+def w_total(msg_sz):
+    nblk = -(-(msg_sz + 81) // 128)
+    return 304 * N_M + 200 * N_S + 4900 * nblk
+
+
+W_DSM = 304 * (N_M - N_M_DECODE) + 200 * (N_S - N_S_DECODE)
+
+
+def write_fdv1(path, sigs, pubs, pool, moff, msz):
+    with open(path, "wb") as f:
+        f.write(b"FDV1")
+        f.write(np.array([sigs.shape[0], pool.size, 0], np.uint64).tobytes())
+        f.write(np.ascontiguousarray(sigs).tobytes()); f.write(np.ascontiguousarray(pubs).tobytes())
+        f.write(np.ascontiguousarray(moff, np.uint32).tobytes()); f.write(np.ascontiguousarray(msz, np.uint32).tobytes())
+        f.write(np.ascontiguousarray(pool).tobytes())
+
+
+def cpu_baseline(sigs, pubs, pool, moff, msz, gpu_codes, threads, target_s):
+    """Time the reference's own verify on the host (bounded sample)."""
+    has_ifma = "avx512ifma" in open("/proc/cpuinfo").read()
+    exe = os.path.join(REPO, "oracle", "_ref", "ref_cpu_bench_avx512" if has_ifma else "ref_cpu_bench_ref")
+    kind, backend = "reference", ("avx512" if has_ifma else "portable")
+    if not os.path.exists(exe):
+        return {"value": None, "unit": "verifies/s", "cores": 0, "kind": "reference",
+                "sample": "unavailable: oracle/_ref not built on this box"}
+    with tempfile.TemporaryDirectory() as td:
+        inp = os.path.join(td, "in.bin"); out = os.path.join(td, "codes.bin")
+        write_fdv1(inp, sigs, pubs, pool, moff, msz)
+        # one core, short pass: per-core rate and calibration
+        r1 = json.loads(subprocess.check_output([exe, inp, "1", "-", "0", "1"], timeout=600).decode())
+        rate1 = r1["rate"]
+        n = sigs.shape[0]
+        rep = max(1, int(round(target_s * rate1 * threads / n)))
+        r = json.loads(subprocess.check_output([exe, inp, str(threads), out, "0", str(rep)], timeout=900).decode())
+        ref_codes = np.fromfile(out, np.int8)
+    return {"value": round(r["rate"], 1), "unit": "verifies/s", "cores": threads, "kind": kind,
+            "backend": backend, "per_core": round(rate1, 1),
+            "sample": f"{n} records of the same C2 batch x {rep} passes ({r['verifies']} verifies, "
+                      f"{r['seconds']:.2f} s wall, {threads} pinned threads)",
+            "bitmap_match": bool(np.array_equal(ref_codes == 0, gpu_codes == 0)),
+            "codes_match": bool(np.array_equal(ref_codes, gpu_codes))}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--sigs", type=int, default=1 << 20, help="signatures per GPU per step")
+    ap.add_argument("--msg-sz", type=int, default=64)
+    ap.add_argument("--mix", default="c2", choices=["c1", "c2"])
+    ap.add_argument("--cpu-threads", type=int, default=16)
+    ap.add_argument("--cpu-seconds", type=float, default=8.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    args = ap.parse_args()
+
+    import torch
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    from firedancer_amd import Verifier
+    from firedancer_amd.workload import make_batch_gpu
+
+    n = args.sigs
+    v = Verifier(device=local, chunk_sigs=n)
+    batch = make_batch_gpu(v, n, msg_sz=args.msg_sz, seed=0x5eed0001 + 7919 * rank, mix=args.mix)
+    dev = batch.dev
+    codes = torch.zeros(n, dtype=torch.int8, device=dev)
+    bitmap = torch.zeros((n + 63) // 64, dtype=torch.int64, device=dev)
+
+    def step():
+        v.verify_dev(n, batch.sigs, batch.pubs, batch.pool, batch.msg_off, batch.msg_sz, codes, bitmap)
+
+    for _ in range(args.warmup):
+        step()
+    v.sync(); torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    v.set_timing(True)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    v.sync(); torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    prep_ms, dsm_ms, launches = v.get_timing()
+    v.set_timing(False)
+    elapsed = t1 - t0
+    if dist:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    c = codes.cpu().numpy()
+    bm = bitmap.cpu().numpy().view(np.uint64)
+    bits = np.unpackbits(bm.view(np.uint8), bitorder="little")[:n].astype(bool)
+    assert np.array_equal(bits, c == 0), "bitmap != codes"
+    reached_dsm = int(np.isin(c, (0, -3)).sum())          # passed every pre-check
+    accept = float((c == 0).mean())
+
+    total = n * world * args.steps
+    value = total / elapsed
+    dsm_avg_ms = dsm_ms / max(launches, 1)
+    prep_avg_ms = prep_ms / max(launches, 1)
+    achieved = reached_dsm * W_DSM / (dsm_avg_ms * 1e-3) / 1e12        # T int32-ops/s, per GPU
+    peak = PEAK_OPS / 1e12
+    pipeline_frac = (n * w_total(args.msg_sz)) / ((prep_avg_ms + dsm_avg_ms) * 1e-3) / PEAK_OPS
+
+    out = None
+    if rank == 0:
+        cpu = None
+        if not args.no_cpu_baseline and world == 1:
+            k = min(65536, n)
+            idx = slice(0, k)
+            sigs = batch.sigs[idx].cpu().numpy(); pubs = batch.pubs[idx].cpu().numpy()
+            moff = batch.msg_off[idx].cpu().numpy().view(np.uint32)
+            msz = batch.msg_sz[idx].cpu().numpy().view(np.uint32)
+            lo = int(moff.min()); hi = int((moff.astype(np.int64) + msz).max())
+            pool = batch.pool[lo:hi].cpu().numpy()
+            threads = max(1, min(args.cpu_threads, os.cpu_count() or 1))
+            cpu = cpu_baseline(sigs, pubs, pool, moff - lo, msz, c[idx], threads, args.cpu_seconds)
+        out = {
+            "metric": METRIC,
+            "value": round(value, 1),
+            "unit": "verifies/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u32",
+            "data": "synthetic (GPU-signed random keys, C2 mutation model)",
+            "config": {"workload": f"config 2: {n} sigs/GPU, {args.msg_sz}-B msgs, "
+                                   f"{'C2 validity mix' if args.mix == 'c2' else 'all valid'}",
+                       "sigs_per_gpu": n, "msg_sz": args.msg_sz, "parallelism": f"dp{world} (signature shards)"},
+            "accept_rate": round(accept, 5),
+            "roofline": {"bound": "valu_int32", "kernel": "k_verify_dsm",
+                         "achieved": round(achieved, 3), "peak": round(peak, 3), "unit": "Tops/s",
+                         "frac": round(achieved / peak, 4), "traffic": None,
+                         "algorithmic_ops_per_unit": round(W_DSM), "units_per_launch": reached_dsm,
+                         "avg_launch_ms": round(dsm_avg_ms, 4)},
+            "pipeline": {"prep_ms": round(prep_avg_ms, 4), "dsm_ms": round(dsm_avg_ms, 4),
+                         "w_total_per_verify": round(w_total(args.msg_sz)),
+                         "int32_valu_frac": round(pipeline_frac, 4)},
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(out), flush=True)
+    v.close()
+    if dist:
+        dist.barrier()
+        dist.destroy_process_group()
+    return out
+
+
+if __name__ == "__main__":
+    main()

@@ -66,6 +66,11 @@ struct fd_ed25519_hip_ctx {
   u32 *        d_state;     /* ST_WORDS * chunk */
   u32 *        d_atab;      /* ATAB_WORDS * chunk */
   int          errmode;
+  /* optional per-kernel timing (HIP events around each launch, on the launch stream) */
+  int          timing;
+  double       prep_ms, dsm_ms;
+  ulong        prep_launches, dsm_launches;
+  hipEvent_t   ev[4];
   /* staging for the host-memory entry points (grown on demand) */
   ulong        h_cap_n, h_cap_pool, h_cap_groups;
   uchar *      d_sigs; uchar * d_pubs; uchar * d_pool; uint * d_moff; uint * d_msz;
@@ -410,6 +415,7 @@ fd_ed25519_hip_ctx_new( int device, ulong chunk_sigs ) {
   FD_CHECK( hipMalloc( (void **)&ctx->d_btab,  BTAB_WORDS * sizeof(u32) ) );
   FD_CHECK( hipMalloc( (void **)&ctx->d_state, (size_t)ST_WORDS * chunk_sigs * sizeof(u32) ) );
   FD_CHECK( hipMalloc( (void **)&ctx->d_atab,  (size_t)ATAB_WORDS * chunk_sigs * sizeof(u32) ) );
+  for( int e=0; e<4; e++ ) FD_CHECK( hipEventCreate( &ctx->ev[e] ) );
   hipLaunchKernelGGL( k_btab_init, dim3( (BTAB_N + 63)/64 ), dim3( 64 ), 0, ctx->stream, ctx->d_btab );
   FD_CHECK( hipGetLastError() );
   FD_CHECK( hipStreamSynchronize( ctx->stream ) );
@@ -429,6 +435,7 @@ fd_ed25519_hip_ctx_delete( fd_ed25519_hip_ctx_t * ctx ) {
   (void)hipStreamSynchronize( ctx->stream );
   (void)hipFree( ctx->d_btab ); (void)hipFree( ctx->d_state ); (void)hipFree( ctx->d_atab );
   free_staging( ctx );
+  for( int e=0; e<4; e++ ) (void)hipEventDestroy( ctx->ev[e] );
   (void)hipStreamDestroy( ctx->stream );
   free( ctx );
 }
@@ -436,6 +443,18 @@ fd_ed25519_hip_ctx_delete( fd_ed25519_hip_ctx_t * ctx ) {
 int   fd_ed25519_hip_ctx_device( fd_ed25519_hip_ctx_t const * ctx ) { return ctx->device; }
 void *fd_ed25519_hip_ctx_stream( fd_ed25519_hip_ctx_t const * ctx ) { return (void *)ctx->stream; }
 void  fd_ed25519_hip_set_errmode( fd_ed25519_hip_ctx_t * ctx, int m ) { ctx->errmode = m; }
+
+void
+fd_ed25519_hip_set_timing( fd_ed25519_hip_ctx_t * ctx, int on ) {
+  ctx->timing = on; ctx->prep_ms = ctx->dsm_ms = 0.0; ctx->prep_launches = ctx->dsm_launches = 0UL;
+}
+
+void
+fd_ed25519_hip_get_timing( fd_ed25519_hip_ctx_t const * ctx, double * prep_ms, double * dsm_ms, ulong * launches ) {
+  if( prep_ms ) *prep_ms = ctx->prep_ms;
+  if( dsm_ms ) *dsm_ms = ctx->dsm_ms;
+  if( launches ) *launches = ctx->dsm_launches;
+}
 
 int
 fd_ed25519_hip_verify_dev( fd_ed25519_hip_ctx_t * ctx, ulong n, uchar const * d_sigs, uchar const * d_pubs,
@@ -446,12 +465,24 @@ fd_ed25519_hip_verify_dev( fd_ed25519_hip_ctx_t * ctx, ulong n, uchar const * d_
   for( ulong off = 0; off < n; off += ctx->chunk ) {
     ulong m = n - off < ctx->chunk ? n - off : ctx->chunk;
     dim3 grid( (unsigned)((m + 255) / 256) ), blk( 256 );
+    if( ctx->timing ) FD_CHECK( hipEventRecord( ctx->ev[0], s ) );
     hipLaunchKernelGGL( k_verify_prep, grid, blk, 0, s, m, ctx->chunk, d_sigs + 64*off, d_pubs + 32*off,
                         d_pool, d_msg_off + off, d_msg_sz + off, ctx->d_state );
     FD_CHECK( hipGetLastError() );
+    if( ctx->timing ) FD_CHECK( hipEventRecord( ctx->ev[1], s ) );
     hipLaunchKernelGGL( k_verify_dsm, grid, blk, 0, s, m, ctx->chunk, ctx->d_state, ctx->d_btab, ctx->d_atab,
                         ctx->errmode, d_codes + off, d_bitmap ? d_bitmap + off/64 : (ulong *)NULL );
     FD_CHECK( hipGetLastError() );
+    if( ctx->timing ) {
+      /* timing mode serialises the host with each chunk; it is meant for the
+         measured bench leg only */
+      FD_CHECK( hipEventRecord( ctx->ev[2], s ) );
+      FD_CHECK( hipEventSynchronize( ctx->ev[2] ) );
+      float a, b;
+      FD_CHECK( hipEventElapsedTime( &a, ctx->ev[0], ctx->ev[1] ) );
+      FD_CHECK( hipEventElapsedTime( &b, ctx->ev[1], ctx->ev[2] ) );
+      ctx->prep_ms += a; ctx->dsm_ms += b; ctx->prep_launches++; ctx->dsm_launches++;
+    }
   }
   return 0;
 }

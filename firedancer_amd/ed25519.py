@@ -28,7 +28,7 @@ EXPORTS = (
     "fd_ed25519_hip_ctx_new", "fd_ed25519_hip_ctx_delete", "fd_ed25519_hip_ctx_device",
     "fd_ed25519_hip_ctx_stream", "fd_ed25519_hip_set_errmode", "fd_ed25519_hip_verify_dev",
     "fd_ed25519_hip_verify_host", "fd_ed25519_hip_group_reduce_dev", "fd_ed25519_hip_sign_dev",
-    "fd_ed25519_hip_sync",
+    "fd_ed25519_hip_sync", "fd_ed25519_hip_set_timing", "fd_ed25519_hip_get_timing",
 )
 
 _lib = None
@@ -65,6 +65,8 @@ def lib():
         L.fd_ed25519_hip_group_reduce_dev.argtypes = [vp, u64, vp, vp, vp, vp, vp]
         L.fd_ed25519_hip_sign_dev.restype = c.c_int
         L.fd_ed25519_hip_sign_dev.argtypes = [vp, u64, vp, vp, vp, vp, vp, vp, vp]
+        L.fd_ed25519_hip_set_timing.argtypes = [vp, c.c_int]
+        L.fd_ed25519_hip_get_timing.argtypes = [vp, c.POINTER(c.c_double), c.POINTER(c.c_double), c.POINTER(u64)]
         L.fd_ed25519_hip_sync.restype = c.c_int
         L.fd_ed25519_hip_sync.argtypes = [vp]
         _lib = L
@@ -159,6 +161,15 @@ class Verifier:
     def sign_dev(self, n, prvs, pool, msg_off, msg_sz, pubs, sigs, stream=None):
         return self._lib.fd_ed25519_hip_sign_dev(self.ctx, int(n), _ptr(prvs), _ptr(pool), _ptr(msg_off),
                                                  _ptr(msg_sz), _ptr(pubs), _ptr(sigs), stream)
+
+    def set_timing(self, on):
+        self._lib.fd_ed25519_hip_set_timing(self.ctx, 1 if on else 0)
+
+    def get_timing(self):
+        """(prep_ms, dsm_ms, launches) accumulated since set_timing()."""
+        a, b, n = ctypes.c_double(), ctypes.c_double(), ctypes.c_ulong()
+        self._lib.fd_ed25519_hip_get_timing(self.ctx, ctypes.byref(a), ctypes.byref(b), ctypes.byref(n))
+        return a.value, b.value, n.value
 
     def sync(self):
         self._lib.fd_ed25519_hip_sync(self.ctx)

@@ -95,6 +95,14 @@ int                    fd_ed25519_hip_ctx_device( fd_ed25519_hip_ctx_t const * c
 void *                 fd_ed25519_hip_ctx_stream( fd_ed25519_hip_ctx_t const * ctx ); /* hipStream_t */
 void                   fd_ed25519_hip_set_errmode( fd_ed25519_hip_ctx_t * ctx, int errmode );
 
+/* Kernel timing for measurement legs: when on, every verify chunk brackets
+   k_verify_prep and k_verify_dsm with HIP events on the launch stream and
+   accumulates their durations (this serialises the host per chunk).
+   set_timing also resets the accumulators. */
+void fd_ed25519_hip_set_timing( fd_ed25519_hip_ctx_t * ctx, int on );
+void fd_ed25519_hip_get_timing( fd_ed25519_hip_ctx_t const * ctx, double * prep_ms, double * dsm_ms,
+                                ulong * launches );
+
 /* Per-signature verify, inputs resident in HBM, asynchronous on `stream`
    (NULL: the context's stream).  bitmap may be NULL.  Returns 0. */
 int

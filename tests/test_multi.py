@@ -1,0 +1,53 @@
+"""CPU: the N>1 path (signature shards + bitmap gather + max-over-ranks) on a
+world_size-2 gloo group."""
+import os
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from firedancer_amd.shard import gather_bitmap, max_over_ranks, shard_bounds
+
+
+def test_shard_bounds_partition():
+    for n in (0, 1, 63, 64, 65, 1000, 1 << 20, (1 << 26) + 5):
+        for world in (1, 2, 3, 4, 8):
+            cover = []
+            for r in range(world):
+                lo, hi = shard_bounds(n, r, world)
+                assert lo % 64 == 0 and (hi % 64 == 0 or hi == n)
+                cover.append((lo, hi))
+            assert cover[0][0] == 0 and cover[-1][1] == n
+            for (a, b), (c, d) in zip(cover, cover[1:]):
+                assert b == c
+
+
+def _worker(rank, world, port, n, ret):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    rng = np.random.default_rng(42)
+    codes = rng.integers(-3, 1, n).astype(np.int8)           # same global "verdicts" on every rank
+    lo, hi = shard_bounds(n, rank, world)
+    mine = codes[lo:hi] == 0                                   # this rank's shard verdicts
+    bits = np.packbits(mine, bitorder="little")
+    bits = np.concatenate([bits, np.zeros((-bits.size) % 8, np.uint8)]).view(np.int64)
+    full = gather_bitmap(torch.from_numpy(bits.copy()), n, rank, world)
+    got = np.unpackbits(full.numpy().view(np.uint8), bitorder="little")[:n].astype(bool)
+    ok = bool(np.array_equal(got, codes == 0))
+    t = max_over_ranks(1.0 + rank)
+    ret[rank] = (ok, t)
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("n", [1000, 4096 + 17])
+def test_gloo_world2_bitmap_gather(n):
+    world = 2
+    mgr = mp.Manager()
+    ret = mgr.dict()
+    port = 29500 + (os.getpid() % 1000)
+    mp.spawn(_worker, args=(world, port, n, ret), nprocs=world, join=True)
+    assert all(ret[r][0] for r in range(world))
+    assert all(ret[r][1] == float(world) for r in range(world))
