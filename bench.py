@@ -18,9 +18,13 @@ N_S = 1518.1 field mul/sqr of the reference algorithm, N_blk SHA-512 blocks);
 W = 7.33e5 at 64 B.  The dominant kernel, k_verify_dsm, carries the
 double-scalar multiplication part: W_dsm = 304*(1378.6-42) + 200*(1518.1-510)
 = 6.08e5 per signature that reaches it (the two point decodes -- 42 M + 510 S
--- and SHA-512 run in k_verify_prep).  Peak: 256 CU x 4 SIMD x 16 lanes x
-2.4 GHz = 39.3e12 32-bit lane-ops/s (VOP3 integer issue rate, measured at
-36-38e12 for v_mad_u64_u32 / v_addc_co_u32 in profiles/r01_valu_rates_*.txt).
+-- and SHA-512 run in k_verify_prep).  W prices a 32x32->64 product as four
+single-rate 32-bit ops (lo, hi, add, addc), so the matching peak is the VALU
+lane rate at which single-rate 32-bit ops issue: 256 CU x 4 SIMD x 32 lanes x
+2.4 GHz = 78.6e12 ops/s (MI355X_MICROARCH.md: CDNA4 SIMDs are 32-wide; the
+157.3 TFLOPS FP32 vector peak is 2 x this).  On gfx950 the fused
+v_mad_u64_u32 (lo+hi+add) and v_addc_co_u32 issue at half that lane rate
+(profiles/r01_valu_rates_*.txt), i.e. two half-rate slots = the four W ops.
 The kernel duration is measured live with HIP events on the launch stream.
 
 cpu_baseline (rank 0, N=1): the reference's own fd_ed25519_verify (AVX-512
@@ -43,7 +47,7 @@ sys.path.insert(0, REPO)
 METRIC = "ed25519 verifies/sec (1/2/4/8 MI355X) + % of INT32 VALU peak"
 N_M, N_S = 1378.6, 1518.1
 N_M_DECODE, N_S_DECODE = 42.0, 510.0
-PEAK_OPS = 256 * 4 * 16 * 2.4e9          # 39.3e12 int32 lane-ops/s
+PEAK_OPS = 256 * 4 * 32 * 2.4e9          # 78.6e12 int32 lane-ops/s (32-wide SIMDs)
 
 
 def w_total(msg_sz):
