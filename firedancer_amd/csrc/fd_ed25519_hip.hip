@@ -11,6 +11,9 @@
                     for A, radix 256 for B: every lane adds at the same
                     positions, so the wave never diverges on digits);
                     projective compare with R; int8 code + verdict bitmap
+     k_compact      final codes of pre-check failures; survivors -> idx[]
+                    (k_verify_dsm runs only survivors)
+     k_bitmap       verdict bitmap from codes (64-bit ballot per wave)
      k_group_reduce batch_single_msg / per-txn semantics over sig codes
 
    Reference semantics: fd_ed25519_user.c:135-310 (see fd_ed25519_dev.h for
@@ -65,6 +68,8 @@ struct fd_ed25519_hip_ctx {
   u32 *        d_btab;      /* BTAB_WORDS */
   u32 *        d_state;     /* ST_WORDS * chunk */
   u32 *        d_atab;      /* ATAB_WORDS * chunk */
+  u32 *        d_idx;       /* chunk: compacted survivor indices */
+  u32 *        d_count;     /* survivor count */
   int          errmode;
   /* optional per-kernel timing (HIP events around each launch, on the launch stream) */
   int          timing;
@@ -196,22 +201,53 @@ DEV void digits_shl( u32 d[8], u32 bits ) {
   d[0] <<= bits;
 }
 
+/* Survivor compaction: signatures that fail a pre-check get their final code
+   here; the others are appended (wave-aggregated atomic) to idx[] so that
+   k_verify_dsm spends no lanes on them (the DSM is VALU-issue bound, so a
+   masked lane costs as much as a live one). */
 __global__ __launch_bounds__(256)
-void k_verify_dsm( ulong n, ulong chunk, u32 const * __restrict__ st, u32 const * __restrict__ btab,
-                   u32 * __restrict__ atab, int errmode, signed char * __restrict__ codes,
-                   ulong * __restrict__ bitmap ) {
-  __shared__ __attribute__((aligned(16))) u32 lds_btab[BTAB_WORDS];
-  for( int t = threadIdx.x; t < BTAB_WORDS/4; t += blockDim.x )
-    ((uint4 *)lds_btab)[t] = ((uint4 const *)btab)[t];
-  __syncthreads();
-
+void k_compact( ulong n, ulong chunk, u32 const * __restrict__ st, int errmode, u32 * __restrict__ idx,
+                u32 * __restrict__ count, signed char * __restrict__ codes ) {
   ulong i = (ulong)blockIdx.x * blockDim.x + threadIdx.x;
   bool active = i < n;
-  ulong ii = active ? i : 0;
-  u32 const * s = st + ii;
-  u32 flags = s[ST_FLAG*chunk];
+  u32 flags = active ? st[ST_FLAG*chunk + i] : 0u;
+  bool pass = active && code_of( flags, FD_ED25519_HIP_ERRMODE_AVX512, true ) == FD_ED25519_SUCCESS;
+  if( active && !pass ) codes[i] = (signed char)code_of( flags, errmode, false );
+  unsigned long long m = __ballot( pass );
+  u32 lane = threadIdx.x & 63u;
+  u32 base = 0;
+  if( lane == 0u && m ) base = atomicAdd( count, (u32)__popcll( m ) );
+  base = __shfl( base, 0 );
+  u32 below = (u32)__popcll( m & ((1ULL << lane) - 1ULL) );
+  if( pass ) idx[base + below] = (u32)i;
+}
+
+/* verdict bitmap from codes: bit i%64 of word i/64 set iff codes[i]==0 */
+__global__ __launch_bounds__(256)
+void k_bitmap( ulong n, signed char const * __restrict__ codes, ulong * __restrict__ bitmap ) {
+  ulong i = (ulong)blockIdx.x * blockDim.x + threadIdx.x;
+  bool ok = i < n && codes[i] == FD_ED25519_SUCCESS;
+  unsigned long long b = __ballot( ok );
+  if( (threadIdx.x & 63u) == 0u && i < n ) bitmap[i >> 6] = b;
+}
+
+__global__ __launch_bounds__(256)
+void k_verify_dsm( ulong chunk, u32 const * __restrict__ st, u32 const * __restrict__ btab,
+                   u32 * __restrict__ atab, u32 const * __restrict__ idx, u32 const * __restrict__ count,
+                   signed char * __restrict__ codes ) {
+  ulong t = (ulong)blockIdx.x * blockDim.x + threadIdx.x;
+  u32 m = *count;
+  if( (ulong)blockIdx.x * blockDim.x >= m ) return;        /* whole workgroup past the survivors */
+  __shared__ __attribute__((aligned(16))) u32 lds_btab[BTAB_WORDS];
+  for( int q = threadIdx.x; q < BTAB_WORDS/4; q += blockDim.x )
+    ((uint4 *)lds_btab)[q] = ((uint4 const *)btab)[q];
+  __syncthreads();
+  if( t >= m ) return;
+  ulong i = idx[t];
+  ulong ii = t;                                            /* A-table slot: dense in t */
+  u32 const * s = st + i;
   bool eq = false;
-  if( active && code_of( flags, FD_ED25519_HIP_ERRMODE_AVX512, true ) == FD_ED25519_SUCCESS ) {
+  {
     /* ---- recode scalars (fixed signed windows) ---- */
     u32 k[8], S[8], kd[8], sd[8];
     #pragma unroll
@@ -279,10 +315,7 @@ void k_verify_dsm( ulong n, ulong chunk, u32 const * __restrict__ st, u32 const 
     fe_mul( t, ry, P.Z ); fe_canon( t, t ); fe_canon( cy, P.Y );
     eq = ex && fe_eq_c( t, cy );
   }
-  int code = code_of( flags, errmode, eq );
-  if( active ) codes[i] = (signed char)code;
-  unsigned long long ball = __ballot( active && code == FD_ED25519_SUCCESS );
-  if( bitmap && (threadIdx.x & 63) == 0 && active ) bitmap[i >> 6] = ball;
+  codes[i] = (signed char)(eq ? FD_ED25519_SUCCESS : FD_ED25519_ERR_MSG);   /* user.c:226-229 */
 }
 
 /* fd_ed25519_verify_batch_single_msg (user.c:232-310) over per-sig codes */
@@ -415,6 +448,8 @@ fd_ed25519_hip_ctx_new( int device, ulong chunk_sigs ) {
   FD_CHECK( hipMalloc( (void **)&ctx->d_btab,  BTAB_WORDS * sizeof(u32) ) );
   FD_CHECK( hipMalloc( (void **)&ctx->d_state, (size_t)ST_WORDS * chunk_sigs * sizeof(u32) ) );
   FD_CHECK( hipMalloc( (void **)&ctx->d_atab,  (size_t)ATAB_WORDS * chunk_sigs * sizeof(u32) ) );
+  FD_CHECK( hipMalloc( (void **)&ctx->d_idx, chunk_sigs * sizeof(u32) ) );
+  FD_CHECK( hipMalloc( (void **)&ctx->d_count, 256 ) );
   for( int e=0; e<4; e++ ) FD_CHECK( hipEventCreate( &ctx->ev[e] ) );
   hipLaunchKernelGGL( k_btab_init, dim3( (BTAB_N + 63)/64 ), dim3( 64 ), 0, ctx->stream, ctx->d_btab );
   FD_CHECK( hipGetLastError() );
@@ -434,6 +469,7 @@ fd_ed25519_hip_ctx_delete( fd_ed25519_hip_ctx_t * ctx ) {
   (void)hipSetDevice( ctx->device );
   (void)hipStreamSynchronize( ctx->stream );
   (void)hipFree( ctx->d_btab ); (void)hipFree( ctx->d_state ); (void)hipFree( ctx->d_atab );
+  (void)hipFree( ctx->d_idx ); (void)hipFree( ctx->d_count );
   free_staging( ctx );
   for( int e=0; e<4; e++ ) (void)hipEventDestroy( ctx->ev[e] );
   (void)hipStreamDestroy( ctx->stream );
@@ -470,9 +506,18 @@ fd_ed25519_hip_verify_dev( fd_ed25519_hip_ctx_t * ctx, ulong n, uchar const * d_
                         d_pool, d_msg_off + off, d_msg_sz + off, ctx->d_state );
     FD_CHECK( hipGetLastError() );
     if( ctx->timing ) FD_CHECK( hipEventRecord( ctx->ev[1], s ) );
-    hipLaunchKernelGGL( k_verify_dsm, grid, blk, 0, s, m, ctx->chunk, ctx->d_state, ctx->d_btab, ctx->d_atab,
-                        ctx->errmode, d_codes + off, d_bitmap ? d_bitmap + off/64 : (ulong *)NULL );
+    FD_CHECK( hipMemsetAsync( ctx->d_count, 0, sizeof(u32), s ) );
+    hipLaunchKernelGGL( k_compact, grid, blk, 0, s, m, ctx->chunk, ctx->d_state, ctx->errmode, ctx->d_idx,
+                        ctx->d_count, d_codes + off );
     FD_CHECK( hipGetLastError() );
+    if( ctx->timing ) FD_CHECK( hipEventRecord( ctx->ev[3], s ) );
+    hipLaunchKernelGGL( k_verify_dsm, grid, blk, 0, s, ctx->chunk, ctx->d_state, ctx->d_btab, ctx->d_atab,
+                        ctx->d_idx, ctx->d_count, d_codes + off );
+    FD_CHECK( hipGetLastError() );
+    if( d_bitmap ) {
+      hipLaunchKernelGGL( k_bitmap, grid, blk, 0, s, m, d_codes + off, d_bitmap + off/64 );
+      FD_CHECK( hipGetLastError() );
+    }
     if( ctx->timing ) {
       /* timing mode serialises the host with each chunk; it is meant for the
          measured bench leg only */
@@ -480,7 +525,7 @@ fd_ed25519_hip_verify_dev( fd_ed25519_hip_ctx_t * ctx, ulong n, uchar const * d_
       FD_CHECK( hipEventSynchronize( ctx->ev[2] ) );
       float a, b;
       FD_CHECK( hipEventElapsedTime( &a, ctx->ev[0], ctx->ev[1] ) );
-      FD_CHECK( hipEventElapsedTime( &b, ctx->ev[1], ctx->ev[2] ) );
+      FD_CHECK( hipEventElapsedTime( &b, ctx->ev[3], ctx->ev[2] ) );   /* k_verify_dsm (+ k_bitmap) */
       ctx->prep_ms += a; ctx->dsm_ms += b; ctx->prep_launches++; ctx->dsm_launches++;
     }
   }
