@@ -98,12 +98,15 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--sigs", type=int, default=1 << 20, help="signatures per GPU per step")
-    ap.add_argument("--msg-sz", type=int, default=64)
-    ap.add_argument("--mix", default="c2", choices=["c1", "c2"])
+    ap.add_argument("--config", default="c2", choices=["c1", "c2", "c3", "c5"],
+                    help="BASELINE.json configs: c1 all-valid 2^20/GPU; c2 (default, the metric's config) "
+                         "C2 mix 2^20/GPU; c3 one 32-B message x 2^22 keys/GPU as batch_single_msg "
+                         "groups of 16; c5 2^26 C2-mix signatures in total, sharded (strong scaling)")
+    ap.add_argument("--sigs", type=int, default=None, help="override signatures per GPU per step")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--cpu-seconds", type=float, default=8.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--force-dist", action="store_true", help="init torch.distributed even at world size 1")
     args = ap.parse_args()
 
     import torch
@@ -112,22 +115,43 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     torch.cuda.set_device(local)
     dist = None
-    if world > 1:
+    if world > 1 or args.force_dist:
         import torch.distributed as dist
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
     from firedancer_amd import Verifier
     from firedancer_amd.workload import make_batch_gpu
 
-    n = args.sigs
-    v = Verifier(device=local, chunk_sigs=n)
-    batch = make_batch_gpu(v, n, msg_sz=args.msg_sz, seed=0x5eed0001 + 7919 * rank, mix=args.mix)
+    from firedancer_amd.shard import shard_bounds
+    cfg = args.config
+    msg_sz = 32 if cfg == "c3" else 64
+    mix = "c1" if cfg in ("c1", "c3") else "c2"
+    scaling = "weak"
+    if cfg == "c5":
+        total = args.sigs * world if args.sigs else 1 << 26
+        lo, hi = shard_bounds(total, rank, world)
+        n = hi - lo
+        scaling = "strong"
+    else:
+        n = args.sigs or ((1 << 22) if cfg == "c3" else (1 << 20))
+    chunk = min(n, 1 << 20)
+    v = Verifier(device=local, chunk_sigs=chunk)
+    batch = make_batch_gpu(v, n, msg_sz=msg_sz, seed=0x5eed0001 + 7919 * rank, mix=mix, shared_msg=(cfg == "c3"))
     dev = batch.dev
     codes = torch.zeros(n, dtype=torch.int8, device=dev)
     bitmap = torch.zeros((n + 63) // 64, dtype=torch.int64, device=dev)
+    groups = None
+    if cfg == "c3":   # fd_ed25519_verify_batch_single_msg in chunks of 16 (fd_ed25519_user.c:238-241)
+        ng = (n + 15) // 16
+        first = torch.arange(ng, dtype=torch.int32, device=dev) * 16
+        cnt = torch.clamp(n - first, max=16).to(torch.uint8)
+        gcodes = torch.zeros(ng, dtype=torch.int8, device=dev)
+        groups = (ng, first, cnt, gcodes)
 
     def step():
         v.verify_dev(n, batch.sigs, batch.pubs, batch.pool, batch.msg_off, batch.msg_sz, codes, bitmap)
+        if groups:
+            v.group_reduce_dev(groups[0], groups[1], groups[2], codes, groups[3])
 
     for _ in range(args.warmup):
         step()
@@ -159,13 +183,32 @@ def main():
     reached_dsm = int(np.isin(c, (0, -3)).sum())          # passed every pre-check
     accept = float((c == 0).mean())
 
-    total = n * world * args.steps
+    if dist:
+        nt = torch.tensor([n], dtype=torch.int64, device=dev)
+        dist.all_reduce(nt)
+        n_all = int(nt.item())
+    else:
+        n_all = n
+    total = n_all * args.steps
     value = total / elapsed
+    launches_per_step = -(-n // chunk)
     dsm_avg_ms = dsm_ms / max(launches, 1)
     prep_avg_ms = prep_ms / max(launches, 1)
-    achieved = reached_dsm * W_DSM / (dsm_avg_ms * 1e-3) / 1e12        # T int32-ops/s, per GPU
+    units_per_launch = reached_dsm / launches_per_step
+    achieved = units_per_launch * W_DSM / (dsm_avg_ms * 1e-3) / 1e12    # T int32-ops/s, per GPU
     peak = PEAK_OPS / 1e12
-    pipeline_frac = (n * w_total(args.msg_sz)) / ((prep_avg_ms + dsm_avg_ms) * 1e-3) / PEAK_OPS
+    pipeline_frac = (n * w_total(msg_sz)) / ((prep_avg_ms + dsm_avg_ms) * 1e-3 * max(launches_per_step, 1)) / PEAK_OPS
+
+    # HBM-side bytes per k_verify_dsm launch from the committed rocprofv3 PMC
+    # passes of this same command (FETCH_SIZE x2 per the gfx950 note + WRITE_SIZE)
+    traffic, traffic_src = None, None
+    pmc = os.path.join(REPO, "profiles", "r01_pmc_summary.json")
+    if cfg == "c2" and n == (1 << 20) and os.path.exists(pmc):
+        with open(pmc) as f:
+            traffic = json.load(f)["kernels"]["k_verify_dsm"]["derived"]["hbm_side_bytes_per_launch"]
+        traffic_src = "profiles/r01_pmc_summary.json: FETCH_SIZE*2 + WRITE_SIZE of k_verify_dsm (rocprofv3 --pmc)"
+    ingest_bytes = 64 + 32 + msg_sz + 8                   # sig, pub, msg, off/sz per signature
+    ingest_gbps = n / launches_per_step * ingest_bytes / (prep_avg_ms * 1e-3) / 1e9
 
     out = None
     if rank == 0:
@@ -180,6 +223,7 @@ def main():
             pool = batch.pool[lo:hi].cpu().numpy()
             threads = max(1, min(args.cpu_threads, os.cpu_count() or 1))
             cpu = cpu_baseline(sigs, pubs, pool, moff - lo, msz, c[idx], threads, args.cpu_seconds)
+            cpu["sample"] = cpu.get("sample", "") + f" [{cfg}]"
         out = {
             "metric": METRIC,
             "value": round(value, 1),
@@ -189,22 +233,28 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(elapsed / args.steps * 1e3, 4),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": scaling,
             "vs_baseline": None,
             "dtype": "u32",
             "data": "synthetic (GPU-signed random keys, C2 mutation model)",
-            "config": {"workload": f"config 2: {n} sigs/GPU, {args.msg_sz}-B msgs, "
-                                   f"{'C2 validity mix' if args.mix == 'c2' else 'all valid'}",
-                       "sigs_per_gpu": n, "msg_sz": args.msg_sz, "parallelism": f"dp{world} (signature shards)"},
+            "config": {"workload": {
+                           "c1": f"config 1: {n} sigs/GPU, 64-B msgs, all valid",
+                           "c2": f"config 2: {n} sigs/GPU, 64-B msgs, C2 validity mix",
+                           "c3": f"config 3: one 32-B msg x {n} keys/GPU, batch_single_msg groups of 16",
+                           "c5": f"config 5: {n_all} C2-mix sigs total, {n} on rank 0"}[cfg],
+                       "config_id": cfg, "sigs_per_gpu": n, "msg_sz": msg_sz,
+                       "parallelism": f"dp{world} (signature shards)"},
             "accept_rate": round(accept, 5),
             "roofline": {"bound": "valu_int32", "kernel": "k_verify_dsm",
                          "achieved": round(achieved, 3), "peak": round(peak, 3), "unit": "Tops/s",
-                         "frac": round(achieved / peak, 4), "traffic": None,
-                         "algorithmic_ops_per_unit": round(W_DSM), "units_per_launch": reached_dsm,
+                         "frac": round(achieved / peak, 4), "traffic": traffic, "traffic_unit": "bytes/launch",
+                         "traffic_source": traffic_src,
+                         "algorithmic_ops_per_unit": round(W_DSM), "units_per_launch": round(units_per_launch),
                          "avg_launch_ms": round(dsm_avg_ms, 4)},
             "pipeline": {"prep_ms": round(prep_avg_ms, 4), "dsm_ms": round(dsm_avg_ms, 4),
-                         "w_total_per_verify": round(w_total(args.msg_sz)),
-                         "int32_valu_frac": round(pipeline_frac, 4)},
+                         "w_total_per_verify": round(w_total(msg_sz)),
+                         "int32_valu_frac": round(pipeline_frac, 4),
+                         "ingest_GBps": round(ingest_gbps, 2), "ingest_bytes_per_sig": ingest_bytes},
             "cpu_baseline": cpu,
         }
         print(json.dumps(out), flush=True)

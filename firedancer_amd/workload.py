@@ -79,7 +79,7 @@ def make_batch_gpu(verifier, n, msg_sz=64, seed=0x5eed0001, mix="c1", shared_msg
     """Config-1 style batch: n random keypairs, one random msg_sz-byte message
     per signature (or one shared message: config 3), signed on the GPU by the
     engine's own signer (fd_ed25519_hip_sign_dev).  mix="c2" applies the C2
-    mutation model on the host afterwards."""
+    mutation model on the device afterwards (c2_mutate_torch)."""
     import torch
     dev = torch.device("cuda", verifier.device)
     rng = np.random.default_rng(seed)
@@ -100,7 +100,65 @@ def make_batch_gpu(verifier, n, msg_sz=64, seed=0x5eed0001, mix="c1", shared_msg
     verifier.sync()
     kinds = None
     if mix == "c2":
-        sigs = d_sig.cpu().numpy(); pubs = d_pub.cpu().numpy()
-        kinds = c2_mutate(sigs, pubs, np.random.default_rng(seed ^ 0xc2))
-        d_sig.copy_(torch.from_numpy(sigs)); d_pub.copy_(torch.from_numpy(pubs))
+        kinds = c2_mutate_torch(d_sig, d_pub, seed ^ 0xc2)
     return Batch(dev, d_sig, d_pub, d_pool, d_off, d_sz, kinds)
+
+
+def c2_mutate_torch(sigs, pubs, seed):
+    """The C2 mutation model on device tensors ((n,64) / (n,32) uint8), in
+    place, for batches too large for the host loop; same distribution as
+    c2_mutate (different draws).  Returns the per-record kind (uint8)."""
+    import torch
+    dev = sigs.device
+    n = sigs.shape[0]
+    g = torch.Generator(device=dev)
+    g.manual_seed(int(seed))
+    roll = torch.rand(n, generator=g, device=dev)
+    edges = torch.tensor(_EDGES, device=dev, dtype=roll.dtype)
+    kinds = torch.tensor(_KIND_OF_BIN, device=dev)[torch.bucketize(roll, edges, right=True)]
+
+    def flip(buf, nbits, mask_kind):
+        idx = torch.nonzero(kinds == mask_kind).flatten()
+        if idx.numel():
+            bit = torch.randint(0, nbits, (idx.numel(),), generator=g, device=dev)
+            buf[idx, bit >> 3] ^= (1 << (bit & 7)).to(torch.uint8)
+
+    flip(sigs, 512, KIND_SIGFLIP)
+    flip(pubs, 256, KIND_PUBFLIP)
+    # S += L on 8 little-endian 32-bit limbs (S < L, so no overflow of 2^256)
+    idx = torch.nonzero(kinds == KIND_S_GE_L).flatten()
+    if idx.numel():
+        s = sigs[idx, 32:].to(torch.int64).view(-1, 8, 4)
+        limbs = s[..., 0] | (s[..., 1] << 8) | (s[..., 2] << 16) | (s[..., 3] << 24)
+        lw = torch.tensor([(L_INT >> (32 * i)) & 0xffffffff for i in range(8)], device=dev, dtype=torch.int64)
+        carry = torch.zeros(idx.numel(), dtype=torch.int64, device=dev)
+        for i in range(8):
+            t = limbs[:, i] + lw[i] + carry
+            limbs[:, i] = t & 0xffffffff
+            carry = t >> 32
+        out = torch.stack([(limbs >> (8 * b)) & 0xff for b in range(4)], dim=-1).reshape(-1, 32)
+        sigs[idx, 32:] = out.to(torch.uint8)
+    so = torch.tensor(list(b"".join(SMALL_ORDER_ENCODINGS)), dtype=torch.uint8, device=dev).view(8, 32)
+    idx = torch.nonzero(kinds == KIND_A_SMALL).flatten()
+    if idx.numel():
+        pubs[idx] = so[torch.randint(0, 8, (idx.numel(),), generator=g, device=dev)]
+    idx = torch.nonzero(kinds == KIND_R_SMALL).flatten()
+    if idx.numel():
+        sigs[idx, :32] = so[torch.randint(0, 8, (idx.numel(),), generator=g, device=dev)]
+
+    def noncanon(buf, cols):
+        # y = p + k (k in [0,18]) < 2^255: byte0 = 0xed + k, bytes 1..30 = 0xff, byte31 = 0x7f | sign
+        k = torch.randint(0, 19, (cols.numel(),), generator=g, device=dev)
+        sign = buf[cols, 31] & 0x80
+        enc = torch.full((cols.numel(), 32), 0xff, dtype=torch.uint8, device=dev)
+        enc[:, 0] = (0xed + k).to(torch.uint8)
+        enc[:, 31] = 0x7f | sign
+        buf[cols, :32] = enc
+
+    idx = torch.nonzero(kinds == KIND_A_NONCANON).flatten()
+    if idx.numel():
+        noncanon(pubs, idx)
+    idx = torch.nonzero(kinds == KIND_R_NONCANON).flatten()
+    if idx.numel():
+        noncanon(sigs, idx)
+    return kinds
