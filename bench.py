@@ -98,10 +98,12 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--config", default="c2", choices=["c1", "c2", "c3", "c5"],
+    ap.add_argument("--config", default="c2", choices=["c1", "c2", "c3", "c4", "c5"],
                     help="BASELINE.json configs: c1 all-valid 2^20/GPU; c2 (default, the metric's config) "
                          "C2 mix 2^20/GPU; c3 one 32-B message x 2^22 keys/GPU as batch_single_msg "
-                         "groups of 16; c5 2^26 C2-mix signatures in total, sharded (strong scaling)")
+                         "groups of 16; c4 synthetic txn stream through the verify tile (GPU parse + verify + "
+                         "host tcache dedup); c5 2^26 C2-mix signatures in total, sharded (strong scaling)")
+    ap.add_argument("--txns", type=int, default=1 << 19, help="c4: frags per batch per GPU")
     ap.add_argument("--sigs", type=int, default=None, help="override signatures per GPU per step")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--cpu-seconds", type=float, default=8.0)
@@ -124,6 +126,8 @@ def main():
 
     from firedancer_amd.shard import shard_bounds
     cfg = args.config
+    if cfg == "c4":
+        return run_c4(args, rank, world, local, dist)
     msg_sz = 32 if cfg == "c3" else 64
     mix = "c1" if cfg in ("c1", "c3") else "c2"
     scaling = "weak"
@@ -258,6 +262,159 @@ def main():
             "cpu_baseline": cpu,
         }
         print(json.dumps(out), flush=True)
+    v.close()
+    if dist:
+        dist.barrier()
+        dist.destroy_process_group()
+    return out
+
+
+def ref_tile_baseline(pool, off, sz, threads, target_s, seed, depth):
+    """The reference's verify tile path (fd_txn_parse + fd_txn_verify with its
+    tcache, compiled from the reference sources) on T pinned host threads, one
+    tile per thread, frags round-robined by seq like before_frag."""
+    import ctypes
+    path = os.path.join(REPO, "oracle", "_ref", "libfdref_txn.so")
+    if not os.path.exists(path):
+        return {"value": None, "unit": "verifies/s", "cores": 0, "kind": "reference",
+                "sample": "unavailable: oracle/_ref not built on this box"}
+    L = ctypes.CDLL(path)
+    c = ctypes
+    L.ref_verify_tile_bench.argtypes = [c.c_int, c.c_int, c.c_uint64, c.c_uint64, c.c_uint64, c.c_uint64,
+                                        c.c_void_p, c.c_void_p, c.c_void_p, c.c_void_p, c.c_void_p]
+    n = off.size
+    res = np.zeros(n, np.int8)
+    o = np.zeros(4, np.float64)
+    L.ref_verify_tile_bench(1, 0, 1, seed, depth, n, pool.ctypes.data, off.ctypes.data, sz.ctypes.data,
+                            res.ctypes.data, o.ctypes.data)
+    per_core = o[2] / o[0]
+    rep = max(1, int(round(target_s * per_core * threads / max(o[2], 1))))
+    L.ref_verify_tile_bench(threads, 0, rep, seed, depth, n, pool.ctypes.data, off.ctypes.data, sz.ctypes.data,
+                            res.ctypes.data, o.ctypes.data)
+    return {"value": round(o[2] / o[0], 1), "unit": "verifies/s", "cores": threads, "kind": "reference",
+            "per_core": round(per_core, 1), "frags_per_s": round(o[1] / o[0], 1),
+            "sample": f"first {n} frags of the same stream x {rep} passes ({int(o[2])} signatures, {o[0]:.2f} s wall, "
+                      f"{threads} pinned threads = {threads} verify tiles, tcache depth {depth} each)"}
+
+
+def run_c4(args, rank, world, local, dist):
+    """Config 4: synthetic Solana txn stream through the verify tile.
+
+    A step is one batch of --txns frags (raw payloads resident in HBM) through
+    fd_verify_hip_tile: GPU parse + sig0 tag + record expansion + verify +
+    per-txn batch_single_msg reduce, then the ordered host pass (tcache dedup,
+    depth 4194302 = the reference default signature_cache_size, and the
+    bundle state).  Batches are submitted one ahead, so the host pass of batch
+    k overlaps the GPU work of batch k+1 (the pipelined steady state of a
+    GPU verify tile).  Each step re-keys the dedup hash so the replayed batch
+    is new traffic to the tcache; in-batch resends still dedup.
+    value = signatures verified per second (all ranks)."""
+    import torch
+    from firedancer_amd import Verifier
+    from firedancer_amd.txn_workload import gpu_signer, make_txn_stream
+    from firedancer_amd.verify_tile import VerifyTile
+    v = Verifier(device=local, chunk_sigs=1 << 20)
+    seed_base = 0x7f4a11 + 104729 * rank
+    s = make_txn_stream(args.txns, gpu_signer(v), seed=0x5eed0004 + 7919 * rank)
+    dev = torch.device("cuda", local)
+    d_pool = torch.from_numpy(s.pool).to(dev)
+    d_off = torch.from_numpy(s.off.view(np.int32)).to(dev)
+    d_sz = torch.from_numpy(s.sz.view(np.int16)).to(dev)
+    depth = 4194302
+    tile = VerifyTile(v, max_txn=s.n, hashmap_seed=seed_base, tcache_depth=depth)
+    k_step = [0]
+
+    def submit():
+        tile.set_seed(seed_base + k_step[0]); k_step[0] += 1
+        tile.submit(s.n, d_pool, d_off, d_sz)
+
+    def run(steps):
+        outs, gpu_ms, host_ms = [], [], []
+        submit()
+        for k in range(steps):
+            if k + 1 < steps:
+                submit()
+            outs.append(tile.complete())
+            t = tile.last_timing(); gpu_ms.append(t["gpu_ms"]); host_ms.append(t["host_ms"])
+        return outs, gpu_ms, host_ms
+
+    run(max(args.warmup, 1))
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    m0 = tile.metrics()
+    t0 = time.perf_counter()
+    outs, gpu_ms, host_ms = run(args.steps)
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    m1 = tile.metrics()
+    sigs = m1["sigs"] - m0["sigs"]
+    frags = s.n * args.steps
+    if dist:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+        tt = torch.tensor([sigs, frags], dtype=torch.int64, device=dev)
+        dist.all_reduce(tt)
+        sigs, frags = int(tt[0].item()), int(tt[1].item())
+    res = outs[-1][0]
+    # kernel roofline: one extra (untimed) batch with per-kernel HIP-event timing
+    v.set_timing(True)
+    submit(); tile.complete()
+    prep_ms, dsm_ms, launches = v.get_timing()
+    dsm_units = v.get_dsm_units()
+    v.set_timing(False)
+    n_sig_batch = int(tile.last_timing()["sigs"])
+    launches = max(launches, 1)
+    out = None
+    if rank == 0:
+        cpu = None
+        if not args.no_cpu_baseline and world == 1:
+            k = min(32768, s.n)
+            hi = int((s.off[:k].astype(np.int64) + s.sz[:k]).max())
+            threads = max(1, min(args.cpu_threads, os.cpu_count() or 1))
+            cpu = ref_tile_baseline(s.pool[:hi + 64].copy(), s.off[:k].copy(), s.sz[:k].copy(), threads,
+                                    args.cpu_seconds, seed_base, depth)
+        counts = {int(a): int(b) for a, b in zip(*np.unique(res, return_counts=True))}
+        names = {0: "publish", -1: "verify_fail", -2: "dedup", -3: "parse_fail", -4: "bundle_peer_fail"}
+        dsm_avg = dsm_ms / launches
+        achieved = dsm_units / launches * W_DSM / (dsm_avg * 1e-3) / 1e12
+        out = {
+            "metric": METRIC,
+            "value": round(sigs / elapsed, 1),
+            "unit": "verifies/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u32",
+            "data": "synthetic txn stream (repo generator, GPU-signed, C2 mutation per signature, "
+                    "1% resends, 0.1% grafted sig0, 0.5% malformed)",
+            "config": {"workload": f"config 4: {s.n} frags/GPU/batch ({n_sig_batch} signatures), legacy+v0 txns "
+                                   f"1-12 sigs, <=1232 B, GPU fd_txn_parse, tcache dedup depth {depth}",
+                       "config_id": "c4", "frags_per_gpu": s.n, "sigs_per_batch": n_sig_batch,
+                       "parallelism": f"dp{world} (frag shards, one verify tile per GPU)"},
+            "frags_per_s": round(frags / elapsed, 1),
+            "frag_outcomes_last_batch": {names[k]: v_ for k, v_ in counts.items()},
+            "batch_gpu_ms": round(float(np.median(gpu_ms)), 4),
+            "batch_host_ms": round(float(np.median(host_ms)), 4),
+            "roofline": {"bound": "valu_int32", "kernel": "k_verify_dsm",
+                         "achieved": round(achieved, 3), "peak": round(PEAK_OPS / 1e12, 3), "unit": "Tops/s",
+                         "frac": round(achieved / (PEAK_OPS / 1e12), 4), "traffic": None,
+                         "algorithmic_ops_per_unit": round(W_DSM), "units_per_launch": round(dsm_units / launches),
+                         "avg_launch_ms": round(dsm_avg, 4), "launches_per_batch": launches,
+                         "prep_ms_per_batch": round(prep_ms, 4)},
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(out), flush=True)
+    tile.close()
     v.close()
     if dist:
         dist.barrier()

@@ -13,7 +13,8 @@ CSRC = os.path.join(PKG, "csrc")
 LIB = os.path.join(PKG, "libfd_ed25519_hip.so")
 SCRATCH_BASE = os.environ.get("FE_SCRATCH_BASE", "124")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
-SOURCES = ["fd_ed25519_hip.hip", "fd_ed25519_dev.h", "gen_fe_asm.py"]
+SOURCES = ["fd_ed25519_hip.hip", "fd_ed25519_dev.h", "gen_fe_asm.py", "fd_txn_hip.hip"]
+UNITS = ["fd_ed25519_hip.hip", "fd_txn_hip.hip"]
 
 
 def _stale(target, deps):
@@ -23,22 +24,33 @@ def _stale(target, deps):
     return any(os.path.getmtime(d) > t for d in deps)
 
 
-def build(force=False, verbose=False):
+def variant_path(name):
+    return LIB if not name else os.path.join(PKG, f"libfd_ed25519_hip_{name}.so")
+
+
+def build(force=False, verbose=False, variant=None, defines=()):
+    """Build the library (or an experimental variant with extra -D defines,
+    loaded when FD_ED25519_HIP_LIB names it)."""
+    lib_path = variant_path(variant)
     asm_h = os.path.join(CSRC, "fe25519_asm.h")
     gen = os.path.join(CSRC, "gen_fe_asm.py")
     env = dict(os.environ, FE_SCRATCH_BASE=SCRATCH_BASE)
     if force or _stale(asm_h, [gen]) or f"FE_ASM_SCRATCH_BASE {SCRATCH_BASE}\n" not in open(asm_h).read():
         subprocess.check_call([sys.executable, gen, asm_h], env=env)
-    deps = [os.path.join(CSRC, s) for s in SOURCES] + [asm_h, os.path.join(PKG, "..", "include", "fd_ed25519_hip.h")]
-    if force or _stale(LIB, deps):
-        cmd = [HIPCC, "--offload-arch=gfx950", "-O3", "-fPIC", "-shared", "-std=c++17",
-               "-o", LIB + ".tmp", os.path.join(CSRC, "fd_ed25519_hip.hip")]
+    deps = [os.path.join(CSRC, s) for s in SOURCES] + [asm_h] + [os.path.join(PKG, "..", "include", h) for h in ("fd_ed25519_hip.h", "fd_verify_hip.h")]
+    if force or _stale(lib_path, deps):
+        cmd = [HIPCC, "--offload-arch=gfx950", "-O3", "-fPIC", "-shared", "-std=c++17"] + \
+              [f"-D{d}" for d in defines] + ["-o", lib_path + ".tmp"] + [os.path.join(CSRC, u) for u in UNITS]
         if verbose:
             print(" ".join(cmd))
         subprocess.check_call(cmd)
-        os.replace(LIB + ".tmp", LIB)
-    return LIB
+        os.replace(lib_path + ".tmp", lib_path)
+    return lib_path
 
 
 if __name__ == "__main__":
-    print(build(force="--force" in sys.argv, verbose=True))
+    args = [a for a in sys.argv[1:] if not a.startswith("--")]
+    if args:   # python build.py <variant> DEF=1 ...
+        print(build(force="--force" in sys.argv, verbose=True, variant=args[0], defines=args[1:]))
+    else:
+        print(build(force="--force" in sys.argv, verbose=True))

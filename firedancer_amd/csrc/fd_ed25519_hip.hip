@@ -74,7 +74,7 @@ struct fd_ed25519_hip_ctx {
   /* optional per-kernel timing (HIP events around each launch, on the launch stream) */
   int          timing;
   double       prep_ms, dsm_ms;
-  ulong        prep_launches, dsm_launches;
+  ulong        prep_launches, dsm_launches, dsm_units;
   hipEvent_t   ev[4];
   /* staging for the host-memory entry points (grown on demand) */
   ulong        h_cap_n, h_cap_pool, h_cap_groups;
@@ -231,7 +231,18 @@ void k_bitmap( ulong n, signed char const * __restrict__ codes, ulong * __restri
   if( (threadIdx.x & 63u) == 0u && i < n ) bitmap[i >> 6] = b;
 }
 
-__global__ __launch_bounds__(256)
+/* FD_DSM_WAVES: waves per SIMD the register allocation of k_verify_dsm is
+   held to (0: compiler's choice, 173 VGPRs -> 2 waves) */
+#ifndef FD_DSM_WAVES
+#define FD_DSM_WAVES 0
+#endif
+#if FD_DSM_WAVES
+#define DSM_OCCUPANCY __attribute__((amdgpu_waves_per_eu(FD_DSM_WAVES, FD_DSM_WAVES)))
+#else
+#define DSM_OCCUPANCY
+#endif
+
+__global__ __launch_bounds__(256) DSM_OCCUPANCY
 void k_verify_dsm( ulong chunk, u32 const * __restrict__ st, u32 const * __restrict__ btab,
                    u32 * __restrict__ atab, u32 const * __restrict__ idx, u32 const * __restrict__ count,
                    signed char * __restrict__ codes ) {
@@ -483,7 +494,11 @@ void  fd_ed25519_hip_set_errmode( fd_ed25519_hip_ctx_t * ctx, int m ) { ctx->err
 void
 fd_ed25519_hip_set_timing( fd_ed25519_hip_ctx_t * ctx, int on ) {
   ctx->timing = on; ctx->prep_ms = ctx->dsm_ms = 0.0; ctx->prep_launches = ctx->dsm_launches = 0UL;
+  ctx->dsm_units = 0UL;
 }
+
+ulong
+fd_ed25519_hip_get_dsm_units( fd_ed25519_hip_ctx_t const * ctx ) { return ctx->dsm_units; }
 
 void
 fd_ed25519_hip_get_timing( fd_ed25519_hip_ctx_t const * ctx, double * prep_ms, double * dsm_ms, ulong * launches ) {
@@ -526,7 +541,9 @@ fd_ed25519_hip_verify_dev( fd_ed25519_hip_ctx_t * ctx, ulong n, uchar const * d_
       float a, b;
       FD_CHECK( hipEventElapsedTime( &a, ctx->ev[0], ctx->ev[1] ) );
       FD_CHECK( hipEventElapsedTime( &b, ctx->ev[3], ctx->ev[2] ) );   /* k_verify_dsm (+ k_bitmap) */
-      ctx->prep_ms += a; ctx->dsm_ms += b; ctx->prep_launches++; ctx->dsm_launches++;
+      u32 survivors = 0;
+      FD_CHECK( hipMemcpy( &survivors, ctx->d_count, sizeof(u32), hipMemcpyDeviceToHost ) );
+      ctx->prep_ms += a; ctx->dsm_ms += b; ctx->prep_launches++; ctx->dsm_launches++; ctx->dsm_units += survivors;
     }
   }
   return 0;

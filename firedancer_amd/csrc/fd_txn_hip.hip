@@ -1,0 +1,595 @@
+/* fd_txn_hip.hip -- verify-tile layer of the gfx950 engine: GPU txn parse,
+   sig0 tags, txn -> signature-record expansion, and the ordered host pass
+   (tcache dedup + bundle state).  C ABI: include/fd_verify_hip.h.
+
+   Per batch of frags (one lane per frag, 256-thread workgroups):
+
+     k_txn_parse   fd_txn_parse_core (fd_txn_parse.c:7-254) on the payload,
+                   fd_txn_t out, tag = fd_hash(seed, sig0, 64), and the
+                   signature span to verify
+     k_txn_expand  slot allocation (one atomic per wave, ballot prefix sums)
+                   and 16-B-aligned signature records for the verify
+                   pipeline; first/cnt per txn for the reduce
+     fd_ed25519_hip_verify_dev + fd_ed25519_hip_group_reduce_dev
+     D2H           txn_t_sz (2 B), code (1 B), tag (8 B) per frag
+
+   The ordered host pass restates after_frag (fd_verify_tile.c:101-161)
+   around fd_txn_verify (fd_verify_tile.h:61-111) with the tcache of
+   fd_tcache.h:237-410, prefetching map slots a few frags ahead. */
+
+#include "../../include/fd_verify_hip.h"
+
+#include <hip/hip_runtime.h>
+#include <chrono>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#define TX_CHECK( x ) do {                                                            \
+    hipError_t e_ = (x);                                                               \
+    if( e_ != hipSuccess ) {                                                           \
+      fprintf( stderr, "fd_verify_hip: %s failed at %s:%d: %s\n", #x, __FILE__,      \
+               __LINE__, hipGetErrorString( e_ ) );                                    \
+      abort();                                                                         \
+    }                                                                                  \
+  } while( 0 )
+
+typedef uint8_t  u8;
+typedef uint16_t u16;
+typedef uint32_t u32;
+typedef uint64_t u64;
+
+#define DEVI __device__ __forceinline__
+#define HD   __host__ __device__ __forceinline__
+
+#define SIG_VERIFY_MAX 16u   /* fd_ed25519_user.c:238: batch_sz > 16 -> ERR_SIG */
+
+/**********************************************************************/
+/* fd_hash (util/fd_hash.c:6-72), shared by host and device            */
+
+#define XH_P1 11400714785074694791ULL
+#define XH_P2 14029467366897019727ULL
+#define XH_P3  1609587929392839161ULL
+#define XH_P4  9650029242287828579ULL
+#define XH_P5  2870177450012600261ULL
+
+HD u64 xh_rotl( u64 x, int r ) { return (x << r) | (x >> (64 - r)); }
+HD u64 xh_round( u64 acc, u64 w ) { return xh_rotl( acc + w*XH_P2, 31 ) * XH_P1; }
+HD u64 xh_avalanche( u64 h ) {
+  h ^= h >> 33; h *= XH_P2; h ^= h >> 29; h *= XH_P3; h ^= h >> 32;
+  return h;
+}
+
+/* the 64-byte case the verify tile hashes (sig0): two 32-byte stripes, no tail */
+HD u64 xh_hash64( u64 seed, u64 const w[8] ) {
+  u64 a = seed + XH_P1 + XH_P2, b = seed + XH_P2, c = seed, d = seed - XH_P1;
+  a = xh_round( a, w[0] ); b = xh_round( b, w[1] ); c = xh_round( c, w[2] ); d = xh_round( d, w[3] );
+  a = xh_round( a, w[4] ); b = xh_round( b, w[5] ); c = xh_round( c, w[6] ); d = xh_round( d, w[7] );
+  u64 h = xh_rotl( a, 1 ) + xh_rotl( b, 7 ) + xh_rotl( c, 12 ) + xh_rotl( d, 18 );
+  h ^= xh_round( 0, a ); h = h*XH_P1 + XH_P4;
+  h ^= xh_round( 0, b ); h = h*XH_P1 + XH_P4;
+  h ^= xh_round( 0, c ); h = h*XH_P1 + XH_P4;
+  h ^= xh_round( 0, d ); h = h*XH_P1 + XH_P4;
+  h += 64u;
+  return xh_avalanche( h );
+}
+
+extern "C" ulong fd_verify_hip_hash( ulong seed, void const * buf, ulong sz ) {
+  u8 const * p = (u8 const *)buf, * end = p + sz;
+  u64 h;
+  if( sz < 32 ) h = seed + XH_P5;
+  else {
+    u64 a = seed + XH_P1 + XH_P2, b = seed + XH_P2, c = seed, d = seed - XH_P1, w[4];
+    do {
+      memcpy( w, p, 32 );
+      a = xh_round( a, w[0] ); b = xh_round( b, w[1] ); c = xh_round( c, w[2] ); d = xh_round( d, w[3] );
+      p += 32;
+    } while( end - p >= 32 );
+    h = xh_rotl( a, 1 ) + xh_rotl( b, 7 ) + xh_rotl( c, 12 ) + xh_rotl( d, 18 );
+    h ^= xh_round( 0, a ); h = h*XH_P1 + XH_P4;
+    h ^= xh_round( 0, b ); h = h*XH_P1 + XH_P4;
+    h ^= xh_round( 0, c ); h = h*XH_P1 + XH_P4;
+    h ^= xh_round( 0, d ); h = h*XH_P1 + XH_P4;
+  }
+  h += sz;
+  for( ; end - p >= 8; p += 8 ) { u64 w; memcpy( &w, p, 8 ); h ^= xh_round( 0, w ); h = xh_rotl( h, 27 )*XH_P1 + XH_P4; }
+  if( end - p >= 4 ) { u32 w; memcpy( &w, p, 4 ); h ^= (u64)w*XH_P1; h = xh_rotl( h, 23 )*XH_P2 + XH_P3; p += 4; }
+  for( ; p < end; p++ ) { h ^= (u64)p[0]*XH_P5; h = xh_rotl( h, 11 )*XH_P1; }
+  return xh_avalanche( h );
+}
+
+/**********************************************************************/
+/* GPU parse                                                           */
+
+/* Unaligned 32-bit load from global memory: two aligned dwords and a funnel
+   shift.  Only used inside a payload at offsets with >= 4 valid bytes after
+   the loaded word's last byte (signatures and pubkeys are followed by more
+   payload), so the second dword never leaves the payload. */
+DEVI u32 ld_u32u( u8 const * p ) {
+  uintptr_t a = (uintptr_t)p;
+  u32 const * q = (u32 const *)(a & ~(uintptr_t)3);
+  u32 sh = (u32)(a & 3u) * 8u;
+  u32 lo = q[0];
+  if( !sh ) return lo;
+  return __builtin_amdgcn_alignbit( q[1], lo, sh );
+}
+
+/* The per-frag verify span produced by the parse. */
+struct txn_span {
+  u32 sig_at, acct_at, msg_at, msg_sz;
+  u32 nsig;          /* signatures to verify: sig_cnt if parsed and <= 16, else 0 */
+  u32 tsz;           /* fd_txn_t footprint or 0 */
+};
+
+/* fd_cu16_dec_sz + fd_cu16_dec_fixed (fd_compact_u16.h:38-92) */
+DEVI bool cu16_rd( u8 const * p, u32 sz, u32 & i, u32 & v ) {
+  u32 left = sz - i;
+  u32 b0 = left >= 1 ? p[i] : 0u;
+  if( left >= 1 && !(b0 & 0x80u) ) { v = b0; i += 1; return true; }
+  u32 b1 = left >= 2 ? p[i+1] : 0u;
+  if( left >= 2 && !(b1 & 0x80u) ) {
+    if( !b1 ) return false;
+    v = (b0 & 0x7fu) | (b1 << 7); i += 2; return true;
+  }
+  u32 b2 = left >= 3 ? p[i+2] : 0u;
+  if( left >= 3 && !(b2 & 0xfcu) ) {
+    if( !b2 ) return false;
+    v = (b0 & 0x7fu) | ((b1 & 0x7fu) << 7) | (b2 << 14); i += 3; return true;
+  }
+  return false;
+}
+
+DEVI void put8 ( u8 * o, u32 off, u32 v ) { if( o ) o[off] = (u8)v; }
+DEVI void put16( u8 * o, u32 off, u32 v ) { if( o ) *(u16 *)(o + off) = (u16)v; }   /* off even, o 2-aligned */
+
+/* fd_txn_parse_core(payload, sz, out, NULL, NULL, FD_TXN_INSTR_MAX): returns
+   the footprint or 0.  Check order follows fd_txn_parse.c line by line;
+   `need(n)` is CHECK_LEFT. */
+DEVI u32 txn_parse( u8 const * p, u32 sz, u8 * out, txn_span & sp ) {
+  u32 i = 0;
+#define NEED( n ) do { if( (u32)(n) > sz - i ) return 0u; } while( 0 )
+  if( sz > (u32)FD_TXN_HIP_MTU ) return 0u;                                 /* :82 */
+  NEED( 1 ); u32 sig_cnt = p[i]; i++;
+  if( sig_cnt < 1u || sig_cnt > 127u ) return 0u;                           /* :91 */
+  NEED( 64u*sig_cnt ); u32 sig_off = i; i += 64u*sig_cnt;
+  u32 msg_off = i;
+  NEED( 1 ); u32 b0 = p[i]; i++;
+  u32 version;
+  if( b0 & 0x80u ) {                                                        /* :98-104 */
+    version = b0 & 0x7fu;
+    if( version != 0u ) return 0u;
+    NEED( 1 ); if( p[i] != sig_cnt ) return 0u; i++;
+  } else {
+    version = 0xffu;
+    if( b0 != sig_cnt ) return 0u;
+  }
+  NEED( 1 ); u32 ro_signed = p[i]; i++;
+  if( ro_signed >= sig_cnt ) return 0u;                                     /* :111 */
+  NEED( 1 ); u32 ro_unsigned = p[i]; i++;
+  u32 acct_cnt;
+  if( !cu16_rd( p, sz, i, acct_cnt ) ) return 0u;
+  if( sig_cnt > acct_cnt || acct_cnt > 128u ) return 0u;                    /* :117 */
+  if( sig_cnt + ro_unsigned > acct_cnt ) return 0u;                         /* :118 */
+  NEED( 32u*acct_cnt ); u32 acct_off = i; i += 32u*acct_cnt;
+  NEED( 32 ); u32 bh_off = i; i += 32u;
+  u32 instr_cnt;
+  if( !cu16_rd( p, sz, i, instr_cnt ) ) return 0u;
+  if( instr_cnt > 64u ) return 0u;                                          /* :129 */
+  NEED( 3u*instr_cnt );
+  if( !( acct_cnt > (instr_cnt ? 1u : 0u) ) ) return 0u;                    /* :134 */
+  put8( out, 0, version ); put8( out, 1, sig_cnt ); put16( out, 2, sig_off ); put16( out, 4, msg_off );
+  put8( out, 6, ro_signed ); put8( out, 7, ro_unsigned ); put16( out, 8, acct_cnt ); put16( out, 10, acct_off );
+  put16( out, 12, bh_off ); put16( out, 18, instr_cnt );
+  u32 max_acct = 0;
+  for( u32 j = 0; j < instr_cnt; j++ ) {                                    /* :153-184 */
+    NEED( 3 ); u32 prog = p[i]; i++;
+    u32 ia_cnt, data_sz;
+    if( !cu16_rd( p, sz, i, ia_cnt ) ) return 0u;
+    NEED( ia_cnt ); u32 ia_off = i;
+    for( u32 k = 0; k < ia_cnt; k++ ) { u32 x = p[ia_off + k]; max_acct = x > max_acct ? x : max_acct; }
+    i += ia_cnt;
+    if( !cu16_rd( p, sz, i, data_sz ) ) return 0u;
+    NEED( data_sz ); u32 data_off = i; i += data_sz;
+    if( !( prog > 0u && prog < acct_cnt ) ) return 0u;                      /* :171 */
+    u32 o = 20u + 10u*j;
+    put8( out, o, prog ); put8( out, o+1, 0 ); put16( out, o+2, ia_cnt ); put16( out, o+4, data_sz );
+    put16( out, o+6, ia_off ); put16( out, o+8, data_off );
+  }
+  u32 lut_cnt = 0, adtl_w = 0, adtl = 0;
+  if( version == 0u ) {                                                     /* :193-226 */
+    if( !cu16_rd( p, sz, i, lut_cnt ) ) return 0u;
+    if( lut_cnt > 127u ) return 0u;
+    NEED( 34u*lut_cnt );
+    for( u32 j = 0; j < lut_cnt; j++ ) {
+      NEED( 32 ); u32 a_off = i; i += 32u;
+      u32 w, ro;
+      if( !cu16_rd( p, sz, i, w ) ) return 0u;
+      NEED( w ); u32 w_off = i; i += w;
+      if( !cu16_rd( p, sz, i, ro ) ) return 0u;
+      NEED( ro ); u32 ro_off = i; i += ro;
+      if( w > 128u - acct_cnt || ro > 128u - acct_cnt || w + ro < 1u ) return 0u;
+      u32 o = 20u + 10u*instr_cnt + 8u*j;
+      put16( out, o, a_off ); put8( out, o+2, w ); put8( out, o+3, ro ); put16( out, o+4, w_off ); put16( out, o+6, ro_off );
+      adtl_w += w; adtl += w + ro;
+    }
+  }
+  if( i != sz ) return 0u;                                                  /* :229 */
+  if( acct_cnt + adtl > 128u ) return 0u;                                   /* :231 */
+  if( !( max_acct < acct_cnt + adtl ) ) return 0u;                          /* :234 */
+#undef NEED
+  put8( out, 14, lut_cnt ); put8( out, 15, adtl_w ); put8( out, 16, adtl ); put8( out, 17, 0 );
+  sp.sig_at = sig_off; sp.acct_at = acct_off; sp.msg_at = msg_off; sp.msg_sz = sz - msg_off;
+  sp.nsig = sig_cnt <= SIG_VERIFY_MAX ? sig_cnt : 0u;
+  return 20u + 10u*instr_cnt + 8u*lut_cnt;
+}
+
+/* per-frag SoA scratch written by k_txn_parse */
+struct parse_out {
+  u16 * tsz;      /* fd_txn_t footprint, 0 = parse failure */
+  u8  * nsig;     /* signatures to verify */
+  u32 * sig_at;   /* absolute pool offsets */
+  u32 * acct_at;
+  u32 * msg_at;
+  u32 * msg_sz;
+  u64 * tag;
+};
+
+__global__ __launch_bounds__(256)
+void k_txn_parse( ulong n, u8 const * __restrict__ pool, u32 const * __restrict__ off,
+                  u16 const * __restrict__ sz, u8 * __restrict__ txn_out, u64 seed, parse_out po ) {
+  ulong j = (ulong)blockIdx.x * blockDim.x + threadIdx.x;
+  if( j >= n ) return;
+  u32 base = off[j];
+  u8 const * p = pool + base;
+  u8 * out = txn_out ? txn_out + (ulong)FD_TXN_HIP_MAX_SZ * j : (u8 *)0;
+  txn_span sp = { 0u, 0u, 0u, 0u, 0u, 0u };
+  u32 tsz = txn_parse( p, sz[j], out, sp );
+  if( !po.tsz ) { return; }
+  po.tsz[j] = (u16)tsz;
+  if( !po.nsig ) return;
+  u64 tag = 0;
+  if( tsz ) {
+    u64 w[8];
+    u8 const * s = p + sp.sig_at;
+    #pragma unroll
+    for( int q = 0; q < 8; q++ ) w[q] = (u64)ld_u32u( s + 8*q ) | ((u64)ld_u32u( s + 8*q + 4 ) << 32);
+    tag = xh_hash64( seed, w );
+  }
+  po.nsig[j]    = (u8)(tsz ? sp.nsig : 0u);
+  po.sig_at[j]  = base + sp.sig_at;
+  po.acct_at[j] = base + sp.acct_at;
+  po.msg_at[j]  = base + sp.msg_at;
+  po.msg_sz[j]  = sp.msg_sz;
+  po.tag[j]     = tag;
+}
+
+/* Slot allocation + record expansion.  Each wave computes exclusive prefix
+   sums of its lanes' nsig (< 32, five ballots + mbcnt) and takes one
+   atomicAdd on the record counter.  Records of a wave are contiguous and in
+   frag order; waves land in any order (first[] says where). */
+__global__ __launch_bounds__(256)
+void k_txn_expand( ulong n, u8 const * __restrict__ pool, u8 const * __restrict__ nsig_a,
+                   u32 const * __restrict__ sig_at, u32 const * __restrict__ acct_at,
+                   u32 const * __restrict__ msg_at, u32 const * __restrict__ msg_sz,
+                   u32 * __restrict__ counter, u32 * __restrict__ first, u8 * __restrict__ cnt,
+                   u8 * __restrict__ rsig, u8 * __restrict__ rpub, u32 * __restrict__ rmoff,
+                   u32 * __restrict__ rmsz, ulong cap ) {
+  ulong j = (ulong)blockIdx.x * blockDim.x + threadIdx.x;
+  u32 c = j < n ? nsig_a[j] : 0u;
+  u32 excl = 0, tot = 0;
+  #pragma unroll
+  for( int b = 0; b < 5; b++ ) {
+    unsigned long long m = __ballot( (c >> b) & 1u );
+    u32 below = __builtin_amdgcn_mbcnt_hi( (u32)(m >> 32), __builtin_amdgcn_mbcnt_lo( (u32)m, 0u ) );
+    excl += below << b;
+    tot  += (u32)__popcll( m ) << b;
+  }
+  u32 base = 0;
+  if( (threadIdx.x & 63u) == 0u && tot ) base = atomicAdd( counter, tot );
+  base = __shfl( base, 0 );
+  if( j >= n ) return;
+  u32 f = base + excl;
+  first[j] = f; cnt[j] = (u8)c;
+  if( (ulong)f + c > cap ) { cnt[j] = 0; return; }      /* host sizes cap; never taken */
+  u8 const * s = pool + sig_at[j];
+  u8 const * a = pool + acct_at[j];
+  u32 mo = msg_at[j], ms = msg_sz[j];
+  for( u32 k = 0; k < c; k++ ) {
+    u32 r = f + k;
+    uint4 * ds = (uint4 *)(rsig + 64ul*r);
+    #pragma unroll
+    for( int q = 0; q < 4; q++ ) {
+      u8 const * src = s + 64u*k + 16u*q;
+      ds[q] = make_uint4( ld_u32u( src ), ld_u32u( src + 4 ), ld_u32u( src + 8 ), ld_u32u( src + 12 ) );
+    }
+    uint4 * dp = (uint4 *)(rpub + 32ul*r);
+    #pragma unroll
+    for( int q = 0; q < 2; q++ ) {
+      u8 const * src = a + 32u*k + 16u*q;
+      dp[q] = make_uint4( ld_u32u( src ), ld_u32u( src + 4 ), ld_u32u( src + 8 ), ld_u32u( src + 12 ) );
+    }
+    rmoff[r] = mo; rmsz[r] = ms;
+  }
+}
+
+extern "C" int
+fd_txn_hip_parse_dev( fd_ed25519_hip_ctx_t * ctx, ulong n, uchar const * d_pool, uint const * d_txn_off,
+                      ushort const * d_txn_sz, uchar * d_txn_out, ushort * d_txn_t_sz, void * stream ) {
+  hipStream_t s = stream ? (hipStream_t)stream : (hipStream_t)fd_ed25519_hip_ctx_stream( ctx );
+  TX_CHECK( hipSetDevice( fd_ed25519_hip_ctx_device( ctx ) ) );
+  if( !n ) return 0;
+  parse_out po = { d_txn_t_sz, 0, 0, 0, 0, 0, 0 };
+  hipLaunchKernelGGL( k_txn_parse, dim3( (unsigned)((n + 255)/256) ), dim3( 256 ), 0, s,
+                      n, d_pool, d_txn_off, d_txn_sz, d_txn_out, (u64)0, po );
+  TX_CHECK( hipGetLastError() );
+  return 0;
+}
+
+/**********************************************************************/
+/* tcache (fd_tcache.h:115-410) on the reference memory layout          */
+
+static inline ulong tc_probe( ulong const * map, ulong map_cnt, ulong tag, int & found ) {
+  ulong m = map_cnt - 1, i = tag & m;
+  for( ;; ) {
+    ulong t = map[i];
+    if( t == tag ) { found = 1; return i; }
+    if( !t )       { found = 0; return i; }
+    i = (i + 1) & m;
+  }
+}
+
+static inline void tc_remove( ulong * map, ulong map_cnt, ulong tag ) {
+  if( !tag ) return;
+  int f; ulong hole = tc_probe( map, map_cnt, tag, f );
+  if( !f ) return;
+  ulong m = map_cnt - 1;
+  for( ;; ) {
+    map[hole] = 0;
+    ulong s = hole;
+    for( ;; ) {
+      s = (s + 1) & m;
+      ulong t = map[s];
+      if( !t ) return;
+      ulong home = t & m;
+      bool chained = hole <= s ? (home > hole && home <= s) : (home > hole || home <= s);
+      if( !chained ) { map[hole] = t; hole = s; break; }
+    }
+  }
+}
+
+extern "C" ulong fd_verify_hip_tcache_map_cnt_default( ulong depth ) {
+  if( !depth || depth == ~0ul ) return 0;
+  int lg = 63 - __builtin_clzl( depth + 1 ) + 2;     /* FD_TCACHE_SPARSE_DEFAULT */
+  return lg > 63 ? 0 : 1ul << lg;
+}
+
+extern "C" ulong fd_verify_hip_tcache_reset( ulong * ring, ulong depth, ulong * map, ulong map_cnt ) {
+  memset( ring, 0, depth*sizeof(ulong) ); memset( map, 0, map_cnt*sizeof(ulong) );
+  return 0;
+}
+
+extern "C" int fd_verify_hip_tcache_query( ulong const * map, ulong map_cnt, ulong tag ) {
+  int f; tc_probe( map, map_cnt, tag, f ); return f;
+}
+
+extern "C" int fd_verify_hip_tcache_insert( ulong * oldest, ulong * ring, ulong depth, ulong * map,
+                                            ulong map_cnt, ulong tag ) {
+  int f; ulong slot = tc_probe( map, map_cnt, tag, f );
+  if( f ) return 1;
+  map[slot] = tag;
+  ulong o = *oldest, ev = ring[o];
+  ring[o] = tag;
+  *oldest = o + 1 >= depth ? 0 : o + 1;
+  tc_remove( map, map_cnt, ev );
+  return 0;
+}
+
+/**********************************************************************/
+/* verify tile engine                                                  */
+
+struct tile_slot {
+  ulong         n, nsig;
+  /* per frag, device */
+  u16 *         d_tsz; u8 * d_nsig; u32 * d_sig_at; u32 * d_acct_at; u32 * d_msg_at; u32 * d_msg_sz;
+  u64 *         d_tag; u32 * d_first; u8 * d_cnt; signed char * d_tcode; u32 * d_counter;
+  /* per signature record, device (grown on demand) */
+  ulong         rcap;
+  u8 *          d_rsig; u8 * d_rpub; u32 * d_rmoff; u32 * d_rmsz; signed char * d_rcode;
+  /* per frag, pinned host */
+  u16 *         h_tsz; signed char * h_tcode; u64 * h_tag; u32 * h_counter;
+  hipEvent_t    ev_start, ev_done;
+  int           busy;
+};
+
+struct fd_verify_hip_tile {
+  fd_ed25519_hip_ctx_t * ctx;
+  ulong      max_txn, seed;
+  /* tcache: the tile's own, or the caller's (join_tcache) */
+  ulong *    own_mem;
+  ulong      own_oldest;
+  ulong *    oldest; ulong * ring; ulong depth; ulong * map; ulong map_cnt;
+  /* bundle state (fd_verify_ctx_t bundle_failed / bundle_id) */
+  int        bundle_failed; ulong bundle_id;
+  ulong      m_parse, m_verify, m_dedup, m_bundle, m_pub, m_sigs;
+  tile_slot  slot[2];
+  ulong      submitted, completed;
+  double     last_gpu_ms, last_host_ms, last_sigs;
+};
+
+static void slot_alloc( tile_slot & s, ulong n ) {
+  memset( &s, 0, sizeof(s) );
+  TX_CHECK( hipMalloc( &s.d_tsz, 2*n ) );     TX_CHECK( hipMalloc( &s.d_nsig, n ) );
+  TX_CHECK( hipMalloc( &s.d_sig_at, 4*n ) );  TX_CHECK( hipMalloc( &s.d_acct_at, 4*n ) );
+  TX_CHECK( hipMalloc( &s.d_msg_at, 4*n ) );  TX_CHECK( hipMalloc( &s.d_msg_sz, 4*n ) );
+  TX_CHECK( hipMalloc( &s.d_tag, 8*n ) );     TX_CHECK( hipMalloc( &s.d_first, 4*n ) );
+  TX_CHECK( hipMalloc( &s.d_cnt, n ) );       TX_CHECK( hipMalloc( &s.d_tcode, n ) );
+  TX_CHECK( hipMalloc( &s.d_counter, 4 ) );
+  TX_CHECK( hipHostMalloc( &s.h_tsz, 2*n, 0 ) );  TX_CHECK( hipHostMalloc( &s.h_tcode, n, 0 ) );
+  TX_CHECK( hipHostMalloc( &s.h_tag, 8*n, 0 ) );  TX_CHECK( hipHostMalloc( &s.h_counter, 4, 0 ) );
+  TX_CHECK( hipEventCreate( &s.ev_start ) ); TX_CHECK( hipEventCreate( &s.ev_done ) );
+}
+
+static void slot_free_records( tile_slot & s ) {
+  (void)hipFree( s.d_rsig ); (void)hipFree( s.d_rpub ); (void)hipFree( s.d_rmoff );
+  (void)hipFree( s.d_rmsz ); (void)hipFree( s.d_rcode );
+  s.d_rsig = s.d_rpub = 0; s.d_rmoff = s.d_rmsz = 0; s.d_rcode = 0; s.rcap = 0;
+}
+
+static void slot_free( tile_slot & s ) {
+  (void)hipFree( s.d_tsz ); (void)hipFree( s.d_nsig ); (void)hipFree( s.d_sig_at ); (void)hipFree( s.d_acct_at );
+  (void)hipFree( s.d_msg_at ); (void)hipFree( s.d_msg_sz ); (void)hipFree( s.d_tag ); (void)hipFree( s.d_first );
+  (void)hipFree( s.d_cnt ); (void)hipFree( s.d_tcode ); (void)hipFree( s.d_counter );
+  (void)hipHostFree( s.h_tsz ); (void)hipHostFree( s.h_tcode ); (void)hipHostFree( s.h_tag );
+  (void)hipHostFree( s.h_counter );
+  (void)hipEventDestroy( s.ev_start ); (void)hipEventDestroy( s.ev_done );
+  slot_free_records( s );
+}
+
+extern "C" fd_verify_hip_tile_t *
+fd_verify_hip_tile_new( fd_ed25519_hip_ctx_t * ctx, ulong max_txn, ulong seed, ulong depth, ulong map_cnt ) {
+  if( !ctx || !max_txn || !depth ) return 0;
+  if( !map_cnt ) map_cnt = fd_verify_hip_tcache_map_cnt_default( depth );
+  if( !map_cnt || (map_cnt & (map_cnt - 1)) || map_cnt < depth + 2 ) return 0;
+  TX_CHECK( hipSetDevice( fd_ed25519_hip_ctx_device( ctx ) ) );
+  fd_verify_hip_tile_t * t = (fd_verify_hip_tile_t *)calloc( 1, sizeof(fd_verify_hip_tile_t) );
+  t->ctx = ctx; t->max_txn = max_txn; t->seed = seed;
+  t->own_mem = (ulong *)malloc( sizeof(ulong)*(depth + map_cnt) );
+  t->oldest = &t->own_oldest; t->ring = t->own_mem; t->depth = depth; t->map = t->own_mem + depth; t->map_cnt = map_cnt;
+  t->own_oldest = fd_verify_hip_tcache_reset( t->ring, depth, t->map, map_cnt );
+  slot_alloc( t->slot[0], max_txn ); slot_alloc( t->slot[1], max_txn );
+  return t;
+}
+
+extern "C" void
+fd_verify_hip_tile_join_tcache( fd_verify_hip_tile_t * t, ulong * sync, ulong * ring, ulong depth, ulong * map,
+                                ulong map_cnt ) {
+  t->oldest = sync; t->ring = ring; t->depth = depth; t->map = map; t->map_cnt = map_cnt;
+}
+
+extern "C" void fd_verify_hip_tile_tcache_reset( fd_verify_hip_tile_t * t ) {
+  *t->oldest = fd_verify_hip_tcache_reset( t->ring, t->depth, t->map, t->map_cnt );
+}
+
+extern "C" void fd_verify_hip_tile_set_seed( fd_verify_hip_tile_t * t, ulong seed ) { t->seed = seed; }
+
+extern "C" void fd_verify_hip_tile_delete( fd_verify_hip_tile_t * t ) {
+  if( !t ) return;
+  (void)hipSetDevice( fd_ed25519_hip_ctx_device( t->ctx ) );
+  (void)hipStreamSynchronize( (hipStream_t)fd_ed25519_hip_ctx_stream( t->ctx ) );
+  slot_free( t->slot[0] ); slot_free( t->slot[1] );
+  free( t->own_mem ); free( t );
+}
+
+extern "C" int
+fd_verify_hip_tile_submit( fd_verify_hip_tile_t * t, ulong n, uchar const * d_pool, uint const * d_txn_off,
+                           ushort const * d_txn_sz, uchar * d_txn_out ) {
+  if( n > t->max_txn ) return -1;
+  tile_slot & s = t->slot[t->submitted & 1];
+  if( s.busy ) return -2;                                   /* two batches outstanding */
+  hipStream_t st = (hipStream_t)fd_ed25519_hip_ctx_stream( t->ctx );
+  TX_CHECK( hipSetDevice( fd_ed25519_hip_ctx_device( t->ctx ) ) );
+  s.n = n; s.nsig = 0; s.busy = 1; t->submitted++;
+  TX_CHECK( hipEventRecord( s.ev_start, st ) );
+  if( !n ) { TX_CHECK( hipEventRecord( s.ev_done, st ) ); return 0; }
+  dim3 grid( (unsigned)((n + 255)/256) ), blk( 256 );
+  parse_out po = { s.d_tsz, s.d_nsig, s.d_sig_at, s.d_acct_at, s.d_msg_at, s.d_msg_sz, s.d_tag };
+  hipLaunchKernelGGL( k_txn_parse, grid, blk, 0, st, n, d_pool, d_txn_off, d_txn_sz, d_txn_out, (u64)t->seed, po );
+  TX_CHECK( hipGetLastError() );
+  /* record capacity: a parsed frag carries at most 12 signatures (96 B of
+     sig + pubkey each within FD_TXN_MTU, fd_txn.h:68); grow to that bound
+     once instead of reading the count back twice */
+  ulong need = 12ul * n;
+  if( s.rcap < need ) {
+    TX_CHECK( hipStreamSynchronize( st ) );
+    slot_free_records( s );
+    TX_CHECK( hipMalloc( &s.d_rsig, 64*need ) ); TX_CHECK( hipMalloc( &s.d_rpub, 32*need ) );
+    TX_CHECK( hipMalloc( &s.d_rmoff, 4*need ) ); TX_CHECK( hipMalloc( &s.d_rmsz, 4*need ) );
+    TX_CHECK( hipMalloc( &s.d_rcode, need ) );
+    s.rcap = need;
+  }
+  TX_CHECK( hipMemsetAsync( s.d_counter, 0, 4, st ) );
+  hipLaunchKernelGGL( k_txn_expand, grid, blk, 0, st, n, d_pool, s.d_nsig, s.d_sig_at, s.d_acct_at, s.d_msg_at,
+                      s.d_msg_sz, s.d_counter, s.d_first, s.d_cnt, s.d_rsig, s.d_rpub, s.d_rmoff, s.d_rmsz, s.rcap );
+  TX_CHECK( hipGetLastError() );
+  TX_CHECK( hipMemcpyAsync( s.h_counter, s.d_counter, 4, hipMemcpyDeviceToHost, st ) );
+  TX_CHECK( hipStreamSynchronize( st ) );                 /* the signature count sizes the verify launch */
+  s.nsig = *s.h_counter;
+  fd_ed25519_hip_verify_dev( t->ctx, s.nsig, s.d_rsig, s.d_rpub, d_pool, s.d_rmoff, s.d_rmsz, s.d_rcode, NULL, st );
+  fd_ed25519_hip_group_reduce_dev( t->ctx, n, s.d_first, s.d_cnt, s.d_rcode, s.d_tcode, st );
+  TX_CHECK( hipMemcpyAsync( s.h_tsz, s.d_tsz, 2*n, hipMemcpyDeviceToHost, st ) );
+  TX_CHECK( hipMemcpyAsync( s.h_tcode, s.d_tcode, n, hipMemcpyDeviceToHost, st ) );
+  TX_CHECK( hipMemcpyAsync( s.h_tag, s.d_tag, 8*n, hipMemcpyDeviceToHost, st ) );
+  TX_CHECK( hipEventRecord( s.ev_done, st ) );
+  return 0;
+}
+
+extern "C" int
+fd_verify_hip_tile_complete( fd_verify_hip_tile_t * t, ulong const * bundle_id, signed char * result,
+                             ulong * tag_out, ushort * txn_t_sz ) {
+  if( t->completed == t->submitted ) return -1;
+  tile_slot & s = t->slot[t->completed & 1];
+  TX_CHECK( hipSetDevice( fd_ed25519_hip_ctx_device( t->ctx ) ) );
+  TX_CHECK( hipEventSynchronize( s.ev_done ) );
+  float gpu_ms = 0.f;
+  TX_CHECK( hipEventElapsedTime( &gpu_ms, s.ev_start, s.ev_done ) );
+  auto h0 = std::chrono::steady_clock::now();
+
+  /* ordered pass: after_frag (fd_verify_tile.c:101-161) per frag */
+  ulong const n = s.n;
+  ulong * const map = t->map; ulong const mask = t->map_cnt - 1;
+  ulong * const ring = t->ring;
+  ulong const depth = t->depth;
+  const ulong PF = 8;
+  for( ulong j = 0; j < n && j < PF; j++ ) __builtin_prefetch( map + (s.h_tag[j] & mask) );
+  for( ulong j = 0; j < n; j++ ) {
+    if( j + PF < n ) {
+      __builtin_prefetch( map + (s.h_tag[j + PF] & mask) );
+      ulong o = *t->oldest + PF; if( o >= depth ) o -= depth;
+      if( o < depth ) __builtin_prefetch( map + (ring[o] & mask) );
+    }
+    u32 tsz = s.h_tsz[j];
+    if( txn_t_sz ) txn_t_sz[j] = (ushort)tsz;
+    if( tag_out ) tag_out[j] = 0;
+    ulong bid = bundle_id ? bundle_id[j] : 0ul;
+    int is_bundle = bid != 0ul;
+    if( is_bundle && bid != t->bundle_id ) { t->bundle_failed = 0; t->bundle_id = bid; }
+    if( is_bundle && t->bundle_failed ) { t->m_bundle++; result[j] = FD_VERIFY_HIP_FRAG_BUNDLE_PEER; continue; }
+    if( !tsz ) {
+      if( is_bundle ) t->bundle_failed = 1;
+      t->m_parse++; result[j] = FD_VERIFY_HIP_FRAG_PARSE_FAIL; continue;
+    }
+    /* fd_txn_verify with dedup = !is_bundle */
+    ulong tag = s.h_tag[j];
+    int res;
+    if( !is_bundle && fd_verify_hip_tcache_query( map, t->map_cnt, tag ) )       res = FD_TXN_VERIFY_DEDUP;
+    else if( s.h_tcode[j] != FD_ED25519_SUCCESS )                                 res = FD_TXN_VERIFY_FAILED;
+    else if( !is_bundle && fd_verify_hip_tcache_insert( t->oldest, ring, depth, map, t->map_cnt, tag ) )
+                                                                                  res = FD_TXN_VERIFY_DEDUP;
+    else                                                                          res = FD_TXN_VERIFY_SUCCESS;
+    if( res != FD_TXN_VERIFY_SUCCESS ) {
+      if( is_bundle ) t->bundle_failed = 1;
+      if( res == FD_TXN_VERIFY_DEDUP ) t->m_dedup++; else t->m_verify++;
+      result[j] = (signed char)res; continue;
+    }
+    if( tag_out ) tag_out[j] = tag;
+    t->m_pub++;
+    result[j] = FD_VERIFY_HIP_FRAG_PUBLISH;
+  }
+  auto h1 = std::chrono::steady_clock::now();
+  t->m_sigs += s.nsig;
+  t->last_gpu_ms  = gpu_ms;
+  t->last_host_ms = std::chrono::duration<double, std::milli>( h1 - h0 ).count();
+  t->last_sigs    = (double)s.nsig;
+  s.busy = 0; t->completed++;
+  return 0;
+}
+
+extern "C" void fd_verify_hip_tile_metrics( fd_verify_hip_tile_t const * t, ulong out[6] ) {
+  out[0] = t->m_parse; out[1] = t->m_verify; out[2] = t->m_dedup; out[3] = t->m_bundle;
+  out[4] = t->m_pub; out[5] = t->m_sigs;
+}
+
+extern "C" void fd_verify_hip_tile_last_timing( fd_verify_hip_tile_t const * t, double out[3] ) {
+  out[0] = t->last_gpu_ms; out[1] = t->last_host_ms; out[2] = t->last_sigs;
+}

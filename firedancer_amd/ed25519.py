@@ -12,7 +12,7 @@ import os
 
 import numpy as np
 
-from .build import LIB
+from .build import LIB, variant_path
 
 FD_ED25519_SUCCESS = 0
 FD_ED25519_ERR_SIG = -1
@@ -29,6 +29,7 @@ EXPORTS = (
     "fd_ed25519_hip_ctx_stream", "fd_ed25519_hip_set_errmode", "fd_ed25519_hip_verify_dev",
     "fd_ed25519_hip_verify_host", "fd_ed25519_hip_group_reduce_dev", "fd_ed25519_hip_sign_dev",
     "fd_ed25519_hip_sync", "fd_ed25519_hip_set_timing", "fd_ed25519_hip_get_timing",
+    "fd_ed25519_hip_get_dsm_units",
 )
 
 _lib = None
@@ -38,9 +39,13 @@ def lib():
     """Load the engine library (raises if it was not built)."""
     global _lib
     if _lib is None:
-        if not os.path.exists(LIB):
-            raise RuntimeError(f"{LIB} missing: run __graft_entry__.build() (no CPU fallback exists)")
-        L = ctypes.CDLL(LIB)
+        path = LIB
+        v = os.environ.get("FD_ED25519_HIP_LIB")
+        if v:   # an experimental build variant (firedancer_amd/build.py <variant> ...)
+            path = v if os.sep in v else variant_path(v)
+        if not os.path.exists(path):
+            raise RuntimeError(f"{path} missing: run __graft_entry__.build() (no CPU fallback exists)")
+        L = ctypes.CDLL(path)
         c = ctypes
         vp, u64 = c.c_void_p, c.c_ulong
         L.fd_ed25519_verify.restype = c.c_int
@@ -67,6 +72,8 @@ def lib():
         L.fd_ed25519_hip_sign_dev.argtypes = [vp, u64, vp, vp, vp, vp, vp, vp, vp]
         L.fd_ed25519_hip_set_timing.argtypes = [vp, c.c_int]
         L.fd_ed25519_hip_get_timing.argtypes = [vp, c.POINTER(c.c_double), c.POINTER(c.c_double), c.POINTER(u64)]
+        L.fd_ed25519_hip_get_dsm_units.restype = u64
+        L.fd_ed25519_hip_get_dsm_units.argtypes = [vp]
         L.fd_ed25519_hip_sync.restype = c.c_int
         L.fd_ed25519_hip_sync.argtypes = [vp]
         _lib = L
@@ -170,6 +177,10 @@ class Verifier:
         a, b, n = ctypes.c_double(), ctypes.c_double(), ctypes.c_ulong()
         self._lib.fd_ed25519_hip_get_timing(self.ctx, ctypes.byref(a), ctypes.byref(b), ctypes.byref(n))
         return a.value, b.value, n.value
+
+    def get_dsm_units(self):
+        """Signatures that ran through k_verify_dsm while timing was on."""
+        return int(self._lib.fd_ed25519_hip_get_dsm_units(self.ctx))
 
     def sync(self):
         self._lib.fd_ed25519_hip_sync(self.ctx)

@@ -1,0 +1,190 @@
+"""Host-side mirror of the reference verify tile's per-frag path, backed by the
+gfx950 engine (C ABI: include/fd_verify_hip.h, same library as ed25519.py).
+
+Reference interface it mirrors:
+  fd_txn_parse          src/ballet/txn/fd_txn.h:712-715 (fd_txn_parse.c:7-254)
+  fd_hash               src/util/fd_hash.c:14-72
+  fd_txn_verify         src/disco/verify/fd_verify_tile.h:61-111
+                        (codes FD_TXN_VERIFY_SUCCESS / FAILED / DEDUP, :9-11)
+  after_frag            src/disco/verify/fd_verify_tile.c:101-161
+  tcache                src/tango/tcache/fd_tcache.h
+
+`VerifyTile.after_frags` takes a batch of frags in arrival order and returns,
+per frag, what after_frag would have done with it (publish, or which metric
+it bumped), the dedup tag published with it and the fd_txn_t footprint.
+There is no CPU fallback: everything runs through the HIP library.
+"""
+import ctypes
+
+import numpy as np
+
+from .ed25519 import Verifier, _ptr, lib as _ed_lib
+
+FD_TXN_MAX_SZ = 852
+FD_TXN_MTU = 1232
+FD_TXN_VERIFY_SUCCESS, FD_TXN_VERIFY_FAILED, FD_TXN_VERIFY_DEDUP = 0, -1, -2
+
+FRAG_PUBLISH = 0
+FRAG_VERIFY_FAIL = -1
+FRAG_DEDUP = -2
+FRAG_PARSE_FAIL = -3
+FRAG_BUNDLE_PEER = -4
+
+# Every symbol include/fd_verify_hip.h declares (checked by tests/test_abi.py).
+EXPORTS = (
+    "fd_txn_hip_parse_dev", "fd_verify_hip_hash", "fd_verify_hip_tcache_map_cnt_default",
+    "fd_verify_hip_tcache_reset", "fd_verify_hip_tcache_query", "fd_verify_hip_tcache_insert",
+    "fd_verify_hip_tile_new", "fd_verify_hip_tile_join_tcache", "fd_verify_hip_tile_tcache_reset",
+    "fd_verify_hip_tile_delete", "fd_verify_hip_tile_set_seed", "fd_verify_hip_tile_submit", "fd_verify_hip_tile_complete",
+    "fd_verify_hip_tile_metrics", "fd_verify_hip_tile_last_timing",
+)
+
+_bound = False
+
+
+def lib():
+    global _bound
+    L = _ed_lib()
+    if not _bound:
+        c = ctypes
+        vp, u64 = c.c_void_p, c.c_ulong
+        L.fd_txn_hip_parse_dev.restype = c.c_int
+        L.fd_txn_hip_parse_dev.argtypes = [vp, u64, vp, vp, vp, vp, vp, vp]
+        L.fd_verify_hip_hash.restype = u64
+        L.fd_verify_hip_hash.argtypes = [u64, c.c_char_p, u64]
+        L.fd_verify_hip_tcache_map_cnt_default.restype = u64
+        L.fd_verify_hip_tcache_map_cnt_default.argtypes = [u64]
+        L.fd_verify_hip_tcache_reset.restype = u64
+        L.fd_verify_hip_tcache_reset.argtypes = [vp, u64, vp, u64]
+        L.fd_verify_hip_tcache_query.restype = c.c_int
+        L.fd_verify_hip_tcache_query.argtypes = [vp, u64, u64]
+        L.fd_verify_hip_tcache_insert.restype = c.c_int
+        L.fd_verify_hip_tcache_insert.argtypes = [vp, vp, u64, vp, u64, u64]
+        L.fd_verify_hip_tile_new.restype = vp
+        L.fd_verify_hip_tile_new.argtypes = [vp, u64, u64, u64, u64]
+        L.fd_verify_hip_tile_join_tcache.argtypes = [vp, vp, vp, u64, vp, u64]
+        L.fd_verify_hip_tile_tcache_reset.argtypes = [vp]
+        L.fd_verify_hip_tile_delete.argtypes = [vp]
+        L.fd_verify_hip_tile_set_seed.argtypes = [vp, u64]
+        L.fd_verify_hip_tile_submit.restype = c.c_int
+        L.fd_verify_hip_tile_submit.argtypes = [vp, u64, vp, vp, vp, vp]
+        L.fd_verify_hip_tile_complete.restype = c.c_int
+        L.fd_verify_hip_tile_complete.argtypes = [vp, vp, vp, vp, vp]
+        L.fd_verify_hip_tile_metrics.argtypes = [vp, vp]
+        L.fd_verify_hip_tile_last_timing.argtypes = [vp, vp]
+        _bound = True
+    return L
+
+
+def fd_hash(seed, buf):
+    """util/fd_hash.c:14-72 (host entry of the engine; the GPU computes the same)."""
+    b = bytes(buf)
+    return lib().fd_verify_hip_hash(int(seed) & (2**64 - 1), b, len(b))
+
+
+class Tcache:
+    """A tcache in the reference layout (ring[depth], map[map_cnt], oldest)."""
+
+    def __init__(self, depth, map_cnt=0):
+        L = lib()
+        self.depth = int(depth)
+        self.map_cnt = int(map_cnt) or int(L.fd_verify_hip_tcache_map_cnt_default(self.depth))
+        self.ring = np.zeros(self.depth, np.uint64)
+        self.map = np.zeros(self.map_cnt, np.uint64)
+        self.oldest = np.zeros(1, np.uint64)
+        self.reset()
+
+    def reset(self):
+        self.oldest[0] = lib().fd_verify_hip_tcache_reset(self.ring.ctypes.data, self.depth, self.map.ctypes.data,
+                                                          self.map_cnt)
+
+    def query(self, tag):
+        return bool(lib().fd_verify_hip_tcache_query(self.map.ctypes.data, self.map_cnt, int(tag)))
+
+    def insert(self, tag):
+        return bool(lib().fd_verify_hip_tcache_insert(self.oldest.ctypes.data, self.ring.ctypes.data, self.depth,
+                                                      self.map.ctypes.data, self.map_cnt, int(tag)))
+
+
+def parse_dev(verifier, n, pool, txn_off, txn_sz, txn_out, txn_t_sz, stream=None):
+    """fd_txn_parse over n device-resident payloads (torch tensors / pointers)."""
+    return lib().fd_txn_hip_parse_dev(verifier.ctx, int(n), _ptr(pool), _ptr(txn_off), _ptr(txn_sz), _ptr(txn_out),
+                                      _ptr(txn_t_sz), stream)
+
+
+class VerifyTile:
+    """One verify tile on one GPU: fd_verify_ctx_t's tcache, hashmap_seed,
+    bundle state and metrics, with frags processed in device-resident batches."""
+
+    def __init__(self, verifier=None, max_txn=1 << 16, hashmap_seed=0, tcache_depth=4194302, tcache_map_cnt=0,
+                 device=0, chunk_sigs=1 << 20):
+        self._lib = lib()
+        self.verifier = verifier if verifier is not None else Verifier(device=device, chunk_sigs=chunk_sigs)
+        self.max_txn = int(max_txn)
+        self.tile = self._lib.fd_verify_hip_tile_new(self.verifier.ctx, self.max_txn, int(hashmap_seed) & (2**64 - 1),
+                                                     int(tcache_depth), int(tcache_map_cnt))
+        if not self.tile:
+            raise RuntimeError("fd_verify_hip_tile_new failed (bad tcache depth / map_cnt?)")
+        self._joined = None
+        self._pending = []
+
+    def join_tcache(self, tc: Tcache):
+        """Use an external tcache (the reference tile's ctx->tcache_* arrays)."""
+        self._joined = tc
+        self._lib.fd_verify_hip_tile_join_tcache(self.tile, tc.oldest.ctypes.data, tc.ring.ctypes.data, tc.depth,
+                                                 tc.map.ctypes.data, tc.map_cnt)
+
+    def tcache_reset(self):
+        self._lib.fd_verify_hip_tile_tcache_reset(self.tile)
+
+    def set_seed(self, seed):
+        self._lib.fd_verify_hip_tile_set_seed(self.tile, int(seed) & (2**64 - 1))
+
+    def submit(self, n, pool, txn_off, txn_sz, txn_out=None):
+        """Device tensors: pool uint8, txn_off int32 (u32 bits), txn_sz int16 (u16 bits)."""
+        rc = self._lib.fd_verify_hip_tile_submit(self.tile, int(n), _ptr(pool), _ptr(txn_off), _ptr(txn_sz),
+                                                 _ptr(txn_out))
+        if rc:
+            raise RuntimeError(f"fd_verify_hip_tile_submit: {rc}")
+        self._pending.append((int(n), (pool, txn_off, txn_sz, txn_out)))   # keep buffers alive
+
+    def complete(self, bundle_id=None):
+        n, _keep = self._pending.pop(0)
+        result = np.zeros(n, np.int8)
+        tag = np.zeros(n, np.uint64)
+        tsz = np.zeros(n, np.uint16)
+        bid = None
+        if bundle_id is not None:
+            bid = np.ascontiguousarray(bundle_id, np.uint64)
+            assert bid.shape == (n,)
+        rc = self._lib.fd_verify_hip_tile_complete(self.tile, None if bid is None else bid.ctypes.data,
+                                                   result.ctypes.data, tag.ctypes.data, tsz.ctypes.data)
+        if rc:
+            raise RuntimeError(f"fd_verify_hip_tile_complete: {rc}")
+        return result, tag, tsz
+
+    def after_frags(self, n, pool, txn_off, txn_sz, bundle_id=None, txn_out=None):
+        self.submit(n, pool, txn_off, txn_sz, txn_out)
+        return self.complete(bundle_id)
+
+    def metrics(self):
+        out = np.zeros(6, np.uint64)
+        self._lib.fd_verify_hip_tile_metrics(self.tile, out.ctypes.data)
+        keys = ("parse_fail_cnt", "verify_fail_cnt", "dedup_fail_cnt", "bundle_peer_fail_cnt", "published", "sigs")
+        return dict(zip(keys, (int(x) for x in out)))
+
+    def last_timing(self):
+        out = np.zeros(3, np.float64)
+        self._lib.fd_verify_hip_tile_last_timing(self.tile, out.ctypes.data)
+        return {"gpu_ms": float(out[0]), "host_ms": float(out[1]), "sigs": int(out[2])}
+
+    def close(self):
+        if self.tile:
+            self._lib.fd_verify_hip_tile_delete(self.tile)
+            self.tile = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

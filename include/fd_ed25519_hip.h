@@ -102,6 +102,9 @@ void                   fd_ed25519_hip_set_errmode( fd_ed25519_hip_ctx_t * ctx, i
 void fd_ed25519_hip_set_timing( fd_ed25519_hip_ctx_t * ctx, int on );
 void fd_ed25519_hip_get_timing( fd_ed25519_hip_ctx_t const * ctx, double * prep_ms, double * dsm_ms,
                                 ulong * launches );
+/* signatures that passed every pre-check and ran through k_verify_dsm,
+   accumulated while timing is on (the unit of the DSM roofline) */
+ulong fd_ed25519_hip_get_dsm_units( fd_ed25519_hip_ctx_t const * ctx );
 
 /* Per-signature verify, inputs resident in HBM, asynchronous on `stream`
    (NULL: the context's stream).  bitmap may be NULL.  Returns 0. */

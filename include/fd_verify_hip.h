@@ -1,0 +1,175 @@
+#ifndef HEADER_fd_verify_hip_h
+#define HEADER_fd_verify_hip_h
+
+/* fd_verify_hip.h -- C ABI of the verify-tile layer of the MI355X engine
+   (verify-tile integration and GPU txn parse).
+
+   It takes the verify tile's raw frags (UDP payloads, fd_txn_m_payload) in
+   device memory and reproduces, for a batch of frags in arrival order, what
+   the reference verify tile does per frag:
+
+     after_frag     src/disco/verify/fd_verify_tile.c:101-161
+                    fd_txn_parse -> bundle bookkeeping -> fd_txn_verify ->
+                    publish / count the failure
+     fd_txn_verify  src/disco/verify/fd_verify_tile.h:61-111
+                    tag = fd_hash(seed, sig0, 64); tcache query (dedup);
+                    fd_ed25519_verify_batch_single_msg over the txn's
+                    signatures; tcache insert
+
+   Work split (MI355X-first):
+     GPU  k_txn_parse   one lane per frag: fd_txn_parse_core restated
+                        (fd_txn_parse.c:7-254), fd_txn_t written out, sig0
+                        tag (fd_hash, util/fd_hash.c:14-72)
+          k_txn_expand  wave-aggregated slot allocation, txn -> signature
+                        records (sig, pubkey, message span)
+          verify        fd_ed25519_hip_verify_dev over all records
+          group reduce  fd_ed25519_verify_batch_single_msg per txn
+     host the order-dependent part: the tcache (dedup) and the bundle state
+          machine, over 11 bytes per frag, in arrival order.  The tcache is
+          the reference's own memory layout (fd_tcache.h), so a verify tile
+          can hand its ctx->tcache_{sync,ring,map} to the engine.
+
+   Every verdict equals the reference's sequential per-frag result: a frag
+   the reference would drop before verifying (dedup hit, failed bundle peer)
+   is verified here too and the extra verdict discarded.
+
+   Library: firedancer_amd/libfd_ed25519_hip.so (same library as
+   fd_ed25519_hip.h).  No torch or HIP types in any signature. */
+
+#include "fd_ed25519_hip.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef unsigned short ushort;
+
+/* fd_txn.h:60,65 */
+#define FD_TXN_HIP_MAX_SZ  852UL    /* FD_TXN_MAX_SZ: out stride of the parse */
+#define FD_TXN_HIP_MTU     1232UL   /* FD_TXN_MTU */
+
+/* fd_verify_tile.h:9-11 */
+#define FD_TXN_VERIFY_SUCCESS  0
+#define FD_TXN_VERIFY_FAILED  -1
+#define FD_TXN_VERIFY_DEDUP   -2
+
+/* Per-frag outcome of after_frag.  PUBLISH / FAILED / DEDUP are
+   fd_txn_verify's codes; the two others are the early returns of
+   after_frag (fd_verify_tile.c:125-134), each with its metric. */
+#define FD_VERIFY_HIP_FRAG_PUBLISH      ( 0)
+#define FD_VERIFY_HIP_FRAG_VERIFY_FAIL  (-1)   /* metrics.verify_fail_cnt      */
+#define FD_VERIFY_HIP_FRAG_DEDUP        (-2)   /* metrics.dedup_fail_cnt       */
+#define FD_VERIFY_HIP_FRAG_PARSE_FAIL   (-3)   /* metrics.parse_fail_cnt       */
+#define FD_VERIFY_HIP_FRAG_BUNDLE_PEER  (-4)   /* metrics.bundle_peer_fail_cnt */
+
+/* ---- GPU txn parse ------------------------------------------------------
+
+   Parses n payloads: payload j = d_pool[ d_txn_off[j], +d_txn_sz[j] ).
+   d_txn_t_sz[j] = fd_txn_parse( payload, sz, out, NULL ) (the fd_txn_t
+   footprint 20+10*instr_cnt+8*lut_cnt, or 0 on a parse failure);
+   replaces fd_txn_parse / fd_txn_parse_core with instr_max =
+   FD_TXN_INSTR_MAX (fd_txn.h:712-715, fd_txn_parse.c:7-254).
+   d_txn_out (may be NULL) receives each fd_txn_t at stride
+   FD_TXN_HIP_MAX_SZ, bytes identical to the reference's output (only the
+   first d_txn_t_sz[j] bytes are defined).  Async on stream (NULL: the
+   ctx's stream). */
+int
+fd_txn_hip_parse_dev( fd_ed25519_hip_ctx_t * ctx,
+                      ulong                  n,
+                      uchar const *          d_pool,
+                      uint const *           d_txn_off,
+                      ushort const *         d_txn_sz,
+                      uchar *                d_txn_out,
+                      ushort *               d_txn_t_sz,
+                      void *                 stream );
+
+/* fd_hash (util/fd_hash.c:14-72) on the host, for callers that need the
+   same tag the engine computes on the GPU. */
+ulong
+fd_verify_hip_hash( ulong seed, void const * buf, ulong sz );
+
+/* ---- tcache on the reference layout (fd_tcache.h:115-410) ---------------
+
+   ring[depth], map[map_cnt] (power of 2, >= depth+2), oldest in [0,depth).
+   Same memory effects as fd_tcache_reset / FD_TCACHE_QUERY /
+   FD_TCACHE_INSERT, so the arrays stay interchangeable with the
+   reference's.  Tag 0 is the null tag (a query for it always "finds"). */
+ulong fd_verify_hip_tcache_map_cnt_default( ulong depth );
+ulong fd_verify_hip_tcache_reset ( ulong * ring, ulong depth, ulong * map, ulong map_cnt );
+int   fd_verify_hip_tcache_query ( ulong const * map, ulong map_cnt, ulong tag );
+int   fd_verify_hip_tcache_insert( ulong * oldest, ulong * ring, ulong depth,
+                                   ulong * map, ulong map_cnt, ulong tag );
+
+/* ---- verify tile engine --------------------------------------------------
+
+   A tile owns device scratch for up to max_txn frags per batch (two batches
+   in flight), a tcache (internal, or joined from the caller), the bundle
+   state and the metrics.  It runs on ctx's device and stream.
+
+     submit(k)   enqueues parse, expand, verify and per-txn reduce of batch k
+                 and returns once the GPU has counted k's signatures (so it
+                 also waits for batch k-1's GPU work);
+     complete(k) waits for batch k and runs the ordered host pass, writing
+                 result[j] (FD_VERIFY_HIP_FRAG_*), tag[j] (opt_sig on
+                 publish, else 0) and txn_t_sz[j] (parse footprint).
+
+   Pipelined use: submit(0); for k: submit(k+1); complete(k).  The host pass
+   of batch k then overlaps the GPU work of batch k+1.  Batches must be
+   completed in submission order; at most two may be outstanding.
+   Payload memory (d_pool, offsets, sizes, d_txn_out) must stay valid until
+   the batch completes.  bundle_id (host, NULL: none) is given at completion,
+   it only affects the ordered pass. */
+
+typedef struct fd_verify_hip_tile fd_verify_hip_tile_t;
+
+fd_verify_hip_tile_t *
+fd_verify_hip_tile_new( fd_ed25519_hip_ctx_t * ctx,
+                        ulong                  max_txn,
+                        ulong                  hashmap_seed,   /* fd_verify_ctx_t.hashmap_seed */
+                        ulong                  tcache_depth,   /* tile->verify.tcache_depth    */
+                        ulong                  tcache_map_cnt );/* 0: fd_tcache_map_cnt_default */
+
+/* Use the caller's tcache (fd_verify_ctx_t tcache_sync/ring/depth/map/map_cnt,
+   fd_verify_tile.c:196-200) instead of the tile's own from now on. */
+void
+fd_verify_hip_tile_join_tcache( fd_verify_hip_tile_t * tile, ulong * sync, ulong * ring, ulong depth,
+                                ulong * map, ulong map_cnt );
+
+void fd_verify_hip_tile_tcache_reset( fd_verify_hip_tile_t * tile );
+
+/* Replace hashmap_seed for batches submitted from now on (the reference
+   draws it once per tile boot, fd_verify_tile.c:170; a new seed gives the
+   same traffic fresh tags, which the bench uses to replay one batch). */
+void fd_verify_hip_tile_set_seed( fd_verify_hip_tile_t * tile, ulong hashmap_seed );
+void fd_verify_hip_tile_delete( fd_verify_hip_tile_t * tile );
+
+int
+fd_verify_hip_tile_submit( fd_verify_hip_tile_t * tile,
+                           ulong                  n,
+                           uchar const *          d_pool,
+                           uint const *           d_txn_off,
+                           ushort const *         d_txn_sz,
+                           uchar *                d_txn_out );   /* NULL or n*FD_TXN_HIP_MAX_SZ */
+
+int
+fd_verify_hip_tile_complete( fd_verify_hip_tile_t * tile,
+                             ulong const *          bundle_id,   /* host, n entries or NULL */
+                             signed char *          result,      /* host, n */
+                             ulong *                tag,         /* host, n or NULL */
+                             ushort *               txn_t_sz );  /* host, n or NULL */
+
+/* metrics (cumulative): out[0..3] = parse_fail, verify_fail, dedup_fail,
+   bundle_peer_fail (fd_verify_tile.h:51-57); out[4] = published,
+   out[5] = signatures sent to the GPU verify */
+void fd_verify_hip_tile_metrics( fd_verify_hip_tile_t const * tile, ulong out[ 6 ] );
+
+/* timing of the last completed batch (ms): out[0] = GPU (first kernel to
+   results on host, HIP events), out[1] = host ordered pass, out[2] =
+   signatures in the batch */
+void fd_verify_hip_tile_last_timing( fd_verify_hip_tile_t const * tile, double out[ 3 ] );
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* HEADER_fd_verify_hip_h */

@@ -5,24 +5,25 @@ import os
 import re
 import subprocess
 
-from firedancer_amd import ed25519
+from firedancer_amd import ed25519, verify_tile
 from firedancer_amd.build import LIB, build
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def declared_functions():
-    hdr = open(os.path.join(REPO, "include", "fd_ed25519_hip.h")).read()
+def declared_functions(header="fd_ed25519_hip.h"):
+    hdr = open(os.path.join(REPO, "include", header)).read()
     hdr = re.sub(r"/\*.*?\*/", "", hdr, flags=re.S)
-    names = set(re.findall(r"\b(fd_ed25519\w*)\s*\(", hdr))
+    names = set(re.findall(r"\b(fd_\w*)\s*\(", hdr))
     return names
 
 
 def test_build_and_exports():
     build()
     assert os.path.exists(LIB)
-    names = declared_functions()
-    assert names == set(ed25519.EXPORTS)
+    assert declared_functions("fd_ed25519_hip.h") == set(ed25519.EXPORTS)
+    assert declared_functions("fd_verify_hip.h") == set(verify_tile.EXPORTS)
+    names = set(ed25519.EXPORTS) | set(verify_tile.EXPORTS)
     out = subprocess.check_output(["nm", "-D", "--defined-only", LIB]).decode()
     exported = set(re.findall(r" T (\w+)", out))
     assert names <= exported, names - exported
