@@ -1,8 +1,8 @@
 """Build the gfx950 engine in-tree: firedancer_amd/libfd_ed25519_hip.so.
 
-Steps: regenerate csrc/fe25519_asm.h from csrc/gen_fe_asm.py, then one hipcc
-invocation (--offload-arch=gfx950) producing a C-ABI shared library.  hipcc
-cross-compiles without a GPU, so this runs in the build container too.
+One hipcc invocation (--offload-arch=gfx950) producing a C-ABI shared
+library.  hipcc cross-compiles without a GPU, so this runs in the build
+container too.
 """
 import os
 import subprocess
@@ -11,9 +11,8 @@ import sys
 PKG = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(PKG, "csrc")
 LIB = os.path.join(PKG, "libfd_ed25519_hip.so")
-SCRATCH_BASE = os.environ.get("FE_SCRATCH_BASE", "124")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
-SOURCES = ["fd_ed25519_hip.hip", "fd_ed25519_dev.h", "gen_fe_asm.py", "fd_txn_hip.hip"]
+SOURCES = ["fd_ed25519_hip.hip", "fd_ed25519_dev.h", "fd_txn_hip.hip"]
 UNITS = ["fd_ed25519_hip.hip", "fd_txn_hip.hip"]
 
 
@@ -32,12 +31,7 @@ def build(force=False, verbose=False, variant=None, defines=()):
     """Build the library (or an experimental variant with extra -D defines,
     loaded when FD_ED25519_HIP_LIB names it)."""
     lib_path = variant_path(variant)
-    asm_h = os.path.join(CSRC, "fe25519_asm.h")
-    gen = os.path.join(CSRC, "gen_fe_asm.py")
-    env = dict(os.environ, FE_SCRATCH_BASE=SCRATCH_BASE)
-    if force or _stale(asm_h, [gen]) or f"FE_ASM_SCRATCH_BASE {SCRATCH_BASE}\n" not in open(asm_h).read():
-        subprocess.check_call([sys.executable, gen, asm_h], env=env)
-    deps = [os.path.join(CSRC, s) for s in SOURCES] + [asm_h] + [os.path.join(PKG, "..", "include", h) for h in ("fd_ed25519_hip.h", "fd_verify_hip.h")]
+    deps = [os.path.join(CSRC, s) for s in SOURCES] + [os.path.join(PKG, "..", "include", h) for h in ("fd_ed25519_hip.h", "fd_verify_hip.h")]
     if force or _stale(lib_path, deps):
         cmd = [HIPCC, "--offload-arch=gfx950", "-O3", "-fPIC", "-shared", "-std=c++17"] + \
               [f"-D{d}" for d in defines] + ["-o", lib_path + ".tmp"] + [os.path.join(CSRC, u) for u in UNITS]

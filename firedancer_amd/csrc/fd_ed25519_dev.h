@@ -1,16 +1,30 @@
 /* fd_ed25519_dev.h -- device-side building blocks of the gfx950 ed25519
-   verify engine: GF(2^255-19) helpers on top of the generated fe25519_asm.h,
-   extended-coordinate group law, point decode, SHA-512 and scalar mod L.
+   verify engine: GF(2^255-19) arithmetic, extended-coordinate group law,
+   point decode, SHA-512 and scalar mod L.
 
    Every function restates the semantics of the reference verify path
    (anoushk1234/firedancer src/ballet/ed25519/, cited per function); the
-   arithmetic is organised for one signature per 64-wide-wave lane with
-   8x32-bit limbs (see gen_fe_asm.py for the limb/bound conventions:
-   "loose" < 2^256, "tight" < 2^255 + 2^43). */
+   arithmetic is organised for one signature per 64-wide-wave lane.
+
+   Field representation (unsaturated, 9 limbs of u32):
+     value = sum_{i<8} v[i] 2^(29 i) + v[8] 2^232
+   A product column of 29-bit limbs is < 2^62, so a 64-bit accumulator
+   (v_mad_u64_u32 with 64-bit addend) takes a whole column with no carry
+   tracking, squaring doubles an operand limb instead of the product, and
+   add is 9 plain v_add_u32.  Bounds (proved worst case by
+   tools/fe29_bounds.py, which mirrors every formula here; run by
+   tests/test_fe_bounds.py):
+     "tight"  (every fe_mul / fe_sq output): v[i] <= 2^29-1, except
+              v[1] < 2^29 + 2^17 and v[8] <= 2^23-1
+     fe_add   no carry: limb-wise sums (< 2^32)
+     fe_sub   a + 2p - b, b must be tight (2p's limbs dominate tight limbs)
+     fe_norm  one carry pass, restores ~tight limbs; used where a product's
+              operands would otherwise overflow a column (dbl: F, and E when T
+              is needed; add: E)
+   fe_canon gives the unique representative in [0, p) with limbs in range. */
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
-#include "fe25519_asm.h"
 
 typedef uint32_t u32;
 typedef uint64_t u64;
@@ -21,22 +35,118 @@ typedef uint8_t  u8;
 /**********************************************************************/
 /* Field elements                                                      */
 
-struct fe { u32 v[8]; };
+#define FE_M29 0x1fffffffu
+#define FE_M23 0x007fffffu
 
-DEV void fe_set( fe & r, u32 c0, u32 c1, u32 c2, u32 c3, u32 c4, u32 c5, u32 c6, u32 c7 ) {
-  r.v[0]=c0; r.v[1]=c1; r.v[2]=c2; r.v[3]=c3; r.v[4]=c4; r.v[5]=c5; r.v[6]=c6; r.v[7]=c7;
+struct fe { u32 v[9]; };
+
+/* Scheduling fence after every multiply: left free, the machine scheduler
+   overlaps consecutive multiplies of a long chain (pow22523, the ladder) until
+   the kernel runs out of VGPRs and spills to AGPRs; fencing each multiply
+   keeps the live set to ~one product column pair plus the operands. */
+#ifndef FE_NO_FENCE
+#define FE_SCHED_FENCE() __builtin_amdgcn_sched_barrier( 0 )
+#else
+#define FE_SCHED_FENCE()
+#endif
+
+DEV void fe_set( fe & r, u32 c0, u32 c1, u32 c2, u32 c3, u32 c4, u32 c5, u32 c6, u32 c7, u32 c8 ) {
+  r.v[0]=c0; r.v[1]=c1; r.v[2]=c2; r.v[3]=c3; r.v[4]=c4; r.v[5]=c5; r.v[6]=c6; r.v[7]=c7; r.v[8]=c8;
 }
-DEV void fe_0( fe & r ) { fe_set( r, 0,0,0,0,0,0,0,0 ); }
-DEV void fe_1( fe & r ) { fe_set( r, 1,0,0,0,0,0,0,0 ); }
-/* d = -121665/121666, 2d, sqrt(-1): fd_f25519_table_ref.c:28-47 */
-DEV void fe_d( fe & r )      { fe_set( r, 0x135978a3u,0x75eb4dcau,0x4141d8abu,0x00700a4du,0x7779e898u,0x8cc74079u,0x2b6ffe73u,0x52036ceeu ); }
-DEV void fe_d2( fe & r )     { fe_set( r, 0x26b2f159u,0xebd69b94u,0x8283b156u,0x00e0149au,0xeef3d130u,0x198e80f2u,0x56dffce7u,0x2406d9dcu ); }
-DEV void fe_sqrtm1( fe & r ) { fe_set( r, 0x4a0ea0b0u,0xc4ee1b27u,0xad2fe478u,0x2f431806u,0x3dfbd7a7u,0x2b4d0099u,0x4fc1df0bu,0x2b832480u ); }
+DEV void fe_0( fe & r ) { fe_set( r, 0,0,0,0,0,0,0,0,0 ); }
+DEV void fe_1( fe & r ) { fe_set( r, 1,0,0,0,0,0,0,0,0 ); }
+/* d = -121665/121666, 2d, sqrt(-1) (fd_f25519_table_ref.c:28-47), 1/2 */
+DEV void fe_d( fe & r )      { fe_set( r, 0x135978a3u,0x0f5a6e50u,0x10762addu,0x00149a82u,0x1e898007u,0x003cbbbcu,0x19ce331du,0x1dc56dffu,0x0052036cu ); }
+DEV void fe_d2( fe & r )     { fe_set( r, 0x06b2f159u,0x1eb4dca1u,0x00ec55bau,0x00293505u,0x1d13000eu,0x00797779u,0x139c663au,0x1b8adbffu,0x002406d9u ); }
+DEV void fe_sqrtm1( fe & r ) { fe_set( r, 0x0a0ea0b0u,0x0770d93au,0x0bf91e31u,0x06300d5au,0x1d7a72f4u,0x004c9efdu,0x1c2cad34u,0x1009f83bu,0x002b8324u ); }
+DEV void fe_inv2( fe & r )   { fe_set( r, 0x1ffffff7u,0x1fffffffu,0x1fffffffu,0x1fffffffu,0x1fffffffu,0x1fffffffu,0x1fffffffu,0x1fffffffu,0x003fffffu ); }
 
-DEV void fe_mul( fe & r, fe const & a, fe const & b ) { fe_mul( r.v, a.v, b.v ); }
-DEV void fe_sq ( fe & r, fe const & a )               { fe_mul( r.v, a.v, a.v ); }
-DEV void fe_add( fe & r, fe const & a, fe const & b ) { fe_add( r.v, a.v, b.v ); }
-DEV void fe_sub( fe & r, fe const & a, fe const & b ) { fe_sub( r.v, a.v, b.v ); }
+/* Column k of the product: sum over i+j=k, 0<=i,j<=8.  fe_mul computes the
+   high columns 9..16 first (normalised to 29-bit limbs z[0..7], z[8] = the
+   carry out of column 16), then the low columns 0..8 each led by
+   1216*z[k] (2^261 == 19*2^6 mod p), carrying 29 bits at a time; column 8
+   splits at bit 255 and its overflow folds back into limb 0 with 19. */
+DEV void fe_mul( fe & r, fe const & a, fe const & b ) {
+  u32 z[9], o[9];
+  u64 acc = 0;
+  #pragma unroll
+  for( int k=9; k<=16; k++ ) {
+    acc = (k == 9) ? 0ull : (acc >> 29);
+    #pragma unroll
+    for( int i=k-8; i<=8; i++ ) acc += (u64)a.v[i] * b.v[k-i];
+    z[k-9] = (u32)acc & FE_M29;
+  }
+  z[8] = (u32)(acc >> 29);
+  #pragma unroll
+  for( int k=0; k<=8; k++ ) {
+    acc = (k == 0 ? 0ull : (acc >> 29)) + (u64)z[k] * 1216u;
+    #pragma unroll
+    for( int i=0; i<=k; i++ ) acc += (u64)a.v[i] * b.v[k-i];
+    if( k < 8 ) o[k] = (u32)acc & FE_M29;
+  }
+  o[8] = (u32)acc & FE_M23;
+  u64 t = (acc >> 23) * 19u + o[0];
+  o[0] = (u32)t & FE_M29;
+  o[1] += (u32)(t >> 29);
+  #pragma unroll
+  for( int i=0; i<9; i++ ) r.v[i] = o[i];
+  FE_SCHED_FENCE();
+}
+
+/* a^2: same columns, off-diagonal products taken once against 2*a_i */
+DEV void fe_sq( fe & r, fe const & a ) {
+  u32 d[9], z[9], o[9];
+  #pragma unroll
+  for( int i=0; i<9; i++ ) d[i] = a.v[i] << 1;
+  u64 acc = 0;
+  #pragma unroll
+  for( int k=9; k<=16; k++ ) {
+    acc = (k == 9) ? 0ull : (acc >> 29);
+    #pragma unroll
+    for( int i=k-8; 2*i<k; i++ ) acc += (u64)d[i] * a.v[k-i];
+    if( (k & 1) == 0 ) acc += (u64)a.v[k/2] * a.v[k/2];
+    z[k-9] = (u32)acc & FE_M29;
+  }
+  z[8] = (u32)(acc >> 29);
+  #pragma unroll
+  for( int k=0; k<=8; k++ ) {
+    acc = (k == 0 ? 0ull : (acc >> 29)) + (u64)z[k] * 1216u;
+    #pragma unroll
+    for( int i=0; 2*i<k; i++ ) acc += (u64)d[i] * a.v[k-i];
+    if( (k & 1) == 0 ) acc += (u64)a.v[k/2] * a.v[k/2];
+    if( k < 8 ) o[k] = (u32)acc & FE_M29;
+  }
+  o[8] = (u32)acc & FE_M23;
+  u64 t = (acc >> 23) * 19u + o[0];
+  o[0] = (u32)t & FE_M29;
+  o[1] += (u32)(t >> 29);
+  #pragma unroll
+  for( int i=0; i<9; i++ ) r.v[i] = o[i];
+  FE_SCHED_FENCE();
+}
+
+DEV void fe_add( fe & r, fe const & a, fe const & b ) {
+  #pragma unroll
+  for( int i=0; i<9; i++ ) r.v[i] = a.v[i] + b.v[i];
+}
+
+/* a - b + 2p (b tight) */
+DEV void fe_sub( fe & r, fe const & a, fe const & b ) {
+  r.v[0] = (a.v[0] - b.v[0]) + 0x3fffffdau;
+  #pragma unroll
+  for( int i=1; i<8; i++ ) r.v[i] = (a.v[i] - b.v[i]) + 0x3ffffffeu;
+  r.v[8] = (a.v[8] - b.v[8]) + 0x00fffffeu;
+}
+
+/* one carry pass (no overflow for limbs < 2^32 - 8) */
+DEV void fe_norm( fe & r, fe const & a ) {
+  u32 c = 0;
+  #pragma unroll
+  for( int i=0; i<8; i++ ) { u32 x = a.v[i] + c; c = x >> 29; r.v[i] = x & FE_M29; }
+  u32 x = a.v[8] + c;
+  r.v[8] = x & FE_M23;
+  r.v[0] += 19u * (x >> 23);
+}
 
 DEV void fe_sqn( fe & r, fe const & a, int n ) {
   fe_sq( r, a );
@@ -44,48 +154,41 @@ DEV void fe_sqn( fe & r, fe const & a, int n ) {
   for( int i=1; i<n; i++ ) fe_sq( r, r );
 }
 
-/* loose (< 2^256) -> canonical [0,p).  Fold bit 255 with 19, then subtract
-   p once if needed (t = v+19 >= 2^255  <=>  v >= p). */
+/* any bounded a -> canonical [0,p): two carry passes leave limbs in range and
+   the value < 2^255; then subtract p once iff value + 19 >= 2^255. */
 DEV void fe_canon( fe & r, fe const & a ) {
-  u32 top = a.v[7] >> 31;
-  u64 c = (u64)a.v[0] + 19u*top;
-  u32 v[8];
-  v[0] = (u32)c; c >>= 32;
+  fe t; fe_norm( t, a ); fe_norm( t, t );
+  u32 c = (t.v[0] + 19u) >> 29;
   #pragma unroll
-  for( int i=1; i<7; i++ ) { c += a.v[i]; v[i] = (u32)c; c >>= 32; }
-  v[7] = (u32)(c + (a.v[7] & 0x7fffffffu));
-  /* now v < 2^255 + 19; t = v + 19 */
-  u32 t[8]; c = (u64)v[0] + 19u;
-  t[0] = (u32)c; c >>= 32;
+  for( int i=1; i<8; i++ ) c = (t.v[i] + c) >> 29;
+  u32 q = (t.v[8] + c) >> 23;              /* t >= p */
+  u32 x = t.v[0] + 19u*q;
+  r.v[0] = x & FE_M29; c = x >> 29;
   #pragma unroll
-  for( int i=1; i<8; i++ ) { c += v[i]; t[i] = (u32)c; c >>= 32; }
-  u32 ge = t[7] >> 31;                      /* v >= p */
-  u32 m = 0u - ge;
-  t[7] &= 0x7fffffffu;
-  #pragma unroll
-  for( int i=0; i<8; i++ ) r.v[i] = (t[i] & m) | (v[i] & ~m);
+  for( int i=1; i<8; i++ ) { x = t.v[i] + c; r.v[i] = x & FE_M29; c = x >> 29; }
+  r.v[8] = (t.v[8] + c) & FE_M23;
 }
 
 DEV bool fe_is_zero_c( fe const & c ) {   /* c canonical */
-  return (c.v[0]|c.v[1]|c.v[2]|c.v[3]|c.v[4]|c.v[5]|c.v[6]|c.v[7]) == 0u;
+  return (c.v[0]|c.v[1]|c.v[2]|c.v[3]|c.v[4]|c.v[5]|c.v[6]|c.v[7]|c.v[8]) == 0u;
 }
 DEV bool fe_eq_c( fe const & a, fe const & b ) {   /* both canonical */
-  return ((a.v[0]^b.v[0])|(a.v[1]^b.v[1])|(a.v[2]^b.v[2])|(a.v[3]^b.v[3])|
-          (a.v[4]^b.v[4])|(a.v[5]^b.v[5])|(a.v[6]^b.v[6])|(a.v[7]^b.v[7])) == 0u;
+  return ((a.v[0]^b.v[0])|(a.v[1]^b.v[1])|(a.v[2]^b.v[2])|(a.v[3]^b.v[3])|(a.v[4]^b.v[4])|
+          (a.v[5]^b.v[5])|(a.v[6]^b.v[6])|(a.v[7]^b.v[7])|(a.v[8]^b.v[8])) == 0u;
 }
-DEV bool fe_is_zero( fe const & a ) { fe c; fe_canon( c, a ); return fe_is_zero_c( c ); }
 
-/* r = -a for tight a (result loose) */
+/* r = -a for tight a (result 2p-bounded; fe_norm it before use as tight) */
 DEV void fe_neg( fe & r, fe const & a ) { fe z; fe_0( z ); fe_sub( r, z, a ); }
 
-/* conditional swap (mask is 0 or ~0 per lane) */
+/* conditional swap / move (mask is 0 or ~0 per lane; xor form: v_cndmask_b32
+   issues at 1/8 the rate of v_xor_b32 on gfx950, profiles/r01_valu_rates_b.txt) */
 DEV void fe_cswap( fe & a, fe & b, u32 mask ) {
   #pragma unroll
-  for( int i=0; i<8; i++ ) { u32 t = (a.v[i] ^ b.v[i]) & mask; a.v[i] ^= t; b.v[i] ^= t; }
+  for( int i=0; i<9; i++ ) { u32 t = (a.v[i] ^ b.v[i]) & mask; a.v[i] ^= t; b.v[i] ^= t; }
 }
 DEV void fe_cmov( fe & r, fe const & a, u32 mask ) {   /* r = mask ? a : r */
   #pragma unroll
-  for( int i=0; i<8; i++ ) r.v[i] ^= (r.v[i] ^ a.v[i]) & mask;
+  for( int i=0; i<9; i++ ) r.v[i] ^= (r.v[i] ^ a.v[i]) & mask;
 }
 
 /* z^(2^252-3): fd_f25519.c:25-74 (same exponent; this addition chain) */
@@ -116,35 +219,58 @@ DEV void fe_invert( fe & out, fe const & z ) {
 /* 32 little-endian bytes (as 8 LE u32 words) -> fe, masking bit 255
    (fd_f25519.h frombytes accepts non-canonical y in [p, 2^255)) */
 DEV void fe_from_words( fe & r, u32 const w[8] ) {
+  r.v[0] = w[0] & FE_M29;
   #pragma unroll
-  for( int i=0; i<7; i++ ) r.v[i] = w[i];
-  r.v[7] = w[7] & 0x7fffffffu;
+  for( int i=1; i<8; i++ ) {
+    int b = 29*i, j = b >> 5, s = b & 31;
+    u32 x = (s + 29 <= 32) ? (w[j] >> s) : __builtin_amdgcn_alignbit( w[j+1], w[j], (u32)s );
+    r.v[i] = x & FE_M29;
+  }
+  r.v[8] = (w[7] >> 8) & FE_M23;
+}
+
+/* canonical fe -> 8 LE u32 words */
+DEV void fe_to_words( u32 w[8], fe const & a ) {
+  w[0] = a.v[0]        | (a.v[1] << 29);
+  w[1] = (a.v[1] >> 3)  | (a.v[2] << 26);
+  w[2] = (a.v[2] >> 6)  | (a.v[3] << 23);
+  w[3] = (a.v[3] >> 9)  | (a.v[4] << 20);
+  w[4] = (a.v[4] >> 12) | (a.v[5] << 17);
+  w[5] = (a.v[5] >> 15) | (a.v[6] << 14);
+  w[6] = (a.v[6] >> 18) | (a.v[7] << 11);
+  w[7] = (a.v[7] >> 21) | (a.v[8] << 8);
 }
 
 /**********************************************************************/
 /* Group: twisted Edwards a=-1, extended coordinates, HWCD'08 formulas
-   (ref/fd_curve25519.c:25-92 add, ref/fd_curve25519.h:190-211 dbl).     */
+   (ref/fd_curve25519.c:25-92 add, ref/fd_curve25519.h:190-211 dbl).
+   Normalisation points are the ones tools/fe29_bounds.py proves.        */
 
 struct ge_p3     { fe X, Y, Z, T; };
-struct ge_cached { fe YmX, YpX, T2d, Z2; };   /* (Y-X, Y+X, 2d*T, 2*Z) */
-struct ge_affc   { fe YmX, YpX, T2d; };       /* Z == 1 */
+struct ge_cached { fe YmX, YpX, T2d, Z2; };   /* (Y-X, Y+X, 2d*T, 2*Z), each normalised */
+/* affine cached point scaled by 1/2: ((y-x)/2, (y+x)/2, d*x*y); the implied
+   2*Z is 1, so the addition's D = Z1*2*Z2 is just Z1 (the result is the same
+   projective point, every output coordinate scaled by 1/4) */
+struct ge_affc   { fe YmX, YpX, T2d; };
 
 DEV void ge_identity( ge_p3 & r ) { fe_0( r.X ); fe_1( r.Y ); fe_1( r.Z ); fe_0( r.T ); }
 
 /* r = 2p.  partial_dbl + final mul; T produced only when asked. */
 DEV void ge_dbl( ge_p3 & r, ge_p3 const & p, bool needT ) {
-  fe A, B, C, S, Tp, Zp, Yp, Xp;
+  fe A, B, C, S, H, G, F, E;
   fe_add( S, p.X, p.Y );
   fe_sq( A, p.X ); fe_sq( B, p.Y ); fe_sq( C, p.Z ); fe_sq( S, S );
-  fe_add( C, C, C );          /* 2Z^2            tight */
-  fe_add( Tp, A, B );         /* A+B             tight */
-  fe_sub( Zp, A, B );         /* A-B             loose */
-  fe_add( Yp, C, Zp );        /* 2Z^2+A-B        tight */
-  fe_sub( Xp, Tp, S );        /* A+B-(X+Y)^2     loose */
-  fe_mul( r.X, Xp, Yp );
-  fe_mul( r.Y, Zp, Tp );
-  fe_mul( r.Z, Yp, Zp );
-  if( needT ) fe_mul( r.T, Xp, Tp );
+  fe_add( C, C, C );          /* 2Z^2            */
+  fe_add( H, A, B );          /* A+B             */
+  fe_sub( G, A, B );          /* A-B             */
+  fe_add( F, C, G );          /* 2Z^2+A-B        */
+  fe_norm( F, F );
+  fe_sub( E, H, S );          /* A+B-(X+Y)^2     */
+  if( needT ) fe_norm( E, E );
+  fe_mul( r.X, E, F );
+  fe_mul( r.Y, G, H );
+  fe_mul( r.Z, F, G );
+  if( needT ) fe_mul( r.T, E, H );
 }
 
 /* r = p +/- q (q in cached form).  neg is a per-lane mask (0 or ~0). */
@@ -154,22 +280,22 @@ DEV void ge_add_cached( ge_p3 & r, ge_p3 const & p, ge_cached q, u32 neg, bool n
   fe_sub( a, p.Y, p.X ); fe_add( b, p.Y, p.X );
   fe_mul( A, a, q.YmX ); fe_mul( B, b, q.YpX );
   fe_mul( C, p.T, q.T2d ); fe_mul( D, p.Z, q.Z2 );
-  fe_sub( E, B, A ); fe_add( H, B, A );
+  fe_sub( E, B, A ); fe_norm( E, E ); fe_add( H, B, A );
   fe_sub( F, D, C ); fe_add( G, D, C );
   fe_cswap( F, G, neg );                   /* ... and negate 2dT: C -> -C swaps F and G */
   fe_mul( r.X, E, F ); fe_mul( r.Y, G, H ); fe_mul( r.Z, F, G );
   if( needT ) fe_mul( r.T, E, H );
 }
 
-/* r = p +/- q with q affine (Z == 1): D = 2*Z1 */
+/* r = p +/- q with q an affine cached point scaled by 1/2 (D = Z1) */
 DEV void ge_add_affc( ge_p3 & r, ge_p3 const & p, ge_affc q, u32 neg, bool needT ) {
-  fe a, b, A, B, C, D, E, F, G, H;
+  fe a, b, A, B, C, E, F, G, H;
   fe_cswap( q.YmX, q.YpX, neg );
   fe_sub( a, p.Y, p.X ); fe_add( b, p.Y, p.X );
   fe_mul( A, a, q.YmX ); fe_mul( B, b, q.YpX );
-  fe_mul( C, p.T, q.T2d ); fe_add( D, p.Z, p.Z );
-  fe_sub( E, B, A ); fe_add( H, B, A );
-  fe_sub( F, D, C ); fe_add( G, D, C );
+  fe_mul( C, p.T, q.T2d );
+  fe_sub( E, B, A ); fe_norm( E, E ); fe_add( H, B, A );
+  fe_sub( F, p.Z, C ); fe_add( G, p.Z, C );
   fe_cswap( F, G, neg );
   fe_mul( r.X, E, F ); fe_mul( r.Y, G, H ); fe_mul( r.Z, F, G );
   if( needT ) fe_mul( r.T, E, H );
@@ -178,8 +304,10 @@ DEV void ge_add_affc( ge_p3 & r, ge_p3 const & p, ge_affc q, u32 neg, bool needT
 /* fd_curve25519_into_precomputed (ref/fd_curve25519.h:141-151) with Z doubled */
 DEV void ge_to_cached( ge_cached & c, ge_p3 const & p ) {
   fe d2; fe_d2( d2 );
-  fe_sub( c.YmX, p.Y, p.X ); fe_add( c.YpX, p.Y, p.X );
-  fe_mul( c.T2d, p.T, d2 );  fe_add( c.Z2, p.Z, p.Z );
+  fe_sub( c.YmX, p.Y, p.X ); fe_norm( c.YmX, c.YmX );
+  fe_add( c.YpX, p.Y, p.X ); fe_norm( c.YpX, c.YpX );
+  fe_mul( c.T2d, p.T, d2 );
+  fe_add( c.Z2, p.Z, p.Z );  fe_norm( c.Z2, c.Z2 );
 }
 
 /* Point decompression: fd_curve25519.c:34-61 + fd_f25519.c:122-158, with the
@@ -214,17 +342,18 @@ DEV u32 ge_decode( ge_p3 & r, u32 const w[8] ) {
   fe nx; fe_neg( nx, x ); fe_canon( nx, nx );
   fe_cmov( x, nx, ((x.v[0] & 1u) != sign) ? ~0u : 0u );
   fe_canon( r.Y, y );
-  r.X = x; fe_1( r.Z ); fe_mul( r.T, x, y );
+  r.X = x; fe_1( r.Z ); fe_mul( r.T, x, r.Y );
   return flags;
 }
 
 /* fd_curve25519.h:88-118: x==0 | y==0 | y==y0 | y==y1 (affine, canonical x,y) */
 DEV bool ge_affine_is_small_order( ge_p3 const & p ) {
   fe y0, y1;
-  fe_set( y0, 0x8f95e826u,0xb027b2c2u,0x89f4c345u,0xf098eff2u,0x05acdfd5u,0x3933c6d3u,0x880238b1u,0x05fc536du );
-  fe_set( y1, 0x706a17c7u,0x4fd84d3du,0x760b3cbau,0x0f67100du,0xfa53202au,0xc6cc392cu,0x77fdc74eu,0x7a03ac92u );
+  fe_set( y0, 0x0f95e826u,0x013d9614u,0x1d30d16cu,0x11dfe513u,0x0dfd5f09u,0x036982d6u,0x02c4e4cfu,0x0db10047u,0x0005fc53u );
+  fe_set( y1, 0x106a17c7u,0x1ec269ebu,0x02cf2e93u,0x0e201aecu,0x1202a0f6u,0x1c967d29u,0x1d3b1b30u,0x124effb8u,0x007a03acu );
   return fe_is_zero_c( p.X ) | fe_is_zero_c( p.Y ) | fe_eq_c( p.Y, y0 ) | fe_eq_c( p.Y, y1 );
 }
+
 
 /**********************************************************************/
 /* Scalars mod L (fd_curve25519_scalar.h / .c)                         */
@@ -334,8 +463,9 @@ DEV void sc_recode256( u32 out[8], u32 const s[8] ) {
 
 DEV u64 ror64( u64 x, int n ) { return (x >> n) | (x << (64 - n)); }
 
-DEV void sha512_block( u64 st[8], u64 W[16] ) {
-  const u64 K[80] = {
+/* round constants in constant memory: the round index is wave-uniform, so
+   each K[t] is a scalar load rather than 160 VGPRs of hoisted literals */
+__constant__ u64 SHA512_K[80] = {
     0x428a2f98d728ae22ULL,0x7137449123ef65cdULL,0xb5c0fbcfec4d3b2fULL,0xe9b5dba58189dbbcULL,
     0x3956c25bf348b538ULL,0x59f111f1b605d019ULL,0x923f82a4af194f9bULL,0xab1c5ed5da6d8118ULL,
     0xd807aa98a3030242ULL,0x12835b0145706fbeULL,0x243185be4ee4b28cULL,0x550c7dc3d5ffb4e2ULL,
@@ -356,21 +486,42 @@ DEV void sha512_block( u64 st[8], u64 W[16] ) {
     0x06f067aa72176fbaULL,0x0a637dc5a2c898a6ULL,0x113f9804bef90daeULL,0x1b710b35131c471bULL,
     0x28db77f523047d84ULL,0x32caab7b40c72493ULL,0x3c9ebe0a15c9bebcULL,0x431d67c49c100d4cULL,
     0x4cc5d4becb3e42b6ULL,0x597f299cfc657e2aULL,0x5fcb6fab3ad6faecULL,0x6c44198c4a475817ULL };
+
+DEV void sha512_round( u64 & a, u64 & b, u64 & c, u64 & d, u64 & e, u64 & f, u64 & g, u64 & h, u64 w, u64 k ) {
+  u64 S1 = ror64( e, 14 ) ^ ror64( e, 18 ) ^ ror64( e, 41 );
+  u64 ch = (e & f) ^ (~e & g);
+  u64 t1 = h + S1 + ch + k + w;
+  u64 S0 = ror64( a, 28 ) ^ ror64( a, 34 ) ^ ror64( a, 39 );
+  u64 mj = (a & b) ^ (a & c) ^ (b & c);
+  d += t1; h = t1 + S0 + mj;
+}
+
+/* 80 rounds as 5 x 16: inside a 16-round group the W ring index and the
+   a..h rotation are static (no register moves); the groups stay rolled. */
+DEV void sha512_block( u64 st[8], u64 W[16] ) {
   u64 a=st[0],b=st[1],c=st[2],d=st[3],e=st[4],f=st[5],g=st[6],h=st[7];
-  #pragma unroll
-  for( int t=0; t<80; t++ ) {
-    if( t >= 16 ) {
-      u64 w15 = W[(t-15)&15], w2 = W[(t-2)&15];
-      u64 s0 = ror64( w15, 1 ) ^ ror64( w15, 8 ) ^ (w15 >> 7);
-      u64 s1 = ror64( w2, 19 ) ^ ror64( w2, 61 ) ^ (w2 >> 6);
-      W[t&15] += s0 + W[(t-7)&15] + s1;
+  #pragma unroll 1
+  for( int t0=0; t0<80; t0+=16 ) {
+    #pragma unroll
+    for( int j=0; j<16; j++ ) {
+      if( t0 ) {
+        u64 w15 = W[(j+1)&15], w2 = W[(j+14)&15];
+        u64 s0 = ror64( w15, 1 ) ^ ror64( w15, 8 ) ^ (w15 >> 7);
+        u64 s1 = ror64( w2, 19 ) ^ ror64( w2, 61 ) ^ (w2 >> 6);
+        W[j] += s0 + W[(j+9)&15] + s1;
+      }
+      u64 k = SHA512_K[t0+j];
+      switch( j & 7 ) {
+        case 0: sha512_round( a,b,c,d,e,f,g,h, W[j], k ); break;
+        case 1: sha512_round( h,a,b,c,d,e,f,g, W[j], k ); break;
+        case 2: sha512_round( g,h,a,b,c,d,e,f, W[j], k ); break;
+        case 3: sha512_round( f,g,h,a,b,c,d,e, W[j], k ); break;
+        case 4: sha512_round( e,f,g,h,a,b,c,d, W[j], k ); break;
+        case 5: sha512_round( d,e,f,g,h,a,b,c, W[j], k ); break;
+        case 6: sha512_round( c,d,e,f,g,h,a,b, W[j], k ); break;
+        case 7: sha512_round( b,c,d,e,f,g,h,a, W[j], k ); break;
+      }
     }
-    u64 S1 = ror64( e, 14 ) ^ ror64( e, 18 ) ^ ror64( e, 41 );
-    u64 ch = (e & f) ^ (~e & g);
-    u64 t1 = h + S1 + ch + K[t] + W[t&15];
-    u64 S0 = ror64( a, 28 ) ^ ror64( a, 34 ) ^ ror64( a, 39 );
-    u64 mj = (a & b) ^ (a & c) ^ (b & c);
-    h = g; g = f; f = e; e = d + t1; d = c; c = b; b = a; a = t1 + S0 + mj;
   }
   st[0]+=a; st[1]+=b; st[2]+=c; st[3]+=d; st[4]+=e; st[5]+=f; st[6]+=g; st[7]+=h;
 }

@@ -47,8 +47,10 @@
 #define F_R_SMALL    (1u<<6)
 
 #define BTAB_N      129            /* 0..128 multiples of B */
-#define BTAB_WORDS  (BTAB_N*24)    /* affine cached: YmX, YpX, T2d */
-#define ATAB_WORDS  (9*32)         /* per lane: [0..8](-A) cached: YmX, YpX, T2d, Z2 */
+#define BTAB_STRIDE 28             /* affine cached (1/2-scaled): YmX, YpX, T2d (9 limbs each) + pad */
+#define BTAB_WORDS  (BTAB_N*BTAB_STRIDE)
+#define ATAB_ENT    36             /* cached: YmX, YpX, T2d, Z2 (9 limbs each) */
+#define ATAB_WORDS  (9*ATAB_ENT)   /* per lane: [0..8](-A) */
 
 /* state record: 32 u32 words per field group, laid out SoA per chunk for
    coalescing: word w of signature i lives at st[ w*chunk + i ]. */
@@ -101,11 +103,14 @@ DEV void ge_base( ge_p3 & B ) {
   ge_decode( B, w );
 }
 
-DEV void ge_to_affc_canon( ge_affc & a, ge_p3 const & p ) {
-  fe zi, x, y, t, d2;
+/* affine cached form scaled by 1/2: ((y-x)/2, (y+x)/2, d*x*y), canonical */
+DEV void ge_to_affc_half( ge_affc & a, ge_p3 const & p ) {
+  fe zi, x, y, t, d, h;
   fe_invert( zi, p.Z ); fe_mul( x, p.X, zi ); fe_mul( y, p.Y, zi );
-  fe_d2( d2 ); fe_mul( t, x, y ); fe_mul( t, t, d2 );
-  fe_sub( a.YmX, y, x ); fe_add( a.YpX, y, x );
+  fe_d( d ); fe_inv2( h );
+  fe_mul( t, x, y ); fe_mul( t, t, d );
+  fe_sub( a.YmX, y, x ); fe_mul( a.YmX, a.YmX, h );
+  fe_add( a.YpX, y, x ); fe_mul( a.YpX, a.YpX, h );
   fe_canon( a.YmX, a.YmX ); fe_canon( a.YpX, a.YpX ); fe_canon( a.T2d, t );
 }
 
@@ -121,9 +126,11 @@ __global__ void k_btab_init( u32 * btab ) {
     ge_dbl( P, P, true );
     if( (j >> bit) & 1 ) ge_add_cached( P, P, Bc, 0u, true );
   }
-  ge_affc a; ge_to_affc_canon( a, P );
+  ge_affc a; ge_to_affc_half( a, P );
+  u32 * e = btab + j*BTAB_STRIDE;
   #pragma unroll
-  for( int i=0; i<8; i++ ) { btab[j*24+i] = a.YmX.v[i]; btab[j*24+8+i] = a.YpX.v[i]; btab[j*24+16+i] = a.T2d.v[i]; }
+  for( int i=0; i<9; i++ ) { e[i] = a.YmX.v[i]; e[9+i] = a.YpX.v[i]; e[18+i] = a.T2d.v[i]; }
+  e[27] = 0u;
 }
 
 __global__ __launch_bounds__(256)
@@ -136,24 +143,31 @@ void k_verify_prep( ulong n, ulong chunk, uchar const * __restrict__ sigs, uchar
   load_words( sig, sigs + 64*i, 16 );
   load_words( pub, pubs + 32*i, 8 );
   u32 flags = sc_is_canonical( sig + 8 ) ? 0u : F_S_BAD;                 /* user.c:159-161 */
-  ge_p3 A, R;
-  u32 fa = ge_decode( A, pub );                                            /* user.c:165 */
-  u32 fr = ge_decode( R, sig );
-  flags |= ((fa & 1u) ? F_A_NOTSQ : 0u) | ((fa & 2u) ? F_A_ZX : 0u)
-        |  ((fr & 1u) ? F_R_NOTSQ : 0u) | ((fr & 2u) ? F_R_ZX : 0u);
-  if( !(fa & 1u) && ge_affine_is_small_order( A ) ) flags |= F_A_SMALL;   /* user.c:194-199 */
-  if( !(fr & 1u) && ge_affine_is_small_order( R ) ) flags |= F_R_SMALL;
+  u32 * s = st + i;
+  /* decode A then R (user.c:165), one at a time: a rolled loop keeps the two
+     pow22523 chains from being interleaved into one register-hungry block */
+  #pragma unroll 1
+  for( int pt=0; pt<2; pt++ ) {
+    u32 w[8];
+    #pragma unroll
+    for( int q=0; q<8; q++ ) w[q] = pt ? sig[q] : pub[q];
+    ge_p3 P;
+    u32 f = ge_decode( P, w );
+    bool small = !(f & 1u) && ge_affine_is_small_order( P );              /* user.c:194-199 */
+    if( pt == 0 ) flags |= ((f & 1u) ? F_A_NOTSQ : 0u) | ((f & 2u) ? F_A_ZX : 0u) | (small ? F_A_SMALL : 0u);
+    else          flags |= ((f & 1u) ? F_R_NOTSQ : 0u) | ((f & 2u) ? F_R_ZX : 0u) | (small ? F_R_SMALL : 0u);
+    u32 xw[8], yw[8];
+    fe_to_words( xw, P.X ); fe_to_words( yw, P.Y );
+    u32 base = pt ? ST_RX : ST_AX;
+    #pragma unroll
+    for( int q=0; q<8; q++ ) { s[(base+q)*chunk] = xw[q]; s[(base+8+q)*chunk] = yw[q]; }
+  }
   u32 k[8];
   hram_mod_l( k, sig, pub, pool + moff[i], msz[i] );                       /* user.c:205-207 */
-  u32 * s = st + i;
   #pragma unroll
   for( int w=0; w<8; w++ ) {
     s[(ST_K +w)*chunk] = k[w];
     s[(ST_S +w)*chunk] = sig[8+w];
-    s[(ST_AX+w)*chunk] = A.X.v[w];
-    s[(ST_AY+w)*chunk] = A.Y.v[w];
-    s[(ST_RX+w)*chunk] = R.X.v[w];
-    s[(ST_RY+w)*chunk] = R.Y.v[w];
   }
   s[ST_FLAG*chunk] = flags;
 }
@@ -174,24 +188,30 @@ DEV int code_of( u32 f, int errmode, bool eq ) {
   return eq ? FD_ED25519_SUCCESS : FD_ED25519_ERR_MSG;
 }
 
-DEV void store_cached( u32 * t, ge_cached const & c ) {   /* 32 words, 16-byte aligned */
+DEV void store_cached( u32 * t, ge_cached const & c ) {   /* 36 words, 16-byte aligned */
+  u32 w[36];
+  #pragma unroll
+  for( int i=0; i<9; i++ ) { w[i] = c.YmX.v[i]; w[9+i] = c.YpX.v[i]; w[18+i] = c.T2d.v[i]; w[27+i] = c.Z2.v[i]; }
   uint4 * q = (uint4 *)t;
-  q[0] = make_uint4( c.YmX.v[0], c.YmX.v[1], c.YmX.v[2], c.YmX.v[3] );
-  q[1] = make_uint4( c.YmX.v[4], c.YmX.v[5], c.YmX.v[6], c.YmX.v[7] );
-  q[2] = make_uint4( c.YpX.v[0], c.YpX.v[1], c.YpX.v[2], c.YpX.v[3] );
-  q[3] = make_uint4( c.YpX.v[4], c.YpX.v[5], c.YpX.v[6], c.YpX.v[7] );
-  q[4] = make_uint4( c.T2d.v[0], c.T2d.v[1], c.T2d.v[2], c.T2d.v[3] );
-  q[5] = make_uint4( c.T2d.v[4], c.T2d.v[5], c.T2d.v[6], c.T2d.v[7] );
-  q[6] = make_uint4( c.Z2.v[0],  c.Z2.v[1],  c.Z2.v[2],  c.Z2.v[3] );
-  q[7] = make_uint4( c.Z2.v[4],  c.Z2.v[5],  c.Z2.v[6],  c.Z2.v[7] );
+  #pragma unroll
+  for( int k=0; k<9; k++ ) q[k] = make_uint4( w[4*k], w[4*k+1], w[4*k+2], w[4*k+3] );
 }
 DEV void load_cached( ge_cached & c, u32 const * t ) {
   uint4 const * q = (uint4 const *)t;
-  uint4 v;
-  v = q[0]; fe_set( c.YmX, v.x, v.y, v.z, v.w, 0,0,0,0 ); v = q[1]; c.YmX.v[4]=v.x; c.YmX.v[5]=v.y; c.YmX.v[6]=v.z; c.YmX.v[7]=v.w;
-  v = q[2]; fe_set( c.YpX, v.x, v.y, v.z, v.w, 0,0,0,0 ); v = q[3]; c.YpX.v[4]=v.x; c.YpX.v[5]=v.y; c.YpX.v[6]=v.z; c.YpX.v[7]=v.w;
-  v = q[4]; fe_set( c.T2d, v.x, v.y, v.z, v.w, 0,0,0,0 ); v = q[5]; c.T2d.v[4]=v.x; c.T2d.v[5]=v.y; c.T2d.v[6]=v.z; c.T2d.v[7]=v.w;
-  v = q[6]; fe_set( c.Z2,  v.x, v.y, v.z, v.w, 0,0,0,0 ); v = q[7]; c.Z2.v[4]=v.x;  c.Z2.v[5]=v.y;  c.Z2.v[6]=v.z;  c.Z2.v[7]=v.w;
+  u32 w[36];
+  #pragma unroll
+  for( int k=0; k<9; k++ ) { uint4 v = q[k]; w[4*k] = v.x; w[4*k+1] = v.y; w[4*k+2] = v.z; w[4*k+3] = v.w; }
+  #pragma unroll
+  for( int i=0; i<9; i++ ) { c.YmX.v[i] = w[i]; c.YpX.v[i] = w[9+i]; c.T2d.v[i] = w[18+i]; c.Z2.v[i] = w[27+i]; }
+}
+/* one 1/2-scaled affine B-table entry from LDS (7 x ds_read_b128) */
+DEV void load_affc( ge_affc & b, u32 const * bt ) {
+  uint4 const * q = (uint4 const *)bt;
+  u32 w[28];
+  #pragma unroll
+  for( int k=0; k<7; k++ ) { uint4 v = q[k]; w[4*k] = v.x; w[4*k+1] = v.y; w[4*k+2] = v.z; w[4*k+3] = v.w; }
+  #pragma unroll
+  for( int i=0; i<9; i++ ) { b.YmX.v[i] = w[i]; b.YpX.v[i] = w[9+i]; b.T2d.v[i] = w[18+i]; }
 }
 
 /* shift a packed 256-bit digit vector left by `bits` (4 or 8) */
@@ -271,21 +291,23 @@ void k_verify_dsm( ulong chunk, u32 const * __restrict__ st, u32 const * __restr
     {
       ge_p3 Q;
       fe ax;
+      u32 aw[8], yw[8];
       #pragma unroll
-      for( int w=0; w<8; w++ ) { ax.v[w] = s[(ST_AX+w)*chunk]; Q.Y.v[w] = s[(ST_AY+w)*chunk]; }
-      fe_neg( Q.X, ax ); fe_1( Q.Z ); fe_mul( Q.T, Q.X, Q.Y );
+      for( int w=0; w<8; w++ ) { aw[w] = s[(ST_AX+w)*chunk]; yw[w] = s[(ST_AY+w)*chunk]; }
+      fe_from_words( ax, aw ); fe_from_words( Q.Y, yw );
+      fe_neg( Q.X, ax ); fe_norm( Q.X, Q.X ); fe_1( Q.Z ); fe_mul( Q.T, Q.X, Q.Y );
       ge_cached c;
-      fe_1( c.YmX ); fe_1( c.YpX ); fe_0( c.T2d ); fe_set( c.Z2, 2,0,0,0,0,0,0,0 );
-      store_cached( tab + 0*32, c );                                  /* identity */
-      ge_cached c1; ge_to_cached( c1, Q ); store_cached( tab + 1*32, c1 );
+      fe_1( c.YmX ); fe_1( c.YpX ); fe_0( c.T2d ); fe_set( c.Z2, 2,0,0,0,0,0,0,0,0 );
+      store_cached( tab + 0*ATAB_ENT, c );                                  /* identity */
+      ge_cached c1; ge_to_cached( c1, Q ); store_cached( tab + 1*ATAB_ENT, c1 );
       ge_p3 P2, P3, P4, P5, P6, P7, P8;
-      ge_dbl( P2, Q, true );            ge_to_cached( c, P2 ); store_cached( tab + 2*32, c );
-      ge_add_cached( P3, P2, c1, 0u, true ); ge_to_cached( c, P3 ); store_cached( tab + 3*32, c );
-      ge_dbl( P4, P2, true );           ge_to_cached( c, P4 ); store_cached( tab + 4*32, c );
-      ge_add_cached( P5, P4, c1, 0u, true ); ge_to_cached( c, P5 ); store_cached( tab + 5*32, c );
-      ge_dbl( P6, P3, true );           ge_to_cached( c, P6 ); store_cached( tab + 6*32, c );
-      ge_add_cached( P7, P6, c1, 0u, true ); ge_to_cached( c, P7 ); store_cached( tab + 7*32, c );
-      ge_dbl( P8, P4, true );           ge_to_cached( c, P8 ); store_cached( tab + 8*32, c );
+      ge_dbl( P2, Q, true );            ge_to_cached( c, P2 ); store_cached( tab + 2*ATAB_ENT, c );
+      ge_add_cached( P3, P2, c1, 0u, true ); ge_to_cached( c, P3 ); store_cached( tab + 3*ATAB_ENT, c );
+      ge_dbl( P4, P2, true );           ge_to_cached( c, P4 ); store_cached( tab + 4*ATAB_ENT, c );
+      ge_add_cached( P5, P4, c1, 0u, true ); ge_to_cached( c, P5 ); store_cached( tab + 5*ATAB_ENT, c );
+      ge_dbl( P6, P3, true );           ge_to_cached( c, P6 ); store_cached( tab + 6*ATAB_ENT, c );
+      ge_add_cached( P7, P6, c1, 0u, true ); ge_to_cached( c, P7 ); store_cached( tab + 7*ATAB_ENT, c );
+      ge_dbl( P8, P4, true );           ge_to_cached( c, P8 ); store_cached( tab + 8*ATAB_ENT, c );
     }
 
     /* ---- [k]Q + [S]B (user.c:217; fd_curve25519.c:121-165) ---- */
@@ -296,7 +318,7 @@ void k_verify_dsm( ulong chunk, u32 const * __restrict__ st, u32 const * __restr
       int sa = (int)da - 8;
       u32 nega = sa < 0 ? ~0u : 0u;
       u32 ia = (u32)(sa < 0 ? -sa : sa);
-      ge_cached e; load_cached( e, tab + ia*32 );
+      ge_cached e; load_cached( e, tab + ia*ATAB_ENT );
       if( w != 63 ) {
         #pragma unroll 1
         for( int j=0; j<3; j++ ) ge_dbl( P, P, false );
@@ -309,18 +331,17 @@ void k_verify_dsm( ulong chunk, u32 const * __restrict__ st, u32 const * __restr
         int sb = (int)db - 128;
         u32 negb = sb < 0 ? ~0u : 0u;
         u32 ib = (u32)(sb < 0 ? -sb : sb);
-        ge_affc b;
-        u32 const * bt = lds_btab + ib*24;
-        #pragma unroll
-        for( int q=0; q<8; q++ ) { b.YmX.v[q] = bt[q]; b.YpX.v[q] = bt[8+q]; b.T2d.v[q] = bt[16+q]; }
+        ge_affc b; load_affc( b, lds_btab + ib*BTAB_STRIDE );
         ge_add_affc( P, P, b, negb, false );
       }
     }
 
     /* ---- projective compare with R (user.c:226; fd_r43x6_ge.h:52-82) ---- */
     fe rx, ry, t, cx, cy;
+    u32 rxw[8], ryw[8];
     #pragma unroll
-    for( int w=0; w<8; w++ ) { rx.v[w] = s[(ST_RX+w)*chunk]; ry.v[w] = s[(ST_RY+w)*chunk]; }
+    for( int w=0; w<8; w++ ) { rxw[w] = s[(ST_RX+w)*chunk]; ryw[w] = s[(ST_RY+w)*chunk]; }
+    fe_from_words( rx, rxw ); fe_from_words( ry, ryw );
     fe_mul( t, rx, P.Z ); fe_canon( t, t ); fe_canon( cx, P.X );
     bool ex = fe_eq_c( t, cx );
     fe_mul( t, ry, P.Z ); fe_canon( t, t ); fe_canon( cy, P.Y );
@@ -365,10 +386,7 @@ DEV void ge_scalarmult_base( ge_p3 & P, u32 const s[8], u32 const * lds_btab ) {
     int sb = (int)db - 128;
     u32 negb = sb < 0 ? ~0u : 0u;
     u32 ib = (u32)(sb < 0 ? -sb : sb);
-    ge_affc b;
-    u32 const * bt = lds_btab + ib*24;
-    #pragma unroll
-    for( int q=0; q<8; q++ ) { b.YmX.v[q] = bt[q]; b.YpX.v[q] = bt[8+q]; b.T2d.v[q] = bt[16+q]; }
+    ge_affc b; load_affc( b, lds_btab + ib*BTAB_STRIDE );
     ge_add_affc( P, P, b, negb, true );
   }
 }
@@ -378,8 +396,7 @@ DEV void ge_encode( u32 out[8], ge_p3 const & P ) {
   fe zi, x, y;
   fe_invert( zi, P.Z ); fe_mul( x, P.X, zi ); fe_mul( y, P.Y, zi );
   fe_canon( x, x ); fe_canon( y, y );
-  #pragma unroll
-  for( int i=0; i<8; i++ ) out[i] = y.v[i];
+  fe_to_words( out, y );
   out[7] |= (x.v[0] & 1u) << 31;
 }
 

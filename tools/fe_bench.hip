@@ -8,7 +8,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <vector>
-#include "../firedancer_amd/csrc/fe25519_asm.h"
+#include "fe25519_asm.h"
 
 #define CHK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { fprintf(stderr, "%s:%d %s\n", __FILE__, __LINE__, hipGetErrorString(e_)); exit(1); } } while (0)
 
