@@ -61,31 +61,40 @@ DEV void fe_d2( fe & r )     { fe_set( r, 0x06b2f159u,0x1eb4dca1u,0x00ec55bau,0x
 DEV void fe_sqrtm1( fe & r ) { fe_set( r, 0x0a0ea0b0u,0x0770d93au,0x0bf91e31u,0x06300d5au,0x1d7a72f4u,0x004c9efdu,0x1c2cad34u,0x1009f83bu,0x002b8324u ); }
 DEV void fe_inv2( fe & r )   { fe_set( r, 0x1ffffff7u,0x1fffffffu,0x1fffffffu,0x1fffffffu,0x1fffffffu,0x1fffffffu,0x1fffffffu,0x1fffffffu,0x003fffffu ); }
 
-/* Column k of the product: sum over i+j=k, 0<=i,j<=8.  fe_mul computes the
-   high columns 9..16 first (normalised to 29-bit limbs z[0..7], z[8] = the
-   carry out of column 16), then the low columns 0..8 each led by
-   1216*z[k] (2^261 == 19*2^6 mod p), carrying 29 bits at a time; column 8
-   splits at bit 255 and its overflow folds back into limb 0 with 19. */
+/* 64-bit multiply-accumulate kept in program order: the empty asm makes
+   each partial sum opaque, so the compiler cannot re-associate a column into
+   two half-chains joined by v_lshl_add_u64 (one extra 64-bit op per column). */
+DEV u64 fe_mad64( u32 a, u32 b, u64 c ) { u64 r = c + (u64)a * b; asm( "" : "+v"(r) ); return r; }
+DEV u64 fe_mul64( u32 a, u32 b )        { u64 r = (u64)a * b;     asm( "" : "+v"(r) ); return r; }
+
+/* Column k of the product: sum over i+j=k, 0<=i,j<=8.  Two independent
+   carry chains run interleaved (back-to-back dependent v_mad_u64_u32 need a
+   wait state; two chains fill it):
+     H: high columns 9..16, normalised to 29-bit limbs z[0..7] (z[8] = the
+        carry out of column 16);
+     L: low columns 0..8, each = carry + its products + 1216*z[k]
+        (2^261 == 19*2^6 mod p), carrying 29 bits at a time.
+   Column 8 splits at bit 255 and its overflow folds into limb 0 with 19. */
 DEV void fe_mul( fe & r, fe const & a, fe const & b ) {
   u32 z[9], o[9];
-  u64 acc = 0;
-  #pragma unroll
-  for( int k=9; k<=16; k++ ) {
-    acc = (k == 9) ? 0ull : (acc >> 29);
-    #pragma unroll
-    for( int i=k-8; i<=8; i++ ) acc += (u64)a.v[i] * b.v[k-i];
-    z[k-9] = (u32)acc & FE_M29;
-  }
-  z[8] = (u32)(acc >> 29);
+  u64 h = 0, l = 0;
   #pragma unroll
   for( int k=0; k<=8; k++ ) {
-    acc = (k == 0 ? 0ull : (acc >> 29)) + (u64)z[k] * 1216u;
+    if( k < 8 ) {
+      int c = 9 + k;
+      #pragma unroll
+      for( int i=c-8; i<=8; i++ ) h = (k == 0 && i == 1) ? fe_mul64( a.v[i], b.v[c-i] ) : fe_mad64( a.v[i], b.v[c-i], h );
+      z[k] = (u32)h & FE_M29; h >>= 29;
+    } else {
+      z[8] = (u32)h;
+    }
     #pragma unroll
-    for( int i=0; i<=k; i++ ) acc += (u64)a.v[i] * b.v[k-i];
-    if( k < 8 ) o[k] = (u32)acc & FE_M29;
+    for( int i=0; i<=k; i++ ) l = (k == 0) ? fe_mul64( a.v[0], b.v[0] ) : fe_mad64( a.v[i], b.v[k-i], l );
+    l = fe_mad64( z[k], 1216u, l );
+    if( k < 8 ) { o[k] = (u32)l & FE_M29; l >>= 29; }
   }
-  o[8] = (u32)acc & FE_M23;
-  u64 t = (acc >> 23) * 19u + o[0];
+  o[8] = (u32)l & FE_M23;
+  u64 t = (l >> 23) * 19u + o[0];
   o[0] = (u32)t & FE_M29;
   o[1] += (u32)(t >> 29);
   #pragma unroll
@@ -98,30 +107,110 @@ DEV void fe_sq( fe & r, fe const & a ) {
   u32 d[9], z[9], o[9];
   #pragma unroll
   for( int i=0; i<9; i++ ) d[i] = a.v[i] << 1;
-  u64 acc = 0;
-  #pragma unroll
-  for( int k=9; k<=16; k++ ) {
-    acc = (k == 9) ? 0ull : (acc >> 29);
-    #pragma unroll
-    for( int i=k-8; 2*i<k; i++ ) acc += (u64)d[i] * a.v[k-i];
-    if( (k & 1) == 0 ) acc += (u64)a.v[k/2] * a.v[k/2];
-    z[k-9] = (u32)acc & FE_M29;
-  }
-  z[8] = (u32)(acc >> 29);
+  u64 h = 0, l = 0;
   #pragma unroll
   for( int k=0; k<=8; k++ ) {
-    acc = (k == 0 ? 0ull : (acc >> 29)) + (u64)z[k] * 1216u;
+    if( k < 8 ) {
+      int c = 9 + k;
+      bool first = (k == 0);
+      #pragma unroll
+      for( int i=c-8; 2*i<c; i++ ) { h = first ? fe_mul64( d[i], a.v[c-i] ) : fe_mad64( d[i], a.v[c-i], h ); first = false; }
+      if( (c & 1) == 0 ) h = fe_mad64( a.v[c/2], a.v[c/2], h );
+      z[k] = (u32)h & FE_M29; h >>= 29;
+    } else {
+      z[8] = (u32)h;
+    }
     #pragma unroll
-    for( int i=0; 2*i<k; i++ ) acc += (u64)d[i] * a.v[k-i];
-    if( (k & 1) == 0 ) acc += (u64)a.v[k/2] * a.v[k/2];
-    if( k < 8 ) o[k] = (u32)acc & FE_M29;
+    for( int i=0; 2*i<k; i++ ) l = fe_mad64( d[i], a.v[k-i], l );
+    if( (k & 1) == 0 ) l = (k == 0) ? fe_mul64( a.v[0], a.v[0] ) : fe_mad64( a.v[k/2], a.v[k/2], l );
+    l = fe_mad64( z[k], 1216u, l );
+    if( k < 8 ) { o[k] = (u32)l & FE_M29; l >>= 29; }
   }
-  o[8] = (u32)acc & FE_M23;
-  u64 t = (acc >> 23) * 19u + o[0];
+  o[8] = (u32)l & FE_M23;
+  u64 t = (l >> 23) * 19u + o[0];
   o[0] = (u32)t & FE_M29;
   o[1] += (u32)(t >> 29);
   #pragma unroll
   for( int i=0; i<9; i++ ) r.v[i] = o[i];
+  FE_SCHED_FENCE();
+}
+
+/* Two independent products interleaved (four carry chains: no two
+   consecutive multiply-adds depend on each other, so no wait states).  Used
+   wherever a formula has two independent multiplies. */
+DEV void fe_fin2( fe & r, u32 o[9], u64 l ) {   /* column-8 split + fold, output copy */
+  o[8] = (u32)l & FE_M23;
+  u64 t = (l >> 23) * 19u + o[0];
+  o[0] = (u32)t & FE_M29;
+  o[1] += (u32)(t >> 29);
+  #pragma unroll
+  for( int i=0; i<9; i++ ) r.v[i] = o[i];
+}
+
+DEV void fe_mul2( fe & r, fe const & a, fe const & b, fe & s, fe const & c, fe const & d ) {
+  u32 z[9], o[9], y[9], p[9];
+  u64 h1 = 0, l1 = 0, h2 = 0, l2 = 0;
+  #pragma unroll
+  for( int k=0; k<=8; k++ ) {
+    if( k < 8 ) {
+      int cc = 9 + k;
+      #pragma unroll
+      for( int i=cc-8; i<=8; i++ ) {
+        bool f = (k == 0 && i == 1);
+        h1 = f ? fe_mul64( a.v[i], b.v[cc-i] ) : fe_mad64( a.v[i], b.v[cc-i], h1 );
+        h2 = f ? fe_mul64( c.v[i], d.v[cc-i] ) : fe_mad64( c.v[i], d.v[cc-i], h2 );
+      }
+      z[k] = (u32)h1 & FE_M29; h1 >>= 29;
+      y[k] = (u32)h2 & FE_M29; h2 >>= 29;
+    } else {
+      z[8] = (u32)h1; y[8] = (u32)h2;
+    }
+    #pragma unroll
+    for( int i=0; i<=k; i++ ) {
+      l1 = (k == 0) ? fe_mul64( a.v[0], b.v[0] ) : fe_mad64( a.v[i], b.v[k-i], l1 );
+      l2 = (k == 0) ? fe_mul64( c.v[0], d.v[0] ) : fe_mad64( c.v[i], d.v[k-i], l2 );
+    }
+    l1 = fe_mad64( z[k], 1216u, l1 );
+    l2 = fe_mad64( y[k], 1216u, l2 );
+    if( k < 8 ) { o[k] = (u32)l1 & FE_M29; l1 >>= 29; p[k] = (u32)l2 & FE_M29; l2 >>= 29; }
+  }
+  fe_fin2( r, o, l1 ); fe_fin2( s, p, l2 );
+  FE_SCHED_FENCE();
+}
+
+DEV void fe_sq2( fe & r, fe const & a, fe & s, fe const & c ) {
+  u32 da[9], dc[9], z[9], o[9], y[9], p[9];
+  #pragma unroll
+  for( int i=0; i<9; i++ ) { da[i] = a.v[i] << 1; dc[i] = c.v[i] << 1; }
+  u64 h1 = 0, l1 = 0, h2 = 0, l2 = 0;
+  #pragma unroll
+  for( int k=0; k<=8; k++ ) {
+    if( k < 8 ) {
+      int cc = 9 + k;
+      bool first = (k == 0);
+      #pragma unroll
+      for( int i=cc-8; 2*i<cc; i++ ) {
+        h1 = first ? fe_mul64( da[i], a.v[cc-i] ) : fe_mad64( da[i], a.v[cc-i], h1 );
+        h2 = first ? fe_mul64( dc[i], c.v[cc-i] ) : fe_mad64( dc[i], c.v[cc-i], h2 );
+        first = false;
+      }
+      if( (cc & 1) == 0 ) { h1 = fe_mad64( a.v[cc/2], a.v[cc/2], h1 ); h2 = fe_mad64( c.v[cc/2], c.v[cc/2], h2 ); }
+      z[k] = (u32)h1 & FE_M29; h1 >>= 29;
+      y[k] = (u32)h2 & FE_M29; h2 >>= 29;
+    } else {
+      z[8] = (u32)h1; y[8] = (u32)h2;
+    }
+    #pragma unroll
+    for( int i=0; 2*i<k; i++ ) { l1 = fe_mad64( da[i], a.v[k-i], l1 ); l2 = fe_mad64( dc[i], c.v[k-i], l2 ); }
+    if( (k & 1) == 0 ) {
+      l1 = (k == 0) ? fe_mul64( a.v[0], a.v[0] ) : fe_mad64( a.v[k/2], a.v[k/2], l1 );
+      l2 = (k == 0) ? fe_mul64( c.v[0], c.v[0] ) : fe_mad64( c.v[k/2], c.v[k/2], l2 );
+    }
+    l1 = fe_mad64( z[k], 1216u, l1 );
+    l2 = fe_mad64( y[k], 1216u, l2 );
+    if( k < 8 ) { o[k] = (u32)l1 & FE_M29; l1 >>= 29; p[k] = (u32)l2 & FE_M29; l2 >>= 29; }
+  }
+  fe_fin2( r, o, l1 ); fe_fin2( s, p, l2 );
   FE_SCHED_FENCE();
 }
 
@@ -259,7 +348,7 @@ DEV void ge_identity( ge_p3 & r ) { fe_0( r.X ); fe_1( r.Y ); fe_1( r.Z ); fe_0(
 DEV void ge_dbl( ge_p3 & r, ge_p3 const & p, bool needT ) {
   fe A, B, C, S, H, G, F, E;
   fe_add( S, p.X, p.Y );
-  fe_sq( A, p.X ); fe_sq( B, p.Y ); fe_sq( C, p.Z ); fe_sq( S, S );
+  fe_sq2( A, p.X, B, p.Y ); fe_sq2( C, p.Z, S, S );
   fe_add( C, C, C );          /* 2Z^2            */
   fe_add( H, A, B );          /* A+B             */
   fe_sub( G, A, B );          /* A-B             */
@@ -267,10 +356,9 @@ DEV void ge_dbl( ge_p3 & r, ge_p3 const & p, bool needT ) {
   fe_norm( F, F );
   fe_sub( E, H, S );          /* A+B-(X+Y)^2     */
   if( needT ) fe_norm( E, E );
-  fe_mul( r.X, E, F );
-  fe_mul( r.Y, G, H );
-  fe_mul( r.Z, F, G );
-  if( needT ) fe_mul( r.T, E, H );
+  fe_mul2( r.X, E, F, r.Y, G, H );
+  if( needT ) fe_mul2( r.Z, F, G, r.T, E, H );
+  else        fe_mul( r.Z, F, G );
 }
 
 /* r = p +/- q (q in cached form).  neg is a per-lane mask (0 or ~0). */
@@ -278,13 +366,14 @@ DEV void ge_add_cached( ge_p3 & r, ge_p3 const & p, ge_cached q, u32 neg, bool n
   fe a, b, A, B, C, D, E, F, G, H;
   fe_cswap( q.YmX, q.YpX, neg );           /* -q: swap Y-X / Y+X ... */
   fe_sub( a, p.Y, p.X ); fe_add( b, p.Y, p.X );
-  fe_mul( A, a, q.YmX ); fe_mul( B, b, q.YpX );
-  fe_mul( C, p.T, q.T2d ); fe_mul( D, p.Z, q.Z2 );
+  fe_mul2( A, a, q.YmX, B, b, q.YpX );
+  fe_mul2( C, p.T, q.T2d, D, p.Z, q.Z2 );
   fe_sub( E, B, A ); fe_norm( E, E ); fe_add( H, B, A );
   fe_sub( F, D, C ); fe_add( G, D, C );
   fe_cswap( F, G, neg );                   /* ... and negate 2dT: C -> -C swaps F and G */
-  fe_mul( r.X, E, F ); fe_mul( r.Y, G, H ); fe_mul( r.Z, F, G );
-  if( needT ) fe_mul( r.T, E, H );
+  fe_mul2( r.X, E, F, r.Y, G, H );
+  if( needT ) fe_mul2( r.Z, F, G, r.T, E, H );
+  else        fe_mul( r.Z, F, G );
 }
 
 /* r = p +/- q with q an affine cached point scaled by 1/2 (D = Z1) */
@@ -292,13 +381,14 @@ DEV void ge_add_affc( ge_p3 & r, ge_p3 const & p, ge_affc q, u32 neg, bool needT
   fe a, b, A, B, C, E, F, G, H;
   fe_cswap( q.YmX, q.YpX, neg );
   fe_sub( a, p.Y, p.X ); fe_add( b, p.Y, p.X );
-  fe_mul( A, a, q.YmX ); fe_mul( B, b, q.YpX );
+  fe_mul2( A, a, q.YmX, B, b, q.YpX );
   fe_mul( C, p.T, q.T2d );
   fe_sub( E, B, A ); fe_norm( E, E ); fe_add( H, B, A );
   fe_sub( F, p.Z, C ); fe_add( G, p.Z, C );
   fe_cswap( F, G, neg );
-  fe_mul( r.X, E, F ); fe_mul( r.Y, G, H ); fe_mul( r.Z, F, G );
-  if( needT ) fe_mul( r.T, E, H );
+  fe_mul2( r.X, E, F, r.Y, G, H );
+  if( needT ) fe_mul2( r.Z, F, G, r.T, E, H );
+  else        fe_mul( r.Z, F, G );
 }
 
 /* fd_curve25519_into_precomputed (ref/fd_curve25519.h:141-151) with Z doubled */

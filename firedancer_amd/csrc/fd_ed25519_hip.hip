@@ -117,7 +117,7 @@ DEV void ge_to_affc_half( ge_affc & a, ge_p3 const & p ) {
 /* j*B for j in [0,128] in affine cached form (the reference's verify uses a
    128-entry odd-multiple B table, fd_curve25519_table_ref.c:32; ours holds
    all multiples 0..128 for signed radix-256 windows). */
-__global__ void k_btab_init( u32 * btab ) {
+__global__ __launch_bounds__(64) void k_btab_init( u32 * btab ) {
   int j = blockIdx.x * blockDim.x + threadIdx.x;
   if( j >= BTAB_N ) return;
   ge_p3 B, P; ge_base( B ); ge_identity( P );
@@ -300,14 +300,13 @@ void k_verify_dsm( ulong chunk, u32 const * __restrict__ st, u32 const * __restr
       fe_1( c.YmX ); fe_1( c.YpX ); fe_0( c.T2d ); fe_set( c.Z2, 2,0,0,0,0,0,0,0,0 );
       store_cached( tab + 0*ATAB_ENT, c );                                  /* identity */
       ge_cached c1; ge_to_cached( c1, Q ); store_cached( tab + 1*ATAB_ENT, c1 );
-      ge_p3 P2, P3, P4, P5, P6, P7, P8;
-      ge_dbl( P2, Q, true );            ge_to_cached( c, P2 ); store_cached( tab + 2*ATAB_ENT, c );
-      ge_add_cached( P3, P2, c1, 0u, true ); ge_to_cached( c, P3 ); store_cached( tab + 3*ATAB_ENT, c );
-      ge_dbl( P4, P2, true );           ge_to_cached( c, P4 ); store_cached( tab + 4*ATAB_ENT, c );
-      ge_add_cached( P5, P4, c1, 0u, true ); ge_to_cached( c, P5 ); store_cached( tab + 5*ATAB_ENT, c );
-      ge_dbl( P6, P3, true );           ge_to_cached( c, P6 ); store_cached( tab + 6*ATAB_ENT, c );
-      ge_add_cached( P7, P6, c1, 0u, true ); ge_to_cached( c, P7 ); store_cached( tab + 7*ATAB_ENT, c );
-      ge_dbl( P8, P4, true );           ge_to_cached( c, P8 ); store_cached( tab + 8*ATAB_ENT, c );
+      /* 2Q, then (j+1)Q = jQ + Q: a chain keeps one point and c1 live */
+      ge_p3 Pj;
+      ge_dbl( Pj, Q, true ); ge_to_cached( c, Pj ); store_cached( tab + 2*ATAB_ENT, c );
+      #pragma unroll 1
+      for( int j=3; j<=8; j++ ) {
+        ge_add_cached( Pj, Pj, c1, 0u, true ); ge_to_cached( c, Pj ); store_cached( tab + j*ATAB_ENT, c );
+      }
     }
 
     /* ---- [k]Q + [S]B (user.c:217; fd_curve25519.c:121-165) ---- */

@@ -74,18 +74,136 @@ DEV void f29_sq(u32 r[9], const u32 a[9]) {
   for (int i = 0; i < 9; i++) r[i] = o[i];
 }
 
+
+DEV u64 mad64(u32 a, u32 b, u64 c) {
+  u64 r = c + (u64)a * b; asm("" : "+v"(r)); return r;
+}
+DEV u64 mul64(u32 a, u32 b) {
+  u64 r = (u64)a * b; asm("" : "+v"(r)); return r;
+}
+// serial column chains: every product of a column accumulates into one chain
+DEV void f29s_mul(u32 r[9], const u32 a[9], const u32 b[9]) {
+  u32 o[9], z[9]; u64 acc = 0;
+#pragma unroll
+  for (int k = 9; k <= 16; k++) {
+#pragma unroll
+    for (int i = k - 8; i <= 8; i++) acc = (k == 9 && i == 1) ? mul64(a[i], b[k - i]) : mad64(a[i], b[k - i], acc);
+    z[k - 9] = (u32)acc & M29; acc >>= 29;
+  }
+  z[8] = (u32)acc;
+#pragma unroll
+  for (int k = 0; k <= 8; k++) {
+    acc = (k == 0) ? mul64(z[k], 1216u) : mad64(z[k], 1216u, acc);
+#pragma unroll
+    for (int i = 0; i <= k; i++) acc = mad64(a[i], b[k - i], acc);
+    if (k < 8) { o[k] = (u32)acc & M29; acc >>= 29; }
+  }
+  o[8] = (u32)acc & M23;
+  u64 t = mad64((u32)(acc >> 23), 19u, (u64)o[0]);
+  t += (u64)((u32)(acc >> 55) * 19u) << 32;
+  o[0] = (u32)t & M29;
+  o[1] += (u32)(t >> 29);
+#pragma unroll
+  for (int i = 0; i < 9; i++) r[i] = o[i];
+}
+DEV void f29s_sq(u32 r[9], const u32 a[9]) {
+  u32 d[9], o[9], z[9]; u64 acc = 0;
+#pragma unroll
+  for (int i = 0; i < 9; i++) d[i] = a[i] << 1;
+#pragma unroll
+  for (int k = 9; k <= 16; k++) {
+    bool first = (k == 9);
+#pragma unroll
+    for (int i = k - 8; 2 * i < k; i++) { acc = first ? mul64(d[i], a[k - i]) : mad64(d[i], a[k - i], acc); first = false; }
+    if ((k & 1) == 0) acc = mad64(a[k / 2], a[k / 2], acc);
+    z[k - 9] = (u32)acc & M29; acc >>= 29;
+  }
+  z[8] = (u32)acc;
+#pragma unroll
+  for (int k = 0; k <= 8; k++) {
+    acc = (k == 0) ? mul64(z[k], 1216u) : mad64(z[k], 1216u, acc);
+#pragma unroll
+    for (int i = 0; 2 * i < k; i++) acc = mad64(d[i], a[k - i], acc);
+    if ((k & 1) == 0) acc = mad64(a[k / 2], a[k / 2], acc);
+    if (k < 8) { o[k] = (u32)acc & M29; acc >>= 29; }
+  }
+  o[8] = (u32)acc & M23;
+  u64 t = mad64((u32)(acc >> 23), 19u, (u64)o[0]);
+  t += (u64)((u32)(acc >> 55) * 19u) << 32;
+  o[0] = (u32)t & M29;
+  o[1] += (u32)(t >> 29);
+#pragma unroll
+  for (int i = 0; i < 9; i++) r[i] = o[i];
+}
+
+
+// two independent serial chains interleaved: high column 9+k next to low
+// column k (products first, then the 1216*z_k fold)
+DEV void f29p_mul(u32 r[9], const u32 a[9], const u32 b[9]) {
+  u32 o[9], z[9]; u64 h = 0, l = 0;
+#pragma unroll
+  for (int k = 0; k <= 8; k++) {
+    if (k < 8) {
+      int c = 9 + k;
+#pragma unroll
+      for (int i = c - 8; i <= 8; i++) h = (k == 0 && i == 1) ? mul64(a[i], b[c - i]) : mad64(a[i], b[c - i], h);
+      z[k] = (u32)h & M29; h >>= 29;
+    } else z[8] = (u32)h;
+#pragma unroll
+    for (int i = 0; i <= k; i++) l = (k == 0) ? mul64(a[0], b[0]) : mad64(a[i], b[k - i], l);
+    l = mad64(z[k], 1216u, l);
+    if (k < 8) { o[k] = (u32)l & M29; l >>= 29; }
+  }
+  o[8] = (u32)l & M23;
+  u64 t = (l >> 23) * 19u + o[0];
+  o[0] = (u32)t & M29;
+  o[1] += (u32)(t >> 29);
+#pragma unroll
+  for (int i = 0; i < 9; i++) r[i] = o[i];
+}
+DEV void f29p_sq(u32 r[9], const u32 a[9]) {
+  u32 d[9], o[9], z[9]; u64 h = 0, l = 0;
+#pragma unroll
+  for (int i = 0; i < 9; i++) d[i] = a[i] << 1;
+#pragma unroll
+  for (int k = 0; k <= 8; k++) {
+    if (k < 8) {
+      int c = 9 + k; bool first = (k == 0);
+#pragma unroll
+      for (int i = c - 8; 2 * i < c; i++) { h = first ? mul64(d[i], a[c - i]) : mad64(d[i], a[c - i], h); first = false; }
+      if ((c & 1) == 0) h = mad64(a[c / 2], a[c / 2], h);
+      z[k] = (u32)h & M29; h >>= 29;
+    } else z[8] = (u32)h;
+    bool first = (k == 0);
+#pragma unroll
+    for (int i = 0; 2 * i < k; i++) { l = mad64(d[i], a[k - i], l); }
+    if ((k & 1) == 0) l = first ? mul64(a[0], a[0]) : mad64(a[k / 2], a[k / 2], l);
+    l = mad64(z[k], 1216u, l);
+    if (k < 8) { o[k] = (u32)l & M29; l >>= 29; }
+  }
+  o[8] = (u32)l & M23;
+  u64 t = (l >> 23) * 19u + o[0];
+  o[0] = (u32)t & M29;
+  o[1] += (u32)(t >> 29);
+#pragma unroll
+  for (int i = 0; i < 9; i++) r[i] = o[i];
+}
+
+template <bool SER>
 __global__ void k_dump(const uint32_t* in, uint32_t* out, int n) {
   int t = blockIdx.x * blockDim.x + threadIdx.x;
   if (t >= n) return;
   u32 a[9], b[9], r[9];
   for (int i = 0; i < 9; ++i) { a[i] = in[t * 18 + i]; b[i] = in[t * 18 + 9 + i]; }
-  f29_mul(r, a, b); for (int i = 0; i < 9; ++i) out[t * 36 + i] = r[i];
-  f29_sq(r, a);     for (int i = 0; i < 9; ++i) out[t * 36 + 9 + i] = r[i];
+  if (SER) f29p_mul(r, a, b); else f29_mul(r, a, b);
+  for (int i = 0; i < 9; ++i) out[t * 36 + i] = r[i];
+  if (SER) f29p_sq(r, a); else f29_sq(r, a);
+  for (int i = 0; i < 9; ++i) out[t * 36 + 9 + i] = r[i];
   u32 x[9]; for (int i = 0; i < 9; ++i) x[i] = r[i];
-  for (int k = 0; k < 100; ++k) f29_mul(x, x, b);
+  for (int k = 0; k < 100; ++k) { if (SER) f29p_mul(x, x, b); else f29_mul(x, x, b); }
   for (int i = 0; i < 9; ++i) out[t * 36 + 18 + i] = x[i];
   for (int i = 0; i < 9; ++i) x[i] = a[i];
-  for (int k = 0; k < 100; ++k) f29_sq(x, x);
+  for (int k = 0; k < 100; ++k) { if (SER) f29p_sq(x, x); else f29_sq(x, x); }
   for (int i = 0; i < 9; ++i) out[t * 36 + 27 + i] = x[i];
 }
 
@@ -98,6 +216,10 @@ __global__ __launch_bounds__(256) void k_bench(uint32_t* out, int iters, uint32_
     if (KIND == 0) { fe_mul(x, x, y); if (CHAINS > 1) fe_mul(z, z, y); }
     if (KIND == 1) { f29_mul(x, x, y); if (CHAINS > 1) f29_mul(z, z, y); }
     if (KIND == 2) { f29_sq(x, x); if (CHAINS > 1) f29_sq(z, z); }
+    if (KIND == 3) { f29s_mul(x, x, y); if (CHAINS > 1) f29s_mul(z, z, y); }
+    if (KIND == 4) { f29s_sq(x, x); if (CHAINS > 1) f29s_sq(z, z); }
+    if (KIND == 5) { f29p_mul(x, x, y); if (CHAINS > 1) f29p_mul(z, z, y); }
+    if (KIND == 6) { f29p_sq(x, x); if (CHAINS > 1) f29p_sq(z, z); }
   }
   uint32_t s = 0; for (int i = 0; i < 9; ++i) s ^= x[i] ^ z[i];
   out[blockIdx.x * 256 + threadIdx.x] = s;
@@ -127,7 +249,8 @@ int main(int argc, char** argv) {
     FILE* f = fopen(argv[3], "rb"); if (!f) return 1; if (fread(in.data(), 4, n * 18, f) != (size_t)n * 18) return 1; fclose(f);
     uint32_t *din, *dout; CHK(hipMalloc(&din, n * 72)); CHK(hipMalloc(&dout, n * 144));
     CHK(hipMemcpy(din, in.data(), n * 72, hipMemcpyHostToDevice));
-    hipLaunchKernelGGL(k_dump, dim3((n + 255) / 256), dim3(256), 0, 0, din, dout, n);
+    if (argc > 5) hipLaunchKernelGGL(k_dump<true>, dim3((n + 255) / 256), dim3(256), 0, 0, din, dout, n);
+    else hipLaunchKernelGGL(k_dump<false>, dim3((n + 255) / 256), dim3(256), 0, 0, din, dout, n);
     CHK(hipDeviceSynchronize());
     std::vector<uint32_t> out(n * 36);
     CHK(hipMemcpy(out.data(), dout, n * 144, hipMemcpyDeviceToHost));
@@ -139,11 +262,17 @@ int main(int argc, char** argv) {
   int cus = p.multiProcessorCount;
   uint32_t* out; CHK(hipMalloc(&out, (size_t)cus * 8 * 256 * 4));
   hipEvent_t e0, e1; CHK(hipEventCreate(&e0)); CHK(hipEventCreate(&e1));
-  run<0, 1>(cus, out, e0, e1, "asm32_mul");
-  run<0, 2>(cus, out, e0, e1, "asm32_mul");
   run<1, 1>(cus, out, e0, e1, "f29_mul");
   run<1, 2>(cus, out, e0, e1, "f29_mul");
   run<2, 1>(cus, out, e0, e1, "f29_sq");
   run<2, 2>(cus, out, e0, e1, "f29_sq");
+  run<3, 1>(cus, out, e0, e1, "f29s_mul");
+  run<3, 2>(cus, out, e0, e1, "f29s_mul");
+  run<4, 1>(cus, out, e0, e1, "f29s_sq");
+  run<4, 2>(cus, out, e0, e1, "f29s_sq");
+  run<5, 1>(cus, out, e0, e1, "f29p_mul");
+  run<5, 2>(cus, out, e0, e1, "f29p_mul");
+  run<6, 1>(cus, out, e0, e1, "f29p_sq");
+  run<6, 2>(cus, out, e0, e1, "f29p_sq");
   return 0;
 }
