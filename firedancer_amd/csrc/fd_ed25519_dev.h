@@ -67,150 +67,133 @@ DEV void fe_inv2( fe & r )   { fe_set( r, 0x1ffffff7u,0x1fffffffu,0x1fffffffu,0x
 DEV u64 fe_mad64( u32 a, u32 b, u64 c ) { u64 r = c + (u64)a * b; asm( "" : "+v"(r) ); return r; }
 DEV u64 fe_mul64( u32 a, u32 b )        { u64 r = (u64)a * b;     asm( "" : "+v"(r) ); return r; }
 
-/* Column k of the product: sum over i+j=k, 0<=i,j<=8.  Two independent
-   carry chains run interleaved (back-to-back dependent v_mad_u64_u32 need a
-   wait state; two chains fill it):
-     H: high columns 9..16, normalised to 29-bit limbs z[0..7] (z[8] = the
-        carry out of column 16);
-     L: low columns 0..8, each = carry + its products + 1216*z[k]
-        (2^261 == 19*2^6 mod p), carrying 29 bits at a time.
-   Column 8 splits at bit 255 and its overflow folds into limb 0 with 19. */
-DEV void fe_mul( fe & r, fe const & a, fe const & b ) {
-  u32 z[9], o[9];
-  u64 h = 0, l = 0;
-  #pragma unroll
-  for( int k=0; k<=8; k++ ) {
-    if( k < 8 ) {
-      int c = 9 + k;
-      #pragma unroll
-      for( int i=c-8; i<=8; i++ ) h = (k == 0 && i == 1) ? fe_mul64( a.v[i], b.v[c-i] ) : fe_mad64( a.v[i], b.v[c-i], h );
-      z[k] = (u32)h & FE_M29; h >>= 29;
-    } else {
-      z[8] = (u32)h;
-    }
-    #pragma unroll
-    for( int i=0; i<=k; i++ ) l = (k == 0) ? fe_mul64( a.v[0], b.v[0] ) : fe_mad64( a.v[i], b.v[k-i], l );
-    l = fe_mad64( z[k], 1216u, l );
-    if( k < 8 ) { o[k] = (u32)l & FE_M29; l >>= 29; }
-  }
+/* Product columns (column k = sum over i+j=k, 0<=i,j<=8):
+     high column 9+j is kept as an unsplit 64-bit sum H_{9+j} (< 2^63): a
+       fresh, independent chain of 8-j multiply-adds;
+     low column j = carry + its products + 1216*lo32(H_{9+j})
+       + 9728*hi32(H_{8+j})  (2^261 == 19*2^6 == 1216 mod p, and the high
+       word of H_{8+j} sits 32 bits up = 3 bits into the next limb: 1216*8),
+       then split at 29 bits (v_and + v_lshrrev_b64).
+   H_{9+j} is computed interleaved with low column j (independent chains fill
+   each other's wait states), so only two H sums are live.  Column 8 splits
+   at bit 255 and its overflow folds into limb 0 with 19. */
+DEV void fe_fin( fe & r, u32 o[9], u64 l ) {   /* column-8 split + fold, output copy */
   o[8] = (u32)l & FE_M23;
   u64 t = (l >> 23) * 19u + o[0];
   o[0] = (u32)t & FE_M29;
   o[1] += (u32)(t >> 29);
   #pragma unroll
   for( int i=0; i<9; i++ ) r.v[i] = o[i];
+}
+
+DEV void fe_mul( fe & r, fe const & a, fe const & b ) {
+  u32 o[9];
+  u64 l = 0, hp = 0, h = 0;
+  #pragma unroll
+  for( int j=0; j<=8; j++ ) {
+    int c = 9 + j;
+    #pragma unroll
+    for( int i=0; i<=8; i++ ) {
+      if( j < 8 && i <= 7-j ) h = (i == 0) ? fe_mul64( a.v[c-8+i], b.v[8-i] ) : fe_mad64( a.v[c-8+i], b.v[8-i], h );
+      if( i <= j ) l = (j == 0) ? fe_mul64( a.v[0], b.v[0] ) : fe_mad64( a.v[i], b.v[j-i], l );
+    }
+    if( j < 8 ) l = fe_mad64( (u32)h, 1216u, l );
+    if( j > 0 ) l = fe_mad64( (u32)(hp >> 32), 9728u, l );
+    if( j < 8 ) { o[j] = (u32)l & FE_M29; l >>= 29; }
+    hp = h;
+  }
+  fe_fin( r, o, l );
   FE_SCHED_FENCE();
 }
 
 /* a^2: same columns, off-diagonal products taken once against 2*a_i */
 DEV void fe_sq( fe & r, fe const & a ) {
-  u32 d[9], z[9], o[9];
+  u32 d[9], o[9];
   #pragma unroll
   for( int i=0; i<9; i++ ) d[i] = a.v[i] << 1;
-  u64 h = 0, l = 0;
+  u64 l = 0, hp = 0, h = 0;
   #pragma unroll
-  for( int k=0; k<=8; k++ ) {
-    if( k < 8 ) {
-      int c = 9 + k;
-      bool first = (k == 0);
-      #pragma unroll
-      for( int i=c-8; 2*i<c; i++ ) { h = first ? fe_mul64( d[i], a.v[c-i] ) : fe_mad64( d[i], a.v[c-i], h ); first = false; }
-      if( (c & 1) == 0 ) h = fe_mad64( a.v[c/2], a.v[c/2], h );
-      z[k] = (u32)h & FE_M29; h >>= 29;
-    } else {
-      z[8] = (u32)h;
-    }
+  for( int j=0; j<=8; j++ ) {
+    int c = 9 + j;
     #pragma unroll
-    for( int i=0; 2*i<k; i++ ) l = fe_mad64( d[i], a.v[k-i], l );
-    if( (k & 1) == 0 ) l = (k == 0) ? fe_mul64( a.v[0], a.v[0] ) : fe_mad64( a.v[k/2], a.v[k/2], l );
-    l = fe_mad64( z[k], 1216u, l );
-    if( k < 8 ) { o[k] = (u32)l & FE_M29; l >>= 29; }
+    for( int i=0; i<=8; i++ ) {
+      int hi = c - 8 + i;                             /* high: d[hi]*a[c-hi], 2*hi < c */
+      if( j < 8 && 2*hi < c ) h = (i == 0) ? fe_mul64( d[hi], a.v[c-hi] ) : fe_mad64( d[hi], a.v[c-hi], h );
+      if( 2*i < j ) l = fe_mad64( d[i], a.v[j-i], l );                 /* j >= 1: onto the carry */
+    }
+    if( j < 8 && (c & 1) == 0 ) h = (c == 16) ? fe_mul64( a.v[8], a.v[8] ) : fe_mad64( a.v[c/2], a.v[c/2], h );
+    if( (j & 1) == 0 ) l = (j == 0) ? fe_mul64( a.v[0], a.v[0] ) : fe_mad64( a.v[j/2], a.v[j/2], l );
+    if( j < 8 ) l = fe_mad64( (u32)h, 1216u, l );
+    if( j > 0 ) l = fe_mad64( (u32)(hp >> 32), 9728u, l );
+    if( j < 8 ) { o[j] = (u32)l & FE_M29; l >>= 29; }
+    hp = h;
   }
-  o[8] = (u32)l & FE_M23;
-  u64 t = (l >> 23) * 19u + o[0];
-  o[0] = (u32)t & FE_M29;
-  o[1] += (u32)(t >> 29);
-  #pragma unroll
-  for( int i=0; i<9; i++ ) r.v[i] = o[i];
+  fe_fin( r, o, l );
   FE_SCHED_FENCE();
 }
 
-/* Two independent products interleaved (four carry chains: no two
-   consecutive multiply-adds depend on each other, so no wait states).  Used
-   wherever a formula has two independent multiplies. */
-DEV void fe_fin2( fe & r, u32 o[9], u64 l ) {   /* column-8 split + fold, output copy */
-  o[8] = (u32)l & FE_M23;
-  u64 t = (l >> 23) * 19u + o[0];
-  o[0] = (u32)t & FE_M29;
-  o[1] += (u32)(t >> 29);
-  #pragma unroll
-  for( int i=0; i<9; i++ ) r.v[i] = o[i];
-}
-
+/* Two independent products interleaved (four chains).  Used wherever a
+   formula has two independent multiplies. */
 DEV void fe_mul2( fe & r, fe const & a, fe const & b, fe & s, fe const & c, fe const & d ) {
-  u32 z[9], o[9], y[9], p[9];
-  u64 h1 = 0, l1 = 0, h2 = 0, l2 = 0;
+  u32 o[9], p[9];
+  u64 l1 = 0, hp1 = 0, h1 = 0, l2 = 0, hp2 = 0, h2 = 0;
   #pragma unroll
-  for( int k=0; k<=8; k++ ) {
-    if( k < 8 ) {
-      int cc = 9 + k;
-      #pragma unroll
-      for( int i=cc-8; i<=8; i++ ) {
-        bool f = (k == 0 && i == 1);
-        h1 = f ? fe_mul64( a.v[i], b.v[cc-i] ) : fe_mad64( a.v[i], b.v[cc-i], h1 );
-        h2 = f ? fe_mul64( c.v[i], d.v[cc-i] ) : fe_mad64( c.v[i], d.v[cc-i], h2 );
-      }
-      z[k] = (u32)h1 & FE_M29; h1 >>= 29;
-      y[k] = (u32)h2 & FE_M29; h2 >>= 29;
-    } else {
-      z[8] = (u32)h1; y[8] = (u32)h2;
-    }
+  for( int j=0; j<=8; j++ ) {
+    int cc = 9 + j;
     #pragma unroll
-    for( int i=0; i<=k; i++ ) {
-      l1 = (k == 0) ? fe_mul64( a.v[0], b.v[0] ) : fe_mad64( a.v[i], b.v[k-i], l1 );
-      l2 = (k == 0) ? fe_mul64( c.v[0], d.v[0] ) : fe_mad64( c.v[i], d.v[k-i], l2 );
+    for( int i=0; i<=8; i++ ) {
+      if( j < 8 && i <= 7-j ) {
+        h1 = (i == 0) ? fe_mul64( a.v[cc-8+i], b.v[8-i] ) : fe_mad64( a.v[cc-8+i], b.v[8-i], h1 );
+        h2 = (i == 0) ? fe_mul64( c.v[cc-8+i], d.v[8-i] ) : fe_mad64( c.v[cc-8+i], d.v[8-i], h2 );
+      }
+      if( i <= j ) {
+        l1 = (j == 0) ? fe_mul64( a.v[0], b.v[0] ) : fe_mad64( a.v[i], b.v[j-i], l1 );
+        l2 = (j == 0) ? fe_mul64( c.v[0], d.v[0] ) : fe_mad64( c.v[i], d.v[j-i], l2 );
+      }
     }
-    l1 = fe_mad64( z[k], 1216u, l1 );
-    l2 = fe_mad64( y[k], 1216u, l2 );
-    if( k < 8 ) { o[k] = (u32)l1 & FE_M29; l1 >>= 29; p[k] = (u32)l2 & FE_M29; l2 >>= 29; }
+    if( j < 8 ) { l1 = fe_mad64( (u32)h1, 1216u, l1 ); l2 = fe_mad64( (u32)h2, 1216u, l2 ); }
+    if( j > 0 ) { l1 = fe_mad64( (u32)(hp1 >> 32), 9728u, l1 ); l2 = fe_mad64( (u32)(hp2 >> 32), 9728u, l2 ); }
+    if( j < 8 ) { o[j] = (u32)l1 & FE_M29; l1 >>= 29; p[j] = (u32)l2 & FE_M29; l2 >>= 29; }
+    hp1 = h1; hp2 = h2;
   }
-  fe_fin2( r, o, l1 ); fe_fin2( s, p, l2 );
+  fe_fin( r, o, l1 ); fe_fin( s, p, l2 );
   FE_SCHED_FENCE();
 }
 
 DEV void fe_sq2( fe & r, fe const & a, fe & s, fe const & c ) {
-  u32 da[9], dc[9], z[9], o[9], y[9], p[9];
+  u32 da[9], dc[9], o[9], p[9];
   #pragma unroll
   for( int i=0; i<9; i++ ) { da[i] = a.v[i] << 1; dc[i] = c.v[i] << 1; }
-  u64 h1 = 0, l1 = 0, h2 = 0, l2 = 0;
+  u64 l1 = 0, hp1 = 0, h1 = 0, l2 = 0, hp2 = 0, h2 = 0;
   #pragma unroll
-  for( int k=0; k<=8; k++ ) {
-    if( k < 8 ) {
-      int cc = 9 + k;
-      bool first = (k == 0);
-      #pragma unroll
-      for( int i=cc-8; 2*i<cc; i++ ) {
-        h1 = first ? fe_mul64( da[i], a.v[cc-i] ) : fe_mad64( da[i], a.v[cc-i], h1 );
-        h2 = first ? fe_mul64( dc[i], c.v[cc-i] ) : fe_mad64( dc[i], c.v[cc-i], h2 );
-        first = false;
-      }
-      if( (cc & 1) == 0 ) { h1 = fe_mad64( a.v[cc/2], a.v[cc/2], h1 ); h2 = fe_mad64( c.v[cc/2], c.v[cc/2], h2 ); }
-      z[k] = (u32)h1 & FE_M29; h1 >>= 29;
-      y[k] = (u32)h2 & FE_M29; h2 >>= 29;
-    } else {
-      z[8] = (u32)h1; y[8] = (u32)h2;
-    }
+  for( int j=0; j<=8; j++ ) {
+    int cc = 9 + j;
     #pragma unroll
-    for( int i=0; 2*i<k; i++ ) { l1 = fe_mad64( da[i], a.v[k-i], l1 ); l2 = fe_mad64( dc[i], c.v[k-i], l2 ); }
-    if( (k & 1) == 0 ) {
-      l1 = (k == 0) ? fe_mul64( a.v[0], a.v[0] ) : fe_mad64( a.v[k/2], a.v[k/2], l1 );
-      l2 = (k == 0) ? fe_mul64( c.v[0], c.v[0] ) : fe_mad64( c.v[k/2], c.v[k/2], l2 );
+    for( int i=0; i<=8; i++ ) {
+      int hi = cc - 8 + i;
+      if( j < 8 && 2*hi < cc ) {
+        h1 = (i == 0) ? fe_mul64( da[hi], a.v[cc-hi] ) : fe_mad64( da[hi], a.v[cc-hi], h1 );
+        h2 = (i == 0) ? fe_mul64( dc[hi], c.v[cc-hi] ) : fe_mad64( dc[hi], c.v[cc-hi], h2 );
+      }
+      if( 2*i < j ) {
+        l1 = fe_mad64( da[i], a.v[j-i], l1 );
+        l2 = fe_mad64( dc[i], c.v[j-i], l2 );
+      }
     }
-    l1 = fe_mad64( z[k], 1216u, l1 );
-    l2 = fe_mad64( y[k], 1216u, l2 );
-    if( k < 8 ) { o[k] = (u32)l1 & FE_M29; l1 >>= 29; p[k] = (u32)l2 & FE_M29; l2 >>= 29; }
+    if( j < 8 && (cc & 1) == 0 ) {
+      h1 = (cc == 16) ? fe_mul64( a.v[8], a.v[8] ) : fe_mad64( a.v[cc/2], a.v[cc/2], h1 );
+      h2 = (cc == 16) ? fe_mul64( c.v[8], c.v[8] ) : fe_mad64( c.v[cc/2], c.v[cc/2], h2 );
+    }
+    if( (j & 1) == 0 ) {
+      l1 = (j == 0) ? fe_mul64( a.v[0], a.v[0] ) : fe_mad64( a.v[j/2], a.v[j/2], l1 );
+      l2 = (j == 0) ? fe_mul64( c.v[0], c.v[0] ) : fe_mad64( c.v[j/2], c.v[j/2], l2 );
+    }
+    if( j < 8 ) { l1 = fe_mad64( (u32)h1, 1216u, l1 ); l2 = fe_mad64( (u32)h2, 1216u, l2 ); }
+    if( j > 0 ) { l1 = fe_mad64( (u32)(hp1 >> 32), 9728u, l1 ); l2 = fe_mad64( (u32)(hp2 >> 32), 9728u, l2 ); }
+    if( j < 8 ) { o[j] = (u32)l1 & FE_M29; l1 >>= 29; p[j] = (u32)l2 & FE_M29; l2 >>= 29; }
+    hp1 = h1; hp2 = h2;
   }
-  fe_fin2( r, o, l1 ); fe_fin2( s, p, l2 );
+  fe_fin( r, o, l1 ); fe_fin( s, p, l2 );
   FE_SCHED_FENCE();
 }
 

@@ -34,18 +34,21 @@ U64 = 1 << 64
 
 
 def _mulcols(a, b):
-    acc = 0
-    z = [0] * 9
+    """fe_mul / fe_sq: high columns 9..16 kept as unsplit 64-bit sums H_k;
+    low column j = carry + products + 1216*lo32(H_{j+9}) + 9728*hi32(H_{j+8})."""
+    H = []
     for k in range(9, 17):
-        acc = 0 if k == 9 else acc >> R
-        acc += sum(a[i] * b[k - i] for i in range(k - 8, 9))
-        assert acc < U64, ("mul high column overflow", k, acc.bit_length())
-        z[k - 9] = min(acc, M29)
-    z[8] = acc >> R
+        h = sum(a[i] * b[k - i] for i in range(k - 8, 9))
+        assert h < U64, ("mul high column overflow", k, h.bit_length())
+        H.append(h)
     out = [0] * 9
+    acc = 0
     for k in range(9):
-        acc = (0 if k == 0 else acc >> R) + z[k] * FOLD_HI
-        acc += sum(a[i] * b[k - i] for i in range(k + 1))
+        acc = (0 if k == 0 else acc >> R) + sum(a[i] * b[k - i] for i in range(k + 1))
+        if k < 8:
+            acc += min(H[k], (1 << 32) - 1) * FOLD_HI
+        if k > 0:
+            acc += (H[k - 1] >> 32) * (FOLD_HI << 3)
         assert acc < U64, ("mul low column overflow", k, acc.bit_length())
         if k < 8:
             out[k] = min(acc, M29)
