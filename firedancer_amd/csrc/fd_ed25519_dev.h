@@ -74,9 +74,13 @@ DEV u64 fe_mul64( u32 a, u32 b )        { u64 r = (u64)a * b;     asm( "" : "+v"
        + 9728*hi32(H_{8+j})  (2^261 == 19*2^6 == 1216 mod p, and the high
        word of H_{8+j} sits 32 bits up = 3 bits into the next limb: 1216*8),
        then split at 29 bits (v_and + v_lshrrev_b64).
-   H_{9+j} is computed interleaved with low column j (independent chains fill
-   each other's wait states), so only two H sums are live.  Column 8 splits
-   at bit 255 and its overflow folds into limb 0 with 19. */
+   H_{9+j} is computed interleaved with low column j, so only two H sums are
+   live per product.  Column 8 splits at bit 255 and its overflow folds into
+   limb 0 with 19.
+   fe_mulN / fe_sqN run N independent products interleaved instruction by
+   instruction (2N chains): back-to-back dependent v_mad_u64_u32 need a wait
+   state, which another chain's multiply-add fills.  Formulas pair (N = 2)
+   their independent products; N = 3 measured slower in k_verify_dsm. */
 DEV void fe_fin( fe & r, u32 o[9], u64 l ) {   /* column-8 split + fold, output copy */
   o[8] = (u32)l & FE_M23;
   u64 t = (l >> 23) * 19u + o[0];
@@ -86,115 +90,95 @@ DEV void fe_fin( fe & r, u32 o[9], u64 l ) {   /* column-8 split + fold, output 
   for( int i=0; i<9; i++ ) r.v[i] = o[i];
 }
 
-DEV void fe_mul( fe & r, fe const & a, fe const & b ) {
-  u32 o[9];
-  u64 l = 0, hp = 0, h = 0;
+template<int N>
+DEV void fe_mulN( fe * const r[N], fe const * const a[N], fe const * const b[N] ) {
+  u32 o[N][9];
+  u64 l[N], hp[N], h[N];
   #pragma unroll
   for( int j=0; j<=8; j++ ) {
     int c = 9 + j;
     #pragma unroll
     for( int i=0; i<=8; i++ ) {
-      if( j < 8 && i <= 7-j ) h = (i == 0) ? fe_mul64( a.v[c-8+i], b.v[8-i] ) : fe_mad64( a.v[c-8+i], b.v[8-i], h );
-      if( i <= j ) l = (j == 0) ? fe_mul64( a.v[0], b.v[0] ) : fe_mad64( a.v[i], b.v[j-i], l );
+      if( j < 8 && i <= 7-j ) {
+        #pragma unroll
+        for( int n=0; n<N; n++ ) h[n] = (i == 0) ? fe_mul64( a[n]->v[c-8+i], b[n]->v[8-i] ) : fe_mad64( a[n]->v[c-8+i], b[n]->v[8-i], h[n] );
+      }
+      if( i <= j ) {
+        #pragma unroll
+        for( int n=0; n<N; n++ ) l[n] = (j == 0) ? fe_mul64( a[n]->v[0], b[n]->v[0] ) : fe_mad64( a[n]->v[i], b[n]->v[j-i], l[n] );
+      }
     }
-    if( j < 8 ) l = fe_mad64( (u32)h, 1216u, l );
-    if( j > 0 ) l = fe_mad64( (u32)(hp >> 32), 9728u, l );
-    if( j < 8 ) { o[j] = (u32)l & FE_M29; l >>= 29; }
-    hp = h;
+    #pragma unroll
+    for( int n=0; n<N; n++ ) {
+      if( j < 8 ) l[n] = fe_mad64( (u32)h[n], 1216u, l[n] );
+      if( j > 0 ) l[n] = fe_mad64( (u32)(hp[n] >> 32), 9728u, l[n] );
+      if( j < 8 ) { o[n][j] = (u32)l[n] & FE_M29; l[n] >>= 29; }
+      hp[n] = h[n];
+    }
   }
-  fe_fin( r, o, l );
+  #pragma unroll
+  for( int n=0; n<N; n++ ) fe_fin( *r[n], o[n], l[n] );
   FE_SCHED_FENCE();
 }
 
-/* a^2: same columns, off-diagonal products taken once against 2*a_i */
-DEV void fe_sq( fe & r, fe const & a ) {
-  u32 d[9], o[9];
+/* squares: off-diagonal products taken once against 2*a_i */
+template<int N>
+DEV void fe_sqN( fe * const r[N], fe const * const a[N] ) {
+  u32 d[N][9], o[N][9];
+  u64 l[N], hp[N], h[N];
   #pragma unroll
-  for( int i=0; i<9; i++ ) d[i] = a.v[i] << 1;
-  u64 l = 0, hp = 0, h = 0;
+  for( int n=0; n<N; n++ ) {
+    #pragma unroll
+    for( int i=0; i<9; i++ ) d[n][i] = a[n]->v[i] << 1;
+  }
   #pragma unroll
   for( int j=0; j<=8; j++ ) {
     int c = 9 + j;
     #pragma unroll
     for( int i=0; i<=8; i++ ) {
       int hi = c - 8 + i;                             /* high: d[hi]*a[c-hi], 2*hi < c */
-      if( j < 8 && 2*hi < c ) h = (i == 0) ? fe_mul64( d[hi], a.v[c-hi] ) : fe_mad64( d[hi], a.v[c-hi], h );
-      if( 2*i < j ) l = fe_mad64( d[i], a.v[j-i], l );                 /* j >= 1: onto the carry */
+      if( j < 8 && 2*hi < c ) {
+        #pragma unroll
+        for( int n=0; n<N; n++ ) h[n] = (i == 0) ? fe_mul64( d[n][hi], a[n]->v[c-hi] ) : fe_mad64( d[n][hi], a[n]->v[c-hi], h[n] );
+      }
+      if( 2*i < j ) {                                 /* j >= 1: onto the carry */
+        #pragma unroll
+        for( int n=0; n<N; n++ ) l[n] = fe_mad64( d[n][i], a[n]->v[j-i], l[n] );
+      }
     }
-    if( j < 8 && (c & 1) == 0 ) h = (c == 16) ? fe_mul64( a.v[8], a.v[8] ) : fe_mad64( a.v[c/2], a.v[c/2], h );
-    if( (j & 1) == 0 ) l = (j == 0) ? fe_mul64( a.v[0], a.v[0] ) : fe_mad64( a.v[j/2], a.v[j/2], l );
-    if( j < 8 ) l = fe_mad64( (u32)h, 1216u, l );
-    if( j > 0 ) l = fe_mad64( (u32)(hp >> 32), 9728u, l );
-    if( j < 8 ) { o[j] = (u32)l & FE_M29; l >>= 29; }
-    hp = h;
+    #pragma unroll
+    for( int n=0; n<N; n++ ) {
+      if( j < 8 && (c & 1) == 0 ) h[n] = (c == 16) ? fe_mul64( a[n]->v[8], a[n]->v[8] ) : fe_mad64( a[n]->v[c/2], a[n]->v[c/2], h[n] );
+      if( (j & 1) == 0 ) l[n] = (j == 0) ? fe_mul64( a[n]->v[0], a[n]->v[0] ) : fe_mad64( a[n]->v[j/2], a[n]->v[j/2], l[n] );
+    }
+    #pragma unroll
+    for( int n=0; n<N; n++ ) {
+      if( j < 8 ) l[n] = fe_mad64( (u32)h[n], 1216u, l[n] );
+      if( j > 0 ) l[n] = fe_mad64( (u32)(hp[n] >> 32), 9728u, l[n] );
+      if( j < 8 ) { o[n][j] = (u32)l[n] & FE_M29; l[n] >>= 29; }
+      hp[n] = h[n];
+    }
   }
-  fe_fin( r, o, l );
+  #pragma unroll
+  for( int n=0; n<N; n++ ) fe_fin( *r[n], o[n], l[n] );
   FE_SCHED_FENCE();
 }
 
-/* Two independent products interleaved (four chains).  Used wherever a
-   formula has two independent multiplies. */
+DEV void fe_mul( fe & r, fe const & a, fe const & b ) {
+  fe * const R[1] = { &r }; fe const * const A[1] = { &a }; fe const * const B[1] = { &b };
+  fe_mulN<1>( R, A, B );
+}
 DEV void fe_mul2( fe & r, fe const & a, fe const & b, fe & s, fe const & c, fe const & d ) {
-  u32 o[9], p[9];
-  u64 l1 = 0, hp1 = 0, h1 = 0, l2 = 0, hp2 = 0, h2 = 0;
-  #pragma unroll
-  for( int j=0; j<=8; j++ ) {
-    int cc = 9 + j;
-    #pragma unroll
-    for( int i=0; i<=8; i++ ) {
-      if( j < 8 && i <= 7-j ) {
-        h1 = (i == 0) ? fe_mul64( a.v[cc-8+i], b.v[8-i] ) : fe_mad64( a.v[cc-8+i], b.v[8-i], h1 );
-        h2 = (i == 0) ? fe_mul64( c.v[cc-8+i], d.v[8-i] ) : fe_mad64( c.v[cc-8+i], d.v[8-i], h2 );
-      }
-      if( i <= j ) {
-        l1 = (j == 0) ? fe_mul64( a.v[0], b.v[0] ) : fe_mad64( a.v[i], b.v[j-i], l1 );
-        l2 = (j == 0) ? fe_mul64( c.v[0], d.v[0] ) : fe_mad64( c.v[i], d.v[j-i], l2 );
-      }
-    }
-    if( j < 8 ) { l1 = fe_mad64( (u32)h1, 1216u, l1 ); l2 = fe_mad64( (u32)h2, 1216u, l2 ); }
-    if( j > 0 ) { l1 = fe_mad64( (u32)(hp1 >> 32), 9728u, l1 ); l2 = fe_mad64( (u32)(hp2 >> 32), 9728u, l2 ); }
-    if( j < 8 ) { o[j] = (u32)l1 & FE_M29; l1 >>= 29; p[j] = (u32)l2 & FE_M29; l2 >>= 29; }
-    hp1 = h1; hp2 = h2;
-  }
-  fe_fin( r, o, l1 ); fe_fin( s, p, l2 );
-  FE_SCHED_FENCE();
+  fe * const R[2] = { &r, &s }; fe const * const A[2] = { &a, &c }; fe const * const B[2] = { &b, &d };
+  fe_mulN<2>( R, A, B );
 }
-
+DEV void fe_sq( fe & r, fe const & a ) {
+  fe * const R[1] = { &r }; fe const * const A[1] = { &a };
+  fe_sqN<1>( R, A );
+}
 DEV void fe_sq2( fe & r, fe const & a, fe & s, fe const & c ) {
-  u32 da[9], dc[9], o[9], p[9];
-  #pragma unroll
-  for( int i=0; i<9; i++ ) { da[i] = a.v[i] << 1; dc[i] = c.v[i] << 1; }
-  u64 l1 = 0, hp1 = 0, h1 = 0, l2 = 0, hp2 = 0, h2 = 0;
-  #pragma unroll
-  for( int j=0; j<=8; j++ ) {
-    int cc = 9 + j;
-    #pragma unroll
-    for( int i=0; i<=8; i++ ) {
-      int hi = cc - 8 + i;
-      if( j < 8 && 2*hi < cc ) {
-        h1 = (i == 0) ? fe_mul64( da[hi], a.v[cc-hi] ) : fe_mad64( da[hi], a.v[cc-hi], h1 );
-        h2 = (i == 0) ? fe_mul64( dc[hi], c.v[cc-hi] ) : fe_mad64( dc[hi], c.v[cc-hi], h2 );
-      }
-      if( 2*i < j ) {
-        l1 = fe_mad64( da[i], a.v[j-i], l1 );
-        l2 = fe_mad64( dc[i], c.v[j-i], l2 );
-      }
-    }
-    if( j < 8 && (cc & 1) == 0 ) {
-      h1 = (cc == 16) ? fe_mul64( a.v[8], a.v[8] ) : fe_mad64( a.v[cc/2], a.v[cc/2], h1 );
-      h2 = (cc == 16) ? fe_mul64( c.v[8], c.v[8] ) : fe_mad64( c.v[cc/2], c.v[cc/2], h2 );
-    }
-    if( (j & 1) == 0 ) {
-      l1 = (j == 0) ? fe_mul64( a.v[0], a.v[0] ) : fe_mad64( a.v[j/2], a.v[j/2], l1 );
-      l2 = (j == 0) ? fe_mul64( c.v[0], c.v[0] ) : fe_mad64( c.v[j/2], c.v[j/2], l2 );
-    }
-    if( j < 8 ) { l1 = fe_mad64( (u32)h1, 1216u, l1 ); l2 = fe_mad64( (u32)h2, 1216u, l2 ); }
-    if( j > 0 ) { l1 = fe_mad64( (u32)(hp1 >> 32), 9728u, l1 ); l2 = fe_mad64( (u32)(hp2 >> 32), 9728u, l2 ); }
-    if( j < 8 ) { o[j] = (u32)l1 & FE_M29; l1 >>= 29; p[j] = (u32)l2 & FE_M29; l2 >>= 29; }
-    hp1 = h1; hp2 = h2;
-  }
-  fe_fin( r, o, l1 ); fe_fin( s, p, l2 );
-  FE_SCHED_FENCE();
+  fe * const R[2] = { &r, &s }; fe const * const A[2] = { &a, &c };
+  fe_sqN<2>( R, A );
 }
 
 DEV void fe_add( fe & r, fe const & a, fe const & b ) {

@@ -133,35 +133,58 @@ __global__ __launch_bounds__(64) void k_btab_init( u32 * btab ) {
   e[27] = 0u;
 }
 
-__global__ __launch_bounds__(256)
+/* FD_PREP_WAVES: waves per SIMD the register allocation of k_verify_prep is
+   held to (0: compiler's choice) */
+#ifndef FD_PREP_WAVES
+#define FD_PREP_WAVES 0
+#endif
+#if FD_PREP_WAVES
+#define PREP_OCCUPANCY __attribute__((amdgpu_waves_per_eu(FD_PREP_WAVES, FD_PREP_WAVES)))
+#else
+#define PREP_OCCUPANCY
+#endif
+
+__global__ __launch_bounds__(256) PREP_OCCUPANCY
 void k_verify_prep( ulong n, ulong chunk, uchar const * __restrict__ sigs, uchar const * __restrict__ pubs,
                     uchar const * __restrict__ pool, uint const * __restrict__ moff, uint const * __restrict__ msz,
                     u32 * __restrict__ st ) {
   ulong i = (ulong)blockIdx.x * blockDim.x + threadIdx.x;
   if( i >= n ) return;
-  u32 sig[16], pub[8];
-  load_words( sig, sigs + 64*i, 16 );
-  load_words( pub, pubs + 32*i, 8 );
-  u32 flags = sc_is_canonical( sig + 8 ) ? 0u : F_S_BAD;                 /* user.c:159-161 */
   u32 * s = st + i;
+  u32 flags;
   /* decode A then R (user.c:165), one at a time: a rolled loop keeps the two
-     pow22523 chains from being interleaved into one register-hungry block */
-  #pragma unroll 1
-  for( int pt=0; pt<2; pt++ ) {
-    u32 w[8];
-    #pragma unroll
-    for( int q=0; q<8; q++ ) w[q] = pt ? sig[q] : pub[q];
-    ge_p3 P;
-    u32 f = ge_decode( P, w );
-    bool small = !(f & 1u) && ge_affine_is_small_order( P );              /* user.c:194-199 */
-    if( pt == 0 ) flags |= ((f & 1u) ? F_A_NOTSQ : 0u) | ((f & 2u) ? F_A_ZX : 0u) | (small ? F_A_SMALL : 0u);
-    else          flags |= ((f & 1u) ? F_R_NOTSQ : 0u) | ((f & 2u) ? F_R_ZX : 0u) | (small ? F_R_SMALL : 0u);
-    u32 xw[8], yw[8];
-    fe_to_words( xw, P.X ); fe_to_words( yw, P.Y );
-    u32 base = pt ? ST_RX : ST_AX;
-    #pragma unroll
-    for( int q=0; q<8; q++ ) { s[(base+q)*chunk] = xw[q]; s[(base+8+q)*chunk] = yw[q]; }
+     pow22523 chains from being interleaved into one register-hungry block
+     (measured: pairing the two chains instruction by instruction is slower,
+     it costs a wave per SIMD of occupancy) */
+  {
+    u32 sig[16], pub[8];
+    load_words( sig, sigs + 64*i, 16 );
+    load_words( pub, pubs + 32*i, 8 );
+    flags = sc_is_canonical( sig + 8 ) ? 0u : F_S_BAD;                     /* user.c:159-161 */
+    #pragma unroll 1
+    for( int pt=0; pt<2; pt++ ) {
+      u32 w[8];
+      #pragma unroll
+      for( int q=0; q<8; q++ ) w[q] = pt ? sig[q] : pub[q];
+      ge_p3 P;
+      u32 f = ge_decode( P, w );
+      bool small = !(f & 1u) && ge_affine_is_small_order( P );            /* user.c:194-199 */
+      if( pt == 0 ) flags |= ((f & 1u) ? F_A_NOTSQ : 0u) | ((f & 2u) ? F_A_ZX : 0u) | (small ? F_A_SMALL : 0u);
+      else          flags |= ((f & 1u) ? F_R_NOTSQ : 0u) | ((f & 2u) ? F_R_ZX : 0u) | (small ? F_R_SMALL : 0u);
+      u32 xw[8], yw[8];
+      fe_to_words( xw, P.X ); fe_to_words( yw, P.Y );
+      u32 base = pt ? ST_RX : ST_AX;
+      #pragma unroll
+      for( int q=0; q<8; q++ ) { s[(base+q)*chunk] = xw[q]; s[(base+8+q)*chunk] = yw[q]; }
+    }
   }
+  /* reload the record for the hash rather than holding it across the decode
+     (the opaque pointer keeps the compiler from reusing the first load) */
+  uchar const * sp = sigs + 64*i, * pp = pubs + 32*i;
+  asm volatile( "" : "+v"(sp), "+v"(pp) );
+  u32 sig[16], pub[8];
+  load_words( sig, sp, 16 );
+  load_words( pub, pp, 8 );
   u32 k[8];
   hram_mod_l( k, sig, pub, pool + moff[i], msz[i] );                       /* user.c:205-207 */
   #pragma unroll
