@@ -48,6 +48,7 @@ METRIC = "ed25519 verifies/sec (1/2/4/8 MI355X) + % of INT32 VALU peak"
 N_M, N_S = 1378.6, 1518.1
 N_M_DECODE, N_S_DECODE = 42.0, 510.0
 PEAK_OPS = 256 * 4 * 32 * 2.4e9          # 78.6e12 int32 lane-ops/s (32-wide SIMDs)
+PMC_SUMMARY = "r01b_pmc_summary.json"    # rocprofv3 PMC passes of this kernel build (tools/run_profile.sh)
 
 
 def w_total(msg_sz):
@@ -206,11 +207,11 @@ def main():
     # HBM-side bytes per k_verify_dsm launch from the committed rocprofv3 PMC
     # passes of this same command (FETCH_SIZE x2 per the gfx950 note + WRITE_SIZE)
     traffic, traffic_src = None, None
-    pmc = os.path.join(REPO, "profiles", "r01_pmc_summary.json")
+    pmc = os.path.join(REPO, "profiles", PMC_SUMMARY)
     if cfg == "c2" and n == (1 << 20) and os.path.exists(pmc):
         with open(pmc) as f:
             traffic = json.load(f)["kernels"]["k_verify_dsm"]["derived"]["hbm_side_bytes_per_launch"]
-        traffic_src = "profiles/r01_pmc_summary.json: FETCH_SIZE*2 + WRITE_SIZE of k_verify_dsm (rocprofv3 --pmc)"
+        traffic_src = f"profiles/{PMC_SUMMARY}: FETCH_SIZE*2 + WRITE_SIZE of k_verify_dsm (rocprofv3 --pmc)"
     ingest_bytes = 64 + 32 + msg_sz + 8                   # sig, pub, msg, off/sz per signature
     ingest_gbps = n / launches_per_step * ingest_bytes / (prep_avg_ms * 1e-3) / 1e9
 
