@@ -5,14 +5,14 @@
    256-thread workgroups = 4 wave64):
 
      k_verify_prep  S<L check, decode A and R (sqrt chains), small-order
-                    checks, k = SHA-512(R||A||M) mod L  -> 128-B state record
+                    checks, k = SHA-512(R||A||M) mod L -> 192-B state record;
+                    survivor compaction: final codes of pre-check failures,
+                    survivors -> idx[] (k_verify_dsm runs only them)
      k_verify_dsm   base-point table -> LDS; table [0..8](-A) -> per-lane HBM
                     scratch; [k](-A) + [S]B by fixed signed windows (radix 16
                     for A, radix 256 for B: every lane adds at the same
                     positions, so the wave never diverges on digits);
-                    projective compare with R; int8 code + verdict bitmap
-     k_compact      final codes of pre-check failures; survivors -> idx[]
-                    (k_verify_dsm runs only survivors)
+                    projective compare with R; int8 code
      k_bitmap       verdict bitmap from codes (64-bit ballot per wave)
      k_group_reduce batch_single_msg / per-txn semantics over sig codes
 
@@ -60,8 +60,7 @@
 #define ST_AY   24
 #define ST_RX   32
 #define ST_RY   40
-#define ST_FLAG 48
-#define ST_WORDS 49
+#define ST_WORDS 48
 
 struct fd_ed25519_hip_ctx {
   int          device;
@@ -133,6 +132,22 @@ __global__ __launch_bounds__(64) void k_btab_init( u32 * btab ) {
   e[27] = 0u;
 }
 
+DEV int code_of( u32 f, int errmode, bool eq ) {
+  if( errmode == FD_ED25519_HIP_ERRMODE_AVX512 ) {
+    if( f & F_S_BAD ) return FD_ED25519_ERR_SIG;
+    if( f & (F_A_NOTSQ|F_A_ZX|F_R_NOTSQ|F_R_ZX) ) return FD_ED25519_ERR_SIG;  /* decode2 -> -1/-2 -> ERR_SIG */
+    if( f & F_A_SMALL ) return FD_ED25519_ERR_PUBKEY;
+    if( f & F_R_SMALL ) return FD_ED25519_ERR_SIG;
+  } else {
+    if( f & F_S_BAD ) return FD_ED25519_ERR_SIG;
+    if( f & F_A_NOTSQ ) return FD_ED25519_ERR_PUBKEY;                          /* frombytes_2x -> 1 */
+    if( f & F_R_NOTSQ ) return FD_ED25519_ERR_SIG;                             /*             -> 2 */
+    if( f & (F_A_SMALL|F_A_ZX) ) return FD_ED25519_ERR_PUBKEY;
+    if( f & (F_R_SMALL|F_R_ZX) ) return FD_ED25519_ERR_SIG;
+  }
+  return eq ? FD_ED25519_SUCCESS : FD_ED25519_ERR_MSG;
+}
+
 /* FD_PREP_WAVES: waves per SIMD the register allocation of k_verify_prep is
    held to (0: compiler's choice) */
 #ifndef FD_PREP_WAVES
@@ -147,11 +162,13 @@ __global__ __launch_bounds__(64) void k_btab_init( u32 * btab ) {
 __global__ __launch_bounds__(256) PREP_OCCUPANCY
 void k_verify_prep( ulong n, ulong chunk, uchar const * __restrict__ sigs, uchar const * __restrict__ pubs,
                     uchar const * __restrict__ pool, uint const * __restrict__ moff, uint const * __restrict__ msz,
-                    u32 * __restrict__ st ) {
+                    u32 * __restrict__ st, int errmode, u32 * __restrict__ idx, u32 * __restrict__ count,
+                    signed char * __restrict__ codes ) {
   ulong i = (ulong)blockIdx.x * blockDim.x + threadIdx.x;
-  if( i >= n ) return;
+  bool active = i < n;
+  u32 flags = 0u;
+  if( active ) {
   u32 * s = st + i;
-  u32 flags;
   /* decode A then R (user.c:165), one at a time: a rolled loop keeps the two
      pow22523 chains from being interleaved into one register-hungry block
      (measured: pairing the two chains instruction by instruction is slower,
@@ -192,24 +209,23 @@ void k_verify_prep( ulong n, ulong chunk, uchar const * __restrict__ sigs, uchar
     s[(ST_K +w)*chunk] = k[w];
     s[(ST_S +w)*chunk] = sig[8+w];
   }
-  s[ST_FLAG*chunk] = flags;
+  }
+  /* Survivor compaction: a signature that fails a pre-check gets its final
+     code here; the others are appended (wave-aggregated atomic, spread over
+     the whole prep launch) to idx[] so that k_verify_dsm spends no lanes on
+     them (the DSM is VALU-issue bound: a masked lane costs as much as a live
+     one). */
+  bool pass = active && code_of( flags, FD_ED25519_HIP_ERRMODE_AVX512, true ) == FD_ED25519_SUCCESS;
+  if( active && !pass ) codes[i] = (signed char)code_of( flags, errmode, false );
+  unsigned long long m = __ballot( pass );
+  u32 lane = threadIdx.x & 63u;
+  u32 base = 0;
+  if( lane == 0u && m ) base = atomicAdd( count, (u32)__popcll( m ) );
+  base = __shfl( base, 0 );
+  u32 below = (u32)__popcll( m & ((1ULL << lane) - 1ULL) );
+  if( pass ) idx[base + below] = (u32)i;
 }
 
-DEV int code_of( u32 f, int errmode, bool eq ) {
-  if( errmode == FD_ED25519_HIP_ERRMODE_AVX512 ) {
-    if( f & F_S_BAD ) return FD_ED25519_ERR_SIG;
-    if( f & (F_A_NOTSQ|F_A_ZX|F_R_NOTSQ|F_R_ZX) ) return FD_ED25519_ERR_SIG;  /* decode2 -> -1/-2 -> ERR_SIG */
-    if( f & F_A_SMALL ) return FD_ED25519_ERR_PUBKEY;
-    if( f & F_R_SMALL ) return FD_ED25519_ERR_SIG;
-  } else {
-    if( f & F_S_BAD ) return FD_ED25519_ERR_SIG;
-    if( f & F_A_NOTSQ ) return FD_ED25519_ERR_PUBKEY;                          /* frombytes_2x -> 1 */
-    if( f & F_R_NOTSQ ) return FD_ED25519_ERR_SIG;                             /*             -> 2 */
-    if( f & (F_A_SMALL|F_A_ZX) ) return FD_ED25519_ERR_PUBKEY;
-    if( f & (F_R_SMALL|F_R_ZX) ) return FD_ED25519_ERR_SIG;
-  }
-  return eq ? FD_ED25519_SUCCESS : FD_ED25519_ERR_MSG;
-}
 
 DEV void store_cached( u32 * t, ge_cached const & c ) {   /* 36 words, 16-byte aligned */
   u32 w[36];
@@ -242,27 +258,6 @@ DEV void digits_shl( u32 d[8], u32 bits ) {
   #pragma unroll
   for( int i=7; i>0; i-- ) d[i] = __builtin_amdgcn_alignbit( d[i], d[i-1], 32u - bits );
   d[0] <<= bits;
-}
-
-/* Survivor compaction: signatures that fail a pre-check get their final code
-   here; the others are appended (wave-aggregated atomic) to idx[] so that
-   k_verify_dsm spends no lanes on them (the DSM is VALU-issue bound, so a
-   masked lane costs as much as a live one). */
-__global__ __launch_bounds__(256)
-void k_compact( ulong n, ulong chunk, u32 const * __restrict__ st, int errmode, u32 * __restrict__ idx,
-                u32 * __restrict__ count, signed char * __restrict__ codes ) {
-  ulong i = (ulong)blockIdx.x * blockDim.x + threadIdx.x;
-  bool active = i < n;
-  u32 flags = active ? st[ST_FLAG*chunk + i] : 0u;
-  bool pass = active && code_of( flags, FD_ED25519_HIP_ERRMODE_AVX512, true ) == FD_ED25519_SUCCESS;
-  if( active && !pass ) codes[i] = (signed char)code_of( flags, errmode, false );
-  unsigned long long m = __ballot( pass );
-  u32 lane = threadIdx.x & 63u;
-  u32 base = 0;
-  if( lane == 0u && m ) base = atomicAdd( count, (u32)__popcll( m ) );
-  base = __shfl( base, 0 );
-  u32 below = (u32)__popcll( m & ((1ULL << lane) - 1ULL) );
-  if( pass ) idx[base + below] = (u32)i;
 }
 
 /* verdict bitmap from codes: bit i%64 of word i/64 set iff codes[i]==0 */
@@ -555,15 +550,13 @@ fd_ed25519_hip_verify_dev( fd_ed25519_hip_ctx_t * ctx, ulong n, uchar const * d_
   for( ulong off = 0; off < n; off += ctx->chunk ) {
     ulong m = n - off < ctx->chunk ? n - off : ctx->chunk;
     dim3 grid( (unsigned)((m + 255) / 256) ), blk( 256 );
+    FD_CHECK( hipMemsetAsync( ctx->d_count, 0, sizeof(u32), s ) );
     if( ctx->timing ) FD_CHECK( hipEventRecord( ctx->ev[0], s ) );
     hipLaunchKernelGGL( k_verify_prep, grid, blk, 0, s, m, ctx->chunk, d_sigs + 64*off, d_pubs + 32*off,
-                        d_pool, d_msg_off + off, d_msg_sz + off, ctx->d_state );
-    FD_CHECK( hipGetLastError() );
-    if( ctx->timing ) FD_CHECK( hipEventRecord( ctx->ev[1], s ) );
-    FD_CHECK( hipMemsetAsync( ctx->d_count, 0, sizeof(u32), s ) );
-    hipLaunchKernelGGL( k_compact, grid, blk, 0, s, m, ctx->chunk, ctx->d_state, ctx->errmode, ctx->d_idx,
+                        d_pool, d_msg_off + off, d_msg_sz + off, ctx->d_state, ctx->errmode, ctx->d_idx,
                         ctx->d_count, d_codes + off );
     FD_CHECK( hipGetLastError() );
+    if( ctx->timing ) FD_CHECK( hipEventRecord( ctx->ev[1], s ) );
     if( ctx->timing ) FD_CHECK( hipEventRecord( ctx->ev[3], s ) );
     hipLaunchKernelGGL( k_verify_dsm, grid, blk, 0, s, ctx->chunk, ctx->d_state, ctx->d_btab, ctx->d_atab,
                         ctx->d_idx, ctx->d_count, d_codes + off );
