@@ -162,8 +162,8 @@ DEV int code_of( u32 f, int errmode, bool eq ) {
 __global__ __launch_bounds__(256) PREP_OCCUPANCY
 void k_verify_prep( ulong n, ulong chunk, uchar const * __restrict__ sigs, uchar const * __restrict__ pubs,
                     uchar const * __restrict__ pool, uint const * __restrict__ moff, uint const * __restrict__ msz,
-                    u32 * __restrict__ st, int errmode, u32 * __restrict__ idx, u32 * __restrict__ count,
-                    signed char * __restrict__ codes ) {
+                    u32 fixed_sz, u32 * __restrict__ st, int errmode, u32 * __restrict__ idx,
+                    u32 * __restrict__ count, signed char * __restrict__ codes ) {
   ulong i = (ulong)blockIdx.x * blockDim.x + threadIdx.x;
   bool active = i < n;
   u32 flags = 0u;
@@ -203,7 +203,9 @@ void k_verify_prep( ulong n, ulong chunk, uchar const * __restrict__ sigs, uchar
   load_words( sig, sp, 16 );
   load_words( pub, pp, 8 );
   u32 k[8];
-  hram_mod_l( k, sig, pub, pool + moff[i], msz[i] );                       /* user.c:205-207 */
+  u32 mo = moff ? moff[i] : (u32)i * fixed_sz;                            /* moff NULL: message i = */
+  u32 ms = msz  ? msz[i]  : fixed_sz;                                      /* pool[i*fixed_sz, +fixed_sz) */
+  hram_mod_l( k, sig, pub, pool + mo, ms );                                /* user.c:205-207 */
   #pragma unroll
   for( int w=0; w<8; w++ ) {
     s[(ST_K +w)*chunk] = k[w];
@@ -541,10 +543,11 @@ fd_ed25519_hip_get_timing( fd_ed25519_hip_ctx_t const * ctx, double * prep_ms, d
   if( launches ) *launches = ctx->dsm_launches;
 }
 
-int
-fd_ed25519_hip_verify_dev( fd_ed25519_hip_ctx_t * ctx, ulong n, uchar const * d_sigs, uchar const * d_pubs,
-                           uchar const * d_pool, uint const * d_msg_off, uint const * d_msg_sz,
-                           signed char * d_codes, ulong * d_bitmap, void * stream ) {
+/* d_msg_off NULL: fixed-size messages, message i = d_pool[ i*fixed_sz, +fixed_sz ) */
+static int
+verify_impl( fd_ed25519_hip_ctx_t * ctx, ulong n, uchar const * d_sigs, uchar const * d_pubs,
+             uchar const * d_pool, uint const * d_msg_off, uint const * d_msg_sz, uint fixed_sz,
+             signed char * d_codes, ulong * d_bitmap, void * stream ) {
   hipStream_t s = stream ? (hipStream_t)stream : ctx->stream;
   FD_CHECK( hipSetDevice( ctx->device ) );
   for( ulong off = 0; off < n; off += ctx->chunk ) {
@@ -552,9 +555,11 @@ fd_ed25519_hip_verify_dev( fd_ed25519_hip_ctx_t * ctx, ulong n, uchar const * d_
     dim3 grid( (unsigned)((m + 255) / 256) ), blk( 256 );
     FD_CHECK( hipMemsetAsync( ctx->d_count, 0, sizeof(u32), s ) );
     if( ctx->timing ) FD_CHECK( hipEventRecord( ctx->ev[0], s ) );
+    uchar const * pool = d_msg_off ? d_pool : d_pool + off*(ulong)fixed_sz;
     hipLaunchKernelGGL( k_verify_prep, grid, blk, 0, s, m, ctx->chunk, d_sigs + 64*off, d_pubs + 32*off,
-                        d_pool, d_msg_off + off, d_msg_sz + off, ctx->d_state, ctx->errmode, ctx->d_idx,
-                        ctx->d_count, d_codes + off );
+                        pool, d_msg_off ? d_msg_off + off : (uint const *)0,
+                        d_msg_off ? d_msg_sz + off : (uint const *)0, fixed_sz, ctx->d_state, ctx->errmode,
+                        ctx->d_idx, ctx->d_count, d_codes + off );
     FD_CHECK( hipGetLastError() );
     if( ctx->timing ) FD_CHECK( hipEventRecord( ctx->ev[1], s ) );
     if( ctx->timing ) FD_CHECK( hipEventRecord( ctx->ev[3], s ) );
@@ -579,6 +584,21 @@ fd_ed25519_hip_verify_dev( fd_ed25519_hip_ctx_t * ctx, ulong n, uchar const * d_
     }
   }
   return 0;
+}
+
+int
+fd_ed25519_hip_verify_dev( fd_ed25519_hip_ctx_t * ctx, ulong n, uchar const * d_sigs, uchar const * d_pubs,
+                           uchar const * d_pool, uint const * d_msg_off, uint const * d_msg_sz,
+                           signed char * d_codes, ulong * d_bitmap, void * stream ) {
+  return verify_impl( ctx, n, d_sigs, d_pubs, d_pool, d_msg_off, d_msg_sz, 0u, d_codes, d_bitmap, stream );
+}
+
+int
+fd_ed25519_hip_verify_fixed_dev( fd_ed25519_hip_ctx_t * ctx, ulong n, uchar const * d_sigs, uchar const * d_pubs,
+                                 uchar const * d_msgs, uint msg_sz, signed char * d_codes, ulong * d_bitmap,
+                                 void * stream ) {
+  return verify_impl( ctx, n, d_sigs, d_pubs, d_msgs, (uint const *)0, (uint const *)0, msg_sz, d_codes, d_bitmap,
+                      stream );
 }
 
 int

@@ -15,9 +15,14 @@
 
    The ordered host pass restates after_frag (fd_verify_tile.c:101-161)
    around fd_txn_verify (fd_verify_tile.h:61-111) with the tcache of
-   fd_tcache.h:237-410, prefetching map slots a few frags ahead. */
+   fd_tcache.h:237-410, prefetching map slots a few frags ahead.
+
+   The replay caller (include/fd_replay_hip.h) reuses the expansion and the
+   reduce on caller-parsed transactions: k_desc_spans turns fd_txn_t fields
+   into the same spans, k_exec_codes maps the per-txn code to the runtime's. */
 
 #include "../../include/fd_verify_hip.h"
+#include "../../include/fd_replay_hip.h"
 
 #include <hip/hip_runtime.h>
 #include <chrono>
@@ -592,4 +597,108 @@ extern "C" void fd_verify_hip_tile_metrics( fd_verify_hip_tile_t const * t, ulon
 
 extern "C" void fd_verify_hip_tile_last_timing( fd_verify_hip_tile_t const * t, double out[3] ) {
   out[0] = t->last_gpu_ms; out[1] = t->last_host_ms; out[2] = t->last_sigs;
+}
+
+/**********************************************************************/
+/* replay and shred callers (include/fd_replay_hip.h)                  */
+
+static_assert( sizeof(fd_txn_hip_desc_t) == 16, "fd_txn_hip_desc_t layout" );
+
+/* caller-parsed txn -> the signature span k_txn_expand consumes.
+   fd_executor_txn_verify (fd_executor.c:1607-1623) passes signature_cnt as
+   batch_sz: 0 or > 16 is ERR_SIG before any signature is read
+   (fd_ed25519_user.c:238-241), so such a txn gets no records (cnt 0, which
+   the group reduce turns into ERR_SIG). */
+__global__ __launch_bounds__(256)
+void k_desc_spans( ulong n, fd_txn_hip_desc_t const * __restrict__ desc, u8 * __restrict__ nsig,
+                   u32 * __restrict__ sig_at, u32 * __restrict__ acct_at, u32 * __restrict__ msg_at,
+                   u32 * __restrict__ msg_sz ) {
+  ulong j = (ulong)blockIdx.x * blockDim.x + threadIdx.x;
+  if( j >= n ) return;
+  fd_txn_hip_desc_t d = desc[j];
+  u32 c = d.signature_cnt;
+  nsig[j]    = (u8)((c >= 1u && c <= 16u) ? c : 0u);
+  sig_at[j]  = d.payload_off + d.signature_off;
+  acct_at[j] = d.payload_off + d.acct_addr_off;
+  msg_at[j]  = d.payload_off + d.message_off;
+  msg_sz[j]  = d.payload_sz >= d.message_off ? (u32)(d.payload_sz - d.message_off) : 0u;
+}
+
+/* fd_executor.c:1619-1621 */
+__global__ __launch_bounds__(256)
+void k_exec_codes( ulong n, signed char const * __restrict__ tcode, int * __restrict__ res ) {
+  ulong j = (ulong)blockIdx.x * blockDim.x + threadIdx.x;
+  if( j >= n ) return;
+  res[j] = tcode[j] == FD_ED25519_SUCCESS ? FD_RUNTIME_HIP_EXECUTE_SUCCESS : FD_RUNTIME_HIP_TXN_ERR_SIGNATURE_FAILURE;
+}
+
+struct fd_replay_hip {
+  fd_ed25519_hip_ctx_t * ctx;
+  ulong   max_txn, rcap;
+  u8 *    d_nsig; u32 * d_sig_at; u32 * d_acct_at; u32 * d_msg_at; u32 * d_msg_sz;
+  u32 *   d_first; u8 * d_cnt; signed char * d_tcode; u32 * d_counter; u32 * h_counter;
+  u8 *    d_rsig; u8 * d_rpub; u32 * d_rmoff; u32 * d_rmsz; signed char * d_rcode;
+};
+
+extern "C" fd_replay_hip_t *
+fd_replay_hip_new( fd_ed25519_hip_ctx_t * ctx, ulong max_txn ) {
+  if( !ctx || !max_txn ) return 0;
+  TX_CHECK( hipSetDevice( fd_ed25519_hip_ctx_device( ctx ) ) );
+  fd_replay_hip_t * r = (fd_replay_hip_t *)calloc( 1, sizeof(fd_replay_hip_t) );
+  ulong n = max_txn, rc = 16ul*max_txn;                    /* at most 16 records per txn */
+  r->ctx = ctx; r->max_txn = n; r->rcap = rc;
+  TX_CHECK( hipMalloc( &r->d_nsig, n ) );       TX_CHECK( hipMalloc( &r->d_sig_at, 4*n ) );
+  TX_CHECK( hipMalloc( &r->d_acct_at, 4*n ) );  TX_CHECK( hipMalloc( &r->d_msg_at, 4*n ) );
+  TX_CHECK( hipMalloc( &r->d_msg_sz, 4*n ) );   TX_CHECK( hipMalloc( &r->d_first, 4*n ) );
+  TX_CHECK( hipMalloc( &r->d_cnt, n ) );        TX_CHECK( hipMalloc( &r->d_tcode, n ) );
+  TX_CHECK( hipMalloc( &r->d_counter, 4 ) );    TX_CHECK( hipHostMalloc( &r->h_counter, 4, 0 ) );
+  TX_CHECK( hipMalloc( &r->d_rsig, 64*rc ) );   TX_CHECK( hipMalloc( &r->d_rpub, 32*rc ) );
+  TX_CHECK( hipMalloc( &r->d_rmoff, 4*rc ) );   TX_CHECK( hipMalloc( &r->d_rmsz, 4*rc ) );
+  TX_CHECK( hipMalloc( &r->d_rcode, rc ) );
+  return r;
+}
+
+extern "C" void
+fd_replay_hip_delete( fd_replay_hip_t * r ) {
+  if( !r ) return;
+  (void)hipSetDevice( fd_ed25519_hip_ctx_device( r->ctx ) );
+  (void)hipStreamSynchronize( (hipStream_t)fd_ed25519_hip_ctx_stream( r->ctx ) );
+  (void)hipFree( r->d_nsig ); (void)hipFree( r->d_sig_at ); (void)hipFree( r->d_acct_at ); (void)hipFree( r->d_msg_at );
+  (void)hipFree( r->d_msg_sz ); (void)hipFree( r->d_first ); (void)hipFree( r->d_cnt ); (void)hipFree( r->d_tcode );
+  (void)hipFree( r->d_counter ); (void)hipHostFree( r->h_counter );
+  (void)hipFree( r->d_rsig ); (void)hipFree( r->d_rpub ); (void)hipFree( r->d_rmoff ); (void)hipFree( r->d_rmsz );
+  (void)hipFree( r->d_rcode );
+  free( r );
+}
+
+extern "C" int
+fd_replay_hip_txn_verify_dev( fd_replay_hip_t * r, ulong n, uchar const * d_pool, fd_txn_hip_desc_t const * d_desc,
+                              int * d_result, void * stream ) {
+  if( n > r->max_txn ) return -1;
+  if( !n ) return 0;
+  hipStream_t st = stream ? (hipStream_t)stream : (hipStream_t)fd_ed25519_hip_ctx_stream( r->ctx );
+  TX_CHECK( hipSetDevice( fd_ed25519_hip_ctx_device( r->ctx ) ) );
+  dim3 grid( (unsigned)((n + 255)/256) ), blk( 256 );
+  hipLaunchKernelGGL( k_desc_spans, grid, blk, 0, st, n, d_desc, r->d_nsig, r->d_sig_at, r->d_acct_at, r->d_msg_at,
+                      r->d_msg_sz );
+  TX_CHECK( hipGetLastError() );
+  TX_CHECK( hipMemsetAsync( r->d_counter, 0, 4, st ) );
+  hipLaunchKernelGGL( k_txn_expand, grid, blk, 0, st, n, d_pool, r->d_nsig, r->d_sig_at, r->d_acct_at, r->d_msg_at,
+                      r->d_msg_sz, r->d_counter, r->d_first, r->d_cnt, r->d_rsig, r->d_rpub, r->d_rmoff, r->d_rmsz,
+                      r->rcap );
+  TX_CHECK( hipGetLastError() );
+  TX_CHECK( hipMemcpyAsync( r->h_counter, r->d_counter, 4, hipMemcpyDeviceToHost, st ) );
+  TX_CHECK( hipStreamSynchronize( st ) );                 /* the record count sizes the verify launch */
+  ulong nsig = *r->h_counter;
+  fd_ed25519_hip_verify_dev( r->ctx, nsig, r->d_rsig, r->d_rpub, d_pool, r->d_rmoff, r->d_rmsz, r->d_rcode, NULL, st );
+  fd_ed25519_hip_group_reduce_dev( r->ctx, n, r->d_first, r->d_cnt, r->d_rcode, r->d_tcode, st );
+  hipLaunchKernelGGL( k_exec_codes, grid, blk, 0, st, n, r->d_tcode, d_result );
+  TX_CHECK( hipGetLastError() );
+  return 0;
+}
+
+extern "C" int
+fd_fec_hip_verify_roots_dev( fd_ed25519_hip_ctx_t * ctx, ulong n, uchar const * d_roots, uchar const * d_sigs,
+                             uchar const * d_pubs, signed char * d_codes, void * stream ) {
+  return fd_ed25519_hip_verify_fixed_dev( ctx, n, d_sigs, d_pubs, d_roots, 32u, d_codes, NULL, stream );
 }

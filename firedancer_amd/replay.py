@@ -1,0 +1,102 @@
+"""Host-side mirror of the bulk verify callers outside the verify tile, backed
+by the gfx950 engine (C ABI: include/fd_replay_hip.h, same library as
+ed25519.py).
+
+Reference interfaces mirrored:
+  fd_executor_txn_verify   src/flamenco/runtime/fd_executor.c:1607-1623
+                           (FD_RUNTIME_EXECUTE_SUCCESS / FD_RUNTIME_TXN_ERR_
+                           SIGNATURE_FAILURE, fd_runtime_err.h:4,19), called
+                           per txn by the exec tile (fd_exec_tile.c:161)
+  FEC-set root check       src/disco/shred/fd_fec_resolver.c:476
+                           (fd_ed25519_verify of a 32-B Merkle root)
+
+Both take whole batches (a block's transactions, a poll's FEC sets) in device
+memory.  There is no CPU fallback.
+"""
+import ctypes
+
+import numpy as np
+
+from .ed25519 import _ptr, lib as _ed_lib
+
+FD_RUNTIME_EXECUTE_SUCCESS = 0
+FD_RUNTIME_TXN_ERR_SIGNATURE_FAILURE = -13
+
+# Every symbol include/fd_replay_hip.h declares (checked by tests/test_abi.py).
+EXPORTS = ("fd_replay_hip_new", "fd_replay_hip_delete", "fd_replay_hip_txn_verify_dev",
+           "fd_fec_hip_verify_roots_dev")
+
+# fd_txn_hip_desc_t (16 bytes): the fd_txn_p_t payload span and the fd_txn_t
+# fields fd_executor_txn_verify reads (fd_txn.h:186-249)
+DESC_DTYPE = np.dtype([("payload_off", "<u4"), ("payload_sz", "<u2"), ("signature_off", "<u2"),
+                       ("message_off", "<u2"), ("acct_addr_off", "<u2"), ("signature_cnt", "u1"),
+                       ("_pad", "u1", (3,))])
+assert DESC_DTYPE.itemsize == 16
+
+_bound = False
+
+
+def lib():
+    global _bound
+    L = _ed_lib()
+    if not _bound:
+        c = ctypes
+        vp, u64 = c.c_void_p, c.c_ulong
+        L.fd_replay_hip_new.restype = vp
+        L.fd_replay_hip_new.argtypes = [vp, u64]
+        L.fd_replay_hip_delete.argtypes = [vp]
+        L.fd_replay_hip_txn_verify_dev.restype = c.c_int
+        L.fd_replay_hip_txn_verify_dev.argtypes = [vp, u64, vp, vp, vp, vp]
+        L.fd_fec_hip_verify_roots_dev.restype = c.c_int
+        L.fd_fec_hip_verify_roots_dev.argtypes = [vp, u64, vp, vp, vp, vp, vp]
+        _bound = True
+    return L
+
+
+def descs_from_txn_t(txn_t, payload_off, payload_sz):
+    """fd_txn_hip_desc_t records from fd_txn_t bytes (one row per txn: byte 1
+    signature_cnt, 2-3 signature_off, 4-5 message_off, 10-11 acct_addr_off)."""
+    t = np.ascontiguousarray(txn_t, np.uint8)
+    d = np.zeros(t.shape[0], DESC_DTYPE)
+    d["payload_off"] = payload_off
+    d["payload_sz"] = payload_sz
+    d["signature_cnt"] = t[:, 1]
+    d["signature_off"] = t[:, 2].astype(np.uint16) | (t[:, 3].astype(np.uint16) << 8)
+    d["message_off"] = t[:, 4].astype(np.uint16) | (t[:, 5].astype(np.uint16) << 8)
+    d["acct_addr_off"] = t[:, 10].astype(np.uint16) | (t[:, 11].astype(np.uint16) << 8)
+    return d
+
+
+class ReplayVerifier:
+    """fd_executor_txn_verify over batches of up to max_txn parsed txns."""
+
+    def __init__(self, verifier, max_txn):
+        self._lib = lib()
+        self.verifier = verifier
+        self.r = self._lib.fd_replay_hip_new(verifier.ctx, int(max_txn))
+        if not self.r:
+            raise RuntimeError("fd_replay_hip_new failed")
+        self.max_txn = int(max_txn)
+
+    def txn_verify_dev(self, n, pool, desc, result, stream=None):
+        """pool: device bytes; desc: device fd_txn_hip_desc_t[n]; result: device int32[n]."""
+        rc = self._lib.fd_replay_hip_txn_verify_dev(self.r, int(n), _ptr(pool), _ptr(desc), _ptr(result), stream)
+        if rc:
+            raise ValueError(f"fd_replay_hip_txn_verify_dev: n={n} > max_txn={self.max_txn}")
+
+    def close(self):
+        if self.r:
+            self._lib.fd_replay_hip_delete(self.r)
+            self.r = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def fec_verify_roots_dev(verifier, n, roots, sigs, pubs, codes, stream=None):
+    """FEC-set root check: codes[i] = fd_ed25519_verify(roots[32i:32i+32], sigs[i], pubs[i])."""
+    return lib().fd_fec_hip_verify_roots_dev(verifier.ctx, int(n), _ptr(roots), _ptr(sigs), _ptr(pubs),
+                                             _ptr(codes), stream)

@@ -120,6 +120,21 @@ fd_ed25519_hip_verify_dev( fd_ed25519_hip_ctx_t * ctx,
                            ulong *                d_bitmap,
                            void *                 stream );
 
+/* Fixed-size messages laid out back to back: message i = d_msgs[ i*msg_sz,
+   (i+1)*msg_sz ) (e.g. 32-byte shred Merkle roots, fd_fec_resolver.c:476).
+   Same semantics and requirements as fd_ed25519_hip_verify_dev (d_msgs
+   readable 16 bytes past its end). */
+int
+fd_ed25519_hip_verify_fixed_dev( fd_ed25519_hip_ctx_t * ctx,
+                                 ulong                  n,
+                                 uchar const *          d_sigs,
+                                 uchar const *          d_pubs,
+                                 uchar const *          d_msgs,
+                                 uint                   msg_sz,
+                                 signed char *          d_codes,
+                                 ulong *                d_bitmap,
+                                 void *                 stream );
+
 /* Same from host memory, synchronous (copies in/out over PCIe). */
 int
 fd_ed25519_hip_verify_host( fd_ed25519_hip_ctx_t * ctx,

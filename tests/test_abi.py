@@ -5,7 +5,7 @@ import os
 import re
 import subprocess
 
-from firedancer_amd import ed25519, verify_tile
+from firedancer_amd import ed25519, replay, verify_tile
 from firedancer_amd.build import LIB, build
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -23,7 +23,8 @@ def test_build_and_exports():
     assert os.path.exists(LIB)
     assert declared_functions("fd_ed25519_hip.h") == set(ed25519.EXPORTS)
     assert declared_functions("fd_verify_hip.h") == set(verify_tile.EXPORTS)
-    names = set(ed25519.EXPORTS) | set(verify_tile.EXPORTS)
+    assert declared_functions("fd_replay_hip.h") == set(replay.EXPORTS)
+    names = set(ed25519.EXPORTS) | set(verify_tile.EXPORTS) | set(replay.EXPORTS)
     out = subprocess.check_output(["nm", "-D", "--defined-only", LIB]).decode()
     exported = set(re.findall(r" T (\w+)", out))
     assert names <= exported, names - exported

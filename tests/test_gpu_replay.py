@@ -1,0 +1,143 @@
+"""GPU parity of the replay and shred callers (include/fd_replay_hip.h) against
+the oracle restatement: fd_executor_txn_verify over whole blocks of parsed
+transactions (fd_executor.c:1607-1623), its batch_sz edge cases, and the FEC
+resolver's 32-byte root check (fd_fec_resolver.c:476).  Bit-exact."""
+import numpy as np
+import pytest
+
+import oracle_lib as O
+import txn_lib as T
+
+pytestmark = pytest.mark.gpu
+
+
+def _dev(a):
+    import torch
+    a = np.ascontiguousarray(a)
+    if a.size == 0:
+        a = np.zeros(1, a.dtype)
+    return torch.from_numpy(a).to("cuda:0")
+
+
+def _expected_exec(pool, desc):
+    """fd_executor_txn_verify restated on the oracle, one txn at a time."""
+    out = np.zeros(desc.size, np.int32)
+    for j, d in enumerate(desc):
+        p = pool[int(d["payload_off"]):int(d["payload_off"]) + int(d["payload_sz"])]
+        so, mo, ao, cnt = int(d["signature_off"]), int(d["message_off"]), int(d["acct_addr_off"]), int(d["signature_cnt"])
+        if cnt == 0 or cnt > 16:
+            code = O.verify_batch_single_msg(p[mo:].tobytes(), b"\0" * 64, b"\0" * 32, cnt & 0xff)
+        else:
+            code = O.verify_batch_single_msg(p[mo:].tobytes(), p[so:so + 64 * cnt].tobytes(),
+                                             p[ao:ao + 32 * cnt].tobytes(), cnt)
+        out[j] = 0 if code == 0 else -13
+    return out
+
+
+def _run_replay(verifier, pool, desc, max_txn=None):
+    import torch
+    from firedancer_amd.replay import ReplayVerifier
+    n = desc.size
+    rv = ReplayVerifier(verifier, max_txn or max(n, 1))
+    d_pool = _dev(np.concatenate([pool, np.zeros(16, np.uint8)]))
+    d_desc = _dev(desc.view(np.uint8))
+    d_res = torch.full((max(n, 1),), 7, dtype=torch.int32, device="cuda:0")
+    rv.txn_verify_dev(n, d_pool, d_desc, d_res)
+    verifier.sync()
+    res = d_res.cpu().numpy()[:n]
+    rv.close()
+    return res
+
+
+def test_replay_block_vs_oracle(verifier):
+    """A 3000-txn block (1-12 signers, C2 mutations per signature) parsed by
+    the oracle's fd_txn_parse, verified as fd_executor_txn_verify would."""
+    from firedancer_amd.replay import descs_from_txn_t
+    from firedancer_amd.txn_workload import make_txn_stream
+    s = make_txn_stream(3000, T.oracle_signer, seed=0x5150, dup_frac=0.0, graft_frac=0.0, bad_frac=0.0)
+    tsz, out = T.oracle_parse_many(s.pool, s.off, s.sz)
+    ok = np.nonzero(tsz)[0]
+    desc = descs_from_txn_t(out[ok], s.off[ok], s.sz[ok])
+    exp = _expected_exec(s.pool, desc)
+    got = _run_replay(verifier, s.pool, desc)
+    assert np.array_equal(got, exp)
+    assert 0.3 < (got == 0).mean() < 0.95 and (got == -13).any()
+    assert (desc["signature_cnt"] > 1).sum() > 100
+
+
+def test_replay_batch_sz_edges(verifier):
+    """signature_cnt 0, 1, 16 (all valid), 16 (one bad), 17 (ERR_SIG unread)."""
+    rng = np.random.default_rng(3)
+    msg = rng.integers(0, 256, 100, dtype=np.uint8)
+    prvs = rng.integers(0, 256, (17, 32), dtype=np.uint8)
+    mpool = np.concatenate([msg, np.zeros(16, np.uint8)])
+    pubs, sigs = O.sign_many(prvs, mpool, np.zeros(17, np.uint32), np.full(17, 100, np.uint32))
+    payload = np.concatenate([sigs.reshape(-1), pubs.reshape(-1), msg])
+    bad = payload.copy()
+    bad[64 * 9 + 5] ^= 0x10                                  # signature 9 of 16
+    pool = np.concatenate([payload, bad])
+    from firedancer_amd.replay import DESC_DTYPE
+    rows = []
+    for off, cnt in ((0, 0), (0, 1), (0, 16), (payload.size, 16), (0, 17), (0, 255)):
+        d = np.zeros(1, DESC_DTYPE)
+        d["payload_off"], d["payload_sz"], d["signature_cnt"] = off, payload.size, cnt
+        d["signature_off"], d["acct_addr_off"], d["message_off"] = 0, 64 * 17, 96 * 17
+        rows.append(d)
+    desc = np.concatenate(rows)
+    exp = _expected_exec(pool, desc)
+    assert exp.tolist() == [-13, 0, 0, -13, -13, -13]
+    assert np.array_equal(_run_replay(verifier, pool, desc), exp)
+    assert _run_replay(verifier, pool, desc[:0], max_txn=4).size == 0
+
+
+def test_replay_max_txn_guard(verifier):
+    import torch
+    from firedancer_amd.replay import DESC_DTYPE, ReplayVerifier
+    rv = ReplayVerifier(verifier, 4)
+    d = torch.zeros(16 * 8, dtype=torch.uint8, device="cuda:0")
+    with pytest.raises(ValueError):
+        rv.txn_verify_dev(8, d, d, d)
+    rv.close()
+    assert DESC_DTYPE.itemsize == 16
+
+
+def test_fec_roots_vs_oracle(verifier):
+    """5000 FEC-set roots signed by 4 leaders, C2 mutations, through the
+    fixed-size-message path; codes equal the oracle's fd_ed25519_verify."""
+    import torch
+    from firedancer_amd.replay import fec_verify_roots_dev
+    from firedancer_amd.workload import c2_mutate
+    rng = np.random.default_rng(11)
+    n = 5000
+    roots = rng.integers(0, 256, n * 32, dtype=np.uint8)
+    leaders = rng.integers(0, 256, (4, 32), dtype=np.uint8)
+    prvs = leaders[rng.integers(0, 4, n)]
+    moff = (np.arange(n) * 32).astype(np.uint32)
+    msz = np.full(n, 32, np.uint32)
+    pool = np.concatenate([roots, np.zeros(16, np.uint8)])
+    pubs, sigs = O.sign_many(prvs, pool, moff, msz)
+    assert len(np.unique(pubs, axis=0)) == 4
+    c2_mutate(sigs, pubs, rng)
+    exp = O.verify_many(sigs, pubs, pool, moff, msz)
+    codes = torch.zeros(n, dtype=torch.int8, device="cuda:0")
+    fec_verify_roots_dev(verifier, n, _dev(pool), _dev(sigs), _dev(pubs), codes)
+    verifier.sync()
+    got = codes.cpu().numpy()
+    assert np.array_equal(got, exp)
+    assert 0.6 < (got == 0).mean() < 0.95
+
+
+def test_fixed_matches_offsets(verifier):
+    """verify_fixed_dev(msg_sz) == verify_dev with explicit offsets, across
+    several chunks (the verifier fixture's chunk is 2^18)."""
+    import torch
+    from firedancer_amd.workload import make_batch_gpu
+    n = (1 << 18) + 777
+    b = make_batch_gpu(verifier, n, msg_sz=64, seed=77, mix="c2")
+    c1 = torch.zeros(n, dtype=torch.int8, device="cuda:0")
+    c2 = torch.zeros(n, dtype=torch.int8, device="cuda:0")
+    verifier.verify_dev(n, b.sigs, b.pubs, b.pool, b.msg_off, b.msg_sz, c1)
+    verifier.verify_fixed_dev(n, b.sigs, b.pubs, b.pool, 64, c2)
+    verifier.sync()
+    assert torch.equal(c1, c2)
+    assert 0.7 < float((c1 == 0).float().mean()) < 0.9
