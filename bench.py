@@ -94,6 +94,22 @@ def cpu_baseline(sigs, pubs, pool, moff, msz, gpu_codes, threads, target_s):
             "codes_match": bool(np.array_equal(ref_codes, gpu_codes))}
 
 
+_JSON_FD = [1]
+
+
+def emit(out):
+    """The one JSON line, on the real stdout (see _quiet_stdout)."""
+    os.write(_JSON_FD[0], (json.dumps(out) + "\n").encode())
+
+
+def _quiet_stdout():
+    """RCCL prints its version banner to stdout when a communicator is created;
+    route fd 1 to stderr for the run and keep the real stdout for emit()."""
+    sys.stdout.flush()
+    _JSON_FD[0] = os.dup(1)
+    os.dup2(2, 1)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -120,6 +136,7 @@ def main():
     dist = None
     if world > 1 or args.force_dist:
         import torch.distributed as dist
+        _quiet_stdout()
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
     from firedancer_amd import Verifier
@@ -262,7 +279,7 @@ def main():
                          "ingest_GBps": round(ingest_gbps, 2), "ingest_bytes_per_sig": ingest_bytes},
             "cpu_baseline": cpu,
         }
-        print(json.dumps(out), flush=True)
+        emit(out)
     v.close()
     if dist:
         dist.barrier()
@@ -414,7 +431,7 @@ def run_c4(args, rank, world, local, dist):
                          "prep_ms_per_batch": round(prep_ms, 4)},
             "cpu_baseline": cpu,
         }
-        print(json.dumps(out), flush=True)
+        emit(out)
     tile.close()
     v.close()
     if dist:

@@ -337,6 +337,9 @@ void k_verify_dsm( ulong chunk, u32 const * __restrict__ st, u32 const * __restr
       int sa = (int)da - 8;
       u32 nega = sa < 0 ? ~0u : 0u;
       u32 ia = (u32)(sa < 0 ? -sa : sa);
+      /* issued before the window's 4 doublings, which hide its latency
+         (measured: loading after them, or trading the 36 registers for a
+         4th wave per SIMD, is not faster) */
       ge_cached e; load_cached( e, tab + ia*ATAB_ENT );
       if( w != 63 ) {
         #pragma unroll 1
