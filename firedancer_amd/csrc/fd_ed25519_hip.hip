@@ -163,8 +163,13 @@ __global__ __launch_bounds__(256) PREP_OCCUPANCY
 void k_verify_prep( ulong n, ulong chunk, uchar const * __restrict__ sigs, uchar const * __restrict__ pubs,
                     uchar const * __restrict__ pool, uint const * __restrict__ moff, uint const * __restrict__ msz,
                     u32 fixed_sz, u32 * __restrict__ st, int errmode, u32 * __restrict__ idx,
-                    u32 * __restrict__ count, signed char * __restrict__ codes ) {
+                    u32 * __restrict__ count, signed char * __restrict__ codes, u32 const * __restrict__ d_n,
+                    ulong rec0 ) {
   ulong i = (ulong)blockIdx.x * blockDim.x + threadIdx.x;
+  if( d_n ) {                                   /* device-side count: this chunk starts at record rec0 */
+    ulong c = *d_n;
+    n = c > rec0 ? (c - rec0 < n ? c - rec0 : n) : 0ul;
+  }
   bool active = i < n;
   u32 flags = 0u;
   if( active ) {
@@ -264,8 +269,10 @@ DEV void digits_shl( u32 d[8], u32 bits ) {
 
 /* verdict bitmap from codes: bit i%64 of word i/64 set iff codes[i]==0 */
 __global__ __launch_bounds__(256)
-void k_bitmap( ulong n, signed char const * __restrict__ codes, ulong * __restrict__ bitmap ) {
+void k_bitmap( ulong n, signed char const * __restrict__ codes, ulong * __restrict__ bitmap,
+               u32 const * __restrict__ d_n, ulong rec0 ) {
   ulong i = (ulong)blockIdx.x * blockDim.x + threadIdx.x;
+  if( d_n ) { ulong c = *d_n; n = c > rec0 ? (c - rec0 < n ? c - rec0 : n) : 0ul; }
   bool ok = i < n && codes[i] == FD_ED25519_SUCCESS;
   unsigned long long b = __ballot( ok );
   if( (threadIdx.x & 63u) == 0u && i < n ) bitmap[i >> 6] = b;
@@ -550,7 +557,7 @@ fd_ed25519_hip_get_timing( fd_ed25519_hip_ctx_t const * ctx, double * prep_ms, d
 static int
 verify_impl( fd_ed25519_hip_ctx_t * ctx, ulong n, uchar const * d_sigs, uchar const * d_pubs,
              uchar const * d_pool, uint const * d_msg_off, uint const * d_msg_sz, uint fixed_sz,
-             signed char * d_codes, ulong * d_bitmap, void * stream ) {
+             signed char * d_codes, ulong * d_bitmap, u32 const * d_n, void * stream ) {
   hipStream_t s = stream ? (hipStream_t)stream : ctx->stream;
   FD_CHECK( hipSetDevice( ctx->device ) );
   for( ulong off = 0; off < n; off += ctx->chunk ) {
@@ -562,7 +569,7 @@ verify_impl( fd_ed25519_hip_ctx_t * ctx, ulong n, uchar const * d_sigs, uchar co
     hipLaunchKernelGGL( k_verify_prep, grid, blk, 0, s, m, ctx->chunk, d_sigs + 64*off, d_pubs + 32*off,
                         pool, d_msg_off ? d_msg_off + off : (uint const *)0,
                         d_msg_off ? d_msg_sz + off : (uint const *)0, fixed_sz, ctx->d_state, ctx->errmode,
-                        ctx->d_idx, ctx->d_count, d_codes + off );
+                        ctx->d_idx, ctx->d_count, d_codes + off, d_n, off );
     FD_CHECK( hipGetLastError() );
     if( ctx->timing ) FD_CHECK( hipEventRecord( ctx->ev[1], s ) );
     if( ctx->timing ) FD_CHECK( hipEventRecord( ctx->ev[3], s ) );
@@ -570,7 +577,7 @@ verify_impl( fd_ed25519_hip_ctx_t * ctx, ulong n, uchar const * d_sigs, uchar co
                         ctx->d_idx, ctx->d_count, d_codes + off );
     FD_CHECK( hipGetLastError() );
     if( d_bitmap ) {
-      hipLaunchKernelGGL( k_bitmap, grid, blk, 0, s, m, d_codes + off, d_bitmap + off/64 );
+      hipLaunchKernelGGL( k_bitmap, grid, blk, 0, s, m, d_codes + off, d_bitmap + off/64, d_n, off );
       FD_CHECK( hipGetLastError() );
     }
     if( ctx->timing ) {
@@ -593,7 +600,14 @@ int
 fd_ed25519_hip_verify_dev( fd_ed25519_hip_ctx_t * ctx, ulong n, uchar const * d_sigs, uchar const * d_pubs,
                            uchar const * d_pool, uint const * d_msg_off, uint const * d_msg_sz,
                            signed char * d_codes, ulong * d_bitmap, void * stream ) {
-  return verify_impl( ctx, n, d_sigs, d_pubs, d_pool, d_msg_off, d_msg_sz, 0u, d_codes, d_bitmap, stream );
+  return verify_impl( ctx, n, d_sigs, d_pubs, d_pool, d_msg_off, d_msg_sz, 0u, d_codes, d_bitmap, NULL, stream );
+}
+
+int
+fd_ed25519_hip_verify_dev_count( fd_ed25519_hip_ctx_t * ctx, ulong n_max, uint const * d_n, uchar const * d_sigs,
+                                 uchar const * d_pubs, uchar const * d_pool, uint const * d_msg_off,
+                                 uint const * d_msg_sz, signed char * d_codes, ulong * d_bitmap, void * stream ) {
+  return verify_impl( ctx, n_max, d_sigs, d_pubs, d_pool, d_msg_off, d_msg_sz, 0u, d_codes, d_bitmap, d_n, stream );
 }
 
 int
@@ -601,7 +615,7 @@ fd_ed25519_hip_verify_fixed_dev( fd_ed25519_hip_ctx_t * ctx, ulong n, uchar cons
                                  uchar const * d_msgs, uint msg_sz, signed char * d_codes, ulong * d_bitmap,
                                  void * stream ) {
   return verify_impl( ctx, n, d_sigs, d_pubs, d_msgs, (uint const *)0, (uint const *)0, msg_sz, d_codes, d_bitmap,
-                      stream );
+                      NULL, stream );
 }
 
 int

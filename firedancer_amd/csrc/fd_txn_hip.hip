@@ -10,7 +10,8 @@
      k_txn_expand  slot allocation (one atomic per wave, ballot prefix sums)
                    and 16-B-aligned signature records for the verify
                    pipeline; first/cnt per txn for the reduce
-     fd_ed25519_hip_verify_dev + fd_ed25519_hip_group_reduce_dev
+     fd_ed25519_hip_verify_dev_count + fd_ed25519_hip_group_reduce_dev
+                   (the record count never leaves the device)
      D2H           txn_t_sz (2 B), code (1 B), tag (8 B) per frag
 
    The ordered host pass restates after_frag (fd_verify_tile.c:101-161)
@@ -517,10 +518,11 @@ fd_verify_hip_tile_submit( fd_verify_hip_tile_t * t, ulong n, uchar const * d_po
   hipLaunchKernelGGL( k_txn_expand, grid, blk, 0, st, n, d_pool, s.d_nsig, s.d_sig_at, s.d_acct_at, s.d_msg_at,
                       s.d_msg_sz, s.d_counter, s.d_first, s.d_cnt, s.d_rsig, s.d_rpub, s.d_rmoff, s.d_rmsz, s.rcap );
   TX_CHECK( hipGetLastError() );
-  TX_CHECK( hipMemcpyAsync( s.h_counter, s.d_counter, 4, hipMemcpyDeviceToHost, st ) );
-  TX_CHECK( hipStreamSynchronize( st ) );                 /* the signature count sizes the verify launch */
-  s.nsig = *s.h_counter;
-  fd_ed25519_hip_verify_dev( t->ctx, s.nsig, s.d_rsig, s.d_rpub, d_pool, s.d_rmoff, s.d_rmsz, s.d_rcode, NULL, st );
+  TX_CHECK( hipMemcpyAsync( s.h_counter, s.d_counter, 4, hipMemcpyDeviceToHost, st ) );   /* metrics */
+  /* the record count stays on the device: no host round trip between the
+     expansion and the verify, so submit never waits on the GPU */
+  fd_ed25519_hip_verify_dev_count( t->ctx, need, s.d_counter, s.d_rsig, s.d_rpub, d_pool, s.d_rmoff, s.d_rmsz,
+                                   s.d_rcode, NULL, st );
   fd_ed25519_hip_group_reduce_dev( t->ctx, n, s.d_first, s.d_cnt, s.d_rcode, s.d_tcode, st );
   TX_CHECK( hipMemcpyAsync( s.h_tsz, s.d_tsz, 2*n, hipMemcpyDeviceToHost, st ) );
   TX_CHECK( hipMemcpyAsync( s.h_tcode, s.d_tcode, n, hipMemcpyDeviceToHost, st ) );
@@ -536,6 +538,7 @@ fd_verify_hip_tile_complete( fd_verify_hip_tile_t * t, ulong const * bundle_id, 
   tile_slot & s = t->slot[t->completed & 1];
   TX_CHECK( hipSetDevice( fd_ed25519_hip_ctx_device( t->ctx ) ) );
   TX_CHECK( hipEventSynchronize( s.ev_done ) );
+  s.nsig = *s.h_counter;
   float gpu_ms = 0.f;
   TX_CHECK( hipEventElapsedTime( &gpu_ms, s.ev_start, s.ev_done ) );
   auto h0 = std::chrono::steady_clock::now();
@@ -687,10 +690,8 @@ fd_replay_hip_txn_verify_dev( fd_replay_hip_t * r, ulong n, uchar const * d_pool
                       r->d_msg_sz, r->d_counter, r->d_first, r->d_cnt, r->d_rsig, r->d_rpub, r->d_rmoff, r->d_rmsz,
                       r->rcap );
   TX_CHECK( hipGetLastError() );
-  TX_CHECK( hipMemcpyAsync( r->h_counter, r->d_counter, 4, hipMemcpyDeviceToHost, st ) );
-  TX_CHECK( hipStreamSynchronize( st ) );                 /* the record count sizes the verify launch */
-  ulong nsig = *r->h_counter;
-  fd_ed25519_hip_verify_dev( r->ctx, nsig, r->d_rsig, r->d_rpub, d_pool, r->d_rmoff, r->d_rmsz, r->d_rcode, NULL, st );
+  fd_ed25519_hip_verify_dev_count( r->ctx, 16ul*n, r->d_counter, r->d_rsig, r->d_rpub, d_pool, r->d_rmoff,
+                                   r->d_rmsz, r->d_rcode, NULL, st );
   fd_ed25519_hip_group_reduce_dev( r->ctx, n, r->d_first, r->d_cnt, r->d_rcode, r->d_tcode, st );
   hipLaunchKernelGGL( k_exec_codes, grid, blk, 0, st, n, r->d_tcode, d_result );
   TX_CHECK( hipGetLastError() );

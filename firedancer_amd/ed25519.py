@@ -27,7 +27,7 @@ EXPORTS = (
     "fd_ed25519_verify", "fd_ed25519_verify_batch_single_msg", "fd_ed25519_strerror",
     "fd_ed25519_hip_ctx_new", "fd_ed25519_hip_ctx_delete", "fd_ed25519_hip_ctx_device",
     "fd_ed25519_hip_ctx_stream", "fd_ed25519_hip_set_errmode", "fd_ed25519_hip_verify_dev",
-    "fd_ed25519_hip_verify_fixed_dev",
+    "fd_ed25519_hip_verify_fixed_dev", "fd_ed25519_hip_verify_dev_count",
     "fd_ed25519_hip_verify_host", "fd_ed25519_hip_group_reduce_dev", "fd_ed25519_hip_sign_dev",
     "fd_ed25519_hip_sync", "fd_ed25519_hip_set_timing", "fd_ed25519_hip_get_timing",
     "fd_ed25519_hip_get_dsm_units",
@@ -67,6 +67,8 @@ def lib():
         L.fd_ed25519_hip_verify_dev.argtypes = [vp, u64, vp, vp, vp, vp, vp, vp, vp, vp]
         L.fd_ed25519_hip_verify_fixed_dev.restype = c.c_int
         L.fd_ed25519_hip_verify_fixed_dev.argtypes = [vp, u64, vp, vp, vp, c.c_uint, vp, vp, vp]
+        L.fd_ed25519_hip_verify_dev_count.restype = c.c_int
+        L.fd_ed25519_hip_verify_dev_count.argtypes = [vp, u64, vp, vp, vp, vp, vp, vp, vp, vp, vp]
         L.fd_ed25519_hip_verify_host.restype = c.c_int
         L.fd_ed25519_hip_verify_host.argtypes = [vp, u64, vp, vp, vp, u64, vp, vp, vp, vp]
         L.fd_ed25519_hip_group_reduce_dev.restype = c.c_int
@@ -163,6 +165,12 @@ class Verifier:
     def verify_dev(self, n, sigs, pubs, pool, msg_off, msg_sz, codes, bitmap=None, stream=None):
         return self._lib.fd_ed25519_hip_verify_dev(self.ctx, int(n), _ptr(sigs), _ptr(pubs), _ptr(pool), _ptr(msg_off),
                                                    _ptr(msg_sz), _ptr(codes), _ptr(bitmap), stream)
+
+    def verify_dev_count(self, n_max, d_n, sigs, pubs, pool, msg_off, msg_sz, codes, bitmap=None, stream=None):
+        """verify_dev with the record count in device memory (uint32 *d_n)."""
+        return self._lib.fd_ed25519_hip_verify_dev_count(self.ctx, int(n_max), _ptr(d_n), _ptr(sigs), _ptr(pubs),
+                                                         _ptr(pool), _ptr(msg_off), _ptr(msg_sz), _ptr(codes),
+                                                         _ptr(bitmap), stream)
 
     def verify_fixed_dev(self, n, sigs, pubs, msgs, msg_sz, codes, bitmap=None, stream=None):
         """Fixed-size messages back to back: message i = msgs[i*msg_sz, (i+1)*msg_sz)."""

@@ -120,6 +120,24 @@ fd_ed25519_hip_verify_dev( fd_ed25519_hip_ctx_t * ctx,
                            ulong *                d_bitmap,
                            void *                 stream );
 
+/* Same with the record count in device memory (e.g. written by a preceding
+   kernel): verifies records [0, min(n_max, *d_n)) without a host round trip;
+   codes (and bitmap bits) at or past *d_n are left untouched.  The launch
+   covers n_max records (ceil(n_max/chunk_sigs) chunk launches; threads past
+   the count exit at once). */
+int
+fd_ed25519_hip_verify_dev_count( fd_ed25519_hip_ctx_t * ctx,
+                                 ulong                  n_max,
+                                 uint const *           d_n,
+                                 uchar const *          d_sigs,
+                                 uchar const *          d_pubs,
+                                 uchar const *          d_pool,
+                                 uint const *           d_msg_off,
+                                 uint const *           d_msg_sz,
+                                 signed char *          d_codes,
+                                 ulong *                d_bitmap,
+                                 void *                 stream );
+
 /* Fixed-size messages laid out back to back: message i = d_msgs[ i*msg_sz,
    (i+1)*msg_sz ) (e.g. 32-byte shred Merkle roots, fd_fec_resolver.c:476).
    Same semantics and requirements as fd_ed25519_hip_verify_dev (d_msgs

@@ -64,9 +64,9 @@ void              fd_replay_hip_delete( fd_replay_hip_t * r );
    as the reference returns for transaction j.  signature_cnt 0 or > 16
    fails without reading any signature (fd_ed25519_user.c:238-241).
    d_pool / d_desc / d_result are device pointers; d_pool readable 16 bytes
-   past its last payload.  Returns once the signature records are counted
-   (one 4-byte readback); the verification itself stays asynchronous on
-   stream (NULL: ctx's stream).  Returns 0, or -1 if n > max_txn. */
+   past its last payload.  Asynchronous on stream (NULL: ctx's stream): the
+   signature-record count stays on the device.  Returns 0, or -1 if
+   n > max_txn. */
 int
 fd_replay_hip_txn_verify_dev( fd_replay_hip_t *         r,
                               ulong                     n,

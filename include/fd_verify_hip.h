@@ -107,8 +107,8 @@ int   fd_verify_hip_tcache_insert( ulong * oldest, ulong * ring, ulong depth,
    state and the metrics.  It runs on ctx's device and stream.
 
      submit(k)   enqueues parse, expand, verify and per-txn reduce of batch k
-                 and returns once the GPU has counted k's signatures (so it
-                 also waits for batch k-1's GPU work);
+                 and returns without waiting on the GPU (the signature count
+                 stays on the device and sizes the verify there);
      complete(k) waits for batch k and runs the ordered host pass, writing
                  result[j] (FD_VERIFY_HIP_FRAG_*), tag[j] (opt_sig on
                  publish, else 0) and txn_t_sz[j] (parse footprint).

@@ -141,3 +141,25 @@ def test_fixed_matches_offsets(verifier):
     verifier.sync()
     assert torch.equal(c1, c2)
     assert 0.7 < float((c1 == 0).float().mean()) < 0.9
+
+
+def test_verify_dev_count(verifier):
+    """verify_dev_count: records [0, *d_n) verified exactly as verify_dev,
+    codes past the device-side count untouched; n_max spans three chunks of
+    the fixture's 2^18 (one partial, one empty)."""
+    import torch
+    from firedancer_amd.workload import make_batch_gpu
+    n = (1 << 18) + 4000
+    b = make_batch_gpu(verifier, n, msg_sz=48, seed=91, mix="c2")
+    ref = torch.zeros(n, dtype=torch.int8, device="cuda:0")
+    verifier.verify_dev(n, b.sigs, b.pubs, b.pool, b.msg_off, b.msg_sz, ref)
+    for cnt in (n, (1 << 18) + 17, 1000, 0):
+        d_n = torch.tensor([cnt], dtype=torch.int32, device="cuda:0")
+        codes = torch.full((n,), 5, dtype=torch.int8, device="cuda:0")
+        bm = torch.zeros((n + 63) // 64, dtype=torch.int64, device="cuda:0")
+        verifier.verify_dev_count(3 << 18, d_n, b.sigs, b.pubs, b.pool, b.msg_off, b.msg_sz, codes, bm)
+        verifier.sync()
+        assert torch.equal(codes[:cnt], ref[:cnt]), cnt
+        assert bool((codes[cnt:] == 5).all()), cnt
+        bits = np.unpackbits(bm.cpu().numpy().view(np.uint8), bitorder="little")[:cnt].astype(bool)
+        assert np.array_equal(bits, ref[:cnt].cpu().numpy() == 0), cnt
