@@ -103,6 +103,32 @@ def test_random_mixed_vs_oracle(verifier):
     assert _bitmap_ok(codes, bitmap)
 
 
+def test_random_bytes_vs_oracle(verifier):
+    """fuzz_ed25519_verify.c:33-48 shape: uniformly random sig/pub/msg must
+    not verify; codes (both error modes) equal the oracle's.  Half the S
+    halves are forced < L so decode and the equation are reached too, and a
+    quarter of the keys are valid points (the A decode succeeds)."""
+    rng = np.random.default_rng(0xf022)
+    n = 8192
+    sigs = rng.integers(0, 256, (n, 64), dtype=np.uint8)
+    pubs = rng.integers(0, 256, (n, 32), dtype=np.uint8)
+    sigs[: n // 2, 63] &= 0x0f                                   # S < 2^252 < L
+    good = O.sign_many(rng.integers(0, 256, (n // 4, 32), dtype=np.uint8), np.zeros(17, np.uint8),
+                       np.zeros(n // 4, np.uint32), np.zeros(n // 4, np.uint32))[0]
+    pubs[::4] = good
+    msz = rng.integers(0, 300, n).astype(np.uint32)
+    moff = np.concatenate([[0], np.cumsum(msz)[:-1]]).astype(np.uint32)
+    pool = rng.integers(0, 256, int(msz.sum()) + 1, dtype=np.uint8)
+    for mode in (O.ERRMODE_AVX512, O.ERRMODE_REF):
+        verifier.set_errmode(mode)
+        codes, bitmap = verifier.verify_host(sigs, pubs, pool, moff, msz)
+        exp = O.verify_many(sigs, pubs, pool, moff, msz, mode)
+        assert np.array_equal(codes, exp)
+        assert (codes != 0).all() and _bitmap_ok(codes, bitmap)
+    verifier.set_errmode(O.ERRMODE_AVX512)
+    assert len(set(codes.tolist())) >= 3
+
+
 def test_chunking_and_ragged(kat):
     """n not a multiple of 64, several chunks per call, empty call."""
     from firedancer_amd import Verifier
