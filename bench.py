@@ -121,6 +121,7 @@ def main():
                          "groups of 16; c4 synthetic txn stream through the verify tile (GPU parse + verify + "
                          "host tcache dedup); c5 2^26 C2-mix signatures in total, sharded (strong scaling)")
     ap.add_argument("--txns", type=int, default=1 << 19, help="c4: frags per batch per GPU")
+    ap.add_argument("--tiles", type=int, default=8, help="c4: verify tiles (host threads + contexts) per GPU")
     ap.add_argument("--sigs", type=int, default=None, help="override signatures per GPU per step")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--cpu-seconds", type=float, default=8.0)
@@ -319,49 +320,75 @@ def run_c4(args, rank, world, local, dist):
     """Config 4: synthetic Solana txn stream through the verify tile.
 
     A step is one batch of --txns frags (raw payloads resident in HBM) through
-    fd_verify_hip_tile: GPU parse + sig0 tag + record expansion + verify +
-    per-txn batch_single_msg reduce, then the ordered host pass (tcache dedup,
-    depth 4194302 = the reference default signature_cache_size, and the
-    bundle state).  Batches are submitted one ahead, so the host pass of batch
-    k overlaps the GPU work of batch k+1 (the pipelined steady state of a
-    GPU verify tile).  Each step re-keys the dedup hash so the replayed batch
-    is new traffic to the tcache; in-batch resends still dedup.
-    value = signatures verified per second (all ranks)."""
+    --tiles GPU verify tiles (fd_verify_hip_tile) sharing the GPU, the frags
+    split round robin between them as the reference splits them between its
+    verify tiles (fd_verify_tile.c before_frag: seq % round_robin_cnt).  Each
+    tile owns a context (stream), a tcache of depth 4194302 (the reference
+    default signature_cache_size) and a host thread, and runs GPU parse + sig0
+    tag + record expansion + verify + per-txn batch_single_msg reduce, then
+    the ordered host pass (tcache dedup, bundle state).  Batches are submitted
+    one ahead, so a tile's host pass of batch k overlaps the GPU work of batch
+    k+1.  Each step re-keys the dedup hash so the replayed batch is new traffic
+    to the tcache (once a tcache is full every insert also evicts, the steady
+    state of a long-running tile); in-batch resends still dedup.
+    value = signatures verified per second (all tiles, all ranks)."""
+    import threading
+
     import torch
     from firedancer_amd import Verifier
     from firedancer_amd.txn_workload import gpu_signer, make_txn_stream
     from firedancer_amd.verify_tile import VerifyTile
+    T = max(1, args.tiles)
     v = Verifier(device=local, chunk_sigs=1 << 20)
     seed_base = 0x7f4a11 + 104729 * rank
     s = make_txn_stream(args.txns, gpu_signer(v), seed=0x5eed0004 + 7919 * rank)
     dev = torch.device("cuda", local)
     d_pool = torch.from_numpy(s.pool).to(dev)
-    d_off = torch.from_numpy(s.off.view(np.int32)).to(dev)
-    d_sz = torch.from_numpy(s.sz.view(np.int16)).to(dev)
     depth = 4194302
-    tile = VerifyTile(v, max_txn=s.n, hashmap_seed=seed_base, tcache_depth=depth)
-    k_step = [0]
+    vs = [v] + [Verifier(device=local, chunk_sigs=1 << 16) for _ in range(T - 1)]
+    parts = []
+    for t in range(T):
+        sel = np.arange(t, s.n, T)
+        parts.append((int(sel.size), torch.from_numpy(np.ascontiguousarray(s.off[sel]).view(np.int32)).to(dev),
+                      torch.from_numpy(np.ascontiguousarray(s.sz[sel]).view(np.int16)).to(dev)))
+    tiles = [VerifyTile(vs[t], max_txn=parts[t][0], hashmap_seed=seed_base, tcache_depth=depth) for t in range(T)]
+    k_step = [0] * T
+    diag = os.environ.get("FD_C4_DIAG")
 
-    def submit():
-        tile.set_seed(seed_base + k_step[0]); k_step[0] += 1
-        tile.submit(s.n, d_pool, d_off, d_sz)
+    def submit(t):
+        tiles[t].set_seed(seed_base + 7 * k_step[t]); k_step[t] += 1
+        tiles[t].submit(parts[t][0], d_pool, parts[t][1], parts[t][2])
 
-    def run(steps):
-        outs, gpu_ms, host_ms = [], [], []
-        submit()
+    def tile_loop(t, steps, outs, gpu_ms, host_ms):
+        submit(t)
         for k in range(steps):
             if k + 1 < steps:
-                submit()
-            outs.append(tile.complete())
-            t = tile.last_timing(); gpu_ms.append(t["gpu_ms"]); host_ms.append(t["host_ms"])
+                submit(t)
+            outs[t].append(tiles[t].complete())
+            lt = tiles[t].last_timing(); gpu_ms[t].append(lt["gpu_ms"]); host_ms[t].append(lt["host_ms"])
+            if diag:
+                print(f"c4 tile {t} step {k}: gpu batch {lt['gpu_ms']:.3f} ms, host pass {lt['host_ms']:.3f} ms",
+                      file=sys.stderr)
+
+    def run(steps):
+        outs, gpu_ms, host_ms = [[] for _ in range(T)], [[] for _ in range(T)], [[] for _ in range(T)]
+        th = [threading.Thread(target=tile_loop, args=(t, steps, outs, gpu_ms, host_ms)) for t in range(T)]
+        for x in th:
+            x.start()
+        for x in th:
+            x.join()
         return outs, gpu_ms, host_ms
+
+    def metrics():
+        ms = [tl.metrics() for tl in tiles]
+        return {k: sum(m[k] for m in ms) for k in ms[0]}
 
     run(max(args.warmup, 1))
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
-    m0 = tile.metrics()
+    m0 = metrics()
     t0 = time.perf_counter()
     outs, gpu_ms, host_ms = run(args.steps)
     torch.cuda.synchronize()
@@ -369,7 +396,7 @@ def run_c4(args, rank, world, local, dist):
         dist.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
-    m1 = tile.metrics()
+    m1 = metrics()
     sigs = m1["sigs"] - m0["sigs"]
     frags = s.n * args.steps
     if dist:
@@ -379,14 +406,15 @@ def run_c4(args, rank, world, local, dist):
         tt = torch.tensor([sigs, frags], dtype=torch.int64, device=dev)
         dist.all_reduce(tt)
         sigs, frags = int(tt[0].item()), int(tt[1].item())
-    res = outs[-1][0]
-    # kernel roofline: one extra (untimed) batch with per-kernel HIP-event timing
+    res = np.concatenate([o[-1][0] for o in outs])
+    gpu_ms = [x for g in gpu_ms for x in g]; host_ms = [x for h in host_ms for x in h]
+    # kernel roofline: one extra (untimed) batch of tile 0 with per-kernel HIP-event timing
     v.set_timing(True)
-    submit(); tile.complete()
+    submit(0); tiles[0].complete()
     prep_ms, dsm_ms, launches = v.get_timing()
     dsm_units = v.get_dsm_units()
     v.set_timing(False)
-    n_sig_batch = int(tile.last_timing()["sigs"])
+    n_sig_batch = int(m1["sigs"] - m0["sigs"]) // max(args.steps, 1)
     launches = max(launches, 1)
     out = None
     if rank == 0:
@@ -416,9 +444,10 @@ def run_c4(args, rank, world, local, dist):
             "data": "synthetic txn stream (repo generator, GPU-signed, C2 mutation per signature, "
                     "1% resends, 0.1% grafted sig0, 0.5% malformed)",
             "config": {"workload": f"config 4: {s.n} frags/GPU/batch ({n_sig_batch} signatures), legacy+v0 txns "
-                                   f"1-12 sigs, <=1232 B, GPU fd_txn_parse, tcache dedup depth {depth}",
-                       "config_id": "c4", "frags_per_gpu": s.n, "sigs_per_batch": n_sig_batch,
-                       "parallelism": f"dp{world} (frag shards, one verify tile per GPU)"},
+                                   f"1-12 sigs, <=1232 B, GPU fd_txn_parse, {T} verify tiles (round robin), "
+                                   f"tcache dedup depth {depth} each",
+                       "config_id": "c4", "frags_per_gpu": s.n, "sigs_per_batch": n_sig_batch, "verify_tiles": T,
+                       "parallelism": f"dp{world} (frag shards; {T} verify tiles per GPU)"},
             "frags_per_s": round(frags / elapsed, 1),
             "frag_outcomes_last_batch": {names[k]: v_ for k, v_ in counts.items()},
             "batch_gpu_ms": round(float(np.median(gpu_ms)), 4),
@@ -432,8 +461,10 @@ def run_c4(args, rank, world, local, dist):
             "cpu_baseline": cpu,
         }
         emit(out)
-    tile.close()
-    v.close()
+    for tl in tiles:
+        tl.close()
+    for x in vs:
+        x.close()
     if dist:
         dist.barrier()
         dist.destroy_process_group()

@@ -514,6 +514,19 @@ fd_ed25519_hip_ctx_new( int device, ulong chunk_sigs ) {
   return ctx;
 }
 
+void
+fd_ed25519_hip_ctx_reserve( fd_ed25519_hip_ctx_t * ctx, ulong chunk_sigs ) {
+  chunk_sigs = (chunk_sigs + 255UL) & ~255UL;
+  if( chunk_sigs <= ctx->chunk ) return;
+  FD_CHECK( hipSetDevice( ctx->device ) );
+  FD_CHECK( hipDeviceSynchronize() );                      /* the scratch may be in use on any stream */
+  (void)hipFree( ctx->d_state ); (void)hipFree( ctx->d_atab ); (void)hipFree( ctx->d_idx );
+  FD_CHECK( hipMalloc( (void **)&ctx->d_state, (size_t)ST_WORDS * chunk_sigs * sizeof(u32) ) );
+  FD_CHECK( hipMalloc( (void **)&ctx->d_atab,  (size_t)ATAB_WORDS * chunk_sigs * sizeof(u32) ) );
+  FD_CHECK( hipMalloc( (void **)&ctx->d_idx, chunk_sigs * sizeof(u32) ) );
+  ctx->chunk = chunk_sigs;
+}
+
 static void free_staging( fd_ed25519_hip_ctx_t * ctx ) {
   (void)hipFree( ctx->d_sigs ); (void)hipFree( ctx->d_pubs ); (void)hipFree( ctx->d_pool ); (void)hipFree( ctx->d_moff );
   (void)hipFree( ctx->d_msz ); (void)hipFree( ctx->d_codes ); (void)hipFree( ctx->d_bitmap );

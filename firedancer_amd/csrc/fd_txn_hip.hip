@@ -458,6 +458,7 @@ fd_verify_hip_tile_new( fd_ed25519_hip_ctx_t * ctx, ulong max_txn, ulong seed, u
   if( !map_cnt ) map_cnt = fd_verify_hip_tcache_map_cnt_default( depth );
   if( !map_cnt || (map_cnt & (map_cnt - 1)) || map_cnt < depth + 2 ) return 0;
   TX_CHECK( hipSetDevice( fd_ed25519_hip_ctx_device( ctx ) ) );
+  fd_ed25519_hip_ctx_reserve( ctx, 12ul*max_txn );        /* one verify launch pair per batch */
   fd_verify_hip_tile_t * t = (fd_verify_hip_tile_t *)calloc( 1, sizeof(fd_verify_hip_tile_t) );
   t->ctx = ctx; t->max_txn = max_txn; t->seed = seed;
   t->own_mem = (ulong *)malloc( sizeof(ulong)*(depth + map_cnt) );
@@ -647,6 +648,7 @@ extern "C" fd_replay_hip_t *
 fd_replay_hip_new( fd_ed25519_hip_ctx_t * ctx, ulong max_txn ) {
   if( !ctx || !max_txn ) return 0;
   TX_CHECK( hipSetDevice( fd_ed25519_hip_ctx_device( ctx ) ) );
+  fd_ed25519_hip_ctx_reserve( ctx, 16ul*max_txn );
   fd_replay_hip_t * r = (fd_replay_hip_t *)calloc( 1, sizeof(fd_replay_hip_t) );
   ulong n = max_txn, rc = 16ul*max_txn;                    /* at most 16 records per txn */
   r->ctx = ctx; r->max_txn = n; r->rcap = rc;

@@ -26,7 +26,7 @@ ERRMODE_REF = 1
 EXPORTS = (
     "fd_ed25519_verify", "fd_ed25519_verify_batch_single_msg", "fd_ed25519_strerror",
     "fd_ed25519_hip_ctx_new", "fd_ed25519_hip_ctx_delete", "fd_ed25519_hip_ctx_device",
-    "fd_ed25519_hip_ctx_stream", "fd_ed25519_hip_set_errmode", "fd_ed25519_hip_verify_dev",
+    "fd_ed25519_hip_ctx_stream", "fd_ed25519_hip_ctx_reserve", "fd_ed25519_hip_set_errmode", "fd_ed25519_hip_verify_dev",
     "fd_ed25519_hip_verify_fixed_dev", "fd_ed25519_hip_verify_dev_count",
     "fd_ed25519_hip_verify_host", "fd_ed25519_hip_group_reduce_dev", "fd_ed25519_hip_sign_dev",
     "fd_ed25519_hip_sync", "fd_ed25519_hip_set_timing", "fd_ed25519_hip_get_timing",
@@ -63,6 +63,7 @@ def lib():
         L.fd_ed25519_hip_ctx_stream.restype = vp
         L.fd_ed25519_hip_ctx_stream.argtypes = [vp]
         L.fd_ed25519_hip_set_errmode.argtypes = [vp, c.c_int]
+        L.fd_ed25519_hip_ctx_reserve.argtypes = [vp, u64]
         L.fd_ed25519_hip_verify_dev.restype = c.c_int
         L.fd_ed25519_hip_verify_dev.argtypes = [vp, u64, vp, vp, vp, vp, vp, vp, vp, vp]
         L.fd_ed25519_hip_verify_fixed_dev.restype = c.c_int
