@@ -121,6 +121,8 @@ def main():
                          "groups of 16; c4 synthetic txn stream through the verify tile (GPU parse + verify + "
                          "host tcache dedup); c5 2^26 C2-mix signatures in total, sharded (strong scaling)")
     ap.add_argument("--txns", type=int, default=1 << 19, help="c4: frags per batch per GPU")
+    ap.add_argument("--contexts", type=int, default=1,
+                    help="c1/c2/c3/c5: verify contexts (streams) each step is split over (measured: 1-3 equal, 4+ slower)")
     ap.add_argument("--tiles", type=int, default=8, help="c4: verify tiles (host threads + contexts) per GPU")
     ap.add_argument("--sigs", type=int, default=None, help="override signatures per GPU per step")
     ap.add_argument("--cpu-threads", type=int, default=16)
@@ -158,41 +160,70 @@ def main():
     else:
         n = args.sigs or ((1 << 22) if cfg == "c3" else (1 << 20))
     chunk = min(n, 1 << 20)
-    v = Verifier(device=local, chunk_sigs=chunk)
+    v = Verifier(device=local, chunk_sigs=chunk)      # signs the batch; runs the roofline leg
     batch = make_batch_gpu(v, n, msg_sz=msg_sz, seed=0x5eed0001 + 7919 * rank, mix=mix, shared_msg=(cfg == "c3"))
     dev = batch.dev
     codes = torch.zeros(n, dtype=torch.int8, device=dev)
     bitmap = torch.zeros((n + 63) // 64, dtype=torch.int64, device=dev)
-    groups = None
-    if cfg == "c3":   # fd_ed25519_verify_batch_single_msg in chunks of 16 (fd_ed25519_user.c:238-241)
-        ng = (n + 15) // 16
-        first = torch.arange(ng, dtype=torch.int32, device=dev) * 16
-        cnt = torch.clamp(n - first, max=16).to(torch.uint8)
-        gcodes = torch.zeros(ng, dtype=torch.int8, device=dev)
-        groups = (ng, first, cnt, gcodes)
+    gcodes = torch.zeros((n + 15) // 16, dtype=torch.int8, device=dev)
 
-    def step():
-        v.verify_dev(n, batch.sigs, batch.pubs, batch.pool, batch.msg_off, batch.msg_sz, codes, bitmap)
-        if groups:
-            v.group_reduce_dev(groups[0], groups[1], groups[2], codes, groups[3])
+    # Each step's batch is split over C verify contexts (one HIP stream each),
+    # as the reference spreads a stream of transactions over several verify
+    # tiles: with no synchronisation between steps, one context's prep runs in
+    # the issue slots another's k_verify_dsm leaves idle in its last partial
+    # round of workgroups.  Slices are multiples of 256 signatures (whole
+    # bitmap words and whole 16-signature groups).
+    C = max(1, args.contexts)
+    per = ((n + C - 1) // C + 255) // 256 * 256
+    slices = [(lo, min(n, lo + per)) for lo in range(0, n, per)]
+    ctxs = [Verifier(device=local, chunk_sigs=min(hi - lo, 1 << 20)) for lo, hi in slices]
+
+    def groups_of(lo, hi):   # fd_ed25519_verify_batch_single_msg in chunks of 16 (fd_ed25519_user.c:238-241)
+        ng = (hi - lo + 15) // 16
+        first = torch.arange(ng, dtype=torch.int32, device=dev) * 16
+        cnt = torch.clamp((hi - lo) - first, max=16).to(torch.uint8)
+        return ng, first, cnt, gcodes[lo // 16:lo // 16 + ng]
+
+    jobs = [(vv, lo, hi, groups_of(lo, hi) if cfg == "c3" else None) for vv, (lo, hi) in zip(ctxs, slices)]
+    whole = [(v, 0, n, groups_of(0, n) if cfg == "c3" else None)]
+
+    def step(jl):
+        for vv, lo, hi, g in jl:
+            vv.verify_dev(hi - lo, batch.sigs[lo:hi], batch.pubs[lo:hi], batch.pool, batch.msg_off[lo:hi],
+                          batch.msg_sz[lo:hi], codes[lo:hi], bitmap[lo // 64:(hi + 63) // 64])
+            if g:
+                vv.group_reduce_dev(g[0], g[1], g[2], codes[lo:hi], g[3])
+
+    def sync_all():
+        for vv in ctxs + [v]:
+            vv.sync()
+        torch.cuda.synchronize()
 
     for _ in range(args.warmup):
-        step()
-    v.sync(); torch.cuda.synchronize()
+        step(jobs)
+    sync_all()
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
-    v.set_timing(True)
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        step()
-    v.sync(); torch.cuda.synchronize()
+        step(jobs)
+    sync_all()
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
     t1 = time.perf_counter()
+    timed_codes, timed_gcodes = codes.clone(), gcodes.clone()
+    # roofline leg: the whole batch through one context with HIP events around
+    # every launch (timing mode), so each k_verify_dsm runs alone on the GPU;
+    # its verdicts must equal the timed multi-context steps'
+    v.set_timing(True)
+    for _ in range(max(1, min(args.steps, 3))):
+        step(whole)
+    sync_all()
     prep_ms, dsm_ms, launches = v.get_timing()
     v.set_timing(False)
+    assert torch.equal(codes, timed_codes) and torch.equal(gcodes, timed_gcodes), "contexts != whole batch"
     elapsed = t1 - t0
     if dist:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
@@ -266,14 +297,17 @@ def main():
                            "c3": f"config 3: one 32-B msg x {n} keys/GPU, batch_single_msg groups of 16",
                            "c5": f"config 5: {n_all} C2-mix sigs total, {n} on rank 0"}[cfg],
                        "config_id": cfg, "sigs_per_gpu": n, "msg_sz": msg_sz,
-                       "parallelism": f"dp{world} (signature shards)"},
+                       "parallelism": f"dp{world} (signature shards)",
+                       "verify_contexts": len(ctxs)},
             "accept_rate": round(accept, 5),
             "roofline": {"bound": "valu_int32", "kernel": "k_verify_dsm",
                          "achieved": round(achieved, 3), "peak": round(peak, 3), "unit": "Tops/s",
                          "frac": round(achieved / peak, 4), "traffic": traffic, "traffic_unit": "bytes/launch",
                          "traffic_source": traffic_src,
                          "algorithmic_ops_per_unit": round(W_DSM), "units_per_launch": round(units_per_launch),
-                         "avg_launch_ms": round(dsm_avg_ms, 4)},
+                         "avg_launch_ms": round(dsm_avg_ms, 4),
+                         "timing_leg": "after the timed steps: the whole batch through one context, HIP events "
+                                       "around each launch, each k_verify_dsm alone on the GPU"},
             "pipeline": {"prep_ms": round(prep_avg_ms, 4), "dsm_ms": round(dsm_avg_ms, 4),
                          "w_total_per_verify": round(w_total(msg_sz)),
                          "int32_valu_frac": round(pipeline_frac, 4),
@@ -281,7 +315,8 @@ def main():
             "cpu_baseline": cpu,
         }
         emit(out)
-    v.close()
+    for vv in ctxs + [v]:
+        vv.close()
     if dist:
         dist.barrier()
         dist.destroy_process_group()
