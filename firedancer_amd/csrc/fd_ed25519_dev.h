@@ -515,6 +515,212 @@ DEV void sc_recode256( u32 out[8], u32 const s[8] ) {
   }
 }
 
+/* Signed radix-16 digits in [-7,8] of k < 2^252 packed (biased by 7) 8 per
+   u32: nibble i of out[i/8] = d_i + 7.  With digit 8 allowed, a k of b bits
+   has all digits from floor(b/4)+1 up zero (the carry out of the top nibble
+   needs it >= 8 plus a carry in, i.e. b % 4 == 0). */
+DEV void sc_recode16s( u32 out[8], u32 const k[8] ) {
+  u32 carry = 0;
+  #pragma unroll
+  for( int w=0; w<8; w++ ) {
+    u32 o = 0;
+    #pragma unroll
+    for( int n=0; n<8; n++ ) {
+      u32 d = ((k[w] >> (4*n)) & 15u) + carry;
+      carry = (d + 7u) >> 4;               /* d >= 9 */
+      d = d + 7u - (carry << 4);
+      o |= d << (4*n);
+    }
+    out[w] = o;
+  }
+}
+
+/* ---- multiword integers, little-endian u32 words ---- */
+
+DEV u32 mw_sel( u32 m, u32 a, u32 b ) { return (a & m) | (b & ~m); }   /* m ? a : b, m 0 or ~0 */
+
+/* o = a - q*b mod 2^(32N); returns 1 when a < q*b (a, b unsigned, the
+   difference above -2^(32N)) */
+template<int N>
+DEV u32 mw_submul( u32 o[N], u32 const a[N], u32 const b[N], u32 q ) {
+  u32 c = 0, bw = 0;
+  #pragma unroll
+  for( int i=0; i<N; i++ ) {
+    u64 p = (u64)b[i] * q + c; c = (u32)(p >> 32);
+    u64 d = (u64)a[i] - (u32)p - bw; o[i] = (u32)d; bw = (u32)(d >> 32) & 1u;
+  }
+  return (c | bw) != 0u;
+}
+template<int N>
+DEV void mw_add( u32 o[N], u32 const a[N], u32 const b[N] ) {
+  u64 c = 0;
+  #pragma unroll
+  for( int i=0; i<N; i++ ) { c += (u64)a[i] + b[i]; o[i] = (u32)c; c >>= 32; }
+}
+template<int N>
+DEV u32 mw_sub( u32 o[N], u32 const a[N], u32 const b[N] ) {   /* returns the borrow (a < b unsigned) */
+  u32 bw = 0;
+  #pragma unroll
+  for( int i=0; i<N; i++ ) { u64 d = (u64)a[i] - b[i] - bw; o[i] = (u32)d; bw = (u32)(d >> 32) & 1u; }
+  return bw;
+}
+template<int N>
+DEV void mw_cneg( u32 x[N], u32 m ) {       /* x = m ? -x : x (two's complement), m 0 or ~0 */
+  u64 c = m & 1u;
+  #pragma unroll
+  for( int i=0; i<N; i++ ) { c += (u64)(x[i] ^ m); x[i] = (u32)c; c >>= 32; }
+}
+template<int N>
+DEV u32 mw_bitlen( u32 const x[N] ) {       /* unsigned bit length */
+  u32 b = 0;
+  #pragma unroll
+  for( int i=0; i<N; i++ ) b = x[i] ? 32u*(u32)i + 32u - (u32)__builtin_clz( x[i] ) : b;
+  return b;
+}
+template<int N>
+DEV u32 mw_abs_bitlen( u32 const x[N] ) {   /* bit length of |x|, x two's complement */
+  u32 a[N];
+  #pragma unroll
+  for( int i=0; i<N; i++ ) a[i] = x[i];
+  mw_cneg<N>( a, (u32)((int)x[N-1] >> 31) );
+  return mw_bitlen<N>( a );
+}
+DEV double mw_to_f64( u32 const a[8] ) {   /* approximation, relative error < 2^-49 */
+  double d = (double)a[7];
+  #pragma unroll
+  for( int i=6; i>=0; i-- ) d = fma( d, 4294967296.0, (double)a[i] );
+  return d;
+}
+
+/* r = a*b mod L for a, b < 2^256 */
+DEV void sc_mul( u32 r[8], u32 const a[8], u32 const b[8] ) {
+  u32 prod[16];
+  u64 lo = 0, hi = 0;
+  #pragma unroll
+  for( int c=0; c<16; c++ ) {
+    #pragma unroll
+    for( int i=0; i<8; i++ ) {
+      int j = c - i; if( j < 0 || j > 7 ) continue;
+      u64 p = (u64)a[i] * b[j]; lo += p; hi += (lo < p) ? 1u : 0u;
+    }
+    prod[c] = (u32)lo; lo = (lo >> 32) | (hi << 32); hi >>= 32;
+  }
+  sc_reduce512( r, prod );
+}
+
+/* ---- half-size scalars -------------------------------------------------
+
+   For k < L find k1, k2 with k1 == k*k2 (mod 8L), k2 odd and 0 < k2 < L,
+   both near 2^128.  Then with D = [S]B - [k]A - R (the point whose being
+   the identity is the reference's accept condition, fd_ed25519_user.c:
+   216-226):
+
+     [k2]D = [k2*S mod L]B - [k1]A - [k2]R
+
+   (B has order L; A and R lie in the group of order 8L, so k2*k may be
+   replaced by anything congruent to it mod 8L), and [k2]D == O iff D == O
+   since k2 is prime to 8L.  The cofactorless verdict is unchanged bit for
+   bit, while the double-scalar multiplication needs ~128 doublings instead
+   of ~252.  The technique is the half-size-scalar EdDSA verification of
+   T. Pornin, "Optimized Lattice Basis Reduction In Dimension 2, and Fast
+   Schnorr and EdDSA Signature Verification" (IACR eprint 2020/454); the
+   reduction here is truncated Euclid on (8L, k) with cofactors (remainder
+   r_i == k*t_i mod 8L), float-estimated 32-bit quotients corrected exactly,
+   stopped when the remainder falls below 2^128; the result is the shortest
+   odd-t vector among three consecutive (r_i, t_i) and their sums and
+   differences.  A lane that meets a quotient >= 2^32 (probability ~2^-30
+   for a hashed k) keeps the full-length pair (k, 1).  tools/halfsize_model.py
+   models it.
+
+   Out: k1 = |k1| (< 2^251), k1neg = k1 < 0 (0 or ~0), k2 > 0 (< 2^160);
+   returns max(bitlen k1, bitlen k2). */
+DEV void hs_pick( u32 br[9], u32 bt[5], u32 & bc, u32 const r[9], u32 const t[5] ) {
+  u32 c = max( mw_abs_bitlen<9>( r ), mw_abs_bitlen<5>( t ) ) | ((~t[0] & 1u) << 10);   /* even t: 1024+ */
+  u32 take = c < bc ? ~0u : 0u;
+  #pragma unroll
+  for( int i=0; i<9; i++ ) br[i] = mw_sel( take, r[i], br[i] );
+  #pragma unroll
+  for( int i=0; i<5; i++ ) bt[i] = mw_sel( take, t[i], bt[i] );
+  bc = mw_sel( take, c, bc );
+}
+DEV void hs_pick2( u32 br[9], u32 bt[5], u32 & bc, u32 const ra[9], u32 const ta[5], u32 const rb[9],
+                   u32 const tb[5] ) {
+  u32 r[9], t[5];
+  mw_add<9>( r, ra, rb ); mw_add<5>( t, ta, tb ); hs_pick( br, bt, bc, r, t );
+  mw_sub<9>( r, ra, rb ); mw_sub<5>( t, ta, tb ); hs_pick( br, bt, bc, r, t );
+}
+
+DEV u32 sc_halfsize( u32 k1[8], u32 & k1neg, u32 k2[8], u32 const k[8] ) {
+  u32 rp[8] = { 0xe7ae9f68u,0xc09318d2u,0x17bce6b2u,0xa6f7cef5u,0u,0u,0u,0x80000000u };   /* 8L */
+  u32 rc[8], tp[5] = { 0u,0u,0u,0u,0u }, tc[5] = { 1u,0u,0u,0u,0u };
+  #pragma unroll
+  for( int i=0; i<8; i++ ) rc[i] = k[i];
+  double dp = mw_to_f64( rp ), dc = mw_to_f64( rc );
+  bool fb = false;
+  #pragma unroll 1
+  for( int it=0; (rc[4] | rc[5] | rc[6] | rc[7]) != 0u; it++ ) {   /* while r_c >= 2^128 */
+    double qd = floor( dp / dc );
+    if( qd >= 4294967296.0 || it >= 512 ) { fb = true; break; }
+    u32 q = (u32)qd;
+    u32 rn[8], tn[5];
+    u32 neg = mw_submul<8>( rn, rp, rc, q );
+    mw_submul<5>( tn, tp, tc, q );
+    if( neg ) { mw_add<8>( rn, rn, rc ); mw_add<5>( tn, tn, tc ); }   /* estimate one too high */
+    u32 tmp[8];
+    u32 lt = 0u - mw_sub<8>( tmp, rn, rc );      /* ~0: r_n < r_c, swap; else the estimate
+                                                    was one too low: keep r_c */
+    double dn = mw_to_f64( rn );
+    /* selects as masks (v_bfi_b32), not v_cndmask */
+    #pragma unroll
+    for( int i=0; i<8; i++ ) { u32 a = mw_sel( lt, rc[i], rn[i] ); rc[i] = mw_sel( lt, rn[i], rc[i] ); rp[i] = a; }
+    #pragma unroll
+    for( int i=0; i<5; i++ ) { u32 a = mw_sel( lt, tc[i], tn[i] ); tc[i] = mw_sel( lt, tn[i], tc[i] ); tp[i] = a; }
+    u64 m64 = ((u64)lt << 32) | lt;
+    u64 bc_ = (u64)__double_as_longlong( dc ), bn = (u64)__double_as_longlong( dn );
+    dp = __longlong_as_double( (long long)((bc_ & m64) | (bn & ~m64)) );
+    dc = __longlong_as_double( (long long)((bn & m64) | (bc_ & ~m64)) );
+  }
+  u32 bc = 999u, br[9], bt[5];
+  #pragma unroll
+  for( int i=0; i<9; i++ ) br[i] = 0u;
+  #pragma unroll
+  for( int i=0; i<5; i++ ) bt[i] = 0u;
+  if( !fb ) {
+    /* one more Euclid step (q = 0 when r_c == 0 or q >= 2^30: v2 then
+       repeats v0).  |t_c| <= 8L/r_p <= 2^128, so q < 2^30 keeps |t_n| below
+       2^159, inside the 5-word two's complement cofactors. */
+    u32 rn[8], tn[5];
+    double qd = floor( dp / dc );
+    bool ok = (rc[0] | rc[1] | rc[2] | rc[3]) != 0u && qd < 1073741824.0;
+    u32 q = ok ? (u32)qd : 0u;
+    u32 neg = mw_submul<8>( rn, rp, rc, q );
+    mw_submul<5>( tn, tp, tc, q );
+    if( neg ) { mw_add<8>( rn, rn, rc ); mw_add<5>( tn, tn, tc ); }
+    u32 v0[9], v1[9], v2[9];
+    #pragma unroll
+    for( int i=0; i<8; i++ ) { v0[i] = rp[i]; v1[i] = rc[i]; v2[i] = rn[i]; }
+    v0[8] = v1[8] = v2[8] = 0u;
+    hs_pick( br, bt, bc, v0, tp ); hs_pick( br, bt, bc, v1, tc ); hs_pick( br, bt, bc, v2, tn );
+    hs_pick2( br, bt, bc, v0, tp, v1, tc );
+    hs_pick2( br, bt, bc, v0, tp, v2, tn );
+    hs_pick2( br, bt, bc, v1, tc, v2, tn );
+  }
+  if( bc > 250u ) {                           /* fallback: (k, 1) */
+    #pragma unroll
+    for( int i=0; i<8; i++ ) br[i] = k[i];
+    br[8] = 0u;
+    bt[0] = 1u; bt[1] = bt[2] = bt[3] = bt[4] = 0u;
+    bc = mw_bitlen<8>( k );
+  }
+  u32 tneg = (u32)((int)bt[4] >> 31);         /* make k2 > 0: negate the pair */
+  mw_cneg<9>( br, tneg ); mw_cneg<5>( bt, tneg );
+  k1neg = (u32)((int)br[8] >> 31);
+  mw_cneg<9>( br, k1neg );
+  #pragma unroll
+  for( int i=0; i<8; i++ ) { k1[i] = br[i]; k2[i] = i < 5 ? bt[i] : 0u; }
+  return bc;
+}
+
 /**********************************************************************/
 /* SHA-512 (fd_sha512.c:264-399 semantics), one message per lane.      */
 

@@ -48,9 +48,10 @@
 
 #define BTAB_N      129            /* 0..128 multiples of B */
 #define BTAB_STRIDE 28             /* affine cached (1/2-scaled): YmX, YpX, T2d (9 limbs each) + pad */
-#define BTAB_WORDS  (BTAB_N*BTAB_STRIDE)
+#define BTAB_WORDS  (BTAB_N*BTAB_STRIDE)   /* one table; d_btab holds [j]B then [j](2^128 B) */
 #define ATAB_ENT    36             /* cached: YmX, YpX, T2d, Z2 (9 limbs each) */
-#define ATAB_WORDS  (9*ATAB_ENT)   /* per lane: [0..8](-A) */
+#define RTAB_OFF    (9*ATAB_ENT)   /* per lane: [0..8](+-A), then [0..8](-R) */
+#define ATAB_WORDS  (2*RTAB_OFF)
 
 /* state record: 32 u32 words per field group, laid out SoA per chunk for
    coalescing: word w of signature i lives at st[ w*chunk + i ]. */
@@ -113,20 +114,26 @@ DEV void ge_to_affc_half( ge_affc & a, ge_p3 const & p ) {
   fe_canon( a.YmX, a.YmX ); fe_canon( a.YpX, a.YpX ); fe_canon( a.T2d, t );
 }
 
-/* j*B for j in [0,128] in affine cached form (the reference's verify uses a
-   128-entry odd-multiple B table, fd_curve25519_table_ref.c:32; ours holds
-   all multiples 0..128 for signed radix-256 windows). */
+/* j*B for j in [0,128] in affine cached form, then j*(2^128 B) (the
+   reference's verify uses a 128-entry odd-multiple B table,
+   fd_curve25519_table_ref.c:32; ours holds all multiples 0..128 for signed
+   radix-256 windows, and a second table for the high half of the
+   half-size-scalar B coefficient, see sc_halfsize). */
 __global__ __launch_bounds__(64) void k_btab_init( u32 * btab ) {
   int j = blockIdx.x * blockDim.x + threadIdx.x;
-  if( j >= BTAB_N ) return;
+  if( j >= 2*BTAB_N ) return;
+  u32 * e = btab + j*BTAB_STRIDE;
   ge_p3 B, P; ge_base( B ); ge_identity( P );
+  if( j >= BTAB_N ) {
+    j -= BTAB_N;
+    for( int q=0; q<128; q++ ) ge_dbl( B, B, true );
+  }
   ge_cached Bc; ge_to_cached( Bc, B );
   for( int bit=7; bit>=0; bit-- ) {
     ge_dbl( P, P, true );
     if( (j >> bit) & 1 ) ge_add_cached( P, P, Bc, 0u, true );
   }
   ge_affc a; ge_to_affc_half( a, P );
-  u32 * e = btab + j*BTAB_STRIDE;
   #pragma unroll
   for( int i=0; i<9; i++ ) { e[i] = a.YmX.v[i]; e[9+i] = a.YpX.v[i]; e[18+i] = a.T2d.v[i]; }
   e[27] = 0u;
@@ -278,8 +285,48 @@ void k_bitmap( ulong n, signed char const * __restrict__ codes, ulong * __restri
   if( (threadIdx.x & 63u) == 0u && i < n ) bitmap[i >> 6] = b;
 }
 
+/* table [0..8]Q in cached form for Q = (qx, qy) affine (fd_curve25519.c:
+   130-143): identity, Q, 2Q, then (j+1)Q = jQ + Q -- a chain keeps one point
+   and Q's cached form live */
+DEV void build_cached_table( u32 * tab, fe const & qx, fe const & qy ) {
+  ge_p3 Q; Q.X = qx; Q.Y = qy; fe_1( Q.Z ); fe_mul( Q.T, Q.X, Q.Y );
+  ge_cached c;
+  fe_1( c.YmX ); fe_1( c.YpX ); fe_0( c.T2d ); fe_set( c.Z2, 2,0,0,0,0,0,0,0,0 );
+  store_cached( tab + 0*ATAB_ENT, c );                                  /* identity */
+  ge_cached c1; ge_to_cached( c1, Q ); store_cached( tab + 1*ATAB_ENT, c1 );
+  ge_p3 Pj;
+  ge_dbl( Pj, Q, true ); ge_to_cached( c, Pj ); store_cached( tab + 2*ATAB_ENT, c );
+  #pragma unroll 1
+  for( int j=3; j<=8; j++ ) {
+    ge_add_cached( Pj, Pj, c1, 0u, true ); ge_to_cached( c, Pj ); store_cached( tab + j*ATAB_ENT, c );
+  }
+}
+
+/* biased signed digit -> (negate mask, magnitude) */
+DEV void digit_split( u32 d, u32 bias, u32 & neg, u32 & mag ) {
+  int v = (int)d - (int)bias;
+  neg = v < 0 ? ~0u : 0u;
+  mag = (u32)(v < 0 ? -v : v);
+}
+
+/* shift 16 packed radix-256 digits left by one digit */
+DEV void digits_shl4( u32 d[4] ) {
+  d[3] = __builtin_amdgcn_alignbit( d[3], d[2], 24u );
+  d[2] = __builtin_amdgcn_alignbit( d[2], d[1], 24u );
+  d[1] = __builtin_amdgcn_alignbit( d[1], d[0], 24u );
+  d[0] <<= 8;
+}
+
+/* maximum of v < 128 over the wave's active lanes (wave-uniform result) */
+DEV u32 wave_max7( u32 v ) {
+  u32 m = 0u;
+  #pragma unroll
+  for( int b=6; b>=0; b-- ) { u32 c = m | (1u << b); if( __ballot( v >= c ) ) m = c; }
+  return m;
+}
+
 /* FD_DSM_WAVES: waves per SIMD the register allocation of k_verify_dsm is
-   held to (0: compiler's choice, 173 VGPRs -> 2 waves) */
+   held to (0: compiler's choice) */
 #ifndef FD_DSM_WAVES
 #define FD_DSM_WAVES 0
 #endif
@@ -296,85 +343,85 @@ void k_verify_dsm( ulong chunk, u32 const * __restrict__ st, u32 const * __restr
   ulong t = (ulong)blockIdx.x * blockDim.x + threadIdx.x;
   u32 m = *count;
   if( (ulong)blockIdx.x * blockDim.x >= m ) return;        /* whole workgroup past the survivors */
-  __shared__ __attribute__((aligned(16))) u32 lds_btab[BTAB_WORDS];
-  for( int q = threadIdx.x; q < BTAB_WORDS/4; q += blockDim.x )
+  __shared__ __attribute__((aligned(16))) u32 lds_btab[2*BTAB_WORDS];
+  for( int q = threadIdx.x; q < 2*BTAB_WORDS/4; q += blockDim.x )
     ((uint4 *)lds_btab)[q] = ((uint4 const *)btab)[q];
   __syncthreads();
   if( t >= m ) return;
   ulong i = idx[t];
-  ulong ii = t;                                            /* A-table slot: dense in t */
+  ulong ii = t;                                            /* table slot: dense in t */
   u32 const * s = st + i;
   bool eq = false;
   {
-    /* ---- recode scalars (fixed signed windows) ---- */
-    u32 k[8], S[8], kd[8], sd[8];
-    #pragma unroll
-    for( int w=0; w<8; w++ ) { k[w] = s[(ST_K+w)*chunk]; S[w] = s[(ST_S+w)*chunk]; }
-    sc_recode16( kd, k );
-    sc_recode256( sd, S );
-
-    /* ---- table [0..8]Q, Q = -A (user.c:216; fd_curve25519.c:130-143) ---- */
-    u32 * tab = atab + ii * ATAB_WORDS;
+    /* ---- half-size scalars (sc_halfsize): the reference's check
+       [S]B - [k]A == R (user.c:216-226) becomes
+       [k2*S mod L]B - [k1]A - [k2]R == O with k1, k2 ~ 2^128 ---- */
+    u32 kd1[8], kd2[8], sd[8], k1neg, D;
     {
-      ge_p3 Q;
-      fe ax;
-      u32 aw[8], yw[8];
+      u32 k[8], S[8], k1[8], k2[8], sp[8];
       #pragma unroll
-      for( int w=0; w<8; w++ ) { aw[w] = s[(ST_AX+w)*chunk]; yw[w] = s[(ST_AY+w)*chunk]; }
-      fe_from_words( ax, aw ); fe_from_words( Q.Y, yw );
-      fe_neg( Q.X, ax ); fe_norm( Q.X, Q.X ); fe_1( Q.Z ); fe_mul( Q.T, Q.X, Q.Y );
-      ge_cached c;
-      fe_1( c.YmX ); fe_1( c.YpX ); fe_0( c.T2d ); fe_set( c.Z2, 2,0,0,0,0,0,0,0,0 );
-      store_cached( tab + 0*ATAB_ENT, c );                                  /* identity */
-      ge_cached c1; ge_to_cached( c1, Q ); store_cached( tab + 1*ATAB_ENT, c1 );
-      /* 2Q, then (j+1)Q = jQ + Q: a chain keeps one point and c1 live */
-      ge_p3 Pj;
-      ge_dbl( Pj, Q, true ); ge_to_cached( c, Pj ); store_cached( tab + 2*ATAB_ENT, c );
-      #pragma unroll 1
-      for( int j=3; j<=8; j++ ) {
-        ge_add_cached( Pj, Pj, c1, 0u, true ); ge_to_cached( c, Pj ); store_cached( tab + j*ATAB_ENT, c );
-      }
+      for( int w=0; w<8; w++ ) { k[w] = s[(ST_K+w)*chunk]; S[w] = s[(ST_S+w)*chunk]; }
+      u32 bits = sc_halfsize( k1, k1neg, k2, k );
+      sc_mul( sp, k2, S );
+      sc_recode16s( kd1, k1 ); sc_recode16s( kd2, k2 );
+      sc_recode256( sd, sp );       /* digits 0..15: B; 16..31: 2^128 B (second LDS table) */
+      D = max( (bits >> 2) + 1u, 31u );   /* windows; >= 31 so all 16 B digit pairs are reached */
+    }
+    D = wave_max7( D );             /* one window count per wave: no divergence in the loop */
+    #pragma unroll 1
+    for( u32 q = D; q < 64u; q++ ) { digits_shl( kd1, 4u ); digits_shl( kd2, 4u ); }
+
+    /* ---- tables [0..8](+-A) and [0..8](-R) (fd_curve25519.c:130-143) ---- */
+    u32 * tabA = atab + ii * ATAB_WORDS, * tabR = tabA + RTAB_OFF;
+    {
+      fe x, y, nx;
+      u32 xw[8], yw[8];
+      #pragma unroll
+      for( int w=0; w<8; w++ ) { xw[w] = s[(ST_AX+w)*chunk]; yw[w] = s[(ST_AY+w)*chunk]; }
+      fe_from_words( x, xw ); fe_from_words( y, yw );
+      fe_neg( nx, x ); fe_norm( nx, nx ); fe_cmov( nx, x, k1neg );      /* k1 < 0: [|k1|](+A) */
+      build_cached_table( tabA, nx, y );
+      #pragma unroll
+      for( int w=0; w<8; w++ ) { xw[w] = s[(ST_RX+w)*chunk]; yw[w] = s[(ST_RY+w)*chunk]; }
+      fe_from_words( x, xw ); fe_from_words( y, yw );
+      fe_neg( nx, x ); fe_norm( nx, nx );
+      build_cached_table( tabR, nx, y );
     }
 
-    /* ---- [k]Q + [S]B (user.c:217; fd_curve25519.c:121-165) ---- */
+    /* ---- [k1](+-A) + [k2](-R) + [s']B, signed radix-16 windows for k1, k2
+       and radix-256 digit pairs for s' every other window ---- */
     ge_p3 P; ge_identity( P );
     #pragma unroll 1
-    for( int w=63; w>=0; w-- ) {
-      u32 da = kd[7] >> 28; digits_shl( kd, 4u );
-      int sa = (int)da - 8;
-      u32 nega = sa < 0 ? ~0u : 0u;
-      u32 ia = (u32)(sa < 0 ? -sa : sa);
-      /* issued before the window's 4 doublings, which hide its latency
-         (measured: loading after them, or trading the 36 registers for a
-         4th wave per SIMD, is not faster) */
-      ge_cached e; load_cached( e, tab + ia*ATAB_ENT );
-      if( w != 63 ) {
+    for( int w=(int)D-1; w>=0; w-- ) {
+      u32 nega, ia, negr, ir;
+      digit_split( kd1[7] >> 28, 7u, nega, ia ); digits_shl( kd1, 4u );
+      digit_split( kd2[7] >> 28, 7u, negr, ir ); digits_shl( kd2, 4u );
+      /* issued before the window's 4 doublings, which hide its latency */
+      ge_cached e; load_cached( e, tabA + ia*ATAB_ENT );
+      if( w != (int)D-1 ) {
         #pragma unroll 1
         for( int j=0; j<3; j++ ) ge_dbl( P, P, false );
         ge_dbl( P, P, true );
       }
-      bool even = (w & 1) == 0;
-      ge_add_cached( P, P, e, nega, even );
-      if( even ) {
-        u32 db = sd[7] >> 24; digits_shl( sd, 8u );
-        int sb = (int)db - 128;
-        u32 negb = sb < 0 ? ~0u : 0u;
-        u32 ib = (u32)(sb < 0 ? -sb : sb);
+      ge_add_cached( P, P, e, nega, true );
+      load_cached( e, tabR + ir*ATAB_ENT );
+      bool bw = (w & 1) == 0 && w <= 30;
+      ge_add_cached( P, P, e, negr, bw );
+      if( bw ) {
+        u32 negb, ib, negc, ic;
+        digit_split( sd[3] >> 24, 128u, negb, ib ); digits_shl4( sd );
+        digit_split( sd[7] >> 24, 128u, negc, ic ); digits_shl4( sd + 4 );
         ge_affc b; load_affc( b, lds_btab + ib*BTAB_STRIDE );
-        ge_add_affc( P, P, b, negb, false );
+        ge_add_affc( P, P, b, negb, true );
+        load_affc( b, lds_btab + BTAB_WORDS + ic*BTAB_STRIDE );
+        ge_add_affc( P, P, b, negc, false );
       }
     }
 
-    /* ---- projective compare with R (user.c:226; fd_r43x6_ge.h:52-82) ---- */
-    fe rx, ry, t, cx, cy;
-    u32 rxw[8], ryw[8];
-    #pragma unroll
-    for( int w=0; w<8; w++ ) { rxw[w] = s[(ST_RX+w)*chunk]; ryw[w] = s[(ST_RY+w)*chunk]; }
-    fe_from_words( rx, rxw ); fe_from_words( ry, ryw );
-    fe_mul( t, rx, P.Z ); fe_canon( t, t ); fe_canon( cx, P.X );
-    bool ex = fe_eq_c( t, cx );
-    fe_mul( t, ry, P.Z ); fe_canon( t, t ); fe_canon( cy, P.Y );
-    eq = ex && fe_eq_c( t, cy );
+    /* ---- P == O: X == 0 and Y == Z (Z != 0: complete formulas) ---- */
+    fe x, y, z;
+    fe_canon( x, P.X ); fe_canon( y, P.Y ); fe_canon( z, P.Z );
+    eq = fe_is_zero_c( x ) && fe_eq_c( y, z );
   }
   codes[i] = (signed char)(eq ? FD_ED25519_SUCCESS : FD_ED25519_ERR_MSG);   /* user.c:226-229 */
 }
@@ -502,13 +549,13 @@ fd_ed25519_hip_ctx_new( int device, ulong chunk_sigs ) {
   ctx->chunk  = chunk_sigs;
   FD_CHECK( hipSetDevice( device ) );
   FD_CHECK( hipStreamCreateWithFlags( &ctx->stream, hipStreamNonBlocking ) );
-  FD_CHECK( hipMalloc( (void **)&ctx->d_btab,  BTAB_WORDS * sizeof(u32) ) );
+  FD_CHECK( hipMalloc( (void **)&ctx->d_btab,  2 * BTAB_WORDS * sizeof(u32) ) );
   FD_CHECK( hipMalloc( (void **)&ctx->d_state, (size_t)ST_WORDS * chunk_sigs * sizeof(u32) ) );
   FD_CHECK( hipMalloc( (void **)&ctx->d_atab,  (size_t)ATAB_WORDS * chunk_sigs * sizeof(u32) ) );
   FD_CHECK( hipMalloc( (void **)&ctx->d_idx, chunk_sigs * sizeof(u32) ) );
   FD_CHECK( hipMalloc( (void **)&ctx->d_count, 256 ) );
   for( int e=0; e<4; e++ ) FD_CHECK( hipEventCreate( &ctx->ev[e] ) );
-  hipLaunchKernelGGL( k_btab_init, dim3( (BTAB_N + 63)/64 ), dim3( 64 ), 0, ctx->stream, ctx->d_btab );
+  hipLaunchKernelGGL( k_btab_init, dim3( (2*BTAB_N + 63)/64 ), dim3( 64 ), 0, ctx->stream, ctx->d_btab );
   FD_CHECK( hipGetLastError() );
   FD_CHECK( hipStreamSynchronize( ctx->stream ) );
   return ctx;
