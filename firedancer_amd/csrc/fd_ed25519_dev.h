@@ -541,34 +541,35 @@ DEV u32 mw_sel( u32 m, u32 a, u32 b ) { return (a & m) | (b & ~m); }   /* m ? a 
 
 /* o = a - q*b mod 2^(32N); returns 1 when a < q*b (a, b unsigned, the
    difference above -2^(32N)) */
+/* carry chains through v_add_co / v_addc_co (v_sub_co / v_subb_co) */
 template<int N>
 DEV u32 mw_submul( u32 o[N], u32 const a[N], u32 const b[N], u32 q ) {
   u32 c = 0, bw = 0;
   #pragma unroll
   for( int i=0; i<N; i++ ) {
     u64 p = (u64)b[i] * q + c; c = (u32)(p >> 32);
-    u64 d = (u64)a[i] - (u32)p - bw; o[i] = (u32)d; bw = (u32)(d >> 32) & 1u;
+    o[i] = __builtin_subc( a[i], (u32)p, bw, &bw );
   }
   return (c | bw) != 0u;
 }
 template<int N>
 DEV void mw_add( u32 o[N], u32 const a[N], u32 const b[N] ) {
-  u64 c = 0;
+  u32 c = 0;
   #pragma unroll
-  for( int i=0; i<N; i++ ) { c += (u64)a[i] + b[i]; o[i] = (u32)c; c >>= 32; }
+  for( int i=0; i<N; i++ ) o[i] = __builtin_addc( a[i], b[i], c, &c );
 }
 template<int N>
 DEV u32 mw_sub( u32 o[N], u32 const a[N], u32 const b[N] ) {   /* returns the borrow (a < b unsigned) */
   u32 bw = 0;
   #pragma unroll
-  for( int i=0; i<N; i++ ) { u64 d = (u64)a[i] - b[i] - bw; o[i] = (u32)d; bw = (u32)(d >> 32) & 1u; }
+  for( int i=0; i<N; i++ ) o[i] = __builtin_subc( a[i], b[i], bw, &bw );
   return bw;
 }
 template<int N>
 DEV void mw_cneg( u32 x[N], u32 m ) {       /* x = m ? -x : x (two's complement), m 0 or ~0 */
-  u64 c = m & 1u;
+  u32 c = m & 1u;
   #pragma unroll
-  for( int i=0; i<N; i++ ) { c += (u64)(x[i] ^ m); x[i] = (u32)c; c >>= 32; }
+  for( int i=0; i<N; i++ ) x[i] = __builtin_addc( x[i] ^ m, 0u, c, &c );
 }
 template<int N>
 DEV u32 mw_bitlen( u32 const x[N] ) {       /* unsigned bit length */
@@ -650,36 +651,64 @@ DEV void hs_pick2( u32 br[9], u32 bt[5], u32 & bc, u32 const ra[9], u32 const ta
   mw_sub<9>( r, ra, rb ); mw_sub<5>( t, ta, tb ); hs_pick( br, bt, bc, r, t );
 }
 
-DEV u32 sc_halfsize( u32 k1[8], u32 & k1neg, u32 k2[8], u32 const k[8] ) {
-  u32 rp[8] = { 0xe7ae9f68u,0xc09318d2u,0x17bce6b2u,0xa6f7cef5u,0u,0u,0u,0x80000000u };   /* 8L */
-  u32 rc[8], tp[5] = { 0u,0u,0u,0u,0u }, tc[5] = { 1u,0u,0u,0u,0u };
-  #pragma unroll
-  for( int i=0; i<8; i++ ) rc[i] = k[i];
-  double dp = mw_to_f64( rp ), dc = mw_to_f64( rc );
-  bool fb = false;
-  #pragma unroll 1
-  for( int it=0; (rc[4] | rc[5] | rc[6] | rc[7]) != 0u; it++ ) {   /* while r_c >= 2^128 */
-    double qd = floor( dp / dc );
-    if( qd >= 4294967296.0 || it >= 512 ) { fb = true; break; }
-    u32 q = (u32)qd;
-    u32 rn[8], tn[5];
-    u32 neg = mw_submul<8>( rn, rp, rc, q );
-    mw_submul<5>( tn, tp, tc, q );
-    if( neg ) { mw_add<8>( rn, rn, rc ); mw_add<5>( tn, tn, tc ); }   /* estimate one too high */
-    u32 tmp[8];
-    u32 lt = 0u - mw_sub<8>( tmp, rn, rc );      /* ~0: r_n < r_c, swap; else the estimate
-                                                    was one too low: keep r_c */
-    double dn = mw_to_f64( rn );
-    /* selects as masks (v_bfi_b32), not v_cndmask */
-    #pragma unroll
-    for( int i=0; i<8; i++ ) { u32 a = mw_sel( lt, rc[i], rn[i] ); rc[i] = mw_sel( lt, rn[i], rc[i] ); rp[i] = a; }
-    #pragma unroll
-    for( int i=0; i<5; i++ ) { u32 a = mw_sel( lt, tc[i], tn[i] ); tc[i] = mw_sel( lt, tn[i], tc[i] ); tp[i] = a; }
-    u64 m64 = ((u64)lt << 32) | lt;
-    u64 bc_ = (u64)__double_as_longlong( dc ), bn = (u64)__double_as_longlong( dn );
-    dp = __longlong_as_double( (long long)((bc_ & m64) | (bn & ~m64)) );
-    dc = __longlong_as_double( (long long)((bn & m64) | (bc_ & ~m64)) );
+/* One Euclid step in place: x = x mod y, t_x -= q*t_y, for remainders
+   x >= y >= 2^128.  q comes from the float quotient (relative error < 2^-47,
+   so it is the exact quotient or one off either way); the rare corrections
+   run behind wave-wide votes so the common path carries no selects.
+   Returns false when q >= 2^32. */
+DEV bool hs_step( u32 x[8], u32 tx[5], double & dx, u32 const y[8], u32 const ty[5], double dy ) {
+  double r = __builtin_amdgcn_rcp( dy );
+  r = fma( r, fma( -dy, r, 1.0 ), r );
+  r = fma( r, fma( -dy, r, 1.0 ), r );
+  double qd = floor( dx * r );
+  if( !(qd < 4294967296.0) ) return false;
+  u32 q = (u32)qd;
+  u32 neg = mw_submul<8>( x, x, y, q );
+  mw_submul<5>( tx, tx, ty, q );
+  if( __ballot( neg ) ) {                        /* estimate one too high */
+    if( neg ) { mw_add<8>( x, x, y ); mw_add<5>( tx, tx, ty ); }
   }
+  #pragma unroll 1
+  for( ;; ) {                                    /* estimate too low */
+    u32 tmp[8];
+    bool ge = mw_sub<8>( tmp, x, y ) == 0u;
+    if( !__ballot( ge ) ) break;
+    if( ge ) {
+      #pragma unroll
+      for( int i=0; i<8; i++ ) x[i] = tmp[i];
+      mw_sub<5>( tx, tx, ty );
+    }
+  }
+  dx = mw_to_f64( x );
+  return true;
+}
+
+DEV bool mw_below128( u32 const x[8] ) { return (x[4] | x[5] | x[6] | x[7]) == 0u; }
+
+DEV u32 sc_halfsize( u32 k1[8], u32 & k1neg, u32 k2[8], u32 const k[8] ) {
+  /* Euclid on (a, b) = (8L, k), remainders alternating between a and b so
+     the step needs no swap; on exit (rp, tp) is the last remainder >= 2^128
+     and (rc, tc) the first one below */
+  u32 a[8] = { 0xe7ae9f68u,0xc09318d2u,0x17bce6b2u,0xa6f7cef5u,0u,0u,0u,0x80000000u };   /* 8L */
+  u32 b[8], ta[5] = { 0u,0u,0u,0u,0u }, tb[5] = { 1u,0u,0u,0u,0u };
+  #pragma unroll
+  for( int i=0; i<8; i++ ) b[i] = k[i];
+  double da = mw_to_f64( a ), db = mw_to_f64( b );
+  bool fb = false, in_a = false;                 /* in_a: the newest remainder is a */
+  #pragma unroll 1
+  for( int it=0; ; it++ ) {
+    if( mw_below128( b ) ) break;
+    if( it >= 256 || !hs_step( a, ta, da, b, tb, db ) ) { fb = true; break; }
+    if( mw_below128( a ) ) { in_a = true; break; }
+    if( !hs_step( b, tb, db, a, ta, da ) ) { fb = true; break; }
+  }
+  u32 im = in_a ? ~0u : 0u;
+  u32 rp[8], rc[8], tp[5], tc[5];
+  #pragma unroll
+  for( int i=0; i<8; i++ ) { rp[i] = mw_sel( im, b[i], a[i] ); rc[i] = mw_sel( im, a[i], b[i] ); }
+  #pragma unroll
+  for( int i=0; i<5; i++ ) { tp[i] = mw_sel( im, tb[i], ta[i] ); tc[i] = mw_sel( im, ta[i], tb[i] ); }
+  double dp = in_a ? db : da, dc = in_a ? da : db;
   u32 bc = 999u, br[9], bt[5];
   #pragma unroll
   for( int i=0; i<9; i++ ) br[i] = 0u;
