@@ -8,11 +8,13 @@
                     checks, k = SHA-512(R||A||M) mod L -> 192-B state record;
                     survivor compaction: final codes of pre-check failures,
                     survivors -> idx[] (k_verify_dsm runs only them)
-     k_verify_dsm   base-point table -> LDS; table [0..8](-A) -> per-lane HBM
-                    scratch; [k](-A) + [S]B by fixed signed windows (radix 16
-                    for A, radix 256 for B: every lane adds at the same
-                    positions, so the wave never diverges on digits);
-                    projective compare with R; int8 code
+     k_verify_dsm   half-size scalars k1 = k*k2 (mod 8L), k2 odd, ~128 bits
+                    each (sc_halfsize); tables B and 2^128 B -> LDS; tables
+                    [0..8](+-A) and [0..8](-R) -> per-lane HBM scratch;
+                    [k1](+-A) + [k2](-R) + [k2*S mod L]B by fixed signed
+                    windows (radix 16 for k1, k2; radix-256 digit pairs for
+                    the B coefficient: every lane adds at the same positions,
+                    one window count per wave); identity check; int8 code
      k_bitmap       verdict bitmap from codes (64-bit ballot per wave)
      k_group_reduce batch_single_msg / per-txn semantics over sig codes
 
@@ -73,6 +75,7 @@ struct fd_ed25519_hip_ctx {
   u32 *        d_idx;       /* chunk: compacted survivor indices */
   u32 *        d_count;     /* survivor count */
   int          errmode;
+  int          halfsize;    /* 1: half-size scalars (default); 0: full-length (k, 1) */
   /* optional per-kernel timing (HIP events around each launch, on the launch stream) */
   int          timing;
   double       prep_ms, dsm_ms;
@@ -339,7 +342,7 @@ DEV u32 wave_max7( u32 v ) {
 __global__ __launch_bounds__(256) DSM_OCCUPANCY
 void k_verify_dsm( ulong chunk, u32 const * __restrict__ st, u32 const * __restrict__ btab,
                    u32 * __restrict__ atab, u32 const * __restrict__ idx, u32 const * __restrict__ count,
-                   signed char * __restrict__ codes ) {
+                   signed char * __restrict__ codes, int halfsize ) {
   ulong t = (ulong)blockIdx.x * blockDim.x + threadIdx.x;
   u32 m = *count;
   if( (ulong)blockIdx.x * blockDim.x >= m ) return;        /* whole workgroup past the survivors */
@@ -361,7 +364,13 @@ void k_verify_dsm( ulong chunk, u32 const * __restrict__ st, u32 const * __restr
       u32 k[8], S[8], k1[8], k2[8], sp[8];
       #pragma unroll
       for( int w=0; w<8; w++ ) { k[w] = s[(ST_K+w)*chunk]; S[w] = s[(ST_S+w)*chunk]; }
-      u32 bits = sc_halfsize( k1, k1neg, k2, k );
+      u32 bits;
+      if( halfsize ) bits = sc_halfsize( k1, k1neg, k2, k );
+      else {                        /* full-length pair (k, 1): the same equation, 64 windows */
+        #pragma unroll
+        for( int w=0; w<8; w++ ) { k1[w] = k[w]; k2[w] = w ? 0u : 1u; }
+        k1neg = 0u; bits = 253u;
+      }
       sc_mul( sp, k2, S );
       sc_recode16s( kd1, k1 ); sc_recode16s( kd2, k2 );
       sc_recode256( sd, sp );       /* digits 0..15: B; 16..31: 2^128 B (second LDS table) */
@@ -545,8 +554,9 @@ fd_ed25519_hip_ctx_new( int device, ulong chunk_sigs ) {
   chunk_sigs = (chunk_sigs + 255UL) & ~255UL;
   fd_ed25519_hip_ctx_t * ctx = (fd_ed25519_hip_ctx_t *)calloc( 1, sizeof(*ctx) );
   if( !ctx ) { fprintf( stderr, "fd_ed25519_hip: out of host memory\n" ); abort(); }
-  ctx->device = device;
-  ctx->chunk  = chunk_sigs;
+  ctx->device   = device;
+  ctx->chunk    = chunk_sigs;
+  ctx->halfsize = 1;
   FD_CHECK( hipSetDevice( device ) );
   FD_CHECK( hipStreamCreateWithFlags( &ctx->stream, hipStreamNonBlocking ) );
   FD_CHECK( hipMalloc( (void **)&ctx->d_btab,  2 * BTAB_WORDS * sizeof(u32) ) );
@@ -596,6 +606,32 @@ fd_ed25519_hip_ctx_delete( fd_ed25519_hip_ctx_t * ctx ) {
 int   fd_ed25519_hip_ctx_device( fd_ed25519_hip_ctx_t const * ctx ) { return ctx->device; }
 void *fd_ed25519_hip_ctx_stream( fd_ed25519_hip_ctx_t const * ctx ) { return (void *)ctx->stream; }
 void  fd_ed25519_hip_set_errmode( fd_ed25519_hip_ctx_t * ctx, int m ) { ctx->errmode = m; }
+void  fd_ed25519_hip_set_halfsize( fd_ed25519_hip_ctx_t * ctx, int on ) { ctx->halfsize = on ? 1 : 0; }
+
+/* test hook: sc_halfsize on n scalars k < L (8 LE words each); out per
+   scalar: k1 (8 words), k2 (8 words), k1neg (0 or ~0), bits */
+__global__ void k_test_halfsize( ulong n, u32 const * k, u32 * out ) {
+  ulong i = (ulong)blockIdx.x * blockDim.x + threadIdx.x;
+  if( i >= n ) return;
+  u32 kk[8], k1[8], k2[8], neg;
+  #pragma unroll
+  for( int w=0; w<8; w++ ) kk[w] = k[8*i+w];
+  u32 bits = sc_halfsize( k1, neg, k2, kk );
+  u32 * o = out + 18*i;
+  #pragma unroll
+  for( int w=0; w<8; w++ ) { o[w] = k1[w]; o[8+w] = k2[w]; }
+  o[16] = neg; o[17] = bits;
+}
+
+int
+fd_ed25519_hip_test_halfsize( fd_ed25519_hip_ctx_t * ctx, ulong n, uint const * d_k, uint * d_out, void * stream ) {
+  hipStream_t s = stream ? (hipStream_t)stream : ctx->stream;
+  FD_CHECK( hipSetDevice( ctx->device ) );
+  if( !n ) return 0;
+  hipLaunchKernelGGL( k_test_halfsize, dim3( (unsigned)((n + 63)/64) ), dim3( 64 ), 0, s, n, d_k, d_out );
+  FD_CHECK( hipGetLastError() );
+  return 0;
+}
 
 void
 fd_ed25519_hip_set_timing( fd_ed25519_hip_ctx_t * ctx, int on ) {
@@ -634,7 +670,7 @@ verify_impl( fd_ed25519_hip_ctx_t * ctx, ulong n, uchar const * d_sigs, uchar co
     if( ctx->timing ) FD_CHECK( hipEventRecord( ctx->ev[1], s ) );
     if( ctx->timing ) FD_CHECK( hipEventRecord( ctx->ev[3], s ) );
     hipLaunchKernelGGL( k_verify_dsm, grid, blk, 0, s, ctx->chunk, ctx->d_state, ctx->d_btab, ctx->d_atab,
-                        ctx->d_idx, ctx->d_count, d_codes + off );
+                        ctx->d_idx, ctx->d_count, d_codes + off, ctx->halfsize );
     FD_CHECK( hipGetLastError() );
     if( d_bitmap ) {
       hipLaunchKernelGGL( k_bitmap, grid, blk, 0, s, m, d_codes + off, d_bitmap + off/64, d_n, off );

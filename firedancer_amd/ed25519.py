@@ -30,7 +30,7 @@ EXPORTS = (
     "fd_ed25519_hip_verify_fixed_dev", "fd_ed25519_hip_verify_dev_count",
     "fd_ed25519_hip_verify_host", "fd_ed25519_hip_group_reduce_dev", "fd_ed25519_hip_sign_dev",
     "fd_ed25519_hip_sync", "fd_ed25519_hip_set_timing", "fd_ed25519_hip_get_timing",
-    "fd_ed25519_hip_get_dsm_units",
+    "fd_ed25519_hip_get_dsm_units", "fd_ed25519_hip_set_halfsize", "fd_ed25519_hip_test_halfsize",
 )
 
 _lib = None
@@ -63,6 +63,8 @@ def lib():
         L.fd_ed25519_hip_ctx_stream.restype = vp
         L.fd_ed25519_hip_ctx_stream.argtypes = [vp]
         L.fd_ed25519_hip_set_errmode.argtypes = [vp, c.c_int]
+        L.fd_ed25519_hip_set_halfsize.argtypes = [vp, c.c_int]
+        L.fd_ed25519_hip_test_halfsize.argtypes = [vp, c.c_ulong, vp, vp, vp]
         L.fd_ed25519_hip_ctx_reserve.argtypes = [vp, u64]
         L.fd_ed25519_hip_verify_dev.restype = c.c_int
         L.fd_ed25519_hip_verify_dev.argtypes = [vp, u64, vp, vp, vp, vp, vp, vp, vp, vp]
@@ -185,6 +187,14 @@ class Verifier:
     def sign_dev(self, n, prvs, pool, msg_off, msg_sz, pubs, sigs, stream=None):
         return self._lib.fd_ed25519_hip_sign_dev(self.ctx, int(n), _ptr(prvs), _ptr(pool), _ptr(msg_off),
                                                  _ptr(msg_sz), _ptr(pubs), _ptr(sigs), stream)
+
+    def set_halfsize(self, on):
+        """Half-size scalars (default) or the full-length pair (k, 1): same verdicts."""
+        self._lib.fd_ed25519_hip_set_halfsize(self.ctx, 1 if on else 0)
+
+    def test_halfsize(self, n, d_k, d_out, stream=None):
+        """Test hook: device half-size reduction (see fd_ed25519_hip_test_halfsize)."""
+        return self._lib.fd_ed25519_hip_test_halfsize(self.ctx, int(n), _ptr(d_k), _ptr(d_out), stream)
 
     def set_timing(self, on):
         self._lib.fd_ed25519_hip_set_timing(self.ctx, 1 if on else 0)

@@ -100,6 +100,19 @@ void                   fd_ed25519_hip_ctx_reserve( fd_ed25519_hip_ctx_t * ctx, u
 void *                 fd_ed25519_hip_ctx_stream( fd_ed25519_hip_ctx_t const * ctx ); /* hipStream_t */
 void                   fd_ed25519_hip_set_errmode( fd_ed25519_hip_ctx_t * ctx, int errmode );
 
+/* The double-scalar multiplication checks [k2*S mod L]B - [k1]A - [k2]R == O
+   with k1 == k*k2 (mod 8L), k2 odd, both ~2^128 (half-size scalars, ~128
+   doublings); the verdict equals the reference's [S]B - [k]A == R bit for
+   bit.  set_halfsize(ctx, 0) runs every signature with the full-length pair
+   (k, 1) instead (252 doublings): an A/B and test switch, same results. */
+void                   fd_ed25519_hip_set_halfsize( fd_ed25519_hip_ctx_t * ctx, int on );
+
+/* Test hook: the device half-size reduction of n scalars k < L (d_k: 8 LE
+   u32 words each) into d_out (18 words each: |k1| (8), k2 (8), k1 < 0 ? ~0 :
+   0, max bit length).  Asynchronous on stream. */
+int fd_ed25519_hip_test_halfsize( fd_ed25519_hip_ctx_t * ctx, ulong n, uint const * d_k, uint * d_out,
+                                  void * stream );
+
 /* Kernel timing for measurement legs: when on, every verify chunk brackets
    k_verify_prep and k_verify_dsm with HIP events on the launch stream and
    accumulates their durations (this serialises the host per chunk).
