@@ -27,6 +27,13 @@ v_mad_u64_u32 (lo+hi+add) and v_addc_co_u32 issue at half that lane rate
 (profiles/r01_valu_rates_*.txt), i.e. two half-rate slots = the four W ops.
 The kernel duration is measured live with HIP events on the launch stream.
 
+W is fixed from the reference algorithm whatever scalar
+method the GPU uses.  k_verify_dsm runs half-size scalars (k1, k2 ~ 2^128
+with k1 = k*k2 mod 8L, see sc_halfsize): 4*(D-1) doublings for D ~ 33.2
+windows per wave instead of 252, so it executes ~5.05e5 op-equivalents per
+signature (W_DSM_EXEC: 1261.8 M + 522.7 S + ~1.65e4 for the reduction), not
+6.08e5.  The JSON reports both fractions; "frac" keeps the 8(d) definition.
+
 cpu_baseline (rank 0, N=1): the reference's own fd_ed25519_verify (AVX-512
 IFMA build, compiled from the reference sources into oracle/_ref/) on a
 bounded 65536-record sample of the same batch, one pinned thread per core.
@@ -48,7 +55,7 @@ METRIC = "ed25519 verifies/sec (1/2/4/8 MI355X) + % of INT32 VALU peak"
 N_M, N_S = 1378.6, 1518.1
 N_M_DECODE, N_S_DECODE = 42.0, 510.0
 PEAK_OPS = 256 * 4 * 32 * 2.4e9          # 78.6e12 int32 lane-ops/s (32-wide SIMDs)
-PMC_SUMMARY = "r01c_pmc_summary.json"    # rocprofv3 PMC passes of this kernel build (tools/run_profile.sh)
+PMC_SUMMARY = "r01d_pmc_summary.json"    # rocprofv3 PMC passes of this kernel build (tools/run_profile.sh)
 
 
 def w_total(msg_sz):
@@ -57,6 +64,7 @@ def w_total(msg_sz):
 
 
 W_DSM = 304 * (N_M - N_M_DECODE) + 200 * (N_S - N_S_DECODE)
+W_DSM_EXEC = 304 * 1261.8 + 200 * 522.7 + 1.65e4   # executed by the half-size k_verify_dsm (docstring)
 
 
 def write_fdv1(path, sigs, pubs, pool, moff, msz):
@@ -306,6 +314,8 @@ def main():
                          "traffic_source": traffic_src,
                          "algorithmic_ops_per_unit": round(W_DSM), "units_per_launch": round(units_per_launch),
                          "avg_launch_ms": round(dsm_avg_ms, 4),
+                         "executed_ops_per_unit": round(W_DSM_EXEC),
+                         "executed_frac": round(achieved * W_DSM_EXEC / W_DSM / peak, 4),
                          "timing_leg": "after the timed steps: the whole batch through one context, HIP events "
                                        "around each launch, each k_verify_dsm alone on the GPU"},
             "pipeline": {"prep_ms": round(prep_avg_ms, 4), "dsm_ms": round(dsm_avg_ms, 4),
