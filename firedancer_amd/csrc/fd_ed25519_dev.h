@@ -537,7 +537,14 @@ DEV void sc_recode16s( u32 out[8], u32 const k[8] ) {
 
 /* ---- multiword integers, little-endian u32 words ---- */
 
-DEV u32 mw_sel( u32 m, u32 a, u32 b ) { return (a & m) | (b & ~m); }   /* m ? a : b, m 0 or ~0 */
+/* m ? a : b for a mask m (0 or ~0), as v_bfi_b32: the compiler would
+   otherwise turn a compare-derived mask into v_cndmask, which issues at ~1/5
+   the rate on gfx950 (profiles/r01_valu_rates_b.txt) */
+DEV u32 mw_sel( u32 m, u32 a, u32 b ) {
+  u32 r;
+  asm( "v_bfi_b32 %0, %1, %2, %3" : "=v"(r) : "v"(m), "v"(a), "v"(b) );
+  return r;
+}
 
 /* o = a - q*b mod 2^(32N); returns 1 when a < q*b (a, b unsigned, the
    difference above -2^(32N)) */
@@ -637,7 +644,7 @@ DEV void sc_mul( u32 r[8], u32 const a[8], u32 const b[8] ) {
    returns max(bitlen k1, bitlen k2). */
 DEV void hs_pick( u32 br[9], u32 bt[5], u32 & bc, u32 const r[9], u32 const t[5] ) {
   u32 c = max( mw_abs_bitlen<9>( r ), mw_abs_bitlen<5>( t ) ) | ((~t[0] & 1u) << 10);   /* even t: 1024+ */
-  u32 take = c < bc ? ~0u : 0u;
+  u32 take = (u32)((int)(c - bc) >> 31);       /* c < bc (both < 2^11) */
   #pragma unroll
   for( int i=0; i<9; i++ ) br[i] = mw_sel( take, r[i], br[i] );
   #pragma unroll

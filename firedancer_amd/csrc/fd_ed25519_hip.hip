@@ -308,8 +308,8 @@ DEV void build_cached_table( u32 * tab, fe const & qx, fe const & qy ) {
 /* biased signed digit -> (negate mask, magnitude) */
 DEV void digit_split( u32 d, u32 bias, u32 & neg, u32 & mag ) {
   int v = (int)d - (int)bias;
-  neg = v < 0 ? ~0u : 0u;
-  mag = (u32)(v < 0 ? -v : v);
+  neg = (u32)(v >> 31);
+  mag = ((u32)v ^ neg) - neg;
 }
 
 /* shift 16 packed radix-256 digits left by one digit */
@@ -347,8 +347,16 @@ void k_verify_dsm( ulong chunk, u32 const * __restrict__ st, u32 const * __restr
   u32 m = *count;
   if( (ulong)blockIdx.x * blockDim.x >= m ) return;        /* whole workgroup past the survivors */
   __shared__ __attribute__((aligned(16))) u32 lds_btab[2*BTAB_WORDS];
-  for( int q = threadIdx.x; q < 2*BTAB_WORDS/4; q += blockDim.x )
-    ((uint4 *)lds_btab)[q] = ((uint4 const *)btab)[q];
+  {
+    /* 28.9 KB: all of a thread's 16-B loads in flight before the LDS stores
+       (a load-store loop waits out one L2 round trip per iteration) */
+    constexpr int NQ = 2*BTAB_WORDS/4, PER = (NQ + 255)/256;
+    uint4 v[PER];
+    #pragma unroll
+    for( int u=0; u<PER; u++ ) { int q = threadIdx.x + 256*u; if( q < NQ ) v[u] = ((uint4 const *)btab)[q]; }
+    #pragma unroll
+    for( int u=0; u<PER; u++ ) { int q = threadIdx.x + 256*u; if( q < NQ ) ((uint4 *)lds_btab)[q] = v[u]; }
+  }
   __syncthreads();
   if( t >= m ) return;
   ulong i = idx[t];
