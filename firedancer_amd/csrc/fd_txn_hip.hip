@@ -270,10 +270,30 @@ void k_txn_parse( ulong n, u8 const * __restrict__ pool, u32 const * __restrict_
   po.tag[j]     = tag;
 }
 
+/* NW little-endian words from an unaligned byte address: NW (+1 when
+   unaligned) aligned dword loads and one funnel shift per word; never reads
+   past the dword holding the last byte */
+template<int NW>
+DEVI void ld_words_u( u32 w[NW], u8 const * p ) {
+  uintptr_t a = (uintptr_t)p;
+  u32 const * q = (u32 const *)(a & ~(uintptr_t)3);
+  u32 sh = (u32)(a & 3u) * 8u;
+  u32 d[NW+1];
+  #pragma unroll
+  for( int i=0; i<NW; i++ ) d[i] = q[i];
+  d[NW] = sh ? q[NW] : 0u;
+  #pragma unroll
+  for( int i=0; i<NW; i++ ) w[i] = __builtin_amdgcn_alignbit( d[i+1], d[i], sh );
+}
+
 /* Slot allocation + record expansion.  Each wave computes exclusive prefix
    sums of its lanes' nsig (< 32, five ballots + mbcnt) and takes one
    atomicAdd on the record counter.  Records of a wave are contiguous and in
-   frag order; waves land in any order (first[] says where). */
+   frag order; waves land in any order (first[] says where).  The wave then
+   copies its records cooperatively, one record per lane per round (the frag
+   of record t found by binary search over the wave's prefix sums in LDS):
+   ceil(records/64) rounds instead of the largest per-frag count, and the
+   record writes coalesce. */
 __global__ __launch_bounds__(256)
 void k_txn_expand( ulong n, u8 const * __restrict__ pool, u8 const * __restrict__ nsig_a,
                    u32 const * __restrict__ sig_at, u32 const * __restrict__ acct_at,
@@ -281,6 +301,7 @@ void k_txn_expand( ulong n, u8 const * __restrict__ pool, u8 const * __restrict_
                    u32 * __restrict__ counter, u32 * __restrict__ first, u8 * __restrict__ cnt,
                    u8 * __restrict__ rsig, u8 * __restrict__ rpub, u32 * __restrict__ rmoff,
                    u32 * __restrict__ rmsz, ulong cap ) {
+  __shared__ u32 l_excl[256], l_c[256], l_sig[256], l_acct[256], l_mo[256], l_ms[256];
   ulong j = (ulong)blockIdx.x * blockDim.x + threadIdx.x;
   u32 c = j < n ? nsig_a[j] : 0u;
   u32 excl = 0, tot = 0;
@@ -294,28 +315,38 @@ void k_txn_expand( ulong n, u8 const * __restrict__ pool, u8 const * __restrict_
   u32 base = 0;
   if( (threadIdx.x & 63u) == 0u && tot ) base = atomicAdd( counter, tot );
   base = __shfl( base, 0 );
-  if( j >= n ) return;
-  u32 f = base + excl;
-  first[j] = f; cnt[j] = (u8)c;
-  if( (ulong)f + c > cap ) { cnt[j] = 0; return; }      /* host sizes cap; never taken */
-  u8 const * s = pool + sig_at[j];
-  u8 const * a = pool + acct_at[j];
-  u32 mo = msg_at[j], ms = msg_sz[j];
-  for( u32 k = 0; k < c; k++ ) {
-    u32 r = f + k;
+  u32 lc = c;
+  if( j < n ) {
+    u32 f = base + excl;
+    first[j] = f; cnt[j] = (u8)c;
+    if( (ulong)f + c > cap ) { cnt[j] = 0; lc = 0; }      /* host sizes cap; never taken */
+    l_sig[threadIdx.x] = sig_at[j]; l_acct[threadIdx.x] = acct_at[j];
+    l_mo[threadIdx.x] = msg_at[j];  l_ms[threadIdx.x] = msg_sz[j];
+  }
+  l_excl[threadIdx.x] = excl; l_c[threadIdx.x] = lc;
+  __syncthreads();
+  u32 w0 = threadIdx.x & ~63u;
+  for( u32 t = threadIdx.x & 63u; t < tot; t += 64u ) {
+    u32 lo = 0, hi = 63;                                  /* last lane with excl <= t */
+    #pragma unroll
+    for( int s = 0; s < 6; s++ ) {
+      u32 mid = (lo + hi + 1u) >> 1;
+      bool le = l_excl[w0 + mid] <= t;
+      lo = le ? mid : lo; hi = le ? hi : mid - 1u;
+    }
+    u32 L = w0 + lo, k = t - l_excl[L];
+    if( k >= l_c[L] ) continue;                           /* capped frag */
+    u32 r = base + t;
+    u32 w[16];
+    ld_words_u<16>( w, pool + l_sig[L] + 64u*k );
     uint4 * ds = (uint4 *)(rsig + 64ul*r);
     #pragma unroll
-    for( int q = 0; q < 4; q++ ) {
-      u8 const * src = s + 64u*k + 16u*q;
-      ds[q] = make_uint4( ld_u32u( src ), ld_u32u( src + 4 ), ld_u32u( src + 8 ), ld_u32u( src + 12 ) );
-    }
+    for( int q = 0; q < 4; q++ ) ds[q] = make_uint4( w[4*q], w[4*q+1], w[4*q+2], w[4*q+3] );
+    ld_words_u<8>( w, pool + l_acct[L] + 32u*k );
     uint4 * dp = (uint4 *)(rpub + 32ul*r);
     #pragma unroll
-    for( int q = 0; q < 2; q++ ) {
-      u8 const * src = a + 32u*k + 16u*q;
-      dp[q] = make_uint4( ld_u32u( src ), ld_u32u( src + 4 ), ld_u32u( src + 8 ), ld_u32u( src + 12 ) );
-    }
-    rmoff[r] = mo; rmsz[r] = ms;
+    for( int q = 0; q < 2; q++ ) dp[q] = make_uint4( w[4*q], w[4*q+1], w[4*q+2], w[4*q+3] );
+    rmoff[r] = l_mo[L]; rmsz[r] = l_ms[L];
   }
 }
 
