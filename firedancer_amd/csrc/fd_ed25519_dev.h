@@ -343,6 +343,20 @@ DEV void ge_add_cached( ge_p3 & r, ge_p3 const & p, ge_cached q, u32 neg, bool n
   else        fe_mul( r.Z, F, G );
 }
 
+/* r = p + q with q the cached form of an affine point (2*Z = 2): D = 2*Z1
+   is an add, not a multiply (table chains, whose addend is the base point) */
+DEV void ge_add_cached_z1( ge_p3 & r, ge_p3 const & p, ge_cached const & q ) {
+  fe a, b, A, B, C, D, E, F, G, H;
+  fe_sub( a, p.Y, p.X ); fe_add( b, p.Y, p.X );
+  fe_mul2( A, a, q.YmX, B, b, q.YpX );
+  fe_mul( C, p.T, q.T2d );
+  fe_add( D, p.Z, p.Z ); fe_norm( D, D );
+  fe_sub( E, B, A ); fe_norm( E, E ); fe_add( H, B, A );
+  fe_sub( F, D, C ); fe_add( G, D, C );
+  fe_mul2( r.X, E, F, r.Y, G, H );
+  fe_mul2( r.Z, F, G, r.T, E, H );
+}
+
 /* r = p +/- q with q an affine cached point scaled by 1/2 (D = Z1) */
 DEV void ge_add_affc( ge_p3 & r, ge_p3 const & p, ge_affc q, u32 neg, bool needT ) {
   fe a, b, A, B, C, E, F, G, H;

@@ -301,7 +301,7 @@ DEV void build_cached_table( u32 * tab, fe const & qx, fe const & qy ) {
   ge_dbl( Pj, Q, true ); ge_to_cached( c, Pj ); store_cached( tab + 2*ATAB_ENT, c );
   #pragma unroll 1
   for( int j=3; j<=8; j++ ) {
-    ge_add_cached( Pj, Pj, c1, 0u, true ); ge_to_cached( c, Pj ); store_cached( tab + j*ATAB_ENT, c );
+    ge_add_cached_z1( Pj, Pj, c1 ); ge_to_cached( c, Pj ); store_cached( tab + j*ATAB_ENT, c );
   }
 }
 

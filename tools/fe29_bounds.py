@@ -128,13 +128,18 @@ def ge_dbl(P, needT):
 
 
 def ge_add(P, q, affine):
-    """q = (YmX, YpX, T2d[, Z2]) table entries; neg swaps YmX/YpX and F/G."""
+    """q = (YmX, YpX, T2d[, Z2]) table entries; neg swaps YmX/YpX and F/G.
+    affine: True (1/2-scaled affine entry, D = Z1), False (cached, D = Z1*Z2)
+    or "z1" (ge_add_cached_z1: cached form of an affine point, D = norm(2 Z1))."""
     X, Y, Z, T = P
     qa = qb = mx(q[0], q[1])
     a = sub(Y, X)
     b = add(Y, X)
     A, B, C = mul(a, qa), mul(b, qb), mul(T, q[2])
-    D = Z if affine else mul(Z, q[3])
+    if affine == "z1":
+        D = norm(add(Z, Z))
+    else:
+        D = Z if affine else mul(Z, q[3])
     E = norm(sub(B, A))
     H = add(B, A)
     F = sub(D, C)
@@ -150,7 +155,7 @@ def check():
         assert all(le(o, TIGHT) for o in r if o), "dbl output not tight"
     # A-table entries (ge_to_cached): norm(Y-X), norm(Y+X), T*2d, norm(2Z)
     entry = [norm(sub(TIGHT, TIGHT)), norm(add(TIGHT, TIGHT)), TIGHT, norm(add(TIGHT, TIGHT))]
-    for affine in (False, True):
+    for affine in (False, True, "z1"):
         r = ge_add(pt, entry, affine)
         assert all(le(o, TIGHT) for o in r), "add output not tight"
     # decode (ge_decode): y from words
