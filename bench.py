@@ -129,6 +129,8 @@ def main():
                          "groups of 16; c4 synthetic txn stream through the verify tile (GPU parse + verify + "
                          "host tcache dedup); c5 2^26 C2-mix signatures in total, sharded (strong scaling)")
     ap.add_argument("--txns", type=int, default=1 << 19, help="c4: frags per batch per GPU")
+    ap.add_argument("--halfsize", type=int, default=1, choices=[0, 1],
+                    help="0: full-length scalars (k, 1) in k_verify_dsm, an A/B switch (same verdicts)")
     ap.add_argument("--contexts", type=int, default=1,
                     help="c1/c2/c3/c5: verify contexts (streams) each step is split over (measured: 1-3 equal, 4+ slower)")
     ap.add_argument("--tiles", type=int, default=8, help="c4: verify tiles (host threads + contexts) per GPU")
@@ -185,6 +187,8 @@ def main():
     per = ((n + C - 1) // C + 255) // 256 * 256
     slices = [(lo, min(n, lo + per)) for lo in range(0, n, per)]
     ctxs = [Verifier(device=local, chunk_sigs=min(hi - lo, 1 << 20)) for lo, hi in slices]
+    for vv in ctxs + [v]:
+        vv.set_halfsize(args.halfsize)
 
     def groups_of(lo, hi):   # fd_ed25519_verify_batch_single_msg in chunks of 16 (fd_ed25519_user.c:238-241)
         ng = (hi - lo + 15) // 16
