@@ -50,3 +50,28 @@ def test_no_reference_or_oracle_in_product():
             if f.endswith((".py", ".hip", ".h")):
                 s = open(os.path.join(root, f)).read()
                 assert "liboracle" not in s and "oracle_lib" not in s and "/root/reference" not in s, f
+
+
+def test_headers_compile_and_link_as_c(tmp_path):
+    """The boundary is a C ABI: a C11 translation unit (as the reference's C
+    tiles would be) includes all three headers next to the system headers
+    with -Wall -Wextra -Werror, takes the address of every declared function,
+    links against the library and runs (no GPU call)."""
+    build()
+    names = set()
+    for h in ("fd_ed25519_hip.h", "fd_verify_hip.h", "fd_replay_hip.h"):
+        names |= declared_functions(h)
+    src = ['#include <stdio.h>', '#include <stdint.h>', '#include <sys/types.h>',
+           '#include "fd_ed25519_hip.h"', '#include "fd_verify_hip.h"', '#include "fd_replay_hip.h"',
+           'static void * const fns[] = {']
+    src += ['  (void *)%s,' % n for n in sorted(names)]
+    src += ['};', 'int main( void ) { printf( "%d\\n", (int)(sizeof(fns)/sizeof(fns[0])) ); return 0; }']
+    c = tmp_path / "abi.c"
+    c.write_text("\n".join(src) + "\n")
+    exe = tmp_path / "abi"
+    libdir = os.path.dirname(LIB)
+    subprocess.check_call(["gcc", "-std=c11", "-Wall", "-Wextra", "-Werror", "-I", os.path.join(REPO, "include"),
+                           str(c), "-L", libdir, "-lfd_ed25519_hip", "-Wl,-rpath-link,/opt/rocm/lib",
+                           "-Wl,-rpath," + libdir, "-o", str(exe)])
+    out = subprocess.check_output([str(exe)]).decode().strip()
+    assert int(out) == len(names)
