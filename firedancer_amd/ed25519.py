@@ -107,12 +107,26 @@ def fd_ed25519_strerror(err):
     return lib().fd_ed25519_strerror(int(err)).decode()
 
 
-def _ptr(a):
+def _ptr(a, nbytes=0, name="buffer", device=None):
+    """Device pointer of a GPU tensor for a *_dev entry point.  A host array
+    would reach a GPU kernel as an unmapped address (a fault that can take the
+    device down), and a tensor shorter than the records it is called for
+    would be read out of bounds: both raise here instead.  A plain int is
+    taken as a raw device pointer (the caller vouches for it)."""
     if a is None:
         return None
-    if isinstance(a, np.ndarray):
-        return a.ctypes.data
-    return a.data_ptr()   # torch tensor on the device
+    if isinstance(a, int):
+        return a
+    if isinstance(a, np.ndarray) or not getattr(a, "is_cuda", False):
+        raise TypeError(f"{name}: a GPU tensor is required (host data goes through verify_host)")
+    if not a.is_contiguous():
+        raise ValueError(f"{name}: tensor must be contiguous")
+    if device is not None and a.device.index != device:
+        raise ValueError(f"{name}: tensor on cuda:{a.device.index}, context on cuda:{device}")
+    have = a.numel() * a.element_size()
+    if have < nbytes:
+        raise ValueError(f"{name}: {have} bytes, {nbytes} needed")
+    return a.data_ptr()
 
 
 class Verifier:
@@ -165,28 +179,43 @@ class Verifier:
         return codes, bitmap
 
     # ---- device memory (torch tensors or raw pointers) ---------------------
+    def _p(self, a, nbytes=0, name="buffer"):
+        return _ptr(a, nbytes, name, self.device)
+
     def verify_dev(self, n, sigs, pubs, pool, msg_off, msg_sz, codes, bitmap=None, stream=None):
-        return self._lib.fd_ed25519_hip_verify_dev(self.ctx, int(n), _ptr(sigs), _ptr(pubs), _ptr(pool), _ptr(msg_off),
-                                                   _ptr(msg_sz), _ptr(codes), _ptr(bitmap), stream)
+        n = int(n)
+        return self._lib.fd_ed25519_hip_verify_dev(
+            self.ctx, n, self._p(sigs, 64 * n, "sigs"), self._p(pubs, 32 * n, "pubs"), self._p(pool, 1, "pool"),
+            self._p(msg_off, 4 * n, "msg_off"), self._p(msg_sz, 4 * n, "msg_sz"), self._p(codes, n, "codes"),
+            self._p(bitmap, 8 * ((n + 63) // 64), "bitmap"), stream)
 
     def verify_dev_count(self, n_max, d_n, sigs, pubs, pool, msg_off, msg_sz, codes, bitmap=None, stream=None):
         """verify_dev with the record count in device memory (uint32 *d_n)."""
-        return self._lib.fd_ed25519_hip_verify_dev_count(self.ctx, int(n_max), _ptr(d_n), _ptr(sigs), _ptr(pubs),
-                                                         _ptr(pool), _ptr(msg_off), _ptr(msg_sz), _ptr(codes),
-                                                         _ptr(bitmap), stream)
+        n = int(n_max)
+        return self._lib.fd_ed25519_hip_verify_dev_count(
+            self.ctx, n, self._p(d_n, 4, "d_n"), self._p(sigs, 64 * n, "sigs"), self._p(pubs, 32 * n, "pubs"),
+            self._p(pool, 1, "pool"), self._p(msg_off, 4 * n, "msg_off"), self._p(msg_sz, 4 * n, "msg_sz"),
+            self._p(codes, n, "codes"), self._p(bitmap, 8 * ((n + 63) // 64), "bitmap"), stream)
 
     def verify_fixed_dev(self, n, sigs, pubs, msgs, msg_sz, codes, bitmap=None, stream=None):
         """Fixed-size messages back to back: message i = msgs[i*msg_sz, (i+1)*msg_sz)."""
-        return self._lib.fd_ed25519_hip_verify_fixed_dev(self.ctx, int(n), _ptr(sigs), _ptr(pubs), _ptr(msgs),
-                                                         int(msg_sz), _ptr(codes), _ptr(bitmap), stream)
+        n = int(n)
+        return self._lib.fd_ed25519_hip_verify_fixed_dev(
+            self.ctx, n, self._p(sigs, 64 * n, "sigs"), self._p(pubs, 32 * n, "pubs"),
+            self._p(msgs, max(1, n * int(msg_sz)), "msgs"), int(msg_sz), self._p(codes, n, "codes"),
+            self._p(bitmap, 8 * ((n + 63) // 64), "bitmap"), stream)
 
     def group_reduce_dev(self, n_groups, first, cnt, sig_codes, group_codes, stream=None):
-        return self._lib.fd_ed25519_hip_group_reduce_dev(self.ctx, int(n_groups), _ptr(first), _ptr(cnt),
-                                                         _ptr(sig_codes), _ptr(group_codes), stream)
+        ng = int(n_groups)
+        return self._lib.fd_ed25519_hip_group_reduce_dev(
+            self.ctx, ng, self._p(first, 4 * ng, "first"), self._p(cnt, ng, "cnt"),
+            self._p(sig_codes, 1, "sig_codes"), self._p(group_codes, ng, "group_codes"), stream)
 
     def sign_dev(self, n, prvs, pool, msg_off, msg_sz, pubs, sigs, stream=None):
-        return self._lib.fd_ed25519_hip_sign_dev(self.ctx, int(n), _ptr(prvs), _ptr(pool), _ptr(msg_off),
-                                                 _ptr(msg_sz), _ptr(pubs), _ptr(sigs), stream)
+        n = int(n)
+        return self._lib.fd_ed25519_hip_sign_dev(
+            self.ctx, n, self._p(prvs, 32 * n, "prvs"), self._p(pool, 1, "pool"), self._p(msg_off, 4 * n, "msg_off"),
+            self._p(msg_sz, 4 * n, "msg_sz"), self._p(pubs, 32 * n, "pubs"), self._p(sigs, 64 * n, "sigs"), stream)
 
     def set_halfsize(self, on):
         """Half-size scalars (default) or the full-length pair (k, 1): same verdicts."""
@@ -194,7 +223,9 @@ class Verifier:
 
     def test_halfsize(self, n, d_k, d_out, stream=None):
         """Test hook: device half-size reduction (see fd_ed25519_hip_test_halfsize)."""
-        return self._lib.fd_ed25519_hip_test_halfsize(self.ctx, int(n), _ptr(d_k), _ptr(d_out), stream)
+        n = int(n)
+        return self._lib.fd_ed25519_hip_test_halfsize(self.ctx, n, self._p(d_k, 32 * n, "k"),
+                                                      self._p(d_out, 72 * n, "out"), stream)
 
     def set_timing(self, on):
         self._lib.fd_ed25519_hip_set_timing(self.ctx, 1 if on else 0)

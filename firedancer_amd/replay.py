@@ -80,7 +80,10 @@ class ReplayVerifier:
 
     def txn_verify_dev(self, n, pool, desc, result, stream=None):
         """pool: device bytes; desc: device fd_txn_hip_desc_t[n]; result: device int32[n]."""
-        rc = self._lib.fd_replay_hip_txn_verify_dev(self.r, int(n), _ptr(pool), _ptr(desc), _ptr(result), stream)
+        n, dev = int(n), self.verifier.device
+        rc = self._lib.fd_replay_hip_txn_verify_dev(self.r, n, _ptr(pool, 1, "pool", dev),
+                                                    _ptr(desc, 16 * n, "desc", dev),
+                                                    _ptr(result, 4 * n, "result", dev), stream)
         if rc:
             raise ValueError(f"fd_replay_hip_txn_verify_dev: n={n} > max_txn={self.max_txn}")
 
@@ -98,5 +101,7 @@ class ReplayVerifier:
 
 def fec_verify_roots_dev(verifier, n, roots, sigs, pubs, codes, stream=None):
     """FEC-set root check: codes[i] = fd_ed25519_verify(roots[32i:32i+32], sigs[i], pubs[i])."""
-    return lib().fd_fec_hip_verify_roots_dev(verifier.ctx, int(n), _ptr(roots), _ptr(sigs), _ptr(pubs),
-                                             _ptr(codes), stream)
+    n, dev = int(n), verifier.device
+    return lib().fd_fec_hip_verify_roots_dev(verifier.ctx, n, _ptr(roots, 32 * n, "roots", dev),
+                                             _ptr(sigs, 64 * n, "sigs", dev), _ptr(pubs, 32 * n, "pubs", dev),
+                                             _ptr(codes, n, "codes", dev), stream)

@@ -108,8 +108,10 @@ class Tcache:
 
 def parse_dev(verifier, n, pool, txn_off, txn_sz, txn_out, txn_t_sz, stream=None):
     """fd_txn_parse over n device-resident payloads (torch tensors / pointers)."""
-    return lib().fd_txn_hip_parse_dev(verifier.ctx, int(n), _ptr(pool), _ptr(txn_off), _ptr(txn_sz), _ptr(txn_out),
-                                      _ptr(txn_t_sz), stream)
+    n, dev = int(n), verifier.device
+    return lib().fd_txn_hip_parse_dev(verifier.ctx, n, _ptr(pool, 1, "pool", dev), _ptr(txn_off, 4 * n, "txn_off", dev),
+                                      _ptr(txn_sz, 2 * n, "txn_sz", dev), _ptr(txn_out, 0, "txn_out", dev),
+                                      _ptr(txn_t_sz, 2 * n, "txn_t_sz", dev), stream)
 
 
 class VerifyTile:
@@ -142,8 +144,10 @@ class VerifyTile:
 
     def submit(self, n, pool, txn_off, txn_sz, txn_out=None):
         """Device tensors: pool uint8, txn_off int32 (u32 bits), txn_sz int16 (u16 bits)."""
-        rc = self._lib.fd_verify_hip_tile_submit(self.tile, int(n), _ptr(pool), _ptr(txn_off), _ptr(txn_sz),
-                                                 _ptr(txn_out))
+        n, dev = int(n), self.verifier.device
+        rc = self._lib.fd_verify_hip_tile_submit(self.tile, n, _ptr(pool, 1, "pool", dev),
+                                                 _ptr(txn_off, 4 * n, "txn_off", dev),
+                                                 _ptr(txn_sz, 2 * n, "txn_sz", dev), _ptr(txn_out, 0, "txn_out", dev))
         if rc:
             raise RuntimeError(f"fd_verify_hip_tile_submit: {rc}")
         self._pending.append((int(n), (pool, txn_off, txn_sz, txn_out)))   # keep buffers alive

@@ -146,20 +146,39 @@ def test_fixed_matches_offsets(verifier):
 def test_verify_dev_count(verifier):
     """verify_dev_count: records [0, *d_n) verified exactly as verify_dev,
     codes past the device-side count untouched; n_max spans three chunks of
-    the fixture's 2^18 (one partial, one empty)."""
+    the fixture's 2^18 (counts ending inside the second chunk, inside the
+    first, and zero).  Buffers hold n_max records (the host cannot see *d_n)."""
     import torch
+    n = 3 << 18
     from firedancer_amd.workload import make_batch_gpu
-    n = (1 << 18) + 4000
     b = make_batch_gpu(verifier, n, msg_sz=48, seed=91, mix="c2")
     ref = torch.zeros(n, dtype=torch.int8, device="cuda:0")
     verifier.verify_dev(n, b.sigs, b.pubs, b.pool, b.msg_off, b.msg_sz, ref)
-    for cnt in (n, (1 << 18) + 17, 1000, 0):
+    for cnt in (n, (1 << 18) + 4000, (1 << 18) + 17, 1000, 0):
         d_n = torch.tensor([cnt], dtype=torch.int32, device="cuda:0")
         codes = torch.full((n,), 5, dtype=torch.int8, device="cuda:0")
         bm = torch.zeros((n + 63) // 64, dtype=torch.int64, device="cuda:0")
-        verifier.verify_dev_count(3 << 18, d_n, b.sigs, b.pubs, b.pool, b.msg_off, b.msg_sz, codes, bm)
+        verifier.verify_dev_count(n, d_n, b.sigs, b.pubs, b.pool, b.msg_off, b.msg_sz, codes, bm)
         verifier.sync()
         assert torch.equal(codes[:cnt], ref[:cnt]), cnt
         assert bool((codes[cnt:] == 5).all()), cnt
         bits = np.unpackbits(bm.cpu().numpy().view(np.uint8), bitorder="little")[:cnt].astype(bool)
         assert np.array_equal(bits, ref[:cnt].cpu().numpy() == 0), cnt
+
+
+def test_device_entry_points_reject_bad_buffers(verifier):
+    """Host arrays, short tensors and non-contiguous tensors are refused
+    before any launch (they would fault or read out of bounds on the GPU)."""
+    import torch
+    n = 1024
+    d = lambda k: torch.zeros(k, dtype=torch.uint8, device="cuda:0")  # noqa: E731
+    good = dict(sigs=d(64 * n), pubs=d(32 * n), pool=d(64), msg_off=d(4 * n), msg_sz=d(4 * n), codes=d(n))
+    args = lambda **kw: [kw.get(k, v) for k, v in good.items()]  # noqa: E731
+    with pytest.raises(TypeError):
+        verifier.verify_dev(n, *args(sigs=np.zeros(64 * n, np.uint8)))
+    with pytest.raises(ValueError):
+        verifier.verify_dev(n, *args(pubs=d(32 * n - 1)))
+    with pytest.raises(ValueError):
+        verifier.verify_dev(n, *args(codes=d(2 * n)[::2]))
+    with pytest.raises(ValueError):
+        verifier.verify_dev(n, *args(), bitmap=d(8))
