@@ -789,6 +789,7 @@ fd_ed25519_hip_verify_host( fd_ed25519_hip_ctx_t * ctx, ulong n, uchar const * s
                             uchar const * pool, ulong pool_sz, uint const * msg_off, uint const * msg_sz,
                             signed char * codes, ulong * bitmap ) {
   if( !n ) return 0;
+  for( ulong i=0; i<n; i++ ) if( (ulong)msg_off[i] + msg_sz[i] > pool_sz ) return -1;   /* device reads stay in the copy */
   FD_CHECK( hipSetDevice( ctx->device ) );
   ensure_staging( ctx, n, pool_sz, 0 );
   hipStream_t s = ctx->stream;

@@ -171,7 +171,8 @@ fd_ed25519_hip_verify_fixed_dev( fd_ed25519_hip_ctx_t * ctx,
                                  ulong *                d_bitmap,
                                  void *                 stream );
 
-/* Same from host memory, synchronous (copies in/out over PCIe). */
+/* Same from host memory, synchronous (copies in/out over PCIe).  Returns 0,
+   or -1 without touching the GPU if a message lies outside [0, pool_sz). */
 int
 fd_ed25519_hip_verify_host( fd_ed25519_hip_ctx_t * ctx,
                             ulong                  n,
