@@ -64,6 +64,15 @@ DEV void fe_inv2( fe & r )   { fe_set( r, 0x1ffffff7u,0x1fffffffu,0x1fffffffu,0x
 /* 64-bit multiply-accumulate kept in program order: the empty asm makes
    each partial sum opaque, so the compiler cannot re-associate a column into
    two half-chains joined by v_lshl_add_u64 (one extra 64-bit op per column). */
+/* split limbs pass through an empty asm so the compiler keeps the masked
+   limb instead of re-deriving 2*limb from the unmasked column as
+   (col << 1) & 0x3ffffffe (an extra v_and per limb in squaring chains) */
+#ifndef FE_NO_OPAQUE_LIMB
+#define FE_OPAQUE( x ) asm( "" : "+v"( x ) )
+#else
+#define FE_OPAQUE( x )
+#endif
+
 DEV u64 fe_mad64( u32 a, u32 b, u64 c ) { u64 r = c + (u64)a * b; asm( "" : "+v"(r) ); return r; }
 DEV u64 fe_mul64( u32 a, u32 b )        { u64 r = (u64)a * b;     asm( "" : "+v"(r) ); return r; }
 
@@ -112,7 +121,7 @@ DEV void fe_mulN( fe * const r[N], fe const * const a[N], fe const * const b[N] 
     for( int n=0; n<N; n++ ) {
       if( j < 8 ) l[n] = fe_mad64( (u32)h[n], 1216u, l[n] );
       if( j > 0 ) l[n] = fe_mad64( (u32)(hp[n] >> 32), 9728u, l[n] );
-      if( j < 8 ) { o[n][j] = (u32)l[n] & FE_M29; l[n] >>= 29; }
+      if( j < 8 ) { o[n][j] = (u32)l[n] & FE_M29; FE_OPAQUE( o[n][j] ); l[n] >>= 29; }
       hp[n] = h[n];
     }
   }
@@ -155,7 +164,7 @@ DEV void fe_sqN( fe * const r[N], fe const * const a[N] ) {
     for( int n=0; n<N; n++ ) {
       if( j < 8 ) l[n] = fe_mad64( (u32)h[n], 1216u, l[n] );
       if( j > 0 ) l[n] = fe_mad64( (u32)(hp[n] >> 32), 9728u, l[n] );
-      if( j < 8 ) { o[n][j] = (u32)l[n] & FE_M29; l[n] >>= 29; }
+      if( j < 8 ) { o[n][j] = (u32)l[n] & FE_M29; FE_OPAQUE( o[n][j] ); l[n] >>= 29; }
       hp[n] = h[n];
     }
   }
