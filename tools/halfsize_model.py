@@ -5,7 +5,8 @@ among three consecutive remainders and their +-1 combinations.
 
 Checks k1 == k*k2 (mod 8L), k2 odd and > 0, and prints the distribution of
 the window count D = floor(bits/4) + 1 (digits in [-7, 8]) per lane and per
-64-lane wave, and of the Euclid iteration count.
+64-lane wave (in index order, and after k_verify_scalar's bucketing of short
+and long lanes), and of the Euclid iteration count.
 
 Usage: python tools/halfsize_model.py [n]"""
 import collections
@@ -87,7 +88,12 @@ def main():
     for i in range(0, n, 64):
         wd[max(lane_d[i:i + 64])] += 1
         wi[max(lane_i[i:i + 64])] += 1
+    # k_verify_scalar's bucketing: lanes with D <= 32 listed first, the rest after
+    ld = lane_d[:n]
+    srt = [d for d in ld if d <= 32] + [d for d in ld if d > 32]
+    wb = [max(srt[i:i + 64]) for i in range(0, n, 64)]
     print("lane windows", sorted(D.items()))
+    print("bucketed wave windows mean", sum(wb) / len(wb), "lane mean", sum(ld) / len(ld))
     print("wave windows", sorted(wd.items()), "mean", sum(k * v for k, v in wd.items()) / sum(wd.values()))
     print("lane iters mean", sum(lane_i) / len(lane_i), "wave iters mean", sum(k * v for k, v in wi.items()) / sum(wi.values()),
           "max", max(lane_i))
