@@ -55,3 +55,25 @@ def test_device_constants():
     m = re.search(r"DEV void fe_sub\(.*?\n\}", src, re.S).group(0)
     c = [int(x, 16) for x in re.findall(r"\+ 0x([0-9a-f]+)u", m)]
     assert _limbs_to_int([c[0]] + [c[1]] * 7 + [c[2]]) == 2 * P
+
+
+def test_pack_layout_round_trip():
+    """fe_pack / fe_unpack's bit layout (8 words per element, one 30-bit limb):
+    fields tile [0, 256) exactly and a pack/unpack round trip is the identity
+    for limbs at their maximum widths."""
+    import random
+    rng = random.Random(5)
+    for w30 in (0, 1):
+        spans = [(B.pack_offset(w30, j), B.pack_width(w30, j)) for j in range(9)]
+        pos = 0
+        for o, w in spans:
+            assert o == pos
+            pos += w
+        assert pos == 256
+        cases = [[2**w - 1 for _, w in spans]] + [[rng.randrange(2**w) for _, w in spans] for _ in range(200)]
+        for limbs in cases:
+            x = sum(v << o for v, (o, _) in zip(limbs, spans))
+            words = [(x >> (32 * k)) & 0xffffffff for k in range(8)]
+            y = sum(wd << (32 * k) for k, wd in enumerate(words))
+            out = [(y >> o) & (2**w - 1) for o, w in spans]
+            assert out == limbs

@@ -148,6 +148,15 @@ def ge_add(P, q, affine):
     return [mul(E, Fs), mul(Gs, H), mul(F, G), mul(E, H)]
 
 
+def pack_width(w30, j):
+    """limb j's field width in an 8-word packed element (fe_pack_layout)"""
+    return 23 if j == 8 else (30 if j == w30 else 29)
+
+
+def pack_offset(w30, j):
+    return 0 if j == 0 else (0 if j <= w30 else 1) + 29 * j
+
+
 def check():
     pt = [TIGHT] * 4
     for needT in (False, True):
@@ -158,6 +167,10 @@ def check():
     for affine in (False, True, "z1"):
         r = ge_add(pt, entry, affine)
         assert all(le(o, TIGHT) for o in r), "add output not tight"
+    # packed table entries (fe_pack<W30>, fd_ed25519_hip.hip): Y-X, Y+X, 2Z
+    # with the wide limb 0, 2d*T with the wide limb 1
+    for e, w30 in zip(entry, (0, 0, 1, 0)):
+        assert all(v < 2**pack_width(w30, j) for j, v in enumerate(e)), "table element does not pack"
     # decode (ge_decode): y from words
     one = [1] + [0] * 8
     y2 = sq(WORDS)
