@@ -9,5 +9,5 @@ for v in "$@"; do
   i=$((i+1))
   if [ "$v" = default ]; then lib=""; else lib="$PWD/firedancer_amd/libfd_ed25519_hip_$v.so"; fi
   FD_ED25519_HIP_LIB=$lib timeout -k 10 300 python bench.py --no-cpu-baseline --steps ${STEPS:-10} --warmup 2 ${BENCH_ARGS} > gpurun_out/ab_$i.json 2> gpurun_out/ab_$i.err || { tail -20 gpurun_out/ab_$i.err; exit 1; }
-  python3 -c "import json; d=json.load(open('gpurun_out/ab_$i.json')); print('$v', d['value'], 'prep', d['pipeline']['prep_ms'], 'dsm', d['pipeline']['dsm_ms'])"
+  python3 -c "import json; d=json.load(open('gpurun_out/ab_$i.json')); p = d.get('pipeline') or {}; print('$v', d['value'], 'prep', p.get('prep_ms'), 'dsm', p.get('dsm_ms', d['roofline']['avg_launch_ms']))"
 done
