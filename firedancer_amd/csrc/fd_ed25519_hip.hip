@@ -85,7 +85,8 @@ struct fd_ed25519_hip_ctx {
   u32 *        d_state;     /* ST_WORDS * chunk */
   u32 *        d_atab;      /* ATAB_WORDS * chunk */
   u32 *        d_idx;       /* chunk: compacted survivor indices */
-  u32 *        d_count;     /* survivor count */
+  u32 *        d_count;     /* [0] survivor count; [16..47] k_msg_order's histogram and cursors */
+  u32 *        d_order;     /* chunk: k_verify_prep's record order (variable-size message paths) */
   int          errmode;
   int          halfsize;    /* 1: half-size scalars (default); 0: full-length (k, 1) */
   /* optional per-kernel timing (HIP events around each launch, on the launch stream) */
@@ -170,6 +171,55 @@ DEV int code_of( u32 f, int errmode, bool eq ) {
   return eq ? FD_ED25519_SUCCESS : FD_ED25519_ERR_MSG;
 }
 
+/* Records ordered by SHA-512 block count (variable-size message paths: the
+   txn stream, replay).  A wave hashes for its longest message, and a txn
+   stream mixes 2..10-block messages (≤1232-B payloads): in record order a
+   wave's maximum is ~9.3 blocks against a mean of ~3.8.  A counting sort on
+   the block count (keys clamped to 15) gives k_verify_prep an order[] in
+   which waves are uniform; records, state and codes keep their indices.
+   hist = count[16..31], cursor = count[32..47] (zeroed with count[0]). */
+#define ORD_KEYS 16
+DEV u32 msg_key( u32 sz ) { u32 b = (sz + 81u + 127u) >> 7; return b < 15u ? b : 15u; }
+
+DEV ulong dev_count_n( ulong n, u32 const * d_n, ulong rec0 ) {
+  if( !d_n ) return n;
+  ulong c = *d_n;
+  return c > rec0 ? (c - rec0 < n ? c - rec0 : n) : 0ul;
+}
+
+__global__ __launch_bounds__(256)
+void k_msg_hist( ulong n, uint const * __restrict__ msz, u32 * __restrict__ count, u32 const * __restrict__ d_n,
+                 ulong rec0 ) {
+  __shared__ u32 h[ORD_KEYS];
+  if( threadIdx.x < ORD_KEYS ) h[threadIdx.x] = 0u;
+  __syncthreads();
+  n = dev_count_n( n, d_n, rec0 );
+  ulong t = (ulong)blockIdx.x * blockDim.x + threadIdx.x;
+  if( t < n ) atomicAdd( &h[msg_key( msz[t] )], 1u );
+  __syncthreads();
+  if( threadIdx.x < ORD_KEYS && h[threadIdx.x] ) atomicAdd( count + 16 + threadIdx.x, h[threadIdx.x] );
+}
+
+__global__ __launch_bounds__(256)
+void k_msg_order( ulong n, uint const * __restrict__ msz, u32 * __restrict__ count, u32 const * __restrict__ d_n,
+                  ulong rec0, u32 * __restrict__ order ) {
+  __shared__ u32 h[ORD_KEYS], base[ORD_KEYS];
+  if( threadIdx.x < ORD_KEYS ) h[threadIdx.x] = 0u;
+  __syncthreads();
+  n = dev_count_n( n, d_n, rec0 );
+  ulong t = (ulong)blockIdx.x * blockDim.x + threadIdx.x;
+  u32 key = 0u, r = 0u;
+  if( t < n ) { key = msg_key( msz[t] ); r = atomicAdd( &h[key], 1u ); }   /* rank within the block */
+  __syncthreads();
+  if( threadIdx.x < ORD_KEYS ) {
+    u32 k = threadIdx.x, start = 0u;
+    for( u32 j=0; j<k; j++ ) start += count[16 + j];                      /* bucket start: prefix of hist */
+    base[k] = h[k] ? start + atomicAdd( count + 32 + k, h[k] ) : 0u;      /* this block's range */
+  }
+  __syncthreads();
+  if( t < n ) order[base[key] + r] = (u32)t;
+}
+
 /* FD_PREP_WAVES: waves per SIMD the register allocation of k_verify_prep is
    held to (0: compiler's choice) */
 #ifndef FD_PREP_WAVES
@@ -186,13 +236,16 @@ void k_verify_prep( ulong n, ulong chunk, uchar const * __restrict__ sigs, uchar
                     uchar const * __restrict__ pool, uint const * __restrict__ moff, uint const * __restrict__ msz,
                     u32 fixed_sz, u32 * __restrict__ st, int errmode, u32 * __restrict__ idx,
                     u32 * __restrict__ count, signed char * __restrict__ codes, u32 const * __restrict__ d_n,
-                    ulong rec0 ) {
-  ulong i = (ulong)blockIdx.x * blockDim.x + threadIdx.x;
+                    ulong rec0, u32 const * __restrict__ order ) {
+  ulong t = (ulong)blockIdx.x * blockDim.x + threadIdx.x;
   if( d_n ) {                                   /* device-side count: this chunk starts at record rec0 */
     ulong c = *d_n;
     n = c > rec0 ? (c - rec0 < n ? c - rec0 : n) : 0ul;
   }
-  bool active = i < n;
+  bool active = t < n;
+  /* order (k_msg_order): lane t takes record order[t], so a wave's lanes
+     hash messages of the same SHA-512 block count */
+  ulong i = active ? (order ? (ulong)order[t] : t) : 0ul;
   u32 flags = 0u;
   if( active ) {
   u32 * s = st + i;
@@ -629,6 +682,7 @@ fd_ed25519_hip_ctx_new( int device, ulong chunk_sigs ) {
   FD_CHECK( hipMalloc( (void **)&ctx->d_state, (size_t)ST_WORDS * chunk_sigs * sizeof(u32) ) );
   FD_CHECK( hipMalloc( (void **)&ctx->d_atab,  (size_t)ATAB_WORDS * chunk_sigs * sizeof(u32) ) );
   FD_CHECK( hipMalloc( (void **)&ctx->d_idx, chunk_sigs * sizeof(u32) ) );
+  FD_CHECK( hipMalloc( (void **)&ctx->d_order, chunk_sigs * sizeof(u32) ) );
   FD_CHECK( hipMalloc( (void **)&ctx->d_count, 256 ) );
   for( int e=0; e<4; e++ ) FD_CHECK( hipEventCreate( &ctx->ev[e] ) );
   hipLaunchKernelGGL( k_btab_init, dim3( (2*BTAB_N + 63)/64 ), dim3( 64 ), 0, ctx->stream, ctx->d_btab );
@@ -644,9 +698,11 @@ fd_ed25519_hip_ctx_reserve( fd_ed25519_hip_ctx_t * ctx, ulong chunk_sigs ) {
   FD_CHECK( hipSetDevice( ctx->device ) );
   FD_CHECK( hipDeviceSynchronize() );                      /* the scratch may be in use on any stream */
   (void)hipFree( ctx->d_state ); (void)hipFree( ctx->d_atab ); (void)hipFree( ctx->d_idx );
+  (void)hipFree( ctx->d_order );
   FD_CHECK( hipMalloc( (void **)&ctx->d_state, (size_t)ST_WORDS * chunk_sigs * sizeof(u32) ) );
   FD_CHECK( hipMalloc( (void **)&ctx->d_atab,  (size_t)ATAB_WORDS * chunk_sigs * sizeof(u32) ) );
   FD_CHECK( hipMalloc( (void **)&ctx->d_idx, chunk_sigs * sizeof(u32) ) );
+  FD_CHECK( hipMalloc( (void **)&ctx->d_order, chunk_sigs * sizeof(u32) ) );
   ctx->chunk = chunk_sigs;
 }
 
@@ -662,7 +718,7 @@ fd_ed25519_hip_ctx_delete( fd_ed25519_hip_ctx_t * ctx ) {
   (void)hipSetDevice( ctx->device );
   (void)hipStreamSynchronize( ctx->stream );
   (void)hipFree( ctx->d_btab ); (void)hipFree( ctx->d_state ); (void)hipFree( ctx->d_atab );
-  (void)hipFree( ctx->d_idx ); (void)hipFree( ctx->d_count );
+  (void)hipFree( ctx->d_idx ); (void)hipFree( ctx->d_order ); (void)hipFree( ctx->d_count );
   free_staging( ctx );
   for( int e=0; e<4; e++ ) (void)hipEventDestroy( ctx->ev[e] );
   (void)hipStreamDestroy( ctx->stream );
@@ -725,13 +781,22 @@ verify_impl( fd_ed25519_hip_ctx_t * ctx, ulong n, uchar const * d_sigs, uchar co
   for( ulong off = 0; off < n; off += ctx->chunk ) {
     ulong m = n - off < ctx->chunk ? n - off : ctx->chunk;
     dim3 grid( (unsigned)((m + 255) / 256) ), blk( 256 );
-    FD_CHECK( hipMemsetAsync( ctx->d_count, 0, sizeof(u32), s ) );
+    /* the txn paths (device-side count, variable-size messages) hash in
+       block-count order; fixed or uniform batches keep record order */
+    bool ordered = d_n && d_msg_off;
+    FD_CHECK( hipMemsetAsync( ctx->d_count, 0, (ordered ? 48 : 1)*sizeof(u32), s ) );
     if( ctx->timing ) FD_CHECK( hipEventRecord( ctx->ev[0], s ) );
+    if( ordered ) {
+      hipLaunchKernelGGL( k_msg_hist, grid, blk, 0, s, m, d_msg_sz + off, ctx->d_count, d_n, off );
+      FD_CHECK( hipGetLastError() );
+      hipLaunchKernelGGL( k_msg_order, grid, blk, 0, s, m, d_msg_sz + off, ctx->d_count, d_n, off, ctx->d_order );
+      FD_CHECK( hipGetLastError() );
+    }
     uchar const * pool = d_msg_off ? d_pool : d_pool + off*(ulong)fixed_sz;
     hipLaunchKernelGGL( k_verify_prep, grid, blk, 0, s, m, ctx->chunk, d_sigs + 64*off, d_pubs + 32*off,
                         pool, d_msg_off ? d_msg_off + off : (uint const *)0,
                         d_msg_off ? d_msg_sz + off : (uint const *)0, fixed_sz, ctx->d_state, ctx->errmode,
-                        ctx->d_idx, ctx->d_count, d_codes + off, d_n, off );
+                        ctx->d_idx, ctx->d_count, d_codes + off, d_n, off, ordered ? ctx->d_order : (u32 const *)0 );
     FD_CHECK( hipGetLastError() );
     if( ctx->timing ) FD_CHECK( hipEventRecord( ctx->ev[1], s ) );
     if( ctx->timing ) FD_CHECK( hipEventRecord( ctx->ev[3], s ) );
