@@ -260,3 +260,34 @@ def test_verify_host_large(verifier):
     codes2, _ = verifier.verify_host(sigs, pubs, pool, moff2, msz)
     assert np.array_equal(codes2[-5000:], exp)
     assert np.array_equal(codes2[:-5000], codes[:-5000])
+
+
+def test_dev_count_ordered_vs_oracle():
+    """The device-count path hashes in SHA-512 block-count order (k_msg_order).
+    Messages 0..2600 B (1..21 blocks; keys clamp at 15) with C2 mutations,
+    several 256-record chunks, device-side counts ending mid-chunk, on a chunk
+    boundary and at zero: codes equal the oracle's record by record, codes
+    past the count are untouched."""
+    import torch
+    from firedancer_amd import Verifier
+    rng, prvs, pubs, sigs, pool, moff, msz = _random_set(1500, 0x0bd, max_msg=2600)
+    c2_mutate(sigs, pubs, rng)
+    exp = O.verify_many(sigs, pubs, pool, moff, msz)
+    dev = torch.device("cuda", 0)
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)  # noqa: E731
+    d_sigs, d_pubs, d_pool = t(sigs.reshape(-1)), t(pubs.reshape(-1)), t(pool)
+    d_moff, d_msz = t(moff.view(np.int32)), t(msz.view(np.int32))
+    n = sigs.shape[0]
+    v = Verifier(device=0, chunk_sigs=256)
+    try:
+        for cnt in (n, 1000, 768, 77, 0):
+            d_n = torch.tensor([cnt], dtype=torch.int32, device=dev)
+            codes = torch.full((n,), 5, dtype=torch.int8, device=dev)
+            v.verify_dev_count(n, d_n, d_sigs, d_pubs, d_pool, d_moff, d_msz, codes)
+            v.sync()
+            c = codes.cpu().numpy()
+            bad = np.nonzero(c[:cnt] != exp[:cnt])[0]
+            assert bad.size == 0, (cnt, [(int(i), int(c[i]), int(exp[i]), int(msz[i])) for i in bad[:10]])
+            assert (c[cnt:] == 5).all(), cnt
+    finally:
+        v.close()
