@@ -64,8 +64,13 @@
 #else
 #define ATAB_ENT    36             /* cached: YmX, YpX, T2d, Z2 (9 limbs each) */
 #endif
-#define RTAB_OFF    (9*ATAB_ENT)   /* per lane: [0..8](+-A), then [0..8](-R) */
+#define RTAB_OFF    (8*ATAB_ENT)   /* per lane: [1..8](+-A), then [1..8](-R) */
 #define ATAB_WORDS  (2*RTAB_OFF)
+/* the identity entry (digit 0) is shared by every lane: one line in d_btab
+   after the two B tables (128-B aligned), hot in cache, never written per
+   signature */
+#define IDENT_OFF   ((2*BTAB_WORDS + 31) & ~31)
+#define BTAB_ALLOC  (IDENT_OFF + ATAB_ENT)
 
 /* state record: 32 u32 words per field group, laid out SoA per chunk for
    coalescing: word w of signature i lives at st[ w*chunk + i ]. */
@@ -135,6 +140,8 @@ DEV void ge_to_affc_half( ge_affc & a, ge_p3 const & p ) {
    fd_curve25519_table_ref.c:32; ours holds all multiples 0..128 for signed
    radix-256 windows, and a second table for the high half of the
    half-size-scalar B coefficient, see sc_halfsize). */
+DEV void store_cached( u32 * t, ge_cached const & c );   /* A/R table entry layout, below */
+
 __global__ __launch_bounds__(64) void k_btab_init( u32 * btab ) {
   int j = blockIdx.x * blockDim.x + threadIdx.x;
   if( j >= 2*BTAB_N ) return;
@@ -153,6 +160,11 @@ __global__ __launch_bounds__(64) void k_btab_init( u32 * btab ) {
   #pragma unroll
   for( int i=0; i<9; i++ ) { e[i] = a.YmX.v[i]; e[9+i] = a.YpX.v[i]; e[18+i] = a.T2d.v[i]; }
   e[27] = 0u;
+  if( j == 0 && blockIdx.x == 0 ) {             /* the shared identity entry of the A/R tables */
+    ge_cached c;
+    fe_1( c.YmX ); fe_1( c.YpX ); fe_0( c.T2d ); fe_set( c.Z2, 2,0,0,0,0,0,0,0,0 );
+    store_cached( btab + IDENT_OFF, c );
+  }
 }
 
 DEV int code_of( u32 f, int errmode, bool eq ) {
@@ -399,21 +411,29 @@ void k_bitmap( ulong n, signed char const * __restrict__ codes, ulong * __restri
   if( (threadIdx.x & 63u) == 0u && i < n ) bitmap[i >> 6] = b;
 }
 
-/* table [0..8]Q in cached form for Q = (qx, qy) affine (fd_curve25519.c:
-   130-143): identity, Q, 2Q, then (j+1)Q = jQ + Q -- a chain keeps one point
-   and Q's cached form live */
+/* table [1..8]Q in cached form for Q = (qx, qy) affine (fd_curve25519.c:
+   130-143), entry j at (j-1)*ATAB_ENT (the identity is the shared entry at
+   IDENT_OFF): Q, 2Q, then (j+1)Q = jQ + Q -- a chain keeps one point and Q's
+   cached form live */
 DEV void build_cached_table( u32 * tab, fe const & qx, fe const & qy ) {
   ge_p3 Q; Q.X = qx; Q.Y = qy; fe_1( Q.Z ); fe_mul( Q.T, Q.X, Q.Y );
   ge_cached c;
-  fe_1( c.YmX ); fe_1( c.YpX ); fe_0( c.T2d ); fe_set( c.Z2, 2,0,0,0,0,0,0,0,0 );
-  store_cached( tab + 0*ATAB_ENT, c );                                  /* identity */
-  ge_cached c1; ge_to_cached( c1, Q ); store_cached( tab + 1*ATAB_ENT, c1 );
+  ge_cached c1; ge_to_cached( c1, Q ); store_cached( tab + 0*ATAB_ENT, c1 );
   ge_p3 Pj;
-  ge_dbl( Pj, Q, true ); ge_to_cached( c, Pj ); store_cached( tab + 2*ATAB_ENT, c );
+  ge_dbl( Pj, Q, true ); ge_to_cached( c, Pj ); store_cached( tab + 1*ATAB_ENT, c );
   #pragma unroll 1
   for( int j=3; j<=8; j++ ) {
-    ge_add_cached_z1( Pj, Pj, c1 ); ge_to_cached( c, Pj ); store_cached( tab + j*ATAB_ENT, c );
+    ge_add_cached_z1( Pj, Pj, c1 ); ge_to_cached( c, Pj ); store_cached( tab + (j-1)*ATAB_ENT, c );
   }
+}
+
+/* entry for digit magnitude mag in 0..8: the lane's table, or the shared
+   identity for 0 (a select by mask, no v_cndmask) */
+DEV u32 const * tab_entry( u32 const * tab, u32 const * ident, u32 mag ) {
+  u32 m = (u32)((int)(0u - mag) >> 31);                 /* mag != 0 ? ~0 : 0 */
+  u64 t = (u64)(tab + ((mag - 1u) & m) * ATAB_ENT), id = (u64)ident;
+  u64 mm = ((u64)m << 32) | m;
+  return (u32 const *)(id ^ ((t ^ id) & mm));
 }
 
 /* biased signed digit -> (negate mask, magnitude) */
@@ -501,6 +521,7 @@ void k_verify_dsm( ulong chunk, u32 const * __restrict__ st, u32 const * __restr
 
     /* ---- tables [0..8](+-A) and [0..8](-R) (fd_curve25519.c:130-143) ---- */
     u32 * tabA = atab + ii * ATAB_WORDS, * tabR = tabA + RTAB_OFF;
+    u32 const * ident = btab + IDENT_OFF;
     {
       fe x, y, nx;
       u32 xw[8], yw[8];
@@ -525,14 +546,14 @@ void k_verify_dsm( ulong chunk, u32 const * __restrict__ st, u32 const * __restr
       digit_split( kd1[7] >> 28, 7u, nega, ia ); digits_shl( kd1, 4u );
       digit_split( kd2[7] >> 28, 7u, negr, ir ); digits_shl( kd2, 4u );
       /* issued before the window's 4 doublings, which hide its latency */
-      ge_cached e; load_cached( e, tabA + ia*ATAB_ENT );
+      ge_cached e; load_cached( e, tab_entry( tabA, ident, ia ) );
       if( w != (int)D-1 ) {
         #pragma unroll 1
         for( int j=0; j<3; j++ ) ge_dbl( P, P, false );
         ge_dbl( P, P, true );
       }
       ge_add_cached( P, P, e, nega, true );
-      load_cached( e, tabR + ir*ATAB_ENT );
+      load_cached( e, tab_entry( tabR, ident, ir ) );
       bool bw = (w & 1) == 0 && w <= 30;
       ge_add_cached( P, P, e, negr, bw );
       if( bw ) {
@@ -678,7 +699,7 @@ fd_ed25519_hip_ctx_new( int device, ulong chunk_sigs ) {
   ctx->halfsize = 1;
   FD_CHECK( hipSetDevice( device ) );
   FD_CHECK( hipStreamCreateWithFlags( &ctx->stream, hipStreamNonBlocking ) );
-  FD_CHECK( hipMalloc( (void **)&ctx->d_btab,  2 * BTAB_WORDS * sizeof(u32) ) );
+  FD_CHECK( hipMalloc( (void **)&ctx->d_btab,  BTAB_ALLOC * sizeof(u32) ) );
   FD_CHECK( hipMalloc( (void **)&ctx->d_state, (size_t)ST_WORDS * chunk_sigs * sizeof(u32) ) );
   FD_CHECK( hipMalloc( (void **)&ctx->d_atab,  (size_t)ATAB_WORDS * chunk_sigs * sizeof(u32) ) );
   FD_CHECK( hipMalloc( (void **)&ctx->d_idx, chunk_sigs * sizeof(u32) ) );
