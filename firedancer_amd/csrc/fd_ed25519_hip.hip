@@ -481,12 +481,17 @@ void k_verify_dsm( ulong chunk, u32 const * __restrict__ st, u32 const * __restr
   {
     /* 28.9 KB: all of a thread's 16-B loads in flight before the LDS stores
        (a load-store loop waits out one L2 round trip per iteration) */
-    constexpr int NQ = 2*BTAB_WORDS/4, PER = (NQ + 255)/256;
-    uint4 v[PER];
+    /* the full rounds unconditionally and the partial one apart: with a
+       guard on every round the array went to scratch (144 B per lane) */
+    constexpr int NQ = 2*BTAB_WORDS/4, FULL = NQ/256;
+    uint4 v[FULL], last = make_uint4( 0u, 0u, 0u, 0u );
+    bool has_last = (int)threadIdx.x + 256*FULL < NQ;
     #pragma unroll
-    for( int u=0; u<PER; u++ ) { int q = threadIdx.x + 256*u; if( q < NQ ) v[u] = ((uint4 const *)btab)[q]; }
+    for( int u=0; u<FULL; u++ ) v[u] = ((uint4 const *)btab)[threadIdx.x + 256*u];
+    if( has_last ) last = ((uint4 const *)btab)[threadIdx.x + 256*FULL];
     #pragma unroll
-    for( int u=0; u<PER; u++ ) { int q = threadIdx.x + 256*u; if( q < NQ ) ((uint4 *)lds_btab)[q] = v[u]; }
+    for( int u=0; u<FULL; u++ ) ((uint4 *)lds_btab)[threadIdx.x + 256*u] = v[u];
+    if( has_last ) ((uint4 *)lds_btab)[threadIdx.x + 256*FULL] = last;
   }
   __syncthreads();
   if( t >= m ) return;
