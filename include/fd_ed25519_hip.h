@@ -92,7 +92,7 @@ typedef struct fd_ed25519_hip_ctx fd_ed25519_hip_ctx_t;
 fd_ed25519_hip_ctx_t * fd_ed25519_hip_ctx_new   ( int device, ulong chunk_sigs );
 void                   fd_ed25519_hip_ctx_delete( fd_ed25519_hip_ctx_t * ctx );
 int                    fd_ed25519_hip_ctx_device( fd_ed25519_hip_ctx_t const * ctx );
-/* Grow the per-launch scratch to at least chunk_sigs signatures (1.5 KB of
+/* Grow the per-launch scratch to at least chunk_sigs signatures (2.3 KB of
    HBM each); waits for the device to go idle first.  A caller whose record
    count is only known on the device (verify_dev_count) reserves its upper
    bound so one launch pair covers it. */
