@@ -32,9 +32,9 @@ method the GPU uses.  k_verify_dsm runs half-size scalars (k1, k2 ~ 2^128
 with k1 = k*k2 mod 8L, see sc_halfsize): 4*(D-1) doublings for D ~ 33.2
 windows per wave instead of 252, so it executes ~5.05e5 op-equivalents per
 signature (W_DSM_EXEC: 1261.8 M + 522.7 S + ~1.65e4 for the reduction), not
-6.08e5.  "frac" prices the kernel's own work (W_DSM_EXEC); "ref_work_frac"
-keeps the 8(d) definition, which exceeds 1 once the kernel does less work
-than the reference algorithm at more than 83% of the peak.
+6.08e5.  "frac" keeps the 8(d) definition (the contract's per-unit figure),
+which passes 1 once the kernel runs its smaller work at more than 83% of
+the peak; "executed_frac" prices the kernel's own work (W_DSM_EXEC).
 
 cpu_baseline (rank 0, N=1): the reference's own fd_ed25519_verify (AVX-512
 IFMA build, compiled from the reference sources into oracle/_ref/) on a
@@ -263,10 +263,10 @@ def main():
     dsm_avg_ms = dsm_ms / max(launches, 1)
     prep_avg_ms = prep_ms / max(launches, 1)
     units_per_launch = reached_dsm / launches_per_step
-    # T int32-ops/s per GPU: the kernel's own (half-size) work, and the 8(d)
-    # figure that prices the reference algorithm's larger work
-    achieved = units_per_launch * W_DSM_EXEC / (dsm_avg_ms * 1e-3) / 1e12
-    achieved_ref = units_per_launch * W_DSM / (dsm_avg_ms * 1e-3) / 1e12
+    # T int32-ops/s per GPU: SURVEY 8(d)'s per-unit W (the reference
+    # algorithm's work), and the kernel's own smaller half-size work
+    achieved = units_per_launch * W_DSM / (dsm_avg_ms * 1e-3) / 1e12
+    achieved_exec = units_per_launch * W_DSM_EXEC / (dsm_avg_ms * 1e-3) / 1e12
     peak = PEAK_OPS / 1e12
     # whole pipeline (prep + DSM): the prep work (decodes + hash) for every
     # signature, the DSM work only for those that pass the pre-checks
@@ -326,20 +326,21 @@ def main():
                          "achieved": round(achieved, 3), "peak": round(peak, 3), "unit": "Tops/s",
                          "frac": round(achieved / peak, 4), "traffic": traffic, "traffic_unit": "bytes/launch",
                          "traffic_source": traffic_src,
-                         "algorithmic_ops_per_unit": round(W_DSM_EXEC), "units_per_launch": round(units_per_launch),
+                         "algorithmic_ops_per_unit": round(W_DSM), "units_per_launch": round(units_per_launch),
                          "avg_launch_ms": round(dsm_avg_ms, 4),
-                         "ref_work_ops_per_unit": round(W_DSM),
-                         "ref_work_frac": round(achieved_ref / peak, 4),
-                         "ref_work_note": "SURVEY 8(d) W: the reference algorithm's (full-length scalar) work per "
-                                          "verify, larger than the half-size kernel's own, so this can exceed 1",
+                         "executed_ops_per_unit": round(W_DSM_EXEC),
+                         "executed_frac": round(achieved_exec / peak, 4),
+                         "frac_note": "achieved/frac use SURVEY 8(d)'s per-unit W, the reference algorithm's "
+                                      "(full-length scalar) work; the half-size kernel does 17% less, so frac can "
+                                      "pass 1 -- executed_frac prices the kernel's own work",
                          "timing_leg": "after the timed steps: the whole batch through one context, HIP events "
                                        "around each launch, each k_verify_dsm alone on the GPU"},
             "pipeline": {"prep_ms": round(prep_avg_ms, 4), "dsm_ms": round(dsm_avg_ms, 4),
                          "w_total_per_verify": round(w_total(msg_sz)),
-                         "int32_valu_frac": round(pipeline_exec_frac, 4),
-                         "ref_work_frac": round(pipeline_frac, 4),
+                         "int32_valu_frac": round(pipeline_frac, 4),
+                         "executed_frac": round(pipeline_exec_frac, 4),
                          "frac_note": "prep work (decodes + hash) for every signature, DSM work for those "
-                                      "reaching it; ref_work_frac prices the DSM at 8(d)'s reference-algorithm W",
+                                      "reaching it, at 8(d)'s W; executed_frac prices the DSM at its own work",
                          "ingest_GBps": round(ingest_gbps, 2), "ingest_bytes_per_sig": ingest_bytes},
             "cpu_baseline": cpu,
         }
@@ -492,7 +493,7 @@ def run_c4(args, rank, world, local, dist):
         counts = {int(a): int(b) for a, b in zip(*np.unique(res, return_counts=True))}
         names = {0: "publish", -1: "verify_fail", -2: "dedup", -3: "parse_fail", -4: "bundle_peer_fail"}
         dsm_avg = dsm_ms / launches
-        achieved = dsm_units / launches * W_DSM_EXEC / (dsm_avg * 1e-3) / 1e12
+        achieved = dsm_units / launches * W_DSM / (dsm_avg * 1e-3) / 1e12
         out = {
             "metric": METRIC,
             "value": round(sigs / elapsed, 1),
@@ -519,8 +520,8 @@ def run_c4(args, rank, world, local, dist):
             "roofline": {"bound": "valu_int32", "kernel": "k_verify_dsm",
                          "achieved": round(achieved, 3), "peak": round(PEAK_OPS / 1e12, 3), "unit": "Tops/s",
                          "frac": round(achieved / (PEAK_OPS / 1e12), 4), "traffic": None,
-                         "algorithmic_ops_per_unit": round(W_DSM_EXEC), "units_per_launch": round(dsm_units / launches),
-                         "ref_work_frac": round(achieved * W_DSM / W_DSM_EXEC / (PEAK_OPS / 1e12), 4),
+                         "algorithmic_ops_per_unit": round(W_DSM), "units_per_launch": round(dsm_units / launches),
+                         "executed_frac": round(achieved * W_DSM_EXEC / W_DSM / (PEAK_OPS / 1e12), 4),
                          "avg_launch_ms": round(dsm_avg, 4), "launches_per_batch": launches,
                          "prep_ms_per_batch": round(prep_ms, 4)},
             "cpu_baseline": cpu,
