@@ -65,7 +65,10 @@
 #define ATAB_ENT    36             /* cached: YmX, YpX, T2d, Z2 (9 limbs each) */
 #endif
 #define RTAB_OFF    (8*ATAB_ENT)   /* per lane: [1..8](+-A), then [1..8](-R) */
-#define ATAB_WORDS  (2*RTAB_OFF)
+#ifndef FD_ATAB_PAD
+#define FD_ATAB_PAD 0              /* words of padding after each lane's tables (lane stride) */
+#endif
+#define ATAB_WORDS  (2*RTAB_OFF + FD_ATAB_PAD)
 /* the identity entry (digit 0) is shared by every lane: one line in d_btab
    after the two B tables (128-B aligned), hot in cache, never written per
    signature */
@@ -91,6 +94,7 @@ struct fd_ed25519_hip_ctx {
   u32 *        d_atab;      /* ATAB_WORDS * chunk */
   u32 *        d_idx;       /* chunk: compacted survivor indices */
   u32 *        d_count;     /* [0] survivor count; [16..47] k_msg_order's histogram and cursors */
+  ulong        dsm_wgs;     /* resident k_verify_dsm workgroups (FD_DSM_PERSIST grid) */
   u32 *        d_order;     /* chunk: k_verify_prep's record order (variable-size message paths) */
   int          errmode;
   int          halfsize;    /* 1: half-size scalars (default); 0: full-length (k, 1) */
@@ -461,8 +465,15 @@ DEV u32 wave_max7( u32 v ) {
 
 /* FD_DSM_WAVES: waves per SIMD the register allocation of k_verify_dsm is
    held to (0: compiler's choice) */
+#ifndef FD_DSM_PERSIST
+#define FD_DSM_PERSIST 1
+#endif
 #ifndef FD_DSM_WAVES
+#if FD_DSM_PERSIST
+#define FD_DSM_WAVES 3      /* the task loop alone takes the compiler to 172 VGPRs (2 waves) */
+#else
 #define FD_DSM_WAVES 0
+#endif
 #endif
 #if FD_DSM_WAVES
 #define DSM_OCCUPANCY __attribute__((amdgpu_waves_per_eu(FD_DSM_WAVES, FD_DSM_WAVES)))
@@ -470,31 +481,10 @@ DEV u32 wave_max7( u32 v ) {
 #define DSM_OCCUPANCY
 #endif
 
-__global__ __launch_bounds__(256) DSM_OCCUPANCY
-void k_verify_dsm( ulong chunk, u32 const * __restrict__ st, u32 const * __restrict__ btab,
-                   u32 * __restrict__ atab, u32 const * __restrict__ idx, u32 const * __restrict__ count,
-                   signed char * __restrict__ codes, int halfsize ) {
-  ulong t = (ulong)blockIdx.x * blockDim.x + threadIdx.x;
-  u32 m = *count;
-  if( (ulong)blockIdx.x * blockDim.x >= m ) return;        /* whole workgroup past the survivors */
-  __shared__ __attribute__((aligned(16))) u32 lds_btab[2*BTAB_WORDS];
-  {
-    /* 28.9 KB: all of a thread's 16-B loads in flight before the LDS stores
-       (a load-store loop waits out one L2 round trip per iteration) */
-    /* the full rounds unconditionally and the partial one apart: with a
-       guard on every round the array went to scratch (144 B per lane) */
-    constexpr int NQ = 2*BTAB_WORDS/4, FULL = NQ/256;
-    uint4 v[FULL], last = make_uint4( 0u, 0u, 0u, 0u );
-    bool has_last = (int)threadIdx.x + 256*FULL < NQ;
-    #pragma unroll
-    for( int u=0; u<FULL; u++ ) v[u] = ((uint4 const *)btab)[threadIdx.x + 256*u];
-    if( has_last ) last = ((uint4 const *)btab)[threadIdx.x + 256*FULL];
-    #pragma unroll
-    for( int u=0; u<FULL; u++ ) ((uint4 *)lds_btab)[threadIdx.x + 256*u] = v[u];
-    if( has_last ) ((uint4 *)lds_btab)[threadIdx.x + 256*FULL] = last;
-  }
-  __syncthreads();
-  if( t >= m ) return;
+/* one survivor: DSM slot t (tables at slot t), record idx[t] */
+DEV void dsm_verify_slot( ulong t, ulong chunk, u32 const * __restrict__ st, u32 const * __restrict__ btab,
+                          u32 * __restrict__ atab, u32 const * __restrict__ idx, u32 const * lds_btab,
+                          signed char * __restrict__ codes, int halfsize ) {
   ulong i = idx[t];
   ulong ii = t;                                            /* table slot: dense in t */
   u32 const * s = st + i;
@@ -578,6 +568,51 @@ void k_verify_dsm( ulong chunk, u32 const * __restrict__ st, u32 const * __restr
     eq = fe_is_zero_c( x ) && fe_eq_c( y, z );
   }
   codes[i] = (signed char)(eq ? FD_ED25519_SUCCESS : FD_ED25519_ERR_MSG);   /* user.c:226-229 */
+}
+
+/* FD_DSM_PERSIST: resident workgroups (ctx->dsm_wgs, ~3 per CU) pull 64-survivor
+   tasks from a counter (count[1]) until none is left, instead of one
+   workgroup per 256 survivors: no partial last round of waves, and one LDS
+   B-table copy per resident workgroup.  Every wave leaves the loop when the
+   counter passes m, so the grid drains. */
+
+__global__ __launch_bounds__(256) DSM_OCCUPANCY
+void k_verify_dsm( ulong chunk, u32 const * __restrict__ st, u32 const * __restrict__ btab,
+                   u32 * __restrict__ atab, u32 const * __restrict__ idx, u32 * __restrict__ count,
+                   signed char * __restrict__ codes, int halfsize ) {
+  u32 m = count[0];
+  if( (ulong)blockIdx.x * blockDim.x >= m ) return;        /* whole workgroup past the survivors */
+  __shared__ __attribute__((aligned(16))) u32 lds_btab[2*BTAB_WORDS];
+  {
+    /* 28.9 KB: all of a thread's 16-B loads in flight before the LDS stores
+       (a load-store loop waits out one L2 round trip per iteration) */
+    /* the full rounds unconditionally and the partial one apart: with a
+       guard on every round the array went to scratch (144 B per lane) */
+    constexpr int NQ = 2*BTAB_WORDS/4, FULL = NQ/256;
+    uint4 v[FULL], last = make_uint4( 0u, 0u, 0u, 0u );
+    bool has_last = (int)threadIdx.x + 256*FULL < NQ;
+    #pragma unroll
+    for( int u=0; u<FULL; u++ ) v[u] = ((uint4 const *)btab)[threadIdx.x + 256*u];
+    if( has_last ) last = ((uint4 const *)btab)[threadIdx.x + 256*FULL];
+    #pragma unroll
+    for( int u=0; u<FULL; u++ ) ((uint4 *)lds_btab)[threadIdx.x + 256*u] = v[u];
+    if( has_last ) ((uint4 *)lds_btab)[threadIdx.x + 256*FULL] = last;
+  }
+  __syncthreads();
+#if FD_DSM_PERSIST
+  for( ;; ) {
+    u32 task = 0u;
+    if( (threadIdx.x & 63u) == 0u ) task = atomicAdd( count + 1, 1u );
+    task = __shfl( task, 0 );
+    if( (ulong)task * 64ul >= (ulong)m ) break;                       /* wave-uniform exit */
+    ulong t = (ulong)task * 64ul + (threadIdx.x & 63u);
+    if( t < m ) dsm_verify_slot( t, chunk, st, btab, atab, idx, lds_btab, codes, halfsize );
+  }
+#else
+  ulong t = (ulong)blockIdx.x * blockDim.x + threadIdx.x;
+  if( t >= m ) return;
+  dsm_verify_slot( t, chunk, st, btab, atab, idx, lds_btab, codes, halfsize );
+#endif
 }
 
 /* fd_ed25519_verify_batch_single_msg (user.c:232-310) over per-sig codes */
@@ -711,6 +746,12 @@ fd_ed25519_hip_ctx_new( int device, ulong chunk_sigs ) {
   FD_CHECK( hipMalloc( (void **)&ctx->d_order, chunk_sigs * sizeof(u32) ) );
   FD_CHECK( hipMalloc( (void **)&ctx->d_count, 256 ) );
   for( int e=0; e<4; e++ ) FD_CHECK( hipEventCreate( &ctx->ev[e] ) );
+  {
+    int ncu = 0, per = 0;
+    FD_CHECK( hipDeviceGetAttribute( &ncu, hipDeviceAttributeMultiprocessorCount, device ) );
+    FD_CHECK( hipOccupancyMaxActiveBlocksPerMultiprocessor( &per, k_verify_dsm, 256, 0 ) );
+    ctx->dsm_wgs = (ulong)(ncu > 0 ? ncu : 1) * (ulong)(per > 0 ? per : 1);
+  }
   hipLaunchKernelGGL( k_btab_init, dim3( (2*BTAB_N + 63)/64 ), dim3( 64 ), 0, ctx->stream, ctx->d_btab );
   FD_CHECK( hipGetLastError() );
   FD_CHECK( hipStreamSynchronize( ctx->stream ) );
@@ -810,7 +851,7 @@ verify_impl( fd_ed25519_hip_ctx_t * ctx, ulong n, uchar const * d_sigs, uchar co
     /* the txn paths (device-side count, variable-size messages) hash in
        block-count order; fixed or uniform batches keep record order */
     bool ordered = d_n && d_msg_off;
-    FD_CHECK( hipMemsetAsync( ctx->d_count, 0, (ordered ? 48 : 1)*sizeof(u32), s ) );
+    FD_CHECK( hipMemsetAsync( ctx->d_count, 0, (ordered ? 48 : 2)*sizeof(u32), s ) );
     if( ctx->timing ) FD_CHECK( hipEventRecord( ctx->ev[0], s ) );
     if( ordered ) {
       hipLaunchKernelGGL( k_msg_hist, grid, blk, 0, s, m, d_msg_sz + off, ctx->d_count, d_n, off );
@@ -826,7 +867,8 @@ verify_impl( fd_ed25519_hip_ctx_t * ctx, ulong n, uchar const * d_sigs, uchar co
     FD_CHECK( hipGetLastError() );
     if( ctx->timing ) FD_CHECK( hipEventRecord( ctx->ev[1], s ) );
     if( ctx->timing ) FD_CHECK( hipEventRecord( ctx->ev[3], s ) );
-    hipLaunchKernelGGL( k_verify_dsm, grid, blk, 0, s, ctx->chunk, ctx->d_state, ctx->d_btab, ctx->d_atab,
+    dim3 gdsm( FD_DSM_PERSIST && grid.x > ctx->dsm_wgs ? (unsigned)ctx->dsm_wgs : grid.x );
+    hipLaunchKernelGGL( k_verify_dsm, gdsm, blk, 0, s, ctx->chunk, ctx->d_state, ctx->d_btab, ctx->d_atab,
                         ctx->d_idx, ctx->d_count, d_codes + off, ctx->halfsize );
     FD_CHECK( hipGetLastError() );
     if( d_bitmap ) {
