@@ -95,6 +95,7 @@ struct fd_ed25519_hip_ctx {
   u32 *        d_idx;       /* chunk: compacted survivor indices */
   u32 *        d_count;     /* [0] survivor count; [16..47] k_msg_order's histogram and cursors */
   ulong        dsm_wgs;     /* resident k_verify_dsm workgroups (FD_DSM_PERSIST grid) */
+  ulong        prep_wgs;    /* resident k_verify_prep workgroups (FD_PREP_PERSIST grid) */
   u32 *        d_order;     /* chunk: k_verify_prep's record order (variable-size message paths) */
   int          errmode;
   int          halfsize;    /* 1: half-size scalars (default); 0: full-length (k, 1) */
@@ -247,17 +248,12 @@ void k_msg_order( ulong n, uint const * __restrict__ msz, u32 * __restrict__ cou
 #define PREP_OCCUPANCY
 #endif
 
-__global__ __launch_bounds__(256) PREP_OCCUPANCY
-void k_verify_prep( ulong n, ulong chunk, uchar const * __restrict__ sigs, uchar const * __restrict__ pubs,
+/* one record slot t of the chunk (n records): checks, decodes, hash, and the
+   wave's survivor compaction (all 64 lanes of the wave take part) */
+DEV void prep_slot( ulong t, ulong n, ulong chunk, uchar const * __restrict__ sigs, uchar const * __restrict__ pubs,
                     uchar const * __restrict__ pool, uint const * __restrict__ moff, uint const * __restrict__ msz,
                     u32 fixed_sz, u32 * __restrict__ st, int errmode, u32 * __restrict__ idx,
-                    u32 * __restrict__ count, signed char * __restrict__ codes, u32 const * __restrict__ d_n,
-                    ulong rec0, u32 const * __restrict__ order ) {
-  ulong t = (ulong)blockIdx.x * blockDim.x + threadIdx.x;
-  if( d_n ) {                                   /* device-side count: this chunk starts at record rec0 */
-    ulong c = *d_n;
-    n = c > rec0 ? (c - rec0 < n ? c - rec0 : n) : 0ul;
-  }
+                    u32 * __restrict__ count, signed char * __restrict__ codes, u32 const * __restrict__ order ) {
   bool active = t < n;
   /* order (k_msg_order): lane t takes record order[t], so a wave's lanes
      hash messages of the same SHA-512 block count */
@@ -322,6 +318,37 @@ void k_verify_prep( ulong n, ulong chunk, uchar const * __restrict__ sigs, uchar
   base = __shfl( base, 0 );
   u32 below = (u32)__popcll( m & ((1ULL << lane) - 1ULL) );
   if( pass ) idx[base + below] = (u32)i;
+}
+
+/* FD_PREP_PERSIST: resident workgroups pull 64-record tasks from count[2]
+   (as k_verify_dsm does from count[1]); every wave leaves when the counter
+   passes n.  Off: measured A/B on C2, prep 1.98-2.07 vs 1.96-1.98 ms
+   (116.7-117.9 vs 118.3-118.6 M verifies/s); C4 was within noise. */
+#ifndef FD_PREP_PERSIST
+#define FD_PREP_PERSIST 0
+#endif
+
+__global__ __launch_bounds__(256) PREP_OCCUPANCY
+void k_verify_prep( ulong n, ulong chunk, uchar const * __restrict__ sigs, uchar const * __restrict__ pubs,
+                    uchar const * __restrict__ pool, uint const * __restrict__ moff, uint const * __restrict__ msz,
+                    u32 fixed_sz, u32 * __restrict__ st, int errmode, u32 * __restrict__ idx,
+                    u32 * __restrict__ count, signed char * __restrict__ codes, u32 const * __restrict__ d_n,
+                    ulong rec0, u32 const * __restrict__ order ) {
+  n = dev_count_n( n, d_n, rec0 );            /* device-side count: this chunk starts at record rec0 */
+  if( (ulong)blockIdx.x * blockDim.x >= n ) return;
+#if FD_PREP_PERSIST
+  for( ;; ) {
+    u32 task = 0u;
+    if( (threadIdx.x & 63u) == 0u ) task = atomicAdd( count + 2, 1u );
+    task = __shfl( task, 0 );
+    if( (ulong)task * 64ul >= n ) break;                              /* wave-uniform exit */
+    prep_slot( (ulong)task * 64ul + (threadIdx.x & 63u), n, chunk, sigs, pubs, pool, moff, msz, fixed_sz, st,
+               errmode, idx, count, codes, order );
+  }
+#else
+  prep_slot( (ulong)blockIdx.x * blockDim.x + threadIdx.x, n, chunk, sigs, pubs, pool, moff, msz, fixed_sz, st,
+             errmode, idx, count, codes, order );
+#endif
 }
 
 
@@ -751,6 +778,9 @@ fd_ed25519_hip_ctx_new( int device, ulong chunk_sigs ) {
     FD_CHECK( hipDeviceGetAttribute( &ncu, hipDeviceAttributeMultiprocessorCount, device ) );
     FD_CHECK( hipOccupancyMaxActiveBlocksPerMultiprocessor( &per, k_verify_dsm, 256, 0 ) );
     ctx->dsm_wgs = (ulong)(ncu > 0 ? ncu : 1) * (ulong)(per > 0 ? per : 1);
+    per = 0;
+    FD_CHECK( hipOccupancyMaxActiveBlocksPerMultiprocessor( &per, k_verify_prep, 256, 0 ) );
+    ctx->prep_wgs = (ulong)(ncu > 0 ? ncu : 1) * (ulong)(per > 0 ? per : 1);
   }
   hipLaunchKernelGGL( k_btab_init, dim3( (2*BTAB_N + 63)/64 ), dim3( 64 ), 0, ctx->stream, ctx->d_btab );
   FD_CHECK( hipGetLastError() );
@@ -851,7 +881,7 @@ verify_impl( fd_ed25519_hip_ctx_t * ctx, ulong n, uchar const * d_sigs, uchar co
     /* the txn paths (device-side count, variable-size messages) hash in
        block-count order; fixed or uniform batches keep record order */
     bool ordered = d_n && d_msg_off;
-    FD_CHECK( hipMemsetAsync( ctx->d_count, 0, (ordered ? 48 : 2)*sizeof(u32), s ) );
+    FD_CHECK( hipMemsetAsync( ctx->d_count, 0, (ordered ? 48 : 3)*sizeof(u32), s ) );
     if( ctx->timing ) FD_CHECK( hipEventRecord( ctx->ev[0], s ) );
     if( ordered ) {
       hipLaunchKernelGGL( k_msg_hist, grid, blk, 0, s, m, d_msg_sz + off, ctx->d_count, d_n, off );
@@ -860,7 +890,8 @@ verify_impl( fd_ed25519_hip_ctx_t * ctx, ulong n, uchar const * d_sigs, uchar co
       FD_CHECK( hipGetLastError() );
     }
     uchar const * pool = d_msg_off ? d_pool : d_pool + off*(ulong)fixed_sz;
-    hipLaunchKernelGGL( k_verify_prep, grid, blk, 0, s, m, ctx->chunk, d_sigs + 64*off, d_pubs + 32*off,
+    dim3 gprep( FD_PREP_PERSIST && grid.x > ctx->prep_wgs ? (unsigned)ctx->prep_wgs : grid.x );
+    hipLaunchKernelGGL( k_verify_prep, gprep, blk, 0, s, m, ctx->chunk, d_sigs + 64*off, d_pubs + 32*off,
                         pool, d_msg_off ? d_msg_off + off : (uint const *)0,
                         d_msg_off ? d_msg_sz + off : (uint const *)0, fixed_sz, ctx->d_state, ctx->errmode,
                         ctx->d_idx, ctx->d_count, d_codes + off, d_n, off, ordered ? ctx->d_order : (u32 const *)0 );
