@@ -2,7 +2,10 @@
 """bench.py -- ed25519 verifies/s on MI355X (BASELINE.json metric), one JSON line.
 
 A step is one verify pass (k_verify_prep + k_verify_dsm) over one batch of
-2^20 signatures resident in HBM: BASELINE config 2 ("same 1M-sig batch on one
+2^20 signatures resident in HBM, split over two verify contexts (HIP
+streams) so that one half's prep fills the issue slots the other half's DSM
+leaves idle at its end (--contexts; the verdicts are checked against a
+whole-batch pass through one context): BASELINE config 2 ("same 1M-sig batch on one
 MI355X with 10% corrupted sigs plus non-canonical R/A, S>=L and small-order
 points"), 64-byte messages, keys/signatures generated on the GPU by the
 engine's own signer, mutated with the C2 model (firedancer_amd/workload.py).
@@ -57,7 +60,7 @@ METRIC = "ed25519 verifies/sec (1/2/4/8 MI355X) + % of INT32 VALU peak"
 N_M, N_S = 1378.6, 1518.1
 N_M_DECODE, N_S_DECODE = 42.0, 510.0
 PEAK_OPS = 256 * 4 * 32 * 2.4e9          # 78.6e12 int32 lane-ops/s (32-wide SIMDs)
-PMC_SUMMARY = "r01j_pmc_summary.json"    # rocprofv3 PMC passes of this kernel build (tools/run_profile.sh)
+PMC_SUMMARY = "r01k_pmc_summary.json"    # rocprofv3 PMC passes of this kernel build (tools/run_profile.sh)
 
 
 def w_total(msg_sz):
@@ -133,8 +136,9 @@ def main():
     ap.add_argument("--txns", type=int, default=1 << 19, help="c4: frags per batch per GPU")
     ap.add_argument("--halfsize", type=int, default=1, choices=[0, 1],
                     help="0: full-length scalars (k, 1) in k_verify_dsm, an A/B switch (same verdicts)")
-    ap.add_argument("--contexts", type=int, default=1,
-                    help="c1/c2/c3/c5: verify contexts (streams) each step is split over (measured: 1-3 equal, 4+ slower)")
+    ap.add_argument("--contexts", type=int, default=2,
+                    help="c1/c2/c3/c5: verify contexts (streams) each step is split over (measured with the "
+                         "persistent DSM: 1 -> 118.2M, 2 -> 125.0-125.7M, 4 -> 124.5M verifies/s)")
     ap.add_argument("--tiles", type=int, default=8, help="c4: verify tiles (host threads + contexts) per GPU")
     ap.add_argument("--sigs", type=int, default=None, help="override signatures per GPU per step")
     ap.add_argument("--cpu-threads", type=int, default=16)
