@@ -4,13 +4,17 @@
    Pipeline per chunk of up to ctx->chunk signatures (one signature per lane,
    256-thread workgroups = 4 wave64):
 
+     k_msg_hist,    txn paths only: records counting-sorted by SHA-512 block
+     k_msg_order    count, so that prep's waves hash equal-length messages
      k_verify_prep  S<L check, decode A and R (sqrt chains), small-order
                     checks, k = SHA-512(R||A||M) mod L -> 192-B state record;
                     survivor compaction: final codes of pre-check failures,
                     survivors -> idx[] (k_verify_dsm runs only them)
-     k_verify_dsm   half-size scalars k1 = k*k2 (mod 8L), k2 odd, ~128 bits
+     k_verify_dsm   persistent: resident workgroups pull 64-survivor tasks;
+                    half-size scalars k1 = k*k2 (mod 8L), k2 odd, ~128 bits
                     each (sc_halfsize); tables B and 2^128 B -> LDS; tables
-                    [0..8](+-A) and [0..8](-R) -> per-lane HBM scratch;
+                    [1..8](+-A) and [1..8](-R) -> per-lane HBM scratch, one
+                    128-B line per entry (the identity is one shared entry);
                     [k1](+-A) + [k2](-R) + [k2*S mod L]B by fixed signed
                     windows (radix 16 for k1, k2; radix-256 digit pairs for
                     the B coefficient: every lane adds at the same positions,
