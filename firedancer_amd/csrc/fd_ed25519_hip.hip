@@ -53,7 +53,18 @@
 #define F_R_SMALL    (1u<<6)
 
 #define BTAB_N      129            /* 0..128 multiples of B */
+/* FD_BTAB_PACK: LDS B-table entries packed like the A/R entries (3 x 8 words,
+   6 ds_read_b128 per lookup) instead of 3 x 9 limbs + pad (7).  Off: the
+   unpacking costs more than the LDS bytes it saves (A/B 123.8-124.2 vs
+   124.9-125.2 M verifies/s). */
+#ifndef FD_BTAB_PACK
+#define FD_BTAB_PACK 0
+#endif
+#if FD_BTAB_PACK
+#define BTAB_STRIDE 24             /* affine cached (1/2-scaled): YmX, YpX, T2d (8 packed words each) */
+#else
 #define BTAB_STRIDE 28             /* affine cached (1/2-scaled): YmX, YpX, T2d (9 limbs each) + pad */
+#endif
 #define BTAB_WORDS  (BTAB_N*BTAB_STRIDE)   /* one table; d_btab holds [j]B then [j](2^128 B) */
 /* FD_ATAB_PACK: A/R table entries packed to 8 words per element (one 128-B
    line per entry) instead of 9 limbs (144 B, two or three lines).  Measured
@@ -150,6 +161,7 @@ DEV void ge_to_affc_half( ge_affc & a, ge_p3 const & p ) {
    radix-256 windows, and a second table for the high half of the
    half-size-scalar B coefficient, see sc_halfsize). */
 DEV void store_cached( u32 * t, ge_cached const & c );   /* A/R table entry layout, below */
+DEV void store_affc( u32 * e, ge_affc const & a );       /* B table entry layout, below */
 
 __global__ __launch_bounds__(64) void k_btab_init( u32 * btab ) {
   int j = blockIdx.x * blockDim.x + threadIdx.x;
@@ -166,9 +178,7 @@ __global__ __launch_bounds__(64) void k_btab_init( u32 * btab ) {
     if( (j >> bit) & 1 ) ge_add_cached( P, P, Bc, 0u, true );
   }
   ge_affc a; ge_to_affc_half( a, P );
-  #pragma unroll
-  for( int i=0; i<9; i++ ) { e[i] = a.YmX.v[i]; e[9+i] = a.YpX.v[i]; e[18+i] = a.T2d.v[i]; }
-  e[27] = 0u;
+  store_affc( e, a );
   if( j == 0 && blockIdx.x == 0 ) {             /* the shared identity entry of the A/R tables */
     ge_cached c;
     fe_1( c.YmX ); fe_1( c.YpX ); fe_0( c.T2d ); fe_set( c.Z2, 2,0,0,0,0,0,0,0,0 );
@@ -356,7 +366,6 @@ void k_verify_prep( ulong n, ulong chunk, uchar const * __restrict__ sigs, uchar
 }
 
 
-#if FD_ATAB_PACK
 /* 9 limbs <-> 8 words.  Every table element is an fe_norm output (limb 0 <
    2^29 + 2^14, limbs 1..7 < 2^29, limb 8 < 2^23) or a product (limb 1 < 2^29 +
    2^17, the others as fe_norm's): one 30-bit limb, seven of 29 bits and one of
@@ -386,6 +395,7 @@ template<int W30> DEV void fe_unpack( fe & a, u32 const w[8] ) {
     else               a.v[j] = __builtin_amdgcn_alignbit( w[k+1], w[k], (u32)sh ) & m;
   }
 }
+#if FD_ATAB_PACK
 DEV void store_cached( u32 * t, ge_cached const & c ) {   /* 32 words, one 128-B line */
   u32 w[32];
   fe_pack<0>( w, c.YmX ); fe_pack<0>( w + 8, c.YpX ); fe_pack<1>( w + 16, c.T2d ); fe_pack<0>( w + 24, c.Z2 );
@@ -418,14 +428,31 @@ DEV void load_cached( ge_cached & c, u32 const * t ) {
   for( int i=0; i<9; i++ ) { c.YmX.v[i] = w[i]; c.YpX.v[i] = w[9+i]; c.T2d.v[i] = w[18+i]; c.Z2.v[i] = w[27+i]; }
 }
 #endif
-/* one 1/2-scaled affine B-table entry from LDS (7 x ds_read_b128) */
+/* one 1/2-scaled affine B-table entry from LDS (FD_BTAB_PACK: 6 x
+   ds_read_b128 + unpack; else 7 x ds_read_b128) */
+DEV void store_affc( u32 * e, ge_affc const & a ) {      /* canonical elements: any packing layout fits */
+#if FD_BTAB_PACK
+  fe_pack<0>( e, a.YmX ); fe_pack<0>( e + 8, a.YpX ); fe_pack<0>( e + 16, a.T2d );
+#else
+  #pragma unroll
+  for( int i=0; i<9; i++ ) { e[i] = a.YmX.v[i]; e[9+i] = a.YpX.v[i]; e[18+i] = a.T2d.v[i]; }
+  e[27] = 0u;
+#endif
+}
 DEV void load_affc( ge_affc & b, u32 const * bt ) {
   uint4 const * q = (uint4 const *)bt;
+#if FD_BTAB_PACK
+  u32 w[24];
+  #pragma unroll
+  for( int k=0; k<6; k++ ) { uint4 v = q[k]; w[4*k] = v.x; w[4*k+1] = v.y; w[4*k+2] = v.z; w[4*k+3] = v.w; }
+  fe_unpack<0>( b.YmX, w ); fe_unpack<0>( b.YpX, w + 8 ); fe_unpack<0>( b.T2d, w + 16 );
+#else
   u32 w[28];
   #pragma unroll
   for( int k=0; k<7; k++ ) { uint4 v = q[k]; w[4*k] = v.x; w[4*k+1] = v.y; w[4*k+2] = v.z; w[4*k+3] = v.w; }
   #pragma unroll
   for( int i=0; i<9; i++ ) { b.YmX.v[i] = w[i]; b.YpX.v[i] = w[9+i]; b.T2d.v[i] = w[18+i]; }
+#endif
 }
 
 /* shift a packed 256-bit digit vector left by `bits` (4 or 8) */
