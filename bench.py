@@ -60,7 +60,7 @@ METRIC = "ed25519 verifies/sec (1/2/4/8 MI355X) + % of INT32 VALU peak"
 N_M, N_S = 1378.6, 1518.1
 N_M_DECODE, N_S_DECODE = 42.0, 510.0
 PEAK_OPS = 256 * 4 * 32 * 2.4e9          # 78.6e12 int32 lane-ops/s (32-wide SIMDs)
-PMC_SUMMARY = "r01k_pmc_summary.json"    # rocprofv3 PMC passes of this kernel build (tools/run_profile.sh)
+PMC_SUMMARY = "r01l_pmc_summary.json"    # rocprofv3 PMC passes of this kernel build (tools/run_profile.sh)
 
 
 def w_total(msg_sz):
