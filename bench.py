@@ -15,29 +15,25 @@ one process per GPU, each verifies its own 2^20-signature shard (weak scaling,
 no data-path collective: signatures are independent); RCCL is used only for
 the barrier and the max-over-ranks time.
 
-Roofline: INT32 VALU.  Algorithmic work per verify
-W = 304*N_M + 200*N_S + 4900*N_blk 32-bit-op equivalents (N_M = 1378.6,
-N_S = 1518.1 field mul/sqr of the reference algorithm, N_blk SHA-512 blocks);
-W = 7.33e5 at 64 B.  The dominant kernel, k_verify_dsm, carries the
-double-scalar multiplication part: W_dsm = 304*(1378.6-42) + 200*(1518.1-510)
-= 6.08e5 per signature that reaches it (the two point decodes -- 42 M + 510 S
--- and SHA-512 run in k_verify_prep).  W prices a 32x32->64 product as four
-single-rate 32-bit ops (lo, hi, add, addc), so the matching peak is the VALU
-lane rate at which single-rate 32-bit ops issue: 256 CU x 4 SIMD x 32 lanes x
-2.4 GHz = 78.6e12 ops/s (MI355X_MICROARCH.md: CDNA4 SIMDs are 32-wide; the
-157.3 TFLOPS FP32 vector peak is 2 x this).  On gfx950 the fused
-v_mad_u64_u32 (lo+hi+add) and v_addc_co_u32 issue at half that lane rate
-(profiles/r01_valu_rates_*.txt), i.e. two half-rate slots = the four W ops.
-The kernel duration is measured live with HIP events on the launch stream.
+Roofline: VALU issue (the kernels are integer-VALU bound).
+gfx950 issues at most one VALU wave-instruction per SIMD per quad-cycle,
+plus a second one in the same quad-cycle only for "dual-issue" e32 ops from
+another wave (v_add_u32, v_and/or/xor, v_mov, ...; never v_mad_u64_u32, VOP3
+integer ops or carry chains -- profiles/r02a_valu_issue_calibration.json).
+So the roofline of k_verify_dsm is its issue slots, counted by hardware:
+slots = SQ_INSTS_VALU - SQ_ACTIVE_INST_VALU2 per launch (rocprofv3 PMC pass of
+this build), against 1024 SIMDs x clock / 4.  "frac" = achieved / peak at
+the clock the chip holds under this load (GRBM_GUI_ACTIVE per XCD / kernel
+time, same pass): <= 1 by construction; frac_at_max_clock prices the same
+slots against the 2.4 GHz maximum.  The single-issue microbenchmark reaches
+~0.95 of the slots (launch ramp included).  See issue_roofline().
 
-W is fixed from the reference algorithm whatever scalar
-method the GPU uses.  k_verify_dsm runs half-size scalars (k1, k2 ~ 2^128
-with k1 = k*k2 mod 8L, see sc_halfsize): 4*(D-1) doublings for D ~ 33.2
-windows per wave instead of 252, so it executes ~5.05e5 op-equivalents per
-signature (W_DSM_EXEC: 1261.8 M + 522.7 S + ~1.65e4 for the reduction), not
-6.08e5.  "frac" keeps the 8(d) definition (the contract's per-unit figure),
-which passes 1 once the kernel runs its smaller work at more than 83% of
-the peak; "executed_frac" prices the kernel's own work (W_DSM_EXEC).
+SURVEY 8(d)'s W (the reference algorithm's int32-op count, 7.33e5 per verify
+at 64 B; W_dsm = 6.08e5 for the part k_verify_dsm does) is kept as
+ref_work_rate_vs_peak = units x W_dsm / time / 78.6 Tops/s: a speed-up over
+the reference algorithm (the half-size kernel executes ~17% less), not a
+utilisation.  The kernel duration is measured live with HIP events on the
+launch stream.
 
 cpu_baseline (rank 0, N=1): the reference's own fd_ed25519_verify (AVX-512
 IFMA build, compiled from the reference sources into oracle/_ref/) on a
@@ -60,7 +56,10 @@ METRIC = "ed25519 verifies/sec (1/2/4/8 MI355X) + % of INT32 VALU peak"
 N_M, N_S = 1378.6, 1518.1
 N_M_DECODE, N_S_DECODE = 42.0, 510.0
 PEAK_OPS = 256 * 4 * 32 * 2.4e9          # 78.6e12 int32 lane-ops/s (32-wide SIMDs)
+SIMDS, MAX_CLOCK = 256 * 4, 2.4e9         # MI355X_MICROARCH.md: 256 CU x 4 SIMD, 2400 MHz max clock
+PEAK_SLOTS = SIMDS * MAX_CLOCK / 4        # VALU issue slots/s: one quad-cycle per SIMD at the max clock
 PMC_SUMMARY = "r01l_pmc_summary.json"    # rocprofv3 PMC passes of this kernel build (tools/run_profile.sh)
+ISSUE_SUMMARY = "r02a_valu_issue_calibration.json"   # VALU issue-slot pass of this build (tools/run_valu_calib.sh)
 
 
 def w_total(msg_sz):
@@ -70,6 +69,59 @@ def w_total(msg_sz):
 
 W_DSM = 304 * (N_M - N_M_DECODE) + 200 * (N_S - N_S_DECODE)
 W_DSM_EXEC = 304 * 1261.8 + 200 * 522.7 + 1.65e4   # executed by the half-size k_verify_dsm (docstring)
+
+
+def c5_shard(sigs_per_rank, rank, world):
+    """Config 5: 2^26 signatures in total (or sigs_per_rank * world), cut
+    into contiguous shard_bounds ranges, one per rank.
+    Returns (total, lo, hi)."""
+    from firedancer_amd.shard import shard_bounds
+    total = sigs_per_rank * world if sigs_per_rank else 1 << 26
+    lo, hi = shard_bounds(total, rank, world)
+    return total, lo, hi
+
+
+ISSUE_UNITS = 933793      # survivors per launch in that pass (the C2 2^20 batch, seed 0x5eed0001: deterministic)
+
+
+def issue_roofline(dsm_avg_ms, units_per_launch):
+    """VALU issue roofline of k_verify_dsm from the committed PMC pass of this
+    build (profiles/ISSUE_SUMMARY, tools/run_valu_calib.sh):
+      slots per launch  = SQ_INSTS_VALU - SQ_ACTIVE_INST_VALU2 (quad-cycles of a
+                          SIMD with >= 1 VALU issue; dual-issued pairs count once)
+      cycles per launch = GRBM_GUI_ACTIVE / 8 (per XCD), same pass
+      achieved          = slots per launch / live launch time (HIP events)
+      held clock        = cycles per launch / live launch time (the kernel is
+                          issue-bound: its cycle count, not its time, is what
+                          stays fixed from run to run as the clock moves)
+      peak              = 1024 SIMDs x held clock / 4 (one issue slot per
+                          quad-cycle per SIMD)
+      frac              = achieved / peak = slots / (1024 x cycles / 4): the
+                          counters' own ratio (pmc_frac), <= 1 by construction
+      frac_at_max_clock = achieved / (1024 x 2.4 GHz / 4)
+    DESIGN.md 6 states the formula; the single-issue microbenchmark ceiling
+    (tools/valu_rates2 under the same counters) is ~0.95."""
+    path = os.path.join(REPO, "profiles", ISSUE_SUMMARY)
+    if not os.path.exists(path):
+        return None
+    with open(path) as f:
+        cal = json.load(f)
+    e = cal["engine"]["k_verify_dsm"]
+    scale = units_per_launch / ISSUE_UNITS           # exact (1) for C2; per-survivor scaling otherwise
+    slots, cycles = e["issue_slots"] * scale, e["grbm_cycles_per_xcd"] * scale
+    t = dsm_avg_ms * 1e-3
+    achieved = slots / t
+    clock = cycles / t                               # the launch's cycle count over its live duration
+    peak = SIMDS * clock / 4
+    return {"bound": "valu_issue", "unit": "T issue-slots/s", "achieved": round(achieved / 1e12, 5),
+            "peak": round(peak / 1e12, 5), "frac": round(achieved / peak, 4), "pmc_frac": e["slot_util"],
+            "frac_at_max_clock": round(achieved / PEAK_SLOTS, 4), "held_clock_ghz": round(clock / 1e9, 4),
+            "held_clock_ghz_pmc_pass": e["held_clock_ghz"],
+            "issue_slots_per_launch": round(slots), "dual_issue_share": e["dual_issue_share"],
+            "slots_scaled_from_c2": abs(units_per_launch - ISSUE_UNITS) > 0.5,
+            "single_issue_ceiling": cal.get("single_issue_ceiling_slot_util"),
+            "issue_source": f"profiles/{ISSUE_SUMMARY} (rocprofv3 --pmc SQ_INSTS_VALU SQ_ACTIVE_INST_VALU2 "
+                            "GRBM_GUI_ACTIVE ..., one pass, bench.py --contexts 1)"}
 
 
 def write_fdv1(path, sigs, pubs, pool, moff, msz):
@@ -108,6 +160,7 @@ def cpu_baseline(sigs, pubs, pool, moff, msz, gpu_codes, threads, target_s):
 
 
 _JSON_FD = [1]
+COLL_DEV = None          # device of the tensors the collectives reduce (GPU for RCCL, CPU for gloo)
 
 
 def emit(out):
@@ -145,23 +198,32 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=8.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--force-dist", action="store_true", help="init torch.distributed even at world size 1")
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                    help="nccl (RCCL over xGMI, one rank per GPU: the driver's N-GPU runs); gloo rehearses the "
+                         "N>1 path with several ranks sharing one GPU (rank r on GPU r %% device_count)")
     args = ap.parse_args()
 
     import torch
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0")) % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     dist = None
+    global COLL_DEV
     if world > 1 or args.force_dist:
         import torch.distributed as dist
         _quiet_stdout()
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+            COLL_DEV = torch.device("cuda", local)
+        else:
+            dist.init_process_group("gloo")
+            COLL_DEV = torch.device("cpu")
 
     from firedancer_amd import Verifier
+    from firedancer_amd.ed25519 import CTX_STREAM
     from firedancer_amd.workload import make_batch_gpu
 
-    from firedancer_amd.shard import shard_bounds
     cfg = args.config
     if cfg == "c4":
         return run_c4(args, rank, world, local, dist)
@@ -169,8 +231,7 @@ def main():
     mix = "c1" if cfg in ("c1", "c3") else "c2"
     scaling = "weak"
     if cfg == "c5":
-        total = args.sigs * world if args.sigs else 1 << 26
-        lo, hi = shard_bounds(total, rank, world)
+        total, lo, hi = c5_shard(args.sigs, rank, world)
         n = hi - lo
         scaling = "strong"
     else:
@@ -206,17 +267,20 @@ def main():
     whole = [(v, 0, n, groups_of(0, n) if cfg == "c3" else None)]
 
     def step(jl):
+        # each context on its own stream (CTX_STREAM), so the contexts overlap;
+        # the inputs were made on torch's stream and synchronised before warmup
         for vv, lo, hi, g in jl:
             vv.verify_dev(hi - lo, batch.sigs[lo:hi], batch.pubs[lo:hi], batch.pool, batch.msg_off[lo:hi],
-                          batch.msg_sz[lo:hi], codes[lo:hi], bitmap[lo // 64:(hi + 63) // 64])
+                          batch.msg_sz[lo:hi], codes[lo:hi], bitmap[lo // 64:(hi + 63) // 64], stream=CTX_STREAM)
             if g:
-                vv.group_reduce_dev(g[0], g[1], g[2], codes[lo:hi], g[3])
+                vv.group_reduce_dev(g[0], g[1], g[2], codes[lo:hi], g[3], stream=CTX_STREAM)
 
     def sync_all():
         for vv in ctxs + [v]:
             vv.sync()
         torch.cuda.synchronize()
 
+    torch.cuda.synchronize()          # batch generation (torch stream) before the context streams read it
     for _ in range(args.warmup):
         step(jobs)
     sync_all()
@@ -244,7 +308,7 @@ def main():
     assert torch.equal(codes, timed_codes) and torch.equal(gcodes, timed_gcodes), "contexts != whole batch"
     elapsed = t1 - t0
     if dist:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        t = torch.tensor([elapsed], dtype=torch.float64, device=COLL_DEV)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
@@ -256,7 +320,7 @@ def main():
     accept = float((c == 0).mean())
 
     if dist:
-        nt = torch.tensor([n], dtype=torch.int64, device=dev)
+        nt = torch.tensor([n], dtype=torch.int64, device=COLL_DEV)
         dist.all_reduce(nt)
         n_all = int(nt.item())
     else:
@@ -281,6 +345,7 @@ def main():
 
     # HBM-side bytes per k_verify_dsm launch from the committed rocprofv3 PMC
     # passes of this same command (FETCH_SIZE x2 per the gfx950 note + WRITE_SIZE)
+    issue = issue_roofline(dsm_avg_ms, units_per_launch)
     traffic, traffic_src = None, None
     pmc = os.path.join(REPO, "profiles", PMC_SUMMARY)
     if cfg == "c2" and n == (1 << 20) and os.path.exists(pmc):
@@ -326,19 +391,17 @@ def main():
                        "parallelism": f"dp{world} (signature shards)",
                        "verify_contexts": len(ctxs)},
             "accept_rate": round(accept, 5),
-            "roofline": {"bound": "valu_int32", "kernel": "k_verify_dsm",
-                         "achieved": round(achieved, 3), "peak": round(peak, 3), "unit": "Tops/s",
-                         "frac": round(achieved / peak, 4), "traffic": traffic, "traffic_unit": "bytes/launch",
-                         "traffic_source": traffic_src,
-                         "algorithmic_ops_per_unit": round(W_DSM), "units_per_launch": round(units_per_launch),
+            "roofline": dict(issue or {}, **{
+                         "kernel": "k_verify_dsm", "traffic": traffic, "traffic_unit": "bytes/launch",
+                         "traffic_source": traffic_src, "units_per_launch": round(units_per_launch),
                          "avg_launch_ms": round(dsm_avg_ms, 4),
-                         "executed_ops_per_unit": round(W_DSM_EXEC),
-                         "executed_frac": round(achieved_exec / peak, 4),
-                         "frac_note": "achieved/frac use SURVEY 8(d)'s per-unit W, the reference algorithm's "
-                                      "(full-length scalar) work; the half-size kernel does 17% less, so frac can "
-                                      "pass 1 -- executed_frac prices the kernel's own work",
+                         "ref_work_rate_vs_peak": round(achieved / peak, 4),
+                         "ref_work_note": "SURVEY 8(d)'s W (the reference algorithm's full-length-scalar work, "
+                                          f"{round(W_DSM)} int32-op equivalents per unit) x units / time / 78.6 "
+                                          "Tops/s: a speed-up figure over the reference algorithm, NOT a "
+                                          "utilisation (the half-size kernel does 17% less work, so it can pass 1)",
                          "timing_leg": "after the timed steps: the whole batch through one context, HIP events "
-                                       "around each launch, each k_verify_dsm alone on the GPU"},
+                                       "around each launch, each k_verify_dsm alone on the GPU"}),
             "pipeline": {"prep_ms": round(prep_avg_ms, 4), "dsm_ms": round(dsm_avg_ms, 4),
                          "w_total_per_verify": round(w_total(msg_sz)),
                          "int32_valu_frac": round(pipeline_frac, 4),
@@ -452,6 +515,7 @@ def run_c4(args, rank, world, local, dist):
         ms = [tl.metrics() for tl in tiles]
         return {k: sum(m[k] for m in ms) for k in ms[0]}
 
+    torch.cuda.synchronize()          # payload upload before the tile streams read it
     run(max(args.warmup, 1))
     torch.cuda.synchronize()
     if dist:
@@ -469,10 +533,10 @@ def run_c4(args, rank, world, local, dist):
     sigs = m1["sigs"] - m0["sigs"]
     frags = s.n * args.steps
     if dist:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        t = torch.tensor([elapsed], dtype=torch.float64, device=COLL_DEV)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
-        tt = torch.tensor([sigs, frags], dtype=torch.int64, device=dev)
+        tt = torch.tensor([sigs, frags], dtype=torch.int64, device=COLL_DEV)
         dist.all_reduce(tt)
         sigs, frags = int(tt[0].item()), int(tt[1].item())
     res = np.concatenate([o[-1][0] for o in outs])

@@ -124,6 +124,16 @@ struct fd_ed25519_hip_ctx {
   uchar *      d_sigs; uchar * d_pubs; uchar * d_pool; uint * d_moff; uint * d_msz;
   signed char * d_codes; ulong * d_bitmap;
   uint *       d_gfirst; uchar * d_gcnt; signed char * d_gcodes;
+  /* stream ordering of the context's scratch: every verify launch sequence
+     waits for the previous one (on whatever stream it ran) and records its
+     own end, so calls on different streams never overlap on d_state/d_idx/
+     d_count/d_atab */
+  hipEvent_t   ev_last;
+  int          ev_used;
+  /* drop-in entry points (part 1): one pinned, device-mapped staging block
+     the kernels read and write in place (no copies), grown on demand */
+  uchar *      h_stage;
+  ulong        h_stage_cap;
 };
 
 /**********************************************************************/
@@ -470,7 +480,16 @@ void k_bitmap( ulong n, signed char const * __restrict__ codes, ulong * __restri
   if( d_n ) { ulong c = *d_n; n = c > rec0 ? (c - rec0 < n ? c - rec0 : n) : 0ul; }
   bool ok = i < n && codes[i] == FD_ED25519_SUCCESS;
   unsigned long long b = __ballot( ok );
-  if( (threadIdx.x & 63u) == 0u && i < n ) bitmap[i >> 6] = b;
+  if( (threadIdx.x & 63u) == 0u && i < n ) {
+    /* the word holding record n-1: bits at or past n belong to no record of
+       this call and keep their value (include/fd_ed25519_hip.h) */
+    ulong left = n - i;
+    if( left < 64ul ) {
+      unsigned long long m = (1ULL << left) - 1ULL;
+      b = (bitmap[i >> 6] & ~m) | (b & m);
+    }
+    bitmap[i >> 6] = b;
+  }
 }
 
 /* table [1..8]Q in cached form for Q = (qx, qy) affine (fd_curve25519.c:
@@ -804,6 +823,7 @@ fd_ed25519_hip_ctx_new( int device, ulong chunk_sigs ) {
   FD_CHECK( hipMalloc( (void **)&ctx->d_order, chunk_sigs * sizeof(u32) ) );
   FD_CHECK( hipMalloc( (void **)&ctx->d_count, 256 ) );
   for( int e=0; e<4; e++ ) FD_CHECK( hipEventCreate( &ctx->ev[e] ) );
+  FD_CHECK( hipEventCreateWithFlags( &ctx->ev_last, hipEventDisableTiming ) );
   {
     int ncu = 0, per = 0;
     FD_CHECK( hipDeviceGetAttribute( &ncu, hipDeviceAttributeMultiprocessorCount, device ) );
@@ -845,10 +865,13 @@ fd_ed25519_hip_ctx_delete( fd_ed25519_hip_ctx_t * ctx ) {
   if( !ctx ) return;
   (void)hipSetDevice( ctx->device );
   (void)hipStreamSynchronize( ctx->stream );
+  if( ctx->ev_used ) (void)hipEventSynchronize( ctx->ev_last );   /* last call may have run on a caller stream */
   (void)hipFree( ctx->d_btab ); (void)hipFree( ctx->d_state ); (void)hipFree( ctx->d_atab );
   (void)hipFree( ctx->d_idx ); (void)hipFree( ctx->d_order ); (void)hipFree( ctx->d_count );
   free_staging( ctx );
   for( int e=0; e<4; e++ ) (void)hipEventDestroy( ctx->ev[e] );
+  (void)hipEventDestroy( ctx->ev_last );
+  if( ctx->h_stage ) (void)hipHostFree( ctx->h_stage );
   (void)hipStreamDestroy( ctx->stream );
   free( ctx );
 }
@@ -883,6 +906,32 @@ fd_ed25519_hip_test_halfsize( fd_ed25519_hip_ctx_t * ctx, ulong n, uint const * 
   return 0;
 }
 
+/* test hook: plain SHA-512 of n messages with the device hash core used by
+   k_verify_prep (sha512_prefixed with an empty prefix); out: 64-byte digests */
+__global__ void k_test_sha512( ulong n, uchar const * pool, uint const * moff, uint const * msz, uchar * out ) {
+  ulong i = (ulong)blockIdx.x * blockDim.x + threadIdx.x;
+  if( i >= n ) return;
+  u32 pre[16], x[16];
+  #pragma unroll
+  for( int q=0; q<16; q++ ) pre[q] = 0u;
+  sha512_prefixed( x, pre, 0u, pool + moff[i], msz[i] );
+  uint4 * o = (uint4 *)(out + 64ul*i);
+  #pragma unroll
+  for( int q=0; q<4; q++ ) o[q] = make_uint4( x[4*q], x[4*q+1], x[4*q+2], x[4*q+3] );
+}
+
+int
+fd_ed25519_hip_test_sha512( fd_ed25519_hip_ctx_t * ctx, ulong n, uchar const * d_pool, uint const * d_msg_off,
+                            uint const * d_msg_sz, uchar * d_out, void * stream ) {
+  hipStream_t s = stream ? (hipStream_t)stream : ctx->stream;
+  FD_CHECK( hipSetDevice( ctx->device ) );
+  if( !n ) return 0;
+  hipLaunchKernelGGL( k_test_sha512, dim3( (unsigned)((n + 63)/64) ), dim3( 64 ), 0, s, n, d_pool, d_msg_off,
+                      d_msg_sz, d_out );
+  FD_CHECK( hipGetLastError() );
+  return 0;
+}
+
 void
 fd_ed25519_hip_set_timing( fd_ed25519_hip_ctx_t * ctx, int on ) {
   ctx->timing = on; ctx->prep_ms = ctx->dsm_ms = 0.0; ctx->prep_launches = ctx->dsm_launches = 0UL;
@@ -906,6 +955,8 @@ verify_impl( fd_ed25519_hip_ctx_t * ctx, ulong n, uchar const * d_sigs, uchar co
              signed char * d_codes, ulong * d_bitmap, u32 const * d_n, void * stream ) {
   hipStream_t s = stream ? (hipStream_t)stream : ctx->stream;
   FD_CHECK( hipSetDevice( ctx->device ) );
+  if( !n ) return 0;
+  if( ctx->ev_used ) FD_CHECK( hipStreamWaitEvent( s, ctx->ev_last, 0 ) );   /* previous call's scratch use */
   for( ulong off = 0; off < n; off += ctx->chunk ) {
     ulong m = n - off < ctx->chunk ? n - off : ctx->chunk;
     dim3 grid( (unsigned)((m + 255) / 256) ), blk( 256 );
@@ -950,6 +1001,8 @@ verify_impl( fd_ed25519_hip_ctx_t * ctx, ulong n, uchar const * d_sigs, uchar co
       ctx->prep_ms += a; ctx->dsm_ms += b; ctx->prep_launches++; ctx->dsm_launches++; ctx->dsm_units += survivors;
     }
   }
+  FD_CHECK( hipEventRecord( ctx->ev_last, s ) );
+  ctx->ev_used = 1;
   return 0;
 }
 
@@ -1059,7 +1112,21 @@ fd_ed25519_hip_verify_host( fd_ed25519_hip_ctx_t * ctx, ulong n, uchar const * s
   return 0;
 }
 
-/* ---- reference API on a lazily created process-wide context ---------- */
+/* ---- reference API on a lazily created process-wide context ----------
+
+   Each call stages its records in one pinned, device-mapped host block
+   (hipHostMalloc: the kernels read sig/pub/msg and write the codes in place
+   over PCIe, so a call is the kernel launches plus one stream sync, with no
+   hipMemcpy).  Layout, 16-byte aligned: sigs[16*64] pubs[16*32] off[16]
+   sz[16] codes[16] pad, then the message and 16 zero bytes (the kernel's
+   message loads may read up to 12 bytes past the end). */
+
+#define STAGE_SIGS   0ul
+#define STAGE_PUBS   1024ul
+#define STAGE_OFF    1536ul
+#define STAGE_SZ     1600ul
+#define STAGE_CODES  1664ul
+#define STAGE_MSG    1792ul
 
 static fd_ed25519_hip_ctx_t * g_ctx;
 static std::mutex             g_lock;
@@ -1074,16 +1141,54 @@ static fd_ed25519_hip_ctx_t * default_ctx( void ) {
   return g_ctx;
 }
 
+/* The engine addresses messages with 32-bit offsets and sizes.  A longer
+   message cannot be hashed here; verifying a truncated prefix instead would
+   be a silent divergence from the reference (which hashes all of it), so the
+   process aborts loudly (SURVEY.md 8(b) "Errors": never a silent reject or
+   accept). */
+#define DROPIN_MSG_MAX ((ulong)UINT32_MAX - 256ul)
+static void dropin_check_msg_sz( ulong msg_sz, char const * fn ) {
+  if( msg_sz > DROPIN_MSG_MAX ) {
+    fprintf( stderr, "fd_ed25519_hip: %s: msg_sz %lu exceeds the engine's 32-bit message limit (%lu)\n", fn,
+             msg_sz, DROPIN_MSG_MAX );
+    abort();
+  }
+}
+
+/* stage n (sig, pub) pairs sharing one message and run them; codes land in
+   the staging block */
+static signed char const *
+dropin_run( fd_ed25519_hip_ctx_t * ctx, uchar const * msg, ulong msg_sz, uchar const * sigs,
+            uchar const * pubs, ulong n ) {
+  ulong need = STAGE_MSG + ((msg_sz + 16ul + 15ul) & ~15ul);
+  if( need > ctx->h_stage_cap ) {
+    ulong cap = need < 65536ul ? 65536ul : need;
+    FD_CHECK( hipSetDevice( ctx->device ) );
+    if( ctx->h_stage ) FD_CHECK( hipHostFree( ctx->h_stage ) );
+    FD_CHECK( hipHostMalloc( (void **)&ctx->h_stage, cap, hipHostMallocDefault ) );
+    ctx->h_stage_cap = cap;
+  }
+  uchar * st = ctx->h_stage;
+  memcpy( st + STAGE_SIGS, sigs, 64ul*n );
+  memcpy( st + STAGE_PUBS, pubs, 32ul*n );
+  uint * off = (uint *)(st + STAGE_OFF), * sz = (uint *)(st + STAGE_SZ);
+  for( ulong j=0; j<n; j++ ) { off[j] = 0u; sz[j] = (uint)msg_sz; }
+  if( msg_sz ) memcpy( st + STAGE_MSG, msg, msg_sz );
+  memset( st + STAGE_MSG + msg_sz, 0, 16 );
+  verify_impl( ctx, n, st + STAGE_SIGS, st + STAGE_PUBS, st + STAGE_MSG, off, sz, 0u,
+               (signed char *)(st + STAGE_CODES), NULL, NULL, NULL );
+  FD_CHECK( hipStreamSynchronize( ctx->stream ) );
+  return (signed char const *)(st + STAGE_CODES);
+}
+
 int
 fd_ed25519_verify( uchar const msg[], ulong msg_sz, uchar const sig[64], uchar const public_key[32],
                    struct fd_sha512_private * sha ) {
   (void)sha;
+  dropin_check_msg_sz( msg_sz, "fd_ed25519_verify" );
   std::lock_guard<std::mutex> lk( g_lock );
-  fd_ed25519_hip_ctx_t * ctx = default_ctx();
-  uint off = 0, sz = (uint)msg_sz;
-  signed char code;
-  fd_ed25519_hip_verify_host( ctx, 1, sig, public_key, msg_sz ? msg : (uchar const *)"", msg_sz, &off, &sz, &code, NULL );
-  return (int)code;
+  signed char const * codes = dropin_run( default_ctx(), msg, msg_sz, sig, public_key, 1ul );
+  return (int)codes[0];
 }
 
 int
@@ -1092,12 +1197,9 @@ fd_ed25519_verify_batch_single_msg( uchar const msg[], ulong const msg_sz, uchar
                                     uchar const batch_sz ) {
   (void)shas;
   if( batch_sz == 0 || batch_sz > 16 ) return FD_ED25519_ERR_SIG;         /* user.c:238-241 */
+  dropin_check_msg_sz( msg_sz, "fd_ed25519_verify_batch_single_msg" );
   std::lock_guard<std::mutex> lk( g_lock );
-  fd_ed25519_hip_ctx_t * ctx = default_ctx();
-  uint off[16], sz[16]; signed char codes[16];
-  for( int j=0; j<batch_sz; j++ ) { off[j] = 0; sz[j] = (uint)msg_sz; }
-  fd_ed25519_hip_verify_host( ctx, batch_sz, signatures, pubkeys, msg_sz ? msg : (uchar const *)"", msg_sz,
-                              off, sz, codes, NULL );
+  signed char const * codes = dropin_run( default_ctx(), msg, msg_sz, signatures, pubkeys, (ulong)batch_sz );
   int msg_fail = 0;
   for( int j=0; j<batch_sz; j++ ) {                                        /* pass-1 order, then pass 2 */
     if( codes[j] == FD_ED25519_ERR_SIG || codes[j] == FD_ED25519_ERR_PUBKEY ) return codes[j];

@@ -673,6 +673,7 @@ struct fd_replay_hip {
   u8 *    d_nsig; u32 * d_sig_at; u32 * d_acct_at; u32 * d_msg_at; u32 * d_msg_sz;
   u32 *   d_first; u8 * d_cnt; signed char * d_tcode; u32 * d_counter; u32 * h_counter;
   u8 *    d_rsig; u8 * d_rpub; u32 * d_rmoff; u32 * d_rmsz; signed char * d_rcode;
+  hipEvent_t ev_last; int ev_used;   /* calls on different streams run in call order over this scratch */
 };
 
 extern "C" fd_replay_hip_t *
@@ -691,6 +692,7 @@ fd_replay_hip_new( fd_ed25519_hip_ctx_t * ctx, ulong max_txn ) {
   TX_CHECK( hipMalloc( &r->d_rsig, 64*rc ) );   TX_CHECK( hipMalloc( &r->d_rpub, 32*rc ) );
   TX_CHECK( hipMalloc( &r->d_rmoff, 4*rc ) );   TX_CHECK( hipMalloc( &r->d_rmsz, 4*rc ) );
   TX_CHECK( hipMalloc( &r->d_rcode, rc ) );
+  TX_CHECK( hipEventCreateWithFlags( &r->ev_last, hipEventDisableTiming ) );
   return r;
 }
 
@@ -699,6 +701,8 @@ fd_replay_hip_delete( fd_replay_hip_t * r ) {
   if( !r ) return;
   (void)hipSetDevice( fd_ed25519_hip_ctx_device( r->ctx ) );
   (void)hipStreamSynchronize( (hipStream_t)fd_ed25519_hip_ctx_stream( r->ctx ) );
+  if( r->ev_used ) (void)hipEventSynchronize( r->ev_last );
+  (void)hipEventDestroy( r->ev_last );
   (void)hipFree( r->d_nsig ); (void)hipFree( r->d_sig_at ); (void)hipFree( r->d_acct_at ); (void)hipFree( r->d_msg_at );
   (void)hipFree( r->d_msg_sz ); (void)hipFree( r->d_first ); (void)hipFree( r->d_cnt ); (void)hipFree( r->d_tcode );
   (void)hipFree( r->d_counter ); (void)hipHostFree( r->h_counter );
@@ -715,6 +719,7 @@ fd_replay_hip_txn_verify_dev( fd_replay_hip_t * r, ulong n, uchar const * d_pool
   hipStream_t st = stream ? (hipStream_t)stream : (hipStream_t)fd_ed25519_hip_ctx_stream( r->ctx );
   TX_CHECK( hipSetDevice( fd_ed25519_hip_ctx_device( r->ctx ) ) );
   dim3 grid( (unsigned)((n + 255)/256) ), blk( 256 );
+  if( r->ev_used ) TX_CHECK( hipStreamWaitEvent( st, r->ev_last, 0 ) );
   hipLaunchKernelGGL( k_desc_spans, grid, blk, 0, st, n, d_desc, r->d_nsig, r->d_sig_at, r->d_acct_at, r->d_msg_at,
                       r->d_msg_sz );
   TX_CHECK( hipGetLastError() );
@@ -728,6 +733,8 @@ fd_replay_hip_txn_verify_dev( fd_replay_hip_t * r, ulong n, uchar const * d_pool
   fd_ed25519_hip_group_reduce_dev( r->ctx, n, r->d_first, r->d_cnt, r->d_rcode, r->d_tcode, st );
   hipLaunchKernelGGL( k_exec_codes, grid, blk, 0, st, n, r->d_tcode, d_result );
   TX_CHECK( hipGetLastError() );
+  TX_CHECK( hipEventRecord( r->ev_last, st ) );
+  r->ev_used = 1;
   return 0;
 }
 

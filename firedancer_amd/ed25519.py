@@ -7,8 +7,10 @@ Names, argument meaning and result codes follow src/ballet/ed25519/fd_ed25519.h
 fd_ed25519_strerror :137-138).  There is no CPU fallback: if the HIP library is
 missing or no GPU is present, every entry point raises.
 """
+import contextlib
 import ctypes
 import os
+import sys
 
 import numpy as np
 
@@ -31,6 +33,7 @@ EXPORTS = (
     "fd_ed25519_hip_verify_host", "fd_ed25519_hip_group_reduce_dev", "fd_ed25519_hip_sign_dev",
     "fd_ed25519_hip_sync", "fd_ed25519_hip_set_timing", "fd_ed25519_hip_get_timing",
     "fd_ed25519_hip_get_dsm_units", "fd_ed25519_hip_set_halfsize", "fd_ed25519_hip_test_halfsize",
+    "fd_ed25519_hip_test_sha512",
 )
 
 _lib = None
@@ -65,6 +68,7 @@ def lib():
         L.fd_ed25519_hip_set_errmode.argtypes = [vp, c.c_int]
         L.fd_ed25519_hip_set_halfsize.argtypes = [vp, c.c_int]
         L.fd_ed25519_hip_test_halfsize.argtypes = [vp, c.c_ulong, vp, vp, vp]
+        L.fd_ed25519_hip_test_sha512.argtypes = [vp, c.c_ulong, vp, vp, vp, vp, vp]
         L.fd_ed25519_hip_ctx_reserve.argtypes = [vp, u64]
         L.fd_ed25519_hip_verify_dev.restype = c.c_int
         L.fd_ed25519_hip_verify_dev.argtypes = [vp, u64, vp, vp, vp, vp, vp, vp, vp, vp]
@@ -129,8 +133,19 @@ def _ptr(a, nbytes=0, name="buffer", device=None):
     return a.data_ptr()
 
 
+CTX_STREAM = "ctx"   # stream= value naming the context's own (private) HIP stream
+
+
 class Verifier:
-    """One GPU context (device, stream, base-point table, chunk scratch)."""
+    """One GPU context (device, stream, base-point table, chunk scratch).
+
+    Stream of the *_dev calls: by default torch's current stream on the
+    context's device, so a call is ordered after the torch work that produced
+    its inputs and before the torch work that reads its outputs.  Pass
+    stream=CTX_STREAM for the context's private stream (callers that keep
+    several contexts in flight, and order them against torch themselves), or
+    a raw hipStream_t handle (int).  Calls on one context are ordered among
+    themselves whatever streams they name (fd_ed25519_hip.h)."""
 
     def __init__(self, device=0, chunk_sigs=1 << 20, errmode=ERRMODE_AVX512):
         self._lib = lib()
@@ -182,40 +197,81 @@ class Verifier:
     def _p(self, a, nbytes=0, name="buffer"):
         return _ptr(a, nbytes, name, self.device)
 
+    @contextlib.contextmanager
+    def _stream(self, stream):
+        """Resolve a stream= argument to the hipStream_t handle passed to the C
+        ABI (None = the context's stream).  Default (None): torch's current
+        stream.  The C ABI reads a NULL handle as "the context's stream", so
+        torch's legacy default stream (handle 0) cannot be named directly: the
+        call then runs on the context's stream, forked from and joined back to
+        torch's stream with events (the context stream is non-blocking, so
+        without this nothing would order it against torch's work)."""
+        if stream == CTX_STREAM:
+            yield None
+            return
+        if stream is not None:
+            yield int(stream)
+            return
+        torch = sys.modules.get("torch")
+        if torch is None or not torch.cuda.is_available():
+            yield None
+            return
+        cur = torch.cuda.current_stream(self.device)
+        if cur.cuda_stream:
+            yield cur.cuda_stream
+            return
+        ctx_s = torch.cuda.ExternalStream(self.stream, device=torch.device("cuda", self.device))
+        fork = torch.cuda.Event()
+        fork.record(cur)
+        ctx_s.wait_event(fork)
+        yield None
+        join = torch.cuda.Event()
+        join.record(ctx_s)
+        cur.wait_event(join)
+
     def verify_dev(self, n, sigs, pubs, pool, msg_off, msg_sz, codes, bitmap=None, stream=None):
+        """Message i = pool[msg_off[i], +msg_sz[i]).  The pool must stay
+        readable 16 bytes past its last message byte: the caller guarantees
+        it (checking it here would need the offsets on the host)."""
         n = int(n)
-        return self._lib.fd_ed25519_hip_verify_dev(
-            self.ctx, n, self._p(sigs, 64 * n, "sigs"), self._p(pubs, 32 * n, "pubs"), self._p(pool, 1, "pool"),
-            self._p(msg_off, 4 * n, "msg_off"), self._p(msg_sz, 4 * n, "msg_sz"), self._p(codes, n, "codes"),
-            self._p(bitmap, 8 * ((n + 63) // 64), "bitmap"), stream)
+        args = (self.ctx, n, self._p(sigs, 64 * n, "sigs"), self._p(pubs, 32 * n, "pubs"), self._p(pool, 1, "pool"),
+                self._p(msg_off, 4 * n, "msg_off"), self._p(msg_sz, 4 * n, "msg_sz"), self._p(codes, n, "codes"),
+                self._p(bitmap, 8 * ((n + 63) // 64), "bitmap"))
+        with self._stream(stream) as h:
+            return self._lib.fd_ed25519_hip_verify_dev(*args, h)
 
     def verify_dev_count(self, n_max, d_n, sigs, pubs, pool, msg_off, msg_sz, codes, bitmap=None, stream=None):
         """verify_dev with the record count in device memory (uint32 *d_n)."""
         n = int(n_max)
-        return self._lib.fd_ed25519_hip_verify_dev_count(
-            self.ctx, n, self._p(d_n, 4, "d_n"), self._p(sigs, 64 * n, "sigs"), self._p(pubs, 32 * n, "pubs"),
-            self._p(pool, 1, "pool"), self._p(msg_off, 4 * n, "msg_off"), self._p(msg_sz, 4 * n, "msg_sz"),
-            self._p(codes, n, "codes"), self._p(bitmap, 8 * ((n + 63) // 64), "bitmap"), stream)
+        args = (self.ctx, n, self._p(d_n, 4, "d_n"), self._p(sigs, 64 * n, "sigs"), self._p(pubs, 32 * n, "pubs"),
+                self._p(pool, 1, "pool"), self._p(msg_off, 4 * n, "msg_off"), self._p(msg_sz, 4 * n, "msg_sz"),
+                self._p(codes, n, "codes"), self._p(bitmap, 8 * ((n + 63) // 64), "bitmap"))
+        with self._stream(stream) as h:
+            return self._lib.fd_ed25519_hip_verify_dev_count(*args, h)
 
     def verify_fixed_dev(self, n, sigs, pubs, msgs, msg_sz, codes, bitmap=None, stream=None):
-        """Fixed-size messages back to back: message i = msgs[i*msg_sz, (i+1)*msg_sz)."""
+        """Fixed-size messages back to back: message i = msgs[i*msg_sz, (i+1)*msg_sz);
+        msgs must hold 16 readable bytes past the last message."""
         n = int(n)
-        return self._lib.fd_ed25519_hip_verify_fixed_dev(
-            self.ctx, n, self._p(sigs, 64 * n, "sigs"), self._p(pubs, 32 * n, "pubs"),
-            self._p(msgs, max(1, n * int(msg_sz)), "msgs"), int(msg_sz), self._p(codes, n, "codes"),
-            self._p(bitmap, 8 * ((n + 63) // 64), "bitmap"), stream)
+        args = (self.ctx, n, self._p(sigs, 64 * n, "sigs"), self._p(pubs, 32 * n, "pubs"),
+                self._p(msgs, n * int(msg_sz) + 16, "msgs (+16 readable bytes)"), int(msg_sz),
+                self._p(codes, n, "codes"), self._p(bitmap, 8 * ((n + 63) // 64), "bitmap"))
+        with self._stream(stream) as h:
+            return self._lib.fd_ed25519_hip_verify_fixed_dev(*args, h)
 
     def group_reduce_dev(self, n_groups, first, cnt, sig_codes, group_codes, stream=None):
         ng = int(n_groups)
-        return self._lib.fd_ed25519_hip_group_reduce_dev(
-            self.ctx, ng, self._p(first, 4 * ng, "first"), self._p(cnt, ng, "cnt"),
-            self._p(sig_codes, 1, "sig_codes"), self._p(group_codes, ng, "group_codes"), stream)
+        args = (self.ctx, ng, self._p(first, 4 * ng, "first"), self._p(cnt, ng, "cnt"),
+                self._p(sig_codes, 1, "sig_codes"), self._p(group_codes, ng, "group_codes"))
+        with self._stream(stream) as h:
+            return self._lib.fd_ed25519_hip_group_reduce_dev(*args, h)
 
     def sign_dev(self, n, prvs, pool, msg_off, msg_sz, pubs, sigs, stream=None):
         n = int(n)
-        return self._lib.fd_ed25519_hip_sign_dev(
-            self.ctx, n, self._p(prvs, 32 * n, "prvs"), self._p(pool, 1, "pool"), self._p(msg_off, 4 * n, "msg_off"),
-            self._p(msg_sz, 4 * n, "msg_sz"), self._p(pubs, 32 * n, "pubs"), self._p(sigs, 64 * n, "sigs"), stream)
+        args = (self.ctx, n, self._p(prvs, 32 * n, "prvs"), self._p(pool, 1, "pool"), self._p(msg_off, 4 * n, "msg_off"),
+                self._p(msg_sz, 4 * n, "msg_sz"), self._p(pubs, 32 * n, "pubs"), self._p(sigs, 64 * n, "sigs"))
+        with self._stream(stream) as h:
+            return self._lib.fd_ed25519_hip_sign_dev(*args, h)
 
     def set_halfsize(self, on):
         """Half-size scalars (default) or the full-length pair (k, 1): same verdicts."""
@@ -224,8 +280,17 @@ class Verifier:
     def test_halfsize(self, n, d_k, d_out, stream=None):
         """Test hook: device half-size reduction (see fd_ed25519_hip_test_halfsize)."""
         n = int(n)
-        return self._lib.fd_ed25519_hip_test_halfsize(self.ctx, n, self._p(d_k, 32 * n, "k"),
-                                                      self._p(d_out, 72 * n, "out"), stream)
+        args = (self.ctx, n, self._p(d_k, 32 * n, "k"), self._p(d_out, 72 * n, "out"))
+        with self._stream(stream) as h:
+            return self._lib.fd_ed25519_hip_test_halfsize(*args, h)
+
+    def test_sha512(self, n, pool, msg_off, msg_sz, out, stream=None):
+        """Test hook: device SHA-512 of n messages -> out (64 bytes each)."""
+        n = int(n)
+        args = (self.ctx, n, self._p(pool, 1, "pool"), self._p(msg_off, 4 * n, "msg_off"),
+                self._p(msg_sz, 4 * n, "msg_sz"), self._p(out, 64 * n, "out"))
+        with self._stream(stream) as h:
+            return self._lib.fd_ed25519_hip_test_sha512(*args, h)
 
     def set_timing(self, on):
         self._lib.fd_ed25519_hip_set_timing(self.ctx, 1 if on else 0)

@@ -81,9 +81,10 @@ class ReplayVerifier:
     def txn_verify_dev(self, n, pool, desc, result, stream=None):
         """pool: device bytes; desc: device fd_txn_hip_desc_t[n]; result: device int32[n]."""
         n, dev = int(n), self.verifier.device
-        rc = self._lib.fd_replay_hip_txn_verify_dev(self.r, n, _ptr(pool, 1, "pool", dev),
-                                                    _ptr(desc, 16 * n, "desc", dev),
-                                                    _ptr(result, 4 * n, "result", dev), stream)
+        args = (self.r, n, _ptr(pool, 1, "pool", dev), _ptr(desc, 16 * n, "desc", dev),
+                _ptr(result, 4 * n, "result", dev))
+        with self.verifier._stream(stream) as h:
+            rc = self._lib.fd_replay_hip_txn_verify_dev(*args, h)
         if rc:
             raise ValueError(f"fd_replay_hip_txn_verify_dev: n={n} > max_txn={self.max_txn}")
 
@@ -102,6 +103,7 @@ class ReplayVerifier:
 def fec_verify_roots_dev(verifier, n, roots, sigs, pubs, codes, stream=None):
     """FEC-set root check: codes[i] = fd_ed25519_verify(roots[32i:32i+32], sigs[i], pubs[i])."""
     n, dev = int(n), verifier.device
-    return lib().fd_fec_hip_verify_roots_dev(verifier.ctx, n, _ptr(roots, 32 * n, "roots", dev),
-                                             _ptr(sigs, 64 * n, "sigs", dev), _ptr(pubs, 32 * n, "pubs", dev),
-                                             _ptr(codes, n, "codes", dev), stream)
+    args = (verifier.ctx, n, _ptr(roots, 32 * n + 16, "roots (+16 readable bytes)", dev),
+            _ptr(sigs, 64 * n, "sigs", dev), _ptr(pubs, 32 * n, "pubs", dev), _ptr(codes, n, "codes", dev))
+    with verifier._stream(stream) as h:
+        return lib().fd_fec_hip_verify_roots_dev(*args, h)

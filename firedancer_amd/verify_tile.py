@@ -109,9 +109,10 @@ class Tcache:
 def parse_dev(verifier, n, pool, txn_off, txn_sz, txn_out, txn_t_sz, stream=None):
     """fd_txn_parse over n device-resident payloads (torch tensors / pointers)."""
     n, dev = int(n), verifier.device
-    return lib().fd_txn_hip_parse_dev(verifier.ctx, n, _ptr(pool, 1, "pool", dev), _ptr(txn_off, 4 * n, "txn_off", dev),
-                                      _ptr(txn_sz, 2 * n, "txn_sz", dev), _ptr(txn_out, 0, "txn_out", dev),
-                                      _ptr(txn_t_sz, 2 * n, "txn_t_sz", dev), stream)
+    args = (verifier.ctx, n, _ptr(pool, 1, "pool", dev), _ptr(txn_off, 4 * n, "txn_off", dev),
+            _ptr(txn_sz, 2 * n, "txn_sz", dev), _ptr(txn_out, 0, "txn_out", dev), _ptr(txn_t_sz, 2 * n, "txn_t_sz", dev))
+    with verifier._stream(stream) as h:
+        return lib().fd_txn_hip_parse_dev(*args, h)
 
 
 class VerifyTile:

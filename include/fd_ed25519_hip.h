@@ -35,7 +35,11 @@ typedef unsigned int  uint;
    Semantics, including the order of the checks and the error code of every
    reject, are those of the reference's AVX-512 build (fd_ed25519_user.c with
    avx512/fd_r43x6_ge.c decode); fd_ed25519_hip_set_errmode() switches the
-   error codes to the portable build's (the accept/reject bit is the same). */
+   error codes to the portable build's (the accept/reject bit is the same).
+   Each call is synchronous on a process-wide context (device
+   FD_ED25519_HIP_DEVICE, default 0), staged through pinned device-mapped
+   host memory.  msg_sz above 2^32-257 aborts the process (the engine's
+   message offsets are 32-bit; hashing a prefix would silently diverge). */
 
 struct fd_sha512_private;
 
@@ -68,7 +72,10 @@ fd_ed25519_strerror( int err );
    A context owns one HIP device, one stream, the LDS-staged base-point table
    and the scratch for up to chunk_sigs signatures in flight per launch
    (larger requests are processed in chunks of chunk_sigs).  Contexts are not
-   thread-safe; use one per host thread (one per verify tile).
+   thread-safe; use one per host thread (one per verify tile).  Calls on one
+   context may name different streams: each verify waits (hipStreamWaitEvent)
+   for the context's previous verify before it touches the shared scratch, so
+   they run in call order; calls on different contexts run concurrently.
 
    Record layout (all pointers are device pointers for *_dev, host pointers
    otherwise):
@@ -112,6 +119,13 @@ void                   fd_ed25519_hip_set_halfsize( fd_ed25519_hip_ctx_t * ctx, 
    0, max bit length).  Asynchronous on stream. */
 int fd_ed25519_hip_test_halfsize( fd_ed25519_hip_ctx_t * ctx, ulong n, uint const * d_k, uint * d_out,
                                   void * stream );
+
+/* Test hook: plain SHA-512 (fd_sha512_init/append/fini, fd_sha512.c:264-399)
+   of n messages d_pool[ d_msg_off[i], +d_msg_sz[i] ) with the device hash
+   core k_verify_prep uses; 64-byte digests to d_out + 64*i (16-byte aligned).
+   Asynchronous on stream. */
+int fd_ed25519_hip_test_sha512( fd_ed25519_hip_ctx_t * ctx, ulong n, uchar const * d_pool, uint const * d_msg_off,
+                                uint const * d_msg_sz, uchar * d_out, void * stream );
 
 /* Kernel timing for measurement legs: when on, every verify chunk brackets
    k_verify_prep and k_verify_dsm with HIP events on the launch stream and

@@ -51,3 +51,22 @@ def test_gloo_world2_bitmap_gather(n):
     mp.spawn(_worker, args=(world, port, n, ret), nprocs=world, join=True)
     assert all(ret[r][0] for r in range(world))
     assert all(ret[r][1] == float(world) for r in range(world))
+
+
+def test_bench_c5_shards_cover_2p26():
+    """bench.py's C5 shard arithmetic (c5_shard) covers 2^26 signatures
+    exactly, contiguously and disjointly at world 1/2/4/8, with bitmap-word
+    aligned boundaries and per-rank shards the 2^20-signature chunking of a
+    context splits without remainder."""
+    import bench
+    for world in (1, 2, 4, 8):
+        spans = [bench.c5_shard(None, r, world) for r in range(world)]
+        assert all(t == 1 << 26 for t, _, _ in spans)
+        assert spans[0][1] == 0 and spans[-1][2] == 1 << 26
+        for (_, _, hi), (_, lo, _) in zip(spans, spans[1:]):
+            assert hi == lo
+        sizes = [hi - lo for _, lo, hi in spans]
+        assert sum(sizes) == 1 << 26 and len(set(sizes)) == 1
+        assert all(s % 64 == 0 and s % (1 << 20) == 0 for s in sizes)
+    t, lo, hi = bench.c5_shard(1 << 21, 1, 2)               # --sigs per rank (the gloo rehearsal)
+    assert (t, lo, hi) == (1 << 22, 1 << 21, 1 << 22)

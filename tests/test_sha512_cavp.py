@@ -1,0 +1,76 @@
+"""SHA-512 pinned by the reference's own CAVP vectors
+(src/ballet/sha512/cavp/SHA512{Short,Long}Msg.rsp, extracted by
+tests/golden/gen_cavp.py: 129 short messages of 0..128 bytes, 128 long ones of
+up to 6.4 KB).
+
+CPU: the oracle's SHA-512 (oracle/fd_ed25519_oracle.c) and hashlib on every
+vector.  GPU: the device hash core k_verify_prep uses (sha512_prefixed, via
+the fd_ed25519_hip_test_sha512 hook), every vector in one launch, bit-exact.
+"""
+import hashlib
+import os
+
+import numpy as np
+import pytest
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+@pytest.fixture(scope="module")
+def cavp():
+    d = np.load(os.path.join(HERE, "golden", "sha512_cavp.npz"))
+    return {k: d[k] for k in d.files}
+
+
+def test_fixture_shape(cavp):
+    assert cavp["off"].size == 257 and (cavp["src"] == 0).sum() == 129
+    assert cavp["len"].max() > 6000 and cavp["len"].min() == 0
+
+
+def test_oracle_and_hashlib_match_cavp(cavp):
+    import oracle_lib as O
+    pool = cavp["pool"].tobytes()
+    for o, n, md in zip(cavp["off"], cavp["len"], cavp["md"]):
+        m = pool[o:o + n]
+        assert hashlib.sha512(m).digest() == md.tobytes()
+        assert O.sha512(m) == md.tobytes()
+
+
+@pytest.mark.gpu
+def test_device_sha512_matches_cavp(verifier, cavp):
+    import torch
+    dev = torch.device("cuda", 0)
+    n = cavp["off"].size
+    pool = torch.from_numpy(cavp["pool"]).to(dev)
+    off = torch.from_numpy(cavp["off"].view(np.int32)).to(dev)
+    ln = torch.from_numpy(cavp["len"].view(np.int32)).to(dev)
+    out = torch.zeros((n, 64), dtype=torch.uint8, device=dev)
+    verifier.test_sha512(n, pool, off, ln, out)
+    got = out.cpu().numpy()
+    bad = np.nonzero((got != cavp["md"]).any(axis=1))[0]
+    assert bad.size == 0, [(int(i), int(cavp["len"][i])) for i in bad[:10]]
+
+
+@pytest.mark.gpu
+def test_device_sha512_unaligned_and_block_edges(verifier):
+    """Every length 0..300 (all padding cases: message end at each byte of a
+    128-B block, the 0x80 byte and the 16-B length straddling blocks) at all
+    four byte alignments of the pool, against hashlib."""
+    import torch
+    rng = np.random.default_rng(3)
+    lens = np.repeat(np.arange(301, dtype=np.uint32), 4)
+    align = np.tile(np.arange(4, dtype=np.uint32), 301)
+    offs, pos = [], 0
+    for n, a in zip(lens, align):
+        pos = (pos + 15) // 16 * 16 + int(a)
+        offs.append(pos)
+        pos += int(n)
+    raw = rng.integers(0, 256, pos + 16, dtype=np.uint8)
+    dev = torch.device("cuda", 0)
+    out = torch.zeros((lens.size, 64), dtype=torch.uint8, device=dev)
+    verifier.test_sha512(lens.size, torch.from_numpy(raw).to(dev),
+                         torch.from_numpy(np.array(offs, np.uint32).view(np.int32)).to(dev),
+                         torch.from_numpy(lens.view(np.int32)).to(dev), out)
+    got = out.cpu().numpy()
+    for i, (o, n) in enumerate(zip(offs, lens)):
+        assert got[i].tobytes() == hashlib.sha512(raw[o:o + n].tobytes()).digest(), (i, n, o % 4)
