@@ -193,6 +193,8 @@ def main():
                     help="c1/c2/c3/c5: verify contexts (streams) each step is split over (measured with the "
                          "persistent DSM: 1 -> 118.2M, 2 -> 125.0-125.7M, 4 -> 124.5M verifies/s)")
     ap.add_argument("--tiles", type=int, default=8, help="c4: verify tiles (host threads + contexts) per GPU")
+    ap.add_argument("--c4-ingest", default="frags", choices=["frags", "payload"],
+                    help="c4: fd_txn_m_t frags in each tile's in-link dcache (default) or raw payloads + offsets")
     ap.add_argument("--sigs", type=int, default=None, help="override signatures per GPU per step")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--cpu-seconds", type=float, default=8.0)
@@ -451,45 +453,93 @@ def ref_tile_baseline(pool, off, sz, threads, target_s, seed, depth):
 def run_c4(args, rank, world, local, dist):
     """Config 4: synthetic Solana txn stream through the verify tile.
 
-    A step is one batch of --txns frags (raw payloads resident in HBM) through
-    --tiles GPU verify tiles (fd_verify_hip_tile) sharing the GPU, the frags
-    split round robin between them as the reference splits them between its
-    verify tiles (fd_verify_tile.c before_frag: seq % round_robin_cnt).  Each
-    tile owns a context (stream), a tcache of depth 4194302 (the reference
-    default signature_cache_size) and a host thread, and runs GPU parse + sig0
-    tag + record expansion + verify + per-txn batch_single_msg reduce, then
-    the ordered host pass (tcache dedup, bundle state).  Batches are submitted
-    one ahead, so a tile's host pass of batch k overlaps the GPU work of batch
-    k+1.  Each step re-keys the dedup hash so the replayed batch is new traffic
-    to the tcache (once a tcache is full every insert also evicts, the steady
-    state of a long-running tile); in-batch resends still dedup.
-    value = signatures verified per second (all tiles, all ranks)."""
+    A step is one batch of --txns frags through --tiles GPU verify tiles
+    (fd_verify_hip_tile) sharing the GPU, the frags split round robin between
+    them as the reference splits them between its verify tiles
+    (fd_verify_tile.c before_frag: seq % round_robin_cnt).  Ingest (--c4-ingest):
+      frags    (default) the tile's own format: each tile's in-link dcache of
+               fd_txn_m_t frags (src/disco/fd_txn_m.h) in HBM; the GPU does
+               during_frag's copy into the out dcache and after_frag's parse
+               in place (fd_verify_hip_tile_submit_frags)
+      payload  raw payloads + caller-marshalled offsets (round 1's path)
+    Each tile owns a context (stream), a tcache of depth 4194302 (the
+    reference default signature_cache_size) and a host thread, and runs GPU
+    ingest/parse + sig0 tag + record expansion + verify + per-txn
+    batch_single_msg reduce, then the ordered host pass (tcache dedup,
+    bundle state).  Batches are submitted one ahead, so a tile's host pass of
+    batch k overlaps the GPU work of batch k+1.  Each step re-keys the dedup
+    hash so the replayed batch is new traffic to the tcache (once a tcache is
+    full every insert also evicts, the steady state of a long-running tile);
+    in-batch resends still dedup.
+    value = signatures verified per second (all tiles, all ranks), in-link
+    dcaches resident in HBM.  A second timed leg (frags ingest) copies every
+    tile's in-link dcache host->HBM each step from pinned memory on a copy
+    stream, double-buffered so the copy of batch k+1 overlaps the GPU work of
+    batch k: "pcie_inclusive"."""
     import threading
 
     import torch
     from firedancer_amd import Verifier
-    from firedancer_amd.txn_workload import gpu_signer, make_txn_stream
-    from firedancer_amd.verify_tile import VerifyTile
+    from firedancer_amd.txn_workload import PARSED_CHUNKS, gpu_signer, make_txn_stream, txnm_dcache
+    from firedancer_amd.verify_tile import IN_QUIC, VerifyTile
     T = max(1, args.tiles)
+    frags_mode = args.c4_ingest == "frags"
     v = Verifier(device=local, chunk_sigs=1 << 20)
     seed_base = 0x7f4a11 + 104729 * rank
     s = make_txn_stream(args.txns, gpu_signer(v), seed=0x5eed0004 + 7919 * rank)
     dev = torch.device("cuda", local)
-    d_pool = torch.from_numpy(s.pool).to(dev)
     depth = 4194302
     vs = [v] + [Verifier(device=local, chunk_sigs=1 << 16) for _ in range(T - 1)]
-    parts = []
+    to_dev = lambda a, view=None: torch.from_numpy(np.ascontiguousarray(a if view is None else a.view(view))).to(dev)
+    parts, h2d_bytes = [], 0
+    d_pool = None if frags_mode else to_dev(s.pool)
     for t in range(T):
         sel = np.arange(t, s.n, T)
-        parts.append((int(sel.size), torch.from_numpy(np.ascontiguousarray(s.off[sel]).view(np.int32)).to(dev),
-                      torch.from_numpy(np.ascontiguousarray(s.sz[sel]).view(np.int16)).to(dev)))
-    tiles = [VerifyTile(vs[t], max_txn=parts[t][0], hashmap_seed=seed_base, tcache_depth=depth) for t in range(T)]
+        if frags_mode:
+            region, chunk, fsz = txnm_dcache(s.pool, s.off[sel], s.sz[sel], seed=t + 1)
+            h_in = torch.from_numpy(region).pin_memory()
+            d_in = [to_dev(region), torch.empty_like(h_in, device=dev)]
+            d_out = torch.empty(64 * PARSED_CHUNKS * max(int(sel.size), 1), dtype=torch.uint8, device=dev)
+            out_chunk = to_dev((np.arange(sel.size) * PARSED_CHUNKS).astype(np.uint32), np.int32)
+            kinds = to_dev(np.full(sel.size, IN_QUIC, np.uint8))
+            parts.append(dict(n=int(sel.size), h_in=h_in, d_in=d_in, d_out=d_out, in_chunk=to_dev(chunk, np.int32),
+                              in_sz=to_dev(fsz, np.int16), kinds=kinds, out_chunk=out_chunk,
+                              cs=torch.cuda.Stream(dev), ts=torch.cuda.ExternalStream(vs[t].stream, device=dev),
+                              free=[None, None]))
+            h2d_bytes += region.size
+        else:
+            parts.append(dict(n=int(sel.size), off=to_dev(s.off[sel], np.int32), sz=to_dev(s.sz[sel], np.int16)))
+    tiles = [VerifyTile(vs[t], max_txn=parts[t]["n"], hashmap_seed=seed_base, tcache_depth=depth) for t in range(T)]
     k_step = [0] * T
     diag = os.environ.get("FD_C4_DIAG")
+    h2d = [False]
 
     def submit(t):
-        tiles[t].set_seed(seed_base + 7 * k_step[t]); k_step[t] += 1
-        tiles[t].submit(parts[t][0], d_pool, parts[t][1], parts[t][2])
+        P = parts[t]
+        tiles[t].set_seed(seed_base + 7 * k_step[t])
+        if not frags_mode:
+            tiles[t].submit(P["n"], d_pool, P["off"], P["sz"])
+        elif not h2d[0]:
+            tiles[t].submit_frags(P["n"], P["d_in"][0], P["in_chunk"], P["in_sz"], P["kinds"], P["d_out"],
+                                  P["out_chunk"])
+        else:
+            # copy this batch's in-link dcache host -> HBM on the tile's copy
+            # stream (pinned, DMA engine) into the buffer batch k-2 used, once
+            # that batch's GPU work has read it; the tile stream waits for it
+            b = k_step[t] & 1
+            buf = P["d_in"][b]
+            with torch.cuda.stream(P["cs"]):
+                if P["free"][b] is not None:
+                    P["cs"].wait_event(P["free"][b])
+                buf.copy_(P["h_in"], non_blocking=True)
+                ready = torch.cuda.Event()
+                ready.record(P["cs"])
+            P["ts"].wait_event(ready)
+            tiles[t].submit_frags(P["n"], buf, P["in_chunk"], P["in_sz"], P["kinds"], P["d_out"], P["out_chunk"])
+            done = torch.cuda.Event()
+            done.record(P["ts"])
+            P["free"][b] = done
+        k_step[t] += 1
 
     def tile_loop(t, steps, outs, gpu_ms, host_ms):
         submit(t)
@@ -515,30 +565,47 @@ def run_c4(args, rank, world, local, dist):
         ms = [tl.metrics() for tl in tiles]
         return {k: sum(m[k] for m in ms) for k in ms[0]}
 
-    torch.cuda.synchronize()          # payload upload before the tile streams read it
+    def timed(steps):
+        torch.cuda.synchronize()
+        if dist:
+            dist.barrier()
+        torch.cuda.synchronize()
+        m0 = metrics()
+        t0 = time.perf_counter()
+        outs, gpu_ms, host_ms = run(steps)
+        torch.cuda.synchronize()
+        if dist:
+            dist.barrier()
+        torch.cuda.synchronize()
+        elapsed = time.perf_counter() - t0
+        m1 = metrics()
+        sigs = m1["sigs"] - m0["sigs"]
+        frags = s.n * steps
+        if dist:
+            t = torch.tensor([elapsed], dtype=torch.float64, device=COLL_DEV)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            elapsed = float(t.item())
+            tt = torch.tensor([sigs, frags], dtype=torch.int64, device=COLL_DEV)
+            dist.all_reduce(tt)
+            sigs, frags = int(tt[0].item()), int(tt[1].item())
+        return elapsed, sigs, frags, outs, gpu_ms, host_ms, m1["sigs"] - m0["sigs"]
+
+    torch.cuda.synchronize()          # uploads before the tile streams read them
     run(max(args.warmup, 1))
-    torch.cuda.synchronize()
-    if dist:
-        dist.barrier()
-    torch.cuda.synchronize()
-    m0 = metrics()
-    t0 = time.perf_counter()
-    outs, gpu_ms, host_ms = run(args.steps)
-    torch.cuda.synchronize()
-    if dist:
-        dist.barrier()
-    torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
-    m1 = metrics()
-    sigs = m1["sigs"] - m0["sigs"]
-    frags = s.n * args.steps
-    if dist:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=COLL_DEV)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
-        tt = torch.tensor([sigs, frags], dtype=torch.int64, device=COLL_DEV)
-        dist.all_reduce(tt)
-        sigs, frags = int(tt[0].item()), int(tt[1].item())
+    elapsed, sigs, frags, outs, gpu_ms, host_ms, my_sigs = timed(args.steps)
+    pcie = None
+    if frags_mode:
+        h2d[0] = True
+        run(1)
+        e2, sigs2, _, outs2, _, _, _ = timed(args.steps)
+        same = all(np.array_equal(a[-1][0], b[-1][0]) for a, b in zip(outs, outs2))
+        pcie = {"value": round(sigs2 / e2, 1), "unit": "verifies/s", "ms_per_step": round(e2 / args.steps * 1e3, 4),
+                "h2d_bytes_per_step": h2d_bytes * world, "h2d_GBps": round(h2d_bytes * world * args.steps / e2 / 1e9, 2),
+                "results_equal_resident_leg": bool(same),
+                "what": "every tile's in-link dcache (fd_txn_m_t frags) copied host->HBM each step from pinned memory "
+                        "(copy stream per tile, double-buffered, overlapped with the previous batch); per-frag "
+                        "results D2H as in the resident leg; the out dcache stays in HBM"}
+        h2d[0] = False
     res = np.concatenate([o[-1][0] for o in outs])
     gpu_ms = [x for g in gpu_ms for x in g]; host_ms = [x for h in host_ms for x in h]
     # kernel roofline: one extra (untimed) batch of tile 0 with per-kernel HIP-event timing
@@ -547,7 +614,7 @@ def run_c4(args, rank, world, local, dist):
     prep_ms, dsm_ms, launches = v.get_timing()
     dsm_units = v.get_dsm_units()
     v.set_timing(False)
-    n_sig_batch = int(m1["sigs"] - m0["sigs"]) // max(args.steps, 1)
+    n_sig_batch = int(my_sigs) // max(args.steps, 1)
     launches = max(launches, 1)
     out = None
     if rank == 0:
@@ -585,13 +652,14 @@ def run_c4(args, rank, world, local, dist):
             "frag_outcomes_last_batch": {names[k]: v_ for k, v_ in counts.items()},
             "batch_gpu_ms": round(float(np.median(gpu_ms)), 4),
             "batch_host_ms": round(float(np.median(host_ms)), 4),
-            "roofline": {"bound": "valu_int32", "kernel": "k_verify_dsm",
-                         "achieved": round(achieved, 3), "peak": round(PEAK_OPS / 1e12, 3), "unit": "Tops/s",
-                         "frac": round(achieved / (PEAK_OPS / 1e12), 4), "traffic": None,
-                         "algorithmic_ops_per_unit": round(W_DSM), "units_per_launch": round(dsm_units / launches),
-                         "executed_frac": round(achieved * W_DSM_EXEC / W_DSM / (PEAK_OPS / 1e12), 4),
+            "roofline": dict(issue_roofline(dsm_avg, dsm_units / launches) or {}, **{
+                         "kernel": "k_verify_dsm", "traffic": None, "units_per_launch": round(dsm_units / launches),
+                         "ref_work_rate_vs_peak": round(achieved / (PEAK_OPS / 1e12), 4),
                          "avg_launch_ms": round(dsm_avg, 4), "launches_per_batch": launches,
-                         "prep_ms_per_batch": round(prep_ms, 4)},
+                         "prep_ms_per_batch": round(prep_ms, 4),
+                         "timing_leg": "one extra batch of tile 0 alone, HIP events around each launch"}),
+            "ingest": args.c4_ingest,
+            "pcie_inclusive": pcie,
             "cpu_baseline": cpu,
         }
         emit(out)

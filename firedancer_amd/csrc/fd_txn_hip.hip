@@ -241,16 +241,22 @@ struct parse_out {
   u64 * tag;
 };
 
+/* tout (fd_txn_m_t frag mode): fd_txn_t of frag j at pool + tout[j] (the
+   fd_txn_m_txn_t address, fd_txn_m.h:101-104) instead of txn_out + 852*j,
+   and txn_t_sz written into the frag header (pool + off[j] - 80 + 10) as
+   after_frag does (fd_verify_tile.c:120) */
 __global__ __launch_bounds__(256)
 void k_txn_parse( ulong n, u8 const * __restrict__ pool, u32 const * __restrict__ off,
-                  u16 const * __restrict__ sz, u8 * __restrict__ txn_out, u64 seed, parse_out po ) {
+                  u16 const * __restrict__ sz, u8 * __restrict__ txn_out, u64 seed, parse_out po,
+                  u32 const * __restrict__ tout ) {
   ulong j = (ulong)blockIdx.x * blockDim.x + threadIdx.x;
   if( j >= n ) return;
   u32 base = off[j];
   u8 const * p = pool + base;
-  u8 * out = txn_out ? txn_out + (ulong)FD_TXN_HIP_MAX_SZ * j : (u8 *)0;
+  u8 * out = tout ? (u8 *)pool + tout[j] : txn_out ? txn_out + (ulong)FD_TXN_HIP_MAX_SZ * j : (u8 *)0;
   txn_span sp = { 0u, 0u, 0u, 0u, 0u, 0u };
   u32 tsz = txn_parse( p, sz[j], out, sp );
+  if( tout ) *(u16 *)((u8 *)pool + base - FD_VERIFY_HIP_TXNM_SZ + FD_VERIFY_HIP_TXNM_TXN_T_SZ_OFF) = (u16)tsz;
   if( !po.tsz ) { return; }
   po.tsz[j] = (u16)tsz;
   if( !po.nsig ) return;
@@ -350,6 +356,69 @@ void k_txn_expand( ulong n, u8 const * __restrict__ pool, u8 const * __restrict_
   }
 }
 
+/* fd_txn_m_t frag ingest: during_frag (fd_verify_tile.c:64-99) for a batch.
+   One wave per frag (frags strided over the grid's waves), 64 B-aligned
+   dcache chunks in and out (fd_chunk_to_laddr: mem + 64*chunk):
+     QUIC / BUNDLE / SEND  copy the sz-byte frag in -> out (16 B per lane per
+                           round, coalesced); sz > FD_TPU_RAW_MTU or a
+                           header payload_sz > FD_TPU_MTU is a corrupt frag
+     GOSSIP                fd_gossip_update_message_t vote -> fd_txn_m_t:
+                           payload_sz = vote.txn_sz, bundle_id = 0,
+                           source_ipv4 = vote.socket.addr, source_tpu =
+                           GOSSIP, payload = vote.txn; sz > 2048 (or a
+                           txn_sz past the 1232-B vote buffer) is corrupt
+   Per frag it emits the payload span for k_txn_parse, the fd_txn_m_txn_t
+   offset and the header's bundle_id for the ordered host pass.  A corrupt
+   frag sets bit 0 of *flag (the reference's FD_LOG_ERR: the host aborts in
+   complete()) and is parsed as an empty payload. */
+DEVI void copy_bytes( u8 * __restrict__ d, u8 const * __restrict__ s, u32 nb, u32 lane ) {   /* d, s 16-B aligned */
+  u32 full = nb >> 4;
+  for( u32 q = lane; q < full; q += 64u ) ((uint4 *)d)[q] = ((uint4 const *)s)[q];
+  u32 t = full << 4;
+  if( lane < nb - t ) d[t + lane] = s[t + lane];                 /* < 16 tail bytes, one per lane */
+}
+
+__global__ __launch_bounds__(256)
+void k_txnm_ingest( ulong n, u8 const * __restrict__ in, u32 const * __restrict__ in_chunk,
+                    u16 const * __restrict__ in_sz, u8 const * __restrict__ in_kind, u8 * __restrict__ out,
+                    u32 const * __restrict__ out_chunk, u32 * __restrict__ pay_off, u16 * __restrict__ pay_sz,
+                    u32 * __restrict__ tout, u64 * __restrict__ bid, u32 * __restrict__ flag ) {
+  u32 lane = threadIdx.x & 63u;
+  ulong w = ((ulong)blockIdx.x * blockDim.x + threadIdx.x) >> 6, nw = ((ulong)gridDim.x * blockDim.x) >> 6;
+  for( ulong j = w; j < n; j += nw ) {
+    u8 const * src = in + 64ul * in_chunk[j];
+    u32 ob = 64u * out_chunk[j];
+    u8 * dst = out + ob;
+    u32 sz = in_sz[j], kind = in_kind[j], psz = 0u, bad = 0u;
+    u64 b = 0ul;
+    if( kind == FD_VERIFY_HIP_IN_GOSSIP ) {
+      u64 tsz = *(u64 const *)(src + FD_VERIFY_HIP_GOSSIP_VOTE_TXN_SZ_OFF);
+      bad = sz > 2048u || tsz > FD_TXN_HIP_MTU;
+      psz = bad ? 0u : (u32)tsz;
+      copy_bytes( dst + FD_VERIFY_HIP_TXNM_SZ, src + FD_VERIFY_HIP_GOSSIP_VOTE_TXN_OFF, psz, lane );
+      if( lane == 0u ) {
+        *(u16 *)(dst + FD_VERIFY_HIP_TXNM_PAYLOAD_SZ_OFF) = (u16)psz;
+        *(u64 *)(dst + FD_VERIFY_HIP_TXNM_BUNDLE_ID_OFF) = 0ul;
+        *(u32 *)(dst + FD_VERIFY_HIP_TXNM_SRC_IPV4_OFF) = *(u32 const *)(src + FD_VERIFY_HIP_GOSSIP_VOTE_ADDR_OFF);
+        dst[FD_VERIFY_HIP_TXNM_SRC_TPU_OFF] = (u8)FD_VERIFY_HIP_TPU_SOURCE_GOSSIP;
+      }
+    } else {
+      bad = sz > FD_VERIFY_HIP_TPU_RAW_MTU;
+      copy_bytes( dst, src, bad ? 0u : sz, lane );
+      psz = bad ? 0u : *(u16 const *)(src + FD_VERIFY_HIP_TXNM_PAYLOAD_SZ_OFF);
+      b   = bad ? 0ul : *(u64 const *)(src + FD_VERIFY_HIP_TXNM_BUNDLE_ID_OFF);
+      if( psz > FD_TXN_HIP_MTU ) { bad = 1u; psz = 0u; }
+    }
+    if( lane == 0u ) {
+      u32 po = ob + FD_VERIFY_HIP_TXNM_SZ;
+      pay_off[j] = po; pay_sz[j] = (u16)psz;
+      tout[j] = (po + psz + (FD_VERIFY_HIP_TXN_ALIGN - 1u)) & ~(FD_VERIFY_HIP_TXN_ALIGN - 1u);
+      bid[j] = b;
+      if( bad ) atomicOr( flag, 1u );
+    }
+  }
+}
+
 extern "C" int
 fd_txn_hip_parse_dev( fd_ed25519_hip_ctx_t * ctx, ulong n, uchar const * d_pool, uint const * d_txn_off,
                       ushort const * d_txn_sz, uchar * d_txn_out, ushort * d_txn_t_sz, void * stream ) {
@@ -358,7 +427,7 @@ fd_txn_hip_parse_dev( fd_ed25519_hip_ctx_t * ctx, ulong n, uchar const * d_pool,
   if( !n ) return 0;
   parse_out po = { d_txn_t_sz, 0, 0, 0, 0, 0, 0 };
   hipLaunchKernelGGL( k_txn_parse, dim3( (unsigned)((n + 255)/256) ), dim3( 256 ), 0, s,
-                      n, d_pool, d_txn_off, d_txn_sz, d_txn_out, (u64)0, po );
+                      n, d_pool, d_txn_off, d_txn_sz, d_txn_out, (u64)0, po, (u32 const *)0 );
   TX_CHECK( hipGetLastError() );
   return 0;
 }
@@ -435,6 +504,11 @@ struct tile_slot {
   u8 *          d_rsig; u8 * d_rpub; u32 * d_rmoff; u32 * d_rmsz; signed char * d_rcode;
   /* per frag, pinned host */
   u16 *         h_tsz; signed char * h_tcode; u64 * h_tag; u32 * h_counter;
+  /* fd_txn_m_t frag mode (submit_frags): payload spans, fd_txn_t offsets,
+     header bundle ids, in kinds and the corrupt-frag flag */
+  u32 *         d_pay_off; u16 * d_pay_sz; u32 * d_tout; u64 * d_bid; u32 * d_flag;
+  u64 *         h_bid; u8 * h_kind; u32 * h_flag;
+  int           frags;
   hipEvent_t    ev_start, ev_done;
   int           busy;
 };
@@ -448,7 +522,7 @@ struct fd_verify_hip_tile {
   ulong *    oldest; ulong * ring; ulong depth; ulong * map; ulong map_cnt;
   /* bundle state (fd_verify_ctx_t bundle_failed / bundle_id) */
   int        bundle_failed; ulong bundle_id;
-  ulong      m_parse, m_verify, m_dedup, m_bundle, m_pub, m_sigs;
+  ulong      m_parse, m_verify, m_dedup, m_bundle, m_pub, m_sigs, m_gossip;
   tile_slot  slot[2];
   ulong      submitted, completed;
   double     last_gpu_ms, last_host_ms, last_sigs;
@@ -464,6 +538,11 @@ static void slot_alloc( tile_slot & s, ulong n ) {
   TX_CHECK( hipMalloc( &s.d_counter, 4 ) );
   TX_CHECK( hipHostMalloc( &s.h_tsz, 2*n, 0 ) );  TX_CHECK( hipHostMalloc( &s.h_tcode, n, 0 ) );
   TX_CHECK( hipHostMalloc( &s.h_tag, 8*n, 0 ) );  TX_CHECK( hipHostMalloc( &s.h_counter, 4, 0 ) );
+  TX_CHECK( hipMalloc( &s.d_pay_off, 4*n ) );     TX_CHECK( hipMalloc( &s.d_pay_sz, 2*n ) );
+  TX_CHECK( hipMalloc( &s.d_tout, 4*n ) );        TX_CHECK( hipMalloc( &s.d_bid, 8*n ) );
+  TX_CHECK( hipMalloc( &s.d_flag, 4 ) );
+  TX_CHECK( hipHostMalloc( &s.h_bid, 8*n, 0 ) );  TX_CHECK( hipHostMalloc( &s.h_kind, n, 0 ) );
+  TX_CHECK( hipHostMalloc( &s.h_flag, 4, 0 ) );
   TX_CHECK( hipEventCreate( &s.ev_start ) ); TX_CHECK( hipEventCreate( &s.ev_done ) );
 }
 
@@ -479,6 +558,9 @@ static void slot_free( tile_slot & s ) {
   (void)hipFree( s.d_cnt ); (void)hipFree( s.d_tcode ); (void)hipFree( s.d_counter );
   (void)hipHostFree( s.h_tsz ); (void)hipHostFree( s.h_tcode ); (void)hipHostFree( s.h_tag );
   (void)hipHostFree( s.h_counter );
+  (void)hipFree( s.d_pay_off ); (void)hipFree( s.d_pay_sz ); (void)hipFree( s.d_tout ); (void)hipFree( s.d_bid );
+  (void)hipFree( s.d_flag );
+  (void)hipHostFree( s.h_bid ); (void)hipHostFree( s.h_kind ); (void)hipHostFree( s.h_flag );
   (void)hipEventDestroy( s.ev_start ); (void)hipEventDestroy( s.ev_done );
   slot_free_records( s );
 }
@@ -519,21 +601,12 @@ extern "C" void fd_verify_hip_tile_delete( fd_verify_hip_tile_t * t ) {
   free( t->own_mem ); free( t );
 }
 
-extern "C" int
-fd_verify_hip_tile_submit( fd_verify_hip_tile_t * t, ulong n, uchar const * d_pool, uint const * d_txn_off,
-                           ushort const * d_txn_sz, uchar * d_txn_out ) {
-  if( n > t->max_txn ) return -1;
-  tile_slot & s = t->slot[t->submitted & 1];
-  if( s.busy ) return -2;                                   /* two batches outstanding */
-  hipStream_t st = (hipStream_t)fd_ed25519_hip_ctx_stream( t->ctx );
-  TX_CHECK( hipSetDevice( fd_ed25519_hip_ctx_device( t->ctx ) ) );
-  s.n = n; s.nsig = 0; s.busy = 1; t->submitted++;
-  TX_CHECK( hipEventRecord( s.ev_start, st ) );
-  if( !n ) { TX_CHECK( hipEventRecord( s.ev_done, st ) ); return 0; }
+/* the part of a batch both submit forms share: record capacity, expansion,
+   verify, per-txn reduce and the D2H of the per-frag results; the payloads
+   are pool[ off[j], +sz[j] ) after k_txn_parse has filled the slot */
+static void
+submit_verify( fd_verify_hip_tile_t * t, tile_slot & s, hipStream_t st, ulong n, uchar const * d_pool ) {
   dim3 grid( (unsigned)((n + 255)/256) ), blk( 256 );
-  parse_out po = { s.d_tsz, s.d_nsig, s.d_sig_at, s.d_acct_at, s.d_msg_at, s.d_msg_sz, s.d_tag };
-  hipLaunchKernelGGL( k_txn_parse, grid, blk, 0, st, n, d_pool, d_txn_off, d_txn_sz, d_txn_out, (u64)t->seed, po );
-  TX_CHECK( hipGetLastError() );
   /* record capacity: a parsed frag carries at most 12 signatures (96 B of
      sig + pubkey each within FD_TXN_MTU, fd_txn.h:68); grow to that bound
      once instead of reading the count back twice */
@@ -559,6 +632,64 @@ fd_verify_hip_tile_submit( fd_verify_hip_tile_t * t, ulong n, uchar const * d_po
   TX_CHECK( hipMemcpyAsync( s.h_tsz, s.d_tsz, 2*n, hipMemcpyDeviceToHost, st ) );
   TX_CHECK( hipMemcpyAsync( s.h_tcode, s.d_tcode, n, hipMemcpyDeviceToHost, st ) );
   TX_CHECK( hipMemcpyAsync( s.h_tag, s.d_tag, 8*n, hipMemcpyDeviceToHost, st ) );
+}
+
+static tile_slot *
+submit_begin( fd_verify_hip_tile_t * t, ulong n, hipStream_t & st, int & rc ) {
+  rc = 0;
+  if( n > t->max_txn ) { rc = -1; return 0; }
+  tile_slot & s = t->slot[t->submitted & 1];
+  if( s.busy ) { rc = -2; return 0; }                        /* two batches outstanding */
+  st = (hipStream_t)fd_ed25519_hip_ctx_stream( t->ctx );
+  TX_CHECK( hipSetDevice( fd_ed25519_hip_ctx_device( t->ctx ) ) );
+  s.n = n; s.nsig = 0; s.busy = 1; s.frags = 0; t->submitted++;
+  TX_CHECK( hipEventRecord( s.ev_start, st ) );
+  return &s;
+}
+
+extern "C" int
+fd_verify_hip_tile_submit( fd_verify_hip_tile_t * t, ulong n, uchar const * d_pool, uint const * d_txn_off,
+                           ushort const * d_txn_sz, uchar * d_txn_out ) {
+  hipStream_t st; int rc;
+  tile_slot * sp = submit_begin( t, n, st, rc );
+  if( !sp ) return rc;
+  tile_slot & s = *sp;
+  if( !n ) { TX_CHECK( hipEventRecord( s.ev_done, st ) ); return 0; }
+  dim3 grid( (unsigned)((n + 255)/256) ), blk( 256 );
+  parse_out po = { s.d_tsz, s.d_nsig, s.d_sig_at, s.d_acct_at, s.d_msg_at, s.d_msg_sz, s.d_tag };
+  hipLaunchKernelGGL( k_txn_parse, grid, blk, 0, st, n, d_pool, d_txn_off, d_txn_sz, d_txn_out, (u64)t->seed, po,
+                      (u32 const *)0 );
+  TX_CHECK( hipGetLastError() );
+  submit_verify( t, s, st, n, d_pool );
+  TX_CHECK( hipEventRecord( s.ev_done, st ) );
+  return 0;
+}
+
+extern "C" int
+fd_verify_hip_tile_submit_frags( fd_verify_hip_tile_t * t, ulong n, uchar const * d_in, uint const * d_in_chunk,
+                                 ushort const * d_in_sz, uchar const * d_in_kind, uchar * d_out,
+                                 uint const * d_out_chunk ) {
+  hipStream_t st; int rc;
+  tile_slot * sp = submit_begin( t, n, st, rc );
+  if( !sp ) return rc;
+  tile_slot & s = *sp;
+  s.frags = 1;
+  if( !n ) { *s.h_flag = 0u; TX_CHECK( hipEventRecord( s.ev_done, st ) ); return 0; }
+  dim3 grid( (unsigned)((n + 255)/256) ), blk( 256 );
+  TX_CHECK( hipMemsetAsync( s.d_flag, 0, 4, st ) );
+  /* one wave per frag: up to 4 frags per 256-thread workgroup, grid capped */
+  ulong wgs = (n + 3ul) / 4ul; if( wgs > 8192ul ) wgs = 8192ul;
+  hipLaunchKernelGGL( k_txnm_ingest, dim3( (unsigned)wgs ), blk, 0, st, n, d_in, d_in_chunk, d_in_sz, d_in_kind,
+                      d_out, d_out_chunk, s.d_pay_off, s.d_pay_sz, s.d_tout, s.d_bid, s.d_flag );
+  TX_CHECK( hipGetLastError() );
+  parse_out po = { s.d_tsz, s.d_nsig, s.d_sig_at, s.d_acct_at, s.d_msg_at, s.d_msg_sz, s.d_tag };
+  hipLaunchKernelGGL( k_txn_parse, grid, blk, 0, st, n, (u8 const *)d_out, s.d_pay_off, s.d_pay_sz, (u8 *)0,
+                      (u64)t->seed, po, s.d_tout );
+  TX_CHECK( hipGetLastError() );
+  submit_verify( t, s, st, n, d_out );
+  TX_CHECK( hipMemcpyAsync( s.h_bid, s.d_bid, 8*n, hipMemcpyDeviceToHost, st ) );
+  TX_CHECK( hipMemcpyAsync( s.h_kind, d_in_kind, n, hipMemcpyDeviceToHost, st ) );
+  TX_CHECK( hipMemcpyAsync( s.h_flag, s.d_flag, 4, hipMemcpyDeviceToHost, st ) );
   TX_CHECK( hipEventRecord( s.ev_done, st ) );
   return 0;
 }
@@ -570,7 +701,14 @@ fd_verify_hip_tile_complete( fd_verify_hip_tile_t * t, ulong const * bundle_id, 
   tile_slot & s = t->slot[t->completed & 1];
   TX_CHECK( hipSetDevice( fd_ed25519_hip_ctx_device( t->ctx ) ) );
   TX_CHECK( hipEventSynchronize( s.ev_done ) );
-  s.nsig = *s.h_counter;
+  if( s.frags && *s.h_flag ) {
+    /* during_frag's FD_LOG_ERR (fd_verify_tile.c:75-85): a corrupt frag kills the tile */
+    fprintf( stderr, "fd_verify_hip: corrupt frag in batch (size beyond FD_TPU_RAW_MTU / 2048 or payload_sz "
+                     "beyond FD_TPU_MTU)\n" );
+    abort();
+  }
+  if( s.frags ) bundle_id = s.h_bid;                         /* read from the fd_txn_m_t headers on the GPU */
+  s.nsig = s.n ? *s.h_counter : 0u;
   float gpu_ms = 0.f;
   TX_CHECK( hipEventElapsedTime( &gpu_ms, s.ev_start, s.ev_done ) );
   auto h0 = std::chrono::steady_clock::now();
@@ -583,6 +721,10 @@ fd_verify_hip_tile_complete( fd_verify_hip_tile_t * t, ulong const * bundle_id, 
   const ulong PF = 8;
   for( ulong j = 0; j < n && j < PF; j++ ) __builtin_prefetch( map + (s.h_tag[j] & mask) );
   for( ulong j = 0; j < n; j++ ) {
+    if( s.frags ) {                                          /* after_frag's first statement (:112) */
+      u32 k = s.h_kind[j];
+      t->m_gossip += (k == FD_VERIFY_HIP_IN_GOSSIP) | (k == FD_VERIFY_HIP_IN_SEND);
+    }
     if( j + PF < n ) {
       __builtin_prefetch( map + (s.h_tag[j + PF] & mask) );
       ulong o = *t->oldest + PF; if( o >= depth ) o -= depth;
@@ -625,9 +767,20 @@ fd_verify_hip_tile_complete( fd_verify_hip_tile_t * t, ulong const * bundle_id, 
   return 0;
 }
 
-extern "C" void fd_verify_hip_tile_metrics( fd_verify_hip_tile_t const * t, ulong out[6] ) {
+extern "C" void fd_verify_hip_tile_metrics( fd_verify_hip_tile_t const * t, ulong out[7] ) {
   out[0] = t->m_parse; out[1] = t->m_verify; out[2] = t->m_dedup; out[3] = t->m_bundle;
-  out[4] = t->m_pub; out[5] = t->m_sigs;
+  out[4] = t->m_pub; out[5] = t->m_sigs; out[6] = t->m_gossip;
+}
+
+/* before_frag (fd_verify_tile.c:37-58): 1 = skip the frag */
+extern "C" int fd_verify_hip_before_frag( uint in_kind, ulong seq, ulong sig, ulong round_robin_cnt,
+                                          ulong round_robin_idx ) {
+  int is_bundle_packet = in_kind == FD_VERIFY_HIP_IN_BUNDLE && !sig;
+  if( is_bundle_packet || in_kind == FD_VERIFY_HIP_IN_QUIC ) return (seq % round_robin_cnt) != round_robin_idx;
+  if( in_kind == FD_VERIFY_HIP_IN_BUNDLE ) return round_robin_idx != 0ul;
+  if( in_kind == FD_VERIFY_HIP_IN_GOSSIP )
+    return (seq % round_robin_cnt) != round_robin_idx || sig != FD_VERIFY_HIP_GOSSIP_UPDATE_TAG_VOTE;
+  return 0;
 }
 
 extern "C" void fd_verify_hip_tile_last_timing( fd_verify_hip_tile_t const * t, double out[3] ) {

@@ -206,3 +206,31 @@ def gpu_signer(verifier):
         return d_pub.cpu().numpy(), d_sig.cpu().numpy()
 
     return sign
+
+
+TXNM_SZ = 80            # sizeof(fd_txn_m_t) (include/fd_verify_hip.h, src/disco/fd_txn_m.h:15-61)
+PARSED_CHUNKS = 34      # FD_TPU_PARSED_MTU (2168 B) in 64-B dcache chunks
+
+
+def txnm_dcache(pool, off, sz, bundle_id=None, seed=1):
+    """Lay frags out as the verify tile's in-link dcache does: each frag an
+    fd_txn_m_t (80-byte header: payload_sz at 8, block_engine.bundle_id at 24,
+    reference_slot / source fields filled with seeded bytes) followed by its
+    payload, at the next free 64-byte chunk (fd_dcache_compact_next).
+    Returns (region uint8, chunk uint32[n], frag_sz uint16[n])."""
+    n = off.size
+    fsz = TXNM_SZ + sz.astype(np.int64)
+    nchunk = (fsz + 63) // 64
+    chunk = np.concatenate([[0], np.cumsum(nchunk)[:-1]]).astype(np.int64)
+    region = np.zeros(int(64 * (chunk[-1] + nchunk[-1])) + 64 if n else 64, np.uint8)
+    hdr = np.random.default_rng(seed).integers(0, 256, (n, TXNM_SZ), dtype=np.uint8)
+    hdr[:, 8:10] = sz.astype(np.uint16).view(np.uint8).reshape(n, 2)
+    hdr[:, 10:12] = 0
+    hdr[:, 24:32] = (np.zeros(n, np.uint64) if bundle_id is None else
+                     np.asarray(bundle_id, np.uint64)).view(np.uint8).reshape(n, 8)
+    base = 64 * chunk
+    region[base[:, None] + np.arange(TXNM_SZ)] = hdr
+    for j in range(n):
+        b = int(base[j]) + TXNM_SZ
+        region[b:b + int(sz[j])] = pool[int(off[j]):int(off[j]) + int(sz[j])]
+    return region, chunk.astype(np.uint32), fsz.astype(np.uint16)

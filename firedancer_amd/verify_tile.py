@@ -36,8 +36,15 @@ EXPORTS = (
     "fd_verify_hip_tcache_reset", "fd_verify_hip_tcache_query", "fd_verify_hip_tcache_insert",
     "fd_verify_hip_tile_new", "fd_verify_hip_tile_join_tcache", "fd_verify_hip_tile_tcache_reset",
     "fd_verify_hip_tile_delete", "fd_verify_hip_tile_set_seed", "fd_verify_hip_tile_submit", "fd_verify_hip_tile_complete",
-    "fd_verify_hip_tile_metrics", "fd_verify_hip_tile_last_timing",
+    "fd_verify_hip_tile_metrics", "fd_verify_hip_tile_last_timing", "fd_verify_hip_tile_submit_frags",
+    "fd_verify_hip_before_frag",
 )
+
+# fd_txn_m_t / gossip vote layouts (include/fd_verify_hip.h)
+TXNM_SZ, TXNM_PAYLOAD_SZ_OFF, TXNM_TXN_T_SZ_OFF, TXNM_SRC_IPV4_OFF, TXNM_SRC_TPU_OFF, TXNM_BUNDLE_ID_OFF = 80, 8, 10, 12, 16, 24
+TPU_RAW_MTU, TPU_SOURCE_GOSSIP = 1312, 3
+GOSSIP_UPDATE_TAG_VOTE, GOSSIP_VOTE_ADDR_OFF, GOSSIP_VOTE_TXN_SZ_OFF, GOSSIP_VOTE_TXN_OFF = 3, 56, 72, 80
+IN_QUIC, IN_BUNDLE, IN_GOSSIP, IN_SEND = 0, 1, 2, 3
 
 _bound = False
 
@@ -72,6 +79,10 @@ def lib():
         L.fd_verify_hip_tile_complete.argtypes = [vp, vp, vp, vp, vp]
         L.fd_verify_hip_tile_metrics.argtypes = [vp, vp]
         L.fd_verify_hip_tile_last_timing.argtypes = [vp, vp]
+        L.fd_verify_hip_tile_submit_frags.restype = c.c_int
+        L.fd_verify_hip_tile_submit_frags.argtypes = [vp, u64, vp, vp, vp, vp, vp, vp]
+        L.fd_verify_hip_before_frag.restype = c.c_int
+        L.fd_verify_hip_before_frag.argtypes = [c.c_uint, u64, u64, u64, u64]
         _bound = True
     return L
 
@@ -115,6 +126,12 @@ def parse_dev(verifier, n, pool, txn_off, txn_sz, txn_out, txn_t_sz, stream=None
         return lib().fd_txn_hip_parse_dev(*args, h)
 
 
+def before_frag(in_kind, seq, sig, round_robin_cnt, round_robin_idx):
+    """fd_verify_tile.c:37-58: True if this tile skips the frag."""
+    return bool(lib().fd_verify_hip_before_frag(int(in_kind), int(seq), int(sig) & (2**64 - 1),
+                                                int(round_robin_cnt), int(round_robin_idx)))
+
+
 class VerifyTile:
     """One verify tile on one GPU: fd_verify_ctx_t's tcache, hashmap_seed,
     bundle state and metrics, with frags processed in device-resident batches."""
@@ -153,6 +170,19 @@ class VerifyTile:
             raise RuntimeError(f"fd_verify_hip_tile_submit: {rc}")
         self._pending.append((int(n), (pool, txn_off, txn_sz, txn_out)))   # keep buffers alive
 
+    def submit_frags(self, n, d_in, in_chunk, in_sz, in_kind, d_out, out_chunk):
+        """fd_txn_m_t frag batch (fd_verify_hip_tile_submit_frags): device tensors
+        d_in / d_out uint8 dcache regions, in_chunk / out_chunk int32 (u32 64-B
+        chunk indices), in_sz int16 (u16 frag sizes), in_kind uint8 (IN_*)."""
+        n, dev = int(n), self.verifier.device
+        rc = self._lib.fd_verify_hip_tile_submit_frags(
+            self.tile, n, _ptr(d_in, 1, "d_in", dev), _ptr(in_chunk, 4 * n, "in_chunk", dev),
+            _ptr(in_sz, 2 * n, "in_sz", dev), _ptr(in_kind, n, "in_kind", dev), _ptr(d_out, 1, "d_out", dev),
+            _ptr(out_chunk, 4 * n, "out_chunk", dev))
+        if rc:
+            raise RuntimeError(f"fd_verify_hip_tile_submit_frags: {rc}")
+        self._pending.append((n, (d_in, in_chunk, in_sz, in_kind, d_out, out_chunk)))
+
     def complete(self, bundle_id=None):
         n, _keep = self._pending.pop(0)
         result = np.zeros(n, np.int8)
@@ -173,9 +203,10 @@ class VerifyTile:
         return self.complete(bundle_id)
 
     def metrics(self):
-        out = np.zeros(6, np.uint64)
+        out = np.zeros(7, np.uint64)
         self._lib.fd_verify_hip_tile_metrics(self.tile, out.ctypes.data)
-        keys = ("parse_fail_cnt", "verify_fail_cnt", "dedup_fail_cnt", "bundle_peer_fail_cnt", "published", "sigs")
+        keys = ("parse_fail_cnt", "verify_fail_cnt", "dedup_fail_cnt", "bundle_peer_fail_cnt", "published", "sigs",
+                "gossiped_votes_cnt")
         return dict(zip(keys, (int(x) for x in out)))
 
     def last_timing(self):

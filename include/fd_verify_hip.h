@@ -62,6 +62,41 @@ typedef unsigned short ushort;
 #define FD_VERIFY_HIP_FRAG_PARSE_FAIL   (-3)   /* metrics.parse_fail_cnt       */
 #define FD_VERIFY_HIP_FRAG_BUNDLE_PEER  (-4)   /* metrics.bundle_peer_fail_cnt */
 
+/* ---- verify-tile frag formats (x86-64 layouts of the reference structs;
+   tests/test_ref_layout.py checks every offset against the reference headers
+   with offsetof) -------------------------------------------------------- */
+
+/* fd_txn_m_t (src/disco/fd_txn_m.h:15-61): 80-byte header, then payload[],
+   then the fd_txn_t at fd_txn_m_txn_t (:101-104) */
+#define FD_VERIFY_HIP_TXNM_SZ               80u   /* sizeof(fd_txn_m_t)              */
+#define FD_VERIFY_HIP_TXNM_PAYLOAD_SZ_OFF    8u   /* ushort payload_sz               */
+#define FD_VERIFY_HIP_TXNM_TXN_T_SZ_OFF     10u   /* ushort txn_t_sz                 */
+#define FD_VERIFY_HIP_TXNM_SRC_IPV4_OFF     12u   /* uint   source_ipv4              */
+#define FD_VERIFY_HIP_TXNM_SRC_TPU_OFF      16u   /* uchar  source_tpu               */
+#define FD_VERIFY_HIP_TXNM_BUNDLE_ID_OFF    24u   /* ulong  block_engine.bundle_id   */
+#define FD_VERIFY_HIP_TXN_ALIGN              2u   /* alignof(fd_txn_t)               */
+#define FD_VERIFY_HIP_TPU_RAW_MTU         1312u   /* FD_TPU_RAW_MTU (fd_txn_m.h:139) */
+#define FD_VERIFY_HIP_TPU_SOURCE_GOSSIP      3u   /* FD_TXN_M_TPU_SOURCE_GOSSIP      */
+
+/* fd_gossip_update_message_t carrying a vote (src/flamenco/gossip/
+   fd_gossip_types.h:136-141,191-212) */
+#define FD_VERIFY_HIP_GOSSIP_UPDATE_TAG_VOTE  3u  /* FD_GOSSIP_UPDATE_TAG_VOTE       */
+#define FD_VERIFY_HIP_GOSSIP_VOTE_ADDR_OFF   56u  /* vote.socket.addr (uint)         */
+#define FD_VERIFY_HIP_GOSSIP_VOTE_TXN_SZ_OFF 72u  /* vote.txn_sz (ulong)             */
+#define FD_VERIFY_HIP_GOSSIP_VOTE_TXN_OFF    80u  /* vote.txn[1232]                  */
+
+/* in-link kinds (fd_verify_tile.c:7-10) */
+#define FD_VERIFY_HIP_IN_QUIC   0u
+#define FD_VERIFY_HIP_IN_BUNDLE 1u
+#define FD_VERIFY_HIP_IN_GOSSIP 2u
+#define FD_VERIFY_HIP_IN_SEND   3u
+
+/* before_frag (fd_verify_tile.c:37-58) on the host: 1 = this tile skips
+   the frag (round robin over verify tiles by seq; bundles to tile 0;
+   gossip frags other than votes), 0 = it takes it. */
+int
+fd_verify_hip_before_frag( uint in_kind, ulong seq, ulong sig, ulong round_robin_cnt, ulong round_robin_idx );
+
 /* ---- GPU txn parse ------------------------------------------------------
 
    Parses n payloads: payload j = d_pool[ d_txn_off[j], +d_txn_sz[j] ).
@@ -151,6 +186,31 @@ fd_verify_hip_tile_submit( fd_verify_hip_tile_t * tile,
                            ushort const *         d_txn_sz,
                            uchar *                d_txn_out );   /* NULL or n*FD_TXN_HIP_MAX_SZ */
 
+/* The verify tile's own frag format: n frags (those before_frag kept, in
+   arrival order) in the in-link dcache, frag j's sz bytes at
+   d_in + 64*d_in_chunk[j] (fd_chunk_to_laddr), kind d_in_kind[j]
+   (FD_VERIFY_HIP_IN_*).  Per frag the GPU does during_frag
+   (fd_verify_tile.c:64-99) into the out dcache at d_out + 64*d_out_chunk[j]
+   -- the copy of a QUIC/BUNDLE/SEND fd_txn_m_t frag, or the conversion of a
+   gossip vote message into one -- then after_frag's parse (:118-120): the
+   fd_txn_t at fd_txn_m_txn_t and txn_t_sz into the header.  bundle_id comes
+   from each header (complete's bundle_id argument is ignored for such a
+   batch) and GOSSIP/SEND frags count into gossiped_votes_cnt (:112).
+   A corrupt frag (sz > FD_TPU_RAW_MTU, or > 2048 for gossip; payload_sz >
+   FD_TPU_MTU) aborts the process in complete(), as the reference's
+   FD_LOG_ERR ends the tile.  All pointers are device-visible (HBM, or
+   pinned host memory mapped to the device); chunks are 64-byte units, so
+   an out chunk must hold FD_TPU_PARSED_MTU bytes. */
+int
+fd_verify_hip_tile_submit_frags( fd_verify_hip_tile_t * tile,
+                                 ulong                  n,
+                                 uchar const *          d_in,
+                                 uint const *           d_in_chunk,
+                                 ushort const *         d_in_sz,
+                                 uchar const *          d_in_kind,
+                                 uchar *                d_out,
+                                 uint const *           d_out_chunk );
+
 int
 fd_verify_hip_tile_complete( fd_verify_hip_tile_t * tile,
                              ulong const *          bundle_id,   /* host, n entries or NULL */
@@ -160,8 +220,9 @@ fd_verify_hip_tile_complete( fd_verify_hip_tile_t * tile,
 
 /* metrics (cumulative): out[0..3] = parse_fail, verify_fail, dedup_fail,
    bundle_peer_fail (fd_verify_tile.h:51-57); out[4] = published,
-   out[5] = signatures sent to the GPU verify */
-void fd_verify_hip_tile_metrics( fd_verify_hip_tile_t const * tile, ulong out[ 6 ] );
+   out[5] = signatures sent to the GPU verify, out[6] = gossiped_votes
+   (GOSSIP/SEND frags, fd_verify_tile.c:33,112) */
+void fd_verify_hip_tile_metrics( fd_verify_hip_tile_t const * tile, ulong out[ 7 ] );
 
 /* timing of the last completed batch (ms): out[0] = GPU (first kernel to
    results on host, HIP events), out[1] = host ordered pass, out[2] =
