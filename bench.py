@@ -186,15 +186,22 @@ def main():
                          "C2 mix 2^20/GPU; c3 one 32-B message x 2^22 keys/GPU as batch_single_msg "
                          "groups of 16; c4 synthetic txn stream through the verify tile (GPU parse + verify + "
                          "host tcache dedup); c5 2^26 C2-mix signatures in total, sharded (strong scaling)")
-    ap.add_argument("--txns", type=int, default=1 << 19, help="c4: frags per batch per GPU")
+    ap.add_argument("--txns", type=int, default=1 << 20,
+                    help="c4: frags per step per GPU (2^20: 102-106M verifies/s; 2^19 under-fills the DSM launches, "
+                         "84-99M -- profiles/r02c_c4_sweep)")
     ap.add_argument("--halfsize", type=int, default=1, choices=[0, 1],
                     help="0: full-length scalars (k, 1) in k_verify_dsm, an A/B switch (same verdicts)")
     ap.add_argument("--contexts", type=int, default=2,
                     help="c1/c2/c3/c5: verify contexts (streams) each step is split over (measured with the "
                          "persistent DSM: 1 -> 118.2M, 2 -> 125.0-125.7M, 4 -> 124.5M verifies/s)")
-    ap.add_argument("--tiles", type=int, default=8, help="c4: verify tiles (host threads + contexts) per GPU")
+    ap.add_argument("--tiles", type=int, default=2,
+                    help="c4: verify tiles (host threads + contexts) per GPU; more tiles than the 4 hardware queues "
+                         "per process share queues (16 tiles: -18%%)")
     ap.add_argument("--c4-ingest", default="frags", choices=["frags", "payload"],
                     help="c4: fd_txn_m_t frags in each tile's in-link dcache (default) or raw payloads + offsets")
+    ap.add_argument("--c4-pcie", default="dma", choices=["zerocopy", "dma"],
+                    help="c4 PCIe-inclusive leg: the GPU reads each in-link dcache in place from pinned mapped host "
+                         "memory (zerocopy), or it is copied host->HBM by DMA each step (dma)")
     ap.add_argument("--sigs", type=int, default=None, help="override signatures per GPU per step")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--cpu-seconds", type=float, default=8.0)
@@ -480,6 +487,7 @@ def run_c4(args, rank, world, local, dist):
 
     import torch
     from firedancer_amd import Verifier
+    from firedancer_amd.ed25519 import HostBuffer
     from firedancer_amd.txn_workload import PARSED_CHUNKS, gpu_signer, make_txn_stream, txnm_dcache
     from firedancer_amd.verify_tile import IN_QUIC, VerifyTile
     T = max(1, args.tiles)
@@ -497,12 +505,15 @@ def run_c4(args, rank, world, local, dist):
         sel = np.arange(t, s.n, T)
         if frags_mode:
             region, chunk, fsz = txnm_dcache(s.pool, s.off[sel], s.sz[sel], seed=t + 1)
-            h_in = torch.from_numpy(region).pin_memory()
+            hb = HostBuffer(region.size)                     # pinned, device-mapped (fd_ed25519_hip_host_alloc)
+            hb.array[:] = region
+            h_in = torch.from_numpy(hb.array)
             d_in = [to_dev(region), torch.empty_like(h_in, device=dev)]
             d_out = torch.empty(64 * PARSED_CHUNKS * max(int(sel.size), 1), dtype=torch.uint8, device=dev)
             out_chunk = to_dev((np.arange(sel.size) * PARSED_CHUNKS).astype(np.uint32), np.int32)
             kinds = to_dev(np.full(sel.size, IN_QUIC, np.uint8))
-            parts.append(dict(n=int(sel.size), h_in=h_in, d_in=d_in, d_out=d_out, in_chunk=to_dev(chunk, np.int32),
+            parts.append(dict(n=int(sel.size), hb=hb, h_in=h_in, d_in=d_in, d_out=d_out,
+                              in_chunk=to_dev(chunk, np.int32),
                               in_sz=to_dev(fsz, np.int16), kinds=kinds, out_chunk=out_chunk,
                               cs=torch.cuda.Stream(dev), ts=torch.cuda.ExternalStream(vs[t].stream, device=dev),
                               free=[None, None]))
@@ -521,6 +532,10 @@ def run_c4(args, rank, world, local, dist):
             tiles[t].submit(P["n"], d_pool, P["off"], P["sz"])
         elif not h2d[0]:
             tiles[t].submit_frags(P["n"], P["d_in"][0], P["in_chunk"], P["in_sz"], P["kinds"], P["d_out"],
+                                  P["out_chunk"])
+        elif args.c4_pcie == "zerocopy":
+            # the ingest kernel reads the in-link dcache in place over PCIe
+            tiles[t].submit_frags(P["n"], P["hb"].ptr, P["in_chunk"], P["in_sz"], P["kinds"], P["d_out"],
                                   P["out_chunk"])
         else:
             # copy this batch's in-link dcache host -> HBM on the tile's copy
@@ -602,9 +617,12 @@ def run_c4(args, rank, world, local, dist):
         pcie = {"value": round(sigs2 / e2, 1), "unit": "verifies/s", "ms_per_step": round(e2 / args.steps * 1e3, 4),
                 "h2d_bytes_per_step": h2d_bytes * world, "h2d_GBps": round(h2d_bytes * world * args.steps / e2 / 1e9, 2),
                 "results_equal_resident_leg": bool(same),
-                "what": "every tile's in-link dcache (fd_txn_m_t frags) copied host->HBM each step from pinned memory "
-                        "(copy stream per tile, double-buffered, overlapped with the previous batch); per-frag "
-                        "results D2H as in the resident leg; the out dcache stays in HBM"}
+                "mode": args.c4_pcie,
+                "what": ("every tile's in-link dcache (fd_txn_m_t frags) in pinned device-mapped host memory, read in "
+                         "place by the ingest kernel over PCIe each step" if args.c4_pcie == "zerocopy" else
+                         "every tile's in-link dcache (fd_txn_m_t frags) copied host->HBM each step from pinned memory "
+                         "(copy stream per tile, double-buffered, overlapped with the previous batch)") +
+                        "; per-frag results D2H as in the resident leg; the out dcache stays in HBM"}
         h2d[0] = False
     res = np.concatenate([o[-1][0] for o in outs])
     gpu_ms = [x for g in gpu_ms for x in g]; host_ms = [x for h in host_ms for x in h]
@@ -667,6 +685,10 @@ def run_c4(args, rank, world, local, dist):
         tl.close()
     for x in vs:
         x.close()
+    for P in parts:
+        if "hb" in P:
+            P["h_in"] = None
+            P["hb"].close()
     if dist:
         dist.barrier()
         dist.destroy_process_group()

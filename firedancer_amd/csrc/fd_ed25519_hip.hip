@@ -1053,6 +1053,18 @@ fd_ed25519_hip_sign_dev( fd_ed25519_hip_ctx_t * ctx, ulong n, uchar const * d_pr
   return 0;
 }
 
+void *
+fd_ed25519_hip_host_alloc( ulong sz ) {
+  void * p = NULL;
+  FD_CHECK( hipHostMalloc( &p, sz ? sz : 1ul, hipHostMallocMapped | hipHostMallocPortable ) );
+  return p;
+}
+
+void
+fd_ed25519_hip_host_free( void * p ) {
+  if( p ) FD_CHECK( hipHostFree( p ) );
+}
+
 int
 fd_ed25519_hip_sync( fd_ed25519_hip_ctx_t * ctx ) {
   FD_CHECK( hipSetDevice( ctx->device ) );

@@ -33,7 +33,7 @@ EXPORTS = (
     "fd_ed25519_hip_verify_host", "fd_ed25519_hip_group_reduce_dev", "fd_ed25519_hip_sign_dev",
     "fd_ed25519_hip_sync", "fd_ed25519_hip_set_timing", "fd_ed25519_hip_get_timing",
     "fd_ed25519_hip_get_dsm_units", "fd_ed25519_hip_set_halfsize", "fd_ed25519_hip_test_halfsize",
-    "fd_ed25519_hip_test_sha512",
+    "fd_ed25519_hip_test_sha512", "fd_ed25519_hip_host_alloc", "fd_ed25519_hip_host_free",
 )
 
 _lib = None
@@ -70,6 +70,9 @@ def lib():
         L.fd_ed25519_hip_test_halfsize.argtypes = [vp, c.c_ulong, vp, vp, vp]
         L.fd_ed25519_hip_test_sha512.argtypes = [vp, c.c_ulong, vp, vp, vp, vp, vp]
         L.fd_ed25519_hip_ctx_reserve.argtypes = [vp, u64]
+        L.fd_ed25519_hip_host_alloc.restype = vp
+        L.fd_ed25519_hip_host_alloc.argtypes = [u64]
+        L.fd_ed25519_hip_host_free.argtypes = [vp]
         L.fd_ed25519_hip_verify_dev.restype = c.c_int
         L.fd_ed25519_hip_verify_dev.argtypes = [vp, u64, vp, vp, vp, vp, vp, vp, vp, vp]
         L.fd_ed25519_hip_verify_fixed_dev.restype = c.c_int
@@ -90,6 +93,28 @@ def lib():
         L.fd_ed25519_hip_sync.argtypes = [vp]
         _lib = L
     return _lib
+
+
+class HostBuffer:
+    """Pinned, device-mapped host memory (fd_ed25519_hip_host_alloc): .array is
+    a numpy uint8 view for the host, .ptr the address kernels use in place."""
+
+    def __init__(self, nbytes):
+        self.nbytes = int(nbytes)
+        self.ptr = lib().fd_ed25519_hip_host_alloc(self.nbytes)
+        self.array = np.ctypeslib.as_array((ctypes.c_uint8 * max(self.nbytes, 1)).from_address(self.ptr))
+
+    def close(self):
+        if self.ptr:
+            self.array = None
+            lib().fd_ed25519_hip_host_free(self.ptr)
+            self.ptr = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 def fd_ed25519_verify(msg, sig, public_key, sha=None):

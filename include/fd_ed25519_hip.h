@@ -228,6 +228,13 @@ fd_ed25519_hip_sign_dev( fd_ed25519_hip_ctx_t * ctx,
                          uchar *                d_sigs,
                          void *                 stream );
 
+/* Pinned host memory mapped into every device's address space (hipHostMalloc
+   mapped|portable): kernels read and write it in place over PCIe at the same
+   address, so a verify tile's in-link dcache placed here is ingested by the
+   GPU with no copy (fd_verify_hip_tile_submit_frags).  Aborts on failure. */
+void * fd_ed25519_hip_host_alloc( ulong sz );
+void   fd_ed25519_hip_host_free ( void * p );
+
 /* Blocks until all work queued on the context's stream is done. */
 int fd_ed25519_hip_sync( fd_ed25519_hip_ctx_t * ctx );
 

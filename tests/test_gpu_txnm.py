@@ -181,3 +181,26 @@ def test_corrupt_frag_aborts_like_fd_log_err():
                        timeout=120)
     assert r.returncode == -6, (r.returncode, r.stdout[-500:], r.stderr[-2000:])
     assert "corrupt frag" in r.stderr and "returned" not in r.stdout
+
+
+def test_zero_copy_ingest_from_mapped_host_memory(verifier):
+    """The in-link dcache left in pinned device-mapped host memory
+    (fd_ed25519_hip_host_alloc): the ingest kernel reads it in place over PCIe;
+    results and out frags equal the HBM-resident run's."""
+    import torch
+    from firedancer_amd.ed25519 import HostBuffer
+    c4 = dict(np.load(os.path.join(HERE, "golden", "c4_stream_2048.npz")))
+    n = c4["off"].size
+    region, in_chunk, in_sz, kinds, frags = build_in_dcache(c4["pool"], c4["off"], c4["sz"], c4["bundle_id"])
+    hb = HostBuffer(region.size)
+    hb.array[:] = region
+    out_chunk = (np.arange(n) * PARSED_CHUNKS).astype(np.uint32)
+    tile = V.VerifyTile(verifier, max_txn=n, hashmap_seed=int(c4["seed"]), tcache_depth=int(c4["depth"]))
+    d_out = torch.zeros(64 * (int(out_chunk.max()) + PARSED_CHUNKS), dtype=torch.uint8, device="cuda:0")
+    tile.submit_frags(n, hb.ptr, _dev(in_chunk, np.int32), _dev(in_sz, np.int16), _dev(kinds), d_out,
+                      _dev(out_chunk, np.int32))
+    res, tag, tsz = tile.complete(None)
+    tile.close()
+    assert np.array_equal(res, c4["result"]) and np.array_equal(tag, c4["tag"])
+    check_out_frags(d_out.cpu().numpy(), out_chunk, frags, kinds, c4["pool"], c4["off"], c4["sz"], tsz)
+    hb.close()
