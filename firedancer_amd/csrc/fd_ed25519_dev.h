@@ -910,6 +910,110 @@ DEV void sha512_prefixed( u32 x[16], u32 const pre[16], u32 plen, u8 const * msg
   for( int j=0; j<8; j++ ) { x[2*j] = bswap32( (u32)(st[j] >> 32) ); x[2*j+1] = bswap32( (u32)st[j] ); }
 }
 
+/* ---- SHA-512(R||A||M) with LDS-staged, wave-cooperative message blocks ----
+
+   The same hash as sha512_prefixed(pre = R||A, 64), for all 64 lanes of a
+   wave at once (wave-uniform control flow: every lane of the wave calls it;
+   a lane with nothing to hash passes msz = 0).  For each 128-byte block b
+   (up to the wave's largest block count):
+     1. each lane publishes its record's message window for the block -- the
+        16-B-aligned base of message bytes [max(0,128b-64), min(msz,128b+64))
+        and the number of 16-B chunks covering it (<= 9) -- in LDS;
+     2. the wave loads all 64 windows cooperatively: piece p = lane + 64*i
+        (i < 9) is chunk p%9 of record p/9, so lanes 9r..9r+8 read record r's
+        window as contiguous 16-B loads (coalesced: one record's 144 B per 9
+        lanes instead of 64 lanes each walking its own message with dword
+        loads); chunks past a window are stored as zeros;
+     3. each lane fixes its own window in LDS where the message ends (bytes
+        past msz zero, the 0x80 pad byte at msz: fd_sha512.c:365-385);
+     4. each lane reads its window back at its byte offset, forms the block's
+        big-endian words and runs the compression in registers.
+   buf: this wave's 64 x 36 words of LDS; meta: its 64 u64.  The pool must be
+   readable up to the 16-B boundary after each message's last byte. */
+DEV void wave_lds_sync( void ) {
+  __builtin_amdgcn_fence( __ATOMIC_SEQ_CST, "wavefront" );
+  __builtin_amdgcn_wave_barrier();
+}
+
+DEV u32 wave_max_u32( u32 v ) {                 /* v < 2^7, over all lanes of the wave */
+  u32 m = 0u;
+  #pragma unroll
+  for( int b=6; b>=0; b-- ) { u32 c = m | (1u << b); if( __ballot( v >= c ) ) m = c; }
+  return m;
+}
+
+template<u32 PLEN>   /* prefix bytes: 64 (R||A, the verify path) or 0 (plain SHA-512, the test hook) */
+DEV void sha512_prefixed_coop( u32 x[16], u32 const pre[16], u8 const * msg, u32 msz, u32 * buf, u64 * meta,
+                               u32 lane ) {
+  u64 st[8] = { 0x6a09e667f3bcc908ULL,0xbb67ae8584caa73bULL,0x3c6ef372fe94f82bULL,0xa54ff53a5f1d36f1ULL,
+                0x510e527fade682d1ULL,0x9b05688c2b3e6c1fULL,0x1f83d9abfb41bd6bULL,0x5be0cd19137e2179ULL };
+  u32 nb = (PLEN + msz + 17u + 127u) >> 7;
+  u32 nbmax = wave_max_u32( nb );
+  u64 bitlen = (u64)(PLEN + msz) << 3;
+  u32 * own = buf + 36u*lane;
+  #pragma unroll 1
+  for( u32 b=0; b<nbmax; b++ ) {
+    u32 m0 = b ? 128u*b - PLEN : 0u;                      /* message offset of the window */
+    u32 wlen = b ? 128u : 128u - PLEN;                    /* message bytes the block holds */
+    bool act = b < nb;
+    u32 hi = min( msz, m0 + wlen );
+    u32 nbytes = (act && hi > m0) ? hi - m0 : 0u;
+    uintptr_t addr = (uintptr_t)(msg + m0);
+    u32 o = (u32)(addr & 15u);
+    u32 nch = nbytes ? (o + nbytes + 15u) >> 4 : 0u;
+    meta[lane] = ((u64)(addr >> 4) & 0xfffffffffffULL) | ((u64)nch << 44);
+    wave_lds_sync();
+    #pragma unroll
+    for( u32 i=0; i<9u; i++ ) {                            /* 576 pieces = 64 records x 9 chunks */
+      u32 pc = lane + 64u*i, r = pc / 9u, c = pc - 9u*r;
+      u64 mr = meta[r];
+      uint4 v = make_uint4( 0u, 0u, 0u, 0u );
+      if( c < (u32)(mr >> 44) ) v = ((uint4 const *)(uintptr_t)((mr & 0xfffffffffffULL) << 4))[c];
+      ((uint4 *)(buf + 36u*r))[c] = v;
+    }
+    wave_lds_sync();
+    int P = (int)msz - (int)m0;                           /* pad position in the window */
+    if( act && P >= 0 && P < (int)wlen ) {
+      u32 e = o + (u32)P, q = e >> 4;
+      uint4 * cp = (uint4 *)own + q;
+      uint4 v = *cp;
+      u32 w[4] = { v.x, v.y, v.z, v.w };
+      #pragma unroll
+      for( u32 k=0; k<4u; k++ ) {
+        int rel = (int)(e - 16u*q) - (int)(4u*k);        /* bytes of word k before the pad */
+        u32 keep = rel >= 4 ? ~0u : rel <= 0 ? 0u : (1u << (8*rel)) - 1u;
+        u32 pad = (rel >= 0 && rel < 4) ? 0x80u << (8*rel) : 0u;
+        w[k] = (w[k] & keep) | pad;
+      }
+      *cp = make_uint4( w[0], w[1], w[2], w[3] );
+    }
+    wave_lds_sync();
+    u32 mw[33];
+    u32 const * rp = own + (o >> 2);
+    #pragma unroll
+    for( int k=0; k<33; k++ ) mw[k] = rp[k];
+    u32 sh = (o & 3u) * 8u;
+    u32 mm[32];                                           /* message bytes [m0 + 4k, +4) */
+    #pragma unroll
+    for( int k=0; k<32; k++ ) mm[k] = __builtin_amdgcn_alignbit( mw[k+1], mw[k], sh );
+    u64 W[16];
+    if( PLEN && b == 0u ) {                               /* wave-uniform branch */
+      #pragma unroll
+      for( int t=0; t<8; t++ ) W[t] = be64_of_le_words( pre[2*t], pre[2*t+1] );
+      #pragma unroll
+      for( int t=8; t<16; t++ ) W[t] = be64_of_le_words( mm[2*t-16], mm[2*t-15] );
+    } else {
+      #pragma unroll
+      for( int t=0; t<16; t++ ) W[t] = be64_of_le_words( mm[2*t], mm[2*t+1] );
+    }
+    if( b + 1u == nb ) { W[14] = 0ul; W[15] = bitlen; }
+    if( act ) sha512_block( st, W );
+    wave_lds_sync();                                      /* the next block reuses the buffers */
+  }
+  #pragma unroll
+  for( int j=0; j<8; j++ ) { x[2*j] = bswap32( (u32)(st[j] >> 32) ); x[2*j+1] = bswap32( (u32)st[j] ); }
+}
+
 /* k = SHA512( R || A || M ) mod L as 8 LE limbs (fd_ed25519_user.c:205-207). */
 DEV void hram_mod_l( u32 kout[8], u32 const R[8], u32 const A[8], u8 const * msg, u32 msz ) {
   u32 pre[16], x[16];

@@ -272,12 +272,21 @@ void k_msg_order( ulong n, uint const * __restrict__ msz, u32 * __restrict__ cou
 #define PREP_OCCUPANCY
 #endif
 
+/* FD_PREP_LDS_MSG: SHA-512(R||A||M) with wave-cooperative, LDS-staged
+   message blocks (sha512_prefixed_coop) instead of each lane loading its own
+   message with dword loads (sha512_prefixed). */
+#ifndef FD_PREP_LDS_MSG
+#define FD_PREP_LDS_MSG 1
+#endif
+#define PREP_MSG_WORDS (64*36)           /* per wave: 64 windows of 144 B */
+
 /* one record slot t of the chunk (n records): checks, decodes, hash, and the
    wave's survivor compaction (all 64 lanes of the wave take part) */
 DEV void prep_slot( ulong t, ulong n, ulong chunk, uchar const * __restrict__ sigs, uchar const * __restrict__ pubs,
                     uchar const * __restrict__ pool, uint const * __restrict__ moff, uint const * __restrict__ msz,
                     u32 fixed_sz, u32 * __restrict__ st, int errmode, u32 * __restrict__ idx,
-                    u32 * __restrict__ count, signed char * __restrict__ codes, u32 const * __restrict__ order ) {
+                    u32 * __restrict__ count, signed char * __restrict__ codes, u32 const * __restrict__ order,
+                    u32 * lds_msg, u64 * lds_meta ) {
   bool active = t < n;
   /* order (k_msg_order): lane t takes record order[t], so a wave's lanes
      hash messages of the same SHA-512 block count */
@@ -311,6 +320,7 @@ DEV void prep_slot( ulong t, ulong n, ulong chunk, uchar const * __restrict__ si
       for( int q=0; q<8; q++ ) { s[(base+q)*chunk] = xw[q]; s[(base+8+q)*chunk] = yw[q]; }
     }
   }
+#if !FD_PREP_LDS_MSG
   /* reload the record for the hash rather than holding it across the decode
      (the opaque pointer keeps the compiler from reusing the first load) */
   uchar const * sp = sigs + 64*i, * pp = pubs + 32*i;
@@ -327,7 +337,38 @@ DEV void prep_slot( ulong t, ulong n, ulong chunk, uchar const * __restrict__ si
     s[(ST_K +w)*chunk] = k[w];
     s[(ST_S +w)*chunk] = sig[8+w];
   }
+#endif
   }
+#if FD_PREP_LDS_MSG
+  {
+    /* the whole wave hashes together (inactive lanes with an empty message) */
+    u32 pre[16], x[16], k[8], sv[8];
+    uchar const * sp = sigs + 64*i, * pp = pubs + 32*i;
+    asm volatile( "" : "+v"(sp), "+v"(pp) );
+    u32 mo = 0u, ms = 0u;
+    #pragma unroll
+    for( int q=0; q<16; q++ ) pre[q] = 0u;
+    #pragma unroll
+    for( int q=0; q<8; q++ ) sv[q] = 0u;
+    if( active ) {
+      load_words( pre, sp, 8 );                                            /* R */
+      load_words( pre + 8, pp, 8 );                                        /* A */
+      load_words( sv, sp + 32, 8 );                                        /* S */
+      mo = moff ? moff[i] : (u32)i * fixed_sz;
+      ms = msz  ? msz[i]  : fixed_sz;
+    }
+    sha512_prefixed_coop<64u>( x, pre, pool + mo, ms, lds_msg, lds_meta, threadIdx.x & 63u );   /* user.c:205-206 */
+    if( active ) {
+      sc_reduce512( k, x );                                                /* user.c:207 */
+      u32 * s = st + i;
+      #pragma unroll
+      for( int w=0; w<8; w++ ) {
+        s[(ST_K +w)*chunk] = k[w];
+        s[(ST_S +w)*chunk] = sv[w];
+      }
+    }
+  }
+#endif
   /* Survivor compaction: a signature that fails a pre-check gets its final
      code here; the others are appended (wave-aggregated atomic, spread over
      the whole prep launch) to idx[] so that k_verify_dsm spends no lanes on
@@ -360,6 +401,14 @@ void k_verify_prep( ulong n, ulong chunk, uchar const * __restrict__ sigs, uchar
                     ulong rec0, u32 const * __restrict__ order ) {
   n = dev_count_n( n, d_n, rec0 );            /* device-side count: this chunk starts at record rec0 */
   if( (ulong)blockIdx.x * blockDim.x >= n ) return;
+#if FD_PREP_LDS_MSG
+  __shared__ __attribute__((aligned(16))) u32 lds_msg_all[4*PREP_MSG_WORDS];
+  __shared__ u64 lds_meta_all[4*64];
+  u32 * lds_msg = lds_msg_all + PREP_MSG_WORDS*(threadIdx.x >> 6);
+  u64 * lds_meta = lds_meta_all + 64*(threadIdx.x >> 6);
+#else
+  u32 * lds_msg = 0; u64 * lds_meta = 0;
+#endif
 #if FD_PREP_PERSIST
   for( ;; ) {
     u32 task = 0u;
@@ -367,11 +416,11 @@ void k_verify_prep( ulong n, ulong chunk, uchar const * __restrict__ sigs, uchar
     task = __shfl( task, 0 );
     if( (ulong)task * 64ul >= n ) break;                              /* wave-uniform exit */
     prep_slot( (ulong)task * 64ul + (threadIdx.x & 63u), n, chunk, sigs, pubs, pool, moff, msz, fixed_sz, st,
-               errmode, idx, count, codes, order );
+               errmode, idx, count, codes, order, lds_msg, lds_meta );
   }
 #else
   prep_slot( (ulong)blockIdx.x * blockDim.x + threadIdx.x, n, chunk, sigs, pubs, pool, moff, msz, fixed_sz, st,
-             errmode, idx, count, codes, order );
+             errmode, idx, count, codes, order, lds_msg, lds_meta );
 #endif
 }
 
@@ -908,13 +957,22 @@ fd_ed25519_hip_test_halfsize( fd_ed25519_hip_ctx_t * ctx, ulong n, uint const * 
 
 /* test hook: plain SHA-512 of n messages with the device hash core used by
    k_verify_prep (sha512_prefixed with an empty prefix); out: 64-byte digests */
-__global__ void k_test_sha512( ulong n, uchar const * pool, uint const * moff, uint const * msz, uchar * out ) {
+__global__ __launch_bounds__(64) void k_test_sha512( ulong n, uchar const * pool, uint const * moff,
+                                                      uint const * msz, uchar * out, int coop ) {
+  __shared__ __attribute__((aligned(16))) u32 lds_msg[PREP_MSG_WORDS];
+  __shared__ u64 lds_meta[64];
   ulong i = (ulong)blockIdx.x * blockDim.x + threadIdx.x;
-  if( i >= n ) return;
   u32 pre[16], x[16];
   #pragma unroll
   for( int q=0; q<16; q++ ) pre[q] = 0u;
-  sha512_prefixed( x, pre, 0u, pool + moff[i], msz[i] );
+  if( coop ) {            /* the k_verify_prep path: the whole wave, lanes past n hash nothing */
+    sha512_prefixed_coop<0u>( x, pre, pool + (i < n ? moff[i] : 0u), i < n ? msz[i] : 0u, lds_msg, lds_meta,
+                              threadIdx.x & 63u );
+    if( i >= n ) return;
+  } else {
+    if( i >= n ) return;
+    sha512_prefixed( x, pre, 0u, pool + moff[i], msz[i] );
+  }
   uint4 * o = (uint4 *)(out + 64ul*i);
   #pragma unroll
   for( int q=0; q<4; q++ ) o[q] = make_uint4( x[4*q], x[4*q+1], x[4*q+2], x[4*q+3] );
@@ -926,9 +984,11 @@ fd_ed25519_hip_test_sha512( fd_ed25519_hip_ctx_t * ctx, ulong n, uchar const * d
   hipStream_t s = stream ? (hipStream_t)stream : ctx->stream;
   FD_CHECK( hipSetDevice( ctx->device ) );
   if( !n ) return 0;
-  hipLaunchKernelGGL( k_test_sha512, dim3( (unsigned)((n + 63)/64) ), dim3( 64 ), 0, s, n, d_pool, d_msg_off,
-                      d_msg_sz, d_out );
-  FD_CHECK( hipGetLastError() );
+  for( int coop=0; coop<2; coop++ ) {    /* per-lane path into d_out, cooperative path into d_out + 64*n */
+    hipLaunchKernelGGL( k_test_sha512, dim3( (unsigned)((n + 63)/64) ), dim3( 64 ), 0, s, n, d_pool, d_msg_off,
+                        d_msg_sz, d_out + (coop ? 64ul*n : 0ul), coop );
+    FD_CHECK( hipGetLastError() );
+  }
   return 0;
 }
 

@@ -310,10 +310,11 @@ class Verifier:
             return self._lib.fd_ed25519_hip_test_halfsize(*args, h)
 
     def test_sha512(self, n, pool, msg_off, msg_sz, out, stream=None):
-        """Test hook: device SHA-512 of n messages -> out (64 bytes each)."""
+        """Test hook: device SHA-512 of n messages -> out (128 bytes each: the
+        per-lane path's digests, then the cooperative LDS path's)."""
         n = int(n)
         args = (self.ctx, n, self._p(pool, 1, "pool"), self._p(msg_off, 4 * n, "msg_off"),
-                self._p(msg_sz, 4 * n, "msg_sz"), self._p(out, 64 * n, "out"))
+                self._p(msg_sz, 4 * n, "msg_sz"), self._p(out, 128 * n, "out"))
         with self._stream(stream) as h:
             return self._lib.fd_ed25519_hip_test_sha512(*args, h)
 

@@ -121,9 +121,11 @@ int fd_ed25519_hip_test_halfsize( fd_ed25519_hip_ctx_t * ctx, ulong n, uint cons
                                   void * stream );
 
 /* Test hook: plain SHA-512 (fd_sha512_init/append/fini, fd_sha512.c:264-399)
-   of n messages d_pool[ d_msg_off[i], +d_msg_sz[i] ) with the device hash
-   core k_verify_prep uses; 64-byte digests to d_out + 64*i (16-byte aligned).
-   Asynchronous on stream. */
+   of n messages d_pool[ d_msg_off[i], +d_msg_sz[i] ) with both device hash
+   paths: the per-lane one (sha512_prefixed: signing) writes 64-byte digests
+   to d_out + 64*i, the wave-cooperative LDS-staged one k_verify_prep uses
+   (sha512_prefixed_coop) to d_out + 64*(n+i).  d_out holds 128*n bytes,
+   16-byte aligned.  Asynchronous on stream. */
 int fd_ed25519_hip_test_sha512( fd_ed25519_hip_ctx_t * ctx, ulong n, uchar const * d_pool, uint const * d_msg_off,
                                 uint const * d_msg_sz, uchar * d_out, void * stream );
 

@@ -44,22 +44,25 @@ def test_device_sha512_matches_cavp(verifier, cavp):
     pool = torch.from_numpy(cavp["pool"]).to(dev)
     off = torch.from_numpy(cavp["off"].view(np.int32)).to(dev)
     ln = torch.from_numpy(cavp["len"].view(np.int32)).to(dev)
-    out = torch.zeros((n, 64), dtype=torch.uint8, device=dev)
+    out = torch.zeros((2 * n, 64), dtype=torch.uint8, device=dev)
     verifier.test_sha512(n, pool, off, ln, out)
     got = out.cpu().numpy()
-    bad = np.nonzero((got != cavp["md"]).any(axis=1))[0]
-    assert bad.size == 0, [(int(i), int(cavp["len"][i])) for i in bad[:10]]
+    for path, g in (("per-lane", got[:n]), ("cooperative LDS", got[n:])):
+        bad = np.nonzero((g != cavp["md"]).any(axis=1))[0]
+        assert bad.size == 0, (path, [(int(i), int(cavp["len"][i])) for i in bad[:10]])
 
 
 @pytest.mark.gpu
 def test_device_sha512_unaligned_and_block_edges(verifier):
     """Every length 0..300 (all padding cases: message end at each byte of a
     128-B block, the 0x80 byte and the 16-B length straddling blocks) at all
-    four byte alignments of the pool, against hashlib."""
+    sixteen byte offsets mod 16 (through the 16-B pieces of the cooperative
+    path), against hashlib; the pool is readable
+    only 16 bytes past the last message."""
     import torch
     rng = np.random.default_rng(3)
-    lens = np.repeat(np.arange(301, dtype=np.uint32), 4)
-    align = np.tile(np.arange(4, dtype=np.uint32), 301)
+    lens = np.repeat(np.arange(301, dtype=np.uint32), 16)
+    align = np.tile(np.arange(16, dtype=np.uint32), 301)
     offs, pos = [], 0
     for n, a in zip(lens, align):
         pos = (pos + 15) // 16 * 16 + int(a)
@@ -67,10 +70,13 @@ def test_device_sha512_unaligned_and_block_edges(verifier):
         pos += int(n)
     raw = rng.integers(0, 256, pos + 16, dtype=np.uint8)
     dev = torch.device("cuda", 0)
-    out = torch.zeros((lens.size, 64), dtype=torch.uint8, device=dev)
+    out = torch.zeros((2 * lens.size, 64), dtype=torch.uint8, device=dev)
     verifier.test_sha512(lens.size, torch.from_numpy(raw).to(dev),
                          torch.from_numpy(np.array(offs, np.uint32).view(np.int32)).to(dev),
                          torch.from_numpy(lens.view(np.int32)).to(dev), out)
     got = out.cpu().numpy()
+    m = lens.size
     for i, (o, n) in enumerate(zip(offs, lens)):
-        assert got[i].tobytes() == hashlib.sha512(raw[o:o + n].tobytes()).digest(), (i, n, o % 4)
+        d = hashlib.sha512(raw[o:o + n].tobytes()).digest()
+        assert got[i].tobytes() == d, ("per-lane", i, n, o % 16)
+        assert got[m + i].tobytes() == d, ("cooperative LDS", i, n, o % 16)
