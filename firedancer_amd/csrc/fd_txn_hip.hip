@@ -230,6 +230,11 @@ DEVI u32 txn_parse( u8 const * p, u32 sz, u8 * out, txn_span & sp ) {
   return 20u + 10u*instr_cnt + 8u*lut_cnt;
 }
 
+/* packed per-frag results for the host pass (k_tile_results, below) */
+struct __attribute__((packed)) tile_res { u64 tag; u64 bid; u16 tsz; signed char tcode; u8 kind; u32 pad; };
+static_assert( sizeof(tile_res) == 24, "tile_res layout" );
+#define TILE_RES_HDR 16ul
+
 /* per-frag SoA scratch written by k_txn_parse */
 struct parse_out {
   u16 * tsz;      /* fd_txn_t footprint, 0 = parse failure */
@@ -502,12 +507,11 @@ struct tile_slot {
   /* per signature record, device (grown on demand) */
   ulong         rcap;
   u8 *          d_rsig; u8 * d_rpub; u32 * d_rmoff; u32 * d_rmsz; signed char * d_rcode;
-  /* per frag, pinned host */
-  u16 *         h_tsz; signed char * h_tcode; u64 * h_tag; u32 * h_counter;
+  /* per frag results, packed (k_tile_results): device and pinned host */
+  u8 *          d_res; u8 * h_res;
   /* fd_txn_m_t frag mode (submit_frags): payload spans, fd_txn_t offsets,
      header bundle ids, in kinds and the corrupt-frag flag */
   u32 *         d_pay_off; u16 * d_pay_sz; u32 * d_tout; u64 * d_bid; u32 * d_flag;
-  u64 *         h_bid; u8 * h_kind; u32 * h_flag;
   int           frags;
   hipEvent_t    ev_start, ev_done;
   int           busy;
@@ -536,13 +540,10 @@ static void slot_alloc( tile_slot & s, ulong n ) {
   TX_CHECK( hipMalloc( &s.d_tag, 8*n ) );     TX_CHECK( hipMalloc( &s.d_first, 4*n ) );
   TX_CHECK( hipMalloc( &s.d_cnt, n ) );       TX_CHECK( hipMalloc( &s.d_tcode, n ) );
   TX_CHECK( hipMalloc( &s.d_counter, 4 ) );
-  TX_CHECK( hipHostMalloc( &s.h_tsz, 2*n, 0 ) );  TX_CHECK( hipHostMalloc( &s.h_tcode, n, 0 ) );
-  TX_CHECK( hipHostMalloc( &s.h_tag, 8*n, 0 ) );  TX_CHECK( hipHostMalloc( &s.h_counter, 4, 0 ) );
+  TX_CHECK( hipMalloc( &s.d_res, TILE_RES_HDR + 24*n ) );  TX_CHECK( hipHostMalloc( &s.h_res, TILE_RES_HDR + 24*n, 0 ) );
   TX_CHECK( hipMalloc( &s.d_pay_off, 4*n ) );     TX_CHECK( hipMalloc( &s.d_pay_sz, 2*n ) );
   TX_CHECK( hipMalloc( &s.d_tout, 4*n ) );        TX_CHECK( hipMalloc( &s.d_bid, 8*n ) );
   TX_CHECK( hipMalloc( &s.d_flag, 4 ) );
-  TX_CHECK( hipHostMalloc( &s.h_bid, 8*n, 0 ) );  TX_CHECK( hipHostMalloc( &s.h_kind, n, 0 ) );
-  TX_CHECK( hipHostMalloc( &s.h_flag, 4, 0 ) );
   TX_CHECK( hipEventCreate( &s.ev_start ) ); TX_CHECK( hipEventCreate( &s.ev_done ) );
 }
 
@@ -556,11 +557,9 @@ static void slot_free( tile_slot & s ) {
   (void)hipFree( s.d_tsz ); (void)hipFree( s.d_nsig ); (void)hipFree( s.d_sig_at ); (void)hipFree( s.d_acct_at );
   (void)hipFree( s.d_msg_at ); (void)hipFree( s.d_msg_sz ); (void)hipFree( s.d_tag ); (void)hipFree( s.d_first );
   (void)hipFree( s.d_cnt ); (void)hipFree( s.d_tcode ); (void)hipFree( s.d_counter );
-  (void)hipHostFree( s.h_tsz ); (void)hipHostFree( s.h_tcode ); (void)hipHostFree( s.h_tag );
-  (void)hipHostFree( s.h_counter );
+  (void)hipFree( s.d_res ); (void)hipHostFree( s.h_res );
   (void)hipFree( s.d_pay_off ); (void)hipFree( s.d_pay_sz ); (void)hipFree( s.d_tout ); (void)hipFree( s.d_bid );
   (void)hipFree( s.d_flag );
-  (void)hipHostFree( s.h_bid ); (void)hipHostFree( s.h_kind ); (void)hipHostFree( s.h_flag );
   (void)hipEventDestroy( s.ev_start ); (void)hipEventDestroy( s.ev_done );
   slot_free_records( s );
 }
@@ -601,6 +600,28 @@ extern "C" void fd_verify_hip_tile_delete( fd_verify_hip_tile_t * t ) {
   free( t->own_mem ); free( t );
 }
 
+/* Per-frag results to the host as one packed array and one D2H copy per
+   batch (instead of one hipMemcpyAsync per field array, each a blit kernel
+   on the tile's stream): k_tile_results packs txn_t_sz, per-txn code, tag
+   and, in frag mode, the header bundle id and in kind into 24-byte records
+   behind a 16-byte header (record count, corrupt-frag flag).  Writing the
+   fields into mapped host memory from the kernel instead measured slower
+   (C4 99.7 / 75.1 vs 102-104M verifies/s: small PCIe writes from a kernel
+   that holds CU slots). */
+
+__global__ __launch_bounds__(256)
+void k_tile_results( ulong n, u16 const * __restrict__ tsz, signed char const * __restrict__ tcode,
+                     u64 const * __restrict__ tag, u64 const * __restrict__ bid, u8 const * __restrict__ kind,
+                     u32 const * __restrict__ counter, u32 const * __restrict__ flag, u8 * __restrict__ res ) {
+  ulong j = (ulong)blockIdx.x * blockDim.x + threadIdx.x;
+  if( j == 0ul ) { ((u32 *)res)[0] = *counter; ((u32 *)res)[1] = flag ? *flag : 0u; }
+  if( j >= n ) return;
+  tile_res r;
+  r.tag = tag[j]; r.bid = bid ? bid[j] : 0ul; r.tsz = tsz[j]; r.tcode = tcode[j]; r.kind = kind ? kind[j] : 0u;
+  r.pad = 0u;
+  *(tile_res *)(res + TILE_RES_HDR + 24ul*j) = r;
+}
+
 /* the part of a batch both submit forms share: record capacity, expansion,
    verify, per-txn reduce and the D2H of the per-frag results; the payloads
    are pool[ off[j], +sz[j] ) after k_txn_parse has filled the slot */
@@ -623,15 +644,20 @@ submit_verify( fd_verify_hip_tile_t * t, tile_slot & s, hipStream_t st, ulong n,
   hipLaunchKernelGGL( k_txn_expand, grid, blk, 0, st, n, d_pool, s.d_nsig, s.d_sig_at, s.d_acct_at, s.d_msg_at,
                       s.d_msg_sz, s.d_counter, s.d_first, s.d_cnt, s.d_rsig, s.d_rpub, s.d_rmoff, s.d_rmsz, s.rcap );
   TX_CHECK( hipGetLastError() );
-  TX_CHECK( hipMemcpyAsync( s.h_counter, s.d_counter, 4, hipMemcpyDeviceToHost, st ) );   /* metrics */
   /* the record count stays on the device: no host round trip between the
      expansion and the verify, so submit never waits on the GPU */
   fd_ed25519_hip_verify_dev_count( t->ctx, need, s.d_counter, s.d_rsig, s.d_rpub, d_pool, s.d_rmoff, s.d_rmsz,
                                    s.d_rcode, NULL, st );
   fd_ed25519_hip_group_reduce_dev( t->ctx, n, s.d_first, s.d_cnt, s.d_rcode, s.d_tcode, st );
-  TX_CHECK( hipMemcpyAsync( s.h_tsz, s.d_tsz, 2*n, hipMemcpyDeviceToHost, st ) );
-  TX_CHECK( hipMemcpyAsync( s.h_tcode, s.d_tcode, n, hipMemcpyDeviceToHost, st ) );
-  TX_CHECK( hipMemcpyAsync( s.h_tag, s.d_tag, 8*n, hipMemcpyDeviceToHost, st ) );
+}
+
+static void
+submit_results( tile_slot & s, hipStream_t st, ulong n, uchar const * d_in_kind ) {
+  hipLaunchKernelGGL( k_tile_results, dim3( (unsigned)((n + 255)/256) ), dim3( 256 ), 0, st, n, s.d_tsz, s.d_tcode,
+                      s.d_tag, s.frags ? s.d_bid : (u64 const *)0, (u8 const *)d_in_kind, s.d_counter,
+                      s.frags ? s.d_flag : (u32 const *)0, s.d_res );
+  TX_CHECK( hipGetLastError() );
+  TX_CHECK( hipMemcpyAsync( s.h_res, s.d_res, TILE_RES_HDR + 24ul*n, hipMemcpyDeviceToHost, st ) );
 }
 
 static tile_slot *
@@ -661,6 +687,7 @@ fd_verify_hip_tile_submit( fd_verify_hip_tile_t * t, ulong n, uchar const * d_po
                       (u32 const *)0 );
   TX_CHECK( hipGetLastError() );
   submit_verify( t, s, st, n, d_pool );
+  submit_results( s, st, n, (uchar const *)0 );
   TX_CHECK( hipEventRecord( s.ev_done, st ) );
   return 0;
 }
@@ -674,7 +701,7 @@ fd_verify_hip_tile_submit_frags( fd_verify_hip_tile_t * t, ulong n, uchar const 
   if( !sp ) return rc;
   tile_slot & s = *sp;
   s.frags = 1;
-  if( !n ) { *s.h_flag = 0u; TX_CHECK( hipEventRecord( s.ev_done, st ) ); return 0; }
+  if( !n ) { memset( s.h_res, 0, TILE_RES_HDR ); TX_CHECK( hipEventRecord( s.ev_done, st ) ); return 0; }
   dim3 grid( (unsigned)((n + 255)/256) ), blk( 256 );
   TX_CHECK( hipMemsetAsync( s.d_flag, 0, 4, st ) );
   /* one wave per frag: up to 4 frags per 256-thread workgroup, grid capped */
@@ -687,9 +714,7 @@ fd_verify_hip_tile_submit_frags( fd_verify_hip_tile_t * t, ulong n, uchar const 
                       (u64)t->seed, po, s.d_tout );
   TX_CHECK( hipGetLastError() );
   submit_verify( t, s, st, n, d_out );
-  TX_CHECK( hipMemcpyAsync( s.h_bid, s.d_bid, 8*n, hipMemcpyDeviceToHost, st ) );
-  TX_CHECK( hipMemcpyAsync( s.h_kind, d_in_kind, n, hipMemcpyDeviceToHost, st ) );
-  TX_CHECK( hipMemcpyAsync( s.h_flag, s.d_flag, 4, hipMemcpyDeviceToHost, st ) );
+  submit_results( s, st, n, d_in_kind );
   TX_CHECK( hipEventRecord( s.ev_done, st ) );
   return 0;
 }
@@ -701,14 +726,15 @@ fd_verify_hip_tile_complete( fd_verify_hip_tile_t * t, ulong const * bundle_id, 
   tile_slot & s = t->slot[t->completed & 1];
   TX_CHECK( hipSetDevice( fd_ed25519_hip_ctx_device( t->ctx ) ) );
   TX_CHECK( hipEventSynchronize( s.ev_done ) );
-  if( s.frags && *s.h_flag ) {
+  u32 const * hdr = (u32 const *)s.h_res;
+  tile_res const * R = (tile_res const *)(s.h_res + TILE_RES_HDR);
+  if( s.frags && s.n && hdr[1] ) {
     /* during_frag's FD_LOG_ERR (fd_verify_tile.c:75-85): a corrupt frag kills the tile */
     fprintf( stderr, "fd_verify_hip: corrupt frag in batch (size beyond FD_TPU_RAW_MTU / 2048 or payload_sz "
                      "beyond FD_TPU_MTU)\n" );
     abort();
   }
-  if( s.frags ) bundle_id = s.h_bid;                         /* read from the fd_txn_m_t headers on the GPU */
-  s.nsig = s.n ? *s.h_counter : 0u;
+  s.nsig = s.n ? hdr[0] : 0u;
   float gpu_ms = 0.f;
   TX_CHECK( hipEventElapsedTime( &gpu_ms, s.ev_start, s.ev_done ) );
   auto h0 = std::chrono::steady_clock::now();
@@ -719,21 +745,21 @@ fd_verify_hip_tile_complete( fd_verify_hip_tile_t * t, ulong const * bundle_id, 
   ulong * const ring = t->ring;
   ulong const depth = t->depth;
   const ulong PF = 8;
-  for( ulong j = 0; j < n && j < PF; j++ ) __builtin_prefetch( map + (s.h_tag[j] & mask) );
+  for( ulong j = 0; j < n && j < PF; j++ ) __builtin_prefetch( map + (R[j].tag & mask) );
   for( ulong j = 0; j < n; j++ ) {
     if( s.frags ) {                                          /* after_frag's first statement (:112) */
-      u32 k = s.h_kind[j];
+      u32 k = R[j].kind;
       t->m_gossip += (k == FD_VERIFY_HIP_IN_GOSSIP) | (k == FD_VERIFY_HIP_IN_SEND);
     }
     if( j + PF < n ) {
-      __builtin_prefetch( map + (s.h_tag[j + PF] & mask) );
+      __builtin_prefetch( map + (R[j + PF].tag & mask) );
       ulong o = *t->oldest + PF; if( o >= depth ) o -= depth;
       if( o < depth ) __builtin_prefetch( map + (ring[o] & mask) );
     }
-    u32 tsz = s.h_tsz[j];
+    u32 tsz = R[j].tsz;
     if( txn_t_sz ) txn_t_sz[j] = (ushort)tsz;
     if( tag_out ) tag_out[j] = 0;
-    ulong bid = bundle_id ? bundle_id[j] : 0ul;
+    ulong bid = s.frags ? R[j].bid : bundle_id ? bundle_id[j] : 0ul;   /* frag mode: from the fd_txn_m_t header */
     int is_bundle = bid != 0ul;
     if( is_bundle && bid != t->bundle_id ) { t->bundle_failed = 0; t->bundle_id = bid; }
     if( is_bundle && t->bundle_failed ) { t->m_bundle++; result[j] = FD_VERIFY_HIP_FRAG_BUNDLE_PEER; continue; }
@@ -742,10 +768,10 @@ fd_verify_hip_tile_complete( fd_verify_hip_tile_t * t, ulong const * bundle_id, 
       t->m_parse++; result[j] = FD_VERIFY_HIP_FRAG_PARSE_FAIL; continue;
     }
     /* fd_txn_verify with dedup = !is_bundle */
-    ulong tag = s.h_tag[j];
+    ulong tag = R[j].tag;
     int res;
     if( !is_bundle && fd_verify_hip_tcache_query( map, t->map_cnt, tag ) )       res = FD_TXN_VERIFY_DEDUP;
-    else if( s.h_tcode[j] != FD_ED25519_SUCCESS )                                 res = FD_TXN_VERIFY_FAILED;
+    else if( R[j].tcode != FD_ED25519_SUCCESS )                                   res = FD_TXN_VERIFY_FAILED;
     else if( !is_bundle && fd_verify_hip_tcache_insert( t->oldest, ring, depth, map, t->map_cnt, tag ) )
                                                                                   res = FD_TXN_VERIFY_DEDUP;
     else                                                                          res = FD_TXN_VERIFY_SUCCESS;
