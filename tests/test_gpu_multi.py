@@ -75,3 +75,58 @@ def test_bench_world2_c5_gloo(tmp_path):
     assert d["n_gpus"] == 2 and d["scaling"] == "strong" and d["config"]["config_id"] == "c5"
     assert d["value"] > 0 and d["steps"] == 2
     assert str(1 << 22) in d["config"]["workload"]          # n_all all-reduced over both ranks
+
+
+@pytest.mark.gpu
+def test_c5_full_size_sharded_on_one_gpu():
+    """BASELINE configs[4] at its full size: 2^26 C2-mix signatures, cut by
+    bench's c5_shard for world 8 and verified shard by shard on 8 contexts of
+    this one GPU (what 8 ranks do on 8 GPUs); the concatenated shard bitmaps
+    equal the codes, every mutation class lands in its rejection class, the
+    accept rate is the C2 mix's, and a 4K sample is bit-exact against the
+    oracle."""
+    import numpy as np
+    import torch
+
+    import bench
+    import oracle_lib as O
+    from firedancer_amd import Verifier
+    from firedancer_amd import workload as W
+    from firedancer_amd.ed25519 import CTX_STREAM
+    n, world = 1 << 26, 8
+    dev = torch.device("cuda", 0)
+    gen = Verifier(device=0, chunk_sigs=1 << 20)
+    b = W.make_batch_gpu(gen, n, msg_sz=64, seed=0xc5, mix="c2")
+    codes = torch.full((n,), 9, dtype=torch.int8, device=dev)
+    bm = torch.zeros(n // 64, dtype=torch.int64, device=dev)
+    torch.cuda.synchronize()
+    ctxs = []
+    for r in range(world):
+        total, lo, hi = bench.c5_shard(None, r, world)
+        assert total == n
+        v = Verifier(device=0, chunk_sigs=1 << 20)
+        ctxs.append(v)
+        v.verify_dev(hi - lo, b.sigs[lo:hi], b.pubs[lo:hi], b.pool, b.msg_off[lo:hi], b.msg_sz[lo:hi],
+                     codes[lo:hi], bm[lo // 64:hi // 64], stream=CTX_STREAM)
+    for v in ctxs:
+        v.sync()
+    c = codes.cpu().numpy()
+    kinds = b.kinds.cpu().numpy()
+    assert np.isin(c, (0, -1, -2, -3)).all()
+    bits = np.unpackbits(bm.cpu().numpy().view(np.uint8), bitorder="little").astype(bool)
+    assert np.array_equal(bits, c == 0)
+    assert (c[kinds == W.KIND_VALID] == 0).all()
+    assert (c[kinds == W.KIND_S_GE_L] == -1).all()
+    assert (c[kinds == W.KIND_A_SMALL] == -2).all()
+    assert (c[kinds == W.KIND_R_SMALL] == -1).all()
+    assert (c[kinds == W.KIND_SIGFLIP] != 0).all() and (c[kinds == W.KIND_PUBFLIP] != 0).all()
+    assert 0.77 < float((c == 0).mean()) < 0.81
+    idx = np.sort(np.random.default_rng(26).choice(n, 4096, replace=False))
+    ti = torch.from_numpy(idx).to(dev)
+    msgs = b.pool[:n * 64].view(n, 64)[ti].cpu().numpy()                  # message i = pool[64i, +64)
+    pool = np.concatenate([msgs.reshape(-1), np.zeros(16, np.uint8)])
+    exp = O.verify_many(b.sigs[ti].cpu().numpy(), b.pubs[ti].cpu().numpy(), pool,
+                        (np.arange(idx.size) * 64).astype(np.uint32), np.full(idx.size, 64, np.uint32))
+    assert np.array_equal(c[idx], exp)
+    for v in ctxs + [gen]:
+        v.close()
