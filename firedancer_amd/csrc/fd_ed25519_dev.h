@@ -928,6 +928,9 @@ DEV void sha512_prefixed( u32 x[16], u32 const pre[16], u32 plen, u8 const * msg
         past msz zero, the 0x80 pad byte at msz: fd_sha512.c:365-385);
      4. each lane reads its window back at its byte offset, forms the block's
         big-endian words and runs the compression in registers.
+   Lanes whose (message, size) repeats the previous lane's (the signatures of
+   one txn, a batch_single_msg group) skip steps 1-3 and read the first
+   lane's window of their run: a shared message is loaded once per wave.
    buf: this wave's 64 x 36 words of LDS; meta: its 64 u64.  The pool must be
    readable up to the 16-B boundary after each message's last byte. */
 DEV void wave_lds_sync( void ) {
@@ -950,7 +953,18 @@ DEV void sha512_prefixed_coop( u32 x[16], u32 const pre[16], u8 const * msg, u32
   u32 nb = (PLEN + msz + 17u + 127u) >> 7;
   u32 nbmax = wave_max_u32( nb );
   u64 bitlen = (u64)(PLEN + msz) << 3;
+  /* records sharing a message (a txn's signatures, expanded side by side;
+     batch_single_msg groups) load it once: a lane whose (message, size)
+     equals the previous lane's publishes an empty window and reads its
+     run leader's copy */
+  u64 mp = (u64)(uintptr_t)msg;
+  u32 plo = __shfl_up( (u32)mp, 1u ), phi = __shfl_up( (u32)(mp >> 32), 1u ), pms = __shfl_up( msz, 1u );
+  bool dup = lane > 0u && plo == (u32)mp && phi == (u32)(mp >> 32) && pms == msz;
+  unsigned long long dmask = __ballot( dup );
+  unsigned long long below = lane == 63u ? ~0ULL : ((2ULL << lane) - 1ULL);
+  u32 leader = 63u - (u32)__clzll( ~dmask & below );
   u32 * own = buf + 36u*lane;
+  u32 const * src = buf + 36u*leader;
   #pragma unroll 1
   for( u32 b=0; b<nbmax; b++ ) {
     u32 m0 = b ? 128u*b - PLEN : 0u;                      /* message offset of the window */
@@ -961,7 +975,7 @@ DEV void sha512_prefixed_coop( u32 x[16], u32 const pre[16], u8 const * msg, u32
     uintptr_t addr = (uintptr_t)(msg + m0);
     u32 o = (u32)(addr & 15u);
     u32 nch = nbytes ? (o + nbytes + 15u) >> 4 : 0u;
-    meta[lane] = ((u64)(addr >> 4) & 0xfffffffffffULL) | ((u64)nch << 44);
+    meta[lane] = dup ? 0ul : ((u64)(addr >> 4) & 0xfffffffffffULL) | ((u64)nch << 44);
     wave_lds_sync();
     #pragma unroll
     for( u32 i=0; i<9u; i++ ) {                            /* 576 pieces = 64 records x 9 chunks */
@@ -973,7 +987,7 @@ DEV void sha512_prefixed_coop( u32 x[16], u32 const pre[16], u8 const * msg, u32
     }
     wave_lds_sync();
     int P = (int)msz - (int)m0;                           /* pad position in the window */
-    if( act && P >= 0 && P < (int)wlen ) {
+    if( act && !dup && P >= 0 && P < (int)wlen ) {
       u32 e = o + (u32)P, q = e >> 4;
       uint4 * cp = (uint4 *)own + q;
       uint4 v = *cp;
@@ -989,7 +1003,7 @@ DEV void sha512_prefixed_coop( u32 x[16], u32 const pre[16], u8 const * msg, u32
     }
     wave_lds_sync();
     u32 mw[33];
-    u32 const * rp = own + (o >> 2);
+    u32 const * rp = src + (o >> 2);
     #pragma unroll
     for( int k=0; k<33; k++ ) mw[k] = rp[k];
     u32 sh = (o & 3u) * 8u;

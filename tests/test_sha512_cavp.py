@@ -80,3 +80,36 @@ def test_device_sha512_unaligned_and_block_edges(verifier):
         d = hashlib.sha512(raw[o:o + n].tobytes()).digest()
         assert got[i].tobytes() == d, ("per-lane", i, n, o % 16)
         assert got[m + i].tobytes() == d, ("cooperative LDS", i, n, o % 16)
+
+
+@pytest.mark.gpu
+def test_device_sha512_shared_message_runs(verifier):
+    """Adjacent records sharing a message (the cooperative path loads it once
+    per run and the rest of the run reads the leader's LDS copy): runs inside
+    a wave and across wave boundaries, the same start with different sizes
+    and the same size at different starts (neither may be merged), empty
+    messages, against hashlib for both device hash paths."""
+    import torch
+    rng = np.random.default_rng(8)
+    raw = rng.integers(0, 256, 20000, dtype=np.uint8)
+    offs, lens = [], []
+
+    def run(o, n, k):
+        offs.extend([o] * k); lens.extend([n] * k)
+    run(5, 200, 5); run(5, 199, 1); run(5, 200, 3); run(900, 0, 4); run(901, 0, 1)
+    run(1000, 1231, 70)                       # crosses the first wave boundary (lane 63 -> 64)
+    run(3000, 63, 1); run(3063, 63, 1); run(3000, 63, 2)
+    for _ in range(200):                      # random runs of 1..20 over 40 distinct windows
+        o = int(rng.integers(0, 40)) * 400 + int(rng.integers(0, 16)); n = int(rng.integers(0, 390))
+        run(o, n, int(rng.integers(1, 21)))
+    offs, lens = np.array(offs, np.uint32), np.array(lens, np.uint32)
+    m = offs.size
+    dev = torch.device("cuda", 0)
+    out = torch.zeros((2 * m, 64), dtype=torch.uint8, device=dev)
+    verifier.test_sha512(m, torch.from_numpy(raw).to(dev), torch.from_numpy(offs.view(np.int32)).to(dev),
+                         torch.from_numpy(lens.view(np.int32)).to(dev), out)
+    got = out.cpu().numpy()
+    for i, (o, n) in enumerate(zip(offs, lens)):
+        d = hashlib.sha512(raw[o:o + n].tobytes()).digest()
+        assert got[i].tobytes() == d, ("per-lane", i, int(o), int(n))
+        assert got[m + i].tobytes() == d, ("cooperative LDS", i, int(o), int(n))
