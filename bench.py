@@ -202,14 +202,19 @@ def main():
     ap.add_argument("--contexts", type=int, default=2,
                     help="c1/c2/c3/c5: verify contexts (streams) each step is split over (measured with the "
                          "persistent DSM: 1 -> 118.2M, 2 -> 125.0-125.7M, 4 -> 124.5M verifies/s)")
-    ap.add_argument("--tiles", type=int, default=2,
-                    help="c4: verify tiles (host threads + contexts) per GPU; more tiles than the 4 hardware queues "
-                         "per process share queues (16 tiles: -18%%)")
+    ap.add_argument("--tiles", type=int, default=6,
+                    help="c4: verify tiles (host threads + contexts) per GPU (r02n, 2^20 frags per step, resident / "
+                         "PCIe-inclusive M verifies/s: 2 -> 101-103 / 75-85, 4 -> 100-102 / 90-95, 6 -> 106-109 / "
+                         "98-101, 8 -> 100-102 / 97-98)")
     ap.add_argument("--c4-ingest", default="frags", choices=["frags", "payload"],
                     help="c4: fd_txn_m_t frags in each tile's in-link dcache (default) or raw payloads + offsets")
-    ap.add_argument("--c4-pcie", default="dma", choices=["zerocopy", "dma"],
+    ap.add_argument("--c4-pcie", default="dma", choices=["zerocopy", "dma", "dma_tile_stream"],
                     help="c4 PCIe-inclusive leg: the GPU reads each in-link dcache in place from pinned mapped host "
-                         "memory (zerocopy), or it is copied host->HBM by DMA each step (dma)")
+                         "memory (zerocopy), or it is copied host->HBM each step on a copy stream per tile (dma) or "
+                         "on the tile's own stream ahead of its batch (dma_tile_stream)")
+    ap.add_argument("--c4-pcie-steps", type=int, default=24,
+                    help="c4 PCIe-inclusive leg: timed steps (the pipeline's fill, one copy, and drain, one host "
+                         "pass, are paid once per leg; 0: --steps)")
     ap.add_argument("--sigs", type=int, default=None, help="override signatures per GPU per step")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--cpu-seconds", type=float, default=8.0)
@@ -488,13 +493,14 @@ def run_c4(args, rank, world, local, dist):
     value = signatures verified per second (all tiles, all ranks), in-link
     dcaches resident in HBM.  A second timed leg (frags ingest) copies every
     tile's in-link dcache host->HBM each step from pinned memory on a copy
-    stream, double-buffered so the copy of batch k+1 overlaps the GPU work of
-    batch k: "pcie_inclusive"."""
+    stream, triple-buffered and queued one batch ahead, so the copy of batch
+    k+1 overlaps the GPU work of batch k and the host pass of batch k-1:
+    "pcie_inclusive"."""
     import threading
 
     import torch
     from firedancer_amd import Verifier
-    from firedancer_amd.ed25519 import HostBuffer
+    from firedancer_amd.ed25519 import CTX_STREAM, HostBuffer
     from firedancer_amd.txn_workload import PARSED_CHUNKS, gpu_signer, make_txn_stream, txnm_dcache
     from firedancer_amd.verify_tile import IN_QUIC, VerifyTile
     T = max(1, args.tiles)
@@ -515,7 +521,7 @@ def run_c4(args, rank, world, local, dist):
             hb = HostBuffer(region.size)                     # pinned, device-mapped (fd_ed25519_hip_host_alloc)
             hb.array[:] = region
             h_in = torch.from_numpy(hb.array)
-            d_in = [to_dev(region), torch.empty_like(h_in, device=dev)]
+            d_in = [to_dev(region), torch.empty_like(h_in, device=dev), torch.empty_like(h_in, device=dev)]
             d_out = torch.empty(64 * PARSED_CHUNKS * max(int(sel.size), 1), dtype=torch.uint8, device=dev)
             out_chunk = to_dev((np.arange(sel.size) * PARSED_CHUNKS).astype(np.uint32), np.int32)
             kinds = to_dev(np.full(sel.size, IN_QUIC, np.uint8))
@@ -523,7 +529,7 @@ def run_c4(args, rank, world, local, dist):
                               in_chunk=to_dev(chunk, np.int32),
                               in_sz=to_dev(fsz, np.int16), kinds=kinds, out_chunk=out_chunk,
                               cs=torch.cuda.Stream(dev), ts=torch.cuda.ExternalStream(vs[t].stream, device=dev),
-                              free=[None, None]))
+                              free=[None] * 3, ready=[None] * 3))
             h2d_bytes += region.size
         else:
             parts.append(dict(n=int(sel.size), off=to_dev(s.off[sel], np.int32), sz=to_dev(s.sz[sel], np.int16)))
@@ -532,7 +538,21 @@ def run_c4(args, rank, world, local, dist):
     diag = os.environ.get("FD_C4_DIAG")
     h2d = [False]
 
-    def submit(t):
+    def stage(t, j):
+        # copy step j's in-link dcache host -> HBM on the tile's copy stream
+        # (pinned, DMA engine) into buffer j % 3, once batch j-3's GPU work
+        # (the buffer's previous reader) is done
+        P = parts[t]
+        b = j % 3
+        with torch.cuda.stream(P["cs"]):
+            if P["free"][b] is not None:
+                P["cs"].wait_event(P["free"][b])
+            P["d_in"][b].copy_(P["h_in"], non_blocking=True)
+            ready = torch.cuda.Event()
+            ready.record(P["cs"])
+        P["ready"][b] = (j, ready)
+
+    def submit(t, more=False):
         P = parts[t]
         tiles[t].set_seed(seed_base + 7 * k_step[t])
         if not frags_mode:
@@ -544,30 +564,36 @@ def run_c4(args, rank, world, local, dist):
             # the ingest kernel reads the in-link dcache in place over PCIe
             tiles[t].submit_frags(P["n"], P["hb"].ptr, P["in_chunk"], P["in_sz"], P["kinds"], P["d_out"],
                                   P["out_chunk"])
-        else:
-            # copy this batch's in-link dcache host -> HBM on the tile's copy
-            # stream (pinned, DMA engine) into the buffer batch k-2 used, once
-            # that batch's GPU work has read it; the tile stream waits for it
-            b = k_step[t] & 1
-            buf = P["d_in"][b]
-            with torch.cuda.stream(P["cs"]):
-                if P["free"][b] is not None:
-                    P["cs"].wait_event(P["free"][b])
-                buf.copy_(P["h_in"], non_blocking=True)
-                ready = torch.cuda.Event()
-                ready.record(P["cs"])
-            P["ts"].wait_event(ready)
+        elif args.c4_pcie == "dma_tile_stream":
+            # the copy is queued on the tile's own stream right before its batch:
+            # no extra stream (hardware queues are shared beyond 4 per process);
+            # the other tile's GPU work overlaps it
+            buf = P["d_in"][k_step[t] & 1]
+            vs[t].stage_async(buf, P["hb"], P["hb"].nbytes, stream=CTX_STREAM)
             tiles[t].submit_frags(P["n"], buf, P["in_chunk"], P["in_sz"], P["kinds"], P["d_out"], P["out_chunk"])
+        else:
+            # the batch waits for its staged copy; the next batch's copy is
+            # queued right behind this submit, so it overlaps this batch's GPU
+            # work and the host pass of the one before (triple-buffered)
+            j = k_step[t]
+            b = j % 3
+            if P["ready"][b] is None or P["ready"][b][0] != j:
+                stage(t, j)
+            P["ts"].wait_event(P["ready"][b][1])
+            tiles[t].submit_frags(P["n"], P["d_in"][b], P["in_chunk"], P["in_sz"], P["kinds"], P["d_out"],
+                                  P["out_chunk"])
             done = torch.cuda.Event()
             done.record(P["ts"])
             P["free"][b] = done
+            if more:
+                stage(t, j + 1)
         k_step[t] += 1
 
     def tile_loop(t, steps, outs, gpu_ms, host_ms):
-        submit(t)
+        submit(t, more=steps > 1)
         for k in range(steps):
             if k + 1 < steps:
-                submit(t)
+                submit(t, more=k + 2 < steps)
             outs[t].append(tiles[t].complete())
             lt = tiles[t].last_timing(); gpu_ms[t].append(lt["gpu_ms"]); host_ms[t].append(lt["host_ms"])
             if diag:
@@ -619,16 +645,18 @@ def run_c4(args, rank, world, local, dist):
     if frags_mode:
         h2d[0] = True
         run(1)
-        e2, sigs2, _, outs2, _, _, _ = timed(args.steps)
+        k2 = args.c4_pcie_steps or args.steps
+        e2, sigs2, _, outs2, _, _, _ = timed(k2)
         same = all(np.array_equal(a[-1][0], b[-1][0]) for a, b in zip(outs, outs2))
-        pcie = {"value": round(sigs2 / e2, 1), "unit": "verifies/s", "ms_per_step": round(e2 / args.steps * 1e3, 4),
-                "h2d_bytes_per_step": h2d_bytes * world, "h2d_GBps": round(h2d_bytes * world * args.steps / e2 / 1e9, 2),
+        pcie = {"value": round(sigs2 / e2, 1), "unit": "verifies/s", "steps": k2, "ms_per_step": round(e2 / k2 * 1e3, 4),
+                "h2d_bytes_per_step": h2d_bytes * world, "h2d_GBps": round(h2d_bytes * world * k2 / e2 / 1e9, 2),
                 "results_equal_resident_leg": bool(same),
                 "mode": args.c4_pcie,
                 "what": ("every tile's in-link dcache (fd_txn_m_t frags) in pinned device-mapped host memory, read in "
                          "place by the ingest kernel over PCIe each step" if args.c4_pcie == "zerocopy" else
                          "every tile's in-link dcache (fd_txn_m_t frags) copied host->HBM each step from pinned memory "
-                         "(copy stream per tile, double-buffered, overlapped with the previous batch)") +
+                         + ("on the tile's own stream ahead of its batch" if args.c4_pcie == "dma_tile_stream" else
+                            "(copy stream per tile, triple-buffered, queued one batch ahead)")) +
                         "; per-frag results D2H as in the resident leg; the out dcache stays in HBM"}
         h2d[0] = False
     res = np.concatenate([o[-1][0] for o in outs])

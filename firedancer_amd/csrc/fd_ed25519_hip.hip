@@ -1126,6 +1126,14 @@ fd_ed25519_hip_host_free( void * p ) {
 }
 
 int
+fd_ed25519_hip_stage_async( fd_ed25519_hip_ctx_t * ctx, void * d_dst, void const * h_src, ulong sz, void * stream ) {
+  hipStream_t s = stream ? (hipStream_t)stream : ctx->stream;
+  FD_CHECK( hipSetDevice( ctx->device ) );
+  if( sz ) FD_CHECK( hipMemcpyAsync( d_dst, h_src, sz, hipMemcpyHostToDevice, s ) );
+  return 0;
+}
+
+int
 fd_ed25519_hip_sync( fd_ed25519_hip_ctx_t * ctx ) {
   FD_CHECK( hipSetDevice( ctx->device ) );
   FD_CHECK( hipStreamSynchronize( ctx->stream ) );

@@ -34,6 +34,7 @@ EXPORTS = (
     "fd_ed25519_hip_sync", "fd_ed25519_hip_set_timing", "fd_ed25519_hip_get_timing",
     "fd_ed25519_hip_get_dsm_units", "fd_ed25519_hip_set_halfsize", "fd_ed25519_hip_test_halfsize",
     "fd_ed25519_hip_test_sha512", "fd_ed25519_hip_host_alloc", "fd_ed25519_hip_host_free",
+    "fd_ed25519_hip_stage_async",
 )
 
 _lib = None
@@ -73,6 +74,8 @@ def lib():
         L.fd_ed25519_hip_host_alloc.restype = vp
         L.fd_ed25519_hip_host_alloc.argtypes = [u64]
         L.fd_ed25519_hip_host_free.argtypes = [vp]
+        L.fd_ed25519_hip_stage_async.restype = c.c_int
+        L.fd_ed25519_hip_stage_async.argtypes = [vp, vp, vp, u64, vp]
         L.fd_ed25519_hip_verify_dev.restype = c.c_int
         L.fd_ed25519_hip_verify_dev.argtypes = [vp, u64, vp, vp, vp, vp, vp, vp, vp, vp]
         L.fd_ed25519_hip_verify_fixed_dev.restype = c.c_int
@@ -317,6 +320,13 @@ class Verifier:
                 self._p(msg_sz, 4 * n, "msg_sz"), self._p(out, 128 * n, "out"))
         with self._stream(stream) as h:
             return self._lib.fd_ed25519_hip_test_sha512(*args, h)
+
+    def stage_async(self, d_dst, h_src, nbytes, stream=None):
+        """Host -> device copy of nbytes (h_src: a HostBuffer or raw host address) on a stream."""
+        src = h_src.ptr if isinstance(h_src, HostBuffer) else int(h_src)
+        with self._stream(stream) as h:
+            return self._lib.fd_ed25519_hip_stage_async(self.ctx, self._p(d_dst, int(nbytes), "d_dst"), src,
+                                                        int(nbytes), h)
 
     def set_timing(self, on):
         self._lib.fd_ed25519_hip_set_timing(self.ctx, 1 if on else 0)

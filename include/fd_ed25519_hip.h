@@ -237,6 +237,14 @@ fd_ed25519_hip_sign_dev( fd_ed25519_hip_ctx_t * ctx,
 void * fd_ed25519_hip_host_alloc( ulong sz );
 void   fd_ed25519_hip_host_free ( void * p );
 
+/* Enqueue a host->device copy of sz bytes on stream (NULL: the context's
+   stream), e.g. a verify tile's in-link dcache region staged into HBM ahead
+   of fd_verify_hip_tile_submit_frags.  With h_src from
+   fd_ed25519_hip_host_alloc the copy is a DMA transfer that returns at once;
+   the caller keeps h_src unchanged until the stream has passed the copy. */
+int fd_ed25519_hip_stage_async( fd_ed25519_hip_ctx_t * ctx, void * d_dst, void const * h_src, ulong sz,
+                                void * stream );
+
 /* Blocks until all work queued on the context's stream is done. */
 int fd_ed25519_hip_sync( fd_ed25519_hip_ctx_t * ctx );
 

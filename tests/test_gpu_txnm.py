@@ -204,3 +204,33 @@ def test_zero_copy_ingest_from_mapped_host_memory(verifier):
     assert np.array_equal(res, c4["result"]) and np.array_equal(tag, c4["tag"])
     check_out_frags(d_out.cpu().numpy(), out_chunk, frags, kinds, c4["pool"], c4["off"], c4["sz"], tsz)
     hb.close()
+
+
+def test_staged_ingest_from_pinned_host_memory(verifier):
+    """The in-link dcache in pinned host memory staged into HBM with
+    fd_ed25519_hip_stage_async on the tile's own stream (the DMA copy the C4
+    PCIe-inclusive bench leg runs), then submit_frags on the HBM copy; the
+    stream orders the copy before the ingest kernel.  Results and out frags
+    equal the reference tile's."""
+    import torch
+    from firedancer_amd.ed25519 import CTX_STREAM, HostBuffer
+    c4 = dict(np.load(os.path.join(HERE, "golden", "c4_stream_2048.npz")))
+    n = c4["off"].size
+    region, in_chunk, in_sz, kinds, frags = build_in_dcache(c4["pool"], c4["off"], c4["sz"], c4["bundle_id"])
+    hb = HostBuffer(region.size)
+    hb.array[:] = region
+    d_in = torch.full((region.size,), 0xA5, dtype=torch.uint8, device="cuda:0")
+    torch.cuda.synchronize()
+    out_chunk = (np.arange(n) * PARSED_CHUNKS).astype(np.uint32)
+    tile = V.VerifyTile(verifier, max_txn=n, hashmap_seed=int(c4["seed"]), tcache_depth=int(c4["depth"]))
+    d_out = torch.zeros(64 * (int(out_chunk.max()) + PARSED_CHUNKS), dtype=torch.uint8, device="cuda:0")
+    args = (_dev(in_chunk, np.int32), _dev(in_sz, np.int16), _dev(kinds), d_out, _dev(out_chunk, np.int32))
+    torch.cuda.synchronize()
+    verifier.stage_async(d_in, hb, region.size, stream=CTX_STREAM)
+    tile.submit_frags(n, d_in, *args)
+    res, tag, tsz = tile.complete(None)
+    tile.close()
+    assert np.array_equal(d_in.cpu().numpy(), region)
+    assert np.array_equal(res, c4["result"]) and np.array_equal(tag, c4["tag"])
+    check_out_frags(d_out.cpu().numpy(), out_chunk, frags, kinds, c4["pool"], c4["off"], c4["sz"], tsz)
+    hb.close()
