@@ -938,11 +938,10 @@ DEV void wave_lds_sync( void ) {
   __builtin_amdgcn_wave_barrier();
 }
 
-DEV u32 wave_max_u32( u32 v ) {                 /* v < 2^7, over all lanes of the wave */
-  u32 m = 0u;
+DEV u32 wave_max_u32( u32 v ) {                 /* max of v over all lanes of the wave (butterfly) */
   #pragma unroll
-  for( int b=6; b>=0; b-- ) { u32 c = m | (1u << b); if( __ballot( v >= c ) ) m = c; }
-  return m;
+  for( int d=32; d>=1; d>>=1 ) v = max( v, (u32)__shfl_xor( (int)v, d ) );
+  return v;
 }
 
 template<u32 PLEN>   /* prefix bytes: 64 (R||A, the verify path) or 0 (plain SHA-512, the test hook) */
@@ -986,9 +985,9 @@ DEV void sha512_prefixed_coop( u32 x[16], u32 const pre[16], u8 const * msg, u32
       ((uint4 *)(buf + 36u*r))[c] = v;
     }
     wave_lds_sync();
-    int P = (int)msz - (int)m0;                           /* pad position in the window */
-    if( act && !dup && P >= 0 && P < (int)wlen ) {
-      u32 e = o + (u32)P, q = e >> 4;
+    u32 P = msz - m0;                                     /* pad position in the window (unsigned: */
+    if( act && !dup && msz >= m0 && P < wlen ) {          /* messages up to 4 GB)                 */
+      u32 e = o + P, q = e >> 4;
       uint4 * cp = (uint4 *)own + q;
       uint4 v = *cp;
       u32 w[4] = { v.x, v.y, v.z, v.w };

@@ -1221,6 +1221,14 @@ static fd_ed25519_hip_ctx_t * default_ctx( void ) {
   return g_ctx;
 }
 
+/* the process-wide context for the library's other host-memory APIs
+   (fd_sha512_hip.hip batching); not part of the public ABI */
+__attribute__((visibility("hidden"))) fd_ed25519_hip_ctx_t *
+fd_ed25519_hip_private_default_ctx( void ) {
+  std::lock_guard<std::mutex> lk( g_lock );
+  return default_ctx();
+}
+
 /* The engine addresses messages with 32-bit offsets and sizes.  A longer
    message cannot be hashed here; verifying a truncated prefix instead would
    be a silent divergence from the reference (which hashes all of it), so the

@@ -5,7 +5,7 @@ import os
 import re
 import subprocess
 
-from firedancer_amd import ed25519, replay, verify_tile
+from firedancer_amd import ed25519, replay, sha512, verify_tile
 from firedancer_amd.build import LIB, build
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -24,7 +24,8 @@ def test_build_and_exports():
     assert declared_functions("fd_ed25519_hip.h") == set(ed25519.EXPORTS)
     assert declared_functions("fd_verify_hip.h") == set(verify_tile.EXPORTS)
     assert declared_functions("fd_replay_hip.h") == set(replay.EXPORTS)
-    names = set(ed25519.EXPORTS) | set(verify_tile.EXPORTS) | set(replay.EXPORTS)
+    assert declared_functions("fd_sha512_hip.h") == set(sha512.EXPORTS)
+    names = set(ed25519.EXPORTS) | set(verify_tile.EXPORTS) | set(replay.EXPORTS) | set(sha512.EXPORTS)
     out = subprocess.check_output(["nm", "-D", "--defined-only", LIB]).decode()
     exported = set(re.findall(r" T (\w+)", out))
     assert names <= exported, names - exported
@@ -54,15 +55,16 @@ def test_no_reference_or_oracle_in_product():
 
 def test_headers_compile_and_link_as_c(tmp_path):
     """The boundary is a C ABI: a C11 translation unit (as the reference's C
-    tiles would be) includes all three headers next to the system headers
+    tiles would be) includes all four headers next to the system headers
     with -Wall -Wextra -Werror, takes the address of every declared function,
     links against the library and runs (no GPU call)."""
     build()
     names = set()
-    for h in ("fd_ed25519_hip.h", "fd_verify_hip.h", "fd_replay_hip.h"):
+    for h in ("fd_ed25519_hip.h", "fd_verify_hip.h", "fd_replay_hip.h", "fd_sha512_hip.h"):
         names |= declared_functions(h)
     src = ['#include <stdio.h>', '#include <stdint.h>', '#include <sys/types.h>',
            '#include "fd_ed25519_hip.h"', '#include "fd_verify_hip.h"', '#include "fd_replay_hip.h"',
+           '#include "fd_sha512_hip.h"',
            'static void * const fns[] = {']
     src += ['  (void *)%s,' % n for n in sorted(names)]
     src += ['};', 'int main( void ) { printf( "%d\\n", (int)(sizeof(fns)/sizeof(fns[0])) ); return 0; }']
