@@ -922,3 +922,209 @@ fd_fec_hip_verify_roots_dev( fd_ed25519_hip_ctx_t * ctx, ulong n, uchar const * 
                              uchar const * d_pubs, signed char * d_codes, void * stream ) {
   return fd_ed25519_hip_verify_fixed_dev( ctx, n, d_sigs, d_pubs, d_roots, 32u, d_codes, NULL, stream );
 }
+
+/**********************************************************************/
+/* ed25519 program instructions (include/fd_replay_hip.h)             */
+
+static_assert( sizeof(fd_precompile_hip_desc_t) == 16, "fd_precompile_hip_desc_t layout" );
+static_assert( sizeof(fd_precompile_hip_instr_t) == 8, "fd_precompile_hip_instr_t layout" );
+
+#define PC_ERR_SIGNATURE    2u   /* fd_precompiles.h:16-18 */
+#define PC_ERR_DATA_OFFSET  3u
+#define PC_ERR_DATA_SIZE    4u
+#define PC_ERR_DESC         0xFFFFFFFFu
+
+/* fd_precompile_ed25519_verify :130-154: the instruction-level size checks
+   and the signature count (the offset records then lie inside the data) */
+__global__ __launch_bounds__(256)
+void k_pc_count( ulong n, u8 const * __restrict__ pool, fd_precompile_hip_desc_t const * __restrict__ desc,
+                 u8 * __restrict__ cnt, u32 * __restrict__ early ) {
+  ulong j = (ulong)blockIdx.x * blockDim.x + threadIdx.x;
+  if( j >= n ) return;
+  fd_precompile_hip_desc_t d = desc[j];
+  u32 sz = d.data_sz, e = 0u, c = 0u;
+  u8 const * data = pool + d.data_off;
+  if( sz > FD_PRECOMPILE_HIP_DATA_MAX ) e = PC_ERR_DESC;
+  else if( sz < 16u ) e = (sz == 2u && data[0] == 0u) ? 0u : PC_ERR_DATA_SIZE;   /* the [0,0] edge case */
+  else {
+    c = data[0];
+    if( !c || sz < 14u*c + 2u ) { e = PC_ERR_DATA_SIZE; c = 0u; }
+  }
+  cnt[j] = (u8)c; early[j] = e;
+}
+
+/* fd_precompile_get_instr_data (:76-107) */
+DEVI u32 pc_resolve( fd_precompile_hip_desc_t const & d, fd_precompile_hip_instr_t const * __restrict__ tab,
+                     u32 index, u32 offset, u32 sz, u32 & at ) {
+  u32 base, dsz;
+  if( index == 0xFFFFu ) { base = d.data_off; dsz = d.data_sz; }
+  else {
+    if( index >= d.instr_cnt ) return PC_ERR_DATA_OFFSET;
+    fd_precompile_hip_instr_t t = tab[d.instr_base + index];
+    base = t.data_off; dsz = t.data_sz;
+  }
+  if( offset + sz > dsz ) return PC_ERR_SIGNATURE;
+  at = base + offset;
+  return 0u;
+}
+
+/* One record per offset record (signature i of instruction j), allocated as
+   k_txn_expand allocates (wave prefix sums, one atomic per wave, records of a
+   wave contiguous and in order, first[] says where).  A record whose spans
+   fail the fetch checks keeps the error (pre[r]) and a zero signature; the
+   others get their signature and public key copied out and their message
+   span, for one verify pass over every record. */
+__global__ __launch_bounds__(256)
+void k_pc_expand( ulong n, u8 const * __restrict__ pool, fd_precompile_hip_desc_t const * __restrict__ desc,
+                  fd_precompile_hip_instr_t const * __restrict__ tab, u8 * __restrict__ cnt,
+                  u32 * __restrict__ early, u32 * __restrict__ counter, u32 * __restrict__ first,
+                  u8 * __restrict__ rsig, u8 * __restrict__ rpub, u32 * __restrict__ rmoff, u32 * __restrict__ rmsz,
+                  u8 * __restrict__ rpre, ulong cap ) {
+  __shared__ u32 l_excl[256], l_c[256];
+  ulong j = (ulong)blockIdx.x * blockDim.x + threadIdx.x;
+  u32 c = j < n ? cnt[j] : 0u;
+  u32 excl = 0, tot = 0;
+  #pragma unroll
+  for( int b = 0; b < 7; b++ ) {                               /* c <= 87 */
+    unsigned long long m = __ballot( (c >> b) & 1u );
+    u32 below = __builtin_amdgcn_mbcnt_hi( (u32)(m >> 32), __builtin_amdgcn_mbcnt_lo( (u32)m, 0u ) );
+    excl += below << b;
+    tot  += (u32)__popcll( m ) << b;
+  }
+  u32 base = 0;
+  if( (threadIdx.x & 63u) == 0u && tot ) base = atomicAdd( counter, tot );
+  base = __shfl( base, 0 );
+  u32 lc = c;
+  if( j < n ) {
+    u32 f = base + excl;
+    first[j] = f;
+    if( (ulong)f + c > cap ) { cnt[j] = 0; early[j] = PC_ERR_DESC; lc = 0; }   /* never taken: cap = 87 per instruction */
+  }
+  l_excl[threadIdx.x] = excl; l_c[threadIdx.x] = lc;
+  __syncthreads();
+  u32 w0 = threadIdx.x & ~63u;
+  for( u32 t = threadIdx.x & 63u; t < tot; t += 64u ) {
+    u32 lo = 0, hi = 63;                                       /* last lane with excl <= t */
+    #pragma unroll
+    for( int s = 0; s < 6; s++ ) {
+      u32 mid = (lo + hi + 1u) >> 1;
+      bool le = l_excl[w0 + mid] <= t;
+      lo = le ? mid : lo; hi = le ? hi : mid - 1u;
+    }
+    u32 L = w0 + lo, k = t - l_excl[L];
+    if( k >= l_c[L] ) continue;
+    fd_precompile_hip_desc_t d = desc[(ulong)blockIdx.x * blockDim.x + L];
+    u8 const * o = pool + d.data_off + 2u + 14u*k;             /* fd_ed25519_signature_offsets_t, packed LE */
+    u32 f[7];
+    #pragma unroll
+    for( int q = 0; q < 7; q++ ) f[q] = (u32)o[2*q] | ((u32)o[2*q+1] << 8);
+    u32 sig_at = 0, pub_at = 0, msg_at = 0;
+    u32 e = pc_resolve( d, tab, f[1], f[0], 64u, sig_at );               /* :164-172 */
+    if( !e ) e = pc_resolve( d, tab, f[3], f[2], 32u, pub_at );          /* :179-187 */
+    if( !e ) e = pc_resolve( d, tab, f[6], f[4], f[5], msg_at );         /* :194-203 */
+    u32 r = base + t;
+    u32 w[16];
+    if( !e ) ld_words_u<16>( w, pool + sig_at );
+    else {
+      #pragma unroll
+      for( int q = 0; q < 16; q++ ) w[q] = 0u;
+    }
+    uint4 * ds = (uint4 *)(rsig + 64ul*r);
+    #pragma unroll
+    for( int q = 0; q < 4; q++ ) ds[q] = make_uint4( w[4*q], w[4*q+1], w[4*q+2], w[4*q+3] );
+    if( !e ) ld_words_u<8>( w, pool + pub_at );
+    uint4 * dp = (uint4 *)(rpub + 32ul*r);
+    #pragma unroll
+    for( int q = 0; q < 2; q++ ) dp[q] = make_uint4( w[4*q], w[4*q+1], w[4*q+2], w[4*q+3] );
+    rmoff[r] = e ? 0u : msg_at; rmsz[r] = e ? 0u : f[5];
+    rpre[r] = (u8)e;
+  }
+}
+
+/* :156-211: the first offset record in order that fails its fetch checks or
+   its verify decides the instruction's result */
+__global__ __launch_bounds__(256)
+void k_pc_reduce( ulong n, u8 const * __restrict__ cnt, u32 const * __restrict__ first, u32 const * __restrict__ early,
+                  u8 const * __restrict__ rpre, signed char const * __restrict__ rcode, int * __restrict__ err,
+                  u32 * __restrict__ custom ) {
+  ulong j = (ulong)blockIdx.x * blockDim.x + threadIdx.x;
+  if( j >= n ) return;
+  u32 e = early[j];
+  if( e == PC_ERR_DESC ) { err[j] = FD_PRECOMPILE_HIP_ERR_DESC; custom[j] = e; return; }
+  if( !e ) {
+    u32 c = cnt[j], f = first[j];
+    for( u32 k = 0; k < c; k++ ) {
+      u32 p = rpre[f + k];
+      if( p ) { e = p; break; }
+      if( rcode[f + k] != FD_ED25519_SUCCESS ) { e = PC_ERR_SIGNATURE; break; }   /* :205-208 */
+    }
+  }
+  err[j] = e ? FD_PRECOMPILE_HIP_INSTR_ERR_CUSTOM_ERR : FD_PRECOMPILE_HIP_INSTR_SUCCESS;
+  custom[j] = e;
+}
+
+struct fd_precompile_hip {
+  fd_ed25519_hip_ctx_t * ctx;
+  ulong   max_instr, rcap;
+  u8 *    d_cnt; u32 * d_early; u32 * d_first; u32 * d_counter;
+  u8 *    d_rsig; u8 * d_rpub; u32 * d_rmoff; u32 * d_rmsz; u8 * d_rpre; signed char * d_rcode;
+  hipEvent_t ev_last; int ev_used;
+};
+
+extern "C" fd_precompile_hip_t *
+fd_precompile_hip_new( fd_ed25519_hip_ctx_t * ctx, ulong max_instr ) {
+  if( !ctx || !max_instr ) return 0;
+  TX_CHECK( hipSetDevice( fd_ed25519_hip_ctx_device( ctx ) ) );
+  fd_precompile_hip_t * p = (fd_precompile_hip_t *)calloc( 1, sizeof(fd_precompile_hip_t) );
+  ulong n = max_instr, rc = (ulong)FD_PRECOMPILE_HIP_SIG_MAX * max_instr;
+  p->ctx = ctx; p->max_instr = n; p->rcap = rc;
+  TX_CHECK( hipMalloc( &p->d_cnt, n ) );      TX_CHECK( hipMalloc( &p->d_early, 4*n ) );
+  TX_CHECK( hipMalloc( &p->d_first, 4*n ) );  TX_CHECK( hipMalloc( &p->d_counter, 4 ) );
+  TX_CHECK( hipMalloc( &p->d_rsig, 64*rc ) ); TX_CHECK( hipMalloc( &p->d_rpub, 32*rc ) );
+  TX_CHECK( hipMalloc( &p->d_rmoff, 4*rc ) ); TX_CHECK( hipMalloc( &p->d_rmsz, 4*rc ) );
+  TX_CHECK( hipMalloc( &p->d_rpre, rc ) );    TX_CHECK( hipMalloc( &p->d_rcode, rc ) );
+  TX_CHECK( hipEventCreateWithFlags( &p->ev_last, hipEventDisableTiming ) );
+  return p;
+}
+
+extern "C" void
+fd_precompile_hip_delete( fd_precompile_hip_t * p ) {
+  if( !p ) return;
+  (void)hipSetDevice( fd_ed25519_hip_ctx_device( p->ctx ) );
+  (void)hipStreamSynchronize( (hipStream_t)fd_ed25519_hip_ctx_stream( p->ctx ) );
+  if( p->ev_used ) (void)hipEventSynchronize( p->ev_last );
+  (void)hipEventDestroy( p->ev_last );
+  (void)hipFree( p->d_cnt ); (void)hipFree( p->d_early ); (void)hipFree( p->d_first ); (void)hipFree( p->d_counter );
+  (void)hipFree( p->d_rsig ); (void)hipFree( p->d_rpub ); (void)hipFree( p->d_rmoff ); (void)hipFree( p->d_rmsz );
+  (void)hipFree( p->d_rpre ); (void)hipFree( p->d_rcode );
+  free( p );
+}
+
+extern "C" int
+fd_precompile_hip_ed25519_verify_dev( fd_precompile_hip_t * p, ulong n, uchar const * d_pool,
+                                      fd_precompile_hip_desc_t const * d_desc,
+                                      fd_precompile_hip_instr_t const * d_instr_tab, int * d_err,
+                                      uint * d_custom_err, void * stream ) {
+  if( n > p->max_instr ) return -1;
+  if( !n ) return 0;
+  hipStream_t st = stream ? (hipStream_t)stream : (hipStream_t)fd_ed25519_hip_ctx_stream( p->ctx );
+  TX_CHECK( hipSetDevice( fd_ed25519_hip_ctx_device( p->ctx ) ) );
+  dim3 grid( (unsigned)((n + 255)/256) ), blk( 256 );
+  if( p->ev_used ) TX_CHECK( hipStreamWaitEvent( st, p->ev_last, 0 ) );
+  hipLaunchKernelGGL( k_pc_count, grid, blk, 0, st, n, d_pool, d_desc, p->d_cnt, p->d_early );
+  TX_CHECK( hipGetLastError() );
+  TX_CHECK( hipMemsetAsync( p->d_counter, 0, 4, st ) );
+  hipLaunchKernelGGL( k_pc_expand, grid, blk, 0, st, n, d_pool, d_desc, d_instr_tab, p->d_cnt, p->d_early,
+                      p->d_counter, p->d_first, p->d_rsig, p->d_rpub, p->d_rmoff, p->d_rmsz, p->d_rpre, p->rcap );
+  TX_CHECK( hipGetLastError() );
+  fd_ed25519_hip_verify_dev_count( p->ctx, p->rcap < (ulong)FD_PRECOMPILE_HIP_SIG_MAX*n ? p->rcap
+                                                                                           : (ulong)FD_PRECOMPILE_HIP_SIG_MAX*n,
+                                   p->d_counter, p->d_rsig, p->d_rpub, d_pool, p->d_rmoff, p->d_rmsz, p->d_rcode, NULL,
+                                   st );
+  hipLaunchKernelGGL( k_pc_reduce, grid, blk, 0, st, n, p->d_cnt, p->d_first, p->d_early, p->d_rpre, p->d_rcode,
+                      d_err, d_custom_err );
+  TX_CHECK( hipGetLastError() );
+  TX_CHECK( hipEventRecord( p->ev_last, st ) );
+  p->ev_used = 1;
+  return 0;
+}

@@ -9,6 +9,11 @@ Reference interfaces mirrored:
                            per txn by the exec tile (fd_exec_tile.c:161)
   FEC-set root check       src/disco/shred/fd_fec_resolver.c:476
                            (fd_ed25519_verify of a 32-B Merkle root)
+  fd_precompile_ed25519_verify
+                           src/flamenco/runtime/program/fd_precompiles.c:114-211
+                           (ed25519 program instructions: offset records naming
+                           signature / pubkey / message spans, possibly in
+                           other instructions of the txn)
 
 Both take whole batches (a block's transactions, a poll's FEC sets) in device
 memory.  There is no CPU fallback.
@@ -24,7 +29,23 @@ FD_RUNTIME_TXN_ERR_SIGNATURE_FAILURE = -13
 
 # Every symbol include/fd_replay_hip.h declares (checked by tests/test_abi.py).
 EXPORTS = ("fd_replay_hip_new", "fd_replay_hip_delete", "fd_replay_hip_txn_verify_dev",
-           "fd_fec_hip_verify_roots_dev")
+           "fd_fec_hip_verify_roots_dev", "fd_precompile_hip_new", "fd_precompile_hip_delete",
+           "fd_precompile_hip_ed25519_verify_dev")
+
+# fd_executor_err.h:14,40 and fd_precompiles.h:16-18
+FD_EXECUTOR_INSTR_SUCCESS = 0
+FD_EXECUTOR_INSTR_ERR_CUSTOM_ERR = -26
+FD_EXECUTOR_PRECOMPILE_ERR_SIGNATURE = 2
+FD_EXECUTOR_PRECOMPILE_ERR_DATA_OFFSET = 3
+FD_EXECUTOR_PRECOMPILE_ERR_INSTR_DATA_SIZE = 4
+PRECOMPILE_SIG_MAX = 87
+PRECOMPILE_DATA_MAX = 1232
+
+# fd_precompile_hip_desc_t / fd_precompile_hip_instr_t (include/fd_replay_hip.h)
+PC_DESC_DTYPE = np.dtype([("data_off", "<u4"), ("data_sz", "<u2"), ("instr_cnt", "<u2"), ("instr_base", "<u4"),
+                          ("_pad", "<u4")])
+PC_INSTR_DTYPE = np.dtype([("data_off", "<u4"), ("data_sz", "<u4")])
+assert PC_DESC_DTYPE.itemsize == 16 and PC_INSTR_DTYPE.itemsize == 8
 
 # fd_txn_hip_desc_t (16 bytes): the fd_txn_p_t payload span and the fd_txn_t
 # fields fd_executor_txn_verify reads (fd_txn.h:186-249)
@@ -49,6 +70,11 @@ def lib():
         L.fd_replay_hip_txn_verify_dev.argtypes = [vp, u64, vp, vp, vp, vp]
         L.fd_fec_hip_verify_roots_dev.restype = c.c_int
         L.fd_fec_hip_verify_roots_dev.argtypes = [vp, u64, vp, vp, vp, vp, vp]
+        L.fd_precompile_hip_new.restype = vp
+        L.fd_precompile_hip_new.argtypes = [vp, u64]
+        L.fd_precompile_hip_delete.argtypes = [vp]
+        L.fd_precompile_hip_ed25519_verify_dev.restype = c.c_int
+        L.fd_precompile_hip_ed25519_verify_dev.argtypes = [vp, u64, vp, vp, vp, vp, vp, vp]
         _bound = True
     return L
 
@@ -107,3 +133,40 @@ def fec_verify_roots_dev(verifier, n, roots, sigs, pubs, codes, stream=None):
             _ptr(sigs, 64 * n, "sigs", dev), _ptr(pubs, 32 * n, "pubs", dev), _ptr(codes, n, "codes", dev))
     with verifier._stream(stream) as h:
         return lib().fd_fec_hip_verify_roots_dev(*args, h)
+
+
+class PrecompileVerifier:
+    """fd_precompile_ed25519_verify over batches of up to max_instr ed25519
+    program instructions (fd_precompile_hip_ed25519_verify_dev)."""
+
+    def __init__(self, verifier, max_instr):
+        self._lib = lib()
+        self.verifier = verifier
+        self.p = self._lib.fd_precompile_hip_new(verifier.ctx, int(max_instr))
+        if not self.p:
+            raise RuntimeError("fd_precompile_hip_new failed")
+        self.max_instr = int(max_instr)
+
+    def ed25519_verify_dev(self, n, pool, desc, instr_tab, err, custom_err, stream=None):
+        """pool: device bytes (readable 16 bytes past the last span); desc:
+        device PC_DESC_DTYPE[n]; instr_tab: device PC_INSTR_DTYPE[...];
+        err: device int32[n]; custom_err: device uint32[n]."""
+        n, dev = int(n), self.verifier.device
+        args = (self.p, n, _ptr(pool, 1, "pool", dev), _ptr(desc, 16 * n, "desc", dev),
+                _ptr(instr_tab, 8, "instr_tab", dev), _ptr(err, 4 * n, "err", dev),
+                _ptr(custom_err, 4 * n, "custom_err", dev))
+        with self.verifier._stream(stream) as h:
+            rc = self._lib.fd_precompile_hip_ed25519_verify_dev(*args, h)
+        if rc:
+            raise ValueError(f"fd_precompile_hip_ed25519_verify_dev: n={n} > max_instr={self.max_instr}")
+
+    def close(self):
+        if self.p:
+            self._lib.fd_precompile_hip_delete(self.p)
+            self.p = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

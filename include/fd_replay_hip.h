@@ -15,6 +15,12 @@
      shred    FEC-set root check      src/disco/shred/fd_fec_resolver.c:476
               fd_ed25519_verify( root, 32, shred->signature, leader_pubkey ):
               the resolver rejects the set on anything but FD_ED25519_SUCCESS.
+     precompile  ed25519 program      src/flamenco/runtime/program/
+              instructions            fd_precompiles.c:114-211
+              fd_precompile_ed25519_verify, run by the executor for every
+              instruction addressed to the ed25519 program: signature /
+              pubkey / message spans named by 14-byte offset records, possibly
+              inside other instructions of the same transaction.
 
    Replay hands the engine every transaction of a block (or of a batch of
    exec-tile tasks) at once instead of one fd_executor_txn_verify call per
@@ -88,6 +94,67 @@ fd_fec_hip_verify_roots_dev( fd_ed25519_hip_ctx_t * ctx,
                              uchar const *          d_pubs,
                              signed char *          d_codes,
                              void *                 stream );
+
+/* ---- ed25519 program (precompile) instructions -----------------------------
+
+   fd_precompile_ed25519_verify (fd_precompiles.c:114-211, data fetch
+   fd_precompile_get_instr_data :76-107) for n instructions at once, e.g.
+   every ed25519-program instruction of a block.  Instruction j is described
+   by d_desc[j]; the data of every instruction of its transaction (for
+   offset records that name another instruction by index) by the table
+   entries d_instr_tab[ instr_base, instr_base + instr_cnt ).  All data
+   spans live in d_pool (e.g. the block's txn payloads), readable 16 bytes
+   past the last one. */
+
+/* fd_executor_err.h:14,40 and fd_precompiles.h:16-18 */
+#define FD_PRECOMPILE_HIP_INSTR_SUCCESS          (  0)
+#define FD_PRECOMPILE_HIP_INSTR_ERR_CUSTOM_ERR   (-26)
+#define FD_PRECOMPILE_HIP_ERR_SIGNATURE          (  2)
+#define FD_PRECOMPILE_HIP_ERR_DATA_OFFSET        (  3)
+#define FD_PRECOMPILE_HIP_ERR_INSTR_DATA_SIZE    (  4)
+/* a descriptor the reference cannot produce (data_sz above the 1232-byte
+   transaction MTU, fd_txn.h:65): d_err -1, d_custom_err 0xFFFFFFFF */
+#define FD_PRECOMPILE_HIP_ERR_DESC               ( -1)
+#define FD_PRECOMPILE_HIP_DATA_MAX               (1232)
+/* signatures one instruction can name: (1232 - 2) / 14 */
+#define FD_PRECOMPILE_HIP_SIG_MAX                (  87)
+
+typedef struct {
+  uint   data_off;        /* this instruction's data: d_pool[ data_off, +data_sz )  */
+  ushort data_sz;         /* fd_instr_info_t.data_sz                                 */
+  ushort instr_cnt;       /* TXN( txn )->instr_cnt                                   */
+  uint   instr_base;      /* its transaction's first entry in d_instr_tab            */
+  uint   _pad;
+} fd_precompile_hip_desc_t;   /* 16 bytes */
+
+typedef struct {
+  uint data_off;          /* instruction k of the transaction: d_pool[ data_off, +data_sz ) */
+  uint data_sz;
+} fd_precompile_hip_instr_t;  /* 8 bytes */
+
+typedef struct fd_precompile_hip fd_precompile_hip_t;
+
+/* device scratch for up to max_instr instructions per call (and their
+   FD_PRECOMPILE_HIP_SIG_MAX signatures each) on ctx's device */
+fd_precompile_hip_t * fd_precompile_hip_new   ( fd_ed25519_hip_ctx_t * ctx, ulong max_instr );
+void                  fd_precompile_hip_delete( fd_precompile_hip_t * pc );
+
+/* d_err[j] = the reference's return for instruction j
+   (FD_PRECOMPILE_HIP_INSTR_SUCCESS or _INSTR_ERR_CUSTOM_ERR) and
+   d_custom_err[j] the txn_out->err.custom_err it sets (0 on success): the
+   first failing signature in offset-record order decides, its span checks
+   (signature, public key, message) before its verify.  Device pointers,
+   asynchronous on stream (NULL: ctx's stream).  Returns 0, or -1 if
+   n > max_instr. */
+int
+fd_precompile_hip_ed25519_verify_dev( fd_precompile_hip_t *             pc,
+                                      ulong                             n,
+                                      uchar const *                     d_pool,
+                                      fd_precompile_hip_desc_t const *  d_desc,
+                                      fd_precompile_hip_instr_t const * d_instr_tab,
+                                      int *                             d_err,
+                                      uint *                            d_custom_err,
+                                      void *                            stream );
 
 #ifdef __cplusplus
 }
