@@ -88,7 +88,24 @@
    after the two B tables (128-B aligned), hot in cache, never written per
    signature */
 #define IDENT_OFF   ((2*BTAB_WORDS + 31) & ~31)
+/* FD_BTAB_W12: k_verify_dsm takes the [k2*S mod L]B term in signed radix
+   2^12 (11 + 11 digits against [0..2048]B and [0..2048](2^132 B), 22 affine
+   additions) from global tables that stay resident in each XCD's L2 (2 x 2049
+   entries of one 128-B line, 525 KB), instead of radix 2^8 (16 + 16 digits,
+   32 additions) from the two 129-entry LDS tables.  A/B on one box
+   (profiles/r02r_ab_w12): k_verify_dsm 6.59-6.62 vs 6.79-6.87 ms, C2
+   128.7-129.4 vs 126.3-126.4 M verifies/s. */
+#ifndef FD_BTAB_W12
+#define FD_BTAB_W12 1
+#endif
+#define BT12_N      2049           /* 0..2048 multiples */
+#define BT12_ENT    32             /* YmX, YpX, T2d: 9 limbs each + pad to one 128-B line */
+#define BT12_OFF    ((IDENT_OFF + ATAB_ENT + 31) & ~31)
+#if FD_BTAB_W12
+#define BTAB_ALLOC  (BT12_OFF + 2*BT12_N*BT12_ENT)
+#else
 #define BTAB_ALLOC  (IDENT_OFF + ATAB_ENT)
+#endif
 
 /* state record: 32 u32 words per field group, laid out SoA per chunk for
    coalescing: word w of signature i lives at st[ w*chunk + i ]. */
@@ -195,6 +212,31 @@ __global__ __launch_bounds__(64) void k_btab_init( u32 * btab ) {
     store_cached( btab + IDENT_OFF, c );
   }
 }
+
+#if FD_BTAB_W12
+/* [j]B and [j](2^132 B) for j in [0,2048], 1/2-scaled affine cached, one
+   128-B line each at BT12_OFF */
+__global__ __launch_bounds__(64) void k_btab12_init( u32 * btab ) {
+  int j = blockIdx.x * blockDim.x + threadIdx.x;
+  if( j >= 2*BT12_N ) return;
+  u32 * e = btab + BT12_OFF + j*BT12_ENT;
+  ge_p3 B, P; ge_base( B ); ge_identity( P );
+  if( j >= BT12_N ) {
+    j -= BT12_N;
+    for( int q=0; q<132; q++ ) ge_dbl( B, B, true );
+  }
+  ge_cached Bc; ge_to_cached( Bc, B );
+  for( int bit=11; bit>=0; bit-- ) {
+    ge_dbl( P, P, true );
+    if( (j >> bit) & 1 ) ge_add_cached( P, P, Bc, 0u, true );
+  }
+  ge_affc a; ge_to_affc_half( a, P );
+  #pragma unroll
+  for( int i=0; i<9; i++ ) { e[i] = a.YmX.v[i]; e[9+i] = a.YpX.v[i]; e[18+i] = a.T2d.v[i]; }
+  #pragma unroll
+  for( int i=27; i<32; i++ ) e[i] = 0u;
+}
+#endif
 
 DEV int code_of( u32 f, int errmode, bool eq ) {
   if( errmode == FD_ED25519_HIP_ERRMODE_AVX512 ) {
@@ -619,7 +661,11 @@ DEV void dsm_verify_slot( ulong t, ulong chunk, u32 const * __restrict__ st, u32
     /* ---- half-size scalars (sc_halfsize): the reference's check
        [S]B - [k]A == R (user.c:216-226) becomes
        [k2*S mod L]B - [k1]A - [k2]R == O with k1, k2 ~ 2^128 ---- */
+#if FD_BTAB_W12
+    u32 kd1[8], kd2[8], bl[5], bh[5], bmask, k1neg, D;
+#else
     u32 kd1[8], kd2[8], sd[8], k1neg, D;
+#endif
     {
       u32 k[8], S[8], k1[8], k2[8], sp[8];
       #pragma unroll
@@ -633,7 +679,34 @@ DEV void dsm_verify_slot( ulong t, ulong chunk, u32 const * __restrict__ st, u32
       }
       sc_mul( sp, k2, S );
       sc_recode16s( kd1, k1 ); sc_recode16s( kd2, k2 );
+#if FD_BTAB_W12
+      /* signed radix-2^12 digits of sp (< 2^253): digit i = r_i + c_i -
+         4096 c_{i+1}, r_i = bits [12i, 12i+12), carry bits c in bmask;
+         digits 0..10 against [j]B, 11..21 against [j](2^132 B).  Both halves
+         are held as 160-bit groups whose top 12 bits are the next digit
+         (consumed top-down): bl = sp << 28 (bits 0..131), bh = sp >> 104
+         (bits 132..263 on top; the 28 bits below are never read). */
+      {
+        u32 c = 0u; bmask = 0u;
+        #pragma unroll
+        for( int i=0; i<22; i++ ) {
+          int b = 12*i, wi = b >> 5, sh = b & 31;
+          u32 x = (sh + 12 <= 32) ? (sp[wi] >> sh)
+                                  : __builtin_amdgcn_alignbit( wi < 7 ? sp[wi+1] : 0u, sp[wi], (u32)sh );
+          u32 d = (x & 0xfffu) + c;
+          c = d >= 2048u ? 1u : 0u;
+          bmask |= c << (i+1);
+        }
+        bl[0] = sp[0] << 28;
+        #pragma unroll
+        for( int q=1; q<5; q++ ) bl[q] = __builtin_amdgcn_alignbit( sp[q], sp[q-1], 4u );
+        #pragma unroll
+        for( int q=0; q<4; q++ ) bh[q] = __builtin_amdgcn_alignbit( sp[q+4], sp[q+3], 8u );
+        bh[4] = sp[7] >> 8;
+      }
+#else
       sc_recode256( sd, sp );       /* digits 0..15: B; 16..31: 2^128 B (second LDS table) */
+#endif
       D = max( (bits >> 2) + 1u, 31u );   /* windows; >= 31 so all 16 B digit pairs are reached */
     }
     D = wave_max7( D );             /* one window count per wave: no divergence in the loop */
@@ -675,6 +748,31 @@ DEV void dsm_verify_slot( ulong t, ulong chunk, u32 const * __restrict__ st, u32
       }
       ge_add_cached( P, P, e, nega, true );
       load_cached( e, tab_entry( tabR, ident, ir ) );
+#if FD_BTAB_W12
+      bool bw = w <= 30 && w % 3 == 0;                  /* windows 30, 27, .., 0: digits 10..0 (+11) */
+      ge_add_cached( P, P, e, negr, bw );
+      if( bw ) {
+        u32 bi = (u32)w / 3u;
+        u32 negb, ib, negc, ic;
+        {
+          int v = (int)((bl[4] >> 20) + ((bmask >> bi) & 1u)) - (int)(((bmask >> (bi+1u)) & 1u) << 12);
+          negb = (u32)(v >> 31); ib = ((u32)v ^ negb) - negb;
+          v = (int)((bh[4] >> 20) + ((bmask >> (bi+11u)) & 1u)) - (int)(((bmask >> (bi+12u)) & 1u) << 12);
+          negc = (u32)(v >> 31); ic = ((u32)v ^ negc) - negc;
+        }
+        #pragma unroll
+        for( int q=4; q>0; q-- ) {
+          bl[q] = __builtin_amdgcn_alignbit( bl[q], bl[q-1], 20u );
+          bh[q] = __builtin_amdgcn_alignbit( bh[q], bh[q-1], 20u );
+        }
+        bl[0] <<= 12; bh[0] <<= 12;
+        u32 const * bt = btab + BT12_OFF;
+        ge_affc b; load_affc( b, bt + ib*BT12_ENT );
+        ge_add_affc( P, P, b, negb, true );
+        load_affc( b, bt + (BT12_N + ic)*BT12_ENT );
+        ge_add_affc( P, P, b, negc, false );
+      }
+#else
       bool bw = (w & 1) == 0 && w <= 30;
       ge_add_cached( P, P, e, negr, bw );
       if( bw ) {
@@ -686,6 +784,7 @@ DEV void dsm_verify_slot( ulong t, ulong chunk, u32 const * __restrict__ st, u32
         load_affc( b, lds_btab + BTAB_WORDS + ic*BTAB_STRIDE );
         ge_add_affc( P, P, b, negc, false );
       }
+#endif
     }
 
     /* ---- P == O: X == 0 and Y == Z (Z != 0: complete formulas) ---- */
@@ -708,6 +807,9 @@ void k_verify_dsm( ulong chunk, u32 const * __restrict__ st, u32 const * __restr
                    signed char * __restrict__ codes, int halfsize ) {
   u32 m = count[0];
   if( (ulong)blockIdx.x * blockDim.x >= m ) return;        /* whole workgroup past the survivors */
+#if FD_BTAB_W12
+  u32 const * lds_btab = 0;                                /* B tables from global memory (L2) */
+#else
   __shared__ __attribute__((aligned(16))) u32 lds_btab[2*BTAB_WORDS];
   {
     /* 28.9 KB: all of a thread's 16-B loads in flight before the LDS stores
@@ -725,6 +827,7 @@ void k_verify_dsm( ulong chunk, u32 const * __restrict__ st, u32 const * __restr
     if( has_last ) ((uint4 *)lds_btab)[threadIdx.x + 256*FULL] = last;
   }
   __syncthreads();
+#endif
 #if FD_DSM_PERSIST
   for( ;; ) {
     u32 task = 0u;
@@ -884,6 +987,10 @@ fd_ed25519_hip_ctx_new( int device, ulong chunk_sigs ) {
   }
   hipLaunchKernelGGL( k_btab_init, dim3( (2*BTAB_N + 63)/64 ), dim3( 64 ), 0, ctx->stream, ctx->d_btab );
   FD_CHECK( hipGetLastError() );
+#if FD_BTAB_W12
+  hipLaunchKernelGGL( k_btab12_init, dim3( (2*BT12_N + 63)/64 ), dim3( 64 ), 0, ctx->stream, ctx->d_btab );
+  FD_CHECK( hipGetLastError() );
+#endif
   FD_CHECK( hipStreamSynchronize( ctx->stream ) );
   return ctx;
 }
