@@ -98,7 +98,24 @@
 #ifndef FD_BTAB_W12
 #define FD_BTAB_W12 1
 #endif
-#define BT12_N      2049           /* 0..2048 multiples */
+/* FD_BTAB_GW: bits per digit of those global tables, 12 (default) or 16
+   (8 + 8 digits, [0..32768] multiples, 8.4 MB: past L2, served by MALL).
+   A/B (profiles/r02r_ab_gw16): 16 gives k_verify_dsm 6.42-6.49 vs 6.57-6.61
+   ms and C2 130.4 vs 129.5 M verifies/s, for ~1.9 GB more fabric reads per
+   2^20-signature launch; 12 stays the default (traffic, 16x smaller table). */
+#ifndef FD_BTAB_GW
+#define FD_BTAB_GW 12
+#endif
+#if FD_BTAB_GW == 12
+#define BTG_ND      11             /* digits per half */
+#elif FD_BTAB_GW == 16
+#define BTG_ND      8
+#else
+#error "FD_BTAB_GW must be 12 or 16"
+#endif
+#define BTG_HB      (BTG_ND*FD_BTAB_GW)        /* the high table holds multiples of 2^BTG_HB B */
+#define BTG_STEP    (FD_BTAB_GW/4)             /* radix-16 windows between B additions */
+#define BT12_N      ((1 << (FD_BTAB_GW-1)) + 1)
 #define BT12_ENT    32             /* YmX, YpX, T2d: 9 limbs each + pad to one 128-B line */
 #define BT12_OFF    ((IDENT_OFF + ATAB_ENT + 31) & ~31)
 #if FD_BTAB_W12
@@ -223,10 +240,10 @@ __global__ __launch_bounds__(64) void k_btab12_init( u32 * btab ) {
   ge_p3 B, P; ge_base( B ); ge_identity( P );
   if( j >= BT12_N ) {
     j -= BT12_N;
-    for( int q=0; q<132; q++ ) ge_dbl( B, B, true );
+    for( int q=0; q<BTG_HB; q++ ) ge_dbl( B, B, true );
   }
   ge_cached Bc; ge_to_cached( Bc, B );
-  for( int bit=11; bit>=0; bit-- ) {
+  for( int bit=FD_BTAB_GW-1; bit>=0; bit-- ) {
     ge_dbl( P, P, true );
     if( (j >> bit) & 1 ) ge_add_cached( P, P, Bc, 0u, true );
   }
@@ -687,22 +704,31 @@ DEV void dsm_verify_slot( ulong t, ulong chunk, u32 const * __restrict__ st, u32
          (consumed top-down): bl = sp << 28 (bits 0..131), bh = sp >> 104
          (bits 132..263 on top; the 28 bits below are never read). */
       {
+        constexpr int GW = FD_BTAB_GW, ND = BTG_ND, HB = BTG_HB;
         u32 c = 0u; bmask = 0u;
         #pragma unroll
-        for( int i=0; i<22; i++ ) {
-          int b = 12*i, wi = b >> 5, sh = b & 31;
-          u32 x = (sh + 12 <= 32) ? (sp[wi] >> sh)
+        for( int i=0; i<2*ND; i++ ) {
+          int b = GW*i, wi = b >> 5, sh = b & 31;
+          u32 x = (sh + GW <= 32) ? (sp[wi] >> sh)
                                   : __builtin_amdgcn_alignbit( wi < 7 ? sp[wi+1] : 0u, sp[wi], (u32)sh );
-          u32 d = (x & 0xfffu) + c;
-          c = d >= 2048u ? 1u : 0u;
+          u32 d = (x & ((1u << GW) - 1u)) + c;
+          c = d >= (1u << (GW-1)) ? 1u : 0u;
           bmask |= c << (i+1);
         }
-        bl[0] = sp[0] << 28;
+        /* lo = (sp mod 2^HB) << (160-HB): sp bit HB would land at group bit 160,
+           so nothing above the low half enters; hi = sp >> (2HB-160): its top
+           ND*GW bits are sp's bits from HB up (the bits below are never read) */
+        constexpr int LS = 160 - HB, HS = 2*HB - 160;
         #pragma unroll
-        for( int q=1; q<5; q++ ) bl[q] = __builtin_amdgcn_alignbit( sp[q], sp[q-1], 4u );
-        #pragma unroll
-        for( int q=0; q<4; q++ ) bh[q] = __builtin_amdgcn_alignbit( sp[q+4], sp[q+3], 8u );
-        bh[4] = sp[7] >> 8;
+        for( int q=0; q<5; q++ ) {
+          int b = 32*q - LS;                           /* sp bit at the group word's bit 0 */
+          u32 lo_w = b + 32 <= 0 ? 0u : b < 0 ? (sp[0] << (-b)) :
+                     (b & 31) ? __builtin_amdgcn_alignbit( sp[(b>>5)+1], sp[b>>5], (u32)(b & 31) ) : sp[b>>5];
+          bl[q] = lo_w;
+          int hb = 32*q + HS, hw = hb >> 5, hsh = hb & 31;
+          u32 hx = hw + 1 <= 7 ? sp[hw+1] : 0u, hy = hw <= 7 ? sp[hw] : 0u;
+          bh[q] = hsh ? __builtin_amdgcn_alignbit( hx, hy, (u32)hsh ) : hy;
+        }
       }
 #else
       sc_recode256( sd, sp );       /* digits 0..15: B; 16..31: 2^128 B (second LDS table) */
@@ -749,23 +775,25 @@ DEV void dsm_verify_slot( ulong t, ulong chunk, u32 const * __restrict__ st, u32
       ge_add_cached( P, P, e, nega, true );
       load_cached( e, tab_entry( tabR, ident, ir ) );
 #if FD_BTAB_W12
-      bool bw = w <= 30 && w % 3 == 0;                  /* windows 30, 27, .., 0: digits 10..0 (+11) */
+      /* windows (ND-1)*STEP, .., STEP, 0: lo digits ND-1..0, hi digits 2ND-1..ND */
+      bool bw = w <= (BTG_ND-1)*BTG_STEP && w % BTG_STEP == 0;
       ge_add_cached( P, P, e, negr, bw );
       if( bw ) {
-        u32 bi = (u32)w / 3u;
+        constexpr u32 GW = FD_BTAB_GW, ND = BTG_ND;
+        u32 bi = (u32)w / (u32)BTG_STEP;
         u32 negb, ib, negc, ic;
         {
-          int v = (int)((bl[4] >> 20) + ((bmask >> bi) & 1u)) - (int)(((bmask >> (bi+1u)) & 1u) << 12);
+          int v = (int)((bl[4] >> (32u-GW)) + ((bmask >> bi) & 1u)) - (int)(((bmask >> (bi+1u)) & 1u) << GW);
           negb = (u32)(v >> 31); ib = ((u32)v ^ negb) - negb;
-          v = (int)((bh[4] >> 20) + ((bmask >> (bi+11u)) & 1u)) - (int)(((bmask >> (bi+12u)) & 1u) << 12);
+          v = (int)((bh[4] >> (32u-GW)) + ((bmask >> (bi+ND)) & 1u)) - (int)(((bmask >> (bi+ND+1u)) & 1u) << GW);
           negc = (u32)(v >> 31); ic = ((u32)v ^ negc) - negc;
         }
         #pragma unroll
         for( int q=4; q>0; q-- ) {
-          bl[q] = __builtin_amdgcn_alignbit( bl[q], bl[q-1], 20u );
-          bh[q] = __builtin_amdgcn_alignbit( bh[q], bh[q-1], 20u );
+          bl[q] = __builtin_amdgcn_alignbit( bl[q], bl[q-1], 32u-GW );
+          bh[q] = __builtin_amdgcn_alignbit( bh[q], bh[q-1], 32u-GW );
         }
-        bl[0] <<= 12; bh[0] <<= 12;
+        bl[0] <<= GW; bh[0] <<= GW;
         u32 const * bt = btab + BT12_OFF;
         ge_affc b; load_affc( b, bt + ib*BT12_ENT );
         ge_add_affc( P, P, b, negb, true );
