@@ -783,7 +783,40 @@ DEV u32 sc_halfsize( u32 k1[8], u32 & k1neg, u32 k2[8], u32 const k[8] ) {
 /**********************************************************************/
 /* SHA-512 (fd_sha512.c:264-399 semantics), one message per lane.      */
 
+/* 64-bit rotate / shift / 3-input logic on the 32-bit ALU, spelled out: the
+   compiler lowers (x >> n) | (x << (64-n)) to two 64-bit shifts and two ORs,
+   where a rotate is two v_alignbit_b32; and x ^ y ^ z to two XORs per half,
+   where gfx950's v_bitop3_b32 takes any 3-input function in one */
+DEV u32 lo32( u64 x ) { return (u32)x; }
+DEV u32 hi32( u64 x ) { return (u32)(x >> 32); }
+DEV u64 mk64( u32 lo, u32 hi ) { return ((u64)hi << 32) | (u64)lo; }
+#ifndef FD_SHA_ALIGNBIT
+#define FD_SHA_ALIGNBIT 1
+#endif
+#if !FD_SHA_ALIGNBIT                            /* the plain C forms, for A/B runs */
 DEV u64 ror64( u64 x, int n ) { return (x >> n) | (x << (64 - n)); }
+DEV u64 shr64( u64 x, int n ) { return x >> n; }
+DEV u64 xor3_64( u64 a, u64 b, u64 c ) { return a ^ b ^ c; }
+DEV u64 maj64( u64 a, u64 b, u64 c ) { return (a & b) ^ (a & c) ^ (b & c); }
+#else
+DEV u64 ror64( u64 x, int n ) {                 /* n a compile-time constant in (0, 64) */
+  u32 lo = lo32( x ), hi = hi32( x );
+  if( n >= 32 ) { u32 t = lo; lo = hi; hi = t; n -= 32; }
+  if( n == 0 ) return mk64( lo, hi );
+  return mk64( __builtin_amdgcn_alignbit( hi, lo, (u32)n ), __builtin_amdgcn_alignbit( lo, hi, (u32)n ) );
+}
+DEV u64 shr64( u64 x, int n ) {                 /* n a compile-time constant in (0, 32) */
+  return mk64( __builtin_amdgcn_alignbit( hi32( x ), lo32( x ), (u32)n ), hi32( x ) >> n );
+}
+DEV u64 xor3_64( u64 a, u64 b, u64 c ) {
+  return mk64( __builtin_amdgcn_bitop3_b32( lo32( a ), lo32( b ), lo32( c ), 0x96 ),
+               __builtin_amdgcn_bitop3_b32( hi32( a ), hi32( b ), hi32( c ), 0x96 ) );
+}
+DEV u64 maj64( u64 a, u64 b, u64 c ) {          /* majority: (a&b) ^ (a&c) ^ (b&c) */
+  return mk64( __builtin_amdgcn_bitop3_b32( lo32( a ), lo32( b ), lo32( c ), 0xe8 ),
+               __builtin_amdgcn_bitop3_b32( hi32( a ), hi32( b ), hi32( c ), 0xe8 ) );
+}
+#endif
 
 /* round constants in constant memory: the round index is wave-uniform, so
    each K[t] is a scalar load rather than 160 VGPRs of hoisted literals */
@@ -810,11 +843,11 @@ __constant__ u64 SHA512_K[80] = {
     0x4cc5d4becb3e42b6ULL,0x597f299cfc657e2aULL,0x5fcb6fab3ad6faecULL,0x6c44198c4a475817ULL };
 
 DEV void sha512_round( u64 & a, u64 & b, u64 & c, u64 & d, u64 & e, u64 & f, u64 & g, u64 & h, u64 w, u64 k ) {
-  u64 S1 = ror64( e, 14 ) ^ ror64( e, 18 ) ^ ror64( e, 41 );
+  u64 S1 = xor3_64( ror64( e, 14 ), ror64( e, 18 ), ror64( e, 41 ) );
   u64 ch = (e & f) ^ (~e & g);
   u64 t1 = h + S1 + ch + k + w;
-  u64 S0 = ror64( a, 28 ) ^ ror64( a, 34 ) ^ ror64( a, 39 );
-  u64 mj = (a & b) ^ (a & c) ^ (b & c);
+  u64 S0 = xor3_64( ror64( a, 28 ), ror64( a, 34 ), ror64( a, 39 ) );
+  u64 mj = maj64( a, b, c );
   d += t1; h = t1 + S0 + mj;
 }
 
@@ -828,8 +861,8 @@ DEV void sha512_block( u64 st[8], u64 W[16] ) {
     for( int j=0; j<16; j++ ) {
       if( t0 ) {
         u64 w15 = W[(j+1)&15], w2 = W[(j+14)&15];
-        u64 s0 = ror64( w15, 1 ) ^ ror64( w15, 8 ) ^ (w15 >> 7);
-        u64 s1 = ror64( w2, 19 ) ^ ror64( w2, 61 ) ^ (w2 >> 6);
+        u64 s0 = xor3_64( ror64( w15, 1 ), ror64( w15, 8 ), shr64( w15, 7 ) );
+        u64 s1 = xor3_64( ror64( w2, 19 ), ror64( w2, 61 ), shr64( w2, 6 ) );
         W[j] += s0 + W[(j+9)&15] + s1;
       }
       u64 k = SHA512_K[t0+j];
