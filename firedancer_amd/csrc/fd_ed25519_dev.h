@@ -789,7 +789,8 @@ DEV u32 sc_halfsize( u32 k1[8], u32 & k1neg, u32 k2[8], u32 const k[8] ) {
    where gfx950's v_bitop3_b32 takes any 3-input function in one */
 DEV u32 lo32( u64 x ) { return (u32)x; }
 DEV u32 hi32( u64 x ) { return (u32)(x >> 32); }
-DEV u64 mk64( u32 lo, u32 hi ) { return ((u64)hi << 32) | (u64)lo; }
+typedef u32 v2u32 __attribute__((ext_vector_type(2)));
+DEV u64 mk64( u32 lo, u32 hi ) { v2u32 v = { lo, hi }; return __builtin_bit_cast( u64, v ); }
 #ifndef FD_SHA_ALIGNBIT
 #define FD_SHA_ALIGNBIT 1
 #endif
