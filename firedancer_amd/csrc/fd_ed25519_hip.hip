@@ -125,7 +125,17 @@
 #endif
 
 /* state record: 32 u32 words per field group, laid out SoA per chunk for
-   coalescing: word w of signature i lives at st[ w*chunk + i ]. */
+   coalescing: word w of signature i lives at st[ w*chunk + i ].
+   FD_STATE_BY_SLOT: i is k_verify_prep's processing slot t (lane t takes
+   record order[t]), not the record index, and idx[] holds survivor slots.
+   On the txn paths the block-count order scatters records over the chunk:
+   indexed by record, a wave's 48 state stores in prep and 48 loads in
+   k_verify_dsm each touched 64 separate lines.  By slot they are
+   contiguous; the DSM looks up order[slot] once for the code it writes.
+   Batches without an order (order[t] = t) are unchanged. */
+#ifndef FD_STATE_BY_SLOT
+#define FD_STATE_BY_SLOT 1
+#endif
 #define ST_K     0
 #define ST_S     8
 #define ST_AX   16
@@ -350,9 +360,14 @@ DEV void prep_slot( ulong t, ulong n, ulong chunk, uchar const * __restrict__ si
   /* order (k_msg_order): lane t takes record order[t], so a wave's lanes
      hash messages of the same SHA-512 block count */
   ulong i = active ? (order ? (ulong)order[t] : t) : 0ul;
+#if FD_STATE_BY_SLOT
+  ulong const sl = t;                        /* state column and survivor entry: the slot */
+#else
+  ulong const sl = i;
+#endif
   u32 flags = 0u;
   if( active ) {
-  u32 * s = st + i;
+  u32 * s = st + sl;
   /* decode A then R (user.c:165), one at a time: a rolled loop keeps the two
      pow22523 chains from being interleaved into one register-hungry block
      (measured: pairing the two chains instruction by instruction is slower,
@@ -419,7 +434,7 @@ DEV void prep_slot( ulong t, ulong n, ulong chunk, uchar const * __restrict__ si
     sha512_prefixed_coop<64u>( x, pre, pool + mo, ms, lds_msg, lds_meta, threadIdx.x & 63u );   /* user.c:205-206 */
     if( active ) {
       sc_reduce512( k, x );                                                /* user.c:207 */
-      u32 * s = st + i;
+      u32 * s = st + sl;
       #pragma unroll
       for( int w=0; w<8; w++ ) {
         s[(ST_K +w)*chunk] = k[w];
@@ -441,7 +456,7 @@ DEV void prep_slot( ulong t, ulong n, ulong chunk, uchar const * __restrict__ si
   if( lane == 0u && m ) base = atomicAdd( count, (u32)__popcll( m ) );
   base = __shfl( base, 0 );
   u32 below = (u32)__popcll( m & ((1ULL << lane) - 1ULL) );
-  if( pass ) idx[base + below] = (u32)i;
+  if( pass ) idx[base + below] = (u32)sl;
 }
 
 /* FD_PREP_PERSIST: resident workgroups pull 64-record tasks from count[2]
@@ -666,13 +681,19 @@ DEV u32 wave_max7( u32 v ) {
 #define DSM_OCCUPANCY
 #endif
 
-/* one survivor: DSM slot t (tables at slot t), record idx[t] */
+/* one survivor: DSM slot t (tables at slot t), state column idx[t] (prep's
+   slot; record order[idx[t]] under FD_STATE_BY_SLOT, else the record) */
 DEV void dsm_verify_slot( ulong t, ulong chunk, u32 const * __restrict__ st, u32 const * __restrict__ btab,
                           u32 * __restrict__ atab, u32 const * __restrict__ idx, u32 const * lds_btab,
-                          signed char * __restrict__ codes, int halfsize ) {
-  ulong i = idx[t];
+                          signed char * __restrict__ codes, int halfsize, u32 const * __restrict__ order ) {
+  ulong p = idx[t];
+#if FD_STATE_BY_SLOT
+  ulong i = order ? (ulong)order[p] : p;
+#else
+  ulong i = p; (void)order;
+#endif
   ulong ii = t;                                            /* table slot: dense in t */
-  u32 const * s = st + i;
+  u32 const * s = st + p;
   bool eq = false;
   {
     /* ---- half-size scalars (sc_halfsize): the reference's check
@@ -832,7 +853,7 @@ DEV void dsm_verify_slot( ulong t, ulong chunk, u32 const * __restrict__ st, u32
 __global__ __launch_bounds__(256) DSM_OCCUPANCY
 void k_verify_dsm( ulong chunk, u32 const * __restrict__ st, u32 const * __restrict__ btab,
                    u32 * __restrict__ atab, u32 const * __restrict__ idx, u32 * __restrict__ count,
-                   signed char * __restrict__ codes, int halfsize ) {
+                   signed char * __restrict__ codes, int halfsize, u32 const * __restrict__ order ) {
   u32 m = count[0];
   if( (ulong)blockIdx.x * blockDim.x >= m ) return;        /* whole workgroup past the survivors */
 #if FD_BTAB_W12
@@ -863,12 +884,12 @@ void k_verify_dsm( ulong chunk, u32 const * __restrict__ st, u32 const * __restr
     task = __shfl( task, 0 );
     if( (ulong)task * 64ul >= (ulong)m ) break;                       /* wave-uniform exit */
     ulong t = (ulong)task * 64ul + (threadIdx.x & 63u);
-    if( t < m ) dsm_verify_slot( t, chunk, st, btab, atab, idx, lds_btab, codes, halfsize );
+    if( t < m ) dsm_verify_slot( t, chunk, st, btab, atab, idx, lds_btab, codes, halfsize, order );
   }
 #else
   ulong t = (ulong)blockIdx.x * blockDim.x + threadIdx.x;
   if( t >= m ) return;
-  dsm_verify_slot( t, chunk, st, btab, atab, idx, lds_btab, codes, halfsize );
+  dsm_verify_slot( t, chunk, st, btab, atab, idx, lds_btab, codes, halfsize, order );
 #endif
 }
 
@@ -1177,7 +1198,8 @@ verify_impl( fd_ed25519_hip_ctx_t * ctx, ulong n, uchar const * d_sigs, uchar co
     if( ctx->timing ) FD_CHECK( hipEventRecord( ctx->ev[3], s ) );
     dim3 gdsm( FD_DSM_PERSIST && grid.x > ctx->dsm_wgs ? (unsigned)ctx->dsm_wgs : grid.x );
     hipLaunchKernelGGL( k_verify_dsm, gdsm, blk, 0, s, ctx->chunk, ctx->d_state, ctx->d_btab, ctx->d_atab,
-                        ctx->d_idx, ctx->d_count, d_codes + off, ctx->halfsize );
+                        ctx->d_idx, ctx->d_count, d_codes + off, ctx->halfsize,
+                        ordered ? ctx->d_order : (u32 const *)0 );
     FD_CHECK( hipGetLastError() );
     if( d_bitmap ) {
       hipLaunchKernelGGL( k_bitmap, grid, blk, 0, s, m, d_codes + off, d_bitmap + off/64, d_n, off );
