@@ -1111,6 +1111,83 @@ fd_ed25519_hip_test_halfsize( fd_ed25519_hip_ctx_t * ctx, ulong n, uint const * 
   return 0;
 }
 
+/* test hook: one device primitive over n items, 32 u32 words in and 32 out
+   per item (include/fd_ed25519_hip.h FD_ED25519_HIP_PRIM_*).  Field inputs
+   are 9 limbs (value = sum v[i] 2^(29 i)) within the bounds each primitive
+   assumes; field outputs are 9 limbs as the primitive leaves them (products:
+   tight) or canonical where the op says so. */
+__global__ void k_test_prim( int op, ulong n, u32 const * in, u32 * out ) {
+  ulong t = (ulong)blockIdx.x * blockDim.x + threadIdx.x;
+  if( t >= n ) return;
+  u32 const * x = in + 32*t;
+  u32 o[32];
+  #pragma unroll
+  for( int q=0; q<32; q++ ) o[q] = 0u;
+  fe a, b, r, s;
+  #pragma unroll
+  for( int q=0; q<9; q++ ) { a.v[q] = x[q]; b.v[q] = x[9+q]; }
+  switch( op ) {
+  case 0: fe_mul( r, a, b ); break;                                  /* FE_MUL     */
+  case 1: fe_sq( r, a ); break;                                      /* FE_SQ      */
+  case 2: fe_mul2( r, a, b, s, b, a ); break;                        /* FE_MUL2: a*b, b*a */
+  case 3: fe_sq2( r, a, s, b ); break;                               /* FE_SQ2: a^2, b^2 */
+  case 4: fe_canon( r, a ); break;                                   /* FE_CANON   */
+  case 5: { u32 w[8];                                                /* FE_FROMWORDS */
+            #pragma unroll
+            for( int q=0; q<8; q++ ) w[q] = x[q];
+            fe_from_words( r, w ); } break;
+  case 6: fe_sub( r, a, b ); fe_canon( r, r ); break;                /* FE_SUB (b tight) */
+  case 7: fe_pow22523( r, a ); fe_canon( r, r ); break;              /* FE_POW22523 */
+  case 8: fe_invert( r, a ); fe_canon( r, r ); break;                /* FE_INVERT  */
+  case 9: {                                                          /* GE_DECODE  */
+            u32 w[8];
+            #pragma unroll
+            for( int q=0; q<8; q++ ) w[q] = x[q];
+            ge_p3 P;
+            u32 f = ge_decode( P, w );
+            o[0] = f;
+            o[1] = (!(f & 1u) && ge_affine_is_small_order( P )) ? 1u : 0u;
+            u32 xw[8], yw[8];
+            fe_to_words( xw, P.X ); fe_to_words( yw, P.Y );
+            #pragma unroll
+            for( int q=0; q<8; q++ ) { o[2+q] = xw[q]; o[10+q] = yw[q]; }
+          } break;
+  case 10: { u32 w[16], k[8];                                        /* SC_REDUCE  */
+             #pragma unroll
+             for( int q=0; q<16; q++ ) w[q] = x[q];
+             sc_reduce512( k, w );
+             #pragma unroll
+             for( int q=0; q<8; q++ ) o[q] = k[q]; } break;
+  case 11: { u32 w[8];                                               /* SC_CANONICAL */
+             #pragma unroll
+             for( int q=0; q<8; q++ ) w[q] = x[q];
+             o[0] = sc_is_canonical( w ) ? 1u : 0u; } break;
+  default: break;
+  }
+  if( op <= 8 ) {
+    #pragma unroll
+    for( int q=0; q<9; q++ ) o[q] = r.v[q];
+    if( op == 2 || op == 3 ) {
+      #pragma unroll
+      for( int q=0; q<9; q++ ) o[9+q] = s.v[q];
+    }
+  }
+  #pragma unroll
+  for( int q=0; q<32; q++ ) out[32*t+q] = o[q];
+}
+
+int
+fd_ed25519_hip_test_prim( fd_ed25519_hip_ctx_t * ctx, int op, ulong n, uint const * d_in, uint * d_out,
+                          void * stream ) {
+  hipStream_t s = stream ? (hipStream_t)stream : ctx->stream;
+  FD_CHECK( hipSetDevice( ctx->device ) );
+  if( op < 0 || op > 11 ) return -1;
+  if( !n ) return 0;
+  hipLaunchKernelGGL( k_test_prim, dim3( (unsigned)((n + 63)/64) ), dim3( 64 ), 0, s, op, n, d_in, d_out );
+  FD_CHECK( hipGetLastError() );
+  return 0;
+}
+
 /* test hook: plain SHA-512 of n messages with the device hash core used by
    k_verify_prep (sha512_prefixed with an empty prefix); out: 64-byte digests */
 __global__ __launch_bounds__(64) void k_test_sha512( ulong n, uchar const * pool, uint const * moff,

@@ -34,7 +34,7 @@ EXPORTS = (
     "fd_ed25519_hip_sync", "fd_ed25519_hip_set_timing", "fd_ed25519_hip_get_timing",
     "fd_ed25519_hip_get_dsm_units", "fd_ed25519_hip_set_halfsize", "fd_ed25519_hip_test_halfsize",
     "fd_ed25519_hip_test_sha512", "fd_ed25519_hip_host_alloc", "fd_ed25519_hip_host_free",
-    "fd_ed25519_hip_stage_async",
+    "fd_ed25519_hip_stage_async", "fd_ed25519_hip_test_prim",
 )
 
 _lib = None
@@ -70,6 +70,8 @@ def lib():
         L.fd_ed25519_hip_set_halfsize.argtypes = [vp, c.c_int]
         L.fd_ed25519_hip_test_halfsize.argtypes = [vp, c.c_ulong, vp, vp, vp]
         L.fd_ed25519_hip_test_sha512.argtypes = [vp, c.c_ulong, vp, vp, vp, vp, vp]
+        L.fd_ed25519_hip_test_prim.restype = c.c_int
+        L.fd_ed25519_hip_test_prim.argtypes = [vp, c.c_int, c.c_ulong, vp, vp, vp]
         L.fd_ed25519_hip_ctx_reserve.argtypes = [vp, u64]
         L.fd_ed25519_hip_host_alloc.restype = vp
         L.fd_ed25519_hip_host_alloc.argtypes = [u64]
@@ -320,6 +322,17 @@ class Verifier:
                 self._p(msg_sz, 4 * n, "msg_sz"), self._p(out, 128 * n, "out"))
         with self._stream(stream) as h:
             return self._lib.fd_ed25519_hip_test_sha512(*args, h)
+
+    def test_prim(self, op, n, d_in, d_out, stream=None):
+        """Test hook: one device primitive (FD_ED25519_HIP_PRIM_*, see
+        fd_ed25519_hip_test_prim) over n items of 32 u32 words in and out."""
+        n = int(n)
+        args = (self.ctx, int(op), n, self._p(d_in, 128 * n, "in"), self._p(d_out, 128 * n, "out"))
+        with self._stream(stream) as h:
+            rc = self._lib.fd_ed25519_hip_test_prim(*args, h)
+        if rc:
+            raise ValueError(f"test_prim: unknown op {op}")
+        return rc
 
     def stage_async(self, d_dst, h_src, nbytes, stream=None):
         """Host -> device copy of nbytes (h_src: a HostBuffer or raw host address) on a stream."""

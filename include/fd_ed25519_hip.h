@@ -120,6 +120,36 @@ void                   fd_ed25519_hip_set_halfsize( fd_ed25519_hip_ctx_t * ctx, 
 int fd_ed25519_hip_test_halfsize( fd_ed25519_hip_ctx_t * ctx, ulong n, uint const * d_k, uint * d_out,
                                   void * stream );
 
+/* Test hook: one device primitive over n items; d_in and d_out hold 32 u32
+   words per item.  Field elements are 9 limbs, value = sum v[i]*2^(29 i),
+   at words 0..8 (a) and 9..17 (b) of the input.  Ops and outputs:
+     FE_MUL a*b, FE_SQ a^2 (tight limbs, 0..8); FE_MUL2 a*b, b*a and FE_SQ2
+     a^2, b^2 (two products run interleaved, 0..8 and 9..17); FE_CANON a
+     canonical (limbs < 2^32-8); FE_FROMWORDS of input words 0..7 (32 LE
+     bytes, bit 255 masked); FE_SUB a-b canonical (b tight); FE_POW22523
+     a^(2^252-3) and FE_INVERT a^(p-2), canonical (fd_f25519.c:25-74);
+     GE_DECODE of input words 0..7 (fd_ed25519_point_frombytes with the
+     AVX-512 failure split): word 0 flags (bit 0 not on the curve, bit 1
+     x==0 with the sign bit set), word 1 small order
+     (fd_ed25519_affine_is_small_order), words 2..9 x, 10..17 y (canonical
+     LE); SC_REDUCE of 16 input words mod L (fd_curve25519_scalar_reduce);
+     SC_CANONICAL word 0 = input words 0..7 < L (scalar_validate).
+   Returns -1 for an unknown op.  Asynchronous on stream. */
+#define FD_ED25519_HIP_PRIM_FE_MUL        0
+#define FD_ED25519_HIP_PRIM_FE_SQ         1
+#define FD_ED25519_HIP_PRIM_FE_MUL2       2
+#define FD_ED25519_HIP_PRIM_FE_SQ2        3
+#define FD_ED25519_HIP_PRIM_FE_CANON      4
+#define FD_ED25519_HIP_PRIM_FE_FROMWORDS  5
+#define FD_ED25519_HIP_PRIM_FE_SUB        6
+#define FD_ED25519_HIP_PRIM_FE_POW22523   7
+#define FD_ED25519_HIP_PRIM_FE_INVERT     8
+#define FD_ED25519_HIP_PRIM_GE_DECODE     9
+#define FD_ED25519_HIP_PRIM_SC_REDUCE    10
+#define FD_ED25519_HIP_PRIM_SC_CANONICAL 11
+int fd_ed25519_hip_test_prim( fd_ed25519_hip_ctx_t * ctx, int op, ulong n, uint const * d_in, uint * d_out,
+                              void * stream );
+
 /* Test hook: plain SHA-512 (fd_sha512_init/append/fini, fd_sha512.c:264-399)
    of n messages d_pool[ d_msg_off[i], +d_msg_sz[i] ) with both device hash
    paths: the per-lane one (sha512_prefixed: signing) writes 64-byte digests
