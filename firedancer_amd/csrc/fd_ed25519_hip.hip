@@ -7,18 +7,21 @@
      k_msg_hist,    txn paths only: records counting-sorted by SHA-512 block
      k_msg_order    count, so that prep's waves hash equal-length messages
      k_verify_prep  S<L check, decode A and R (sqrt chains), small-order
-                    checks, k = SHA-512(R||A||M) mod L -> 192-B state record;
-                    survivor compaction: final codes of pre-check failures,
-                    survivors -> idx[] (k_verify_dsm runs only them)
+                    checks, k = SHA-512(R||A||M) mod L (wave-cooperative
+                    LDS-staged message blocks) -> 192-B state record at the
+                    lane's slot; survivor compaction: final codes of
+                    pre-check failures, survivor slots -> idx[] (k_verify_dsm
+                    runs only them)
      k_verify_dsm   persistent: resident workgroups pull 64-survivor tasks;
                     half-size scalars k1 = k*k2 (mod 8L), k2 odd, ~128 bits
-                    each (sc_halfsize); tables B and 2^128 B -> LDS; tables
-                    [1..8](+-A) and [1..8](-R) -> per-lane HBM scratch, one
-                    128-B line per entry (the identity is one shared entry);
-                    [k1](+-A) + [k2](-R) + [k2*S mod L]B by fixed signed
-                    windows (radix 16 for k1, k2; radix-256 digit pairs for
-                    the B coefficient: every lane adds at the same positions,
-                    one window count per wave); identity check; int8 code
+                    each (sc_halfsize); tables [1..8](+-A) and [1..8](-R) ->
+                    per-lane HBM scratch, one 128-B line per entry (the
+                    identity is one shared entry); [k1](+-A) + [k2](-R) by
+                    fixed signed radix-16 windows, [k2*S mod L]B in signed
+                    radix 2^12 from two L2-resident global tables ([0..2048]B
+                    and [0..2048]2^132 B, FD_BTAB_W12): every lane adds at the
+                    same positions, one window count per wave; identity
+                    check; int8 code
      k_bitmap       verdict bitmap from codes (64-bit ballot per wave)
      k_group_reduce batch_single_msg / per-txn semantics over sig codes
 

@@ -69,8 +69,8 @@ fd_ed25519_strerror( int err );
 
 /* ---- Part 2: GPU-native bulk interface -----------------------------------
 
-   A context owns one HIP device, one stream, the LDS-staged base-point table
-   and the scratch for up to chunk_sigs signatures in flight per launch
+   A context owns one HIP device, one stream, the base-point tables and the
+   scratch for up to chunk_sigs signatures in flight per launch
    (larger requests are processed in chunks of chunk_sigs).  Contexts are not
    thread-safe; use one per host thread (one per verify tile).  Calls on one
    context may name different streams: each verify waits (hipStreamWaitEvent)
