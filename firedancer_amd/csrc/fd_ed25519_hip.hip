@@ -161,6 +161,10 @@ struct fd_ed25519_hip_ctx {
   u32 *        d_order;     /* chunk: k_verify_prep's record order (variable-size message paths) */
   int          errmode;
   int          halfsize;    /* 1: half-size scalars (default); 0: full-length (k, 1) */
+  ulong        lat_max;     /* calls of at most this many records (no device count) take k_verify_lat */
+  u32          lat_copies;  /* k_verify_lat workgroups per signature for small calls (one per XCD) */
+  u32          lat_seq;     /* call number, the k_verify_lat early-exit tag */
+  u32 *        d_lat_done;  /* LAT_MAX_N: call number of the copy that finished each signature */
   /* optional per-kernel timing (HIP events around each launch, on the launch stream) */
   int          timing;
   double       prep_ms, dsm_ms;
@@ -684,6 +688,65 @@ DEV u32 wave_max7( u32 v ) {
 #define DSM_OCCUPANCY
 #endif
 
+/* signed radix-2^GW digits of sp (< 2^253) for the two global B tables:
+   digit i = r_i + c_i - 2^GW c_{i+1}, r_i = bits [GW i, GW i + GW), carry
+   bits c in bmask; digits 0..ND-1 against [j]B, ND..2ND-1 against
+   [j](2^HB B).  Both halves are held as 160-bit groups whose top GW bits are
+   the next digit (consumed top-down): bl = sp << (160-HB) (bits 0..HB-1),
+   bh = sp >> (2HB-160) (bits HB.. on top; the bits below are never read). */
+DEV void b12_digits( u32 bl[5], u32 bh[5], u32 & bmask, u32 const sp[8] ) {
+  constexpr int GW = FD_BTAB_GW, ND = BTG_ND, HB = BTG_HB;
+  u32 c = 0u; bmask = 0u;
+  #pragma unroll
+  for( int i=0; i<2*ND; i++ ) {
+    int b = GW*i, wi = b >> 5, sh = b & 31;
+    u32 x = (sh + GW <= 32) ? (sp[wi] >> sh)
+                            : __builtin_amdgcn_alignbit( wi < 7 ? sp[wi+1] : 0u, sp[wi], (u32)sh );
+    u32 d = (x & ((1u << GW) - 1u)) + c;
+    c = d >= (1u << (GW-1)) ? 1u : 0u;
+    bmask |= c << (i+1);
+  }
+  /* lo = (sp mod 2^HB) << (160-HB): sp bit HB would land at group bit 160,
+     so nothing above the low half enters; hi = sp >> (2HB-160): its top
+     ND*GW bits are sp's bits from HB up (the bits below are never read) */
+  constexpr int LS = 160 - HB, HS = 2*HB - 160;
+  #pragma unroll
+  for( int q=0; q<5; q++ ) {
+    int b = 32*q - LS;                           /* sp bit at the group word's bit 0 */
+    u32 lo_w = b + 32 <= 0 ? 0u : b < 0 ? (sp[0] << (-b)) :
+               (b & 31) ? __builtin_amdgcn_alignbit( sp[(b>>5)+1], sp[b>>5], (u32)(b & 31) ) : sp[b>>5];
+    bl[q] = lo_w;
+    int hb = 32*q + HS, hw = hb >> 5, hsh = hb & 31;
+    u32 hx = hw + 1 <= 7 ? sp[hw+1] : 0u, hy = hw <= 7 ? sp[hw] : 0u;
+    bh[q] = hsh ? __builtin_amdgcn_alignbit( hx, hy, (u32)hsh ) : hy;
+  }
+}
+
+/* P += [digit bi]B + [digit bi+ND](2^HB B) from the global tables, digits
+   taken off the top of bl / bh (b12_digits); T of the result if needT */
+DEV void b12_step( ge_p3 & P, u32 bl[5], u32 bh[5], u32 bmask, u32 bi, u32 const * __restrict__ btab,
+                   bool needT ) {
+  constexpr u32 GW = FD_BTAB_GW, ND = BTG_ND;
+  u32 negb, ib, negc, ic;
+  {
+    int v = (int)((bl[4] >> (32u-GW)) + ((bmask >> bi) & 1u)) - (int)(((bmask >> (bi+1u)) & 1u) << GW);
+    negb = (u32)(v >> 31); ib = ((u32)v ^ negb) - negb;
+    v = (int)((bh[4] >> (32u-GW)) + ((bmask >> (bi+ND)) & 1u)) - (int)(((bmask >> (bi+ND+1u)) & 1u) << GW);
+    negc = (u32)(v >> 31); ic = ((u32)v ^ negc) - negc;
+  }
+  #pragma unroll
+  for( int q=4; q>0; q-- ) {
+    bl[q] = __builtin_amdgcn_alignbit( bl[q], bl[q-1], 32u-GW );
+    bh[q] = __builtin_amdgcn_alignbit( bh[q], bh[q-1], 32u-GW );
+  }
+  bl[0] <<= GW; bh[0] <<= GW;
+  u32 const * bt = btab + BT12_OFF;
+  ge_affc b; load_affc( b, bt + ib*BT12_ENT );
+  ge_add_affc( P, P, b, negb, true );
+  load_affc( b, bt + (BT12_N + ic)*BT12_ENT );
+  ge_add_affc( P, P, b, negc, needT );
+}
+
 /* one survivor: DSM slot t (tables at slot t), state column idx[t] (prep's
    slot; record order[idx[t]] under FD_STATE_BY_SLOT, else the record) */
 DEV void dsm_verify_slot( ulong t, ulong chunk, u32 const * __restrict__ st, u32 const * __restrict__ btab,
@@ -721,39 +784,7 @@ DEV void dsm_verify_slot( ulong t, ulong chunk, u32 const * __restrict__ st, u32
       sc_mul( sp, k2, S );
       sc_recode16s( kd1, k1 ); sc_recode16s( kd2, k2 );
 #if FD_BTAB_W12
-      /* signed radix-2^12 digits of sp (< 2^253): digit i = r_i + c_i -
-         4096 c_{i+1}, r_i = bits [12i, 12i+12), carry bits c in bmask;
-         digits 0..10 against [j]B, 11..21 against [j](2^132 B).  Both halves
-         are held as 160-bit groups whose top 12 bits are the next digit
-         (consumed top-down): bl = sp << 28 (bits 0..131), bh = sp >> 104
-         (bits 132..263 on top; the 28 bits below are never read). */
-      {
-        constexpr int GW = FD_BTAB_GW, ND = BTG_ND, HB = BTG_HB;
-        u32 c = 0u; bmask = 0u;
-        #pragma unroll
-        for( int i=0; i<2*ND; i++ ) {
-          int b = GW*i, wi = b >> 5, sh = b & 31;
-          u32 x = (sh + GW <= 32) ? (sp[wi] >> sh)
-                                  : __builtin_amdgcn_alignbit( wi < 7 ? sp[wi+1] : 0u, sp[wi], (u32)sh );
-          u32 d = (x & ((1u << GW) - 1u)) + c;
-          c = d >= (1u << (GW-1)) ? 1u : 0u;
-          bmask |= c << (i+1);
-        }
-        /* lo = (sp mod 2^HB) << (160-HB): sp bit HB would land at group bit 160,
-           so nothing above the low half enters; hi = sp >> (2HB-160): its top
-           ND*GW bits are sp's bits from HB up (the bits below are never read) */
-        constexpr int LS = 160 - HB, HS = 2*HB - 160;
-        #pragma unroll
-        for( int q=0; q<5; q++ ) {
-          int b = 32*q - LS;                           /* sp bit at the group word's bit 0 */
-          u32 lo_w = b + 32 <= 0 ? 0u : b < 0 ? (sp[0] << (-b)) :
-                     (b & 31) ? __builtin_amdgcn_alignbit( sp[(b>>5)+1], sp[b>>5], (u32)(b & 31) ) : sp[b>>5];
-          bl[q] = lo_w;
-          int hb = 32*q + HS, hw = hb >> 5, hsh = hb & 31;
-          u32 hx = hw + 1 <= 7 ? sp[hw+1] : 0u, hy = hw <= 7 ? sp[hw] : 0u;
-          bh[q] = hsh ? __builtin_amdgcn_alignbit( hx, hy, (u32)hsh ) : hy;
-        }
-      }
+      b12_digits( bl, bh, bmask, sp );                       /* signed radix-2^12 digits of sp */
 #else
       sc_recode256( sd, sp );       /* digits 0..15: B; 16..31: 2^128 B (second LDS table) */
 #endif
@@ -802,28 +833,7 @@ DEV void dsm_verify_slot( ulong t, ulong chunk, u32 const * __restrict__ st, u32
       /* windows (ND-1)*STEP, .., STEP, 0: lo digits ND-1..0, hi digits 2ND-1..ND */
       bool bw = w <= (BTG_ND-1)*BTG_STEP && w % BTG_STEP == 0;
       ge_add_cached( P, P, e, negr, bw );
-      if( bw ) {
-        constexpr u32 GW = FD_BTAB_GW, ND = BTG_ND;
-        u32 bi = (u32)w / (u32)BTG_STEP;
-        u32 negb, ib, negc, ic;
-        {
-          int v = (int)((bl[4] >> (32u-GW)) + ((bmask >> bi) & 1u)) - (int)(((bmask >> (bi+1u)) & 1u) << GW);
-          negb = (u32)(v >> 31); ib = ((u32)v ^ negb) - negb;
-          v = (int)((bh[4] >> (32u-GW)) + ((bmask >> (bi+ND)) & 1u)) - (int)(((bmask >> (bi+ND+1u)) & 1u) << GW);
-          negc = (u32)(v >> 31); ic = ((u32)v ^ negc) - negc;
-        }
-        #pragma unroll
-        for( int q=4; q>0; q-- ) {
-          bl[q] = __builtin_amdgcn_alignbit( bl[q], bl[q-1], 32u-GW );
-          bh[q] = __builtin_amdgcn_alignbit( bh[q], bh[q-1], 32u-GW );
-        }
-        bl[0] <<= GW; bh[0] <<= GW;
-        u32 const * bt = btab + BT12_OFF;
-        ge_affc b; load_affc( b, bt + ib*BT12_ENT );
-        ge_add_affc( P, P, b, negb, true );
-        load_affc( b, bt + (BT12_N + ic)*BT12_ENT );
-        ge_add_affc( P, P, b, negc, false );
-      }
+      if( bw ) b12_step( P, bl, bh, bmask, (u32)w / (u32)BTG_STEP, btab, false );
 #else
       bool bw = (w & 1) == 0 && w <= 30;
       ge_add_cached( P, P, e, negr, bw );
@@ -894,6 +904,213 @@ void k_verify_dsm( ulong chunk, u32 const * __restrict__ st, u32 const * __restr
   if( t >= m ) return;
   dsm_verify_slot( t, chunk, st, btab, atab, idx, lds_btab, codes, halfsize, order );
 #endif
+}
+
+/**********************************************************************/
+/* Latency path (small batches, the drop-in's single calls): one signature
+   per workgroup of three waves, each wave running one lane.  The bulk
+   kernels spend one lane per signature for the whole verify, which is what
+   throughput wants and what makes a lone call slow (one wave issuing the
+   decodes, the hash and every doubling in sequence).  Here the independent
+   pieces run side by side:
+     phase 1  wave 0 decodes A, wave 1 decodes R (each a pow22523 chain),
+              wave 2 checks S, hashes R||A||M, reduces mod L, splits k into
+              half-size scalars (sc_halfsize) and recodes all digits;
+     phase 2  wave 0 [k1](+-A) and wave 1 [k2](-R) (each its own table and
+              doubling chain), wave 2 [k2*S mod L]B from the two global
+              radix-2^12 tables (10 x 12 doublings, 22 additions);
+     phase 3  one lane adds the three points and checks P == O.
+   The equation, the pre-check order and the codes are k_verify_prep's and
+   k_verify_dsm's (fd_ed25519_user.c:135-230). */
+
+#define LAT_MAX_N 256ul      /* verify_impl takes this path for n <= LAT_MAX_N without a device count */
+#define LAT_COPY_MAX_N 32ul  /* calls of up to 32 signatures run one copy per XCD (k_verify_lat) */
+/* 12 waves = 3 per SIMD, all a CU holds at k_verify_lat's register count:
+   one workgroup per CU, so a call's signatures never share a SIMD.  Waves
+   3..11 leave at once; the three working waves land on three SIMDs. */
+#define LAT_WG 768
+
+struct lat_shared {
+  u32 ax[8], ay[8], rx[8], ry[8];   /* canonical decoded coordinates */
+  u32 fa, fr, fs;                   /* pre-check flags per wave */
+  u32 kd1[8], kd2[8];               /* signed radix-16 digits of |k1|, k2 */
+  u32 k1neg, D;                     /* k1 < 0; windows of the A and R chains */
+  u32 bl[5], bh[5], bmask;          /* radix-2^12 digits of k2*S mod L */
+  u32 P[3][36];                     /* the three partial points (X, Y, Z, T) */
+};
+
+DEV void lat_put( u32 * d, ge_p3 const & P ) {
+  #pragma unroll
+  for( int q=0; q<9; q++ ) { d[q] = P.X.v[q]; d[9+q] = P.Y.v[q]; d[18+q] = P.Z.v[q]; d[27+q] = P.T.v[q]; }
+}
+DEV void lat_get( ge_p3 & P, u32 const * d ) {
+  #pragma unroll
+  for( int q=0; q<9; q++ ) { P.X.v[q] = d[q]; P.Y.v[q] = d[9+q]; P.Z.v[q] = d[18+q]; P.T.v[q] = d[27+q]; }
+}
+
+/* another copy of signature i already finished this call (seq) */
+DEV bool lat_done( u32 const * done, ulong i, u32 seq ) {
+  return __hip_atomic_load( done + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT ) == seq;
+}
+
+/* [k](Q) by fixed signed radix-16 windows over a lane's table (digits kd,
+   biased by 7, D windows from the top); T of the result is produced.  With
+   copies, it stops early once another copy has finished (the result is then
+   never used). */
+DEV void lat_chain( ge_p3 & P, u32 const * tab, u32 const * ident, u32 kd[8], u32 D, u32 const * done, ulong i,
+                    u32 seq, u32 copies ) {
+  #pragma unroll 1
+  for( u32 q = D; q < 64u; q++ ) digits_shl( kd, 4u );
+  ge_identity( P );
+  #pragma unroll 1
+  for( int w=(int)D-1; w>=0; w-- ) {
+    u32 neg, mag;
+    digit_split( kd[7] >> 28, 7u, neg, mag ); digits_shl( kd, 4u );
+    ge_cached e; load_cached( e, tab_entry( tab, ident, mag ) );
+    if( w != (int)D-1 ) {
+      #pragma unroll 1
+      for( int j=0; j<3; j++ ) ge_dbl( P, P, false );
+      ge_dbl( P, P, true );
+    }
+    ge_add_cached( P, P, e, neg, true );
+    if( copies > 1u && lat_done( done, i, seq ) ) break;
+  }
+}
+
+/* the XCD (XCC) this workgroup runs on: hwreg(HW_REG_XCC_ID, 0, 4) */
+DEV u32 xcc_id( void ) { return (u32)__builtin_amdgcn_s_getreg( (3 << 11) | (0 << 6) | 20 ); }
+
+/* the dispatcher deals a launch's consecutive workgroups to the XCDs in turn */
+__global__ void k_xcc_probe( u32 * out ) { if( threadIdx.x == 0u ) out[blockIdx.x] = xcc_id(); }
+
+/* copies > 1: each signature gets that many consecutive workgroups, which the
+   dispatcher deals to different XCDs, all computing the same verdict; the
+   first to finish writes the code and tags done[i] with this call's seq, and
+   the others stop at their next window.  A lone call's time depends on the
+   XCD it lands on (measured 415-1068 us per call, repeating with period 8 as
+   the dispatcher rotates single-workgroup launches over the XCDs); racing one
+   copy per XCD takes the fastest.  Every copy writes the same code, so a tie
+   is harmless, and done[] is only an early-exit hint: the host reads the
+   codes after the whole launch. */
+__global__ __launch_bounds__(LAT_WG)
+void k_verify_lat( ulong n, uchar const * __restrict__ sigs, uchar const * __restrict__ pubs,
+                   uchar const * __restrict__ pool, uint const * __restrict__ moff, uint const * __restrict__ msz,
+                   u32 fixed_sz, u32 const * __restrict__ btab, u32 * __restrict__ atab, int errmode,
+                   int halfsize, signed char * __restrict__ codes, u32 copies, u32 * __restrict__ done, u32 seq ) {
+  __shared__ lat_shared L;
+  ulong i = blockIdx.x / copies;
+  if( i >= n ) return;
+  if( threadIdx.x >= 192u ) return;                        /* waves 3.. only hold the CU (LAT_WG) */
+  u32 wave = threadIdx.x >> 6, lane = threadIdx.x & 63u;
+  u32 * tabA = atab + (ulong)blockIdx.x * ATAB_WORDS, * tabR = tabA + RTAB_OFF;   /* per copy */
+  u32 const * ident = btab + IDENT_OFF;
+
+  /* ---- phase 1 ---- */
+  if( lane == 0u ) {
+    if( wave < 2u ) {                                    /* decode A (wave 0) or R (wave 1), user.c:165-199 */
+      u32 w[8];
+      load_words( w, wave ? sigs + 64*i : pubs + 32*i, 8 );
+      ge_p3 Q;
+      u32 f = ge_decode( Q, w );
+      bool small = !(f & 1u) && ge_affine_is_small_order( Q );
+      u32 xw[8], yw[8];
+      fe_to_words( xw, Q.X ); fe_to_words( yw, Q.Y );
+      if( wave == 0u ) {
+        L.fa = ((f & 1u) ? F_A_NOTSQ : 0u) | ((f & 2u) ? F_A_ZX : 0u) | (small ? F_A_SMALL : 0u);
+        #pragma unroll
+        for( int q=0; q<8; q++ ) { L.ax[q] = xw[q]; L.ay[q] = yw[q]; }
+      } else {
+        L.fr = ((f & 1u) ? F_R_NOTSQ : 0u) | ((f & 2u) ? F_R_ZX : 0u) | (small ? F_R_SMALL : 0u);
+        #pragma unroll
+        for( int q=0; q<8; q++ ) { L.rx[q] = xw[q]; L.ry[q] = yw[q]; }
+      }
+    } else {                                             /* S < L, k = H(R||A||M) mod L, half-size split */
+      u32 sig[16], pub[8], k[8], k1[8], k2[8], sp[8], k1neg, bits;
+      load_words( sig, sigs + 64*i, 16 );
+      load_words( pub, pubs + 32*i, 8 );
+      L.fs = sc_is_canonical( sig + 8 ) ? 0u : F_S_BAD;                   /* user.c:159-161 */
+      u32 mo = moff ? moff[i] : (u32)i * fixed_sz;
+      u32 ms = msz  ? msz[i]  : fixed_sz;
+      hram_mod_l( k, sig, pub, pool + mo, ms );                            /* user.c:205-207 */
+      if( halfsize ) bits = sc_halfsize( k1, k1neg, k2, k );
+      else {
+        #pragma unroll
+        for( int w=0; w<8; w++ ) { k1[w] = k[w]; k2[w] = w ? 0u : 1u; }
+        k1neg = 0u; bits = 253u;
+      }
+      sc_mul( sp, k2, sig + 8 );
+      u32 kd1[8], kd2[8], bl[5], bh[5], bmask;
+      sc_recode16s( kd1, k1 ); sc_recode16s( kd2, k2 );
+      b12_digits( bl, bh, bmask, sp );
+      #pragma unroll
+      for( int q=0; q<8; q++ ) { L.kd1[q] = kd1[q]; L.kd2[q] = kd2[q]; }
+      #pragma unroll
+      for( int q=0; q<5; q++ ) { L.bl[q] = bl[q]; L.bh[q] = bh[q]; }
+      L.bmask = bmask; L.k1neg = k1neg; L.D = (bits >> 2) + 1u;
+    }
+  }
+  __syncthreads();
+  u32 flags = L.fa | L.fr | L.fs;
+  if( code_of( flags, FD_ED25519_HIP_ERRMODE_AVX512, true ) != FD_ED25519_SUCCESS ) {   /* workgroup-uniform */
+    if( threadIdx.x == 0u ) {
+      codes[i] = (signed char)code_of( flags, errmode, false );
+      if( copies > 1u ) __hip_atomic_store( done + i, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT );
+    }
+    return;
+  }
+
+  /* ---- phase 2 ---- */
+  if( lane == 0u ) {
+    ge_p3 P;
+    if( wave < 2u ) {
+      u32 xw[8], yw[8], kd[8];
+      #pragma unroll
+      for( int q=0; q<8; q++ ) {
+        xw[q] = wave ? L.rx[q] : L.ax[q]; yw[q] = wave ? L.ry[q] : L.ay[q];
+        kd[q] = wave ? L.kd2[q] : L.kd1[q];
+      }
+      fe x, y, nx;
+      fe_from_words( x, xw ); fe_from_words( y, yw );
+      fe_neg( nx, x ); fe_norm( nx, nx );
+      if( wave == 0u ) fe_cmov( nx, x, L.k1neg );                          /* k1 < 0: [|k1|](+A) */
+      u32 * tab = wave ? tabR : tabA;
+      build_cached_table( tab, nx, y );
+      lat_chain( P, tab, ident, kd, L.D, done, i, seq, copies );
+    } else {
+      u32 bl[5], bh[5];
+      #pragma unroll
+      for( int q=0; q<5; q++ ) { bl[q] = L.bl[q]; bh[q] = L.bh[q]; }
+      u32 bmask = L.bmask;
+      ge_identity( P );
+      #pragma unroll 1
+      for( int bi=(int)BTG_ND-1; bi>=0; bi-- ) {
+        if( bi != (int)BTG_ND-1 ) {
+          #pragma unroll 1
+          for( int j=0; j<FD_BTAB_GW-1; j++ ) ge_dbl( P, P, false );
+          ge_dbl( P, P, true );
+        }
+        b12_step( P, bl, bh, bmask, (u32)bi, btab, true );
+        if( copies > 1u && lat_done( done, i, seq ) ) break;
+      }
+    }
+    lat_put( L.P[wave], P );
+  }
+  __syncthreads();
+
+  /* ---- phase 3: P_A + P_R + P_B == O (user.c:216-229) ----
+     done is monotonic within a call: a chain that stopped early saw it set,
+     so this check sees it too and the partial points are never used */
+  if( threadIdx.x == 0u && !(copies > 1u && lat_done( done, i, seq )) ) {
+    ge_p3 P, Q; ge_cached c;
+    lat_get( P, L.P[0] );
+    lat_get( Q, L.P[1] ); ge_to_cached( c, Q ); ge_add_cached( P, P, c, 0u, true );
+    lat_get( Q, L.P[2] ); ge_to_cached( c, Q ); ge_add_cached( P, P, c, 0u, false );
+    fe x, y, z;
+    fe_canon( x, P.X ); fe_canon( y, P.Y ); fe_canon( z, P.Z );
+    bool eq = fe_is_zero_c( x ) && fe_eq_c( y, z );
+    codes[i] = (signed char)(eq ? FD_ED25519_SUCCESS : FD_ED25519_ERR_MSG);
+    if( copies > 1u ) __hip_atomic_store( done + i, seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT );
+  }
 }
 
 /* fd_ed25519_verify_batch_single_msg (user.c:232-310) over per-sig codes */
@@ -1018,6 +1235,7 @@ fd_ed25519_hip_ctx_new( int device, ulong chunk_sigs ) {
   ctx->device   = device;
   ctx->chunk    = chunk_sigs;
   ctx->halfsize = 1;
+  ctx->lat_max = LAT_MAX_N;
   FD_CHECK( hipSetDevice( device ) );
   FD_CHECK( hipStreamCreateWithFlags( &ctx->stream, hipStreamNonBlocking ) );
   FD_CHECK( hipMalloc( (void **)&ctx->d_btab,  BTAB_ALLOC * sizeof(u32) ) );
@@ -1043,6 +1261,25 @@ fd_ed25519_hip_ctx_new( int device, ulong chunk_sigs ) {
   hipLaunchKernelGGL( k_btab12_init, dim3( (2*BT12_N + 63)/64 ), dim3( 64 ), 0, ctx->stream, ctx->d_btab );
   FD_CHECK( hipGetLastError() );
 #endif
+  {
+    /* k_verify_lat copies: one per XCD, if the probe sees consecutive
+       workgroups dealt to the XCDs in turn (one partition = one XCD: 1) */
+    enum { NP = 64 };
+    u32 * d_x = 0, h_x[NP];
+    FD_CHECK( hipMalloc( (void **)&d_x, NP*sizeof(u32) ) );
+    hipLaunchKernelGGL( k_xcc_probe, dim3( NP ), dim3( 64 ), 0, ctx->stream, d_x );
+    FD_CHECK( hipGetLastError() );
+    FD_CHECK( hipMemcpyAsync( h_x, d_x, sizeof(h_x), hipMemcpyDeviceToHost, ctx->stream ) );
+    FD_CHECK( hipStreamSynchronize( ctx->stream ) );
+    FD_CHECK( hipFree( d_x ) );
+    u32 nx = 0;
+    for( int j=0; j<NP; j++ ) nx = h_x[j] + 1u > nx ? h_x[j] + 1u : nx;
+    int rr = nx > 1u && nx <= 16u;
+    for( int j=0; rr && j<NP; j++ ) rr = h_x[j] == (h_x[0] + (u32)j) % nx;
+    ctx->lat_copies = rr ? nx : 1u;
+    FD_CHECK( hipMalloc( (void **)&ctx->d_lat_done, LAT_MAX_N * sizeof(u32) ) );
+    FD_CHECK( hipMemsetAsync( ctx->d_lat_done, 0, LAT_MAX_N * sizeof(u32), ctx->stream ) );
+  }
   FD_CHECK( hipStreamSynchronize( ctx->stream ) );
   return ctx;
 }
@@ -1076,6 +1313,7 @@ fd_ed25519_hip_ctx_delete( fd_ed25519_hip_ctx_t * ctx ) {
   if( ctx->ev_used ) (void)hipEventSynchronize( ctx->ev_last );   /* last call may have run on a caller stream */
   (void)hipFree( ctx->d_btab ); (void)hipFree( ctx->d_state ); (void)hipFree( ctx->d_atab );
   (void)hipFree( ctx->d_idx ); (void)hipFree( ctx->d_order ); (void)hipFree( ctx->d_count );
+  (void)hipFree( ctx->d_lat_done );
   free_staging( ctx );
   for( int e=0; e<4; e++ ) (void)hipEventDestroy( ctx->ev[e] );
   (void)hipEventDestroy( ctx->ev_last );
@@ -1088,6 +1326,7 @@ int   fd_ed25519_hip_ctx_device( fd_ed25519_hip_ctx_t const * ctx ) { return ctx
 void *fd_ed25519_hip_ctx_stream( fd_ed25519_hip_ctx_t const * ctx ) { return (void *)ctx->stream; }
 void  fd_ed25519_hip_set_errmode( fd_ed25519_hip_ctx_t * ctx, int m ) { ctx->errmode = m; }
 void  fd_ed25519_hip_set_halfsize( fd_ed25519_hip_ctx_t * ctx, int on ) { ctx->halfsize = on ? 1 : 0; }
+void  fd_ed25519_hip_set_small_batch( fd_ed25519_hip_ctx_t * ctx, ulong max_n ) { ctx->lat_max = max_n; }
 
 /* test hook: sc_halfsize on n scalars k < L (8 LE words each); out per
    scalar: k1 (8 words), k2 (8 words), k1neg (0 or ~0), bits */
@@ -1253,6 +1492,26 @@ verify_impl( fd_ed25519_hip_ctx_t * ctx, ulong n, uchar const * d_sigs, uchar co
   FD_CHECK( hipSetDevice( ctx->device ) );
   if( !n ) return 0;
   if( ctx->ev_used ) FD_CHECK( hipStreamWaitEvent( s, ctx->ev_last, 0 ) );   /* previous call's scratch use */
+  if( !d_n && n <= ctx->lat_max && n <= ctx->chunk && !ctx->timing ) {
+    /* small batch: one workgroup per signature (k_verify_lat) */
+    /* one workgroup per CU (LAT_WG); calls of up to LAT_COPY_MAX_N
+       signatures race one copy per XCD (k_verify_lat) */
+    u32 copies = n <= LAT_COPY_MAX_N && n * ctx->lat_copies <= ctx->chunk ? ctx->lat_copies : 1u;
+    u32 seq = ++ctx->lat_seq;
+    if( !seq ) seq = ++ctx->lat_seq;                       /* 0 is done[]'s initial value */
+    hipLaunchKernelGGL( k_verify_lat, dim3( (unsigned)(n * copies) ), dim3( LAT_WG ), 0, s, n, d_sigs, d_pubs,
+                        d_pool, d_msg_off, d_msg_sz, fixed_sz, ctx->d_btab, ctx->d_atab, ctx->errmode,
+                        ctx->halfsize, d_codes, copies, ctx->d_lat_done, seq );
+    FD_CHECK( hipGetLastError() );
+    if( d_bitmap ) {
+      hipLaunchKernelGGL( k_bitmap, dim3( (unsigned)((n + 255) / 256) ), dim3( 256 ), 0, s, n, d_codes, d_bitmap,
+                          (u32 const *)0, 0ul );
+      FD_CHECK( hipGetLastError() );
+    }
+    FD_CHECK( hipEventRecord( ctx->ev_last, s ) );
+    ctx->ev_used = 1;
+    return 0;
+  }
   for( ulong off = 0; off < n; off += ctx->chunk ) {
     ulong m = n - off < ctx->chunk ? n - off : ctx->chunk;
     dim3 grid( (unsigned)((m + 255) / 256) ), blk( 256 );

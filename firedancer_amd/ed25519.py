@@ -34,7 +34,7 @@ EXPORTS = (
     "fd_ed25519_hip_sync", "fd_ed25519_hip_set_timing", "fd_ed25519_hip_get_timing",
     "fd_ed25519_hip_get_dsm_units", "fd_ed25519_hip_set_halfsize", "fd_ed25519_hip_test_halfsize",
     "fd_ed25519_hip_test_sha512", "fd_ed25519_hip_host_alloc", "fd_ed25519_hip_host_free",
-    "fd_ed25519_hip_stage_async", "fd_ed25519_hip_test_prim",
+    "fd_ed25519_hip_stage_async", "fd_ed25519_hip_test_prim", "fd_ed25519_hip_set_small_batch",
 )
 
 _lib = None
@@ -68,6 +68,7 @@ def lib():
         L.fd_ed25519_hip_ctx_stream.argtypes = [vp]
         L.fd_ed25519_hip_set_errmode.argtypes = [vp, c.c_int]
         L.fd_ed25519_hip_set_halfsize.argtypes = [vp, c.c_int]
+        L.fd_ed25519_hip_set_small_batch.argtypes = [vp, u64]
         L.fd_ed25519_hip_test_halfsize.argtypes = [vp, c.c_ulong, vp, vp, vp]
         L.fd_ed25519_hip_test_sha512.argtypes = [vp, c.c_ulong, vp, vp, vp, vp, vp]
         L.fd_ed25519_hip_test_prim.restype = c.c_int
@@ -306,6 +307,10 @@ class Verifier:
     def set_halfsize(self, on):
         """Half-size scalars (default) or the full-length pair (k, 1): same verdicts."""
         self._lib.fd_ed25519_hip_set_halfsize(self.ctx, 1 if on else 0)
+
+    def set_small_batch(self, max_n):
+        """Calls of at most max_n records take the latency kernel (0: never)."""
+        self._lib.fd_ed25519_hip_set_small_batch(self.ctx, int(max_n))
 
     def test_halfsize(self, n, d_k, d_out, stream=None):
         """Test hook: device half-size reduction (see fd_ed25519_hip_test_halfsize)."""
