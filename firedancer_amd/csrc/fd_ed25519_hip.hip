@@ -163,8 +163,8 @@ struct fd_ed25519_hip_ctx {
   int          halfsize;    /* 1: half-size scalars (default); 0: full-length (k, 1) */
   ulong        lat_max;     /* calls of at most this many records (no device count) take k_verify_lat */
   u32          lat_copies;  /* k_verify_lat workgroups per signature for small calls (one per XCD) */
-  u32          lat_seq;     /* call number, the k_verify_lat early-exit tag */
-  u32 *        d_lat_done;  /* LAT_MAX_N: call number of the copy that finished each signature */
+  ulong        lat_seq;     /* call number, the k_verify_lat early-exit tag (64-bit: never wraps) */
+  ulong *      d_lat_done;  /* LAT_MAX_N: call number of the copy that finished each signature */
   /* optional per-kernel timing (HIP events around each launch, on the launch stream) */
   int          timing;
   double       prep_ms, dsm_ms;
@@ -949,7 +949,7 @@ DEV void lat_get( ge_p3 & P, u32 const * d ) {
 }
 
 /* another copy of signature i already finished this call (seq) */
-DEV bool lat_done( u32 const * done, ulong i, u32 seq ) {
+DEV bool lat_done( ulong const * done, ulong i, ulong seq ) {
   return __hip_atomic_load( done + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT ) == seq;
 }
 
@@ -957,8 +957,8 @@ DEV bool lat_done( u32 const * done, ulong i, u32 seq ) {
    biased by 7, D windows from the top); T of the result is produced.  With
    copies, it stops early once another copy has finished (the result is then
    never used). */
-DEV void lat_chain( ge_p3 & P, u32 const * tab, u32 const * ident, u32 kd[8], u32 D, u32 const * done, ulong i,
-                    u32 seq, u32 copies ) {
+DEV void lat_chain( ge_p3 & P, u32 const * tab, u32 const * ident, u32 kd[8], u32 D, ulong const * done, ulong i,
+                    ulong seq, u32 copies ) {
   #pragma unroll 1
   for( u32 q = D; q < 64u; q++ ) digits_shl( kd, 4u );
   ge_identity( P );
@@ -996,7 +996,7 @@ __global__ __launch_bounds__(LAT_WG)
 void k_verify_lat( ulong n, uchar const * __restrict__ sigs, uchar const * __restrict__ pubs,
                    uchar const * __restrict__ pool, uint const * __restrict__ moff, uint const * __restrict__ msz,
                    u32 fixed_sz, u32 const * __restrict__ btab, u32 * __restrict__ atab, int errmode,
-                   int halfsize, signed char * __restrict__ codes, u32 copies, u32 * __restrict__ done, u32 seq ) {
+                   int halfsize, signed char * __restrict__ codes, u32 copies, ulong * __restrict__ done, ulong seq ) {
   __shared__ lat_shared L;
   ulong i = blockIdx.x / copies;
   if( i >= n ) return;
@@ -1277,8 +1277,8 @@ fd_ed25519_hip_ctx_new( int device, ulong chunk_sigs ) {
     int rr = nx > 1u && nx <= 16u;
     for( int j=0; rr && j<NP; j++ ) rr = h_x[j] == (h_x[0] + (u32)j) % nx;
     ctx->lat_copies = rr ? nx : 1u;
-    FD_CHECK( hipMalloc( (void **)&ctx->d_lat_done, LAT_MAX_N * sizeof(u32) ) );
-    FD_CHECK( hipMemsetAsync( ctx->d_lat_done, 0, LAT_MAX_N * sizeof(u32), ctx->stream ) );
+    FD_CHECK( hipMalloc( (void **)&ctx->d_lat_done, LAT_MAX_N * sizeof(ulong) ) );
+    FD_CHECK( hipMemsetAsync( ctx->d_lat_done, 0, LAT_MAX_N * sizeof(ulong), ctx->stream ) );
   }
   FD_CHECK( hipStreamSynchronize( ctx->stream ) );
   return ctx;
@@ -1497,8 +1497,7 @@ verify_impl( fd_ed25519_hip_ctx_t * ctx, ulong n, uchar const * d_sigs, uchar co
     /* one workgroup per CU (LAT_WG); calls of up to LAT_COPY_MAX_N
        signatures race one copy per XCD (k_verify_lat) */
     u32 copies = n <= LAT_COPY_MAX_N && n * ctx->lat_copies <= ctx->chunk ? ctx->lat_copies : 1u;
-    u32 seq = ++ctx->lat_seq;
-    if( !seq ) seq = ++ctx->lat_seq;                       /* 0 is done[]'s initial value */
+    ulong seq = ++ctx->lat_seq;                            /* from 1: 0 is done[]'s initial value */
     hipLaunchKernelGGL( k_verify_lat, dim3( (unsigned)(n * copies) ), dim3( LAT_WG ), 0, s, n, d_sigs, d_pubs,
                         d_pool, d_msg_off, d_msg_sz, fixed_sz, ctx->d_btab, ctx->d_atab, ctx->errmode,
                         ctx->halfsize, d_codes, copies, ctx->d_lat_done, seq );
