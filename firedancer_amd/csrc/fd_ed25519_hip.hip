@@ -185,6 +185,7 @@ struct fd_ed25519_hip_ctx {
      the kernels read and write in place (no copies), grown on demand */
   uchar *      h_stage;
   ulong        h_stage_cap;
+  uchar *      d_stage;     /* device copy of h_stage (drop-in calls, FD_DROPIN_DMA) */
 };
 
 /**********************************************************************/
@@ -1318,6 +1319,7 @@ fd_ed25519_hip_ctx_delete( fd_ed25519_hip_ctx_t * ctx ) {
   for( int e=0; e<4; e++ ) (void)hipEventDestroy( ctx->ev[e] );
   (void)hipEventDestroy( ctx->ev_last );
   if( ctx->h_stage ) (void)hipHostFree( ctx->h_stage );
+  if( ctx->d_stage ) (void)hipFree( ctx->d_stage );
   (void)hipStreamDestroy( ctx->stream );
   free( ctx );
 }
@@ -1738,6 +1740,15 @@ static void dropin_check_msg_sz( ulong msg_sz, char const * fn ) {
   }
 }
 
+/* FD_DROPIN_DMA (default 1): the staged block is copied to HBM with one DMA
+   and the codes come back with another, instead of the kernels reading the
+   records (and the message, a few bytes per load) over PCIe from the mapped
+   host block, a round trip per dependent load.  Measured p50 per call (200-B
+   message, profiles/r02z_latency): see DESIGN.md 3. */
+#ifndef FD_DROPIN_DMA
+#define FD_DROPIN_DMA 1
+#endif
+
 /* stage n (sig, pub) pairs sharing one message and run them; codes land in
    the staging block */
 static signed char const *
@@ -1749,6 +1760,10 @@ dropin_run( fd_ed25519_hip_ctx_t * ctx, uchar const * msg, ulong msg_sz, uchar c
     FD_CHECK( hipSetDevice( ctx->device ) );
     if( ctx->h_stage ) FD_CHECK( hipHostFree( ctx->h_stage ) );
     FD_CHECK( hipHostMalloc( (void **)&ctx->h_stage, cap, hipHostMallocDefault ) );
+    if( FD_DROPIN_DMA ) {
+      if( ctx->d_stage ) FD_CHECK( hipFree( ctx->d_stage ) );
+      FD_CHECK( hipMalloc( (void **)&ctx->d_stage, cap ) );
+    }
     ctx->h_stage_cap = cap;
   }
   uchar * st = ctx->h_stage;
@@ -1758,8 +1773,12 @@ dropin_run( fd_ed25519_hip_ctx_t * ctx, uchar const * msg, ulong msg_sz, uchar c
   for( ulong j=0; j<n; j++ ) { off[j] = 0u; sz[j] = (uint)msg_sz; }
   if( msg_sz ) memcpy( st + STAGE_MSG, msg, msg_sz );
   memset( st + STAGE_MSG + msg_sz, 0, 16 );
-  verify_impl( ctx, n, st + STAGE_SIGS, st + STAGE_PUBS, st + STAGE_MSG, off, sz, 0u,
-               (signed char *)(st + STAGE_CODES), NULL, NULL, NULL );
+  uchar * dv = FD_DROPIN_DMA ? ctx->d_stage : st;          /* what the kernels read and write */
+  if( FD_DROPIN_DMA ) FD_CHECK( hipMemcpyAsync( dv, st, need, hipMemcpyHostToDevice, ctx->stream ) );
+  verify_impl( ctx, n, dv + STAGE_SIGS, dv + STAGE_PUBS, dv + STAGE_MSG, (uint const *)(dv + STAGE_OFF),
+               (uint const *)(dv + STAGE_SZ), 0u, (signed char *)(dv + STAGE_CODES), NULL, NULL, NULL );
+  if( FD_DROPIN_DMA )
+    FD_CHECK( hipMemcpyAsync( st + STAGE_CODES, dv + STAGE_CODES, n, hipMemcpyDeviceToHost, ctx->stream ) );
   FD_CHECK( hipStreamSynchronize( ctx->stream ) );
   return (signed char const *)(st + STAGE_CODES);
 }

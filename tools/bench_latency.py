@@ -31,7 +31,7 @@ def main():
     sigs = b.sigs.cpu().numpy().tobytes(); pubs = b.pubs.cpu().numpy().tobytes()
     msg = b.pool[:msg_sz].cpu().numpy().tobytes()
     v.close()
-    L = ctypes.CDLL(LIB)
+    L = ctypes.CDLL(os.environ.get("FD_ED25519_HIP_LIB") or LIB)   # a build variant, as firedancer_amd.ed25519 loads it
     c = ctypes
     L.fd_ed25519_verify.argtypes = [c.c_char_p, c.c_ulong, c.c_char_p, c.c_char_p, c.c_void_p]
     L.fd_ed25519_verify_batch_single_msg.argtypes = [c.c_char_p, c.c_ulong, c.c_char_p, c.c_char_p, c.c_void_p,
