@@ -926,6 +926,9 @@ void k_verify_dsm( ulong chunk, u32 const * __restrict__ st, u32 const * __restr
 
 #define LAT_MAX_N 256ul      /* verify_impl takes this path for n <= LAT_MAX_N without a device count */
 #define LAT_COPY_MAX_N 32ul  /* calls of up to 32 signatures run one copy per XCD (k_verify_lat) */
+#ifndef FD_LAT_COPIES
+#define FD_LAT_COPIES 1      /* 0: one workgroup per signature always (A/B switch) */
+#endif
 /* 12 waves = 3 per SIMD, all a CU holds at k_verify_lat's register count:
    one workgroup per CU, so a call's signatures never share a SIMD.  Waves
    3..11 leave at once; the three working waves land on three SIMDs. */
@@ -987,9 +990,10 @@ __global__ void k_xcc_probe( u32 * out ) { if( threadIdx.x == 0u ) out[blockIdx.
 /* copies > 1: each signature gets that many consecutive workgroups, which the
    dispatcher deals to different XCDs, all computing the same verdict; the
    first to finish writes the code and tags done[i] with this call's seq, and
-   the others stop at their next window.  A lone call's time depends on the
-   XCD it lands on (measured 415-1068 us per call, repeating with period 8 as
-   the dispatcher rotates single-workgroup launches over the XCDs); racing one
+   the others stop at their next window.  A lone call's time depends on
+   where the dispatcher places it (measured 415-1068 us per call, repeating
+   with period 8 as single-workgroup launches rotate over the XCDs; the shader
+   clock is the same 2.39 GHz on every launch, tools/xcd_clock); racing one
    copy per XCD takes the fastest.  Every copy writes the same code, so a tie
    is harmless, and done[] is only an early-exit hint: the host reads the
    codes after the whole launch. */
@@ -1277,7 +1281,7 @@ fd_ed25519_hip_ctx_new( int device, ulong chunk_sigs ) {
     for( int j=0; j<NP; j++ ) nx = h_x[j] + 1u > nx ? h_x[j] + 1u : nx;
     int rr = nx > 1u && nx <= 16u;
     for( int j=0; rr && j<NP; j++ ) rr = h_x[j] == (h_x[0] + (u32)j) % nx;
-    ctx->lat_copies = rr ? nx : 1u;
+    ctx->lat_copies = rr && FD_LAT_COPIES ? nx : 1u;
     FD_CHECK( hipMalloc( (void **)&ctx->d_lat_done, LAT_MAX_N * sizeof(ulong) ) );
     FD_CHECK( hipMemsetAsync( ctx->d_lat_done, 0, LAT_MAX_N * sizeof(ulong), ctx->stream ) );
   }
