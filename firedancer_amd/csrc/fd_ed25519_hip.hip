@@ -569,6 +569,36 @@ DEV void load_cached( ge_cached & c, u32 const * t ) {
   for( int i=0; i<9; i++ ) { c.YmX.v[i] = w[i]; c.YpX.v[i] = w[9+i]; c.T2d.v[i] = w[18+i]; c.Z2.v[i] = w[27+i]; }
 }
 #endif
+/* FD_DSM_RLDS: k_verify_dsm prefetches each window's R-table entry straight
+   into LDS (global_load_lds_dwordx4, 8 KB per wave: 8 x 16 B per lane) when it
+   issues the A entry's load, before the window's doublings, and reads it
+   back after the A addition.  Without it the R entry's load is issued after
+   the A addition and its latency is exposed (the 32 VGPRs to hold both
+   entries across the doublings would cost a wave per SIMD).  Off: A/B on one
+   box (profiles/r02z_ab_rlds) C2 130.4/130.6 vs 131.4/130.8 M verifies/s, DSM
+   6.84/6.89 vs 6.65/6.91 ms -- the other two waves of the SIMD already hide
+   that latency. */
+#ifndef FD_DSM_RLDS
+#define FD_DSM_RLDS 0
+#endif
+typedef __attribute__((address_space(3))) u32 lds_u32;
+DEV void entry_prefetch_lds( lds_u32 * wl, u32 const * src ) {
+  #pragma unroll
+  for( int k=0; k<8; k++ )
+    __builtin_amdgcn_global_load_lds( (void const *)(src + 4*k), (__attribute__((address_space(3))) void *)(wl + 256*k),
+                                      16, 0, 0 );
+}
+DEV void entry_load_lds( ge_cached & c, lds_u32 const * wl, u32 lane ) {
+  asm volatile( "s_waitcnt vmcnt(0)" ::: "memory" );      /* the prefetch has landed in LDS */
+  u32 w[32];
+  #pragma unroll
+  for( int k=0; k<8; k++ ) {
+    lds_u32 const * q = wl + 256*k + 4*lane;
+    w[4*k] = q[0]; w[4*k+1] = q[1]; w[4*k+2] = q[2]; w[4*k+3] = q[3];
+  }
+  fe_unpack<0>( c.YmX, w ); fe_unpack<0>( c.YpX, w + 8 ); fe_unpack<1>( c.T2d, w + 16 ); fe_unpack<0>( c.Z2, w + 24 );
+}
+
 /* one 1/2-scaled affine B-table entry from LDS (FD_BTAB_PACK: 6 x
    ds_read_b128 + unpack; else 7 x ds_read_b128) */
 DEV void store_affc( u32 * e, ge_affc const & a ) {      /* canonical elements: any packing layout fits */
@@ -752,7 +782,8 @@ DEV void b12_step( ge_p3 & P, u32 bl[5], u32 bh[5], u32 bmask, u32 bi, u32 const
    slot; record order[idx[t]] under FD_STATE_BY_SLOT, else the record) */
 DEV void dsm_verify_slot( ulong t, ulong chunk, u32 const * __restrict__ st, u32 const * __restrict__ btab,
                           u32 * __restrict__ atab, u32 const * __restrict__ idx, u32 const * lds_btab,
-                          signed char * __restrict__ codes, int halfsize, u32 const * __restrict__ order ) {
+                          signed char * __restrict__ codes, int halfsize, u32 const * __restrict__ order,
+                          lds_u32 * lds_rent ) {
   ulong p = idx[t];
 #if FD_STATE_BY_SLOT
   ulong i = order ? (ulong)order[p] : p;
@@ -823,13 +854,20 @@ DEV void dsm_verify_slot( ulong t, ulong chunk, u32 const * __restrict__ st, u32
       digit_split( kd2[7] >> 28, 7u, negr, ir ); digits_shl( kd2, 4u );
       /* issued before the window's 4 doublings, which hide its latency */
       ge_cached e; load_cached( e, tab_entry( tabA, ident, ia ) );
+#if FD_DSM_RLDS
+      entry_prefetch_lds( lds_rent, tab_entry( tabR, ident, ir ) );
+#endif
       if( w != (int)D-1 ) {
         #pragma unroll 1
         for( int j=0; j<3; j++ ) ge_dbl( P, P, false );
         ge_dbl( P, P, true );
       }
       ge_add_cached( P, P, e, nega, true );
+#if FD_DSM_RLDS
+      entry_load_lds( e, lds_rent, (u32)(threadIdx.x & 63u) );
+#else
       load_cached( e, tab_entry( tabR, ident, ir ) );
+#endif
 #if FD_BTAB_W12
       /* windows (ND-1)*STEP, .., STEP, 0: lo digits ND-1..0, hi digits 2ND-1..ND */
       bool bw = w <= (BTG_ND-1)*BTG_STEP && w % BTG_STEP == 0;
@@ -891,6 +929,12 @@ void k_verify_dsm( ulong chunk, u32 const * __restrict__ st, u32 const * __restr
   }
   __syncthreads();
 #endif
+#if FD_DSM_RLDS
+  __shared__ __attribute__((aligned(16))) u32 lds_rent_all[4*2048];
+  lds_u32 * lds_rent = (lds_u32 *)(lds_rent_all + 2048*(threadIdx.x >> 6));
+#else
+  lds_u32 * lds_rent = 0;
+#endif
 #if FD_DSM_PERSIST
   for( ;; ) {
     u32 task = 0u;
@@ -898,12 +942,12 @@ void k_verify_dsm( ulong chunk, u32 const * __restrict__ st, u32 const * __restr
     task = __shfl( task, 0 );
     if( (ulong)task * 64ul >= (ulong)m ) break;                       /* wave-uniform exit */
     ulong t = (ulong)task * 64ul + (threadIdx.x & 63u);
-    if( t < m ) dsm_verify_slot( t, chunk, st, btab, atab, idx, lds_btab, codes, halfsize, order );
+    if( t < m ) dsm_verify_slot( t, chunk, st, btab, atab, idx, lds_btab, codes, halfsize, order, lds_rent );
   }
 #else
   ulong t = (ulong)blockIdx.x * blockDim.x + threadIdx.x;
   if( t >= m ) return;
-  dsm_verify_slot( t, chunk, st, btab, atab, idx, lds_btab, codes, halfsize, order );
+  dsm_verify_slot( t, chunk, st, btab, atab, idx, lds_btab, codes, halfsize, order, lds_rent );
 #endif
 }
 
