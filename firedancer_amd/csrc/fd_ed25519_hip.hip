@@ -968,7 +968,10 @@ void k_verify_dsm( ulong chunk, u32 const * __restrict__ st, u32 const * __restr
    The equation, the pre-check order and the codes are k_verify_prep's and
    k_verify_dsm's (fd_ed25519_user.c:135-230). */
 
-#define LAT_MAX_N 256ul      /* verify_impl takes this path for n <= LAT_MAX_N without a device count */
+#define LAT_MAX_N 256ul      /* the largest call fd_ed25519_hip_set_small_batch can send down this path */
+#define LAT_DEFAULT_N 8ul    /* default: calls of up to 8 records (tools/bench_batch_latency.py: this path
+                                476-495 us vs 742-744 us at 1-4 records, 720 vs 749 at 8; the bulk
+                                kernels win from 16 up, 750 vs 849 us, profiles/r02z_latency) */
 #define LAT_COPY_MAX_N 32ul  /* calls of up to 32 signatures run one copy per XCD (k_verify_lat) */
 #ifndef FD_LAT_COPIES
 #define FD_LAT_COPIES 1      /* 0: one workgroup per signature always (A/B switch) */
@@ -1284,7 +1287,7 @@ fd_ed25519_hip_ctx_new( int device, ulong chunk_sigs ) {
   ctx->device   = device;
   ctx->chunk    = chunk_sigs;
   ctx->halfsize = 1;
-  ctx->lat_max = LAT_MAX_N;
+  ctx->lat_max = LAT_DEFAULT_N;
   FD_CHECK( hipSetDevice( device ) );
   FD_CHECK( hipStreamCreateWithFlags( &ctx->stream, hipStreamNonBlocking ) );
   FD_CHECK( hipMalloc( (void **)&ctx->d_btab,  BTAB_ALLOC * sizeof(u32) ) );
@@ -1376,7 +1379,9 @@ int   fd_ed25519_hip_ctx_device( fd_ed25519_hip_ctx_t const * ctx ) { return ctx
 void *fd_ed25519_hip_ctx_stream( fd_ed25519_hip_ctx_t const * ctx ) { return (void *)ctx->stream; }
 void  fd_ed25519_hip_set_errmode( fd_ed25519_hip_ctx_t * ctx, int m ) { ctx->errmode = m; }
 void  fd_ed25519_hip_set_halfsize( fd_ed25519_hip_ctx_t * ctx, int on ) { ctx->halfsize = on ? 1 : 0; }
-void  fd_ed25519_hip_set_small_batch( fd_ed25519_hip_ctx_t * ctx, ulong max_n ) { ctx->lat_max = max_n; }
+void  fd_ed25519_hip_set_small_batch( fd_ed25519_hip_ctx_t * ctx, ulong max_n ) {
+  ctx->lat_max = max_n < LAT_MAX_N ? max_n : LAT_MAX_N;
+}
 
 /* test hook: sc_halfsize on n scalars k < L (8 LE words each); out per
    scalar: k1 (8 words), k2 (8 words), k1neg (0 or ~0), bits */

@@ -1,13 +1,13 @@
 """GPU: the small-batch latency path (k_verify_lat, one workgroup of three
 waves per signature) against the bulk kernels and the oracle.
 
-Calls of at most fd_ed25519_hip_set_small_batch records (default 256) whose
-count is known on the host take k_verify_lat; the drop-in entry points and
-the KAT sets of up to 256 records in the other files already do.  Here the
-same records go through both paths and must give the same codes as each
-other and as the oracle: mixed validity (C2 mutations), messages of 0..1232
-bytes, both error modes, the full-length (k, 1) switch, fixed-size messages
-and a bitmap."""
+Calls of at most fd_ed25519_hip_set_small_batch records (default 8, here
+raised to 256) whose count is known on the host take k_verify_lat; the
+drop-in entry points' single calls and the 4-record corpus KAT in the other
+files already do.  Here the same records go through both paths and must give
+the same codes as each other and as the oracle: mixed validity (C2
+mutations), messages of 0..1232 bytes, both error modes, the full-length
+(k, 1) switch, fixed-size messages, the racing copies and a bitmap."""
 import numpy as np
 import pytest
 
@@ -17,6 +17,16 @@ from fdgen import c2_mutate
 pytestmark = pytest.mark.gpu
 
 from firedancer_amd import ERRMODE_AVX512, ERRMODE_REF  # noqa: E402
+
+LAT_DEFAULT = 8
+
+
+@pytest.fixture
+def lat(verifier):
+    """the session verifier with every call of up to 256 records on k_verify_lat"""
+    verifier.set_small_batch(256)
+    yield verifier
+    verifier.set_small_batch(LAT_DEFAULT)
 
 
 def _signed_set(n, seed, max_msg=1232):
@@ -41,7 +51,8 @@ def _sliced(verifier, sigs, pubs, pool, moff, msz, step):
     return np.concatenate(codes), np.concatenate(bits).astype(bool)
 
 
-def test_latency_path_equals_bulk_and_oracle(verifier):
+def test_latency_path_equals_bulk_and_oracle(lat):
+    verifier = lat
     sigs, pubs, pool, moff, msz = _signed_set(3000, 0x1a7)
     exp = O.verify_many(sigs, pubs, pool, moff, msz, O.ERRMODE_AVX512)
     try:
@@ -60,7 +71,8 @@ def test_latency_path_equals_bulk_and_oracle(verifier):
 
 @pytest.mark.parametrize("mode", [ERRMODE_AVX512, ERRMODE_REF])
 @pytest.mark.parametrize("halfsize", [1, 0])
-def test_latency_path_modes(verifier, mode, halfsize):
+def test_latency_path_modes(lat, mode, halfsize):
+    verifier = lat
     sigs, pubs, pool, moff, msz = _signed_set(512, 0x2b8 + 7 * halfsize, max_msg=300)
     exp = O.verify_many(sigs, pubs, pool, moff, msz, mode)
     verifier.set_errmode(mode)
@@ -73,7 +85,8 @@ def test_latency_path_modes(verifier, mode, halfsize):
     assert np.array_equal(lat, exp)
 
 
-def test_latency_path_fixed_messages(verifier):
+def test_latency_path_fixed_messages(lat):
+    verifier = lat
     """verify_fixed_dev (32-byte shred-root-like messages) on the latency path."""
     import torch
     rng = np.random.default_rng(0x3c9)
@@ -99,7 +112,8 @@ def test_latency_path_fixed_messages(verifier):
     assert np.array_equal(bits, got == 0)
 
 
-def test_latency_path_racing_copies(verifier):
+def test_latency_path_racing_copies(lat):
+    verifier = lat
     """Calls of up to 32 records run one copy of each signature per XCD and
     keep the first finisher's verdict (k_verify_lat copies): slices of 1, 5,
     16 and 32 records of a mixed batch, vs the oracle."""
@@ -119,3 +133,17 @@ def test_latency_path_racing_copies(verifier):
     for _ in range(20):                                          # repeated single calls: same verdict every time
         c, _b = verifier.verify_host(sigs[7:8], pubs[7:8], pool, moff[7:8], msz[7:8])
         assert c[0] == exp[7]
+
+
+def test_default_small_batch_limit(verifier):
+    """By default only calls of up to 8 records take k_verify_lat; 1..9-record
+    calls give the oracle's codes either way."""
+    sigs, pubs, pool, moff, msz = _signed_set(45, 0x5eb, max_msg=200)
+    exp = O.verify_many(sigs, pubs, pool, moff, msz, O.ERRMODE_AVX512)
+    got, lo = [], 0
+    for step in range(1, 10):
+        c, _b = verifier.verify_host(sigs[lo:lo + step], pubs[lo:lo + step], pool, moff[lo:lo + step],
+                                     msz[lo:lo + step])
+        got.append(c)
+        lo += step
+    assert lo == 45 and np.array_equal(np.concatenate(got), exp)
