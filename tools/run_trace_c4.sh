@@ -1,6 +1,6 @@
 #!/bin/bash
 # GPU-box script: rocprofv3 kernel + memory-copy trace of the default C4 bench
-# (resident leg only matters; PCIe leg skipped with --c4-pcie-steps 1).
+# (tools/trace_busy.py reads the timed resident steps out of it).
 # Usage: bash tools/run_trace_c4.sh <tag> [bench args...]
 export TMPDIR=/tmp
 T=${1:-c4trace}; shift
