@@ -33,7 +33,8 @@ def build(force=False, verbose=False, variant=None, defines=()):
     lib_path = variant_path(variant)
     deps = [os.path.join(CSRC, s) for s in SOURCES] + [os.path.join(PKG, "..", "include", h) for h in ("fd_ed25519_hip.h", "fd_verify_hip.h", "fd_replay_hip.h", "fd_sha512_hip.h")]
     if force or _stale(lib_path, deps):
-        cmd = [HIPCC, "--offload-arch=gfx950", "-O3", "-fPIC", "-shared", "-std=c++17"] + \
+        extra = os.environ.get("FD_HIPCC_EXTRA", "").split() if variant else []   # variants only: A/B flags
+        cmd = [HIPCC, "--offload-arch=gfx950", "-O3", "-fPIC", "-shared", "-std=c++17"] + extra + \
               [f"-D{d}" for d in defines] + ["-o", lib_path + ".tmp"] + [os.path.join(CSRC, u) for u in UNITS]
         if verbose:
             print(" ".join(cmd))
