@@ -1,0 +1,199 @@
+"""GPU: the engine against the reference itself at scale.
+
+The reference's own verify (fd_ed25519_verify / _batch_single_msg, built from
+/root/reference sources by oracle/Makefile into oracle/_ref/ref_cpu_bench_*)
+and the HIP path run over the same large record sets and must give the same
+code for every record (single mode) or group (batch mode):
+
+- 2^18 GPU-signed records, messages of 0..1232 bytes, the C2 mutation model
+  plus ten extra mutation classes on the remaining valid records (random R,
+  random A, random S, S = 0 / L-1 / L / 2^256-1, message bit flips, truncated
+  messages, swapped keys and signatures, x = 0 encodings with the sign bit set,
+  sign-bit flips of A and R);
+- 2^14 batch_single_msg groups of 1..16 signatures over one per-group message
+  (k_group_reduce over the per-record codes).
+
+The binary is compiled from the reference's sources in this container and
+travels in the tree (oracle/_ref is git-ignored, not gpurun-ignored); without
+it, or when the host lacks the backend it was built for, the test skips.
+The error mode follows the binary's backend: avx512 -> ERRMODE_AVX512,
+portable -> ERRMODE_REF."""
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REF_DIR = os.path.join(os.path.dirname(HERE), "oracle", "_ref")
+L_INT = 2 ** 252 + 27742317777372353535851937790883648493
+THREADS = 16
+
+
+def _ref_exe():
+    has_ifma = "avx512ifma" in open("/proc/cpuinfo").read()
+    exe = os.path.join(REF_DIR, "ref_cpu_bench_avx512" if has_ifma else "ref_cpu_bench_ref")
+    if not os.path.exists(exe):
+        pytest.skip("oracle/_ref reference binary not built")
+    return exe, has_ifma
+
+
+def _write_fdv1(path, sigs, pubs, pool, moff, msz, bfirst=None, bcnt=None):
+    nb = 0 if bfirst is None else len(bfirst)
+    with open(path, "wb") as f:
+        f.write(b"FDV1")
+        f.write(np.array([sigs.shape[0], pool.size, nb], np.uint64).tobytes())
+        for a in (sigs, pubs, moff.astype(np.uint32), msz.astype(np.uint32), pool):
+            f.write(np.ascontiguousarray(a).tobytes())
+        if nb:
+            f.write(np.asarray(bfirst, np.uint32).tobytes())
+            f.write(np.asarray(bcnt, np.uint8).tobytes())
+
+
+def _run_ref(tmp_path, *arrays, **kw):
+    exe, _ = _ref_exe()
+    inp, out = str(tmp_path / "in.bin"), str(tmp_path / "codes.bin")
+    _write_fdv1(inp, *arrays, **kw)
+    subprocess.run([exe, inp, str(THREADS), out], check=True, timeout=300, stdout=subprocess.DEVNULL)
+    return np.fromfile(out, np.int8)
+
+
+def _gpu_sign(verifier, prvs, pool, moff, msz):
+    import torch
+    dev = torch.device("cuda", verifier.device)
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+    n = prvs.shape[0]
+    d_pub = torch.empty((n, 32), dtype=torch.uint8, device=dev)
+    d_sig = torch.empty((n, 64), dtype=torch.uint8, device=dev)
+    verifier.sign_dev(n, t(prvs), t(pool), t(moff.view(np.int32)), t(msz.view(np.int32)), d_pub, d_sig)
+    verifier.sync()
+    return d_pub.cpu().numpy(), d_sig.cpu().numpy()
+
+
+def _msg_sizes(rng, n, hi=1232):
+    r = rng.random(n)
+    msz = np.where(r < 0.6, rng.integers(0, 129, n), np.where(r < 0.9, rng.integers(128, 513, n),
+                                                              rng.integers(512, hi + 1, n)))
+    msz[rng.random(n) < 0.05] = 0
+    return msz.astype(np.uint32)
+
+
+def _le32(x):
+    return np.frombuffer(int(x).to_bytes(32, "little"), np.uint8)
+
+
+def _extra_mutations(rng, sigs, pubs, pool, moff, msz, valid):
+    """Ten mutation classes on disjoint subsets of the still-valid records."""
+    idx = rng.permutation(np.nonzero(valid)[0])
+    k = idx.size // 40                                  # 2.5% of the valid records per class
+    cls = [idx[i * k:(i + 1) * k] for i in range(10)]
+    n = sigs.shape[0]
+    sigs[cls[0], :32] = rng.integers(0, 256, (k, 32), dtype=np.uint8)            # random R
+    pubs[cls[1]] = rng.integers(0, 256, (k, 32), dtype=np.uint8)                 # random A
+    sigs[cls[2], 32:] = rng.integers(0, 256, (k, 32), dtype=np.uint8)            # random S (mostly >= L)
+    edge_s = np.stack([_le32(0), _le32(L_INT - 1), _le32(L_INT), _le32(2 ** 256 - 1)])
+    sigs[cls[3], 32:] = edge_s[rng.integers(0, 4, k)]
+    for i in cls[4]:                                                             # message bit flip
+        if msz[i]:
+            b = int(rng.integers(0, 8 * int(msz[i])))
+            pool[int(moff[i]) + (b >> 3)] ^= np.uint8(1 << (b & 7))
+    msz[cls[5]] = np.maximum(msz[cls[5]].astype(np.int64) - rng.integers(1, 9, k), 0).astype(np.uint32)
+    other = rng.integers(0, n, k)                                                # another record's key
+    pubs[cls[6]] = pubs[other]
+    other = rng.integers(0, n, k)                                                # another record's signature
+    sigs[cls[7]] = sigs[other]
+    x0 = np.zeros((2, 32), np.uint8)                    # y = 1 and y = p-1 (x = 0) with the sign bit set
+    x0[0, 0] = 1
+    x0[0, 31] = 0x80
+    x0[1] = _le32(2 ** 255 - 20)
+    x0[1, 31] |= 0x80
+    half = k // 2
+    sigs[cls[8][:half], :32] = x0[rng.integers(0, 2, half)]
+    pubs[cls[8][half:]] = x0[rng.integers(0, 2, k - half)]
+    sigs[cls[9][:half], 31] ^= 0x80                                              # sign bit of R
+    pubs[cls[9][half:], 31] ^= 0x80                                              # sign bit of A
+    return cls
+
+
+def test_engine_equals_reference_2e18(verifier, tmp_path):
+    import torch
+    from firedancer_amd import ERRMODE_AVX512, ERRMODE_REF
+    from fdgen import c2_mutate
+    _, has_ifma = _ref_exe()
+    rng = np.random.default_rng(0x7e5c)
+    n = 1 << 18
+    msz = _msg_sizes(rng, n)
+    moff = np.concatenate([[0], np.cumsum(msz)[:-1]]).astype(np.uint32)
+    pool = rng.integers(0, 256, int(msz.sum()) + 64, dtype=np.uint8)
+    prvs = rng.integers(0, 256, (n, 32), dtype=np.uint8)
+    pubs, sigs = _gpu_sign(verifier, prvs, pool, moff, msz)
+    kinds = c2_mutate(sigs, pubs, rng)
+    _extra_mutations(rng, sigs, pubs, pool, moff, msz, kinds == 0)
+
+    ref = _run_ref(tmp_path, sigs, pubs, pool, moff, msz)
+    verifier.set_errmode(ERRMODE_AVX512 if has_ifma else ERRMODE_REF)
+    try:
+        dev = torch.device("cuda", verifier.device)
+        t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+        codes = torch.zeros(n, dtype=torch.int8, device=dev)
+        bitmap = torch.zeros((n + 63) // 64, dtype=torch.int64, device=dev)
+        verifier.verify_dev(n, t(sigs), t(pubs), t(pool), t(moff.view(np.int32)), t(msz.view(np.int32)),
+                            codes, bitmap)
+        verifier.sync()
+    finally:
+        verifier.set_errmode(ERRMODE_AVX512)
+    got = codes.cpu().numpy()
+    bad = np.nonzero(got != ref)[0]
+    assert bad.size == 0, (bad.size, [(int(i), int(got[i]), int(ref[i])) for i in bad[:10]])
+    bits = np.unpackbits(bitmap.cpu().numpy().view(np.uint8), bitorder="little")[:n].astype(bool)
+    assert np.array_equal(bits, got == 0)
+    hist = {int(c): int((ref == c).sum()) for c in np.unique(ref)}
+    assert set(hist) == {0, -1, -2, -3}, hist          # every verdict class occurs
+    assert min(hist.values()) > 1000, hist
+
+
+def test_batch_single_msg_equals_reference(verifier, tmp_path):
+    import torch
+    from fdgen import c2_mutate
+    _, has_ifma = _ref_exe()
+    rng = np.random.default_rng(0xba7c)
+    ng = 1 << 14
+    cnt = rng.integers(1, 17, ng).astype(np.uint8)
+    first = np.concatenate([[0], np.cumsum(cnt.astype(np.int64))[:-1]]).astype(np.uint32)
+    n = int(cnt.astype(np.int64).sum())
+    gsz = _msg_sizes(rng, ng, hi=600)
+    goff = np.concatenate([[0], np.cumsum(gsz)[:-1]]).astype(np.uint32)
+    pool = rng.integers(0, 256, int(gsz.sum()) + 64, dtype=np.uint8)
+    grp = np.repeat(np.arange(ng), cnt)
+    moff, msz = goff[grp], gsz[grp]                     # every record of a group signs the group's message
+    prvs = rng.integers(0, 256, (n, 32), dtype=np.uint8)
+    pubs, sigs = _gpu_sign(verifier, prvs, pool, moff, msz)
+    # sparse mutations: about a third of the groups keep every signature valid
+    sub = rng.random(n) < 0.04
+    s_sigs, s_pubs = sigs[sub].copy(), pubs[sub].copy()
+    c2_mutate(s_sigs, s_pubs, rng)
+    sigs[sub], pubs[sub] = s_sigs, s_pubs
+    for g in rng.choice(ng, ng // 50, replace=False):  # message flips hit a whole group
+        if gsz[g]:
+            pool[int(goff[g]) + int(rng.integers(0, int(gsz[g])))] ^= 0x10
+
+    ref = _run_ref(tmp_path, sigs, pubs, pool, moff, msz, bfirst=first, bcnt=cnt)
+    from firedancer_amd import ERRMODE_AVX512, ERRMODE_REF
+    verifier.set_errmode(ERRMODE_AVX512 if has_ifma else ERRMODE_REF)
+    try:
+        dev = torch.device("cuda", verifier.device)
+        t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+        codes = torch.zeros(n, dtype=torch.int8, device=dev)
+        verifier.verify_dev(n, t(sigs), t(pubs), t(pool), t(moff.view(np.int32)), t(msz.view(np.int32)), codes)
+        out = torch.zeros(ng, dtype=torch.int8, device=dev)
+        verifier.group_reduce_dev(ng, t(first.view(np.int32)), t(cnt), codes, out)
+        verifier.sync()
+    finally:
+        verifier.set_errmode(ERRMODE_AVX512)
+    got = out.cpu().numpy()
+    bad = np.nonzero(got != ref)[0]
+    assert bad.size == 0, (bad.size, [(int(g), int(got[g]), int(ref[g]), int(cnt[g])) for g in bad[:10]])
+    hist = {int(c): int((ref == c).sum()) for c in np.unique(ref)}
+    assert hist.get(0, 0) > ng // 5 and len(hist) >= 3, hist
