@@ -581,6 +581,11 @@ DEV void load_cached( ge_cached & c, u32 const * t ) {
 #ifndef FD_DSM_RLDS
 #define FD_DSM_RLDS 0
 #endif
+/* FD_DSM_TRAFFIC_PROBE (diagnostic builds only, wrong verdicts; see
+   dsm_verify_slot and tools/dsm_traffic_probe.py) */
+#ifndef FD_DSM_TRAFFIC_PROBE
+#define FD_DSM_TRAFFIC_PROBE 0
+#endif
 typedef __attribute__((address_space(3))) u32 lds_u32;
 DEV void entry_prefetch_lds( lds_u32 * wl, u32 const * src ) {
   #pragma unroll
@@ -828,6 +833,17 @@ DEV void dsm_verify_slot( ulong t, ulong chunk, u32 const * __restrict__ st, u32
 
     /* ---- tables [0..8](+-A) and [0..8](-R) (fd_curve25519.c:130-143) ---- */
     u32 * tabA = atab + ii * ATAB_WORDS, * tabR = tabA + RTAB_OFF;
+#if FD_DSM_TRAFFIC_PROBE
+    /* diagnostic build, wrong verdicts: the window loop reads 64 shared
+       (L2-resident) tables instead of the survivor's own; level 2 also
+       builds into them.  Same instruction stream, table traffic gone. */
+    u32 * rtabA = atab + (t & 63u) * ATAB_WORDS, * rtabR = rtabA + RTAB_OFF;
+#if FD_DSM_TRAFFIC_PROBE > 1
+    tabA = rtabA; tabR = rtabR;
+#endif
+#else
+    u32 * rtabA = tabA, * rtabR = tabR;
+#endif
     u32 const * ident = btab + IDENT_OFF;
     {
       fe x, y, nx;
@@ -853,9 +869,9 @@ DEV void dsm_verify_slot( ulong t, ulong chunk, u32 const * __restrict__ st, u32
       digit_split( kd1[7] >> 28, 7u, nega, ia ); digits_shl( kd1, 4u );
       digit_split( kd2[7] >> 28, 7u, negr, ir ); digits_shl( kd2, 4u );
       /* issued before the window's 4 doublings, which hide its latency */
-      ge_cached e; load_cached( e, tab_entry( tabA, ident, ia ) );
+      ge_cached e; load_cached( e, tab_entry( rtabA, ident, ia ) );
 #if FD_DSM_RLDS
-      entry_prefetch_lds( lds_rent, tab_entry( tabR, ident, ir ) );
+      entry_prefetch_lds( lds_rent, tab_entry( rtabR, ident, ir ) );
 #endif
       if( w != (int)D-1 ) {
         #pragma unroll 1
@@ -866,7 +882,7 @@ DEV void dsm_verify_slot( ulong t, ulong chunk, u32 const * __restrict__ st, u32
 #if FD_DSM_RLDS
       entry_load_lds( e, lds_rent, (u32)(threadIdx.x & 63u) );
 #else
-      load_cached( e, tab_entry( tabR, ident, ir ) );
+      load_cached( e, tab_entry( rtabR, ident, ir ) );
 #endif
 #if FD_BTAB_W12
       /* windows (ND-1)*STEP, .., STEP, 0: lo digits ND-1..0, hi digits 2ND-1..ND */
