@@ -27,6 +27,7 @@
 
 #include <hip/hip_runtime.h>
 #include <chrono>
+#include <math.h>
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -517,6 +518,36 @@ struct tile_slot {
   int           busy;
 };
 
+/* batch latency histograms in fd_histf's shape (src/util/hist/fd_histf.h:
+   16 buckets, [0,min) and [max,inf) at the ends, integer edges growing
+   geometrically between, no bucket empty) */
+#define HIST_B FD_VERIFY_HIP_HIST_BUCKET_CNT
+struct lat_hist { ulong counts[HIST_B]; ulong edge[HIST_B]; ulong sum; };
+
+/* the edges fd_histf_new computes (fd_histf.h:88-118): each interior edge
+   spreads the remaining ratio max/edge over the buckets left, rounded and
+   kept above the previous edge */
+extern "C" int fd_verify_hip_hist_edges( ulong min_v, ulong max_v, ulong edge[ HIST_B ] ) {
+  if( max_v <= min_v ) return -1;
+  if( min_v < 1ul ) min_v = 1ul;
+  if( max_v < min_v + HIST_B - 2ul ) max_v = min_v + HIST_B - 2ul;
+  edge[0] = 0ul; edge[1] = min_v;
+  for( ulong i = 2; i < HIST_B - 1ul; i++ ) {
+    double prev = (double)edge[i-1];
+    ulong e = (ulong)(0.5 + prev * pow( (double)max_v / prev, 1.0 / (double)(HIST_B - i) ));
+    edge[i] = e > edge[i-1] ? e : edge[i-1] + 1ul;
+  }
+  edge[HIST_B-1] = max_v;
+  return 0;
+}
+
+static void hist_sample( lat_hist & h, ulong v ) {
+  h.sum += v;
+  ulong b = HIST_B - 1ul;
+  while( v < h.edge[b] ) b--;                     /* edge[0] == 0 stops it */
+  h.counts[b]++;
+}
+
 struct fd_verify_hip_tile {
   fd_ed25519_hip_ctx_t * ctx;
   ulong      max_txn, seed;
@@ -530,6 +561,7 @@ struct fd_verify_hip_tile {
   tile_slot  slot[2];
   ulong      submitted, completed;
   double     last_gpu_ms, last_host_ms, last_sigs;
+  lat_hist   hist[2];        /* batch latency: GPU, host pass (ns) */
 };
 
 static void slot_alloc( tile_slot & s, ulong n ) {
@@ -577,7 +609,28 @@ fd_verify_hip_tile_new( fd_ed25519_hip_ctx_t * ctx, ulong max_txn, ulong seed, u
   t->oldest = &t->own_oldest; t->ring = t->own_mem; t->depth = depth; t->map = t->own_mem + depth; t->map_cnt = map_cnt;
   t->own_oldest = fd_verify_hip_tcache_reset( t->ring, depth, t->map, map_cnt );
   slot_alloc( t->slot[0], max_txn ); slot_alloc( t->slot[1], max_txn );
+  fd_verify_hip_tile_hist_init( t, 10000ul, 1000000000ul );   /* 10 us .. 1 s */
   return t;
+}
+
+extern "C" int fd_verify_hip_tile_hist_init( fd_verify_hip_tile_t * t, ulong min_ns, ulong max_ns ) {
+  ulong edge[HIST_B];
+  if( fd_verify_hip_hist_edges( min_ns, max_ns, edge ) ) return -1;
+  for( int w = 0; w < 2; w++ ) {
+    memset( &t->hist[w], 0, sizeof(lat_hist) );
+    memcpy( t->hist[w].edge, edge, sizeof(edge) );
+  }
+  return 0;
+}
+
+extern "C" int fd_verify_hip_tile_hist( fd_verify_hip_tile_t const * t, int which, ulong counts[ HIST_B ],
+                                        ulong left_edge_ns[ HIST_B ], ulong * sum_ns ) {
+  if( which < 0 || which > 1 ) return -1;
+  lat_hist const & h = t->hist[which];
+  if( counts )       memcpy( counts, h.counts, sizeof(h.counts) );
+  if( left_edge_ns ) memcpy( left_edge_ns, h.edge, sizeof(h.edge) );
+  if( sum_ns )       *sum_ns = h.sum;
+  return 0;
 }
 
 extern "C" void
@@ -789,6 +842,8 @@ fd_verify_hip_tile_complete( fd_verify_hip_tile_t * t, ulong const * bundle_id, 
   t->last_gpu_ms  = gpu_ms;
   t->last_host_ms = std::chrono::duration<double, std::milli>( h1 - h0 ).count();
   t->last_sigs    = (double)s.nsig;
+  hist_sample( t->hist[0], (ulong)((double)gpu_ms * 1e6 + 0.5) );
+  hist_sample( t->hist[1], (ulong)std::chrono::duration_cast<std::chrono::nanoseconds>( h1 - h0 ).count() );
   s.busy = 0; t->completed++;
   return 0;
 }

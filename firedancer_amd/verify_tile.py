@@ -37,8 +37,10 @@ EXPORTS = (
     "fd_verify_hip_tile_new", "fd_verify_hip_tile_join_tcache", "fd_verify_hip_tile_tcache_reset",
     "fd_verify_hip_tile_delete", "fd_verify_hip_tile_set_seed", "fd_verify_hip_tile_submit", "fd_verify_hip_tile_complete",
     "fd_verify_hip_tile_metrics", "fd_verify_hip_tile_last_timing", "fd_verify_hip_tile_submit_frags",
-    "fd_verify_hip_before_frag",
+    "fd_verify_hip_before_frag", "fd_verify_hip_hist_edges", "fd_verify_hip_tile_hist_init",
+    "fd_verify_hip_tile_hist",
 )
+HIST_BUCKET_CNT = 16
 
 # fd_txn_m_t / gossip vote layouts (include/fd_verify_hip.h)
 TXNM_SZ, TXNM_PAYLOAD_SZ_OFF, TXNM_TXN_T_SZ_OFF, TXNM_SRC_IPV4_OFF, TXNM_SRC_TPU_OFF, TXNM_BUNDLE_ID_OFF = 80, 8, 10, 12, 16, 24
@@ -83,6 +85,12 @@ def lib():
         L.fd_verify_hip_tile_submit_frags.argtypes = [vp, u64, vp, vp, vp, vp, vp, vp]
         L.fd_verify_hip_before_frag.restype = c.c_int
         L.fd_verify_hip_before_frag.argtypes = [c.c_uint, u64, u64, u64, u64]
+        L.fd_verify_hip_hist_edges.restype = c.c_int
+        L.fd_verify_hip_hist_edges.argtypes = [u64, u64, vp]
+        L.fd_verify_hip_tile_hist_init.restype = c.c_int
+        L.fd_verify_hip_tile_hist_init.argtypes = [vp, u64, u64]
+        L.fd_verify_hip_tile_hist.restype = c.c_int
+        L.fd_verify_hip_tile_hist.argtypes = [vp, c.c_int, vp, vp, vp]
         _bound = True
     return L
 
@@ -124,6 +132,15 @@ def parse_dev(verifier, n, pool, txn_off, txn_sz, txn_out, txn_t_sz, stream=None
             _ptr(txn_sz, 2 * n, "txn_sz", dev), _ptr(txn_out, 0, "txn_out", dev), _ptr(txn_t_sz, 2 * n, "txn_t_sz", dev))
     with verifier._stream(stream) as h:
         return lib().fd_txn_hip_parse_dev(*args, h)
+
+
+def hist_edges(min_v, max_v):
+    """The 16 left edges fd_histf_new(min_v, max_v) gives (fd_histf.h:88-118);
+    ValueError if max_v <= min_v."""
+    edge = np.zeros(HIST_BUCKET_CNT, np.uint64)
+    if lib().fd_verify_hip_hist_edges(int(min_v), int(max_v), edge.ctypes.data):
+        raise ValueError("max_v must exceed min_v")
+    return edge
 
 
 def before_frag(in_kind, seq, sig, round_robin_cnt, round_robin_idx):
@@ -213,6 +230,20 @@ class VerifyTile:
         out = np.zeros(3, np.float64)
         self._lib.fd_verify_hip_tile_last_timing(self.tile, out.ctypes.data)
         return {"gpu_ms": float(out[0]), "host_ms": float(out[1]), "sigs": int(out[2])}
+
+    def hist_init(self, min_ns, max_ns):
+        """Reset both batch latency histograms with fd_histf edges over [min_ns, max_ns)."""
+        if self._lib.fd_verify_hip_tile_hist_init(self.tile, int(min_ns), int(max_ns)):
+            raise ValueError("max_ns must exceed min_ns")
+
+    def hist(self, which="gpu"):
+        """Batch latency histogram ("gpu" or "host"): counts, left edges (ns), sum (ns)."""
+        counts = np.zeros(HIST_BUCKET_CNT, np.uint64)
+        edge = np.zeros(HIST_BUCKET_CNT, np.uint64)
+        total = np.zeros(1, np.uint64)
+        w = {"gpu": 0, "host": 1}[which]
+        self._lib.fd_verify_hip_tile_hist(self.tile, w, counts.ctypes.data, edge.ctypes.data, total.ctypes.data)
+        return {"counts": counts, "left_edge_ns": edge, "sum_ns": int(total[0])}
 
     def close(self):
         if self.tile:

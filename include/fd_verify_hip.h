@@ -229,6 +229,22 @@ void fd_verify_hip_tile_metrics( fd_verify_hip_tile_t const * tile, ulong out[ 7
    signatures in the batch */
 void fd_verify_hip_tile_last_timing( fd_verify_hip_tile_t const * tile, double out[ 3 ] );
 
+/* Batch latency histograms (SURVEY: the tile's counters plus GPU batch
+   latency), laid out as the reference's fd_histf (src/util/hist/fd_histf.h:
+   16 buckets: [0,min), roughly geometric integer edges from min to max, and
+   [max,inf)), in nanoseconds, one sample per completed batch:
+     which = 0: GPU time (first kernel to results on the host, HIP events);
+     which = 1: the host ordered pass.
+   hist_init resets both with the edges fd_histf_new( min_ns, max_ns ) would
+   give (-1 if max_ns <= min_ns); a new tile starts at 10 us .. 1 s.
+   hist copies out counts, left edges and the sum of the samples (NULL: skip);
+   -1 for another which.  hist_edges is the edge rule alone. */
+#define FD_VERIFY_HIP_HIST_BUCKET_CNT 16
+int fd_verify_hip_hist_edges    ( ulong min_v, ulong max_v, ulong edge[ 16 ] );
+int fd_verify_hip_tile_hist_init( fd_verify_hip_tile_t * tile, ulong min_ns, ulong max_ns );
+int fd_verify_hip_tile_hist     ( fd_verify_hip_tile_t const * tile, int which, ulong counts[ 16 ],
+                                  ulong left_edge_ns[ 16 ], ulong * sum_ns );
+
 #ifdef __cplusplus
 }
 #endif

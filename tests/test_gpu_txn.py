@@ -159,12 +159,13 @@ def test_pipelined_batches_vs_oracle(verifier):
         keep.append((d_off, d_sz))
         tile.submit(b - a, d_pool, d_off, d_sz)
 
-    got = []
+    got, gpu_ms = [], []
     submit(*batches[0])
     for k, (a, b) in enumerate(batches):
         if k + 1 < len(batches):
             submit(*batches[k + 1])
         got.append(tile.complete(bid[a:b]))
+        gpu_ms.append(tile.last_timing()["gpu_ms"])
     res = np.concatenate([g[0] for g in got]); tag = np.concatenate([g[1] for g in got])
     tsz = np.concatenate([g[2] for g in got])
     assert np.array_equal(tsz, etsz)
@@ -174,6 +175,21 @@ def test_pipelined_batches_vs_oracle(verifier):
     assert {k: m[k] for k in o.metrics()} == o.metrics()
     assert m["published"] == int((eres == 0).sum())
     assert len(set(np.unique(res).tolist())) == 5
+    # batch latency histograms: one sample per completed batch in each
+    from firedancer_amd.verify_tile import hist_edges
+    hg, hh = tile.hist("gpu"), tile.hist("host")
+    assert int(hg["counts"].sum()) == len(batches) and int(hh["counts"].sum()) == len(batches)
+    assert np.array_equal(hg["left_edge_ns"], hist_edges(10_000, 1_000_000_000))
+    assert abs(hg["sum_ns"] - sum(round(ms * 1e6) for ms in gpu_ms)) <= len(batches)
+    for ms in gpu_ms:                                            # each sample in its bucket
+        b = int(np.searchsorted(hg["left_edge_ns"], round(ms * 1e6), side="right")) - 1
+        assert hg["counts"][b] > 0
+    tile.hist_init(1_000, 50_000_000)
+    hg = tile.hist("gpu")
+    assert int(hg["counts"].sum()) == 0 and hg["sum_ns"] == 0
+    assert np.array_equal(hg["left_edge_ns"], hist_edges(1_000, 50_000_000))
+    with pytest.raises(ValueError):
+        tile.hist_init(5, 5)
     tile.close()
 
 
