@@ -758,8 +758,103 @@ DEV void b12_digits( u32 bl[5], u32 bh[5], u32 & bmask, u32 const sp[8] ) {
   }
 }
 
+/* lane-parallel group law for k_verify_lat (FD_LAT_LP, see there) */
+DEV u32 lp_lane( void ) { return threadIdx.x & 63u; }
+
+/* every lane of the quad gets lane K's value of x (DPP quad_perm [K,K,K,K]) */
+template<int K>
+DEV void fe_bcast( fe & r, fe const & x ) {
+  #pragma unroll
+  for( int q=0; q<9; q++ ) r.v[q] = (u32)__builtin_amdgcn_mov_dpp( (int)x.v[q], K * 0x55, 0xf, 0xf, false );
+}
+
+/* lane l (0..3) picks operand l: three bit-selects (v_bfi) per limb, no branches */
+DEV void fe_pick4( fe & r, fe const & a0, fe const & a1, fe const & a2, fe const & a3, u32 l ) {
+  u32 m0 = 0u - (u32)(l == 0u), m1 = 0u - (u32)(l == 1u), m2 = 0u - (u32)(l == 2u);
+  #pragma unroll
+  for( int q=0; q<9; q++ ) {
+    u32 t = (m2 & a2.v[q]) | (~m2 & a3.v[q]);
+    t = (m1 & a1.v[q]) | (~m1 & t);
+    r.v[q] = (m0 & a0.v[q]) | (~m0 & t);
+  }
+}
+
+/* X3 = E*F, Y3 = G*H, Z3 = F*G, T3 = E*H, one product per lane */
+DEV void lp_efgh( ge_p3 & r, fe const & E, fe const & F, fe const & G, fe const & H ) {
+  u32 l = lp_lane();
+  fe a, b, p;
+  fe_pick4( a, E, G, F, E, l );
+  fe_pick4( b, F, H, G, H, l );
+  fe_mul( p, a, b );
+  fe_bcast<0>( r.X, p ); fe_bcast<1>( r.Y, p ); fe_bcast<2>( r.Z, p ); fe_bcast<3>( r.T, p );
+}
+
+/* ge_dbl on lanes 0..3 (p uniform over them; r uniform on return, T always) */
+DEV void ge_dbl_lp( ge_p3 & r, ge_p3 const & p ) {
+  fe S, o, s, A, B, C, S2, H, G, F, E;
+  fe_add( S, p.X, p.Y );
+  fe_pick4( o, p.X, p.Y, p.Z, S, lp_lane() );
+  fe_sq( s, o );
+  fe_bcast<0>( A, s ); fe_bcast<1>( B, s ); fe_bcast<2>( C, s ); fe_bcast<3>( S2, s );
+  fe_add( C, C, C );          /* 2Z^2            */
+  fe_add( H, A, B );          /* A+B             */
+  fe_sub( G, A, B );          /* A-B             */
+  fe_add( F, C, G );          /* 2Z^2+A-B        */
+  fe_norm( F, F );
+  fe_sub( E, H, S2 );         /* A+B-(X+Y)^2     */
+  fe_norm( E, E );
+  lp_efgh( r, E, F, G, H );
+}
+
+/* ge_add_cached on lanes 0..3 (T always produced) */
+DEV void ge_add_cached_lp( ge_p3 & r, ge_p3 const & p, ge_cached q, u32 neg ) {
+  fe a, b, x, y, m, A, B, C, D, E, F, G, H;
+  fe_cswap( q.YmX, q.YpX, neg );
+  fe_sub( a, p.Y, p.X ); fe_add( b, p.Y, p.X );
+  u32 l = lp_lane();
+  fe_pick4( x, a, b, p.T, p.Z, l );
+  fe_pick4( y, q.YmX, q.YpX, q.T2d, q.Z2, l );
+  fe_mul( m, x, y );
+  fe_bcast<0>( A, m ); fe_bcast<1>( B, m ); fe_bcast<2>( C, m ); fe_bcast<3>( D, m );
+  fe_sub( E, B, A ); fe_norm( E, E ); fe_add( H, B, A );
+  fe_sub( F, D, C ); fe_add( G, D, C );
+  fe_cswap( F, G, neg );
+  lp_efgh( r, E, F, G, H );
+}
+
+/* ge_add_affc on lanes 0..3 (T always produced): products a*YmX, b*YpX,
+   T*T2d (lane 3 repeats lane 2's), then D = Z1 */
+DEV void ge_add_affc_lp( ge_p3 & r, ge_p3 const & p, ge_affc q, u32 neg ) {
+  fe a, b, x, y, m, A, B, C, E, F, G, H;
+  fe_cswap( q.YmX, q.YpX, neg );
+  fe_sub( a, p.Y, p.X ); fe_add( b, p.Y, p.X );
+  u32 l = lp_lane();
+  fe_pick4( x, a, b, p.T, p.T, l );
+  fe_pick4( y, q.YmX, q.YpX, q.T2d, q.T2d, l );
+  fe_mul( m, x, y );
+  fe_bcast<0>( A, m ); fe_bcast<1>( B, m ); fe_bcast<2>( C, m );
+  fe_sub( E, B, A ); fe_norm( E, E ); fe_add( H, B, A );
+  fe_sub( F, p.Z, C ); fe_add( G, p.Z, C );
+  fe_cswap( F, G, neg );
+  lp_efgh( r, E, F, G, H );
+}
+
+/* build_cached_table on lanes 0..3 (k_verify_lat): 2Q and the additions of
+   Q's cached form (2*Z = 2, the general cached addition) lane-parallel */
+DEV void build_cached_table_lp( u32 * tab, fe const & qx, fe const & qy ) {
+  ge_p3 Q; Q.X = qx; Q.Y = qy; fe_1( Q.Z ); fe_mul( Q.T, Q.X, Q.Y );
+  ge_cached c, c1; ge_to_cached( c1, Q ); store_cached( tab + 0*ATAB_ENT, c1 );
+  ge_p3 Pj;
+  ge_dbl_lp( Pj, Q ); ge_to_cached( c, Pj ); store_cached( tab + 1*ATAB_ENT, c );
+  #pragma unroll 1
+  for( int j=3; j<=8; j++ ) {
+    ge_add_cached_lp( Pj, Pj, c1, 0u ); ge_to_cached( c, Pj ); store_cached( tab + (j-1)*ATAB_ENT, c );
+  }
+}
+
 /* P += [digit bi]B + [digit bi+ND](2^HB B) from the global tables, digits
    taken off the top of bl / bh (b12_digits); T of the result if needT */
+template<bool LP = false>
 DEV void b12_step( ge_p3 & P, u32 bl[5], u32 bh[5], u32 bmask, u32 bi, u32 const * __restrict__ btab,
                    bool needT ) {
   constexpr u32 GW = FD_BTAB_GW, ND = BTG_ND;
@@ -778,9 +873,9 @@ DEV void b12_step( ge_p3 & P, u32 bl[5], u32 bh[5], u32 bmask, u32 bi, u32 const
   bl[0] <<= GW; bh[0] <<= GW;
   u32 const * bt = btab + BT12_OFF;
   ge_affc b; load_affc( b, bt + ib*BT12_ENT );
-  ge_add_affc( P, P, b, negb, true );
+  if( LP ) ge_add_affc_lp( P, P, b, negb ); else ge_add_affc( P, P, b, negb, true );
   load_affc( b, bt + (BT12_N + ic)*BT12_ENT );
-  ge_add_affc( P, P, b, negc, needT );
+  if( LP ) ge_add_affc_lp( P, P, b, negc ); else ge_add_affc( P, P, b, negc, needT );
 }
 
 /* one survivor: DSM slot t (tables at slot t), state column idx[t] (prep's
@@ -985,9 +1080,10 @@ void k_verify_dsm( ulong chunk, u32 const * __restrict__ st, u32 const * __restr
    k_verify_dsm's (fd_ed25519_user.c:135-230). */
 
 #define LAT_MAX_N 256ul      /* the largest call fd_ed25519_hip_set_small_batch can send down this path */
-#define LAT_DEFAULT_N 8ul    /* default: calls of up to 8 records (tools/bench_batch_latency.py: this path
-                                476-495 us vs 742-744 us at 1-4 records, 720 vs 749 at 8; the bulk
-                                kernels win from 16 up, 750 vs 849 us, profiles/r02z_latency) */
+#define LAT_DEFAULT_N 32ul   /* default: calls of up to 32 records (tools/bench_batch_latency.py with the
+                                lane-parallel chains: this path 334-493 us vs 770-781 us at 1-32
+                                records; the bulk kernels win from 64 up, 686 vs 721 us,
+                                profiles/r02zd_latency_lp) */
 #define LAT_COPY_MAX_N 32ul  /* calls of up to 32 signatures run one copy per XCD (k_verify_lat) */
 #ifndef FD_LAT_COPIES
 #define FD_LAT_COPIES 1      /* 0: one workgroup per signature always (A/B switch) */
@@ -1015,6 +1111,26 @@ DEV void lat_get( ge_p3 & P, u32 const * d ) {
   for( int q=0; q<9; q++ ) { P.X.v[q] = d[q]; P.Y.v[q] = d[9+q]; P.Z.v[q] = d[18+q]; P.T.v[q] = d[27+q]; }
 }
 
+/* FD_LAT_LP: the latency kernel's chains run their group law on lanes 0..3
+   of the wave instead of lane 0 alone.  Each formula is two rounds of four
+   independent products (dbl: X^2, Y^2, Z^2, (X+Y)^2, then E*F, G*H, F*G,
+   E*H; add: the four operand products, then the same four); lane l computes
+   product l of a round and a DPP quad broadcast hands the four results to every lane,
+   which then holds the whole point.  The values and their normalisation
+   points are those of ge_dbl / ge_add_cached (same bounds), so a chain issues
+   about 2.2x fewer instructions for the same result. */
+#ifndef FD_LAT_LP
+#define FD_LAT_LP 1
+#endif
+
+DEV void lat_dbl( ge_p3 & P, bool needT ) {
+#if FD_LAT_LP
+  (void)needT; ge_dbl_lp( P, P );
+#else
+  ge_dbl( P, P, needT );
+#endif
+}
+
 /* another copy of signature i already finished this call (seq) */
 DEV bool lat_done( ulong const * done, ulong i, ulong seq ) {
   return __hip_atomic_load( done + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT ) == seq;
@@ -1036,10 +1152,14 @@ DEV void lat_chain( ge_p3 & P, u32 const * tab, u32 const * ident, u32 kd[8], u3
     ge_cached e; load_cached( e, tab_entry( tab, ident, mag ) );
     if( w != (int)D-1 ) {
       #pragma unroll 1
-      for( int j=0; j<3; j++ ) ge_dbl( P, P, false );
-      ge_dbl( P, P, true );
+      for( int j=0; j<3; j++ ) lat_dbl( P, false );
+      lat_dbl( P, true );
     }
+#if FD_LAT_LP
+    ge_add_cached_lp( P, P, e, neg );
+#else
     ge_add_cached( P, P, e, neg, true );
+#endif
     if( copies > 1u && lat_done( done, i, seq ) ) break;
   }
 }
@@ -1127,8 +1247,8 @@ void k_verify_lat( ulong n, uchar const * __restrict__ sigs, uchar const * __res
     return;
   }
 
-  /* ---- phase 2 ---- */
-  if( lane == 0u ) {
+  /* ---- phase 2 (lanes 0..3 with FD_LAT_LP, else lane 0) ---- */
+  if( lane < (FD_LAT_LP ? 4u : 1u) ) {
     ge_p3 P;
     if( wave < 2u ) {
       u32 xw[8], yw[8], kd[8];
@@ -1142,7 +1262,11 @@ void k_verify_lat( ulong n, uchar const * __restrict__ sigs, uchar const * __res
       fe_neg( nx, x ); fe_norm( nx, nx );
       if( wave == 0u ) fe_cmov( nx, x, L.k1neg );                          /* k1 < 0: [|k1|](+A) */
       u32 * tab = wave ? tabR : tabA;
+#if FD_LAT_LP
+      build_cached_table_lp( tab, nx, y );
+#else
       build_cached_table( tab, nx, y );
+#endif
       lat_chain( P, tab, ident, kd, L.D, done, i, seq, copies );
     } else {
       u32 bl[5], bh[5];
@@ -1154,14 +1278,14 @@ void k_verify_lat( ulong n, uchar const * __restrict__ sigs, uchar const * __res
       for( int bi=(int)BTG_ND-1; bi>=0; bi-- ) {
         if( bi != (int)BTG_ND-1 ) {
           #pragma unroll 1
-          for( int j=0; j<FD_BTAB_GW-1; j++ ) ge_dbl( P, P, false );
-          ge_dbl( P, P, true );
+          for( int j=0; j<FD_BTAB_GW-1; j++ ) lat_dbl( P, false );
+          lat_dbl( P, true );
         }
-        b12_step( P, bl, bh, bmask, (u32)bi, btab, true );
+        b12_step<FD_LAT_LP != 0>( P, bl, bh, bmask, (u32)bi, btab, true );
         if( copies > 1u && lat_done( done, i, seq ) ) break;
       }
     }
-    lat_put( L.P[wave], P );
+    if( lane == 0u ) lat_put( L.P[wave], P );
   }
   __syncthreads();
 

@@ -114,13 +114,16 @@ void                   fd_ed25519_hip_set_errmode( fd_ed25519_hip_ctx_t * ctx, i
    (k, 1) instead (252 doublings): an A/B and test switch, same results. */
 void                   fd_ed25519_hip_set_halfsize( fd_ed25519_hip_ctx_t * ctx, int on );
 
-/* Calls of at most max_n records (default 8, at most 256) whose count is
+/* Calls of at most max_n records (default 32, at most 256) whose count is
    known on the host run on the latency path: one workgroup of three waves per
    signature (the A and R decodes, the hash, and the [k1]A, [k2]R and B terms
    run side by side; calls of up to 32 records race one copy per XCD),
    instead of one lane per signature through k_verify_prep / k_verify_dsm.
    Same verdicts and codes; 0 sends every call to the bulk kernels.  The
-   drop-in entry points use the context default. */
+   drop-in entry points use the context default.  Each of a latency call's
+   n x copies workgroups holds a whole CU until it ends (a 32-record call:
+   all 256 CUs for ~0.5 ms), so a context whose small calls share the GPU
+   with throughput work on other streams should lower the limit or set 0. */
 void                   fd_ed25519_hip_set_small_batch( fd_ed25519_hip_ctx_t * ctx, ulong max_n );
 
 /* Test hook: the device half-size reduction of n scalars k < L (d_k: 8 LE

@@ -1,7 +1,7 @@
 """GPU: the small-batch latency path (k_verify_lat, one workgroup of three
 waves per signature) against the bulk kernels and the oracle.
 
-Calls of at most fd_ed25519_hip_set_small_batch records (default 8, here
+Calls of at most fd_ed25519_hip_set_small_batch records (default 32, here
 raised to 256) whose count is known on the host take k_verify_lat; the
 drop-in entry points' single calls and the 4-record corpus KAT in the other
 files already do.  Here the same records go through both paths and must give
@@ -18,7 +18,7 @@ pytestmark = pytest.mark.gpu
 
 from firedancer_amd import ERRMODE_AVX512, ERRMODE_REF  # noqa: E402
 
-LAT_DEFAULT = 8
+LAT_DEFAULT = 32
 
 
 @pytest.fixture
@@ -136,14 +136,15 @@ def test_latency_path_racing_copies(lat):
 
 
 def test_default_small_batch_limit(verifier):
-    """By default only calls of up to 8 records take k_verify_lat; 1..9-record
-    calls give the oracle's codes either way."""
-    sigs, pubs, pool, moff, msz = _signed_set(45, 0x5eb, max_msg=200)
+    """By default only calls of up to 32 records take k_verify_lat; calls of
+    1..9, 31..34 records give the oracle's codes either way."""
+    steps = list(range(1, 10)) + [31, 32, 33, 34]
+    sigs, pubs, pool, moff, msz = _signed_set(sum(steps), 0x5eb, max_msg=200)
     exp = O.verify_many(sigs, pubs, pool, moff, msz, O.ERRMODE_AVX512)
     got, lo = [], 0
-    for step in range(1, 10):
+    for step in steps:
         c, _b = verifier.verify_host(sigs[lo:lo + step], pubs[lo:lo + step], pool, moff[lo:lo + step],
                                      msz[lo:lo + step])
         got.append(c)
         lo += step
-    assert lo == 45 and np.array_equal(np.concatenate(got), exp)
+    assert lo == sum(steps) and np.array_equal(np.concatenate(got), exp)

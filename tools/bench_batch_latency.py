@@ -7,7 +7,7 @@ p50 / p99 wall time per call and n / p50 as verifies/s.  Each n up to 256
 runs twice: on k_verify_lat (one workgroup per signature; <= 32 race one
 copy per XCD; set_small_batch(256)) and on k_verify_prep + k_verify_dsm
 (set_small_batch(0), keys "<n>_bulk").  The crossover sets the default
-small-batch limit (8).
+small-batch limit (32).
 
 usage: python tools/bench_batch_latency.py [calls]   -> one JSON line
 """
@@ -58,7 +58,7 @@ def main():
                              "path": "k_verify_lat" + (" x8 copies" if n <= 32 else "") if lat
                              else "k_verify_prep + k_verify_dsm"}
         print(key, out["sizes"][key], file=sys.stderr)
-    v.set_small_batch(8)
+    v.set_small_batch(32)
     v.close()
     print(json.dumps(out))
 
