@@ -25,6 +25,12 @@
      k_bitmap       verdict bitmap from codes (64-bit ballot per wave)
      k_group_reduce batch_single_msg / per-txn semantics over sig codes
 
+   Small calls (count on the host, <= ctx->lat_max records, default 32) take
+   k_verify_lat instead: one 768-thread workgroup per signature (and per
+   racing copy), three working waves that decode A / decode R / hash, then run
+   the [k1]A, [k2]R and B chains with each chain's group law on four lanes
+   (FD_LAT_LP), joined in LDS.
+
    Reference semantics: fd_ed25519_user.c:135-310 (see fd_ed25519_dev.h for
    the per-function citations). */
 
