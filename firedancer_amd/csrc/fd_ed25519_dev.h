@@ -75,6 +75,11 @@ DEV void fe_inv2( fe & r )   { fe_set( r, 0x1ffffff7u,0x1fffffffu,0x1fffffffu,0x
 
 DEV u64 fe_mad64( u32 a, u32 b, u64 c ) { u64 r = c + (u64)a * b; asm( "" : "+v"(r) ); return r; }
 DEV u64 fe_mul64( u32 a, u32 b )        { u64 r = (u64)a * b;     asm( "" : "+v"(r) ); return r; }
+/* FREE = true leaves the sums open to re-association (more independent
+   chains per product for a wave alone on its SIMD, at an extra 64-bit add
+   per split column): the latency kernel's lane-parallel products */
+template<bool FREE> DEV u64 fe_madT( u32 a, u32 b, u64 c ) { return FREE ? c + (u64)a * b : fe_mad64( a, b, c ); }
+template<bool FREE> DEV u64 fe_mulT( u32 a, u32 b )        { return FREE ? (u64)a * b : fe_mul64( a, b ); }
 
 /* Product columns (column k = sum over i+j=k, 0<=i,j<=8):
      high column 9+j is kept as an unsplit 64-bit sum H_{9+j} (< 2^63): a
@@ -99,7 +104,7 @@ DEV void fe_fin( fe & r, u32 o[9], u64 l ) {   /* column-8 split + fold, output 
   for( int i=0; i<9; i++ ) r.v[i] = o[i];
 }
 
-template<int N>
+template<int N, bool FREE = false>
 DEV void fe_mulN( fe * const r[N], fe const * const a[N], fe const * const b[N] ) {
   u32 o[N][9];
   u64 l[N], hp[N], h[N];
@@ -110,17 +115,17 @@ DEV void fe_mulN( fe * const r[N], fe const * const a[N], fe const * const b[N] 
     for( int i=0; i<=8; i++ ) {
       if( j < 8 && i <= 7-j ) {
         #pragma unroll
-        for( int n=0; n<N; n++ ) h[n] = (i == 0) ? fe_mul64( a[n]->v[c-8+i], b[n]->v[8-i] ) : fe_mad64( a[n]->v[c-8+i], b[n]->v[8-i], h[n] );
+        for( int n=0; n<N; n++ ) h[n] = (i == 0) ? fe_mulT<FREE>( a[n]->v[c-8+i], b[n]->v[8-i] ) : fe_madT<FREE>( a[n]->v[c-8+i], b[n]->v[8-i], h[n] );
       }
       if( i <= j ) {
         #pragma unroll
-        for( int n=0; n<N; n++ ) l[n] = (j == 0) ? fe_mul64( a[n]->v[0], b[n]->v[0] ) : fe_mad64( a[n]->v[i], b[n]->v[j-i], l[n] );
+        for( int n=0; n<N; n++ ) l[n] = (j == 0) ? fe_mulT<FREE>( a[n]->v[0], b[n]->v[0] ) : fe_madT<FREE>( a[n]->v[i], b[n]->v[j-i], l[n] );
       }
     }
     #pragma unroll
     for( int n=0; n<N; n++ ) {
-      if( j < 8 ) l[n] = fe_mad64( (u32)h[n], 1216u, l[n] );
-      if( j > 0 ) l[n] = fe_mad64( (u32)(hp[n] >> 32), 9728u, l[n] );
+      if( j < 8 ) l[n] = fe_madT<FREE>( (u32)h[n], 1216u, l[n] );
+      if( j > 0 ) l[n] = fe_madT<FREE>( (u32)(hp[n] >> 32), 9728u, l[n] );
       if( j < 8 ) { o[n][j] = (u32)l[n] & FE_M29; FE_OPAQUE( o[n][j] ); l[n] >>= 29; }
       hp[n] = h[n];
     }
@@ -131,7 +136,7 @@ DEV void fe_mulN( fe * const r[N], fe const * const a[N], fe const * const b[N] 
 }
 
 /* squares: off-diagonal products taken once against 2*a_i */
-template<int N>
+template<int N, bool FREE = false>
 DEV void fe_sqN( fe * const r[N], fe const * const a[N] ) {
   u32 d[N][9], o[N][9];
   u64 l[N], hp[N], h[N];
@@ -148,22 +153,22 @@ DEV void fe_sqN( fe * const r[N], fe const * const a[N] ) {
       int hi = c - 8 + i;                             /* high: d[hi]*a[c-hi], 2*hi < c */
       if( j < 8 && 2*hi < c ) {
         #pragma unroll
-        for( int n=0; n<N; n++ ) h[n] = (i == 0) ? fe_mul64( d[n][hi], a[n]->v[c-hi] ) : fe_mad64( d[n][hi], a[n]->v[c-hi], h[n] );
+        for( int n=0; n<N; n++ ) h[n] = (i == 0) ? fe_mulT<FREE>( d[n][hi], a[n]->v[c-hi] ) : fe_madT<FREE>( d[n][hi], a[n]->v[c-hi], h[n] );
       }
       if( 2*i < j ) {                                 /* j >= 1: onto the carry */
         #pragma unroll
-        for( int n=0; n<N; n++ ) l[n] = fe_mad64( d[n][i], a[n]->v[j-i], l[n] );
+        for( int n=0; n<N; n++ ) l[n] = fe_madT<FREE>( d[n][i], a[n]->v[j-i], l[n] );
       }
     }
     #pragma unroll
     for( int n=0; n<N; n++ ) {
-      if( j < 8 && (c & 1) == 0 ) h[n] = (c == 16) ? fe_mul64( a[n]->v[8], a[n]->v[8] ) : fe_mad64( a[n]->v[c/2], a[n]->v[c/2], h[n] );
-      if( (j & 1) == 0 ) l[n] = (j == 0) ? fe_mul64( a[n]->v[0], a[n]->v[0] ) : fe_mad64( a[n]->v[j/2], a[n]->v[j/2], l[n] );
+      if( j < 8 && (c & 1) == 0 ) h[n] = (c == 16) ? fe_mulT<FREE>( a[n]->v[8], a[n]->v[8] ) : fe_madT<FREE>( a[n]->v[c/2], a[n]->v[c/2], h[n] );
+      if( (j & 1) == 0 ) l[n] = (j == 0) ? fe_mulT<FREE>( a[n]->v[0], a[n]->v[0] ) : fe_madT<FREE>( a[n]->v[j/2], a[n]->v[j/2], l[n] );
     }
     #pragma unroll
     for( int n=0; n<N; n++ ) {
-      if( j < 8 ) l[n] = fe_mad64( (u32)h[n], 1216u, l[n] );
-      if( j > 0 ) l[n] = fe_mad64( (u32)(hp[n] >> 32), 9728u, l[n] );
+      if( j < 8 ) l[n] = fe_madT<FREE>( (u32)h[n], 1216u, l[n] );
+      if( j > 0 ) l[n] = fe_madT<FREE>( (u32)(hp[n] >> 32), 9728u, l[n] );
       if( j < 8 ) { o[n][j] = (u32)l[n] & FE_M29; FE_OPAQUE( o[n][j] ); l[n] >>= 29; }
       hp[n] = h[n];
     }
@@ -180,6 +185,15 @@ DEV void fe_mul( fe & r, fe const & a, fe const & b ) {
 DEV void fe_mul2( fe & r, fe const & a, fe const & b, fe & s, fe const & c, fe const & d ) {
   fe * const R[2] = { &r, &s }; fe const * const A[2] = { &a, &c }; fe const * const B[2] = { &b, &d };
   fe_mulN<2>( R, A, B );
+}
+/* one product / square with open sums (FREE, see fe_madT) */
+DEV void fe_mul_free( fe & r, fe const & a, fe const & b ) {
+  fe * const R[1] = { &r }; fe const * const A[1] = { &a }; fe const * const B[1] = { &b };
+  fe_mulN<1, true>( R, A, B );
+}
+DEV void fe_sq_free( fe & r, fe const & a ) {
+  fe * const R[1] = { &r }; fe const * const A[1] = { &a };
+  fe_sqN<1, true>( R, A );
 }
 DEV void fe_sq( fe & r, fe const & a ) {
   fe * const R[1] = { &r }; fe const * const A[1] = { &a };

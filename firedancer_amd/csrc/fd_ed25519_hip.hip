@@ -765,6 +765,24 @@ DEV void b12_digits( u32 bl[5], u32 bh[5], u32 & bmask, u32 const sp[8] ) {
 }
 
 /* lane-parallel group law for k_verify_lat (FD_LAT_LP, see there) */
+#ifndef FD_LAT_FREE
+#define FD_LAT_FREE 1    /* lane-parallel products with open sums (fe_mul_free) */
+#endif
+DEV void lp_mul( fe & r, fe const & a, fe const & b ) {
+#if FD_LAT_FREE
+  fe_mul_free( r, a, b );
+#else
+  fe_mul( r, a, b );
+#endif
+}
+DEV void lp_sq( fe & r, fe const & a ) {
+#if FD_LAT_FREE
+  fe_sq_free( r, a );
+#else
+  fe_sq( r, a );
+#endif
+}
+
 DEV u32 lp_lane( void ) { return threadIdx.x & 63u; }
 
 /* every lane of the quad gets lane K's value of x (DPP quad_perm [K,K,K,K]) */
@@ -791,7 +809,7 @@ DEV void lp_efgh( ge_p3 & r, fe const & E, fe const & F, fe const & G, fe const 
   fe a, b, p;
   fe_pick4( a, E, G, F, E, l );
   fe_pick4( b, F, H, G, H, l );
-  fe_mul( p, a, b );
+  lp_mul( p, a, b );
   fe_bcast<0>( r.X, p ); fe_bcast<1>( r.Y, p ); fe_bcast<2>( r.Z, p ); fe_bcast<3>( r.T, p );
 }
 
@@ -800,7 +818,7 @@ DEV void ge_dbl_lp( ge_p3 & r, ge_p3 const & p ) {
   fe S, o, s, A, B, C, S2, H, G, F, E;
   fe_add( S, p.X, p.Y );
   fe_pick4( o, p.X, p.Y, p.Z, S, lp_lane() );
-  fe_sq( s, o );
+  lp_sq( s, o );
   fe_bcast<0>( A, s ); fe_bcast<1>( B, s ); fe_bcast<2>( C, s ); fe_bcast<3>( S2, s );
   fe_add( C, C, C );          /* 2Z^2            */
   fe_add( H, A, B );          /* A+B             */
@@ -820,7 +838,7 @@ DEV void ge_add_cached_lp( ge_p3 & r, ge_p3 const & p, ge_cached q, u32 neg ) {
   u32 l = lp_lane();
   fe_pick4( x, a, b, p.T, p.Z, l );
   fe_pick4( y, q.YmX, q.YpX, q.T2d, q.Z2, l );
-  fe_mul( m, x, y );
+  lp_mul( m, x, y );
   fe_bcast<0>( A, m ); fe_bcast<1>( B, m ); fe_bcast<2>( C, m ); fe_bcast<3>( D, m );
   fe_sub( E, B, A ); fe_norm( E, E ); fe_add( H, B, A );
   fe_sub( F, D, C ); fe_add( G, D, C );
@@ -837,7 +855,7 @@ DEV void ge_add_affc_lp( ge_p3 & r, ge_p3 const & p, ge_affc q, u32 neg ) {
   u32 l = lp_lane();
   fe_pick4( x, a, b, p.T, p.T, l );
   fe_pick4( y, q.YmX, q.YpX, q.T2d, q.T2d, l );
-  fe_mul( m, x, y );
+  lp_mul( m, x, y );
   fe_bcast<0>( A, m ); fe_bcast<1>( B, m ); fe_bcast<2>( C, m );
   fe_sub( E, B, A ); fe_norm( E, E ); fe_add( H, B, A );
   fe_sub( F, p.Z, C ); fe_add( G, p.Z, C );
