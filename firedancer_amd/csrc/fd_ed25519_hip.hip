@@ -1155,9 +1155,14 @@ DEV void lat_dbl( ge_p3 & P, bool needT ) {
 #endif
 }
 
-/* another copy of signature i already finished this call (seq) */
+/* another copy of signature i already finished this call (seq); the first
+   active lane's reading, so that a lane-parallel chain leaves its loop as a
+   whole */
 DEV bool lat_done( ulong const * done, ulong i, ulong seq ) {
-  return __hip_atomic_load( done + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT ) == seq;
+  ulong v = __hip_atomic_load( done + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT );
+  u32 lo = (u32)__builtin_amdgcn_readfirstlane( (int)(u32)v );
+  u32 hi = (u32)__builtin_amdgcn_readfirstlane( (int)(u32)(v >> 32) );
+  return (((ulong)hi << 32) | lo) == seq;
 }
 
 /* [k](Q) by fixed signed radix-16 windows over a lane's table (digits kd,
