@@ -227,10 +227,16 @@ DEV void fe_norm( fe & r, fe const & a ) {
   r.v[0] += 19u * (x >> 23);
 }
 
+/* FREE: the open-sum products (fe_mul_free / fe_sq_free), for a wave alone
+   on its SIMD (k_verify_lat); the bulk kernels use the default */
+template<bool FREE> DEV void fe_mulF( fe & r, fe const & a, fe const & b ) { if( FREE ) fe_mul_free( r, a, b ); else fe_mul( r, a, b ); }
+template<bool FREE> DEV void fe_sqF( fe & r, fe const & a ) { if( FREE ) fe_sq_free( r, a ); else fe_sq( r, a ); }
+
+template<bool FREE = false>
 DEV void fe_sqn( fe & r, fe const & a, int n ) {
-  fe_sq( r, a );
+  fe_sqF<FREE>( r, a );
   #pragma unroll 1
-  for( int i=1; i<n; i++ ) fe_sq( r, r );
+  for( int i=1; i<n; i++ ) fe_sqF<FREE>( r, r );
 }
 
 /* any bounded a -> canonical [0,p): two carry passes leave limbs in range and
@@ -271,20 +277,21 @@ DEV void fe_cmov( fe & r, fe const & a, u32 mask ) {   /* r = mask ? a : r */
 }
 
 /* z^(2^252-3): fd_f25519.c:25-74 (same exponent; this addition chain) */
+template<bool FREE = false>
 DEV void fe_pow22523( fe & out, fe const & z ) {
   fe z2, z9, z11, a, b, c, t;
-  fe_sq( z2, z );                         /* 2 */
-  fe_sqn( t, z2, 2 ); fe_mul( z9, t, z ); /* 9 */
-  fe_mul( z11, z9, z2 );                  /* 11 */
-  fe_sq( t, z11 ); fe_mul( a, t, z9 );    /* a = z^(2^5-1) */
-  fe_sqn( t, a, 5 );   fe_mul( b, t, a ); /* 2^10-1 */
-  fe_sqn( t, b, 10 );  fe_mul( c, t, b ); /* 2^20-1 */
-  fe_sqn( t, c, 20 );  fe_mul( t, t, c ); /* 2^40-1 */
-  fe_sqn( t, t, 10 );  fe_mul( b, t, b ); /* b = 2^50-1 */
-  fe_sqn( t, b, 50 );  fe_mul( c, t, b ); /* c = 2^100-1 */
-  fe_sqn( t, c, 100 ); fe_mul( t, t, c ); /* 2^200-1 */
-  fe_sqn( t, t, 50 );  fe_mul( t, t, b ); /* 2^250-1 */
-  fe_sqn( t, t, 2 );   fe_mul( out, t, z );  /* 2^252-3 */
+  fe_sqF<FREE>( z2, z );                                  /* 2 */
+  fe_sqn<FREE>( t, z2, 2 ); fe_mulF<FREE>( z9, t, z );   /* 9 */
+  fe_mulF<FREE>( z11, z9, z2 );                           /* 11 */
+  fe_sqF<FREE>( t, z11 ); fe_mulF<FREE>( a, t, z9 );      /* a = z^(2^5-1) */
+  fe_sqn<FREE>( t, a, 5 );   fe_mulF<FREE>( b, t, a );   /* 2^10-1 */
+  fe_sqn<FREE>( t, b, 10 );  fe_mulF<FREE>( c, t, b );   /* 2^20-1 */
+  fe_sqn<FREE>( t, c, 20 );  fe_mulF<FREE>( t, t, c );   /* 2^40-1 */
+  fe_sqn<FREE>( t, t, 10 );  fe_mulF<FREE>( b, t, b );   /* b = 2^50-1 */
+  fe_sqn<FREE>( t, b, 50 );  fe_mulF<FREE>( c, t, b );   /* c = 2^100-1 */
+  fe_sqn<FREE>( t, c, 100 ); fe_mulF<FREE>( t, t, c );   /* 2^200-1 */
+  fe_sqn<FREE>( t, t, 50 );  fe_mulF<FREE>( t, t, b );   /* 2^250-1 */
+  fe_sqn<FREE>( t, t, 2 );   fe_mulF<FREE>( out, t, z ); /* 2^252-3 */
 }
 
 /* z^(p-2) = (z^(2^252-3))^8 * z^3 */
@@ -409,19 +416,20 @@ DEV void ge_to_cached( ge_cached & c, ge_p3 const & p ) {
    Returns bit0 = not on curve (u/v not a square), bit1 = x==0 with sign bit
    set (AVX-512 rejects in decode; the ref backend keeps x=0 and rejects it
    as small order).  On success r = (x, y, 1, xy) with x, y canonical. */
+template<bool FREE = false>
 DEV u32 ge_decode( ge_p3 & r, u32 const w[8] ) {
   fe y, y2, u, v, v3, v7, t, x, chk, one, d;
   u32 sign = w[7] >> 31;
   fe_from_words( y, w );
   fe_1( one ); fe_d( d );
-  fe_sq( y2, y );
+  fe_sqF<FREE>( y2, y );
   fe_sub( u, y2, one );                 /* u = y^2 - 1 */
-  fe_mul( v, y2, d ); fe_add( v, v, one ); /* v = d y^2 + 1 */
-  fe_sq( v3, v ); fe_mul( v3, v3, v );  /* v^3 */
-  fe_sq( v7, v3 ); fe_mul( v7, v7, v ); /* v^7 */
-  fe_mul( t, u, v7 ); fe_pow22523( t, t );
-  fe_mul( x, u, v3 ); fe_mul( x, x, t ); /* x = u v^3 (u v^7)^((p-5)/8) */
-  fe_sq( chk, x ); fe_mul( chk, chk, v ); /* v x^2 */
+  fe_mulF<FREE>( v, y2, d ); fe_add( v, v, one ); /* v = d y^2 + 1 */
+  fe_sqF<FREE>( v3, v ); fe_mulF<FREE>( v3, v3, v );  /* v^3 */
+  fe_sqF<FREE>( v7, v3 ); fe_mulF<FREE>( v7, v7, v ); /* v^7 */
+  fe_mulF<FREE>( t, u, v7 ); fe_pow22523<FREE>( t, t );
+  fe_mulF<FREE>( x, u, v3 ); fe_mulF<FREE>( x, x, t ); /* x = u v^3 (u v^7)^((p-5)/8) */
+  fe_sqF<FREE>( chk, x ); fe_mulF<FREE>( chk, chk, v ); /* v x^2 */
   fe cu, cc, nu;
   fe_canon( cu, u ); fe_canon( cc, chk );
   fe_neg( nu, cu ); fe_canon( nu, nu );

@@ -1228,7 +1228,7 @@ void k_verify_lat( ulong n, uchar const * __restrict__ sigs, uchar const * __res
       u32 w[8];
       load_words( w, wave ? sigs + 64*i : pubs + 32*i, 8 );
       ge_p3 Q;
-      u32 f = ge_decode( Q, w );
+      u32 f = ge_decode<FD_LAT_FREE != 0>( Q, w );
       bool small = !(f & 1u) && ge_affine_is_small_order( Q );
       u32 xw[8], yw[8];
       fe_to_words( xw, Q.X ); fe_to_words( yw, Q.Y );
