@@ -766,7 +766,7 @@ DEV void b12_digits( u32 bl[5], u32 bh[5], u32 & bmask, u32 const sp[8] ) {
 
 /* lane-parallel group law for k_verify_lat (FD_LAT_LP, see there) */
 #ifndef FD_LAT_FREE
-#define FD_LAT_FREE 1    /* lane-parallel products with open sums (fe_mul_free) */
+#define FD_LAT_FREE 1    /* k_verify_lat: lane-parallel products and the decodes with open sums (fe_mul_free) */
 #endif
 DEV void lp_mul( fe & r, fe const & a, fe const & b ) {
 #if FD_LAT_FREE
