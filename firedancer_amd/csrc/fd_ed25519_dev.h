@@ -44,11 +44,7 @@ struct fe { u32 v[9]; };
    overlaps consecutive multiplies of a long chain (pow22523, the ladder) until
    the kernel runs out of VGPRs and spills to AGPRs; fencing each multiply
    keeps the live set to ~one product column pair plus the operands. */
-#ifndef FE_NO_FENCE
 #define FE_SCHED_FENCE() __builtin_amdgcn_sched_barrier( 0 )
-#else
-#define FE_SCHED_FENCE()
-#endif
 
 DEV void fe_set( fe & r, u32 c0, u32 c1, u32 c2, u32 c3, u32 c4, u32 c5, u32 c6, u32 c7, u32 c8 ) {
   r.v[0]=c0; r.v[1]=c1; r.v[2]=c2; r.v[3]=c3; r.v[4]=c4; r.v[5]=c5; r.v[6]=c6; r.v[7]=c7; r.v[8]=c8;
@@ -67,11 +63,7 @@ DEV void fe_inv2( fe & r )   { fe_set( r, 0x1ffffff7u,0x1fffffffu,0x1fffffffu,0x
 /* split limbs pass through an empty asm so the compiler keeps the masked
    limb instead of re-deriving 2*limb from the unmasked column as
    (col << 1) & 0x3ffffffe (an extra v_and per limb in squaring chains) */
-#ifndef FE_NO_OPAQUE_LIMB
 #define FE_OPAQUE( x ) asm( "" : "+v"( x ) )
-#else
-#define FE_OPAQUE( x )
-#endif
 
 DEV u64 fe_mad64( u32 a, u32 b, u64 c ) { u64 r = c + (u64)a * b; asm( "" : "+v"(r) ); return r; }
 DEV u64 fe_mul64( u32 a, u32 b )        { u64 r = (u64)a * b;     asm( "" : "+v"(r) ); return r; }
@@ -813,15 +805,6 @@ DEV u32 lo32( u64 x ) { return (u32)x; }
 DEV u32 hi32( u64 x ) { return (u32)(x >> 32); }
 typedef u32 v2u32 __attribute__((ext_vector_type(2)));
 DEV u64 mk64( u32 lo, u32 hi ) { v2u32 v = { lo, hi }; return __builtin_bit_cast( u64, v ); }
-#ifndef FD_SHA_ALIGNBIT
-#define FD_SHA_ALIGNBIT 1
-#endif
-#if !FD_SHA_ALIGNBIT                            /* the plain C forms, for A/B runs */
-DEV u64 ror64( u64 x, int n ) { return (x >> n) | (x << (64 - n)); }
-DEV u64 shr64( u64 x, int n ) { return x >> n; }
-DEV u64 xor3_64( u64 a, u64 b, u64 c ) { return a ^ b ^ c; }
-DEV u64 maj64( u64 a, u64 b, u64 c ) { return (a & b) ^ (a & c) ^ (b & c); }
-#else
 DEV u64 ror64( u64 x, int n ) {                 /* n a compile-time constant in (0, 64) */
   u32 lo = lo32( x ), hi = hi32( x );
   if( n >= 32 ) { u32 t = lo; lo = hi; hi = t; n -= 32; }
@@ -839,7 +822,6 @@ DEV u64 maj64( u64 a, u64 b, u64 c ) {          /* majority: (a&b) ^ (a&c) ^ (b&
   return mk64( __builtin_amdgcn_bitop3_b32( lo32( a ), lo32( b ), lo32( c ), 0xe8 ),
                __builtin_amdgcn_bitop3_b32( hi32( a ), hi32( b ), hi32( c ), 0xe8 ) );
 }
-#endif
 
 /* round constants in constant memory: the round index is wave-uniform, so
    each K[t] is a scalar load rather than 160 VGPRs of hoisted literals */

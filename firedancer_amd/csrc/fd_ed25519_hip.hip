@@ -19,7 +19,7 @@
                     identity is one shared entry); [k1](+-A) + [k2](-R) by
                     fixed signed radix-16 windows, [k2*S mod L]B in signed
                     radix 2^12 from two L2-resident global tables ([0..2048]B
-                    and [0..2048]2^132 B, FD_BTAB_W12): every lane adds at the
+                    and [0..2048]2^132 B): every lane adds at the
                     same positions, one window count per wave; identity
                     check; int8 code
      k_bitmap       verdict bitmap from codes (64-bit ballot per wave)
@@ -28,8 +28,8 @@
    Small calls (count on the host, <= ctx->lat_max records, default 32) take
    k_verify_lat instead: one 768-thread workgroup per signature (and per
    racing copy), three working waves that decode A / decode R / hash, then run
-   the [k1]A, [k2]R and B chains with each chain's group law on four lanes
-   (FD_LAT_LP), joined in LDS.
+   the [k1]A, [k2]R and B chains with each chain's group law on four lanes,
+   joined in LDS.
 
    Reference semantics: fd_ed25519_user.c:135-310 (see fd_ed25519_dev.h for
    the per-function citations). */
@@ -41,6 +41,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <condition_variable>
 #include <mutex>
 
 #define FD_CHECK( x ) do {                                                            \
@@ -61,90 +62,50 @@
 #define F_A_SMALL    (1u<<5)
 #define F_R_SMALL    (1u<<6)
 
-#define BTAB_N      129            /* 0..128 multiples of B */
-/* FD_BTAB_PACK: LDS B-table entries packed like the A/R entries (3 x 8 words,
-   6 ds_read_b128 per lookup) instead of 3 x 9 limbs + pad (7).  Off: the
-   unpacking costs more than the LDS bytes it saves (A/B 123.8-124.2 vs
-   124.9-125.2 M verifies/s). */
-#ifndef FD_BTAB_PACK
-#define FD_BTAB_PACK 0
-#endif
-#if FD_BTAB_PACK
-#define BTAB_STRIDE 24             /* affine cached (1/2-scaled): YmX, YpX, T2d (8 packed words each) */
-#else
-#define BTAB_STRIDE 28             /* affine cached (1/2-scaled): YmX, YpX, T2d (9 limbs each) + pad */
-#endif
+/* Signing's radix-256 B tables (k_sign, in LDS): [j]B and [j](2^128 B) for
+   j in 0..128, 1/2-scaled affine cached, 3 x 9 limbs + pad per entry. */
+#define BTAB_N      129
+#define BTAB_STRIDE 28
 #define BTAB_WORDS  (BTAB_N*BTAB_STRIDE)   /* one table; d_btab holds [j]B then [j](2^128 B) */
-/* FD_ATAB_PACK: A/R table entries packed to 8 words per element (one 128-B
-   line per entry) instead of 9 limbs (144 B, two or three lines).  Measured
-   A/B on one box: k_verify_dsm 7.35 vs 7.65 ms, C2 113.2 M vs 108.2 M
-   verifies/s -- the kernel is power-limited and the fetch traffic it saves
-   buys clock; 0 keeps the 9-limb layout for A/B runs. */
-#ifndef FD_ATAB_PACK
-#define FD_ATAB_PACK 1
-#endif
-#if FD_ATAB_PACK
-#define ATAB_ENT    32             /* cached: YmX, YpX, T2d, Z2 (8 packed words each) */
-#else
-#define ATAB_ENT    36             /* cached: YmX, YpX, T2d, Z2 (9 limbs each) */
-#endif
+/* A/R table entries: each element packed from 9 limbs to 8 words
+   (fe_pack), so an entry (Y-X, Y+X, 2dT, 2Z) is one 128-B line.  Measured
+   against the 9-limb layout (144 B, two or three lines): k_verify_dsm 7.35
+   vs 7.65 ms, C2 113.2 vs 108.2 M verifies/s (round 1) -- the kernel is
+   power-limited and the fetch traffic it saves buys clock. */
+#define ATAB_ENT    32
 #define RTAB_OFF    (8*ATAB_ENT)   /* per lane: [1..8](+-A), then [1..8](-R) */
-#ifndef FD_ATAB_PAD
-#define FD_ATAB_PAD 0              /* words of padding after each lane's tables (lane stride) */
-#endif
-#define ATAB_WORDS  (2*RTAB_OFF + FD_ATAB_PAD)
+#define ATAB_WORDS  (2*RTAB_OFF)
 /* the identity entry (digit 0) is shared by every lane: one line in d_btab
    after the two B tables (128-B aligned), hot in cache, never written per
    signature */
 #define IDENT_OFF   ((2*BTAB_WORDS + 31) & ~31)
-/* FD_BTAB_W12: k_verify_dsm takes the [k2*S mod L]B term in signed radix
-   2^12 (11 + 11 digits against [0..2048]B and [0..2048](2^132 B), 22 affine
-   additions) from global tables that stay resident in each XCD's L2 (2 x 2049
-   entries of one 128-B line, 525 KB), instead of radix 2^8 (16 + 16 digits,
-   32 additions) from the two 129-entry LDS tables.  A/B on one box
-   (profiles/r02r_ab_w12): k_verify_dsm 6.59-6.62 vs 6.79-6.87 ms, C2
-   128.7-129.4 vs 126.3-126.4 M verifies/s. */
-#ifndef FD_BTAB_W12
-#define FD_BTAB_W12 1
-#endif
-/* FD_BTAB_GW: bits per digit of those global tables, 12 (default) or 16
-   (8 + 8 digits, [0..32768] multiples, 8.4 MB: past L2, served by MALL).
-   A/B (profiles/r02r_ab_gw16): 16 gives k_verify_dsm 6.42-6.49 vs 6.57-6.61
-   ms and C2 130.4 vs 129.5 M verifies/s, for ~1.9 GB more fabric reads per
-   2^20-signature launch; 12 stays the default (traffic, 16x smaller table). */
-#ifndef FD_BTAB_GW
-#define FD_BTAB_GW 12
-#endif
-#if FD_BTAB_GW == 12
+/* k_verify_dsm takes the [k2*S mod L]B term in signed radix 2^12 (11 + 11
+   digits against [0..2048]B and [0..2048](2^132 B), 22 affine additions)
+   from global tables that stay resident in each XCD's L2 (2 x 2049 entries
+   of one 128-B line, 525 KB).  Measured against radix 2^8 (16 + 16 digits,
+   32 additions) from two 129-entry LDS tables (profiles/r02r_ab_w12):
+   k_verify_dsm 6.59-6.62 vs 6.79-6.87 ms, C2 128.7-129.4 vs 126.3-126.4 M
+   verifies/s; against radix 2^16 (8.4 MB of tables, served by MALL,
+   profiles/r02r_ab_gw16): +0.7% on C2 for ~1.9 GB more fabric reads per
+   launch. */
+#define BTG_GW      12             /* bits per digit */
 #define BTG_ND      11             /* digits per half */
-#elif FD_BTAB_GW == 16
-#define BTG_ND      8
-#else
-#error "FD_BTAB_GW must be 12 or 16"
-#endif
-#define BTG_HB      (BTG_ND*FD_BTAB_GW)        /* the high table holds multiples of 2^BTG_HB B */
-#define BTG_STEP    (FD_BTAB_GW/4)             /* radix-16 windows between B additions */
-#define BT12_N      ((1 << (FD_BTAB_GW-1)) + 1)
+#define BTG_HB      (BTG_ND*BTG_GW)            /* the high table holds multiples of 2^BTG_HB B */
+#define BTG_STEP    (BTG_GW/4)                 /* radix-16 windows between B additions */
+#define BT12_N      ((1 << (BTG_GW-1)) + 1)
 #define BT12_ENT    32             /* YmX, YpX, T2d: 9 limbs each + pad to one 128-B line */
 #define BT12_OFF    ((IDENT_OFF + ATAB_ENT + 31) & ~31)
-#if FD_BTAB_W12
 #define BTAB_ALLOC  (BT12_OFF + 2*BT12_N*BT12_ENT)
-#else
-#define BTAB_ALLOC  (IDENT_OFF + ATAB_ENT)
-#endif
 
 /* state record: 32 u32 words per field group, laid out SoA per chunk for
    coalescing: word w of signature i lives at st[ w*chunk + i ].
-   FD_STATE_BY_SLOT: i is k_verify_prep's processing slot t (lane t takes
-   record order[t]), not the record index, and idx[] holds survivor slots.
+   i is k_verify_prep's processing slot t (lane t takes record order[t]),
+   not the record index, and idx[] holds survivor slots.
    On the txn paths the block-count order scatters records over the chunk:
    indexed by record, a wave's 48 state stores in prep and 48 loads in
    k_verify_dsm each touched 64 separate lines.  By slot they are
    contiguous; the DSM looks up order[slot] once for the code it writes.
    Batches without an order (order[t] = t) are unchanged. */
-#ifndef FD_STATE_BY_SLOT
-#define FD_STATE_BY_SLOT 1
-#endif
 #define ST_K     0
 #define ST_S     8
 #define ST_AX   16
@@ -162,8 +123,7 @@ struct fd_ed25519_hip_ctx {
   u32 *        d_atab;      /* ATAB_WORDS * chunk */
   u32 *        d_idx;       /* chunk: compacted survivor indices */
   u32 *        d_count;     /* [0] survivor count; [16..47] k_msg_order's histogram and cursors */
-  ulong        dsm_wgs;     /* resident k_verify_dsm workgroups (FD_DSM_PERSIST grid) */
-  ulong        prep_wgs;    /* resident k_verify_prep workgroups (FD_PREP_PERSIST grid) */
+  ulong        dsm_wgs;     /* resident k_verify_dsm workgroups (its persistent grid) */
   u32 *        d_order;     /* chunk: k_verify_prep's record order (variable-size message paths) */
   int          errmode;
   int          halfsize;    /* 1: half-size scalars (default); 0: full-length (k, 1) */
@@ -187,11 +147,6 @@ struct fd_ed25519_hip_ctx {
      d_count/d_atab */
   hipEvent_t   ev_last;
   int          ev_used;
-  /* drop-in entry points (part 1): one pinned, device-mapped staging block
-     the kernels read and write in place (no copies), grown on demand */
-  uchar *      h_stage;
-  ulong        h_stage_cap;
-  uchar *      d_stage;     /* device copy of h_stage (drop-in calls, FD_DROPIN_DMA) */
 };
 
 /**********************************************************************/
@@ -254,7 +209,6 @@ __global__ __launch_bounds__(64) void k_btab_init( u32 * btab ) {
   }
 }
 
-#if FD_BTAB_W12
 /* [j]B and [j](2^132 B) for j in [0,2048], 1/2-scaled affine cached, one
    128-B line each at BT12_OFF */
 __global__ __launch_bounds__(64) void k_btab12_init( u32 * btab ) {
@@ -267,7 +221,7 @@ __global__ __launch_bounds__(64) void k_btab12_init( u32 * btab ) {
     for( int q=0; q<BTG_HB; q++ ) ge_dbl( B, B, true );
   }
   ge_cached Bc; ge_to_cached( Bc, B );
-  for( int bit=FD_BTAB_GW-1; bit>=0; bit-- ) {
+  for( int bit=BTG_GW-1; bit>=0; bit-- ) {
     ge_dbl( P, P, true );
     if( (j >> bit) & 1 ) ge_add_cached( P, P, Bc, 0u, true );
   }
@@ -277,7 +231,6 @@ __global__ __launch_bounds__(64) void k_btab12_init( u32 * btab ) {
   #pragma unroll
   for( int i=27; i<32; i++ ) e[i] = 0u;
 }
-#endif
 
 DEV int code_of( u32 f, int errmode, bool eq ) {
   if( errmode == FD_ED25519_HIP_ERRMODE_AVX512 ) {
@@ -344,23 +297,10 @@ void k_msg_order( ulong n, uint const * __restrict__ msz, u32 * __restrict__ cou
   if( t < n ) order[base[key] + r] = (u32)t;
 }
 
-/* FD_PREP_WAVES: waves per SIMD the register allocation of k_verify_prep is
-   held to (0: compiler's choice) */
-#ifndef FD_PREP_WAVES
-#define FD_PREP_WAVES 0
-#endif
-#if FD_PREP_WAVES
-#define PREP_OCCUPANCY __attribute__((amdgpu_waves_per_eu(FD_PREP_WAVES, FD_PREP_WAVES)))
-#else
-#define PREP_OCCUPANCY
-#endif
-
-/* FD_PREP_LDS_MSG: SHA-512(R||A||M) with wave-cooperative, LDS-staged
-   message blocks (sha512_prefixed_coop) instead of each lane loading its own
-   message with dword loads (sha512_prefixed). */
-#ifndef FD_PREP_LDS_MSG
-#define FD_PREP_LDS_MSG 1
-#endif
+/* SHA-512(R||A||M) with wave-cooperative, LDS-staged message blocks
+   (sha512_prefixed_coop; measured against each lane loading its own message
+   with dword loads, profiles/r02e_lds_ab: prep 1.879 vs 1.909 ms at C2, C4
+   104.2 vs 102.3 M verifies/s) */
 #define PREP_MSG_WORDS (64*36)           /* per wave: 64 windows of 144 B */
 
 /* one record slot t of the chunk (n records): checks, decodes, hash, and the
@@ -374,11 +314,7 @@ DEV void prep_slot( ulong t, ulong n, ulong chunk, uchar const * __restrict__ si
   /* order (k_msg_order): lane t takes record order[t], so a wave's lanes
      hash messages of the same SHA-512 block count */
   ulong i = active ? (order ? (ulong)order[t] : t) : 0ul;
-#if FD_STATE_BY_SLOT
   ulong const sl = t;                        /* state column and survivor entry: the slot */
-#else
-  ulong const sl = i;
-#endif
   u32 flags = 0u;
   if( active ) {
   u32 * s = st + sl;
@@ -408,26 +344,7 @@ DEV void prep_slot( ulong t, ulong n, ulong chunk, uchar const * __restrict__ si
       for( int q=0; q<8; q++ ) { s[(base+q)*chunk] = xw[q]; s[(base+8+q)*chunk] = yw[q]; }
     }
   }
-#if !FD_PREP_LDS_MSG
-  /* reload the record for the hash rather than holding it across the decode
-     (the opaque pointer keeps the compiler from reusing the first load) */
-  uchar const * sp = sigs + 64*i, * pp = pubs + 32*i;
-  asm volatile( "" : "+v"(sp), "+v"(pp) );
-  u32 sig[16], pub[8];
-  load_words( sig, sp, 16 );
-  load_words( pub, pp, 8 );
-  u32 k[8];
-  u32 mo = moff ? moff[i] : (u32)i * fixed_sz;                            /* moff NULL: message i = */
-  u32 ms = msz  ? msz[i]  : fixed_sz;                                      /* pool[i*fixed_sz, +fixed_sz) */
-  hram_mod_l( k, sig, pub, pool + mo, ms );                                /* user.c:205-207 */
-  #pragma unroll
-  for( int w=0; w<8; w++ ) {
-    s[(ST_K +w)*chunk] = k[w];
-    s[(ST_S +w)*chunk] = sig[8+w];
   }
-#endif
-  }
-#if FD_PREP_LDS_MSG
   {
     /* the whole wave hashes together (inactive lanes with an empty message) */
     u32 pre[16], x[16], k[8], sv[8];
@@ -456,7 +373,6 @@ DEV void prep_slot( ulong t, ulong n, ulong chunk, uchar const * __restrict__ si
       }
     }
   }
-#endif
   /* Survivor compaction: a signature that fails a pre-check gets its final
      code here; the others are appended (wave-aggregated atomic, spread over
      the whole prep launch) to idx[] so that k_verify_dsm spends no lanes on
@@ -473,15 +389,10 @@ DEV void prep_slot( ulong t, ulong n, ulong chunk, uchar const * __restrict__ si
   if( pass ) idx[base + below] = (u32)sl;
 }
 
-/* FD_PREP_PERSIST: resident workgroups pull 64-record tasks from count[2]
-   (as k_verify_dsm does from count[1]); every wave leaves when the counter
-   passes n.  Off: measured A/B on C2, prep 1.98-2.07 vs 1.96-1.98 ms
-   (116.7-117.9 vs 118.3-118.6 M verifies/s); C4 was within noise. */
-#ifndef FD_PREP_PERSIST
-#define FD_PREP_PERSIST 0
-#endif
-
-__global__ __launch_bounds__(256) PREP_OCCUPANCY
+/* one workgroup per 256 records (a persistent grid pulling 64-record tasks,
+   as k_verify_dsm does, measured slower on C2: prep 1.98-2.07 vs 1.96-1.98
+   ms; C4 within noise) */
+__global__ __launch_bounds__(256)
 void k_verify_prep( ulong n, ulong chunk, uchar const * __restrict__ sigs, uchar const * __restrict__ pubs,
                     uchar const * __restrict__ pool, uint const * __restrict__ moff, uint const * __restrict__ msz,
                     u32 fixed_sz, u32 * __restrict__ st, int errmode, u32 * __restrict__ idx,
@@ -489,27 +400,12 @@ void k_verify_prep( ulong n, ulong chunk, uchar const * __restrict__ sigs, uchar
                     ulong rec0, u32 const * __restrict__ order ) {
   n = dev_count_n( n, d_n, rec0 );            /* device-side count: this chunk starts at record rec0 */
   if( (ulong)blockIdx.x * blockDim.x >= n ) return;
-#if FD_PREP_LDS_MSG
   __shared__ __attribute__((aligned(16))) u32 lds_msg_all[4*PREP_MSG_WORDS];
   __shared__ u64 lds_meta_all[4*64];
   u32 * lds_msg = lds_msg_all + PREP_MSG_WORDS*(threadIdx.x >> 6);
   u64 * lds_meta = lds_meta_all + 64*(threadIdx.x >> 6);
-#else
-  u32 * lds_msg = 0; u64 * lds_meta = 0;
-#endif
-#if FD_PREP_PERSIST
-  for( ;; ) {
-    u32 task = 0u;
-    if( (threadIdx.x & 63u) == 0u ) task = atomicAdd( count + 2, 1u );
-    task = __shfl( task, 0 );
-    if( (ulong)task * 64ul >= n ) break;                              /* wave-uniform exit */
-    prep_slot( (ulong)task * 64ul + (threadIdx.x & 63u), n, chunk, sigs, pubs, pool, moff, msz, fixed_sz, st,
-               errmode, idx, count, codes, order, lds_msg, lds_meta );
-  }
-#else
   prep_slot( (ulong)blockIdx.x * blockDim.x + threadIdx.x, n, chunk, sigs, pubs, pool, moff, msz, fixed_sz, st,
              errmode, idx, count, codes, order, lds_msg, lds_meta );
-#endif
 }
 
 
@@ -542,7 +438,6 @@ template<int W30> DEV void fe_unpack( fe & a, u32 const w[8] ) {
     else               a.v[j] = __builtin_amdgcn_alignbit( w[k+1], w[k], (u32)sh ) & m;
   }
 }
-#if FD_ATAB_PACK
 DEV void store_cached( u32 * t, ge_cached const & c ) {   /* 32 words, one 128-B line */
   u32 w[32];
   fe_pack<0>( w, c.YmX ); fe_pack<0>( w + 8, c.YpX ); fe_pack<1>( w + 16, c.T2d ); fe_pack<0>( w + 24, c.Z2 );
@@ -557,84 +452,19 @@ DEV void load_cached( ge_cached & c, u32 const * t ) {
   for( int k=0; k<8; k++ ) { uint4 v = q[k]; w[4*k] = v.x; w[4*k+1] = v.y; w[4*k+2] = v.z; w[4*k+3] = v.w; }
   fe_unpack<0>( c.YmX, w ); fe_unpack<0>( c.YpX, w + 8 ); fe_unpack<1>( c.T2d, w + 16 ); fe_unpack<0>( c.Z2, w + 24 );
 }
-#else
-DEV void store_cached( u32 * t, ge_cached const & c ) {   /* 36 words, 16-byte aligned */
-  u32 w[36];
-  #pragma unroll
-  for( int i=0; i<9; i++ ) { w[i] = c.YmX.v[i]; w[9+i] = c.YpX.v[i]; w[18+i] = c.T2d.v[i]; w[27+i] = c.Z2.v[i]; }
-  uint4 * q = (uint4 *)t;
-  #pragma unroll
-  for( int k=0; k<9; k++ ) q[k] = make_uint4( w[4*k], w[4*k+1], w[4*k+2], w[4*k+3] );
-}
-DEV void load_cached( ge_cached & c, u32 const * t ) {
-  uint4 const * q = (uint4 const *)t;
-  u32 w[36];
-  #pragma unroll
-  for( int k=0; k<9; k++ ) { uint4 v = q[k]; w[4*k] = v.x; w[4*k+1] = v.y; w[4*k+2] = v.z; w[4*k+3] = v.w; }
-  #pragma unroll
-  for( int i=0; i<9; i++ ) { c.YmX.v[i] = w[i]; c.YpX.v[i] = w[9+i]; c.T2d.v[i] = w[18+i]; c.Z2.v[i] = w[27+i]; }
-}
-#endif
-/* FD_DSM_RLDS: k_verify_dsm prefetches each window's R-table entry straight
-   into LDS (global_load_lds_dwordx4, 8 KB per wave: 8 x 16 B per lane) when it
-   issues the A entry's load, before the window's doublings, and reads it
-   back after the A addition.  Without it the R entry's load is issued after
-   the A addition and its latency is exposed (the 32 VGPRs to hold both
-   entries across the doublings would cost a wave per SIMD).  Off: A/B on one
-   box (profiles/r02z_ab_rlds) C2 130.4/130.6 vs 131.4/130.8 M verifies/s, DSM
-   6.84/6.89 vs 6.65/6.91 ms -- the other two waves of the SIMD already hide
-   that latency. */
-#ifndef FD_DSM_RLDS
-#define FD_DSM_RLDS 0
-#endif
-/* FD_DSM_TRAFFIC_PROBE (diagnostic builds only, wrong verdicts; see
-   dsm_verify_slot and tools/dsm_traffic_probe.py) */
-#ifndef FD_DSM_TRAFFIC_PROBE
-#define FD_DSM_TRAFFIC_PROBE 0
-#endif
-typedef __attribute__((address_space(3))) u32 lds_u32;
-DEV void entry_prefetch_lds( lds_u32 * wl, u32 const * src ) {
-  #pragma unroll
-  for( int k=0; k<8; k++ )
-    __builtin_amdgcn_global_load_lds( (void const *)(src + 4*k), (__attribute__((address_space(3))) void *)(wl + 256*k),
-                                      16, 0, 0 );
-}
-DEV void entry_load_lds( ge_cached & c, lds_u32 const * wl, u32 lane ) {
-  asm volatile( "s_waitcnt vmcnt(0)" ::: "memory" );      /* the prefetch has landed in LDS */
-  u32 w[32];
-  #pragma unroll
-  for( int k=0; k<8; k++ ) {
-    lds_u32 const * q = wl + 256*k + 4*lane;
-    w[4*k] = q[0]; w[4*k+1] = q[1]; w[4*k+2] = q[2]; w[4*k+3] = q[3];
-  }
-  fe_unpack<0>( c.YmX, w ); fe_unpack<0>( c.YpX, w + 8 ); fe_unpack<1>( c.T2d, w + 16 ); fe_unpack<0>( c.Z2, w + 24 );
-}
-
-/* one 1/2-scaled affine B-table entry from LDS (FD_BTAB_PACK: 6 x
-   ds_read_b128 + unpack; else 7 x ds_read_b128) */
+/* one 1/2-scaled affine B-table entry (7 x 16-B loads) */
 DEV void store_affc( u32 * e, ge_affc const & a ) {      /* canonical elements: any packing layout fits */
-#if FD_BTAB_PACK
-  fe_pack<0>( e, a.YmX ); fe_pack<0>( e + 8, a.YpX ); fe_pack<0>( e + 16, a.T2d );
-#else
   #pragma unroll
   for( int i=0; i<9; i++ ) { e[i] = a.YmX.v[i]; e[9+i] = a.YpX.v[i]; e[18+i] = a.T2d.v[i]; }
   e[27] = 0u;
-#endif
 }
 DEV void load_affc( ge_affc & b, u32 const * bt ) {
   uint4 const * q = (uint4 const *)bt;
-#if FD_BTAB_PACK
-  u32 w[24];
-  #pragma unroll
-  for( int k=0; k<6; k++ ) { uint4 v = q[k]; w[4*k] = v.x; w[4*k+1] = v.y; w[4*k+2] = v.z; w[4*k+3] = v.w; }
-  fe_unpack<0>( b.YmX, w ); fe_unpack<0>( b.YpX, w + 8 ); fe_unpack<0>( b.T2d, w + 16 );
-#else
   u32 w[28];
   #pragma unroll
   for( int k=0; k<7; k++ ) { uint4 v = q[k]; w[4*k] = v.x; w[4*k+1] = v.y; w[4*k+2] = v.z; w[4*k+3] = v.w; }
   #pragma unroll
   for( int i=0; i<9; i++ ) { b.YmX.v[i] = w[i]; b.YpX.v[i] = w[9+i]; b.T2d.v[i] = w[18+i]; }
-#endif
 }
 
 /* shift a packed 256-bit digit vector left by `bits` (4 or 8) */
@@ -653,10 +483,12 @@ void k_bitmap( ulong n, signed char const * __restrict__ codes, ulong * __restri
   bool ok = i < n && codes[i] == FD_ED25519_SUCCESS;
   unsigned long long b = __ballot( ok );
   if( (threadIdx.x & 63u) == 0u && i < n ) {
-    /* the word holding record n-1: bits at or past n belong to no record of
-       this call and keep their value (include/fd_ed25519_hip.h) */
+    /* the word holding record n-1: with a device-side count, bits at or past
+       *d_n belong to no record of this call and keep their value; with a
+       host count they are zero, as the ballot leaves them
+       (include/fd_ed25519_hip.h) */
     ulong left = n - i;
-    if( left < 64ul ) {
+    if( d_n && left < 64ul ) {
       unsigned long long m = (1ULL << left) - 1ULL;
       b = (bitmap[i >> 6] & ~m) | (b & m);
     }
@@ -712,23 +544,9 @@ DEV u32 wave_max7( u32 v ) {
   return m;
 }
 
-/* FD_DSM_WAVES: waves per SIMD the register allocation of k_verify_dsm is
-   held to (0: compiler's choice) */
-#ifndef FD_DSM_PERSIST
-#define FD_DSM_PERSIST 1
-#endif
-#ifndef FD_DSM_WAVES
-#if FD_DSM_PERSIST
-#define FD_DSM_WAVES 3      /* the task loop alone takes the compiler to 172 VGPRs (2 waves) */
-#else
-#define FD_DSM_WAVES 0
-#endif
-#endif
-#if FD_DSM_WAVES
-#define DSM_OCCUPANCY __attribute__((amdgpu_waves_per_eu(FD_DSM_WAVES, FD_DSM_WAVES)))
-#else
-#define DSM_OCCUPANCY
-#endif
+/* k_verify_dsm's register allocation is held to 3 waves per SIMD (the task
+   loop alone takes the compiler to 172 VGPRs, 2 waves) */
+#define DSM_OCCUPANCY __attribute__((amdgpu_waves_per_eu(3, 3)))
 
 /* signed radix-2^GW digits of sp (< 2^253) for the two global B tables:
    digit i = r_i + c_i - 2^GW c_{i+1}, r_i = bits [GW i, GW i + GW), carry
@@ -737,7 +555,7 @@ DEV u32 wave_max7( u32 v ) {
    the next digit (consumed top-down): bl = sp << (160-HB) (bits 0..HB-1),
    bh = sp >> (2HB-160) (bits HB.. on top; the bits below are never read). */
 DEV void b12_digits( u32 bl[5], u32 bh[5], u32 & bmask, u32 const sp[8] ) {
-  constexpr int GW = FD_BTAB_GW, ND = BTG_ND, HB = BTG_HB;
+  constexpr int GW = BTG_GW, ND = BTG_ND, HB = BTG_HB;
   u32 c = 0u; bmask = 0u;
   #pragma unroll
   for( int i=0; i<2*ND; i++ ) {
@@ -764,24 +582,12 @@ DEV void b12_digits( u32 bl[5], u32 bh[5], u32 & bmask, u32 const sp[8] ) {
   }
 }
 
-/* lane-parallel group law for k_verify_lat (FD_LAT_LP, see there) */
-#ifndef FD_LAT_FREE
-#define FD_LAT_FREE 1    /* k_verify_lat: lane-parallel products and the decodes with open sums (fe_mul_free) */
-#endif
-DEV void lp_mul( fe & r, fe const & a, fe const & b ) {
-#if FD_LAT_FREE
-  fe_mul_free( r, a, b );
-#else
-  fe_mul( r, a, b );
-#endif
-}
-DEV void lp_sq( fe & r, fe const & a ) {
-#if FD_LAT_FREE
-  fe_sq_free( r, a );
-#else
-  fe_sq( r, a );
-#endif
-}
+/* lane-parallel group law for k_verify_lat (see there).  Its products use
+   open sums (fe_mul_free / fe_sq_free): a wave alone on its SIMD gains from
+   the extra independent chains (single verify p50 299-303 vs 320-323 us,
+   profiles/r02zd_latency_lp/ab_free) */
+DEV void lp_mul( fe & r, fe const & a, fe const & b ) { fe_mul_free( r, a, b ); }
+DEV void lp_sq( fe & r, fe const & a ) { fe_sq_free( r, a ); }
 
 DEV u32 lp_lane( void ) { return threadIdx.x & 63u; }
 
@@ -881,7 +687,7 @@ DEV void build_cached_table_lp( u32 * tab, fe const & qx, fe const & qy ) {
 template<bool LP = false>
 DEV void b12_step( ge_p3 & P, u32 bl[5], u32 bh[5], u32 bmask, u32 bi, u32 const * __restrict__ btab,
                    bool needT ) {
-  constexpr u32 GW = FD_BTAB_GW, ND = BTG_ND;
+  constexpr u32 GW = BTG_GW, ND = BTG_ND;
   u32 negb, ib, negc, ic;
   {
     int v = (int)((bl[4] >> (32u-GW)) + ((bmask >> bi) & 1u)) - (int)(((bmask >> (bi+1u)) & 1u) << GW);
@@ -903,17 +709,12 @@ DEV void b12_step( ge_p3 & P, u32 bl[5], u32 bh[5], u32 bmask, u32 bi, u32 const
 }
 
 /* one survivor: DSM slot t (tables at slot t), state column idx[t] (prep's
-   slot; record order[idx[t]] under FD_STATE_BY_SLOT, else the record) */
+   slot), record order[idx[t]] */
 DEV void dsm_verify_slot( ulong t, ulong chunk, u32 const * __restrict__ st, u32 const * __restrict__ btab,
-                          u32 * __restrict__ atab, u32 const * __restrict__ idx, u32 const * lds_btab,
-                          signed char * __restrict__ codes, int halfsize, u32 const * __restrict__ order,
-                          lds_u32 * lds_rent ) {
+                          u32 * __restrict__ atab, u32 const * __restrict__ idx, signed char * __restrict__ codes,
+                          int halfsize, u32 const * __restrict__ order ) {
   ulong p = idx[t];
-#if FD_STATE_BY_SLOT
   ulong i = order ? (ulong)order[p] : p;
-#else
-  ulong i = p; (void)order;
-#endif
   ulong ii = t;                                            /* table slot: dense in t */
   u32 const * s = st + p;
   bool eq = false;
@@ -921,11 +722,7 @@ DEV void dsm_verify_slot( ulong t, ulong chunk, u32 const * __restrict__ st, u32
     /* ---- half-size scalars (sc_halfsize): the reference's check
        [S]B - [k]A == R (user.c:216-226) becomes
        [k2*S mod L]B - [k1]A - [k2]R == O with k1, k2 ~ 2^128 ---- */
-#if FD_BTAB_W12
     u32 kd1[8], kd2[8], bl[5], bh[5], bmask, k1neg, D;
-#else
-    u32 kd1[8], kd2[8], sd[8], k1neg, D;
-#endif
     {
       u32 k[8], S[8], k1[8], k2[8], sp[8];
       #pragma unroll
@@ -939,12 +736,8 @@ DEV void dsm_verify_slot( ulong t, ulong chunk, u32 const * __restrict__ st, u32
       }
       sc_mul( sp, k2, S );
       sc_recode16s( kd1, k1 ); sc_recode16s( kd2, k2 );
-#if FD_BTAB_W12
       b12_digits( bl, bh, bmask, sp );                       /* signed radix-2^12 digits of sp */
-#else
-      sc_recode256( sd, sp );       /* digits 0..15: B; 16..31: 2^128 B (second LDS table) */
-#endif
-      D = max( (bits >> 2) + 1u, 31u );   /* windows; >= 31 so all 16 B digit pairs are reached */
+      D = max( (bits >> 2) + 1u, 31u );   /* windows; >= 31 so all 11 B digit pairs (windows 30, 27, .., 0) are reached */
     }
     D = wave_max7( D );             /* one window count per wave: no divergence in the loop */
     #pragma unroll 1
@@ -952,17 +745,6 @@ DEV void dsm_verify_slot( ulong t, ulong chunk, u32 const * __restrict__ st, u32
 
     /* ---- tables [0..8](+-A) and [0..8](-R) (fd_curve25519.c:130-143) ---- */
     u32 * tabA = atab + ii * ATAB_WORDS, * tabR = tabA + RTAB_OFF;
-#if FD_DSM_TRAFFIC_PROBE
-    /* diagnostic build, wrong verdicts: the window loop reads 64 shared
-       (L2-resident) tables instead of the survivor's own; level 2 also
-       builds into them.  Same instruction stream, table traffic gone. */
-    u32 * rtabA = atab + (t & 63u) * ATAB_WORDS, * rtabR = rtabA + RTAB_OFF;
-#if FD_DSM_TRAFFIC_PROBE > 1
-    tabA = rtabA; tabR = rtabR;
-#endif
-#else
-    u32 * rtabA = tabA, * rtabR = tabR;
-#endif
     u32 const * ident = btab + IDENT_OFF;
     {
       fe x, y, nx;
@@ -980,7 +762,7 @@ DEV void dsm_verify_slot( ulong t, ulong chunk, u32 const * __restrict__ st, u32
     }
 
     /* ---- [k1](+-A) + [k2](-R) + [s']B, signed radix-16 windows for k1, k2
-       and radix-256 digit pairs for s' every other window ---- */
+       and radix-2^12 digit pairs for s' every third window ---- */
     ge_p3 P; ge_identity( P );
     #pragma unroll 1
     for( int w=(int)D-1; w>=0; w-- ) {
@@ -988,39 +770,18 @@ DEV void dsm_verify_slot( ulong t, ulong chunk, u32 const * __restrict__ st, u32
       digit_split( kd1[7] >> 28, 7u, nega, ia ); digits_shl( kd1, 4u );
       digit_split( kd2[7] >> 28, 7u, negr, ir ); digits_shl( kd2, 4u );
       /* issued before the window's 4 doublings, which hide its latency */
-      ge_cached e; load_cached( e, tab_entry( rtabA, ident, ia ) );
-#if FD_DSM_RLDS
-      entry_prefetch_lds( lds_rent, tab_entry( rtabR, ident, ir ) );
-#endif
+      ge_cached e; load_cached( e, tab_entry( tabA, ident, ia ) );
       if( w != (int)D-1 ) {
         #pragma unroll 1
         for( int j=0; j<3; j++ ) ge_dbl( P, P, false );
         ge_dbl( P, P, true );
       }
       ge_add_cached( P, P, e, nega, true );
-#if FD_DSM_RLDS
-      entry_load_lds( e, lds_rent, (u32)(threadIdx.x & 63u) );
-#else
-      load_cached( e, tab_entry( rtabR, ident, ir ) );
-#endif
-#if FD_BTAB_W12
+      load_cached( e, tab_entry( tabR, ident, ir ) );
       /* windows (ND-1)*STEP, .., STEP, 0: lo digits ND-1..0, hi digits 2ND-1..ND */
       bool bw = w <= (BTG_ND-1)*BTG_STEP && w % BTG_STEP == 0;
       ge_add_cached( P, P, e, negr, bw );
       if( bw ) b12_step( P, bl, bh, bmask, (u32)w / (u32)BTG_STEP, btab, false );
-#else
-      bool bw = (w & 1) == 0 && w <= 30;
-      ge_add_cached( P, P, e, negr, bw );
-      if( bw ) {
-        u32 negb, ib, negc, ic;
-        digit_split( sd[3] >> 24, 128u, negb, ib ); digits_shl4( sd );
-        digit_split( sd[7] >> 24, 128u, negc, ic ); digits_shl4( sd + 4 );
-        ge_affc b; load_affc( b, lds_btab + ib*BTAB_STRIDE );
-        ge_add_affc( P, P, b, negb, true );
-        load_affc( b, lds_btab + BTAB_WORDS + ic*BTAB_STRIDE );
-        ge_add_affc( P, P, b, negc, false );
-      }
-#endif
     }
 
     /* ---- P == O: X == 0 and Y == Z (Z != 0: complete formulas) ---- */
@@ -1031,11 +792,11 @@ DEV void dsm_verify_slot( ulong t, ulong chunk, u32 const * __restrict__ st, u32
   codes[i] = (signed char)(eq ? FD_ED25519_SUCCESS : FD_ED25519_ERR_MSG);   /* user.c:226-229 */
 }
 
-/* FD_DSM_PERSIST: resident workgroups (ctx->dsm_wgs, ~3 per CU) pull 64-survivor
-   tasks from a counter (count[1]) until none is left, instead of one
-   workgroup per 256 survivors: no partial last round of waves, and one LDS
-   B-table copy per resident workgroup.  Every wave leaves the loop when the
-   counter passes m, so the grid drains. */
+/* Persistent grid: resident workgroups (ctx->dsm_wgs, ~3 per CU) pull
+   64-survivor tasks from a counter (count[1]) until none is left, instead of
+   one workgroup per 256 survivors: no partial last round of waves (measured
+   against the one-shot grid at C4: 103.2-103.7 vs 100.0 M verifies/s).
+   Every wave leaves the loop when the counter passes m, so the grid drains. */
 
 __global__ __launch_bounds__(256) DSM_OCCUPANCY
 void k_verify_dsm( ulong chunk, u32 const * __restrict__ st, u32 const * __restrict__ btab,
@@ -1043,47 +804,14 @@ void k_verify_dsm( ulong chunk, u32 const * __restrict__ st, u32 const * __restr
                    signed char * __restrict__ codes, int halfsize, u32 const * __restrict__ order ) {
   u32 m = count[0];
   if( (ulong)blockIdx.x * blockDim.x >= m ) return;        /* whole workgroup past the survivors */
-#if FD_BTAB_W12
-  u32 const * lds_btab = 0;                                /* B tables from global memory (L2) */
-#else
-  __shared__ __attribute__((aligned(16))) u32 lds_btab[2*BTAB_WORDS];
-  {
-    /* 28.9 KB: all of a thread's 16-B loads in flight before the LDS stores
-       (a load-store loop waits out one L2 round trip per iteration) */
-    /* the full rounds unconditionally and the partial one apart: with a
-       guard on every round the array went to scratch (144 B per lane) */
-    constexpr int NQ = 2*BTAB_WORDS/4, FULL = NQ/256;
-    uint4 v[FULL], last = make_uint4( 0u, 0u, 0u, 0u );
-    bool has_last = (int)threadIdx.x + 256*FULL < NQ;
-    #pragma unroll
-    for( int u=0; u<FULL; u++ ) v[u] = ((uint4 const *)btab)[threadIdx.x + 256*u];
-    if( has_last ) last = ((uint4 const *)btab)[threadIdx.x + 256*FULL];
-    #pragma unroll
-    for( int u=0; u<FULL; u++ ) ((uint4 *)lds_btab)[threadIdx.x + 256*u] = v[u];
-    if( has_last ) ((uint4 *)lds_btab)[threadIdx.x + 256*FULL] = last;
-  }
-  __syncthreads();
-#endif
-#if FD_DSM_RLDS
-  __shared__ __attribute__((aligned(16))) u32 lds_rent_all[4*2048];
-  lds_u32 * lds_rent = (lds_u32 *)(lds_rent_all + 2048*(threadIdx.x >> 6));
-#else
-  lds_u32 * lds_rent = 0;
-#endif
-#if FD_DSM_PERSIST
   for( ;; ) {
     u32 task = 0u;
     if( (threadIdx.x & 63u) == 0u ) task = atomicAdd( count + 1, 1u );
     task = __shfl( task, 0 );
     if( (ulong)task * 64ul >= (ulong)m ) break;                       /* wave-uniform exit */
     ulong t = (ulong)task * 64ul + (threadIdx.x & 63u);
-    if( t < m ) dsm_verify_slot( t, chunk, st, btab, atab, idx, lds_btab, codes, halfsize, order, lds_rent );
+    if( t < m ) dsm_verify_slot( t, chunk, st, btab, atab, idx, codes, halfsize, order );
   }
-#else
-  ulong t = (ulong)blockIdx.x * blockDim.x + threadIdx.x;
-  if( t >= m ) return;
-  dsm_verify_slot( t, chunk, st, btab, atab, idx, lds_btab, codes, halfsize, order, lds_rent );
-#endif
 }
 
 /**********************************************************************/
@@ -1109,9 +837,6 @@ void k_verify_dsm( ulong chunk, u32 const * __restrict__ st, u32 const * __restr
                                 records; the bulk kernels win from 64 up, 686 vs 721 us,
                                 profiles/r02zd_latency_lp) */
 #define LAT_COPY_MAX_N 32ul  /* calls of up to 32 signatures run one copy per XCD (k_verify_lat) */
-#ifndef FD_LAT_COPIES
-#define FD_LAT_COPIES 1      /* 0: one workgroup per signature always (A/B switch) */
-#endif
 /* 12 waves = 3 per SIMD, all a CU holds at k_verify_lat's register count:
    one workgroup per CU, so a call's signatures never share a SIMD.  Waves
    3..11 leave at once; the three working waves land on three SIMDs. */
@@ -1135,25 +860,15 @@ DEV void lat_get( ge_p3 & P, u32 const * d ) {
   for( int q=0; q<9; q++ ) { P.X.v[q] = d[q]; P.Y.v[q] = d[9+q]; P.Z.v[q] = d[18+q]; P.T.v[q] = d[27+q]; }
 }
 
-/* FD_LAT_LP: the latency kernel's chains run their group law on lanes 0..3
-   of the wave instead of lane 0 alone.  Each formula is two rounds of four
+/* The latency kernel's chains run their group law on lanes 0..3 of the
+   wave instead of lane 0 alone.  Each formula is two rounds of four
    independent products (dbl: X^2, Y^2, Z^2, (X+Y)^2, then E*F, G*H, F*G,
    E*H; add: the four operand products, then the same four); lane l computes
    product l of a round and a DPP quad broadcast hands the four results to every lane,
    which then holds the whole point.  The values and their normalisation
    points are those of ge_dbl / ge_add_cached (same bounds), so a chain issues
-   about 2.2x fewer instructions for the same result. */
-#ifndef FD_LAT_LP
-#define FD_LAT_LP 1
-#endif
-
-DEV void lat_dbl( ge_p3 & P, bool needT ) {
-#if FD_LAT_LP
-  (void)needT; ge_dbl_lp( P, P );
-#else
-  ge_dbl( P, P, needT );
-#endif
-}
+   about 2.2x fewer instructions for the same result (single verify p50
+   320-322 vs 472-473 us, profiles/r02zd_latency_lp/ab_full). */
 
 /* another copy of signature i already finished this call (seq); the first
    active lane's reading, so that a lane-parallel chain leaves its loop as a
@@ -1181,14 +896,9 @@ DEV void lat_chain( ge_p3 & P, u32 const * tab, u32 const * ident, u32 kd[8], u3
     ge_cached e; load_cached( e, tab_entry( tab, ident, mag ) );
     if( w != (int)D-1 ) {
       #pragma unroll 1
-      for( int j=0; j<3; j++ ) lat_dbl( P, false );
-      lat_dbl( P, true );
+      for( int j=0; j<4; j++ ) ge_dbl_lp( P, P );
     }
-#if FD_LAT_LP
     ge_add_cached_lp( P, P, e, neg );
-#else
-    ge_add_cached( P, P, e, neg, true );
-#endif
     if( copies > 1u && lat_done( done, i, seq ) ) break;
   }
 }
@@ -1216,19 +926,20 @@ void k_verify_lat( ulong n, uchar const * __restrict__ sigs, uchar const * __res
                    int halfsize, signed char * __restrict__ codes, u32 copies, ulong * __restrict__ done, ulong seq ) {
   __shared__ lat_shared L;
   ulong i = blockIdx.x / copies;
-  if( i >= n ) return;
-  if( threadIdx.x >= 192u ) return;                        /* waves 3.. only hold the CU (LAT_WG) */
+  if( i >= n ) return;                                     /* workgroup-uniform */
+  /* waves 3..11 only hold the CU (LAT_WG): they do no work but stay through
+     both barriers */
   u32 wave = threadIdx.x >> 6, lane = threadIdx.x & 63u;
   u32 * tabA = atab + (ulong)blockIdx.x * ATAB_WORDS, * tabR = tabA + RTAB_OFF;   /* per copy */
   u32 const * ident = btab + IDENT_OFF;
 
   /* ---- phase 1 ---- */
-  if( lane == 0u ) {
+  if( lane == 0u && wave < 3u ) {
     if( wave < 2u ) {                                    /* decode A (wave 0) or R (wave 1), user.c:165-199 */
       u32 w[8];
       load_words( w, wave ? sigs + 64*i : pubs + 32*i, 8 );
       ge_p3 Q;
-      u32 f = ge_decode<FD_LAT_FREE != 0>( Q, w );
+      u32 f = ge_decode<true>( Q, w );                     /* open-sum products (lp_mul) */
       bool small = !(f & 1u) && ge_affine_is_small_order( Q );
       u32 xw[8], yw[8];
       fe_to_words( xw, Q.X ); fe_to_words( yw, Q.Y );
@@ -1276,8 +987,8 @@ void k_verify_lat( ulong n, uchar const * __restrict__ sigs, uchar const * __res
     return;
   }
 
-  /* ---- phase 2 (lanes 0..3 with FD_LAT_LP, else lane 0) ---- */
-  if( lane < (FD_LAT_LP ? 4u : 1u) ) {
+  /* ---- phase 2 (lanes 0..3 of waves 0..2) ---- */
+  if( lane < 4u && wave < 3u ) {
     ge_p3 P;
     if( wave < 2u ) {
       u32 xw[8], yw[8], kd[8];
@@ -1291,11 +1002,7 @@ void k_verify_lat( ulong n, uchar const * __restrict__ sigs, uchar const * __res
       fe_neg( nx, x ); fe_norm( nx, nx );
       if( wave == 0u ) fe_cmov( nx, x, L.k1neg );                          /* k1 < 0: [|k1|](+A) */
       u32 * tab = wave ? tabR : tabA;
-#if FD_LAT_LP
       build_cached_table_lp( tab, nx, y );
-#else
-      build_cached_table( tab, nx, y );
-#endif
       lat_chain( P, tab, ident, kd, L.D, done, i, seq, copies );
     } else {
       u32 bl[5], bh[5];
@@ -1307,10 +1014,9 @@ void k_verify_lat( ulong n, uchar const * __restrict__ sigs, uchar const * __res
       for( int bi=(int)BTG_ND-1; bi>=0; bi-- ) {
         if( bi != (int)BTG_ND-1 ) {
           #pragma unroll 1
-          for( int j=0; j<FD_BTAB_GW-1; j++ ) lat_dbl( P, false );
-          lat_dbl( P, true );
+          for( int j=0; j<BTG_GW; j++ ) ge_dbl_lp( P, P );
         }
-        b12_step<FD_LAT_LP != 0>( P, bl, bh, bmask, (u32)bi, btab, true );
+        b12_step<true>( P, bl, bh, bmask, (u32)bi, btab, true );
         if( copies > 1u && lat_done( done, i, seq ) ) break;
       }
     }
@@ -1472,16 +1178,21 @@ fd_ed25519_hip_ctx_new( int device, ulong chunk_sigs ) {
     FD_CHECK( hipDeviceGetAttribute( &ncu, hipDeviceAttributeMultiprocessorCount, device ) );
     FD_CHECK( hipOccupancyMaxActiveBlocksPerMultiprocessor( &per, k_verify_dsm, 256, 0 ) );
     ctx->dsm_wgs = (ulong)(ncu > 0 ? ncu : 1) * (ulong)(per > 0 ? per : 1);
+    /* k_verify_lat assumes one workgroup per CU (LAT_WG): a register-count
+       change that let two share a CU would make small calls slower, not
+       wrong -- say so once */
+    static int lat_warned;
     per = 0;
-    FD_CHECK( hipOccupancyMaxActiveBlocksPerMultiprocessor( &per, k_verify_prep, 256, 0 ) );
-    ctx->prep_wgs = (ulong)(ncu > 0 ? ncu : 1) * (ulong)(per > 0 ? per : 1);
+    FD_CHECK( hipOccupancyMaxActiveBlocksPerMultiprocessor( &per, k_verify_lat, LAT_WG, 0 ) );
+    if( per != 1 && !lat_warned ) {
+      lat_warned = 1;
+      fprintf( stderr, "fd_ed25519_hip: k_verify_lat fits %d workgroups per CU (expected 1)\n", per );
+    }
   }
   hipLaunchKernelGGL( k_btab_init, dim3( (2*BTAB_N + 63)/64 ), dim3( 64 ), 0, ctx->stream, ctx->d_btab );
   FD_CHECK( hipGetLastError() );
-#if FD_BTAB_W12
   hipLaunchKernelGGL( k_btab12_init, dim3( (2*BT12_N + 63)/64 ), dim3( 64 ), 0, ctx->stream, ctx->d_btab );
   FD_CHECK( hipGetLastError() );
-#endif
   {
     /* k_verify_lat copies: one per XCD, if the probe sees consecutive
        workgroups dealt to the XCDs in turn (one partition = one XCD: 1) */
@@ -1497,7 +1208,7 @@ fd_ed25519_hip_ctx_new( int device, ulong chunk_sigs ) {
     for( int j=0; j<NP; j++ ) nx = h_x[j] + 1u > nx ? h_x[j] + 1u : nx;
     int rr = nx > 1u && nx <= 16u;
     for( int j=0; rr && j<NP; j++ ) rr = h_x[j] == (h_x[0] + (u32)j) % nx;
-    ctx->lat_copies = rr && FD_LAT_COPIES ? nx : 1u;
+    ctx->lat_copies = rr ? nx : 1u;
     FD_CHECK( hipMalloc( (void **)&ctx->d_lat_done, LAT_MAX_N * sizeof(ulong) ) );
     FD_CHECK( hipMemsetAsync( ctx->d_lat_done, 0, LAT_MAX_N * sizeof(ulong), ctx->stream ) );
   }
@@ -1538,8 +1249,6 @@ fd_ed25519_hip_ctx_delete( fd_ed25519_hip_ctx_t * ctx ) {
   free_staging( ctx );
   for( int e=0; e<4; e++ ) (void)hipEventDestroy( ctx->ev[e] );
   (void)hipEventDestroy( ctx->ev_last );
-  if( ctx->h_stage ) (void)hipHostFree( ctx->h_stage );
-  if( ctx->d_stage ) (void)hipFree( ctx->d_stage );
   (void)hipStreamDestroy( ctx->stream );
   free( ctx );
 }
@@ -1750,7 +1459,7 @@ verify_impl( fd_ed25519_hip_ctx_t * ctx, ulong n, uchar const * d_sigs, uchar co
       FD_CHECK( hipGetLastError() );
     }
     uchar const * pool = d_msg_off ? d_pool : d_pool + off*(ulong)fixed_sz;
-    dim3 gprep( FD_PREP_PERSIST && grid.x > ctx->prep_wgs ? (unsigned)ctx->prep_wgs : grid.x );
+    dim3 gprep( grid.x );
     hipLaunchKernelGGL( k_verify_prep, gprep, blk, 0, s, m, ctx->chunk, d_sigs + 64*off, d_pubs + 32*off,
                         pool, d_msg_off ? d_msg_off + off : (uint const *)0,
                         d_msg_off ? d_msg_sz + off : (uint const *)0, fixed_sz, ctx->d_state, ctx->errmode,
@@ -1758,7 +1467,7 @@ verify_impl( fd_ed25519_hip_ctx_t * ctx, ulong n, uchar const * d_sigs, uchar co
     FD_CHECK( hipGetLastError() );
     if( ctx->timing ) FD_CHECK( hipEventRecord( ctx->ev[1], s ) );
     if( ctx->timing ) FD_CHECK( hipEventRecord( ctx->ev[3], s ) );
-    dim3 gdsm( FD_DSM_PERSIST && grid.x > ctx->dsm_wgs ? (unsigned)ctx->dsm_wgs : grid.x );
+    dim3 gdsm( grid.x > ctx->dsm_wgs ? (unsigned)ctx->dsm_wgs : grid.x );
     hipLaunchKernelGGL( k_verify_dsm, gdsm, blk, 0, s, ctx->chunk, ctx->d_state, ctx->d_btab, ctx->d_atab,
                         ctx->d_idx, ctx->d_count, d_codes + off, ctx->halfsize,
                         ordered ? ctx->d_order : (u32 const *)0 );
@@ -1911,31 +1620,68 @@ fd_ed25519_hip_verify_host( fd_ed25519_hip_ctx_t * ctx, ulong n, uchar const * s
   return 0;
 }
 
-/* ---- reference API on a lazily created process-wide context ----------
+/* ---- reference API on a process-wide context ------------------------
 
-   Each call stages its records in one pinned, device-mapped host block
-   (hipHostMalloc: the kernels read sig/pub/msg and write the codes in place
-   over PCIe, so a call is the kernel launches plus one stream sync, with no
-   hipMemcpy).  Layout, 16-byte aligned: sigs[16*64] pubs[16*32] off[16]
-   sz[16] codes[16] pad, then the message and 16 zero bytes (the kernel's
-   message loads may read up to 12 bytes past the end). */
+   The reference API is re-entrant with no global mutable state
+   (fd_ed25519.h:89-94) and replay calls it per transaction from many
+   threads (fd_executor.c:1608-1617).  Concurrent drop-in calls are therefore
+   combined: each caller appends its records and message to the open staging
+   batch (one pinned host block, with a device copy), and whichever caller
+   finds the GPU idle closes the open batch and runs it for everyone in it --
+   one DMA in, one launch sequence (k_verify_lat for small batches, the bulk
+   kernels above lat_max), one DMA of the codes back.  Callers arriving while
+   a batch runs gather in the next one, so N threads share launches instead
+   of queueing N launches behind one lock.  A single caller sees the same
+   path as before (one batch of its own records).
 
+   Staging block layout, 16-byte aligned: sigs[256*64] pubs[256*32]
+   off[256] sz[256] codes[256], then the callers' messages, each followed
+   by 16 zero bytes (the kernels' message loads may read past the end). */
+
+#define DROPIN_REC_MAX 256ul
 #define STAGE_SIGS   0ul
-#define STAGE_PUBS   1024ul
-#define STAGE_OFF    1536ul
-#define STAGE_SZ     1600ul
-#define STAGE_CODES  1664ul
-#define STAGE_MSG    1792ul
+#define STAGE_PUBS   (STAGE_SIGS + 64ul*DROPIN_REC_MAX)
+#define STAGE_OFF    (STAGE_PUBS + 32ul*DROPIN_REC_MAX)
+#define STAGE_SZ     (STAGE_OFF + 4ul*DROPIN_REC_MAX)
+#define STAGE_CODES  (STAGE_SZ + 4ul*DROPIN_REC_MAX)
+#define STAGE_MSG    (STAGE_CODES + DROPIN_REC_MAX)
+#define DROPIN_NBUF  3
+#define DROPIN_POOL0 65536ul       /* initial message bytes per staging block */
 
-static fd_ed25519_hip_ctx_t * g_ctx;
-static std::mutex             g_lock;
+enum { DSTAGE_FREE = 0, DSTAGE_OPEN, DSTAGE_RUNNING, DSTAGE_DONE };
+
+struct dropin_stage {
+  uchar * h;           /* pinned host block */
+  uchar * d;           /* its device copy */
+  ulong   cap;         /* bytes of each */
+  ulong   n, pool;     /* records and message bytes taken */
+  int     users;       /* callers attached (read their codes before the block is reused) */
+  int     state;
+  ulong   gen;         /* batch number */
+};
+
+static fd_ed25519_hip_ctx_t *   g_ctx;
+static std::mutex               g_ctx_lock;      /* creation of g_ctx */
+static std::mutex               g_dl;            /* the staging ring below */
+static std::condition_variable  g_dcv;
+static dropin_stage             g_stage[ DROPIN_NBUF ];
+static int                      g_open = -1;     /* the open block, -1: none */
+static int                      g_running;       /* a batch is on the GPU */
+static ulong                    g_gen;
+static ulong                    g_batches, g_batch_calls;   /* launches and the calls they served */
+
+static fd_ed25519_hip_ctx_t * default_ctx_new( int device ) {
+  fd_ed25519_hip_ctx_t * ctx = fd_ed25519_hip_ctx_new( device, 4096 );
+  char const * m = getenv( "FD_ED25519_HIP_ERRMODE" );
+  if( m && !strcmp( m, "ref" ) ) ctx->errmode = FD_ED25519_HIP_ERRMODE_REF;
+  return ctx;
+}
 
 static fd_ed25519_hip_ctx_t * default_ctx( void ) {
+  std::lock_guard<std::mutex> lk( g_ctx_lock );
   if( !g_ctx ) {
     char const * e = getenv( "FD_ED25519_HIP_DEVICE" );
-    g_ctx = fd_ed25519_hip_ctx_new( e ? atoi( e ) : 0, 4096 );
-    char const * m = getenv( "FD_ED25519_HIP_ERRMODE" );
-    if( m && !strcmp( m, "ref" ) ) g_ctx->errmode = FD_ED25519_HIP_ERRMODE_REF;
+    g_ctx = default_ctx_new( e ? atoi( e ) : 0 );
   }
   return g_ctx;
 }
@@ -1944,8 +1690,35 @@ static fd_ed25519_hip_ctx_t * default_ctx( void ) {
    (fd_sha512_hip.hip batching); not part of the public ABI */
 __attribute__((visibility("hidden"))) fd_ed25519_hip_ctx_t *
 fd_ed25519_hip_private_default_ctx( void ) {
-  std::lock_guard<std::mutex> lk( g_lock );
   return default_ctx();
+}
+
+static void stage_grow( fd_ed25519_hip_ctx_t * ctx, dropin_stage * b, ulong cap ) {
+  FD_CHECK( hipSetDevice( ctx->device ) );
+  if( b->h ) FD_CHECK( hipHostFree( b->h ) );
+  if( b->d ) FD_CHECK( hipFree( b->d ) );
+  FD_CHECK( hipHostMalloc( (void **)&b->h, cap, hipHostMallocDefault ) );
+  FD_CHECK( hipMalloc( (void **)&b->d, cap ) );
+  b->cap = cap;
+}
+
+int
+fd_ed25519_hip_dropin_init( int device ) {
+  {
+    std::lock_guard<std::mutex> lk( g_ctx_lock );
+    if( g_ctx ) return g_ctx->device == device ? 0 : -1;
+    g_ctx = default_ctx_new( device );
+  }
+  std::lock_guard<std::mutex> lk( g_dl );
+  for( int j=0; j<DROPIN_NBUF; j++ )
+    if( !g_stage[j].h ) stage_grow( g_ctx, &g_stage[j], STAGE_MSG + DROPIN_POOL0 );
+  return 0;
+}
+
+void
+fd_ed25519_hip_dropin_stats( ulong out[ 2 ] ) {
+  std::lock_guard<std::mutex> lk( g_dl );
+  out[0] = g_batches; out[1] = g_batch_calls;
 }
 
 /* The engine addresses messages with 32-bit offsets and sizes.  A longer
@@ -1953,7 +1726,7 @@ fd_ed25519_hip_private_default_ctx( void ) {
    be a silent divergence from the reference (which hashes all of it), so the
    process aborts loudly (SURVEY.md 8(b) "Errors": never a silent reject or
    accept). */
-#define DROPIN_MSG_MAX ((ulong)UINT32_MAX - 256ul)
+#define DROPIN_MSG_MAX ((ulong)UINT32_MAX - 256ul - STAGE_MSG)
 static void dropin_check_msg_sz( ulong msg_sz, char const * fn ) {
   if( msg_sz > DROPIN_MSG_MAX ) {
     fprintf( stderr, "fd_ed25519_hip: %s: msg_sz %lu exceeds the engine's 32-bit message limit (%lu)\n", fn,
@@ -1962,47 +1735,71 @@ static void dropin_check_msg_sz( ulong msg_sz, char const * fn ) {
   }
 }
 
-/* FD_DROPIN_DMA (default 1): the staged block is copied to HBM with one DMA
-   and the codes come back with another, instead of the kernels reading the
-   records (and the message, a few bytes per load) over PCIe from the mapped
-   host block, a round trip per dependent load.  Measured p50 per call (200-B
-   message, profiles/r02z_latency): see DESIGN.md 3. */
-#ifndef FD_DROPIN_DMA
-#define FD_DROPIN_DMA 1
-#endif
-
-/* stage n (sig, pub) pairs sharing one message and run them; codes land in
-   the staging block */
-static signed char const *
-dropin_run( fd_ed25519_hip_ctx_t * ctx, uchar const * msg, ulong msg_sz, uchar const * sigs,
-            uchar const * pubs, ulong n ) {
-  ulong need = STAGE_MSG + ((msg_sz + 16ul + 15ul) & ~15ul);
-  if( need > ctx->h_stage_cap ) {
-    ulong cap = need < 65536ul ? 65536ul : need;
-    FD_CHECK( hipSetDevice( ctx->device ) );
-    if( ctx->h_stage ) FD_CHECK( hipHostFree( ctx->h_stage ) );
-    FD_CHECK( hipHostMalloc( (void **)&ctx->h_stage, cap, hipHostMallocDefault ) );
-    if( FD_DROPIN_DMA ) {
-      if( ctx->d_stage ) FD_CHECK( hipFree( ctx->d_stage ) );
-      FD_CHECK( hipMalloc( (void **)&ctx->d_stage, cap ) );
-    }
-    ctx->h_stage_cap = cap;
-  }
-  uchar * st = ctx->h_stage;
-  memcpy( st + STAGE_SIGS, sigs, 64ul*n );
-  memcpy( st + STAGE_PUBS, pubs, 32ul*n );
-  uint * off = (uint *)(st + STAGE_OFF), * sz = (uint *)(st + STAGE_SZ);
-  for( ulong j=0; j<n; j++ ) { off[j] = 0u; sz[j] = (uint)msg_sz; }
-  if( msg_sz ) memcpy( st + STAGE_MSG, msg, msg_sz );
-  memset( st + STAGE_MSG + msg_sz, 0, 16 );
-  uchar * dv = FD_DROPIN_DMA ? ctx->d_stage : st;          /* what the kernels read and write */
-  if( FD_DROPIN_DMA ) FD_CHECK( hipMemcpyAsync( dv, st, need, hipMemcpyHostToDevice, ctx->stream ) );
-  verify_impl( ctx, n, dv + STAGE_SIGS, dv + STAGE_PUBS, dv + STAGE_MSG, (uint const *)(dv + STAGE_OFF),
-               (uint const *)(dv + STAGE_SZ), 0u, (signed char *)(dv + STAGE_CODES), NULL, NULL, NULL );
-  if( FD_DROPIN_DMA )
-    FD_CHECK( hipMemcpyAsync( st + STAGE_CODES, dv + STAGE_CODES, n, hipMemcpyDeviceToHost, ctx->stream ) );
+/* run the staging block (caller holds g_dl through lk; released while the
+   GPU works) */
+static void dropin_launch( fd_ed25519_hip_ctx_t * ctx, dropin_stage * b, std::unique_lock<std::mutex> & lk ) {
+  g_running = 1; b->state = DSTAGE_RUNNING; g_open = -1;
+  g_batches++; g_batch_calls += (ulong)b->users;
+  g_dcv.notify_all();                                      /* callers may open the next block now */
+  ulong n = b->n, bytes = STAGE_MSG + b->pool;
+  lk.unlock();
+  FD_CHECK( hipSetDevice( ctx->device ) );
+  FD_CHECK( hipMemcpyAsync( b->d, b->h, bytes, hipMemcpyHostToDevice, ctx->stream ) );
+  verify_impl( ctx, n, b->d + STAGE_SIGS, b->d + STAGE_PUBS, b->d + STAGE_MSG, (uint const *)(b->d + STAGE_OFF),
+               (uint const *)(b->d + STAGE_SZ), 0u, (signed char *)(b->d + STAGE_CODES), NULL, NULL, NULL );
+  FD_CHECK( hipMemcpyAsync( b->h + STAGE_CODES, b->d + STAGE_CODES, n, hipMemcpyDeviceToHost, ctx->stream ) );
   FD_CHECK( hipStreamSynchronize( ctx->stream ) );
-  return (signed char const *)(st + STAGE_CODES);
+  lk.lock();
+  b->state = DSTAGE_DONE; g_running = 0;
+  g_dcv.notify_all();
+}
+
+/* verify n (sig, pub) pairs over one message through the combining staging
+   ring; codes[j] gets the per-signature code */
+static void
+dropin_run( uchar const * msg, ulong msg_sz, uchar const * sigs, uchar const * pubs, ulong n, signed char * codes ) {
+  fd_ed25519_hip_ctx_t * ctx = default_ctx();
+  ulong need = (msg_sz + 16ul + 15ul) & ~15ul;             /* message + 16 zero bytes, 16-B aligned */
+  std::unique_lock<std::mutex> lk( g_dl );
+  dropin_stage * b;
+  for( ;; ) {
+    if( g_open < 0 ) {
+      int f = -1;
+      for( int j=0; j<DROPIN_NBUF; j++ ) if( g_stage[j].state == DSTAGE_FREE ) { f = j; break; }
+      if( f < 0 ) { g_dcv.wait( lk ); continue; }
+      dropin_stage * o = &g_stage[f];
+      if( !o->h ) stage_grow( ctx, o, STAGE_MSG + DROPIN_POOL0 );
+      o->state = DSTAGE_OPEN; o->n = 0; o->pool = 0; o->users = 0; o->gen = ++g_gen;
+      g_open = f;
+    }
+    b = &g_stage[g_open];
+    if( b->n + n <= DROPIN_REC_MAX && STAGE_MSG + b->pool + need <= b->cap ) break;
+    if( !b->n ) {                                          /* empty and too small: grow it */
+      ulong cap = STAGE_MSG + need;
+      stage_grow( ctx, b, cap > 2ul*b->cap ? cap : 2ul*b->cap );
+      break;
+    }
+    /* full: it runs as soon as the GPU is free (one of its callers starts
+       it, or we do), then this caller opens the next block */
+    if( !g_running ) { dropin_launch( ctx, b, lk ); continue; }
+    g_dcv.wait( lk );
+  }
+  ulong r0 = b->n, p0 = b->pool, gen = b->gen;
+  b->n += n; b->pool += need; b->users++;
+  uchar * h = b->h;
+  memcpy( h + STAGE_SIGS + 64ul*r0, sigs, 64ul*n );
+  memcpy( h + STAGE_PUBS + 32ul*r0, pubs, 32ul*n );
+  uint * off = (uint *)(h + STAGE_OFF), * sz = (uint *)(h + STAGE_SZ);
+  for( ulong j=0; j<n; j++ ) { off[r0+j] = (uint)p0; sz[r0+j] = (uint)msg_sz; }
+  if( msg_sz ) memcpy( h + STAGE_MSG + p0, msg, msg_sz );
+  memset( h + STAGE_MSG + p0 + msg_sz, 0, need - msg_sz );
+  for( ;; ) {
+    if( b->gen == gen && b->state == DSTAGE_DONE ) break;
+    if( !g_running && b->state == DSTAGE_OPEN ) { dropin_launch( ctx, b, lk ); break; }
+    g_dcv.wait( lk );
+  }
+  memcpy( codes, h + STAGE_CODES + r0, n );
+  if( !--b->users ) { b->state = DSTAGE_FREE; g_dcv.notify_all(); }
 }
 
 int
@@ -2010,9 +1807,9 @@ fd_ed25519_verify( uchar const msg[], ulong msg_sz, uchar const sig[64], uchar c
                    struct fd_sha512_private * sha ) {
   (void)sha;
   dropin_check_msg_sz( msg_sz, "fd_ed25519_verify" );
-  std::lock_guard<std::mutex> lk( g_lock );
-  signed char const * codes = dropin_run( default_ctx(), msg, msg_sz, sig, public_key, 1ul );
-  return (int)codes[0];
+  signed char code;
+  dropin_run( msg, msg_sz, sig, public_key, 1ul, &code );
+  return (int)code;
 }
 
 int
@@ -2022,8 +1819,8 @@ fd_ed25519_verify_batch_single_msg( uchar const msg[], ulong const msg_sz, uchar
   (void)shas;
   if( batch_sz == 0 || batch_sz > 16 ) return FD_ED25519_ERR_SIG;         /* user.c:238-241 */
   dropin_check_msg_sz( msg_sz, "fd_ed25519_verify_batch_single_msg" );
-  std::lock_guard<std::mutex> lk( g_lock );
-  signed char const * codes = dropin_run( default_ctx(), msg, msg_sz, signatures, pubkeys, (ulong)batch_sz );
+  signed char codes[16];
+  dropin_run( msg, msg_sz, signatures, pubkeys, (ulong)batch_sz, codes );
   int msg_fail = 0;
   for( int j=0; j<batch_sz; j++ ) {                                        /* pass-1 order, then pass 2 */
     if( codes[j] == FD_ED25519_ERR_SIG || codes[j] == FD_ED25519_ERR_PUBKEY ) return codes[j];

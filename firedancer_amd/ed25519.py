@@ -35,6 +35,7 @@ EXPORTS = (
     "fd_ed25519_hip_get_dsm_units", "fd_ed25519_hip_set_halfsize", "fd_ed25519_hip_test_halfsize",
     "fd_ed25519_hip_test_sha512", "fd_ed25519_hip_host_alloc", "fd_ed25519_hip_host_free",
     "fd_ed25519_hip_stage_async", "fd_ed25519_hip_test_prim", "fd_ed25519_hip_set_small_batch",
+    "fd_ed25519_hip_dropin_init", "fd_ed25519_hip_dropin_stats",
 )
 
 _lib = None
@@ -59,6 +60,9 @@ def lib():
         L.fd_ed25519_verify_batch_single_msg.argtypes = [c.c_char_p, u64, c.c_char_p, c.c_char_p, vp, c.c_ubyte]
         L.fd_ed25519_strerror.restype = c.c_char_p
         L.fd_ed25519_strerror.argtypes = [c.c_int]
+        L.fd_ed25519_hip_dropin_init.restype = c.c_int
+        L.fd_ed25519_hip_dropin_init.argtypes = [c.c_int]
+        L.fd_ed25519_hip_dropin_stats.argtypes = [c.POINTER(u64)]
         L.fd_ed25519_hip_ctx_new.restype = vp
         L.fd_ed25519_hip_ctx_new.argtypes = [c.c_int, u64]
         L.fd_ed25519_hip_ctx_delete.argtypes = [vp]
@@ -140,6 +144,19 @@ def fd_ed25519_verify_batch_single_msg(msg, signatures, pubkeys, batch_sz, shas=
 
 def fd_ed25519_strerror(err):
     return lib().fd_ed25519_strerror(int(err)).decode()
+
+
+def fd_ed25519_hip_dropin_init(device=0):
+    """Create the drop-in's process-wide context now (a tile's
+    privileged_init); 0, or -1 if it exists on another device."""
+    return lib().fd_ed25519_hip_dropin_init(int(device))
+
+
+def dropin_stats():
+    """(launches, calls served) of the drop-in's combining staging ring."""
+    out = (ctypes.c_ulong * 2)()
+    lib().fd_ed25519_hip_dropin_stats(out)
+    return int(out[0]), int(out[1])
 
 
 def _ptr(a, nbytes=0, name="buffer", device=None):

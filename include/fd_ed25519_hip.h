@@ -37,9 +37,17 @@ typedef unsigned int  uint;
    avx512/fd_r43x6_ge.c decode); fd_ed25519_hip_set_errmode() switches the
    error codes to the portable build's (the accept/reject bit is the same).
    Each call is synchronous on a process-wide context (device
-   FD_ED25519_HIP_DEVICE, default 0), staged through pinned device-mapped
-   host memory.  msg_sz above 2^32-257 aborts the process (the engine's
-   message offsets are 32-bit; hashing a prefix would silently diverge). */
+   FD_ED25519_HIP_DEVICE, default 0, or fd_ed25519_hip_dropin_init's) and
+   re-entrant: concurrent calls from different threads are combined into
+   one staged batch and one launch sequence (the caller that finds the GPU
+   idle runs the batch for all in it).  msg_sz above about 2^32-27K aborts
+   the process (the engine's message offsets are 32-bit; hashing a prefix
+   would silently diverge).
+
+   Sandboxed callers (a tile's unprivileged_init installs seccomp and closes
+   fds) must call fd_ed25519_hip_dropin_init() from privileged_init, so that
+   the HIP runtime opens /dev/kfd and /dev/dri and maps its memory before
+   the sandbox is up; INTEGRATION.md lists the fds and syscalls to allow. */
 
 struct fd_sha512_private;
 
@@ -67,6 +75,20 @@ fd_ed25519_verify_batch_single_msg( uchar const                msg[], /* msg_sz 
 char const *
 fd_ed25519_strerror( int err );
 
+/* Create the drop-in's process-wide context on `device` now (and its
+   pinned staging), instead of lazily at the first verify.  Returns 0, or -1
+   if the context already exists on another device.  Call it once from a
+   tile's privileged_init (the HIP context must exist before
+   the sandbox). */
+int
+fd_ed25519_hip_dropin_init( int device );
+
+/* Drop-in combining statistics: out[0] = launches (batches run),
+   out[1] = calls they served (>= out[0]; the ratio is the mean number of
+   concurrent calls combined per launch). */
+void
+fd_ed25519_hip_dropin_stats( ulong out[ 2 ] );
+
 /* ---- Part 2: GPU-native bulk interface -----------------------------------
 
    A context owns one HIP device, one stream, the base-point tables and the
@@ -84,7 +106,9 @@ fd_ed25519_strerror( int err );
      pool     message bytes; message i = pool[ msg_off[i], msg_off[i]+msg_sz[i] )
               (several signatures may share one message, as in a txn)
      codes    n int8 results (FD_ED25519_* codes, fd_ed25519_verify semantics)
-     bitmap   ceil(n/64) ulong: bit i%64 of word i/64 set iff codes[i]==0
+     bitmap   ceil(n/64) ulong: bit i%64 of word i/64 set iff codes[i]==0; the
+              bits of the last word past n are zero (device-count calls:
+              left as they were, see verify_dev_count)
    Device buffers for *_dev must be 16-byte aligned and the pool must stay
    readable 16 bytes past its last message byte.
 
