@@ -82,7 +82,8 @@ def test_concurrent_batch_single_msg_equals_reference():
     assert bad.size == 0, [(int(i), int(got[i]), int(exp[i])) for i in bad[:10]]
     assert all(a == b for a, b in single_exp.values())
     launches, calls = after[0] - before[0], after[1] - before[1]
-    assert calls == ng + len(single_exp)
+    real = int(((cnt >= 1) & (cnt <= 16)).sum())           # 0 / 17 return ERR_SIG before staging
+    assert calls == real + len(single_exp), (calls, real, len(single_exp))
     assert launches < calls, (launches, calls)          # concurrent calls shared launches
     print(f"concurrent drop-in: {calls} calls in {launches} launches ({calls / launches:.2f} per launch)")
 
