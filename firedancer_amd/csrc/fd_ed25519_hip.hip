@@ -1254,6 +1254,7 @@ fd_ed25519_hip_ctx_delete( fd_ed25519_hip_ctx_t * ctx ) {
 }
 
 int   fd_ed25519_hip_ctx_device( fd_ed25519_hip_ctx_t const * ctx ) { return ctx->device; }
+int   fd_ed25519_hip_device_cnt( void ) { int n = 0; return hipGetDeviceCount( &n ) == hipSuccess ? n : 0; }
 void *fd_ed25519_hip_ctx_stream( fd_ed25519_hip_ctx_t const * ctx ) { return (void *)ctx->stream; }
 void  fd_ed25519_hip_set_errmode( fd_ed25519_hip_ctx_t * ctx, int m ) { ctx->errmode = m; }
 void  fd_ed25519_hip_set_halfsize( fd_ed25519_hip_ctx_t * ctx, int on ) { ctx->halfsize = on ? 1 : 0; }
@@ -1551,6 +1552,20 @@ fd_ed25519_hip_host_alloc( ulong sz ) {
 void
 fd_ed25519_hip_host_free( void * p ) {
   if( p ) FD_CHECK( hipHostFree( p ) );
+}
+
+void *
+fd_ed25519_hip_host_register( void * p, ulong sz ) {
+  if( !p || !sz ) return NULL;
+  FD_CHECK( hipHostRegister( p, sz, hipHostRegisterMapped | hipHostRegisterPortable ) );
+  void * d = NULL;
+  FD_CHECK( hipHostGetDevicePointer( &d, p, 0 ) );
+  return d;
+}
+
+void
+fd_ed25519_hip_host_unregister( void * p ) {
+  if( p ) FD_CHECK( hipHostUnregister( p ) );
 }
 
 int

@@ -373,6 +373,9 @@ void k_txn_expand( ulong n, u8 const * __restrict__ pool, u8 const * __restrict_
                            source_ipv4 = vote.socket.addr, source_tpu =
                            GOSSIP, payload = vote.txn; sz > 2048 (or a
                            txn_sz past the 1232-B vote buffer) is corrupt
+   A QUIC / BUNDLE / SEND frag whose in chunk is its out chunk is left in
+   place (a host tile whose during_frag already copied the frag into its out
+   dcache, integration/fd_verify_tile_hip.patch).
    Per frag it emits the payload span for k_txn_parse, the fd_txn_m_txn_t
    offset and the header's bundle_id for the ordered host pass.  A corrupt
    frag sets bit 0 of *flag (the reference's FD_LOG_ERR: the host aborts in
@@ -385,8 +388,8 @@ DEVI void copy_bytes( u8 * __restrict__ d, u8 const * __restrict__ s, u32 nb, u3
 }
 
 __global__ __launch_bounds__(256)
-void k_txnm_ingest( ulong n, u8 const * __restrict__ in, u32 const * __restrict__ in_chunk,
-                    u16 const * __restrict__ in_sz, u8 const * __restrict__ in_kind, u8 * __restrict__ out,
+void k_txnm_ingest( ulong n, u8 const * in, u32 const * __restrict__ in_chunk,
+                    u16 const * __restrict__ in_sz, u8 const * __restrict__ in_kind, u8 * out,
                     u32 const * __restrict__ out_chunk, u32 * __restrict__ pay_off, u16 * __restrict__ pay_sz,
                     u32 * __restrict__ tout, u64 * __restrict__ bid, u32 * __restrict__ flag ) {
   u32 lane = threadIdx.x & 63u;
@@ -410,7 +413,7 @@ void k_txnm_ingest( ulong n, u8 const * __restrict__ in, u32 const * __restrict_
       }
     } else {
       bad = sz > FD_VERIFY_HIP_TPU_RAW_MTU;
-      copy_bytes( dst, src, bad ? 0u : sz, lane );
+      if( src != dst ) copy_bytes( dst, src, bad ? 0u : sz, lane );   /* in place: the tile copied it already */
       psz = bad ? 0u : *(u16 const *)(src + FD_VERIFY_HIP_TXNM_PAYLOAD_SZ_OFF);
       b   = bad ? 0ul : *(u64 const *)(src + FD_VERIFY_HIP_TXNM_BUNDLE_ID_OFF);
       if( psz > FD_TXN_HIP_MTU ) { bad = 1u; psz = 0u; }
@@ -771,6 +774,20 @@ fd_verify_hip_tile_submit_frags( fd_verify_hip_tile_t * t, ulong n, uchar const 
   TX_CHECK( hipEventRecord( s.ev_done, st ) );
   return 0;
 }
+
+extern "C" int
+fd_verify_hip_tile_poll( fd_verify_hip_tile_t const * t ) {
+  if( t->completed == t->submitted ) return -1;
+  tile_slot const & s = t->slot[t->completed & 1];
+  TX_CHECK( hipSetDevice( fd_ed25519_hip_ctx_device( t->ctx ) ) );
+  hipError_t e = hipEventQuery( s.ev_done );
+  if( e == hipErrorNotReady ) return 0;
+  TX_CHECK( e );
+  return 1;
+}
+
+extern "C" ulong
+fd_verify_hip_tile_inflight( fd_verify_hip_tile_t const * t ) { return t->submitted - t->completed; }
 
 extern "C" int
 fd_verify_hip_tile_complete( fd_verify_hip_tile_t * t, ulong const * bundle_id, signed char * result,

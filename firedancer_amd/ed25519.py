@@ -35,7 +35,8 @@ EXPORTS = (
     "fd_ed25519_hip_get_dsm_units", "fd_ed25519_hip_set_halfsize", "fd_ed25519_hip_test_halfsize",
     "fd_ed25519_hip_test_sha512", "fd_ed25519_hip_host_alloc", "fd_ed25519_hip_host_free",
     "fd_ed25519_hip_stage_async", "fd_ed25519_hip_test_prim", "fd_ed25519_hip_set_small_batch",
-    "fd_ed25519_hip_dropin_init", "fd_ed25519_hip_dropin_stats",
+    "fd_ed25519_hip_dropin_init", "fd_ed25519_hip_dropin_stats", "fd_ed25519_hip_host_register",
+    "fd_ed25519_hip_host_unregister", "fd_ed25519_hip_device_cnt",
 )
 
 _lib = None

@@ -38,7 +38,7 @@ EXPORTS = (
     "fd_verify_hip_tile_delete", "fd_verify_hip_tile_set_seed", "fd_verify_hip_tile_submit", "fd_verify_hip_tile_complete",
     "fd_verify_hip_tile_metrics", "fd_verify_hip_tile_last_timing", "fd_verify_hip_tile_submit_frags",
     "fd_verify_hip_before_frag", "fd_verify_hip_hist_edges", "fd_verify_hip_tile_hist_init",
-    "fd_verify_hip_tile_hist",
+    "fd_verify_hip_tile_hist", "fd_verify_hip_tile_poll", "fd_verify_hip_tile_inflight",
 )
 HIST_BUCKET_CNT = 16
 
@@ -78,6 +78,10 @@ def lib():
         L.fd_verify_hip_tile_submit.restype = c.c_int
         L.fd_verify_hip_tile_submit.argtypes = [vp, u64, vp, vp, vp, vp]
         L.fd_verify_hip_tile_complete.restype = c.c_int
+        L.fd_verify_hip_tile_poll.restype = c.c_int
+        L.fd_verify_hip_tile_poll.argtypes = [vp]
+        L.fd_verify_hip_tile_inflight.restype = u64
+        L.fd_verify_hip_tile_inflight.argtypes = [vp]
         L.fd_verify_hip_tile_complete.argtypes = [vp, vp, vp, vp, vp]
         L.fd_verify_hip_tile_metrics.argtypes = [vp, vp]
         L.fd_verify_hip_tile_last_timing.argtypes = [vp, vp]
@@ -199,6 +203,13 @@ class VerifyTile:
         if rc:
             raise RuntimeError(f"fd_verify_hip_tile_submit_frags: {rc}")
         self._pending.append((n, (d_in, in_chunk, in_sz, in_kind, d_out, out_chunk)))
+
+    def poll(self):
+        """fd_verify_hip_tile_poll: 1 oldest batch done, 0 running, -1 none (never blocks)."""
+        return int(self._lib.fd_verify_hip_tile_poll(self.tile))
+
+    def inflight(self):
+        return int(self._lib.fd_verify_hip_tile_inflight(self.tile))
 
     def complete(self, bundle_id=None):
         n, _keep = self._pending.pop(0)

@@ -123,6 +123,9 @@ typedef struct fd_ed25519_hip_ctx fd_ed25519_hip_ctx_t;
 fd_ed25519_hip_ctx_t * fd_ed25519_hip_ctx_new   ( int device, ulong chunk_sigs );
 void                   fd_ed25519_hip_ctx_delete( fd_ed25519_hip_ctx_t * ctx );
 int                    fd_ed25519_hip_ctx_device( fd_ed25519_hip_ctx_t const * ctx );
+/* HIP devices visible to the process (0 if none or the runtime fails);
+   a verify tile binds kind_id % this */
+int                    fd_ed25519_hip_device_cnt( void );
 /* Grow the per-launch scratch to at least chunk_sigs signatures (2.3 KB of
    HBM each); waits for the device to go idle first.  A caller whose record
    count is only known on the device (verify_dev_count) reserves its upper
@@ -302,6 +305,13 @@ fd_ed25519_hip_sign_dev( fd_ed25519_hip_ctx_t * ctx,
    GPU with no copy (fd_verify_hip_tile_submit_frags).  Aborts on failure. */
 void * fd_ed25519_hip_host_alloc( ulong sz );
 void   fd_ed25519_hip_host_free ( void * p );
+
+/* Map existing host memory (e.g. a tile's out-link dcache in its
+   workspace) for device access: page-locks [p, p+sz) and returns the
+   address kernels use for it (NULL for a NULL or empty range).  Call it
+   before the sandbox is up (privileged_init).  Aborts on failure. */
+void * fd_ed25519_hip_host_register  ( void * p, ulong sz );
+void   fd_ed25519_hip_host_unregister( void * p );
 
 /* Enqueue a host->device copy of sz bytes on stream (NULL: the context's
    stream), e.g. a verify tile's in-link dcache region staged into HBM ahead

@@ -196,6 +196,9 @@ fd_verify_hip_tile_submit( fd_verify_hip_tile_t * tile,
    fd_txn_t at fd_txn_m_txn_t and txn_t_sz into the header.  bundle_id comes
    from each header (complete's bundle_id argument is ignored for such a
    batch) and GOSSIP/SEND frags count into gossiped_votes_cnt (:112).
+   A QUIC/BUNDLE/SEND frag whose in and out addresses are the same is parsed
+   in place (no copy): a host tile that keeps during_frag's copy into its out
+   dcache passes in = out.
    A corrupt frag (sz > FD_TPU_RAW_MTU, or > 2048 for gossip; payload_sz >
    FD_TPU_MTU) aborts the process in complete(), as the reference's
    FD_LOG_ERR ends the tile.  All pointers are device-visible (HBM, or
@@ -210,6 +213,18 @@ fd_verify_hip_tile_submit_frags( fd_verify_hip_tile_t * tile,
                                  uchar const *          d_in_kind,
                                  uchar *                d_out,
                                  uint const *           d_out_chunk );
+
+/* Non-blocking: 1 if the oldest outstanding batch has finished on the GPU
+   (complete() will not wait), 0 if it is still running, -1 if no batch is
+   outstanding.  A stem loop polls from after_credit and calls complete()
+   only on 1, so its in-links keep draining while the GPU works
+   (integration/fd_verify_tile_hip.patch). */
+int
+fd_verify_hip_tile_poll( fd_verify_hip_tile_t const * tile );
+
+/* batches submitted and not yet completed (0, 1 or 2) */
+ulong
+fd_verify_hip_tile_inflight( fd_verify_hip_tile_t const * tile );
 
 int
 fd_verify_hip_tile_complete( fd_verify_hip_tile_t * tile,

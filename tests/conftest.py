@@ -23,6 +23,8 @@ def pytest_sessionstart(session):
     if os.path.isdir("/root/reference/src/ballet/ed25519"):
         import subprocess
         subprocess.check_call(["make", "-s", "-j8", "-C", os.path.join(REPO, "oracle"), "oracle", "ref"])
+        if os.path.exists(os.path.join(REPO, "firedancer_amd", "libfd_ed25519_hip.so")):
+            subprocess.check_call(["make", "-s", "-j8", "-C", os.path.join(REPO, "oracle"), "tile"])
 
 
 @pytest.fixture(scope="session")
