@@ -42,6 +42,19 @@ def read_fdo1(path, depth):
     return dict(frags=frags, metrics=met, oldest=oldest, ring=ring, map=mp, raw=b)
 
 
+def normalized(out):
+    """The driver output with each frag's alignment pad (the byte between an
+    odd-length payload and the 2-aligned fd_txn_t, fd_txn_m.h:101-104) left
+    out: the reference tile never writes it, so it holds whatever an earlier
+    frag left in the reused out chunk."""
+    frags = []
+    for sig, tsorig, b in out["frags"]:
+        psz, = struct.unpack_from("<H", b, 8)
+        at = (TXNM_SZ + psz + 1) & ~1
+        frags.append((sig, tsorig, b[:TXNM_SZ + psz], b[at:]))
+    return frags, out["metrics"].tobytes(), out["oldest"], out["ring"].tobytes(), out["map"].tobytes()
+
+
 def run_driver(which, in_path, out_path, env=None, timeout=300):
     exe = os.path.join(REF_DIR, f"tile_drv_{which}")
     assert os.path.exists(exe), f"{exe} missing: run __graft_entry__.build() in the build container"
