@@ -588,6 +588,14 @@ static void slot_free_records( tile_slot & s ) {
   s.d_rsig = s.d_rpub = 0; s.d_rmoff = s.d_rmsz = 0; s.d_rcode = 0; s.rcap = 0;
 }
 
+static void slot_records( tile_slot & s, ulong need ) {   /* (re)size the per-signature record buffers */
+  slot_free_records( s );
+  TX_CHECK( hipMalloc( &s.d_rsig, 64*need ) ); TX_CHECK( hipMalloc( &s.d_rpub, 32*need ) );
+  TX_CHECK( hipMalloc( &s.d_rmoff, 4*need ) ); TX_CHECK( hipMalloc( &s.d_rmsz, 4*need ) );
+  TX_CHECK( hipMalloc( &s.d_rcode, need ) );
+  s.rcap = need;
+}
+
 static void slot_free( tile_slot & s ) {
   (void)hipFree( s.d_tsz ); (void)hipFree( s.d_nsig ); (void)hipFree( s.d_sig_at ); (void)hipFree( s.d_acct_at );
   (void)hipFree( s.d_msg_at ); (void)hipFree( s.d_msg_sz ); (void)hipFree( s.d_tag ); (void)hipFree( s.d_first );
@@ -598,6 +606,11 @@ static void slot_free( tile_slot & s ) {
   (void)hipEventDestroy( s.ev_start ); (void)hipEventDestroy( s.ev_done );
   slot_free_records( s );
 }
+
+__global__ __launch_bounds__(256)
+void k_tile_results( ulong n, u16 const * __restrict__ tsz, signed char const * __restrict__ tcode,
+                     u64 const * __restrict__ tag, u64 const * __restrict__ bid, u8 const * __restrict__ kind,
+                     u32 const * __restrict__ counter, u32 const * __restrict__ flag, u8 * __restrict__ res );
 
 extern "C" fd_verify_hip_tile_t *
 fd_verify_hip_tile_new( fd_ed25519_hip_ctx_t * ctx, ulong max_txn, ulong seed, ulong depth, ulong map_cnt ) {
@@ -613,6 +626,21 @@ fd_verify_hip_tile_new( fd_ed25519_hip_ctx_t * ctx, ulong max_txn, ulong seed, u
   t->own_oldest = fd_verify_hip_tcache_reset( t->ring, depth, t->map, map_cnt );
   slot_alloc( t->slot[0], max_txn ); slot_alloc( t->slot[1], max_txn );
   fd_verify_hip_tile_hist_init( t, 10000ul, 1000000000ul );   /* 10 us .. 1 s */
+  /* Everything the batch path would otherwise do lazily, done now: record
+     buffers at their bound (12 signatures per frag) and this module's code
+     object loaded (the runtime loads a translation unit's kernels at their
+     first launch: file opens and NUMA queries).  A tile creates this in
+     privileged_init, so its sandboxed steady state needs neither
+     (integration/fd_verify_tile_hip.patch, verify_hip_seccomp). */
+  hipStream_t st = (hipStream_t)fd_ed25519_hip_ctx_stream( ctx );
+  for( int k = 0; k < 2; k++ ) {
+    slot_records( t->slot[k], 12ul*max_txn );
+    hipLaunchKernelGGL( k_tile_results, dim3( 1 ), dim3( 64 ), 0, st, 0ul, t->slot[k].d_tsz, t->slot[k].d_tcode,
+                        t->slot[k].d_tag, (u64 const *)0, (u8 const *)0, t->slot[k].d_counter, (u32 const *)0,
+                        t->slot[k].d_res );
+    TX_CHECK( hipGetLastError() );
+  }
+  TX_CHECK( hipStreamSynchronize( st ) );
   return t;
 }
 
@@ -688,13 +716,9 @@ submit_verify( fd_verify_hip_tile_t * t, tile_slot & s, hipStream_t st, ulong n,
      sig + pubkey each within FD_TXN_MTU, fd_txn.h:68); grow to that bound
      once instead of reading the count back twice */
   ulong need = 12ul * n;
-  if( s.rcap < need ) {
+  if( s.rcap < need ) {                                    /* n <= max_txn: sized at tile_new */
     TX_CHECK( hipStreamSynchronize( st ) );
-    slot_free_records( s );
-    TX_CHECK( hipMalloc( &s.d_rsig, 64*need ) ); TX_CHECK( hipMalloc( &s.d_rpub, 32*need ) );
-    TX_CHECK( hipMalloc( &s.d_rmoff, 4*need ) ); TX_CHECK( hipMalloc( &s.d_rmsz, 4*need ) );
-    TX_CHECK( hipMalloc( &s.d_rcode, need ) );
-    s.rcap = need;
+    slot_records( s, need );
   }
   TX_CHECK( hipMemsetAsync( s.d_counter, 0, 4, st ) );
   hipLaunchKernelGGL( k_txn_expand, grid, blk, 0, st, n, d_pool, s.d_nsig, s.d_sig_at, s.d_acct_at, s.d_msg_at,

@@ -243,6 +243,9 @@ main( int argc, char ** argv ) {
   if( sandboxed ) {
     FD_LOG_NOTICE(( "seccomp traps: %d", drv_trap_cnt ));
     for( int k=0; k<drv_trap_cnt && k<16; k++ ) FD_LOG_NOTICE(( "seccomp trap: syscall %d", drv_trap_nr[ k ] ));
+    /* a sandboxed tile never returns; leave without the runtime's exit
+       handlers (their munmap/mbind/close are outside the policy) */
+    syscall( SYS_exit_group, drv_trap_cnt ? 1 : 0 );
   }
 #endif
   free( obuf ); free( drv_arena ); free( topo ); free( in );
