@@ -641,6 +641,27 @@ fd_verify_hip_tile_new( fd_ed25519_hip_ctx_t * ctx, ulong max_txn, ulong seed, u
     TX_CHECK( hipGetLastError() );
   }
   TX_CHECK( hipStreamSynchronize( st ) );
+  {
+    /* one empty-payload frag through the whole batch path (ingest, parse,
+       expansion, verify launches, reduce, results, completion), then the
+       counters reset: the first real batch finds nothing left to set up */
+    u8 * d = 0;
+    TX_CHECK( hipMalloc( &d, 512 ) );
+    TX_CHECK( hipMemset( d, 0, 512 ) );
+    u32 * d_chunk = (u32 *)(d + 256); u16 * d_sz = (u16 *)(d + 260); u8 * d_kind = d + 262;
+    u16 const hsz = (u16)FD_VERIFY_HIP_TXNM_SZ;
+    TX_CHECK( hipMemcpy( d_sz, &hsz, 2, hipMemcpyHostToDevice ) );
+    signed char r = 0;
+    if( fd_verify_hip_tile_submit_frags( t, 1, d, d_chunk, d_sz, d_kind, d + 128, d_chunk ) ||
+        fd_verify_hip_tile_complete( t, NULL, &r, NULL, NULL ) || r != FD_VERIFY_HIP_FRAG_PARSE_FAIL ) {
+      fprintf( stderr, "fd_verify_hip: tile warm-up batch failed (%d)\n", (int)r );
+      abort();
+    }
+    TX_CHECK( hipFree( d ) );
+    t->m_parse = t->m_verify = t->m_dedup = t->m_bundle = t->m_pub = t->m_sigs = t->m_gossip = 0;
+    t->bundle_failed = 0; t->bundle_id = 0;
+    fd_verify_hip_tile_hist_init( t, 10000ul, 1000000000ul );
+  }
   return t;
 }
 
