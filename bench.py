@@ -35,7 +35,7 @@ the reference algorithm (the half-size kernel executes ~17% less), not a
 utilisation.  The kernel duration is measured live with HIP events on the
 launch stream.
 
-cpu_baseline (rank 0, N=1): the reference's own fd_ed25519_verify (AVX-512
+cpu_baseline (rank 0, every N, after the timed region): the reference's own fd_ed25519_verify (AVX-512
 IFMA build, compiled from the reference sources into oracle/_ref/) on a
 bounded 65536-record sample of the same batch, one pinned thread per core.
 """
@@ -219,6 +219,7 @@ def main():
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--cpu-seconds", type=float, default=8.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--dump-codes", default=None, help="c1/c2/c3/c5: each rank saves its codes to <prefix>.<rank>.npy")
     ap.add_argument("--force-dist", action="store_true", help="init torch.distributed even at world size 1")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="nccl (RCCL over xGMI, one rank per GPU: the driver's N-GPU runs); gloo rehearses the "
@@ -244,7 +245,7 @@ def main():
 
     from firedancer_amd import Verifier
     from firedancer_amd.ed25519 import CTX_STREAM
-    from firedancer_amd.workload import make_batch_gpu
+    from firedancer_amd.workload import make_batch_gpu, make_batch_gpu_range
 
     cfg = args.config
     if cfg == "c4":
@@ -260,7 +261,13 @@ def main():
         n = args.sigs or ((1 << 22) if cfg == "c3" else (1 << 20))
     chunk = min(n, 1 << 20)
     v = Verifier(device=local, chunk_sigs=chunk)      # signs the batch; runs the roofline leg
-    batch = make_batch_gpu(v, n, msg_sz=msg_sz, seed=0x5eed0001 + 7919 * rank, mix=mix, shared_msg=(cfg == "c3"))
+    if cfg == "c5":
+        # this rank's shard of one global seeded set: a one-process pass over
+        # [0, total) verifies the same records (workload.range_inputs)
+        batch = make_batch_gpu_range(v, lo, hi, msg_sz=msg_sz, mix=mix)
+    else:
+        batch = make_batch_gpu(v, n, msg_sz=msg_sz, seed=0x5eed0001 + 7919 * rank, mix=mix,
+                               shared_msg=(cfg == "c3"))
     dev = batch.dev
     codes = torch.zeros(n, dtype=torch.int8, device=dev)
     bitmap = torch.zeros((n + 63) // 64, dtype=torch.int64, device=dev)
@@ -335,6 +342,8 @@ def main():
         elapsed = float(t.item())
 
     c = codes.cpu().numpy()
+    if args.dump_codes:                       # this rank's verdicts, for the shard-vs-whole-set checks
+        np.save(f"{args.dump_codes}.{rank}.npy", c)
     bm = bitmap.cpu().numpy().view(np.uint64)
     bits = np.unpackbits(bm.view(np.uint8), bitorder="little")[:n].astype(bool)
     assert np.array_equal(bits, c == 0), "bitmap != codes"
@@ -378,7 +387,7 @@ def main():
     out = None
     if rank == 0:
         cpu = None
-        if not args.no_cpu_baseline and world == 1:
+        if not args.no_cpu_baseline:          # rank 0, after every rank's timed region
             k = min(65536, n)
             idx = slice(0, k)
             sigs = batch.sigs[idx].cpu().numpy(); pubs = batch.pubs[idx].cpu().numpy()
@@ -672,7 +681,7 @@ def run_c4(args, rank, world, local, dist):
     out = None
     if rank == 0:
         cpu = None
-        if not args.no_cpu_baseline and world == 1:
+        if not args.no_cpu_baseline:          # rank 0, after every rank's timed region
             k = min(32768, s.n)
             hi = int((s.off[:k].astype(np.int64) + s.sz[:k]).max())
             threads = max(1, min(args.cpu_threads, os.cpu_count() or 1))

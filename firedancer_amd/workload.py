@@ -104,6 +104,59 @@ def make_batch_gpu(verifier, n, msg_sz=64, seed=0x5eed0001, mix="c1", shared_msg
     return Batch(dev, d_sig, d_pub, d_pool, d_off, d_sz, kinds)
 
 
+GLOBAL_BLOCK = 1 << 20
+
+
+def range_inputs(lo, hi, msg_sz=64, seed=0x5eed0005, block=GLOBAL_BLOCK):
+    """Host inputs of records [lo, hi) of a global seeded set (config 5):
+    the set is cut into blocks of `block` records, block b drawn from
+    default_rng([seed, b]) (private keys, then its messages), so any range --
+    one rank's shard or the whole set -- is the same records.  Returns
+    (prvs (hi-lo, 32) u8, pool u8 with 16 zero bytes of tail, moff, msz)."""
+    b0, b1 = lo // block, (hi + block - 1) // block
+    prvs, pool = [], []
+    for b in range(b0, b1):
+        rng = np.random.default_rng([seed, b])
+        p = rng.integers(0, 256, size=(block, 32), dtype=np.uint8)
+        m = rng.integers(0, 256, size=block * msg_sz, dtype=np.uint8)
+        s0, s1 = max(lo, b * block) - b * block, min(hi, (b + 1) * block) - b * block
+        prvs.append(p[s0:s1])
+        pool.append(m[s0 * msg_sz:s1 * msg_sz])
+    n = hi - lo
+    pool = np.concatenate(pool + [np.zeros(16, np.uint8)])
+    moff = (np.arange(n, dtype=np.uint64) * msg_sz).astype(np.uint32)
+    return np.concatenate(prvs), pool, moff, np.full(n, msg_sz, np.uint32)
+
+
+def make_batch_gpu_range(verifier, lo, hi, msg_sz=64, seed=0x5eed0005, mix="c2", block=GLOBAL_BLOCK):
+    """Records [lo, hi) of the global seeded set (range_inputs), signed on
+    the GPU; mix="c2" mutates each block with its own seed, so the verdicts
+    of a range equal that range of a whole-set pass (bench.py config 5: each
+    rank generates and verifies only its shard)."""
+    import torch
+    dev = torch.device("cuda", verifier.device)
+    prvs, pool, moff, msz = range_inputs(lo, hi, msg_sz, seed, block)
+    n = hi - lo
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+    d_pool, d_off, d_sz = t(pool), t(moff.view(np.int32)), t(msz.view(np.int32))
+    d_pub = torch.empty((n, 32), dtype=torch.uint8, device=dev)
+    d_sig = torch.empty((n, 64), dtype=torch.uint8, device=dev)
+    verifier.sign_dev(n, t(prvs), d_pool, d_off, d_sz, d_pub, d_sig)
+    verifier.sync()
+    kinds = None
+    if mix == "c2":
+        kinds = torch.empty(n, dtype=torch.uint8, device=dev)
+        for b in range(lo // block, (hi + block - 1) // block):
+            # mutate whole blocks (a block's draws do not depend on the range)
+            s0, s1 = max(lo, b * block), min(hi, (b + 1) * block)
+            if s0 == b * block and s1 == (b + 1) * block:
+                kinds[s0 - lo:s1 - lo] = c2_mutate_torch(d_sig[s0 - lo:s1 - lo], d_pub[s0 - lo:s1 - lo],
+                                                         ((seed ^ 0xc2) & 0xffffffff) * 4096 + b)
+            else:
+                raise ValueError("make_batch_gpu_range with mix='c2' needs block-aligned ranges")
+    return Batch(dev, d_sig, d_pub, d_pool, d_off, d_sz, kinds)
+
+
 def c2_mutate_torch(sigs, pubs, seed):
     """The C2 mutation model on device tensors ((n,64) / (n,32) uint8), in
     place, for batches too large for the host loop; same distribution as

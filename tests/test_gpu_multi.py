@@ -63,10 +63,21 @@ def test_two_ranks_shard_and_gather(tmp_path):
 @pytest.mark.gpu
 def test_bench_world2_c5_gloo(tmp_path):
     port = _free_port()
+    """bench.py's N>1 path at world 2 (gloo: RCCL refuses two ranks on one
+    GPU): the JSON line carries the CPU baseline, and the two ranks'
+    verdicts -- each rank generates and verifies only its shard of the one
+    global C5 set -- equal a one-process pass over the whole set."""
+    import numpy as np
+    import torch
+
+    import bench
+    from firedancer_amd import Verifier
+    from firedancer_amd.workload import make_batch_gpu_range
+    prefix = str(tmp_path / "codes")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
            "--master-addr", "127.0.0.1", "--master-port", str(port), "bench.py", "--gpus", "2",
            "--config", "c5", "--sigs", str(1 << 21), "--steps", "2", "--warmup", "1",
-           "--dist-backend", "gloo", "--no-cpu-baseline"]
+           "--dist-backend", "gloo", "--cpu-seconds", "1", "--dump-codes", prefix]
     r = subprocess.run(cmd, cwd=REPO, capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stderr[-3000:]
     lines = [x for x in r.stdout.splitlines() if x.startswith("{")]
@@ -75,6 +86,22 @@ def test_bench_world2_c5_gloo(tmp_path):
     assert d["n_gpus"] == 2 and d["scaling"] == "strong" and d["config"]["config_id"] == "c5"
     assert d["value"] > 0 and d["steps"] == 2
     assert str(1 << 22) in d["config"]["workload"]          # n_all all-reduced over both ranks
+    cpu = d["cpu_baseline"]
+    assert cpu and cpu["value"] > 0 and cpu["kind"] == "reference" and cpu.get("codes_match") is True, cpu
+    total = 1 << 22
+    got = np.concatenate([np.load(f"{prefix}.{rk}.npy") for rk in range(2)])
+    for rk in range(2):
+        t, lo, hi = bench.c5_shard(1 << 21, rk, 2)
+        assert t == total and np.load(f"{prefix}.{rk}.npy").size == hi - lo
+    v = Verifier(device=0, chunk_sigs=1 << 20)
+    b = make_batch_gpu_range(v, 0, total)
+    codes = torch.zeros(total, dtype=torch.int8, device=b.dev)
+    v.verify_dev(total, b.sigs, b.pubs, b.pool, b.msg_off, b.msg_sz, codes)
+    v.sync()
+    whole = codes.cpu().numpy()
+    v.close()
+    assert np.array_equal(got, whole)
+    assert 0.75 < float((whole == 0).mean()) < 0.83
 
 
 @pytest.mark.gpu
@@ -96,7 +123,7 @@ def test_c5_full_size_sharded_on_one_gpu():
     n, world = 1 << 26, 8
     dev = torch.device("cuda", 0)
     gen = Verifier(device=0, chunk_sigs=1 << 20)
-    b = W.make_batch_gpu(gen, n, msg_sz=64, seed=0xc5, mix="c2")
+    b = W.make_batch_gpu_range(gen, 0, n)                  # the global set bench.py's C5 ranks shard
     codes = torch.full((n,), 9, dtype=torch.int8, device=dev)
     bm = torch.zeros(n // 64, dtype=torch.int64, device=dev)
     torch.cuda.synchronize()

@@ -70,3 +70,21 @@ def test_bench_c5_shards_cover_2p26():
         assert all(s % 64 == 0 and s % (1 << 20) == 0 for s in sizes)
     t, lo, hi = bench.c5_shard(1 << 21, 1, 2)               # --sigs per rank (the gloo rehearsal)
     assert (t, lo, hi) == (1 << 22, 1 << 21, 1 << 22)
+
+
+def test_c5_global_set_ranges_are_slices():
+    """config 5's global set (workload.range_inputs): any block-aligned or
+    unaligned range [lo, hi) is exactly that slice of the whole set, so a
+    rank that generates only its shard verifies the whole-set records."""
+    import numpy as np
+    from firedancer_amd.workload import range_inputs
+    blk, total = 1 << 10, 1 << 13
+    prv, pool, moff, msz = range_inputs(0, total, block=blk)
+    assert prv.shape == (total, 32) and pool.size == 64 * total + 16
+    for lo, hi in ((0, blk), (blk, 3 * blk), (5 * blk, total), (100, 4000), (2047, 2049)):
+        p2, q2, o2, s2 = range_inputs(lo, hi, block=blk)
+        assert np.array_equal(p2, prv[lo:hi])
+        assert np.array_equal(q2[:-16], pool[64 * lo:64 * hi]) and not q2[-16:].any()
+        assert np.array_equal(o2, moff[:hi - lo]) and (s2 == 64).all()
+    # different blocks draw different keys
+    assert not np.array_equal(prv[:blk], prv[blk:2 * blk])
