@@ -83,6 +83,22 @@ def c5_shard(sigs_per_rank, rank, world):
 ISSUE_UNITS = 933793      # survivors per launch in that pass (the C2 2^20 batch, seed 0x5eed0001: deterministic)
 
 
+def profile_build_check(summary):
+    """Does the committed profile summary describe the kernels of the library
+    this run loaded?  Compares the gfx950 machine-code hashes the summary
+    records (firedancer_amd/kernel_hash.py) with the loaded library's."""
+    want = summary.get("kernel_sha") or {}
+    try:
+        from firedancer_amd.kernel_hash import engine_kernel_hashes
+        have = engine_kernel_hashes()
+    except Exception as e:                     # noqa: BLE001 -- reported, never fatal to the bench line
+        return {"profile_matches_build": None, "kernel_sha_error": str(e)}
+    keys = [k for k in ("k_verify_dsm", "k_verify_prep") if k in want]
+    ok = bool(keys) and all(want[k] == have.get(k) for k in keys)
+    return {"profile_matches_build": ok, "kernel_sha": {k: have.get(k) for k in keys},
+            "profile_kernel_sha": {k: want[k] for k in keys}}
+
+
 def issue_roofline(dsm_avg_ms, units_per_launch):
     """VALU issue roofline of k_verify_dsm from the committed PMC pass of this
     build (profiles/ISSUE_SUMMARY, tools/run_valu_calib.sh):
@@ -118,6 +134,7 @@ def issue_roofline(dsm_avg_ms, units_per_launch):
             "held_clock_ghz_pmc_pass": e["held_clock_ghz"],
             "issue_slots_per_launch": round(slots), "dual_issue_share": e["dual_issue_share"],
             "slots_scaled_from_c2": abs(units_per_launch - ISSUE_UNITS) > 0.5,
+            **profile_build_check(cal),
             "single_issue_ceiling": cal.get("single_issue_ceiling_slot_util"),
             "issue_source": f"profiles/{ISSUE_SUMMARY} (rocprofv3 --pmc SQ_INSTS_VALU SQ_ACTIVE_INST_VALU2 "
                             "GRBM_GUI_ACTIVE ..., one pass, bench.py --contexts 1)"}

@@ -910,9 +910,14 @@ fd_verify_hip_tile_complete( fd_verify_hip_tile_t * t, ulong const * bundle_id, 
   return 0;
 }
 
-extern "C" void fd_verify_hip_tile_metrics( fd_verify_hip_tile_t const * t, ulong out[7] ) {
+extern "C" void fd_verify_hip_tile_metrics( fd_verify_hip_tile_t const * t, ulong out[6] ) {
   out[0] = t->m_parse; out[1] = t->m_verify; out[2] = t->m_dedup; out[3] = t->m_bundle;
-  out[4] = t->m_pub; out[5] = t->m_sigs; out[6] = t->m_gossip;
+  out[4] = t->m_pub; out[5] = t->m_sigs;
+}
+
+extern "C" void fd_verify_hip_tile_metrics2( fd_verify_hip_tile_t const * t, ulong out[7] ) {
+  fd_verify_hip_tile_metrics( t, out );
+  out[6] = t->m_gossip;
 }
 
 /* before_frag (fd_verify_tile.c:37-58): 1 = skip the frag */

@@ -36,7 +36,7 @@ EXPORTS = (
     "fd_verify_hip_tcache_reset", "fd_verify_hip_tcache_query", "fd_verify_hip_tcache_insert",
     "fd_verify_hip_tile_new", "fd_verify_hip_tile_join_tcache", "fd_verify_hip_tile_tcache_reset",
     "fd_verify_hip_tile_delete", "fd_verify_hip_tile_set_seed", "fd_verify_hip_tile_submit", "fd_verify_hip_tile_complete",
-    "fd_verify_hip_tile_metrics", "fd_verify_hip_tile_last_timing", "fd_verify_hip_tile_submit_frags",
+    "fd_verify_hip_tile_metrics", "fd_verify_hip_tile_metrics2", "fd_verify_hip_tile_last_timing", "fd_verify_hip_tile_submit_frags",
     "fd_verify_hip_before_frag", "fd_verify_hip_hist_edges", "fd_verify_hip_tile_hist_init",
     "fd_verify_hip_tile_hist", "fd_verify_hip_tile_poll", "fd_verify_hip_tile_inflight",
 )
@@ -84,6 +84,7 @@ def lib():
         L.fd_verify_hip_tile_inflight.argtypes = [vp]
         L.fd_verify_hip_tile_complete.argtypes = [vp, vp, vp, vp, vp]
         L.fd_verify_hip_tile_metrics.argtypes = [vp, vp]
+        L.fd_verify_hip_tile_metrics2.argtypes = [vp, vp]
         L.fd_verify_hip_tile_last_timing.argtypes = [vp, vp]
         L.fd_verify_hip_tile_submit_frags.restype = c.c_int
         L.fd_verify_hip_tile_submit_frags.argtypes = [vp, u64, vp, vp, vp, vp, vp, vp]
@@ -232,7 +233,7 @@ class VerifyTile:
 
     def metrics(self):
         out = np.zeros(7, np.uint64)
-        self._lib.fd_verify_hip_tile_metrics(self.tile, out.ctypes.data)
+        self._lib.fd_verify_hip_tile_metrics2(self.tile, out.ctypes.data)
         keys = ("parse_fail_cnt", "verify_fail_cnt", "dedup_fail_cnt", "bundle_peer_fail_cnt", "published", "sigs",
                 "gossiped_votes_cnt")
         return dict(zip(keys, (int(x) for x in out)))

@@ -235,9 +235,12 @@ fd_verify_hip_tile_complete( fd_verify_hip_tile_t * tile,
 
 /* metrics (cumulative): out[0..3] = parse_fail, verify_fail, dedup_fail,
    bundle_peer_fail (fd_verify_tile.h:51-57); out[4] = published,
-   out[5] = signatures sent to the GPU verify, out[6] = gossiped_votes
-   (GOSSIP/SEND frags, fd_verify_tile.c:33,112) */
-void fd_verify_hip_tile_metrics( fd_verify_hip_tile_t const * tile, ulong out[ 7 ] );
+   out[5] = signatures sent to the GPU verify.  metrics2 adds out[6] =
+   gossiped_votes (GOSSIP/SEND frags, fd_verify_tile.c:33,112); the 6-slot
+   form keeps the layout of ABI version 1. */
+#define FD_VERIFY_HIP_ABI_VERSION 2
+void fd_verify_hip_tile_metrics ( fd_verify_hip_tile_t const * tile, ulong out[ 6 ] );
+void fd_verify_hip_tile_metrics2( fd_verify_hip_tile_t const * tile, ulong out[ 7 ] );
 
 /* timing of the last completed batch (ms): out[0] = GPU (first kernel to
    results on host, HIP events), out[1] = host ordered pass, out[2] =

@@ -77,3 +77,13 @@ def test_headers_compile_and_link_as_c(tmp_path):
                            "-Wl,-rpath," + libdir, "-o", str(exe)])
     out = subprocess.check_output([str(exe)]).decode().strip()
     assert int(out) == len(names)
+
+
+def test_kernel_hashes_found():
+    """firedancer_amd/kernel_hash.py finds the bulk kernels' gfx950 code in the
+    built library (bench.py uses it to tell whether the committed profile
+    summaries measured this build)."""
+    from firedancer_amd.kernel_hash import engine_kernel_hashes
+    h = engine_kernel_hashes()
+    assert set(h) == {"k_verify_dsm", "k_verify_prep"}, h
+    assert all(len(v) == 16 and int(v, 16) >= 0 for v in h.values())
