@@ -223,6 +223,9 @@ def main():
                     help="c4: verify tiles (host threads + contexts) per GPU (r02n, 2^20 frags per step, resident / "
                          "PCIe-inclusive M verifies/s: 2 -> 101-103 / 75-85, 4 -> 100-102 / 90-95, 6 -> 106-109 / "
                          "98-101, 8 -> 100-102 / 97-98)")
+    ap.add_argument("--dsm-share", type=int, default=1,
+                    help="c4: each tile's k_verify_dsm grid is 1/share of the resident slots, so that many "
+                         "tiles' DSM launches share the GPU")
     ap.add_argument("--c4-ingest", default="frags", choices=["frags", "payload"],
                     help="c4: fd_txn_m_t frags in each tile's in-link dcache (default) or raw payloads + offsets")
     ap.add_argument("--c4-pcie", default="dma", choices=["zerocopy", "dma", "dma_tile_stream"],
@@ -537,6 +540,8 @@ def run_c4(args, rank, world, local, dist):
     dev = torch.device("cuda", local)
     depth = 4194302
     vs = [v] + [Verifier(device=local, chunk_sigs=1 << 16) for _ in range(T - 1)]
+    for vv in vs:
+        vv.set_dsm_share(args.dsm_share)
     to_dev = lambda a, view=None: torch.from_numpy(np.ascontiguousarray(a if view is None else a.view(view))).to(dev)
     parts, h2d_bytes = [], 0
     d_pool = None if frags_mode else to_dev(s.pool)
@@ -726,7 +731,7 @@ def run_c4(args, rank, world, local, dist):
                                    f"1-12 sigs, <=1232 B, GPU fd_txn_parse, {T} verify tiles (round robin), "
                                    f"tcache dedup depth {depth} each",
                        "config_id": "c4", "frags_per_gpu": s.n, "sigs_per_batch": n_sig_batch, "verify_tiles": T,
-                       "parallelism": f"dp{world} (frag shards; {T} verify tiles per GPU)"},
+                       "parallelism": f"dp{world} (frag shards; {T} verify tiles per GPU)", "dsm_share": args.dsm_share},
             "frags_per_s": round(frags / elapsed, 1),
             "frag_outcomes_last_batch": {names[k]: v_ for k, v_ in counts.items()},
             "batch_gpu_ms": round(float(np.median(gpu_ms)), 4),

@@ -124,6 +124,7 @@ struct fd_ed25519_hip_ctx {
   u32 *        d_idx;       /* chunk: compacted survivor indices */
   u32 *        d_count;     /* [0] survivor count; [16..47] k_msg_order's histogram and cursors */
   ulong        dsm_wgs;     /* resident k_verify_dsm workgroups (its persistent grid) */
+  ulong        dsm_share;   /* the grid is dsm_wgs / dsm_share (contexts sharing the GPU) */
   u32 *        d_order;     /* chunk: k_verify_prep's record order (variable-size message paths) */
   int          errmode;
   int          halfsize;    /* 1: half-size scalars (default); 0: full-length (k, 1) */
@@ -1258,6 +1259,7 @@ int   fd_ed25519_hip_device_cnt( void ) { int n = 0; return hipGetDeviceCount( &
 void *fd_ed25519_hip_ctx_stream( fd_ed25519_hip_ctx_t const * ctx ) { return (void *)ctx->stream; }
 void  fd_ed25519_hip_set_errmode( fd_ed25519_hip_ctx_t * ctx, int m ) { ctx->errmode = m; }
 void  fd_ed25519_hip_set_halfsize( fd_ed25519_hip_ctx_t * ctx, int on ) { ctx->halfsize = on ? 1 : 0; }
+void  fd_ed25519_hip_set_dsm_share( fd_ed25519_hip_ctx_t * ctx, ulong share ) { ctx->dsm_share = share ? share : 1ul; }
 void  fd_ed25519_hip_set_small_batch( fd_ed25519_hip_ctx_t * ctx, ulong max_n ) {
   ctx->lat_max = max_n < LAT_MAX_N ? max_n : LAT_MAX_N;
 }
@@ -1468,7 +1470,9 @@ verify_impl( fd_ed25519_hip_ctx_t * ctx, ulong n, uchar const * d_sigs, uchar co
     FD_CHECK( hipGetLastError() );
     if( ctx->timing ) FD_CHECK( hipEventRecord( ctx->ev[1], s ) );
     if( ctx->timing ) FD_CHECK( hipEventRecord( ctx->ev[3], s ) );
-    dim3 gdsm( grid.x > ctx->dsm_wgs ? (unsigned)ctx->dsm_wgs : grid.x );
+    ulong dsm_grid = ctx->dsm_wgs / (ctx->dsm_share ? ctx->dsm_share : 1ul);
+    if( !dsm_grid ) dsm_grid = 1ul;
+    dim3 gdsm( grid.x > dsm_grid ? (unsigned)dsm_grid : grid.x );
     hipLaunchKernelGGL( k_verify_dsm, gdsm, blk, 0, s, ctx->chunk, ctx->d_state, ctx->d_btab, ctx->d_atab,
                         ctx->d_idx, ctx->d_count, d_codes + off, ctx->halfsize,
                         ordered ? ctx->d_order : (u32 const *)0 );

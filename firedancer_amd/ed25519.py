@@ -36,7 +36,7 @@ EXPORTS = (
     "fd_ed25519_hip_test_sha512", "fd_ed25519_hip_host_alloc", "fd_ed25519_hip_host_free",
     "fd_ed25519_hip_stage_async", "fd_ed25519_hip_test_prim", "fd_ed25519_hip_set_small_batch",
     "fd_ed25519_hip_dropin_init", "fd_ed25519_hip_dropin_stats", "fd_ed25519_hip_host_register",
-    "fd_ed25519_hip_host_unregister", "fd_ed25519_hip_device_cnt",
+    "fd_ed25519_hip_host_unregister", "fd_ed25519_hip_device_cnt", "fd_ed25519_hip_set_dsm_share",
 )
 
 _lib = None
@@ -74,6 +74,7 @@ def lib():
         L.fd_ed25519_hip_set_errmode.argtypes = [vp, c.c_int]
         L.fd_ed25519_hip_set_halfsize.argtypes = [vp, c.c_int]
         L.fd_ed25519_hip_set_small_batch.argtypes = [vp, u64]
+        L.fd_ed25519_hip_set_dsm_share.argtypes = [vp, u64]
         L.fd_ed25519_hip_test_halfsize.argtypes = [vp, c.c_ulong, vp, vp, vp]
         L.fd_ed25519_hip_test_sha512.argtypes = [vp, c.c_ulong, vp, vp, vp, vp, vp]
         L.fd_ed25519_hip_test_prim.restype = c.c_int
@@ -321,6 +322,10 @@ class Verifier:
                 self._p(msg_sz, 4 * n, "msg_sz"), self._p(pubs, 32 * n, "pubs"), self._p(sigs, 64 * n, "sigs"))
         with self._stream(stream) as h:
             return self._lib.fd_ed25519_hip_sign_dev(*args, h)
+
+    def set_dsm_share(self, share):
+        """k_verify_dsm grid = 1/share of the resident workgroup slots (contexts sharing the GPU)."""
+        lib().fd_ed25519_hip_set_dsm_share(self.ctx, int(share))
 
     def set_halfsize(self, on):
         """Half-size scalars (default) or the full-length pair (k, 1): same verdicts."""

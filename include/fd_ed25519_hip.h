@@ -153,6 +153,13 @@ void                   fd_ed25519_hip_set_halfsize( fd_ed25519_hip_ctx_t * ctx, 
    with throughput work on other streams should lower the limit or set 0. */
 void                   fd_ed25519_hip_set_small_batch( fd_ed25519_hip_ctx_t * ctx, ulong max_n );
 
+/* k_verify_dsm runs a persistent grid sized to every resident workgroup
+   slot of the GPU.  share > 1 sizes it to 1/share of them, so that that
+   many contexts' DSM launches (verify tiles on other streams) run side by
+   side and fill each other's tails instead of queueing whole-GPU grids.
+   Default 1; same verdicts. */
+void                   fd_ed25519_hip_set_dsm_share( fd_ed25519_hip_ctx_t * ctx, ulong share );
+
 /* Test hook: the device half-size reduction of n scalars k < L (d_k: 8 LE
    u32 words each) into d_out (18 words each: |k1| (8), k2 (8), k1 < 0 ? ~0 :
    0, max bit length).  Asynchronous on stream. */
