@@ -60,6 +60,7 @@ SIMDS, MAX_CLOCK = 256 * 4, 2.4e9         # MI355X_MICROARCH.md: 256 CU x 4 SIMD
 PEAK_SLOTS = SIMDS * MAX_CLOCK / 4        # VALU issue slots/s: one quad-cycle per SIMD at the max clock
 PMC_SUMMARY = "r02zd_pmc_summary.json"    # rocprofv3 PMC passes of this kernel build (tools/run_profile.sh)
 ISSUE_SUMMARY = "r02zd_valu_issue_calibration.json"   # VALU issue-slot pass of this build (tools/run_valu_calib.sh)
+ISSUE_SUMMARY_C4 = "r03c_c4_valu_issue.json"          # the same pass over C4's timing-leg batch (tools/run_c4_issue.sh)
 
 
 def w_total(msg_sz):
@@ -99,7 +100,7 @@ def profile_build_check(summary):
             "profile_kernel_sha": {k: want[k] for k in keys}}
 
 
-def issue_roofline(dsm_avg_ms, units_per_launch):
+def issue_roofline(dsm_avg_ms, units_per_launch, summary=ISSUE_SUMMARY):
     """VALU issue roofline of k_verify_dsm from the committed PMC pass of this
     build (profiles/ISSUE_SUMMARY, tools/run_valu_calib.sh):
       slots per launch  = SQ_INSTS_VALU - SQ_ACTIVE_INST_VALU2 (quad-cycles of a
@@ -116,13 +117,14 @@ def issue_roofline(dsm_avg_ms, units_per_launch):
       frac_at_max_clock = achieved / (1024 x 2.4 GHz / 4)
     DESIGN.md 6 states the formula; the single-issue microbenchmark ceiling
     (tools/valu_rates2 under the same counters) is ~0.95."""
-    path = os.path.join(REPO, "profiles", ISSUE_SUMMARY)
+    path = os.path.join(REPO, "profiles", summary)
     if not os.path.exists(path):
         return None
     with open(path) as f:
         cal = json.load(f)
     e = cal["engine"]["k_verify_dsm"]
-    scale = units_per_launch / ISSUE_UNITS           # exact (1) for C2; per-survivor scaling otherwise
+    units_ref = e.get("units", ISSUE_UNITS)
+    scale = units_per_launch / units_ref             # exact (1) for the profiled batch; per-survivor scaling otherwise
     slots, cycles = e["issue_slots"] * scale, e["grbm_cycles_per_xcd"] * scale
     t = dsm_avg_ms * 1e-3
     achieved = slots / t
@@ -133,11 +135,26 @@ def issue_roofline(dsm_avg_ms, units_per_launch):
             "frac_at_max_clock": round(achieved / PEAK_SLOTS, 4), "held_clock_ghz": round(clock / 1e9, 4),
             "held_clock_ghz_pmc_pass": e["held_clock_ghz"],
             "issue_slots_per_launch": round(slots), "dual_issue_share": e["dual_issue_share"],
-            "slots_scaled_from_c2": abs(units_per_launch - ISSUE_UNITS) > 0.5,
+            "slots_scaled_from_c2": summary == ISSUE_SUMMARY and abs(units_per_launch - units_ref) > 0.5,
+            "slots_scaled_from_profiled_units": abs(units_per_launch - units_ref) > 0.5,
             **profile_build_check(cal),
             "single_issue_ceiling": cal.get("single_issue_ceiling_slot_util"),
-            "issue_source": f"profiles/{ISSUE_SUMMARY} (rocprofv3 --pmc SQ_INSTS_VALU SQ_ACTIVE_INST_VALU2 "
-                            "GRBM_GUI_ACTIVE ..., one pass, bench.py --contexts 1)"}
+            "issue_source": f"profiles/{summary} (rocprofv3 --pmc SQ_INSTS_VALU SQ_ACTIVE_INST_VALU2 "
+                            "GRBM_GUI_ACTIVE ..., one pass, " +
+                            ("bench.py --config c4, the timing leg's dispatch)" if summary == ISSUE_SUMMARY_C4
+                             else "bench.py --contexts 1)")}
+
+
+def c4_issue_roofline(dsm_avg_ms, units_per_launch):
+    """C4 reads its own PMC pass when one of this build is committed (the
+    unit counts agree: the C4 stream is deterministic); otherwise C2's,
+    scaled per survivor (slots_scaled_from_c2 true)."""
+    path = os.path.join(REPO, "profiles", ISSUE_SUMMARY_C4)
+    if os.path.exists(path):
+        r = issue_roofline(dsm_avg_ms, units_per_launch, ISSUE_SUMMARY_C4)
+        if r and r.get("profile_matches_build") and not r["slots_scaled_from_profiled_units"]:
+            return r
+    return issue_roofline(dsm_avg_ms, units_per_launch)
 
 
 def prep_issue_util():
@@ -736,7 +753,7 @@ def run_c4(args, rank, world, local, dist):
             "frag_outcomes_last_batch": {names[k]: v_ for k, v_ in counts.items()},
             "batch_gpu_ms": round(float(np.median(gpu_ms)), 4),
             "batch_host_ms": round(float(np.median(host_ms)), 4),
-            "roofline": dict(issue_roofline(dsm_avg, dsm_units / launches) or {}, **{
+            "roofline": dict(c4_issue_roofline(dsm_avg, dsm_units / launches) or {}, **{
                          "kernel": "k_verify_dsm", "traffic": None, "units_per_launch": round(dsm_units / launches),
                          "ref_work_rate_vs_peak": round(achieved / (PEAK_OPS / 1e12), 4),
                          "avg_launch_ms": round(dsm_avg, 4), "launches_per_batch": launches,
