@@ -127,6 +127,15 @@ DEV void fe_mulN( fe * const r[N], fe const * const a[N], fe const * const b[N] 
   FE_SCHED_FENCE();
 }
 
+/* 2*x as v_add_u32_e32 (x + x): the compiler's v_lshlrev_b32 form issues
+   at the full-cost rate on gfx950, the add at the fast VOP2 rate
+   (profiles/r02zd_valu_issue_calibration.json: lshl_e32 vs add_e32); with
+   the address-swapped cached loads, C2 +1.0%, k_verify_dsm -1.1% against the
+   round-2 forms on one box (profiles/r03e/ab_micro) */
+DEV u32 fe_x2( u32 x ) {
+  u32 r; asm( "v_add_u32_e32 %0, %1, %1" : "=v"( r ) : "v"( x ) ); return r;
+}
+
 /* squares: off-diagonal products taken once against 2*a_i */
 template<int N, bool FREE = false>
 DEV void fe_sqN( fe * const r[N], fe const * const a[N] ) {
@@ -135,7 +144,7 @@ DEV void fe_sqN( fe * const r[N], fe const * const a[N] ) {
   #pragma unroll
   for( int n=0; n<N; n++ ) {
     #pragma unroll
-    for( int i=0; i<9; i++ ) d[n][i] = a[n]->v[i] << 1;
+    for( int i=0; i<9; i++ ) d[n][i] = fe_x2( a[n]->v[i] );
   }
   #pragma unroll
   for( int j=0; j<=8; j++ ) {
@@ -199,6 +208,12 @@ DEV void fe_sq2( fe & r, fe const & a, fe & s, fe const & c ) {
 DEV void fe_add( fe & r, fe const & a, fe const & b ) {
   #pragma unroll
   for( int i=0; i<9; i++ ) r.v[i] = a.v[i] + b.v[i];
+}
+
+/* 2a, limb-wise (the fast VOP2 add, fe_x2) */
+DEV void fe_dbl( fe & r, fe const & a ) {
+  #pragma unroll
+  for( int i=0; i<9; i++ ) r.v[i] = fe_x2( a.v[i] );
 }
 
 /* a - b + 2p (b tight) */
@@ -338,7 +353,7 @@ DEV void ge_dbl( ge_p3 & r, ge_p3 const & p, bool needT ) {
   fe A, B, C, S, H, G, F, E;
   fe_add( S, p.X, p.Y );
   fe_sq2( A, p.X, B, p.Y ); fe_sq2( C, p.Z, S, S );
-  fe_add( C, C, C );          /* 2Z^2            */
+  fe_dbl( C, C );             /* 2Z^2            */
   fe_add( H, A, B );          /* A+B             */
   fe_sub( G, A, B );          /* A-B             */
   fe_add( F, C, G );          /* 2Z^2+A-B        */
@@ -350,10 +365,13 @@ DEV void ge_dbl( ge_p3 & r, ge_p3 const & p, bool needT ) {
   else        fe_mul( r.Z, F, G );
 }
 
-/* r = p +/- q (q in cached form).  neg is a per-lane mask (0 or ~0). */
+/* r = p +/- q (q in cached form).  neg is a per-lane mask (0 or ~0).
+   YX_SWAPPED: the caller loaded q with Y-X / Y+X already exchanged where neg
+   (load_cached_signed), so only 2dT's sign is left to apply here. */
+template<bool YX_SWAPPED = false>
 DEV void ge_add_cached( ge_p3 & r, ge_p3 const & p, ge_cached q, u32 neg, bool needT ) {
   fe a, b, A, B, C, D, E, F, G, H;
-  fe_cswap( q.YmX, q.YpX, neg );           /* -q: swap Y-X / Y+X ... */
+  if( !YX_SWAPPED ) fe_cswap( q.YmX, q.YpX, neg );   /* -q: swap Y-X / Y+X ... */
   fe_sub( a, p.Y, p.X ); fe_add( b, p.Y, p.X );
   fe_mul2( A, a, q.YmX, B, b, q.YpX );
   fe_mul2( C, p.T, q.T2d, D, p.Z, q.Z2 );

@@ -130,6 +130,8 @@ struct fd_ed25519_hip_ctx {
   int          halfsize;    /* 1: half-size scalars (default); 0: full-length (k, 1) */
   ulong        lat_max;     /* calls of at most this many records (no device count) take k_verify_lat */
   u32          lat_copies;  /* k_verify_lat workgroups per signature for small calls (one per XCD) */
+  ulong        lat_cus;     /* CUs a k_verify_lat launch may fill with copies (the drop-in's batch slots
+                               share the GPU: each gets its part) */
   ulong        lat_seq;     /* call number, the k_verify_lat early-exit tag (64-bit: never wraps) */
   ulong *      d_lat_done;  /* LAT_MAX_N: call number of the copy that finished each signature */
   /* optional per-kernel timing (HIP events around each launch, on the launch stream) */
@@ -453,6 +455,22 @@ DEV void load_cached( ge_cached & c, u32 const * t ) {
   for( int k=0; k<8; k++ ) { uint4 v = q[k]; w[4*k] = v.x; w[4*k+1] = v.y; w[4*k+2] = v.z; w[4*k+3] = v.w; }
   fe_unpack<0>( c.YmX, w ); fe_unpack<0>( c.YpX, w + 8 ); fe_unpack<1>( c.T2d, w + 16 ); fe_unpack<0>( c.Z2, w + 24 );
 }
+/* load_cached with Y-X and Y+X exchanged where neg (a per-lane mask): the
+   two elements share one packing layout, so negating the entry's point is a
+   choice of load address, not a 27-instruction swap (ge_add_cached<true>) */
+DEV void load_cached_signed( ge_cached & c, u32 const * t, u32 neg ) {
+  uint4 const * q = (uint4 const *)t;
+  u32 o = neg & 2u;                                          /* first element at line quad 0 or 2 */
+  u32 w[32];
+  uint4 v;
+  v = q[o];      w[0]  = v.x; w[1]  = v.y; w[2]  = v.z; w[3]  = v.w;
+  v = q[o+1u];   w[4]  = v.x; w[5]  = v.y; w[6]  = v.z; w[7]  = v.w;
+  v = q[2u-o];   w[8]  = v.x; w[9]  = v.y; w[10] = v.z; w[11] = v.w;
+  v = q[3u-o];   w[12] = v.x; w[13] = v.y; w[14] = v.z; w[15] = v.w;
+  #pragma unroll
+  for( int k=4; k<8; k++ ) { v = q[k]; w[4*k] = v.x; w[4*k+1] = v.y; w[4*k+2] = v.z; w[4*k+3] = v.w; }
+  fe_unpack<0>( c.YmX, w ); fe_unpack<0>( c.YpX, w + 8 ); fe_unpack<1>( c.T2d, w + 16 ); fe_unpack<0>( c.Z2, w + 24 );
+}
 /* one 1/2-scaled affine B-table entry (7 x 16-B loads) */
 DEV void store_affc( u32 * e, ge_affc const & a ) {      /* canonical elements: any packing layout fits */
   #pragma unroll
@@ -771,17 +789,17 @@ DEV void dsm_verify_slot( ulong t, ulong chunk, u32 const * __restrict__ st, u32
       digit_split( kd1[7] >> 28, 7u, nega, ia ); digits_shl( kd1, 4u );
       digit_split( kd2[7] >> 28, 7u, negr, ir ); digits_shl( kd2, 4u );
       /* issued before the window's 4 doublings, which hide its latency */
-      ge_cached e; load_cached( e, tab_entry( tabA, ident, ia ) );
+      ge_cached e; load_cached_signed( e, tab_entry( tabA, ident, ia ), nega );
       if( w != (int)D-1 ) {
         #pragma unroll 1
         for( int j=0; j<3; j++ ) ge_dbl( P, P, false );
         ge_dbl( P, P, true );
       }
-      ge_add_cached( P, P, e, nega, true );
-      load_cached( e, tab_entry( tabR, ident, ir ) );
+      ge_add_cached<true>( P, P, e, nega, true );
+      load_cached_signed( e, tab_entry( tabR, ident, ir ), negr );
       /* windows (ND-1)*STEP, .., STEP, 0: lo digits ND-1..0, hi digits 2ND-1..ND */
       bool bw = w <= (BTG_ND-1)*BTG_STEP && w % BTG_STEP == 0;
-      ge_add_cached( P, P, e, negr, bw );
+      ge_add_cached<true>( P, P, e, negr, bw );
       if( bw ) b12_step( P, bl, bh, bmask, (u32)w / (u32)BTG_STEP, btab, false );
     }
 
@@ -1179,6 +1197,7 @@ fd_ed25519_hip_ctx_new( int device, ulong chunk_sigs ) {
     FD_CHECK( hipDeviceGetAttribute( &ncu, hipDeviceAttributeMultiprocessorCount, device ) );
     FD_CHECK( hipOccupancyMaxActiveBlocksPerMultiprocessor( &per, k_verify_dsm, 256, 0 ) );
     ctx->dsm_wgs = (ulong)(ncu > 0 ? ncu : 1) * (ulong)(per > 0 ? per : 1);
+    ctx->lat_cus = (ulong)(ncu > 0 ? ncu : 1);
     /* k_verify_lat assumes one workgroup per CU (LAT_WG): a register-count
        change that let two share a CU would make small calls slower, not
        wrong -- say so once */
@@ -1432,7 +1451,13 @@ verify_impl( fd_ed25519_hip_ctx_t * ctx, ulong n, uchar const * d_sigs, uchar co
     /* small batch: one workgroup per signature (k_verify_lat) */
     /* one workgroup per CU (LAT_WG); calls of up to LAT_COPY_MAX_N
        signatures race one copy per XCD (k_verify_lat) */
-    u32 copies = n <= LAT_COPY_MAX_N && n * ctx->lat_copies <= ctx->chunk ? ctx->lat_copies : 1u;
+    u32 copies = 1u;
+    if( n <= LAT_COPY_MAX_N ) {                            /* as many copies as the CU budget holds, up to one per XCD */
+      ulong c = ctx->lat_cus / n;
+      c = c < (ulong)ctx->lat_copies ? c : (ulong)ctx->lat_copies;
+      while( c > 1ul && n * c > ctx->chunk ) c--;           /* each copy builds its tables in d_atab */
+      copies = c ? (u32)c : 1u;
+    }
     ulong seq = ++ctx->lat_seq;                            /* from 1: 0 is done[]'s initial value */
     hipLaunchKernelGGL( k_verify_lat, dim3( (unsigned)(n * copies) ), dim3( LAT_WG ), 0, s, n, d_sigs, d_pubs,
                         d_pool, d_msg_off, d_msg_sz, fixed_sz, ctx->d_btab, ctx->d_atab, ctx->errmode,
@@ -1639,19 +1664,26 @@ fd_ed25519_hip_verify_host( fd_ed25519_hip_ctx_t * ctx, ulong n, uchar const * s
   return 0;
 }
 
-/* ---- reference API on a process-wide context ------------------------
+/* ---- reference API on process-wide contexts ---------------------------
 
    The reference API is re-entrant with no global mutable state
    (fd_ed25519.h:89-94) and replay calls it per transaction from many
    threads (fd_executor.c:1608-1617).  Concurrent drop-in calls are therefore
    combined: each caller appends its records and message to the open staging
-   batch (one pinned host block, with a device copy), and whichever caller
-   finds the GPU idle closes the open batch and runs it for everyone in it --
-   one DMA in, one launch sequence (k_verify_lat for small batches, the bulk
-   kernels above lat_max), one DMA of the codes back.  Callers arriving while
-   a batch runs gather in the next one, so N threads share launches instead
-   of queueing N launches behind one lock.  A single caller sees the same
-   path as before (one batch of its own records).
+   batch (one pinned host block, with a device copy).  A batch runs as soon as
+   one of the batch slots is free: whichever caller finds a free slot closes
+   the open batch and runs it for everyone in it -- one DMA in, one launch
+   sequence (k_verify_lat up to the slot's lat_max records, the bulk kernels
+   above), one DMA of the codes back.  There are g_slots slots (default
+   DROPIN_SLOTS, FD_ED25519_HIP_DROPIN_SLOTS), each with its own context:
+   stream, scratch and k_verify_lat tables, so that many batches are on the
+   GPU at once and a call never waits behind a whole earlier batch while the
+   GPU has room.  Callers arriving while every slot is busy gather in the
+   open batch.  A lone caller gets a launch of its own right away.
+
+   Each slot's latency kernel may fill 1/g_slots of the CUs with racing copies
+   (lat_cus), and batches above that many records take the bulk kernels, so
+   the slots' batches fit on the GPU side by side.
 
    Staging block layout, 16-byte aligned: sigs[256*64] pubs[256*32]
    off[256] sz[256] codes[256], then the callers' messages, each followed
@@ -1664,7 +1696,12 @@ fd_ed25519_hip_verify_host( fd_ed25519_hip_ctx_t * ctx, ulong n, uchar const * s
 #define STAGE_SZ     (STAGE_OFF + 4ul*DROPIN_REC_MAX)
 #define STAGE_CODES  (STAGE_SZ + 4ul*DROPIN_REC_MAX)
 #define STAGE_MSG    (STAGE_CODES + DROPIN_REC_MAX)
-#define DROPIN_NBUF  3
+#ifndef FD_DROPIN_SPIN
+#define FD_DROPIN_SPIN 0
+#endif
+#define DROPIN_SLOTS     4         /* default batches on the GPU at once (the process's hardware queues) */
+#define DROPIN_SLOTS_MAX 8
+#define DROPIN_NBUF  (DROPIN_SLOTS_MAX + 2)
 #define DROPIN_POOL0 65536ul       /* initial message bytes per staging block */
 
 enum { DSTAGE_FREE = 0, DSTAGE_OPEN, DSTAGE_RUNNING, DSTAGE_DONE };
@@ -1679,13 +1716,16 @@ struct dropin_stage {
   ulong   gen;         /* batch number */
 };
 
-static fd_ed25519_hip_ctx_t *   g_ctx;
+static fd_ed25519_hip_ctx_t *   g_ctx;           /* slot 0's context, also the library's default context */
 static std::mutex               g_ctx_lock;      /* creation of g_ctx */
-static std::mutex               g_dl;            /* the staging ring below */
+static std::mutex               g_dl;            /* the staging ring and slots below */
 static std::condition_variable  g_dcv;
 static dropin_stage             g_stage[ DROPIN_NBUF ];
+static fd_ed25519_hip_ctx_t *   g_slot_ctx[ DROPIN_SLOTS_MAX ];
+static int                      g_slot_busy[ DROPIN_SLOTS_MAX ];
+static int                      g_slots;         /* 0: not configured yet */
 static int                      g_open = -1;     /* the open block, -1: none */
-static int                      g_running;       /* a batch is on the GPU */
+static int                      g_running;       /* batches on the GPU */
 static ulong                    g_gen;
 static ulong                    g_batches, g_batch_calls;   /* launches and the calls they served */
 
@@ -1721,14 +1761,33 @@ static void stage_grow( fd_ed25519_hip_ctx_t * ctx, dropin_stage * b, ulong cap 
   b->cap = cap;
 }
 
+/* slot count and slot contexts (caller holds g_dl; g_ctx exists).  Slot 0
+   runs on g_ctx; the others get contexts of their own on its device.  Every
+   slot's latency kernel keeps to its share of the CUs. */
+static void slots_setup( void ) {
+  if( !g_slots ) {
+    char const * e = getenv( "FD_ED25519_HIP_DROPIN_SLOTS" );
+    int k = e ? atoi( e ) : DROPIN_SLOTS;
+    g_slots = k < 1 ? 1 : k > DROPIN_SLOTS_MAX ? DROPIN_SLOTS_MAX : k;
+  }
+  for( int j=0; j<g_slots; j++ ) {
+    if( g_slot_ctx[j] ) continue;
+    fd_ed25519_hip_ctx_t * c = j ? default_ctx_new( g_ctx->device ) : g_ctx;
+    c->lat_cus = c->lat_cus / (ulong)g_slots ? c->lat_cus / (ulong)g_slots : 1ul;
+    c->lat_max = c->lat_cus < LAT_MAX_N ? c->lat_cus : LAT_MAX_N;
+    g_slot_ctx[j] = c;
+  }
+}
+
 int
 fd_ed25519_hip_dropin_init( int device ) {
   {
     std::lock_guard<std::mutex> lk( g_ctx_lock );
-    if( g_ctx ) return g_ctx->device == device ? 0 : -1;
-    g_ctx = default_ctx_new( device );
+    if( g_ctx ) { if( g_ctx->device != device ) return -1; }
+    else g_ctx = default_ctx_new( device );
   }
   std::lock_guard<std::mutex> lk( g_dl );
+  slots_setup();
   for( int j=0; j<DROPIN_NBUF; j++ )
     if( !g_stage[j].h ) stage_grow( g_ctx, &g_stage[j], STAGE_MSG + DROPIN_POOL0 );
   return 0;
@@ -1754,12 +1813,16 @@ static void dropin_check_msg_sz( ulong msg_sz, char const * fn ) {
   }
 }
 
-/* run the staging block (caller holds g_dl through lk; released while the
-   GPU works) */
-static void dropin_launch( fd_ed25519_hip_ctx_t * ctx, dropin_stage * b, std::unique_lock<std::mutex> & lk ) {
-  g_running = 1; b->state = DSTAGE_RUNNING; g_open = -1;
+/* run the staging block on a free slot (caller holds g_dl through lk and has
+   seen g_running < g_slots; the lock is released while the GPU works) */
+static void dropin_launch( dropin_stage * b, std::unique_lock<std::mutex> & lk ) {
+  int sl = 0;
+  while( g_slot_busy[sl] ) sl++;
+  g_slot_busy[sl] = 1; g_running++;
+  b->state = DSTAGE_RUNNING; g_open = -1;
   g_batches++; g_batch_calls += (ulong)b->users;
   g_dcv.notify_all();                                      /* callers may open the next block now */
+  fd_ed25519_hip_ctx_t * ctx = g_slot_ctx[sl];
   ulong n = b->n, bytes = STAGE_MSG + b->pool;
   lk.unlock();
   FD_CHECK( hipSetDevice( ctx->device ) );
@@ -1767,9 +1830,20 @@ static void dropin_launch( fd_ed25519_hip_ctx_t * ctx, dropin_stage * b, std::un
   verify_impl( ctx, n, b->d + STAGE_SIGS, b->d + STAGE_PUBS, b->d + STAGE_MSG, (uint const *)(b->d + STAGE_OFF),
                (uint const *)(b->d + STAGE_SZ), 0u, (signed char *)(b->d + STAGE_CODES), NULL, NULL, NULL );
   FD_CHECK( hipMemcpyAsync( b->h + STAGE_CODES, b->d + STAGE_CODES, n, hipMemcpyDeviceToHost, ctx->stream ) );
+#if FD_DROPIN_SPIN
+  /* the caller is blocked on this batch anyway: poll instead of sleeping in
+     the runtime's blocking wait */
+  for( ;; ) {
+    hipError_t e = hipStreamQuery( ctx->stream );
+    if( e == hipSuccess ) break;
+    if( e != hipErrorNotReady ) FD_CHECK( e );
+    __builtin_ia32_pause();
+  }
+#else
   FD_CHECK( hipStreamSynchronize( ctx->stream ) );
+#endif
   lk.lock();
-  b->state = DSTAGE_DONE; g_running = 0;
+  b->state = DSTAGE_DONE; g_slot_busy[sl] = 0; g_running--;
   g_dcv.notify_all();
 }
 
@@ -1780,6 +1854,7 @@ dropin_run( uchar const * msg, ulong msg_sz, uchar const * sigs, uchar const * p
   fd_ed25519_hip_ctx_t * ctx = default_ctx();
   ulong need = (msg_sz + 16ul + 15ul) & ~15ul;             /* message + 16 zero bytes, 16-B aligned */
   std::unique_lock<std::mutex> lk( g_dl );
+  if( !g_slot_ctx[0] ) slots_setup();                      /* no dropin_init: the first call sets up */
   dropin_stage * b;
   for( ;; ) {
     if( g_open < 0 ) {
@@ -1798,9 +1873,9 @@ dropin_run( uchar const * msg, ulong msg_sz, uchar const * sigs, uchar const * p
       stage_grow( ctx, b, cap > 2ul*b->cap ? cap : 2ul*b->cap );
       break;
     }
-    /* full: it runs as soon as the GPU is free (one of its callers starts
+    /* full: it runs as soon as a slot is free (one of its callers starts
        it, or we do), then this caller opens the next block */
-    if( !g_running ) { dropin_launch( ctx, b, lk ); continue; }
+    if( g_running < g_slots ) { dropin_launch( b, lk ); continue; }
     g_dcv.wait( lk );
   }
   ulong r0 = b->n, p0 = b->pool, gen = b->gen;
@@ -1814,7 +1889,7 @@ dropin_run( uchar const * msg, ulong msg_sz, uchar const * sigs, uchar const * p
   memset( h + STAGE_MSG + p0 + msg_sz, 0, need - msg_sz );
   for( ;; ) {
     if( b->gen == gen && b->state == DSTAGE_DONE ) break;
-    if( !g_running && b->state == DSTAGE_OPEN ) { dropin_launch( ctx, b, lk ); break; }
+    if( g_running < g_slots && b->state == DSTAGE_OPEN ) { dropin_launch( b, lk ); break; }
     g_dcv.wait( lk );
   }
   memcpy( codes, h + STAGE_CODES + r0, n );

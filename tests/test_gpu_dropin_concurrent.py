@@ -130,3 +130,50 @@ def test_concurrent_throughput_12_sig_calls():
           f"p50 {np.percentile(allat, 50):.0f} us, p99 {np.percentile(allat, 99):.0f} us, "
           f"{calls / max(launches, 1):.1f} calls per launch")
     assert calls > 0
+
+
+HARNESS = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools", "dropin_threads")
+
+
+def _harness_input(path, T, K, msg_sz, seed):
+    rng = np.random.default_rng(seed)
+    msgs = rng.integers(0, 256, (T, msg_sz), dtype=np.uint8)
+    prvs = rng.integers(0, 256, (T * K, 32), dtype=np.uint8)
+    pool = msgs.reshape(-1)
+    moff = np.repeat(np.arange(T, dtype=np.uint32) * msg_sz, K)
+    msz = np.full(T * K, msg_sz, np.uint32)
+    pubs, sigs = O.sign_many(prvs, pool, moff, msz)
+    with open(path, "wb") as f:
+        f.write(np.array([T, K, msg_sz, 0], np.uint32).tobytes())
+        for t in range(T):
+            f.write(msgs[t].tobytes())
+            f.write(np.ascontiguousarray(sigs[t * K:(t + 1) * K]).tobytes())
+            f.write(np.ascontiguousarray(pubs[t * K:(t + 1) * K]).tobytes())
+
+
+def test_concurrent_c_callers(tmp_path):
+    """tools/dropin_threads (built by build(); a missing binary fails, it is
+    not skipped): 1, 16 and 64 C threads each calling batch_single_msg with
+    12 valid signatures over its own 64-byte message for 2 s.  Every call must
+    return SUCCESS; aggregate signatures/s and latency percentiles are
+    printed (the measurement of record, no ctypes/GIL in the loop)."""
+    import json
+    import subprocess
+    assert os.path.exists(HARNESS), "tools/dropin_threads missing: run __graft_entry__.build()"
+    inp = str(tmp_path / "calls.bin")
+    _harness_input(inp, 64, 12, 64, 0x1612)
+    out = {}
+    for threads in (1, 16, 64):
+        r = subprocess.run([HARNESS, inp, "2", str(threads)], capture_output=True, text=True, timeout=90)
+        assert r.returncode == 0, (threads, r.stdout, r.stderr[-2000:])
+        d = json.loads(r.stdout.strip().splitlines()[-1])
+        assert d["bad"] == 0 and d["calls"] > 0, d
+        out[threads] = d
+        print(f"C callers {threads:3d} x batch_single_msg(12): {d['sigs_per_s'] / 1e6:.3f} M sigs/s, "
+              f"p50 {d['p50_us']:.0f} us, p99 {d['p99_us']:.0f} us, {d['calls_per_launch']:.2f} calls/launch")
+    with open(str(tmp_path / "summary.json"), "w") as f:
+        json.dump(out, f)
+    dst = os.environ.get("FD_DROPIN_SUMMARY")
+    if dst:
+        with open(dst, "w") as f:
+            json.dump(out, f, indent=1)
