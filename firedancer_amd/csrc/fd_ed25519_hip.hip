@@ -1279,6 +1279,7 @@ void *fd_ed25519_hip_ctx_stream( fd_ed25519_hip_ctx_t const * ctx ) { return (vo
 void  fd_ed25519_hip_set_errmode( fd_ed25519_hip_ctx_t * ctx, int m ) { ctx->errmode = m; }
 void  fd_ed25519_hip_set_halfsize( fd_ed25519_hip_ctx_t * ctx, int on ) { ctx->halfsize = on ? 1 : 0; }
 void  fd_ed25519_hip_set_dsm_share( fd_ed25519_hip_ctx_t * ctx, ulong share ) { ctx->dsm_share = share ? share : 1ul; }
+void  fd_ed25519_hip_set_lat_cus( fd_ed25519_hip_ctx_t * ctx, ulong cus ) { ctx->lat_cus = cus ? cus : 1ul; }
 void  fd_ed25519_hip_set_small_batch( fd_ed25519_hip_ctx_t * ctx, ulong max_n ) {
   ctx->lat_max = max_n < LAT_MAX_N ? max_n : LAT_MAX_N;
 }
@@ -1696,9 +1697,6 @@ fd_ed25519_hip_verify_host( fd_ed25519_hip_ctx_t * ctx, ulong n, uchar const * s
 #define STAGE_SZ     (STAGE_OFF + 4ul*DROPIN_REC_MAX)
 #define STAGE_CODES  (STAGE_SZ + 4ul*DROPIN_REC_MAX)
 #define STAGE_MSG    (STAGE_CODES + DROPIN_REC_MAX)
-#ifndef FD_DROPIN_SPIN
-#define FD_DROPIN_SPIN 0
-#endif
 #define DROPIN_SLOTS     4         /* default batches on the GPU at once (the process's hardware queues) */
 #define DROPIN_SLOTS_MAX 8
 #define DROPIN_NBUF  (DROPIN_SLOTS_MAX + 2)
@@ -1830,18 +1828,7 @@ static void dropin_launch( dropin_stage * b, std::unique_lock<std::mutex> & lk )
   verify_impl( ctx, n, b->d + STAGE_SIGS, b->d + STAGE_PUBS, b->d + STAGE_MSG, (uint const *)(b->d + STAGE_OFF),
                (uint const *)(b->d + STAGE_SZ), 0u, (signed char *)(b->d + STAGE_CODES), NULL, NULL, NULL );
   FD_CHECK( hipMemcpyAsync( b->h + STAGE_CODES, b->d + STAGE_CODES, n, hipMemcpyDeviceToHost, ctx->stream ) );
-#if FD_DROPIN_SPIN
-  /* the caller is blocked on this batch anyway: poll instead of sleeping in
-     the runtime's blocking wait */
-  for( ;; ) {
-    hipError_t e = hipStreamQuery( ctx->stream );
-    if( e == hipSuccess ) break;
-    if( e != hipErrorNotReady ) FD_CHECK( e );
-    __builtin_ia32_pause();
-  }
-#else
   FD_CHECK( hipStreamSynchronize( ctx->stream ) );
-#endif
   lk.lock();
   b->state = DSTAGE_DONE; g_slot_busy[sl] = 0; g_running--;
   g_dcv.notify_all();

@@ -37,6 +37,7 @@ EXPORTS = (
     "fd_ed25519_hip_stage_async", "fd_ed25519_hip_test_prim", "fd_ed25519_hip_set_small_batch",
     "fd_ed25519_hip_dropin_init", "fd_ed25519_hip_dropin_stats", "fd_ed25519_hip_host_register",
     "fd_ed25519_hip_host_unregister", "fd_ed25519_hip_device_cnt", "fd_ed25519_hip_set_dsm_share",
+    "fd_ed25519_hip_set_lat_cus",
 )
 
 _lib = None
@@ -75,6 +76,7 @@ def lib():
         L.fd_ed25519_hip_set_halfsize.argtypes = [vp, c.c_int]
         L.fd_ed25519_hip_set_small_batch.argtypes = [vp, u64]
         L.fd_ed25519_hip_set_dsm_share.argtypes = [vp, u64]
+        L.fd_ed25519_hip_set_lat_cus.argtypes = [vp, u64]
         L.fd_ed25519_hip_test_halfsize.argtypes = [vp, c.c_ulong, vp, vp, vp]
         L.fd_ed25519_hip_test_sha512.argtypes = [vp, c.c_ulong, vp, vp, vp, vp, vp]
         L.fd_ed25519_hip_test_prim.restype = c.c_int
@@ -334,6 +336,10 @@ class Verifier:
     def set_small_batch(self, max_n):
         """Calls of at most max_n records take the latency kernel (0: never)."""
         self._lib.fd_ed25519_hip_set_small_batch(self.ctx, int(max_n))
+
+    def set_lat_cus(self, cus):
+        """CUs a latency-path call may fill with racing copies (1: one copy)."""
+        self._lib.fd_ed25519_hip_set_lat_cus(self.ctx, int(cus))
 
     def test_halfsize(self, n, d_k, d_out, stream=None):
         """Test hook: device half-size reduction (see fd_ed25519_hip_test_halfsize)."""

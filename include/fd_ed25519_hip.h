@@ -153,6 +153,11 @@ void                   fd_ed25519_hip_set_halfsize( fd_ed25519_hip_ctx_t * ctx, 
    with throughput work on other streams should lower the limit or set 0. */
 void                   fd_ed25519_hip_set_small_batch( fd_ed25519_hip_ctx_t * ctx, ulong max_n );
 
+/* CUs a latency-path call may fill with racing copies (default: every CU;
+   the drop-in's batch slots each get 1/slots): calls of up to 32 records run
+   min(cus / n, one per XCD) copies of each signature, at least one. */
+void                   fd_ed25519_hip_set_lat_cus( fd_ed25519_hip_ctx_t * ctx, ulong cus );
+
 /* k_verify_dsm runs a persistent grid sized to every resident workgroup
    slot of the GPU.  share > 1 sizes it to 1/share of them, so that that
    many contexts' DSM launches (verify tiles on other streams) run side by
