@@ -26,7 +26,7 @@
      k_group_reduce batch_single_msg / per-txn semantics over sig codes
 
    Small calls (count on the host, <= ctx->lat_max records, default 32) take
-   k_verify_lat instead: one 768-thread workgroup per signature (and per
+   k_verify_lat instead: one 256-thread workgroup per signature (and per
    racing copy), three working waves that decode A / decode R / hash, then run
    the [k1]A, [k2]R and B chains with each chain's group law on four lanes,
    joined in LDS.
@@ -130,8 +130,8 @@ struct fd_ed25519_hip_ctx {
   int          halfsize;    /* 1: half-size scalars (default); 0: full-length (k, 1) */
   ulong        lat_max;     /* calls of at most this many records (no device count) take k_verify_lat */
   u32          lat_copies;  /* k_verify_lat workgroups per signature for small calls (one per XCD) */
-  ulong        lat_cus;     /* CUs a k_verify_lat launch may fill with copies (the drop-in's batch slots
-                               share the GPU: each gets its part) */
+  ulong        lat_cus;     /* k_verify_lat workgroup slots a launch may fill with copies (CUs x 4; the
+                               drop-in's batch slots share the GPU: each gets its part) */
   ulong        lat_seq;     /* call number, the k_verify_lat early-exit tag (64-bit: never wraps) */
   ulong *      d_lat_done;  /* LAT_MAX_N: call number of the copy that finished each signature */
   /* optional per-kernel timing (HIP events around each launch, on the launch stream) */
@@ -855,11 +855,17 @@ void k_verify_dsm( ulong chunk, u32 const * __restrict__ st, u32 const * __restr
                                 lane-parallel chains: this path 334-493 us vs 770-781 us at 1-32
                                 records; the bulk kernels win from 64 up, 686 vs 721 us,
                                 profiles/r02zd_latency_lp) */
-#define LAT_COPY_MAX_N 32ul  /* calls of up to 32 signatures run one copy per XCD (k_verify_lat) */
-/* 12 waves = 3 per SIMD, all a CU holds at k_verify_lat's register count:
-   one workgroup per CU, so a call's signatures never share a SIMD.  Waves
-   3..11 leave at once; the three working waves land on three SIMDs. */
-#define LAT_WG 768
+/* Four waves: three working, one that only waits through the barriers.  At
+   k_verify_lat's 120 VGPRs a CU holds four such workgroups.  A lone working
+   wave is latency-bound, so workgroups sharing a CU barely slow each other
+   (192 signatures x 4 copies on 768 workgroups: 771 us vs 698 us for one copy,
+   profiles/r03l); and the copies are what matter: a lone workgroup runs
+   ~270 us on some CU slots and ~600 us on the others (profiles/r03k).  Against
+   768-thread workgroups (one per CU): 16 C callers x 12 signatures through the
+   drop-in 0.32-0.33 vs 0.23 M signatures/s, lone calls the same
+   (profiles/r03n). */
+#define LAT_WG 256
+#define LAT_WG_PER_CU 4
 
 struct lat_shared {
   u32 ax[8], ay[8], rx[8], ry[8];   /* canonical decoded coordinates */
@@ -946,8 +952,7 @@ void k_verify_lat( ulong n, uchar const * __restrict__ sigs, uchar const * __res
   __shared__ lat_shared L;
   ulong i = blockIdx.x / copies;
   if( i >= n ) return;                                     /* workgroup-uniform */
-  /* waves 3..11 only hold the CU (LAT_WG): they do no work but stay through
-     both barriers */
+  /* wave 3 does no work but stays through both barriers */
   u32 wave = threadIdx.x >> 6, lane = threadIdx.x & 63u;
   u32 * tabA = atab + (ulong)blockIdx.x * ATAB_WORDS, * tabR = tabA + RTAB_OFF;   /* per copy */
   u32 const * ident = btab + IDENT_OFF;
@@ -1197,16 +1202,17 @@ fd_ed25519_hip_ctx_new( int device, ulong chunk_sigs ) {
     FD_CHECK( hipDeviceGetAttribute( &ncu, hipDeviceAttributeMultiprocessorCount, device ) );
     FD_CHECK( hipOccupancyMaxActiveBlocksPerMultiprocessor( &per, k_verify_dsm, 256, 0 ) );
     ctx->dsm_wgs = (ulong)(ncu > 0 ? ncu : 1) * (ulong)(per > 0 ? per : 1);
-    ctx->lat_cus = (ulong)(ncu > 0 ? ncu : 1);
-    /* k_verify_lat assumes one workgroup per CU (LAT_WG): a register-count
-       change that let two share a CU would make small calls slower, not
-       wrong -- say so once */
+    ctx->lat_cus = (ulong)(ncu > 0 ? ncu : 1);                /* x k_verify_lat workgroups per CU, below */
+    /* the copy budget counts k_verify_lat workgroup slots: a register-count
+       change that moved the per-CU fit would change the budget, not the
+       results -- say so once */
     static int lat_warned;
     per = 0;
     FD_CHECK( hipOccupancyMaxActiveBlocksPerMultiprocessor( &per, k_verify_lat, LAT_WG, 0 ) );
-    if( per != 1 && !lat_warned ) {
+    ctx->lat_cus *= (ulong)(per > 0 ? per : 1);
+    if( per != LAT_WG_PER_CU && !lat_warned ) {
       lat_warned = 1;
-      fprintf( stderr, "fd_ed25519_hip: k_verify_lat fits %d workgroups per CU (expected 1)\n", per );
+      fprintf( stderr, "fd_ed25519_hip: k_verify_lat fits %d workgroups per CU (expected %d)\n", per, LAT_WG_PER_CU );
     }
   }
   hipLaunchKernelGGL( k_btab_init, dim3( (2*BTAB_N + 63)/64 ), dim3( 64 ), 0, ctx->stream, ctx->d_btab );
@@ -1449,11 +1455,11 @@ verify_impl( fd_ed25519_hip_ctx_t * ctx, ulong n, uchar const * d_sigs, uchar co
   if( !n ) return 0;
   if( ctx->ev_used ) FD_CHECK( hipStreamWaitEvent( s, ctx->ev_last, 0 ) );   /* previous call's scratch use */
   if( !d_n && n <= ctx->lat_max && n <= ctx->chunk && !ctx->timing ) {
-    /* small batch: one workgroup per signature (k_verify_lat) */
-    /* one workgroup per CU (LAT_WG); calls of up to LAT_COPY_MAX_N
-       signatures race one copy per XCD (k_verify_lat) */
+    /* small batch: one workgroup per signature (k_verify_lat), racing as
+       many copies as the context's workgroup-slot budget holds, up to one
+       per XCD */
     u32 copies = 1u;
-    if( n <= LAT_COPY_MAX_N ) {                            /* as many copies as the CU budget holds, up to one per XCD */
+    {
       ulong c = ctx->lat_cus / n;
       c = c < (ulong)ctx->lat_copies ? c : (ulong)ctx->lat_copies;
       while( c > 1ul && n * c > ctx->chunk ) c--;           /* each copy builds its tables in d_atab */
@@ -1682,9 +1688,11 @@ fd_ed25519_hip_verify_host( fd_ed25519_hip_ctx_t * ctx, ulong n, uchar const * s
    GPU has room.  Callers arriving while every slot is busy gather in the
    open batch.  A lone caller gets a launch of its own right away.
 
-   Each slot's latency kernel may fill 1/g_slots of the CUs with racing copies
-   (lat_cus), and batches above that many records take the bulk kernels, so
-   the slots' batches fit on the GPU side by side.
+   Each slot's latency kernel may fill 1/g_slots of the k_verify_lat
+   workgroup slots with racing copies (lat_cus), so the slots' batches fit on
+   the GPU side by side.  More slots than the process's 4 hardware queues only
+   queue launches behind each other (16 C callers x 12 signatures: 0.32 M/s
+   at 4 slots, 0.18 M/s at 8, 0.09 M/s at 16, profiles/r03m).
 
    Staging block layout, 16-byte aligned: sigs[256*64] pubs[256*32]
    off[256] sz[256] codes[256], then the callers' messages, each followed
@@ -1698,7 +1706,7 @@ fd_ed25519_hip_verify_host( fd_ed25519_hip_ctx_t * ctx, ulong n, uchar const * s
 #define STAGE_CODES  (STAGE_SZ + 4ul*DROPIN_REC_MAX)
 #define STAGE_MSG    (STAGE_CODES + DROPIN_REC_MAX)
 #define DROPIN_SLOTS     4         /* default batches on the GPU at once (the process's hardware queues) */
-#define DROPIN_SLOTS_MAX 8
+#define DROPIN_SLOTS_MAX 16
 #define DROPIN_NBUF  (DROPIN_SLOTS_MAX + 2)
 #define DROPIN_POOL0 65536ul       /* initial message bytes per staging block */
 
@@ -1771,7 +1779,9 @@ static void slots_setup( void ) {
   for( int j=0; j<g_slots; j++ ) {
     if( g_slot_ctx[j] ) continue;
     fd_ed25519_hip_ctx_t * c = j ? default_ctx_new( g_ctx->device ) : g_ctx;
-    c->lat_cus = c->lat_cus / (ulong)g_slots ? c->lat_cus / (ulong)g_slots : 1ul;
+    char const * lc = getenv( "FD_ED25519_HIP_DROPIN_LAT_CUS" );   /* A/B override of the share */
+    c->lat_cus = lc ? (ulong)atol( lc ) : c->lat_cus / (ulong)g_slots;
+    if( !c->lat_cus ) c->lat_cus = 1ul;
     c->lat_max = c->lat_cus < LAT_MAX_N ? c->lat_cus : LAT_MAX_N;
     g_slot_ctx[j] = c;
   }

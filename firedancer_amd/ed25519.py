@@ -338,7 +338,7 @@ class Verifier:
         self._lib.fd_ed25519_hip_set_small_batch(self.ctx, int(max_n))
 
     def set_lat_cus(self, cus):
-        """CUs a latency-path call may fill with racing copies (1: one copy)."""
+        """k_verify_lat workgroup slots a latency-path call may fill with racing copies (1: one copy)."""
         self._lib.fd_ed25519_hip_set_lat_cus(self.ctx, int(cus))
 
     def test_halfsize(self, n, d_k, d_out, stream=None):

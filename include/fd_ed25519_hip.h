@@ -144,18 +144,21 @@ void                   fd_ed25519_hip_set_halfsize( fd_ed25519_hip_ctx_t * ctx, 
 /* Calls of at most max_n records (default 32, at most 256) whose count is
    known on the host run on the latency path: one workgroup of three waves per
    signature (the A and R decodes, the hash, and the [k1]A, [k2]R and B terms
-   run side by side; calls of up to 32 records race one copy per XCD),
-   instead of one lane per signature through k_verify_prep / k_verify_dsm.
-   Same verdicts and codes; 0 sends every call to the bulk kernels.  The
-   drop-in entry points use the context default.  Each of a latency call's
-   n x copies workgroups holds a whole CU until it ends (a 32-record call:
-   all 256 CUs for ~0.5 ms), so a context whose small calls share the GPU
-   with throughput work on other streams should lower the limit or set 0. */
+   run side by side; each signature races copies on other XCDs as far as the
+   context's budget, fd_ed25519_hip_set_lat_cus, allows), instead of one lane
+   per signature through k_verify_prep / k_verify_dsm.  Same verdicts and
+   codes; 0 sends every call to the bulk kernels.  The drop-in entry points
+   run on their own batch-slot contexts.  A latency call's n x copies
+   workgroups each hold a quarter of a CU until they end (a 32-record call
+   with 8 copies: 256 workgroups for ~0.5 ms), so a context whose small calls
+   share the GPU with throughput work on other streams should lower the
+   limit or set 0. */
 void                   fd_ed25519_hip_set_small_batch( fd_ed25519_hip_ctx_t * ctx, ulong max_n );
 
-/* CUs a latency-path call may fill with racing copies (default: every CU;
-   the drop-in's batch slots each get 1/slots): calls of up to 32 records run
-   min(cus / n, one per XCD) copies of each signature, at least one. */
+/* k_verify_lat workgroup slots a latency-path call may fill with racing
+   copies (default: all of them, 4 per CU; the drop-in's batch slots each get
+   1/slots): a call of n records runs min(slots / n, one per XCD) copies of
+   each signature, at least one. */
 void                   fd_ed25519_hip_set_lat_cus( fd_ed25519_hip_ctx_t * ctx, ulong cus );
 
 /* k_verify_dsm runs a persistent grid sized to every resident workgroup

@@ -14,16 +14,18 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 def main():
     reps = int(sys.argv[1]) if len(sys.argv) > 1 else 60
+    ns = [int(x) for x in sys.argv[2].split(",")] if len(sys.argv) > 2 else [1, 12]
+    cps = [int(x) for x in sys.argv[3].split(",")] if len(sys.argv) > 3 else [1, 2, 4, 8]
     import torch
     from firedancer_amd import Verifier
     from firedancer_amd.workload import make_batch_gpu
     v = Verifier(device=0, chunk_sigs=4096)
     v.set_small_batch(256)
     out = {}
-    for n in (1, 12):
+    for n in ns:
         b = make_batch_gpu(v, n, msg_sz=64, seed=11, mix="c1")
         codes = torch.empty(n, dtype=torch.int8, device="cuda")
-        for cus in (1, 2 * n, 4 * n, 8 * n):
+        for cus in [max(c * n, 1) for c in cps]:
             v.set_lat_cus(cus)
             ts = []
             for r in range(reps + 3):
