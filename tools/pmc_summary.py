@@ -43,5 +43,9 @@ for k in ("k_verify_prep", "k_verify_dsm"):
         der["hbm_side_bytes_per_launch"] = der["fetch_bytes_x2_corrected"] + der["write_bytes"]
     m["derived"] = der
     res["kernels"][k] = m
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from firedancer_amd.kernel_hash import kernel_hashes  # noqa: E402  (the machine code these counters describe)
+res["kernel_sha"] = kernel_hashes(os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                               "firedancer_amd", "libfd_ed25519_hip.so"))
 json.dump(res, open(out, "w"), indent=1)
 print(json.dumps({k: v["derived"] for k, v in res["kernels"].items()}, indent=1))

@@ -80,6 +80,11 @@ def main():
     single = [v["slot_util"] for v in res["microbench_8_waves_per_simd"].values() if v["dual_issue_share"] < 0.01
               and v["ipc_per_simd"] > 0.1]
     res["single_issue_ceiling_slot_util"] = round(max(single), 4) if single else None
+    # which machine code these counters describe (bench.py checks it against the loaded library)
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    from firedancer_amd.kernel_hash import kernel_hashes
+    res["kernel_sha"] = kernel_hashes(os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                                   "firedancer_amd", "libfd_ed25519_hip.so"))
     json.dump(res, open(out, "w"), indent=1)
     print(json.dumps(res["engine"], indent=1))
     print("single-issue microbench ceiling:", res["single_issue_ceiling_slot_util"])
