@@ -262,6 +262,14 @@ def main():
                     help="nccl (RCCL over xGMI, one rank per GPU: the driver's N-GPU runs); gloo rehearses the "
                          "N>1 path with several ranks sharing one GPU (rank r on GPU r %% device_count)")
     args = ap.parse_args()
+    if args.config == "c4":
+        # The reference runs each verify tile as its own process, each with the
+        # HIP runtime's own hardware queues; here the tiles are threads of one
+        # process, so give that process a queue per tile (HIP default 4).
+        # Resident C4 is unchanged, the PCIe-inclusive leg +6% (profiles/r03u:
+        # 113.8/113.6 vs 113.8/114.5 M resident, 100.6/100.9 vs 106.4/106.5 M).
+        # Set before the runtime initialises (the torch import below).
+        os.environ.setdefault("GPU_MAX_HW_QUEUES", str(max(4, min(args.tiles + 2, 8))))
 
     import torch
     rank = int(os.environ.get("RANK", "0"))
