@@ -177,3 +177,43 @@ def test_concurrent_c_callers(tmp_path):
     if dst:
         with open(dst, "w") as f:
             json.dump(out, f, indent=1)
+
+
+def test_concurrent_mixed_sizes_and_long_messages():
+    """12 threads mixing single verifies and batch_single_msg calls of 1..16
+    signatures over messages of 0 B .. 200 KB (past a staging block's initial
+    64-KB message area, so blocks grow while other batch slots run), with
+    corrupted signatures mixed in: every code equals the oracle's."""
+    from firedancer_amd import fd_ed25519_verify, fd_ed25519_verify_batch_single_msg
+    rng = np.random.default_rng(0x5107)
+    T, CALLS = 12, 12
+    jobs = []
+    for t in range(T):
+        for c in range(CALLS):
+            sz = int(rng.choice([0, 1, 63, 200, 1232, 5000, 70000, 200000]))
+            k = int(rng.integers(1, 17))
+            msg = rng.integers(0, 256, sz, dtype=np.uint8)
+            prvs = rng.integers(0, 256, (k, 32), dtype=np.uint8)
+            pubs, sigs = O.sign_many(prvs, msg, np.zeros(k, np.uint32), np.full(k, sz, np.uint32))
+            sigs = sigs.copy()
+            if rng.random() < 0.3:                          # corrupt one signature's R or S
+                j = int(rng.integers(0, k)); sigs[j, int(rng.integers(0, 64))] ^= 0x40
+            jobs.append((t, msg.tobytes(), sigs, pubs, k))
+    got = {}
+
+    def worker(t):
+        for ji, (tt, m, s, p, k) in enumerate(jobs):
+            if tt != t:
+                continue
+            if k == 1 and ji % 2 == 0:
+                got[ji] = fd_ed25519_verify(m, s[0].tobytes(), p[0].tobytes())
+            else:
+                got[ji] = fd_ed25519_verify_batch_single_msg(m, s.tobytes(), p.tobytes(), k)
+
+    _run_threads(T, worker)
+    for ji, (t, m, s, p, k) in enumerate(jobs):
+        if k == 1 and ji % 2 == 0:
+            exp = O.verify(m, s[0].tobytes(), p[0].tobytes())
+        else:
+            exp = O.verify_batch_single_msg(m, s.tobytes(), p.tobytes(), k)
+        assert got[ji] == exp, (ji, len(m), k, got[ji], exp)
