@@ -1723,12 +1723,13 @@ struct dropin_stage {
   int     users;       /* callers attached (read their codes before the block is reused) */
   int     state;
   ulong   gen;         /* batch number */
+  std::condition_variable cv;   /* its callers wait here: the batch is done, or a slot is free to run it */
 };
 
 static fd_ed25519_hip_ctx_t *   g_ctx;           /* slot 0's context, also the library's default context */
 static std::mutex               g_ctx_lock;      /* creation of g_ctx */
 static std::mutex               g_dl;            /* the staging ring and slots below */
-static std::condition_variable  g_dcv;
+static std::condition_variable  g_dcv;           /* a block freed or closed, or a slot freed (callers without a block) */
 static dropin_stage             g_stage[ DROPIN_NBUF ];
 static fd_ed25519_hip_ctx_t *   g_slot_ctx[ DROPIN_SLOTS_MAX ];
 static int                      g_slot_busy[ DROPIN_SLOTS_MAX ];
@@ -1844,7 +1845,9 @@ static void dropin_launch( dropin_stage * b, std::unique_lock<std::mutex> & lk )
   FD_CHECK( hipStreamSynchronize( ctx->stream ) );
   lk.lock();
   b->state = DSTAGE_DONE; g_slot_busy[sl] = 0; g_running--;
-  g_dcv.notify_all();
+  b->cv.notify_all();                                      /* this batch's callers */
+  if( g_open >= 0 ) g_stage[g_open].cv.notify_one();       /* one caller of the open batch runs it on the freed slot */
+  g_dcv.notify_all();                                      /* callers waiting to close a full batch */
 }
 
 /* verify n (sig, pub) pairs over one message through the combining staging
@@ -1890,7 +1893,7 @@ dropin_run( uchar const * msg, ulong msg_sz, uchar const * sigs, uchar const * p
   for( ;; ) {
     if( b->gen == gen && b->state == DSTAGE_DONE ) break;
     if( g_running < g_slots && b->state == DSTAGE_OPEN ) { dropin_launch( b, lk ); break; }
-    g_dcv.wait( lk );
+    b->cv.wait( lk );
   }
   memcpy( codes, h + STAGE_CODES + r0, n );
   if( !--b->users ) { b->state = DSTAGE_FREE; g_dcv.notify_all(); }

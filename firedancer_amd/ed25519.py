@@ -53,6 +53,15 @@ def lib():
             path = v if os.sep in v else variant_path(v)
         if not os.path.exists(path):
             raise RuntimeError(f"{path} missing: run __graft_entry__.build() (no CPU fallback exists)")
+        # torch (device memory, streams) ships its own libamdhip64.so.7 with the
+        # same soname as the system runtime this library links: whichever loads
+        # first serves the whole process.  Load torch's first, always, so the
+        # engine and torch share one runtime in every process and test order
+        # (loaded the other way round, torch's CUDA init could fail afterwards).
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
         L = ctypes.CDLL(path)
         c = ctypes
         vp, u64 = c.c_void_p, c.c_ulong
