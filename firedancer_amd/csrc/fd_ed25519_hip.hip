@@ -1289,6 +1289,22 @@ void  fd_ed25519_hip_set_errmode( fd_ed25519_hip_ctx_t * ctx, int m ) { ctx->err
 void  fd_ed25519_hip_set_halfsize( fd_ed25519_hip_ctx_t * ctx, int on ) { ctx->halfsize = on ? 1 : 0; }
 void  fd_ed25519_hip_set_dsm_share( fd_ed25519_hip_ctx_t * ctx, ulong share ) { ctx->dsm_share = share ? share : 1ul; }
 void  fd_ed25519_hip_set_lat_cus( fd_ed25519_hip_ctx_t * ctx, ulong cus ) { ctx->lat_cus = cus ? cus : 1ul; }
+
+int
+fd_ed25519_hip_ctx_set_cu_mask( fd_ed25519_hip_ctx_t * ctx, uint const * mask, uint words ) {
+  /* the context's stream, recreated on the CUs the mask names (bit i of
+     word w = the runtime's CU 32w+i): work queued on it before is drained */
+  FD_CHECK( hipSetDevice( ctx->device ) );
+  FD_CHECK( hipStreamSynchronize( ctx->stream ) );
+  if( ctx->ev_used ) FD_CHECK( hipEventSynchronize( ctx->ev_last ) );
+  hipStream_t s = 0;
+  hipError_t e = words ? hipExtStreamCreateWithCUMask( &s, words, mask )
+                       : hipStreamCreateWithFlags( &s, hipStreamNonBlocking );
+  if( e != hipSuccess ) return -1;
+  FD_CHECK( hipStreamDestroy( ctx->stream ) );
+  ctx->stream = s;
+  return 0;
+}
 void  fd_ed25519_hip_set_small_batch( fd_ed25519_hip_ctx_t * ctx, ulong max_n ) {
   ctx->lat_max = max_n < LAT_MAX_N ? max_n : LAT_MAX_N;
 }

@@ -37,7 +37,7 @@ EXPORTS = (
     "fd_ed25519_hip_stage_async", "fd_ed25519_hip_test_prim", "fd_ed25519_hip_set_small_batch",
     "fd_ed25519_hip_dropin_init", "fd_ed25519_hip_dropin_stats", "fd_ed25519_hip_host_register",
     "fd_ed25519_hip_host_unregister", "fd_ed25519_hip_device_cnt", "fd_ed25519_hip_set_dsm_share",
-    "fd_ed25519_hip_set_lat_cus",
+    "fd_ed25519_hip_set_lat_cus", "fd_ed25519_hip_ctx_set_cu_mask",
 )
 
 _lib = None
@@ -86,6 +86,8 @@ def lib():
         L.fd_ed25519_hip_set_small_batch.argtypes = [vp, u64]
         L.fd_ed25519_hip_set_dsm_share.argtypes = [vp, u64]
         L.fd_ed25519_hip_set_lat_cus.argtypes = [vp, u64]
+        L.fd_ed25519_hip_ctx_set_cu_mask.restype = c.c_int
+        L.fd_ed25519_hip_ctx_set_cu_mask.argtypes = [vp, vp, c.c_uint]
         L.fd_ed25519_hip_test_halfsize.argtypes = [vp, c.c_ulong, vp, vp, vp]
         L.fd_ed25519_hip_test_sha512.argtypes = [vp, c.c_ulong, vp, vp, vp, vp, vp]
         L.fd_ed25519_hip_test_prim.restype = c.c_int
@@ -345,6 +347,17 @@ class Verifier:
     def set_small_batch(self, max_n):
         """Calls of at most max_n records take the latency kernel (0: never)."""
         self._lib.fd_ed25519_hip_set_small_batch(self.ctx, int(max_n))
+
+    def set_cu_mask(self, cus=None):
+        """Run the context's stream on the listed CU indices only (None: all)."""
+        if not cus:
+            return self._lib.fd_ed25519_hip_ctx_set_cu_mask(self.ctx, None, 0)
+        words = (max(cus) // 32) + 1
+        m = np.zeros(words, np.uint32)
+        for c_ in cus:
+            m[c_ // 32] |= np.uint32(1 << (c_ % 32))
+        self._m = m
+        return self._lib.fd_ed25519_hip_ctx_set_cu_mask(self.ctx, m.ctypes.data, words)
 
     def set_lat_cus(self, cus):
         """k_verify_lat workgroup slots a latency-path call may fill with racing copies (1: one copy)."""

@@ -161,6 +161,12 @@ void                   fd_ed25519_hip_set_small_batch( fd_ed25519_hip_ctx_t * ct
    each signature, at least one. */
 void                   fd_ed25519_hip_set_lat_cus( fd_ed25519_hip_ctx_t * ctx, ulong cus );
 
+/* Recreates the context's stream restricted to the CUs whose bits are set in
+   mask[0..words) (hipExtStreamCreateWithCUMask numbering; words 0: all CUs
+   again).  Work already queued on the old stream is drained first.  Returns
+   0, or -1 if the runtime refused the mask. */
+int                    fd_ed25519_hip_ctx_set_cu_mask( fd_ed25519_hip_ctx_t * ctx, uint const * mask, uint words );
+
 /* k_verify_dsm runs a persistent grid sized to every resident workgroup
    slot of the GPU.  share > 1 sizes it to 1/share of them, so that that
    many contexts' DSM launches (verify tiles on other streams) run side by

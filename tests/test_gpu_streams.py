@@ -91,3 +91,30 @@ def test_c3_full_size_groups_of_16(verifier):
         g1 = torch.full((1,), 9, dtype=torch.int8, device=dev)
         verifier.group_reduce_dev(1, first[:1], cnt[:1], c16, g1)
         assert int(g1.item()) == exp != 0, (grp, j, bit)
+
+
+def test_cu_masked_context_stream():
+    """fd_ed25519_hip_ctx_set_cu_mask: a context whose stream runs on 8 CUs
+    only (bulk path, 4096 C2 records, and a latency-path call of 12) gives
+    the oracle's codes, and returns to every CU with an empty mask."""
+    from firedancer_amd import Verifier
+    from firedancer_amd.ed25519 import CTX_STREAM
+    v = Verifier(device=0, chunk_sigs=1 << 14)
+    try:
+        assert v.set_cu_mask([0, 1, 40, 77, 128, 129, 200, 255]) == 0
+        n = 4096
+        b = W.make_batch_gpu(v, n, msg_sz=80, seed=0xc0, mix="c2")
+        codes = torch.empty(n, dtype=torch.int8, device="cuda")
+        torch.cuda.synchronize()
+        v.verify_dev(n, b.sigs, b.pubs, b.pool, b.msg_off, b.msg_sz, codes, stream=CTX_STREAM)
+        v.verify_dev(12, b.sigs, b.pubs, b.pool, b.msg_off, b.msg_sz, codes[:12], stream=CTX_STREAM)   # latency path
+        v.sync()
+        exp = O.verify_many(b.sigs.cpu().numpy(), b.pubs.cpu().numpy(), b.pool.cpu().numpy(),
+                            b.msg_off.cpu().numpy().view(np.uint32), b.msg_sz.cpu().numpy().view(np.uint32))
+        assert np.array_equal(codes.cpu().numpy(), exp)
+        assert v.set_cu_mask(None) == 0
+        v.verify_dev(n, b.sigs, b.pubs, b.pool, b.msg_off, b.msg_sz, codes, stream=CTX_STREAM)
+        v.sync()
+        assert np.array_equal(codes.cpu().numpy(), exp)
+    finally:
+        v.close()
