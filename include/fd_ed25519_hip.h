@@ -36,11 +36,12 @@ typedef unsigned int  uint;
    reject, are those of the reference's AVX-512 build (fd_ed25519_user.c with
    avx512/fd_r43x6_ge.c decode); fd_ed25519_hip_set_errmode() switches the
    error codes to the portable build's (the accept/reject bit is the same).
-   Each call is synchronous on a process-wide context (device
+   Each call is synchronous on process-wide contexts (device
    FD_ED25519_HIP_DEVICE, default 0, or fd_ed25519_hip_dropin_init's) and
    re-entrant: concurrent calls from different threads are combined into
-   one staged batch and one launch sequence (the caller that finds the GPU
-   idle runs the batch for all in it).  msg_sz above about 2^32-27K aborts
+   staged batches, and up to 4 batches run at once, each on its own context
+   and stream (FD_ED25519_HIP_DROPIN_SLOTS, 1..16; a caller that finds a slot
+   free runs the open batch for all in it).  msg_sz above about 2^32-27K aborts
    the process (the engine's message offsets are 32-bit; hashing a prefix
    would silently diverge).
 
@@ -75,8 +76,9 @@ fd_ed25519_verify_batch_single_msg( uchar const                msg[], /* msg_sz 
 char const *
 fd_ed25519_strerror( int err );
 
-/* Create the drop-in's process-wide context on `device` now (and its
-   pinned staging), instead of lazily at the first verify.  Returns 0, or -1
+/* Create the drop-in's process-wide contexts (one per batch slot) on
+   `device` now, with their pinned staging, instead of lazily at the first
+   verify.  Returns 0, or -1
    if the context already exists on another device.  Call it once from a
    tile's privileged_init (the HIP context must exist before
    the sandbox). */
