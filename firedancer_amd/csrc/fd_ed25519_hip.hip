@@ -129,7 +129,8 @@ struct fd_ed25519_hip_ctx {
   int          errmode;
   int          halfsize;    /* 1: half-size scalars (default); 0: full-length (k, 1) */
   ulong        lat_max;     /* calls of at most this many records (no device count) take k_verify_lat */
-  u32          lat_copies;  /* k_verify_lat workgroups per signature for small calls (one per XCD) */
+  u32          lat_copies;  /* k_verify_lat racing copies per signature at most (LAT_COPIES_MAX) */
+  ulong        ncu;         /* CUs: a call's copies stop at one workgroup per CU */
   ulong        lat_cus;     /* k_verify_lat workgroup slots a launch may fill with copies (CUs x 4; the
                                drop-in's batch slots share the GPU: each gets its part) */
   ulong        lat_seq;     /* call number, the k_verify_lat early-exit tag (64-bit: never wraps) */
@@ -869,6 +870,7 @@ void k_verify_dsm( ulong chunk, u32 const * __restrict__ st, u32 const * __restr
    (profiles/r03n). */
 #define LAT_WG 256
 #define LAT_WG_PER_CU 4
+#define LAT_COPIES_MAX 16u   /* racing copies of a signature (a lone call's 8..16: p50 323 vs 437 us at 12 signatures) */
 
 struct lat_shared {
   u32 ax[8], ay[8], rx[8], ry[8];   /* canonical decoded coordinates */
@@ -934,8 +936,6 @@ DEV void lat_chain( ge_p3 & P, u32 const * tab, u32 const * ident, u32 kd[8], u3
 /* the XCD (XCC) this workgroup runs on: hwreg(HW_REG_XCC_ID, 0, 4) */
 DEV u32 xcc_id( void ) { return (u32)__builtin_amdgcn_s_getreg( (3 << 11) | (0 << 6) | 20 ); }
 
-/* the dispatcher deals a launch's consecutive workgroups to the XCDs in turn */
-__global__ void k_xcc_probe( u32 * out ) { if( threadIdx.x == 0u ) out[blockIdx.x] = xcc_id(); }
 
 /* copies > 1: each signature gets that many consecutive workgroups, which the
    dispatcher deals to different XCDs, all computing the same verdict; the
@@ -1223,21 +1223,17 @@ fd_ed25519_hip_ctx_new( int device, ulong chunk_sigs ) {
   hipLaunchKernelGGL( k_btab12_init, dim3( (2*BT12_N + 63)/64 ), dim3( 64 ), 0, ctx->stream, ctx->d_btab );
   FD_CHECK( hipGetLastError() );
   {
-    /* k_verify_lat copies: one per XCD, if the probe sees consecutive
-       workgroups dealt to the XCDs in turn (one partition = one XCD: 1) */
-    enum { NP = 64 };
-    u32 * d_x = 0, h_x[NP];
-    FD_CHECK( hipMalloc( (void **)&d_x, NP*sizeof(u32) ) );
-    hipLaunchKernelGGL( k_xcc_probe, dim3( NP ), dim3( 64 ), 0, ctx->stream, d_x );
-    FD_CHECK( hipGetLastError() );
-    FD_CHECK( hipMemcpyAsync( h_x, d_x, sizeof(h_x), hipMemcpyDeviceToHost, ctx->stream ) );
-    FD_CHECK( hipStreamSynchronize( ctx->stream ) );
-    FD_CHECK( hipFree( d_x ) );
-    u32 nx = 0;
-    for( int j=0; j<NP; j++ ) nx = h_x[j] + 1u > nx ? h_x[j] + 1u : nx;
-    int rr = nx > 1u && nx <= 16u;
-    for( int j=0; rr && j<NP; j++ ) rr = h_x[j] == (h_x[0] + (u32)j) % nx;
-    ctx->lat_copies = rr ? nx : 1u;
+    /* Racing copies pay off per CU, not per XCD: a lone workgroup is fast or
+       slow by the state of the CU it lands on (profiles/r03k, r03x), so up to
+       LAT_COPIES_MAX copies of a signature run (consecutive workgroups go to
+       the XCDs in turn), bounded by one workgroup per CU in verify_impl.
+       Against one copy per XCD (8): a lone 12-signature drop-in call p50
+       323 vs 437 us, 16 concurrent callers unchanged (profiles/r03aa). */
+    int ncu_ = 0;
+    FD_CHECK( hipDeviceGetAttribute( &ncu_, hipDeviceAttributeMultiprocessorCount, device ) );
+    ctx->lat_copies = LAT_COPIES_MAX;
+    { char const * lc = getenv( "FD_ED25519_HIP_LAT_COPIES" ); if( lc && atoi( lc ) > 0 ) ctx->lat_copies = (u32)atoi( lc ); }
+    ctx->ncu = (ulong)(ncu_ > 0 ? ncu_ : 1);
     FD_CHECK( hipMalloc( (void **)&ctx->d_lat_done, LAT_MAX_N * sizeof(ulong) ) );
     FD_CHECK( hipMemsetAsync( ctx->d_lat_done, 0, LAT_MAX_N * sizeof(ulong), ctx->stream ) );
   }
@@ -1481,6 +1477,7 @@ verify_impl( fd_ed25519_hip_ctx_t * ctx, ulong n, uchar const * d_sigs, uchar co
     {
       ulong c = ctx->lat_cus / n;
       c = c < (ulong)ctx->lat_copies ? c : (ulong)ctx->lat_copies;
+      c = c < ctx->ncu / n ? c : ctx->ncu / n;              /* copies beyond one per CU pile up (profiles/r03aa) */
       while( c > 1ul && n * c > ctx->chunk ) c--;           /* each copy builds its tables in d_atab */
       copies = c ? (u32)c : 1u;
     }
