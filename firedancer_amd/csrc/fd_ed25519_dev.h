@@ -1001,8 +1001,11 @@ DEV u32 wave_max_u32( u32 v ) {                 /* max of v over all lanes of th
 }
 
 template<u32 PLEN>   /* prefix bytes: 64 (R||A, the verify path) or 0 (plain SHA-512, the test hook) */
-DEV void sha512_prefixed_coop( u32 x[16], u32 const pre[16], u8 const * msg, u32 msz, u32 * buf, u64 * meta,
-                               u32 lane ) {
+DEV void sha512_prefixed_coop( u32 x[16], u8 const * pre_r, u8 const * pre_a, u8 const * msg, u32 msz, u32 * buf,
+                               u64 * meta, u32 lane ) {
+  /* pre_r / pre_a: the 32-byte R and A (16-B aligned) hashed ahead of M when
+     PLEN = 64, read in block 0 only (not held in registers across blocks);
+     unused (may be null) when PLEN = 0 */
   u64 st[8] = { 0x6a09e667f3bcc908ULL,0xbb67ae8584caa73bULL,0x3c6ef372fe94f82bULL,0xa54ff53a5f1d36f1ULL,
                 0x510e527fade682d1ULL,0x9b05688c2b3e6c1fULL,0x1f83d9abfb41bd6bULL,0x5be0cd19137e2179ULL };
   u32 nb = (PLEN + msz + 17u + 127u) >> 7;
@@ -1067,6 +1070,13 @@ DEV void sha512_prefixed_coop( u32 x[16], u32 const pre[16], u8 const * msg, u32
     for( int k=0; k<32; k++ ) mm[k] = __builtin_amdgcn_alignbit( mw[k+1], mw[k], sh );
     u64 W[16];
     if( PLEN && b == 0u ) {                               /* wave-uniform branch */
+      u32 pre[16];
+      uint4 const * qr = (uint4 const *)pre_r, * qa = (uint4 const *)pre_a;
+      #pragma unroll
+      for( int k=0; k<2; k++ ) {
+        uint4 v = qr[k]; pre[4*k] = v.x; pre[4*k+1] = v.y; pre[4*k+2] = v.z; pre[4*k+3] = v.w;
+        v = qa[k]; pre[8+4*k] = v.x; pre[8+4*k+1] = v.y; pre[8+4*k+2] = v.z; pre[8+4*k+3] = v.w;
+      }
       #pragma unroll
       for( int t=0; t<8; t++ ) W[t] = be64_of_le_words( pre[2*t], pre[2*t+1] );
       #pragma unroll

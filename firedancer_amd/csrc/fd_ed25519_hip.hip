@@ -330,15 +330,13 @@ DEV void prep_slot( ulong t, ulong n, ulong chunk, uchar const * __restrict__ si
      (measured: pairing the two chains instruction by instruction is slower,
      it costs a wave per SIMD of occupancy) */
   {
-    u32 sig[16], pub[8];
-    load_words( sig, sigs + 64*i, 16 );
-    load_words( pub, pubs + 32*i, 8 );
-    flags = sc_is_canonical( sig + 8 ) ? 0u : F_S_BAD;                     /* user.c:159-161 */
+    u32 sv[8];
+    load_words( sv, sigs + 64*i + 32, 8 );
+    flags = sc_is_canonical( sv ) ? 0u : F_S_BAD;                          /* user.c:159-161 */
     #pragma unroll 1
     for( int pt=0; pt<2; pt++ ) {
-      u32 w[8];
-      #pragma unroll
-      for( int q=0; q<8; q++ ) w[q] = pt ? sig[q] : pub[q];
+      u32 w[8];                      /* loaded per point: nothing stays live across the decodes */
+      load_words( w, pt ? sigs + 64*i : pubs + 32*i, 8 );
       ge_p3 P;
       u32 f = ge_decode( P, w );
       bool small = !(f & 1u) && ge_affine_is_small_order( P );            /* user.c:194-199 */
@@ -354,30 +352,25 @@ DEV void prep_slot( ulong t, ulong n, ulong chunk, uchar const * __restrict__ si
   }
   {
     /* the whole wave hashes together (inactive lanes with an empty message) */
-    u32 pre[16], x[16], k[8], sv[8];
-    uchar const * sp = sigs + 64*i, * pp = pubs + 32*i;
+    u32 x[16], k[8];
+    uchar const * sp = sigs + 64*i, * pp = pubs + 32*i;  /* inactive lanes: record 0's (valid) R, A */
     asm volatile( "" : "+v"(sp), "+v"(pp) );
     u32 mo = 0u, ms = 0u;
-    #pragma unroll
-    for( int q=0; q<16; q++ ) pre[q] = 0u;
-    #pragma unroll
-    for( int q=0; q<8; q++ ) sv[q] = 0u;
     if( active ) {
-      load_words( pre, sp, 8 );                                            /* R */
-      load_words( pre + 8, pp, 8 );                                        /* A */
-      load_words( sv, sp + 32, 8 );                                        /* S */
+      u32 sv[8];                                                           /* S to the state before the */
+      load_words( sv, sp + 32, 8 );                                        /* hash: not live across it  */
+      u32 * s = st + sl;
+      #pragma unroll
+      for( int w=0; w<8; w++ ) s[(ST_S+w)*chunk] = sv[w];
       mo = moff ? moff[i] : (u32)i * fixed_sz;
       ms = msz  ? msz[i]  : fixed_sz;
     }
-    sha512_prefixed_coop<64u>( x, pre, pool + mo, ms, lds_msg, lds_meta, threadIdx.x & 63u );   /* user.c:205-206 */
+    sha512_prefixed_coop<64u>( x, sp, pp, pool + mo, ms, lds_msg, lds_meta, threadIdx.x & 63u );   /* user.c:205-206 */
     if( active ) {
       sc_reduce512( k, x );                                                /* user.c:207 */
       u32 * s = st + sl;
       #pragma unroll
-      for( int w=0; w<8; w++ ) {
-        s[(ST_K +w)*chunk] = k[w];
-        s[(ST_S +w)*chunk] = sv[w];
-      }
+      for( int w=0; w<8; w++ ) s[(ST_K+w)*chunk] = k[w];
     }
   }
   /* Survivor compaction: a signature that fails a pre-check gets its final
@@ -399,7 +392,12 @@ DEV void prep_slot( ulong t, ulong n, ulong chunk, uchar const * __restrict__ si
 /* one workgroup per 256 records (a persistent grid pulling 64-record tasks,
    as k_verify_dsm does, measured slower on C2: prep 1.98-2.07 vs 1.96-1.98
    ms; C4 within noise) */
-__global__ __launch_bounds__(256)
+/* 4 waves per SIMD (128 VGPRs, ~10 spilled; the LDS windows allow exactly
+   4 workgroups per CU) against 3 at the natural 132: C2 134.05 vs 132.92 M
+   verifies/s over 6 alternating pairs on two boxes, C4 112.7 vs 112.8
+   (profiles/r03ae, profiles/r03af) */
+#define PREP_OCCUPANCY __attribute__((amdgpu_waves_per_eu(4, 4)))
+__global__ __launch_bounds__(256) PREP_OCCUPANCY
 void k_verify_prep( ulong n, ulong chunk, uchar const * __restrict__ sigs, uchar const * __restrict__ pubs,
                     uchar const * __restrict__ pool, uint const * __restrict__ moff, uint const * __restrict__ msz,
                     u32 fixed_sz, u32 * __restrict__ st, int errmode, u32 * __restrict__ idx,
@@ -1418,7 +1416,7 @@ __global__ __launch_bounds__(64) void k_test_sha512( ulong n, uchar const * pool
   #pragma unroll
   for( int q=0; q<16; q++ ) pre[q] = 0u;
   if( coop ) {            /* the k_verify_prep path: the whole wave, lanes past n hash nothing */
-    sha512_prefixed_coop<0u>( x, pre, pool + (i < n ? moff[i] : 0u), i < n ? msz[i] : 0u, lds_msg, lds_meta,
+    sha512_prefixed_coop<0u>( x, nullptr, nullptr, pool + (i < n ? moff[i] : 0u), i < n ? msz[i] : 0u, lds_msg, lds_meta,
                               threadIdx.x & 63u );
     if( i >= n ) return;
   } else {

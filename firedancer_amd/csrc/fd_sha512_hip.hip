@@ -40,10 +40,8 @@ void k_sha512_batch( ulong n, uchar const * __restrict__ pool, uint const * __re
   u32 lane = threadIdx.x & 63u;
   ulong i = wave0 + lane;
   bool live = i < n;
-  u32 pre[16], x[16];
-  #pragma unroll
-  for( int q=0; q<16; q++ ) pre[q] = 0u;
-  sha512_prefixed_coop<0u>( x, pre, pool + (live ? off[i] : 0u), live ? sz[i] : 0u,
+  u32 x[16];
+  sha512_prefixed_coop<0u>( x, nullptr, nullptr, pool + (live ? off[i] : 0u), live ? sz[i] : 0u,
                             lds_msg_all + SHA_WAVE_WORDS*(threadIdx.x >> 6), lds_meta_all + 64*(threadIdx.x >> 6),
                             lane );
   if( !live ) return;
