@@ -40,7 +40,7 @@ def main():
                                                    "firedancer_amd", "libfd_ed25519_hip.so"))
     res["bench_value"] = bench["value"]
     cal = json.load(open(os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "profiles",
-                                      os.environ.get("FD_ISSUE_CALIBRATION", "r03p_valu_issue_calibration.json"))))
+                                      os.environ.get("FD_ISSUE_CALIBRATION", "r03ag_valu_issue_calibration.json"))))
     res["single_issue_ceiling_slot_util"] = cal.get("single_issue_ceiling_slot_util")   # same microbenchmark
     json.dump(res, open(out, "w"), indent=1)
     print(json.dumps(res["engine"], indent=1))
