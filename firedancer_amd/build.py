@@ -12,7 +12,7 @@ PKG = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(PKG, "csrc")
 LIB = os.path.join(PKG, "libfd_ed25519_hip.so")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
-SOURCES = ["fd_ed25519_hip.hip", "fd_ed25519_dev.h", "fd_txn_hip.hip", "fd_sha512_hip.hip"]
+SOURCES = ["fd_ed25519_hip.hip", "fd_ed25519_dev.h", "fd_hip_order.h", "fd_txn_hip.hip", "fd_sha512_hip.hip"]
 UNITS = ["fd_ed25519_hip.hip", "fd_txn_hip.hip", "fd_sha512_hip.hip"]
 
 

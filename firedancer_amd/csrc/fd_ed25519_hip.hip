@@ -35,6 +35,7 @@
    the per-function citations). */
 
 #include "fd_ed25519_dev.h"
+#include "fd_hip_order.h"
 #include "../../include/fd_ed25519_hip.h"
 
 #include <hip/hip_runtime.h>
@@ -262,8 +263,8 @@ DEV int code_of( u32 f, int errmode, bool eq ) {
    (0.68-0.74 vs 0.77-0.78 ms) but C4 with six tiles loses 2-3% (110.6/111.9
    vs 113.7/114.3 M, profiles/r03q_ab_order).
    hist = count[16..31], cursor = count[32..47] (zeroed with count[0]). */
-#define ORD_KEYS 16
-DEV u32 msg_key( u32 sz ) { u32 b = (sz + 81u + 127u) >> 7; return b < 15u ? b : 15u; }
+#define ORD_KEYS FD_HIP_ORD_KEYS
+DEV u32 msg_key( u32 sz ) { return fd_hip_msg_key( sz ); }
 
 DEV ulong dev_count_n( ulong n, u32 const * d_n, ulong rec0 ) {
   if( !d_n ) return n;
@@ -284,16 +285,45 @@ void k_msg_hist( ulong n, uint const * __restrict__ msz, u32 * __restrict__ coun
   if( threadIdx.x < ORD_KEYS && h[threadIdx.x] ) atomicAdd( count + 16 + threadIdx.x, h[threadIdx.x] );
 }
 
+/* Segmented records (fd_hip_order.h): the segments' histograms summed into
+   count[16..31] (k_msg_order's hist) and their record counts into *total
+   (prep's device count).  One workgroup. */
+__global__ __launch_bounds__(256)
+void k_seg_reduce( u32 const * __restrict__ seg, u32 n_seg, u32 * __restrict__ count, u32 * __restrict__ total ) {
+  u32 k = threadIdx.x;
+  if( k < ORD_KEYS ) {
+    u32 h = 0u;
+    for( u32 x = 0; x < n_seg; x++ ) h += seg[x*FD_HIP_SEG_STRIDE + FD_HIP_SEG_HIST_W + k];
+    count[16 + k] = h;
+  } else if( k == ORD_KEYS ) {
+    u32 c = 0u;
+    for( u32 x = 0; x < n_seg; x++ ) c += seg[x*FD_HIP_SEG_STRIDE + FD_HIP_SEG_CNT_W];
+    *total = c;
+  }
+}
+
+/* count[16..31] = histogram, count[32..47] = cursors.  Record t of the
+   launch is active if t < the device count, or, for segmented records
+   (seg_cap != 0), if t's place in its segment is below that segment's count;
+   order[] receives record indices, densely by block count.  A position past
+   the chunk (a histogram that disagrees with msz[]: never, both sides key
+   with fd_hip_msg_key) is dropped rather than written out of bounds. */
 __global__ __launch_bounds__(256)
 void k_msg_order( ulong n, uint const * __restrict__ msz, u32 * __restrict__ count, u32 const * __restrict__ d_n,
-                  ulong rec0, u32 * __restrict__ order ) {
+                  ulong rec0, u32 * __restrict__ order, ulong chunk, u32 const * __restrict__ seg, ulong seg_cap ) {
   __shared__ u32 h[ORD_KEYS], base[ORD_KEYS];
   if( threadIdx.x < ORD_KEYS ) h[threadIdx.x] = 0u;
   __syncthreads();
-  n = dev_count_n( n, d_n, rec0 );
   ulong t = (ulong)blockIdx.x * blockDim.x + threadIdx.x;
+  bool act;
+  if( seg_cap ) {
+    ulong sx = t / seg_cap;
+    act = t < n && t - sx*seg_cap < (ulong)seg[sx*FD_HIP_SEG_STRIDE + FD_HIP_SEG_CNT_W];
+  } else {
+    act = t < dev_count_n( n, d_n, rec0 );
+  }
   u32 key = 0u, r = 0u;
-  if( t < n ) { key = msg_key( msz[t] ); r = atomicAdd( &h[key], 1u ); }   /* rank within the block */
+  if( act ) { key = msg_key( msz[t] ); r = atomicAdd( &h[key], 1u ); }   /* rank within the block */
   __syncthreads();
   if( threadIdx.x < ORD_KEYS ) {
     u32 k = threadIdx.x, start = 0u;
@@ -301,7 +331,10 @@ void k_msg_order( ulong n, uint const * __restrict__ msz, u32 * __restrict__ cou
     base[k] = h[k] ? start + atomicAdd( count + 32 + k, h[k] ) : 0u;      /* this block's range */
   }
   __syncthreads();
-  if( t < n ) order[base[key] + r] = (u32)t;
+  if( act ) {
+    ulong pos = (ulong)base[key] + r;
+    if( pos < chunk ) order[pos] = (u32)t;
+  }
 }
 
 /* SHA-512(R||A||M) with wave-cooperative, LDS-staged message blocks
@@ -1462,10 +1495,13 @@ fd_ed25519_hip_get_timing( fd_ed25519_hip_ctx_t const * ctx, double * prep_ms, d
 static int
 verify_impl( fd_ed25519_hip_ctx_t * ctx, ulong n, uchar const * d_sigs, uchar const * d_pubs,
              uchar const * d_pool, uint const * d_msg_off, uint const * d_msg_sz, uint fixed_sz,
-             signed char * d_codes, ulong * d_bitmap, u32 const * d_n, void * stream ) {
+             signed char * d_codes, ulong * d_bitmap, u32 const * d_n, void * stream,
+             fd_hip_segs_t const * segs = (fd_hip_segs_t const *)0 ) {
   hipStream_t s = stream ? (hipStream_t)stream : ctx->stream;
   FD_CHECK( hipSetDevice( ctx->device ) );
   if( !n ) return 0;
+  if( segs && (n > ctx->chunk || !segs->n_seg || segs->n_seg > FD_HIP_SEG_MAX || !segs->total) ) return -1;
+  if( segs ) d_n = segs->total;                            /* written by k_seg_reduce below */
   if( ctx->ev_used ) FD_CHECK( hipStreamWaitEvent( s, ctx->ev_last, 0 ) );   /* previous call's scratch use */
   if( !d_n && n <= ctx->lat_max && n <= ctx->chunk && !ctx->timing ) {
     /* small batch: one workgroup per signature (k_verify_lat), racing as
@@ -1502,9 +1538,17 @@ verify_impl( fd_ed25519_hip_ctx_t * ctx, ulong n, uchar const * d_sigs, uchar co
     FD_CHECK( hipMemsetAsync( ctx->d_count, 0, (ordered ? 48 : 3)*sizeof(u32), s ) );
     if( ctx->timing ) FD_CHECK( hipEventRecord( ctx->ev[0], s ) );
     if( ordered ) {
-      hipLaunchKernelGGL( k_msg_hist, grid, blk, 0, s, m, d_msg_sz + off, ctx->d_count, d_n, off );
+      /* the block-count histogram: summed from the segments' (k_txnm_batch
+         built them while expanding the records) or k_msg_hist's */
+      if( segs ) {
+        hipLaunchKernelGGL( k_seg_reduce, dim3( 1 ), dim3( 256 ), 0, s, segs->seg, segs->n_seg, ctx->d_count,
+                            segs->total );
+      } else {
+        hipLaunchKernelGGL( k_msg_hist, grid, blk, 0, s, m, d_msg_sz + off, ctx->d_count, d_n, off );
+      }
       FD_CHECK( hipGetLastError() );
-      hipLaunchKernelGGL( k_msg_order, grid, blk, 0, s, m, d_msg_sz + off, ctx->d_count, d_n, off, ctx->d_order );
+      hipLaunchKernelGGL( k_msg_order, grid, blk, 0, s, m, d_msg_sz + off, ctx->d_count, d_n, off, ctx->d_order,
+                          ctx->chunk, segs ? segs->seg : (u32 const *)0, segs ? segs->seg_cap : 0ul );
       FD_CHECK( hipGetLastError() );
     }
     uchar const * pool = d_msg_off ? d_pool : d_pool + off*(ulong)fixed_sz;
@@ -1557,6 +1601,15 @@ fd_ed25519_hip_verify_dev_count( fd_ed25519_hip_ctx_t * ctx, ulong n_max, uint c
                                  uchar const * d_pubs, uchar const * d_pool, uint const * d_msg_off,
                                  uint const * d_msg_sz, signed char * d_codes, ulong * d_bitmap, void * stream ) {
   return verify_impl( ctx, n_max, d_sigs, d_pubs, d_pool, d_msg_off, d_msg_sz, 0u, d_codes, d_bitmap, d_n, stream );
+}
+
+int
+fd_ed25519_hip_verify_segs( fd_ed25519_hip_ctx_t * ctx, fd_hip_segs_t segs, uchar const * d_sigs,
+                            uchar const * d_pubs, uchar const * d_pool, uint const * d_msg_off,
+                            uint const * d_msg_sz, signed char * d_codes, void * stream ) {
+  if( !d_msg_off || !d_msg_sz || !segs.seg_cap ) return -1;
+  return verify_impl( ctx, (ulong)segs.n_seg * segs.seg_cap, d_sigs, d_pubs, d_pool, d_msg_off, d_msg_sz, 0u,
+                      d_codes, NULL, NULL, stream, &segs );
 }
 
 int

@@ -24,6 +24,7 @@
 
 #include "../../include/fd_verify_hip.h"
 #include "../../include/fd_replay_hip.h"
+#include "fd_hip_order.h"
 
 #include <hip/hip_runtime.h>
 #include <chrono>
@@ -130,7 +131,8 @@ struct txn_span {
 };
 
 /* fd_cu16_dec_sz + fd_cu16_dec_fixed (fd_compact_u16.h:38-92) */
-DEVI bool cu16_rd( u8 const * p, u32 sz, u32 & i, u32 & v ) {
+template<class P>
+DEVI bool cu16_rd( P const & p, u32 sz, u32 & i, u32 & v ) {
   u32 left = sz - i;
   u32 b0 = left >= 1 ? p[i] : 0u;
   if( left >= 1 && !(b0 & 0x80u) ) { v = b0; i += 1; return true; }
@@ -152,8 +154,10 @@ DEVI void put16( u8 * o, u32 off, u32 v ) { if( o ) *(u16 *)(o + off) = (u16)v; 
 
 /* fd_txn_parse_core(payload, sz, out, NULL, NULL, FD_TXN_INSTR_MAX): returns
    the footprint or 0.  Check order follows fd_txn_parse.c line by line;
-   `need(n)` is CHECK_LEFT. */
-DEVI u32 txn_parse( u8 const * p, u32 sz, u8 * out, txn_span & sp ) {
+   `need(n)` is CHECK_LEFT.  P: a byte pointer, or any type with a byte
+   operator[] (k_txnm_batch's out-frag view). */
+template<class P>
+DEVI u32 txn_parse( P const & p, u32 sz, u8 * out, txn_span & sp ) {
   u32 i = 0;
 #define NEED( n ) do { if( (u32)(n) > sz - i ) return 0u; } while( 0 )
   if( sz > (u32)FD_TXN_HIP_MTU ) return 0u;                                 /* :82 */
@@ -234,7 +238,7 @@ DEVI u32 txn_parse( u8 const * p, u32 sz, u8 * out, txn_span & sp ) {
 /* packed per-frag results for the host pass (k_tile_results, below) */
 struct __attribute__((packed)) tile_res { u64 tag; u64 bid; u16 tsz; signed char tcode; u8 kind; u32 pad; };
 static_assert( sizeof(tile_res) == 24, "tile_res layout" );
-#define TILE_RES_HDR 16ul
+#define TILE_RES_HDR 32ul   /* u32 record count, u32 flag, u64 pad, u64 ingest bytes read, written */
 
 /* per-frag SoA scratch written by k_txn_parse */
 struct parse_out {
@@ -428,6 +432,514 @@ void k_txnm_ingest( ulong n, u8 const * in, u32 const * __restrict__ in_chunk,
   }
 }
 
+/**********************************************************************/
+/* k_txnm_batch: ingest + parse + record expansion in one pass          */
+
+/* One 64-thread workgroup per group of F fd_txn_m_t frags; the frags go
+   through LDS once:
+
+   1. stage   every 16-B piece of the group's frags (the header and the
+              bytes during_frag copies; for a gossip vote its txn) is loaded
+              once, pieces dealt to lanes over the group's piece prefix sums
+              so that all 64 lanes load and the loads coalesce; each piece is
+              stored to LDS at its prefix position (packed: a frag takes its
+              own size, ~30 pieces in a txn stream, not the 82 of the MTU)
+              and, where during_frag copies it, to the out dcache
+              (fd_verify_tile.c:64-99)
+   2. parse   lane f parses frag f's payload from LDS (fd_txn_parse_core,
+              fd_txn_parse.c:7-254, restated as txn_parse above but reading
+              4 bytes per LDS access), writes the fd_txn_t at fd_txn_m_txn_t
+              and txn_t_sz into the out header (after_frag, :118-120), and
+              hashes sig0 for the tcache tag (fd_txn_verify, fd_verify_tile.h:76)
+   3. expand  the group's signatures get one contiguous record range (one
+              atomic per group), and the wave copies each record's signature
+              and public key out of LDS as 16-B pieces (coalesced stores);
+              per-record message spans; the block-count histogram prep's
+              order is built from (fd_hip_order.h)
+
+   Against k_txnm_ingest + k_txn_parse + k_txn_expand (+ k_msg_hist) this
+   reads each frag from HBM once instead of three times, and the parse's
+   dependent byte loads hit LDS instead of HBM.  The kernel is bound by the
+   bytes it keeps in flight, so the LDS per group is a budget of
+   FB_PIECES_PER_FRAG pieces per frag (10 KB for 16 frags: 16 workgroups per
+   CU) rather than an MTU-sized slot per frag (21 KB: 7 workgroups per CU,
+   profiles/r04b trace: the staging phase was 58% of a workgroup's life).
+
+   The global path: after_frag parses the OUT frag, so where during_frag's
+   copy did not reach (a header whose payload_sz exceeds the frag, a frag
+   shorter than its header) it reads the out dcache's stale bytes.  A group
+   with such a frag, or whose pieces overflow the budget, parses, hashes and
+   expands through frag_view (in-frag bytes below the copy's end, out-frag
+   bytes past it, loaded from global memory) instead of LDS: the same bytes
+   the reference's parse sees.  A corrupt frag sets *flag (the host aborts
+   in complete()) and parses as an empty payload, as in k_txnm_ingest. */
+
+/* FD_TXNM_TRACE builds (diagnostic variants only, firedancer_amd/build.py
+   <variant> FD_TXNM_TRACE=1): lane 0 of every k_txnm_batch workgroup
+   records s_memtime at each phase boundary; fd_verify_hip_txnm_trace()
+   copies them out. */
+#ifndef FD_TXNM_TRACE
+#define FD_TXNM_TRACE 0
+#endif
+#if FD_TXNM_TRACE
+#define TXTR_SLOTS 8
+#define TXTR_MAX   (1ul << 17)
+__device__ u64 g_txnm_trace[ TXTR_MAX * TXTR_SLOTS ];
+#define TXTR( k ) do { if( threadIdx.x == 0u && blockIdx.x < TXTR_MAX ) \
+    g_txnm_trace[ (ulong)blockIdx.x * TXTR_SLOTS + (k) ] = __builtin_amdgcn_s_memtime(); } while( 0 )
+extern "C" int fd_verify_hip_txnm_trace( void * out, ulong n_wg ) {
+  if( n_wg > TXTR_MAX ) n_wg = TXTR_MAX;
+  return (int)hipMemcpyFromSymbol( out, HIP_SYMBOL( g_txnm_trace ), n_wg * TXTR_SLOTS * sizeof(u64), 0,
+                                   hipMemcpyDeviceToHost );
+}
+#else
+#define TXTR( k ) do {} while( 0 )
+#endif
+
+/* FD_TXNM_ABLATE (diagnostic variants only; results are wrong): bit 0 no
+   fd_txn_t stores, bit 1 no out-frag copy stores, bit 2 no parse, bit 3 no
+   record stores */
+#ifndef FD_TXNM_ABLATE
+#define FD_TXNM_ABLATE 0
+#endif
+
+#define FB_PIECES_PER_FRAG 40u   /* LDS budget: 640 B per frag on average (a normal stream's mean is ~30 pieces) */
+#define FB_LB        8    /* pieces in flight per lane */
+
+/* 4 bytes at LDS byte offset i (two aligned dword reads and a funnel shift;
+   reads up to 7 bytes past i) */
+DEVI u32 lds_ld4( u8 const * l, u32 i ) {
+  u32 const * q = (u32 const *)(l + (i & ~3u));
+  return __builtin_amdgcn_alignbit( q[1], q[0], (i & 3u) * 8u );
+}
+
+/* fd_cu16_dec (fd_compact_u16.h:38-92) on the 4 bytes w = p[i..i+3], left =
+   sz - i bytes remaining: same accept/reject as cu16_rd */
+DEVI bool cu16_w( u32 w, u32 left, u32 & len, u32 & v ) {
+  u32 b0 = w & 0xffu, b1 = (w >> 8) & 0xffu, b2 = (w >> 16) & 0xffu;
+  if( left >= 1u && !(b0 & 0x80u) ) { v = b0; len = 1u; return true; }
+  if( left >= 2u && !(b1 & 0x80u) ) {
+    if( !b1 ) return false;
+    v = (b0 & 0x7fu) | (b1 << 7); len = 2u; return true;
+  }
+  if( left >= 3u && !(b2 & 0xfcu) ) {
+    if( !b2 ) return false;
+    v = (b0 & 0x7fu) | ((b1 & 0x7fu) << 7) | (b2 << 14); len = 3u; return true;
+  }
+  return false;
+}
+
+/* txn_parse (above) over a payload in LDS: identical checks, order and
+   output; out (global, 2-aligned) receives the fd_txn_t */
+DEVI u32 txn_parse_lds( u8 const * p, u32 sz, u8 * out, txn_span & sp ) {
+  u32 i = 0, len, w;
+#define NEED( n ) do { if( (u32)(n) > sz - i ) return 0u; } while( 0 )
+  if( sz > (u32)FD_TXN_HIP_MTU ) return 0u;                                 /* :82 */
+  NEED( 1 ); u32 sig_cnt = p[0]; i = 1u;
+  if( sig_cnt < 1u || sig_cnt > 127u ) return 0u;                           /* :91 */
+  NEED( 64u*sig_cnt ); u32 sig_off = i; i += 64u*sig_cnt;
+  u32 msg_off = i;
+  u32 h0 = lds_ld4( p, i ), h1 = lds_ld4( p, i + 4u );                       /* message header, one LDS round */
+  NEED( 1 ); u32 b0 = h0 & 0xffu; i++;
+  u32 version, hb = 1u;                                                     /* hb: header bytes consumed from h */
+  if( b0 & 0x80u ) {                                                        /* :98-104 */
+    version = b0 & 0x7fu;
+    if( version != 0u ) return 0u;
+    NEED( 1 ); if( ((h0 >> 8) & 0xffu) != sig_cnt ) return 0u; i++; hb = 2u;
+  } else {
+    version = 0xffu;
+    if( b0 != sig_cnt ) return 0u;
+  }
+  u32 h = __builtin_amdgcn_alignbit( h1, h0, hb * 8u );                     /* bytes msg_off+hb .. +hb+3 */
+  NEED( 1 ); u32 ro_signed = h & 0xffu; i++;
+  if( ro_signed >= sig_cnt ) return 0u;                                     /* :111 */
+  NEED( 1 ); u32 ro_unsigned = (h >> 8) & 0xffu; i++;
+  u32 acct_cnt;
+  w = hb == 1u ? __builtin_amdgcn_alignbit( h1, h0, 24u ) : h1;            /* the varint's (up to) 3 bytes */
+  if( !cu16_w( w, sz - i, len, acct_cnt ) ) return 0u;
+  i += len;
+  if( sig_cnt > acct_cnt || acct_cnt > 128u ) return 0u;                    /* :117 */
+  if( sig_cnt + ro_unsigned > acct_cnt ) return 0u;                         /* :118 */
+  NEED( 32u*acct_cnt ); u32 acct_off = i; i += 32u*acct_cnt;
+  NEED( 32 ); u32 bh_off = i; i += 32u;
+  u32 instr_cnt;
+  if( !cu16_w( lds_ld4( p, i ), sz - i, len, instr_cnt ) ) return 0u;
+  i += len;
+  if( instr_cnt > 64u ) return 0u;                                          /* :129 */
+  NEED( 3u*instr_cnt );
+  if( !( acct_cnt > (instr_cnt ? 1u : 0u) ) ) return 0u;                    /* :134 */
+  put8( out, 0, version ); put8( out, 1, sig_cnt ); put16( out, 2, sig_off ); put16( out, 4, msg_off );
+  put8( out, 6, ro_signed ); put8( out, 7, ro_unsigned ); put16( out, 8, acct_cnt ); put16( out, 10, acct_off );
+  put16( out, 12, bh_off ); put16( out, 18, instr_cnt );
+  u32 max_acct = 0;
+  for( u32 j = 0; j < instr_cnt; j++ ) {                                    /* :153-184 */
+    NEED( 3 );
+    w = lds_ld4( p, i );
+    u32 prog = w & 0xffu; i++;
+    u32 ia_cnt, data_sz;
+    if( !cu16_w( w >> 8, sz - i, len, ia_cnt ) ) return 0u;
+    i += len;
+    NEED( ia_cnt ); u32 ia_off = i;
+    i += ia_cnt;
+    u32 wd = lds_ld4( p, i );                                               /* data_sz varint: before the max loop */
+    for( u32 k = 0; k < ia_cnt; k += 4u ) {                                 /* max account index, 4 bytes a read */
+      u32 x = lds_ld4( p, ia_off + k ), left = ia_cnt - k;
+      if( left < 4u ) x &= (1u << (8u*left)) - 1u;
+      u32 m = max( max( x & 0xffu, (x >> 8) & 0xffu ), max( (x >> 16) & 0xffu, x >> 24 ) );
+      max_acct = m > max_acct ? m : max_acct;
+    }
+    if( !cu16_w( wd, sz - i, len, data_sz ) ) return 0u;
+    i += len;
+    NEED( data_sz ); u32 data_off = i; i += data_sz;
+    if( !( prog > 0u && prog < acct_cnt ) ) return 0u;                      /* :171 */
+    u32 o = 20u + 10u*j;
+    put8( out, o, prog ); put8( out, o+1, 0 ); put16( out, o+2, ia_cnt ); put16( out, o+4, data_sz );
+    put16( out, o+6, ia_off ); put16( out, o+8, data_off );
+  }
+  u32 lut_cnt = 0, adtl_w = 0, adtl = 0;
+  if( version == 0u ) {                                                     /* :193-226 */
+    if( !cu16_w( lds_ld4( p, i ), sz - i, len, lut_cnt ) ) return 0u;
+    i += len;
+    if( lut_cnt > 127u ) return 0u;
+    NEED( 34u*lut_cnt );
+    for( u32 j = 0; j < lut_cnt; j++ ) {
+      NEED( 32 ); u32 a_off = i; i += 32u;
+      u32 wl, ro;
+      if( !cu16_w( lds_ld4( p, i ), sz - i, len, wl ) ) return 0u;
+      i += len;
+      NEED( wl ); u32 w_off = i; i += wl;
+      if( !cu16_w( lds_ld4( p, i ), sz - i, len, ro ) ) return 0u;
+      i += len;
+      NEED( ro ); u32 ro_off = i; i += ro;
+      if( wl > 128u - acct_cnt || ro > 128u - acct_cnt || wl + ro < 1u ) return 0u;
+      u32 o = 20u + 10u*instr_cnt + 8u*j;
+      put16( out, o, a_off ); put8( out, o+2, wl ); put8( out, o+3, ro ); put16( out, o+4, w_off ); put16( out, o+6, ro_off );
+      adtl_w += wl; adtl += wl + ro;
+    }
+  }
+  if( i != sz ) return 0u;                                                  /* :229 */
+  if( acct_cnt + adtl > 128u ) return 0u;                                   /* :231 */
+  if( !( max_acct < acct_cnt + adtl ) ) return 0u;                          /* :234 */
+#undef NEED
+  put8( out, 14, lut_cnt ); put8( out, 15, adtl_w ); put8( out, 16, adtl ); put8( out, 17, 0 );
+  sp.sig_at = sig_off; sp.acct_at = acct_off; sp.msg_at = msg_off; sp.msg_sz = sz - msg_off;
+  sp.nsig = sig_cnt <= SIG_VERIFY_MAX ? sig_cnt : 0u;
+  return 20u + 10u*instr_cnt + 8u*lut_cnt;
+}
+
+/* 16 bytes at LDS byte offset a, any alignment */
+DEVI uint4 lds_ld16u( u8 const * l, u32 a ) {
+  u32 const * q = (u32 const *)(l + (a & ~3u));
+  u32 sh = (a & 3u) * 8u;
+  u32 d0 = q[0], d1 = q[1], d2 = q[2], d3 = q[3], d4 = q[4];
+  return make_uint4( __builtin_amdgcn_alignbit( d1, d0, sh ), __builtin_amdgcn_alignbit( d2, d1, sh ),
+                     __builtin_amdgcn_alignbit( d3, d2, sh ), __builtin_amdgcn_alignbit( d4, d3, sh ) );
+}
+
+/* the first nb (< 16) bytes of v to d (16-B aligned): whole dwords, then bytes */
+DEVI void store_head( u8 * d, uint4 v, u32 nb ) {
+  u32 w[4] = { v.x, v.y, v.z, v.w };
+  u32 nd = nb >> 2;
+  #pragma unroll
+  for( u32 k = 0; k < 3; k++ ) if( k < nd ) ((u32 *)d)[k] = w[k];
+  u32 t = nb & 3u, x = w[nd & 3u];
+  u8 * e = d + 4u*nd;
+  if( t > 0u ) e[0] = (u8)x;
+  if( t > 1u ) e[1] = (u8)(x >> 8);
+  if( t > 2u ) e[2] = (u8)(x >> 16);
+}
+
+/* which of the group's F frags item q belongs to: the last f with
+   start_f <= q, where lane f holds start_f (ascending over the lanes, start_0
+   = 0; lanes past the group's frags hold the total, past every item).  A
+   binary search over __shfl reads: call with every lane of the wave active. */
+template<int F>
+DEVI u32 group_of( u32 start, u32 q ) {
+  u32 f = 0u;
+  #pragma unroll
+  for( u32 step = (u32)F / 2u; step; step >>= 1 ) {
+    u32 c = f + step;
+    f = (u32)__shfl( (int)start, (int)c ) <= q ? c : f;
+  }
+  return f;
+}
+
+/* a tile slot's misc block (memset per batch): a header line ([0] total
+   record count, written by the verify's k_seg_reduce; [1] corrupt-frag
+   flag), then one fd_hip_order.h segment per record segment: its counter
+   line (count, and the u64 ingest byte counter at SEG_BYTES_W) and its
+   block-count histogram line */
+#define SEG_BYTES_W        2u
+#define FB_SEGS           64u      /* record segments of a batch at most (fd_hip_order.h: ~1000 claims per counter) */
+#define SLOT_MISC_WORDS   (32u + FD_HIP_SEG_MAX*FD_HIP_SEG_STRIDE)
+#define SLOT_MISC_BYTES   (4ul*SLOT_MISC_WORDS)
+#define SLOT_SEG_SLACK    (16ul*(FB_SEGS + 1ul))   /* frags of rounding per batch: records sized 12 x (n + slack) */
+
+/* The out frag as after_frag reads it, byte by byte: during_frag's copy
+   [lo, cend) comes from the in frag, everything else is the out dcache's
+   (k_txnm_batch's global path) */
+struct frag_view {
+  u8 const * src; u8 const * dst; u32 cend;
+  DEVI u32 operator[]( u32 x ) const { return x < cend ? src[x] : dst[x]; }
+};
+struct pay_view {                                          /* the payload: frag offset 80 + i */
+  frag_view f;
+  DEVI u32 operator[]( u32 i ) const { return f[FD_VERIFY_HIP_TXNM_SZ + i]; }
+};
+
+template<int F>
+__global__ __launch_bounds__(64)
+void k_txnm_batch( ulong n, u8 const * in, u32 const * __restrict__ in_chunk, u16 const * __restrict__ in_sz,
+                   u8 const * __restrict__ in_kind, u8 * out, u32 const * __restrict__ out_chunk, u64 seed,
+                   u16 * __restrict__ tsz_o, u64 * __restrict__ tag_o, u64 * __restrict__ bid_o,
+                   u32 * __restrict__ first_o, u8 * __restrict__ cnt_o, u32 * __restrict__ misc,
+                   u8 * __restrict__ rsig, u8 * __restrict__ rpub, u32 * __restrict__ rmoff,
+                   u32 * __restrict__ rmsz, u32 n_seg, ulong seg_cap ) {
+  constexpr u32 BUDGET = FB_PIECES_PER_FRAG * (u32)F;                        /* staged pieces per group */
+  __shared__ __attribute__((aligned(16))) u8 lds[16u * BUDGET + 32u];       /* + over-read of the last piece */
+  /* this group's record segment (fd_hip_order.h): claims, histogram and
+     byte counts go to its own lines, ~nwg/n_seg groups per counter */
+  u32 const sx = blockIdx.x % n_seg;
+  u32 * const flag = misc + 1, * const seg = misc + 32u + sx * FD_HIP_SEG_STRIDE;
+  u32 const lane = threadIdx.x;
+  ulong const j0 = (ulong)blockIdx.x * (ulong)F;
+  if( j0 >= n ) return;
+  u32 const nf = n - j0 < (ulong)F ? (u32)(n - j0) : (u32)F;
+  TXTR( 0 );
+
+  /* per-frag metadata on lanes [0, nf) */
+  bool const fl = lane < nf;
+  ulong const j = j0 + lane;
+  u32 ic = 0u, oc = 0u, sz = 0u, kind = 0u;
+  if( fl ) { ic = in_chunk[j]; oc = out_chunk[j]; sz = in_sz[j]; kind = in_kind[j]; }
+  u8 const * src = in + 64ul * ic;
+  u8 *       dst = out + 64ul * oc;
+  bool const gossip = fl && kind == FD_VERIFY_HIP_IN_GOSSIP;
+  u32 tsz_g = 0u;
+  if( __ballot( gossip ) && gossip ) {
+    u64 t = *(u64 const *)(src + FD_VERIFY_HIP_GOSSIP_VOTE_TXN_SZ_OFF);
+    tsz_g = t > (u64)FD_TXN_HIP_MTU ? 0xffffffffu : (u32)t;
+  }
+  /* staged byte range [lo, hi) of the in frag (whole pieces); the bytes
+     during_frag copies to the same offsets of the out frag: [lo, cend) */
+  u32 bad = 0u, lo = 0u, hi = 0u, cend = 0u;
+  if( fl ) {
+    if( gossip ) {
+      bad = sz > 2048u || tsz_g == 0xffffffffu;
+      u32 psz = bad ? 0u : tsz_g;
+      lo = FD_VERIFY_HIP_GOSSIP_VOTE_TXN_OFF; hi = lo + psz; cend = hi;     /* vote.txn -> the payload */
+    } else {
+      bad = sz > FD_VERIFY_HIP_TPU_RAW_MTU;
+      if( !bad ) {
+        hi = sz > FD_VERIFY_HIP_TXNM_SZ ? sz : FD_VERIFY_HIP_TXNM_SZ;       /* with the whole header */
+        cend = src == dst ? 0u : sz;                                        /* in place: copied by the host tile */
+      }
+    }
+  }
+  u32 const np = (((hi + 15u) & ~15u) - lo) >> 4;                           /* pieces, <= 82 */
+
+  /* piece prefix sums over the group (np < 128: seven ballots): frag f's
+     pieces are the group's pieces [excl_f, excl_f + np_f), staged at LDS
+     byte 16 excl_f (packed: a frag takes its own size, not the MTU) */
+  u32 excl = 0u, tot = 0u;
+  #pragma unroll
+  for( int b = 0; b < 7; b++ ) {
+    unsigned long long m = __ballot( (np >> b) & 1u );
+    excl += __builtin_amdgcn_mbcnt_hi( (u32)(m >> 32), __builtin_amdgcn_mbcnt_lo( (u32)m, 0u ) ) << b;
+    tot  += (u32)__popcll( m ) << b;
+  }
+  bool const packed = tot <= BUDGET;                                        /* wave-uniform */
+  TXTR( 1 );
+
+  /* 1. stage: piece q of the group -> lane q % 64; to LDS (if the group
+     fits) and, where during_frag copies it, to the out frag */
+  for( u32 q0 = 0u; q0 < tot; q0 += 64u * FB_LB ) {
+    uint4 v[FB_LB];
+    u32 ce[FB_LB];
+    u8 * da[FB_LB];
+    #pragma unroll
+    for( int r = 0; r < FB_LB; r++ ) {
+      u32 q = q0 + 64u * (u32)r + lane;
+      u32 f = group_of<F>( excl, q < tot ? q : 0u );
+      u32 fic = __shfl( ic, (int)f ), foc = __shfl( oc, (int)f ), flo = __shfl( lo, (int)f );
+      u32 fce = __shfl( cend, (int)f ), fex = __shfl( excl, (int)f );
+      u32 b = flo + 16u * (q - fex);                                         /* byte offset in the frag */
+      da[r] = out + 64ul * foc + b;
+      ce[r] = q < tot ? (fce > b ? fce - b : 0u) : 0u;                       /* bytes of this piece to copy */
+      if( q < tot ) v[r] = *(uint4 const *)(in + 64ul * fic + b);
+    }
+    #pragma unroll
+    for( int r = 0; r < FB_LB; r++ ) {
+      u32 q = q0 + 64u * (u32)r + lane;
+      if( packed && q < tot ) *(uint4 *)(lds + 16u * q) = v[r];
+      if( FD_TXNM_ABLATE & 2 ) continue;
+      if( ce[r] >= 16u )     *(uint4 *)da[r] = v[r];
+      else if( ce[r] )       store_head( da[r], v[r], ce[r] );
+    }
+  }
+  __syncthreads();
+  TXTR( 2 );
+
+  /* 2. header and parse (lanes [0, nf)).  after_frag reads the OUT frag:
+     where during_frag's copy did not reach (a frag shorter than its header,
+     a payload_sz past the frag) those are the out dcache's own bytes.  A
+     group with such a frag, or one whose pieces overflow the LDS budget,
+     parses through frag_view from global memory instead of LDS. */
+  frag_view const fv = { src, dst, cend };
+  u32 const hb = 16u * excl;                                                /* the frag's first staged byte in LDS */
+  u32 psz = 0u, tsz = 0u, nsig = 0u, side = 0u;
+  u64 bid = 0ul, tag = 0ul;
+  txn_span sp = { 0u, 0u, 0u, 0u, 0u, 0u };
+  if( fl ) {
+    if( gossip ) {
+      psz = bad ? 0u : tsz_g;
+    } else if( !bad ) {
+      bool short_hdr = src != dst && sz < FD_VERIFY_HIP_TXNM_SZ;
+      if( packed && !short_hdr ) {
+        psz = *(u16 const *)(lds + hb + FD_VERIFY_HIP_TXNM_PAYLOAD_SZ_OFF);
+        bid = *(u64 const *)(lds + hb + FD_VERIFY_HIP_TXNM_BUNDLE_ID_OFF);
+      } else {
+        psz = fv[FD_VERIFY_HIP_TXNM_PAYLOAD_SZ_OFF] | (fv[FD_VERIFY_HIP_TXNM_PAYLOAD_SZ_OFF + 1u] << 8);
+        #pragma unroll
+        for( u32 k = 0; k < 8u; k++ ) bid |= (u64)fv[FD_VERIFY_HIP_TXNM_BUNDLE_ID_OFF + k] << (8u*k);
+      }
+      if( psz > FD_TXN_HIP_MTU ) { bad = 1u; psz = 0u; }
+      u32 have = src == dst ? ((hi + 15u) & ~15u) : sz;                     /* bytes of the out frag staged */
+      side = short_hdr || FD_VERIFY_HIP_TXNM_SZ + psz > have;               /* parse reads bytes not staged */
+    }
+    if( bad ) atomicOr( flag, 1u );
+  }
+  bool const glob = !packed || __ballot( side );
+  /* the copy's stores precede the parse's where they can meet: a lying
+     payload_sz can place the fd_txn_t over copied bytes, and the reference
+     writes it after the copy (no frag of a normal stream: its fd_txn_t
+     starts at or past the copied end) */
+  u32 const po = FD_VERIFY_HIP_TXNM_SZ + psz;
+  u32 const to = (po + (FD_VERIFY_HIP_TXN_ALIGN - 1u)) & ~(FD_VERIFY_HIP_TXN_ALIGN - 1u);
+  if( __ballot( fl && to < cend ) ) __builtin_amdgcn_s_waitcnt( 0 );
+  TXTR( 3 );
+  u32 const pb = hb + FD_VERIFY_HIP_TXNM_SZ - lo;                           /* payload byte 0 in LDS */
+  pay_view const pv = { fv };
+  if( fl ) {
+    if( gossip ) {                                                          /* fd_verify_tile.c:90-95 */
+      *(u16 *)(dst + FD_VERIFY_HIP_TXNM_PAYLOAD_SZ_OFF) = (u16)psz;
+      *(u64 *)(dst + FD_VERIFY_HIP_TXNM_BUNDLE_ID_OFF) = 0ul;
+      *(u32 *)(dst + FD_VERIFY_HIP_TXNM_SRC_IPV4_OFF) = *(u32 const *)(src + FD_VERIFY_HIP_GOSSIP_VOTE_ADDR_OFF);
+      dst[FD_VERIFY_HIP_TXNM_SRC_TPU_OFF] = (u8)FD_VERIFY_HIP_TPU_SOURCE_GOSSIP;
+    }
+    u8 * tout = (FD_TXNM_ABLATE & 1) ? (u8 *)0 : dst + to;
+    u32 psz_p = (FD_TXNM_ABLATE & 4) ? 0u : psz;
+    tsz = glob ? txn_parse( pv, psz_p, tout, sp ) : txn_parse_lds( lds + pb, psz_p, tout, sp );
+    *(u16 *)(dst + FD_VERIFY_HIP_TXNM_TXN_T_SZ_OFF) = (u16)tsz;
+    nsig = tsz ? sp.nsig : 0u;
+  }
+  TXTR( 4 );
+
+  /* 3. expand: records of the group contiguous, in frag order; the range
+     is claimed before the tag hash so that the atomic's round trip overlaps
+     it */
+  u32 rex = 0u, rtot = 0u;
+  #pragma unroll
+  for( int b = 0; b < 5; b++ ) {                                            /* nsig <= 16 */
+    unsigned long long m = __ballot( (nsig >> b) & 1u );
+    rex  += __builtin_amdgcn_mbcnt_hi( (u32)(m >> 32), __builtin_amdgcn_mbcnt_lo( (u32)m, 0u ) ) << b;
+    rtot += (u32)__popcll( m ) << b;
+  }
+  u32 base = 0u;
+  if( lane == 0u && rtot ) base = atomicAdd( seg + FD_HIP_SEG_CNT_W, rtot );
+  if( fl && tsz ) {
+    u64 w[8];
+    if( glob ) {
+      #pragma unroll
+      for( int q = 0; q < 8; q++ ) {
+        u64 x = 0ul;
+        #pragma unroll
+        for( u32 k = 0; k < 8u; k++ ) x |= (u64)pv[sp.sig_at + 8u*q + k] << (8u*k);
+        w[q] = x;
+      }
+    } else {
+      #pragma unroll
+      for( int q = 0; q < 8; q++ )
+        w[q] = (u64)lds_ld4( lds, pb + sp.sig_at + 8u*q ) | ((u64)lds_ld4( lds, pb + sp.sig_at + 8u*q + 4u ) << 32);
+    }
+    tag = xh_hash64( seed, w );
+  }
+  base = (u32)__builtin_amdgcn_readfirstlane( (int)base );
+  TXTR( 5 );
+  u32 lc = nsig;
+  if( fl ) {
+    if( (ulong)base + rex + nsig > seg_cap ) lc = 0u;                       /* sized 12 per frag: never taken */
+    tsz_o[j] = (u16)tsz; tag_o[j] = tag; bid_o[j] = bid;
+    first_o[j] = (u32)((ulong)sx * seg_cap + base + rex); cnt_o[j] = (u8)lc;
+  }
+  base = (u32)((ulong)sx * seg_cap + base);                                 /* the group's first record index */
+  u32 const msz = sp.msg_sz, mat = sp.msg_at, aat = sp.acct_at, sat = sp.sig_at;
+  /* sig (4 pieces) and pubkey (2 pieces) of each record.  Trip counts are
+     wave-uniform: every lane takes part in the __shfl (ds_bpermute) reads
+     of the frag lanes' values, whatever its own piece. */
+  for( u32 q0 = 0u; q0 < 6u * rtot; q0 += 64u ) {
+    u32 q = q0 + lane;
+    u32 t = (q * 0xaaabu) >> 18, p = q - 6u * t;                            /* q / 6 (q < 2^17) */
+    u32 f = group_of<F>( rex, t );
+    u32 k = t - __shfl( rex, (int)f ), flc = __shfl( lc, (int)f );
+    u32 fs = __shfl( sat, (int)f ), fa = __shfl( aat, (int)f ), fpb = __shfl( pb, (int)f );
+    u32 at = p < 4u ? fs + 64u*k + 16u*p : fa + 32u*k + 16u*(p - 4u);       /* payload offset of the piece */
+    bool live = q < 6u * rtot && k < flc;                                   /* k >= flc: a capped frag */
+    uint4 v;
+    if( glob ) {
+      u32 fic = __shfl( ic, (int)f ), foc = __shfl( oc, (int)f ), fce = __shfl( cend, (int)f );
+      pay_view const fp = { { in + 64ul * fic, out + 64ul * foc, fce } };
+      u32 w[4] = { 0u, 0u, 0u, 0u };
+      if( live )
+        for( u32 x = 0; x < 16u; x++ ) w[x >> 2] |= fp[at + x] << (8u*(x & 3u));
+      v = make_uint4( w[0], w[1], w[2], w[3] );
+    } else {
+      v = live ? lds_ld16u( lds, fpb + at ) : make_uint4( 0u, 0u, 0u, 0u );
+    }
+    if( live && !(FD_TXNM_ABLATE & 8) ) {
+      ulong r = (ulong)base + t;
+      if( p < 4u ) *(uint4 *)(rsig + 64ul*r + 16u*p) = v;
+      else         *(uint4 *)(rpub + 32ul*r + 16u*(p - 4u)) = v;
+    }
+  }
+  for( u32 t0 = 0u; t0 < rtot; t0 += 64u ) {
+    u32 t = t0 + lane;
+    u32 f = group_of<F>( rex, t );
+    u32 k = t - __shfl( rex, (int)f ), flc = __shfl( lc, (int)f );
+    u32 fo = __shfl( oc, (int)f ), fm = __shfl( mat, (int)f ), fz = __shfl( msz, (int)f );
+    if( t < rtot && k < flc ) {
+      ulong r = (ulong)base + t;
+      rmoff[r] = 64u * fo + FD_VERIFY_HIP_TXNM_SZ + fm; rmsz[r] = fz;
+    }
+  }
+  TXTR( 6 );
+  /* block-count histogram: one atomic per distinct key in the group, on the
+     segment's histogram line */
+  u32 key = fd_hip_msg_key( msz );
+  bool has = fl && lc;
+  u32 * hc = seg + FD_HIP_SEG_HIST_W;
+  for( unsigned long long pend = __ballot( has ); pend; ) {
+    u32 k0 = (u32)__builtin_amdgcn_readlane( (int)key, (int)__builtin_ctzll( pend ) );
+    bool mine = has && key == k0;
+    unsigned long long mm = __ballot( mine );
+    u32 c = 0u;
+    #pragma unroll
+    for( int b = 0; b < 5; b++ ) c += (u32)__popcll( __ballot( mine && ((lc >> b) & 1u) ) ) << b;
+    if( lane == 0u ) atomicAdd( hc + k0, c );
+    pend &= ~mm;
+  }
+  /* ingest byte accounting (fd_verify_hip_tile_ingest_stats): in-frag bytes
+     during_frag reads (low word) and writes (high word), one 64-bit atomic
+     per group on its segment's counter line */
+  u32 rd = fl && !bad ? (gossip ? psz : sz) : 0u, wr = cend > lo ? cend - lo : 0u;
+  u64 acc = 0ul;
+  #pragma unroll
+  for( int g = 0; g < F; g++ )
+    acc += (u64)(u32)__builtin_amdgcn_readlane( (int)rd, g ) | ((u64)(u32)__builtin_amdgcn_readlane( (int)wr, g ) << 32);
+  if( lane == 0u ) atomicAdd( (unsigned long long *)(seg + SEG_BYTES_W), (unsigned long long)acc );
+  TXTR( 7 );
+}
+
 extern "C" int
 fd_txn_hip_parse_dev( fd_ed25519_hip_ctx_t * ctx, ulong n, uchar const * d_pool, uint const * d_txn_off,
                       ushort const * d_txn_sz, uchar * d_txn_out, ushort * d_txn_t_sz, void * stream ) {
@@ -516,6 +1028,10 @@ struct tile_slot {
   /* fd_txn_m_t frag mode (submit_frags): payload spans, fd_txn_t offsets,
      header bundle ids, in kinds and the corrupt-frag flag */
   u32 *         d_pay_off; u16 * d_pay_sz; u32 * d_tout; u64 * d_bid; u32 * d_flag;
+  u32 *         d_misc;     /* counter, flag, record segments (SLOT_MISC_*) */
+  u32           n_seg;      /* the last batch's record segments (0: not k_txnm_batch) */
+  hipEvent_t    ev_ing0, ev_ing1;   /* around the ingest kernel (ingest timing) */
+  int           ing_timed;
   int           frags;
   hipEvent_t    ev_start, ev_done;
   int           busy;
@@ -563,6 +1079,10 @@ struct fd_verify_hip_tile {
   ulong      m_parse, m_verify, m_dedup, m_bundle, m_pub, m_sigs, m_gossip;
   tile_slot  slot[2];
   ulong      submitted, completed;
+  int        ingest_split;   /* FD_VERIFY_HIP_INGEST=split: the three-kernel frag ingest (A/B runs) */
+  int        fb;             /* k_txnm_batch frags per workgroup (FD_VERIFY_HIP_FB: 8 or 16) */
+  int        ingest_timing;  /* fd_verify_hip_tile_set_ingest_timing */
+  double     last_ingest[4]; /* fd_verify_hip_tile_ingest_stats */
   double     last_gpu_ms, last_host_ms, last_sigs;
   lat_hist   hist[2];        /* batch latency: GPU, host pass (ns) */
 };
@@ -574,12 +1094,14 @@ static void slot_alloc( tile_slot & s, ulong n ) {
   TX_CHECK( hipMalloc( &s.d_msg_at, 4*n ) );  TX_CHECK( hipMalloc( &s.d_msg_sz, 4*n ) );
   TX_CHECK( hipMalloc( &s.d_tag, 8*n ) );     TX_CHECK( hipMalloc( &s.d_first, 4*n ) );
   TX_CHECK( hipMalloc( &s.d_cnt, n ) );       TX_CHECK( hipMalloc( &s.d_tcode, n ) );
-  TX_CHECK( hipMalloc( &s.d_counter, 4 ) );
+  TX_CHECK( hipMalloc( &s.d_misc, SLOT_MISC_BYTES ) );
+  TX_CHECK( hipMemset( s.d_misc, 0, SLOT_MISC_BYTES ) );
+  s.d_counter = s.d_misc; s.d_flag = s.d_misc + 1;
   TX_CHECK( hipMalloc( &s.d_res, TILE_RES_HDR + 24*n ) );  TX_CHECK( hipHostMalloc( &s.h_res, TILE_RES_HDR + 24*n, 0 ) );
   TX_CHECK( hipMalloc( &s.d_pay_off, 4*n ) );     TX_CHECK( hipMalloc( &s.d_pay_sz, 2*n ) );
   TX_CHECK( hipMalloc( &s.d_tout, 4*n ) );        TX_CHECK( hipMalloc( &s.d_bid, 8*n ) );
-  TX_CHECK( hipMalloc( &s.d_flag, 4 ) );
   TX_CHECK( hipEventCreate( &s.ev_start ) ); TX_CHECK( hipEventCreate( &s.ev_done ) );
+  TX_CHECK( hipEventCreate( &s.ev_ing0 ) ); TX_CHECK( hipEventCreate( &s.ev_ing1 ) );
 }
 
 static void slot_free_records( tile_slot & s ) {
@@ -599,18 +1121,19 @@ static void slot_records( tile_slot & s, ulong need ) {   /* (re)size the per-si
 static void slot_free( tile_slot & s ) {
   (void)hipFree( s.d_tsz ); (void)hipFree( s.d_nsig ); (void)hipFree( s.d_sig_at ); (void)hipFree( s.d_acct_at );
   (void)hipFree( s.d_msg_at ); (void)hipFree( s.d_msg_sz ); (void)hipFree( s.d_tag ); (void)hipFree( s.d_first );
-  (void)hipFree( s.d_cnt ); (void)hipFree( s.d_tcode ); (void)hipFree( s.d_counter );
+  (void)hipFree( s.d_cnt ); (void)hipFree( s.d_tcode ); (void)hipFree( s.d_misc );
   (void)hipFree( s.d_res ); (void)hipHostFree( s.h_res );
   (void)hipFree( s.d_pay_off ); (void)hipFree( s.d_pay_sz ); (void)hipFree( s.d_tout ); (void)hipFree( s.d_bid );
-  (void)hipFree( s.d_flag );
   (void)hipEventDestroy( s.ev_start ); (void)hipEventDestroy( s.ev_done );
+  (void)hipEventDestroy( s.ev_ing0 ); (void)hipEventDestroy( s.ev_ing1 );
   slot_free_records( s );
 }
 
 __global__ __launch_bounds__(256)
 void k_tile_results( ulong n, u16 const * __restrict__ tsz, signed char const * __restrict__ tcode,
                      u64 const * __restrict__ tag, u64 const * __restrict__ bid, u8 const * __restrict__ kind,
-                     u32 const * __restrict__ counter, u32 const * __restrict__ flag, u8 * __restrict__ res );
+                     u32 const * __restrict__ counter, u32 const * __restrict__ flag, u32 n_seg,
+                     u8 * __restrict__ res );
 
 extern "C" fd_verify_hip_tile_t *
 fd_verify_hip_tile_new( fd_ed25519_hip_ctx_t * ctx, ulong max_txn, ulong seed, ulong depth, ulong map_cnt ) {
@@ -618,9 +1141,15 @@ fd_verify_hip_tile_new( fd_ed25519_hip_ctx_t * ctx, ulong max_txn, ulong seed, u
   if( !map_cnt ) map_cnt = fd_verify_hip_tcache_map_cnt_default( depth );
   if( !map_cnt || (map_cnt & (map_cnt - 1)) || map_cnt < depth + 2 ) return 0;
   TX_CHECK( hipSetDevice( fd_ed25519_hip_ctx_device( ctx ) ) );
-  fd_ed25519_hip_ctx_reserve( ctx, 12ul*max_txn );        /* one verify launch pair per batch */
+  fd_ed25519_hip_ctx_reserve( ctx, 12ul*(max_txn + SLOT_SEG_SLACK) );   /* one verify launch pair per batch */
   fd_verify_hip_tile_t * t = (fd_verify_hip_tile_t *)calloc( 1, sizeof(fd_verify_hip_tile_t) );
   t->ctx = ctx; t->max_txn = max_txn; t->seed = seed;
+  {
+    char const * e = getenv( "FD_VERIFY_HIP_INGEST" );
+    t->ingest_split = e && !strcmp( e, "split" );
+    char const * f = getenv( "FD_VERIFY_HIP_FB" );
+    t->fb = f && atoi( f ) == 8 ? 8 : 16;
+  }
   t->own_mem = (ulong *)malloc( sizeof(ulong)*(depth + map_cnt) );
   t->oldest = &t->own_oldest; t->ring = t->own_mem; t->depth = depth; t->map = t->own_mem + depth; t->map_cnt = map_cnt;
   t->own_oldest = fd_verify_hip_tcache_reset( t->ring, depth, t->map, map_cnt );
@@ -634,9 +1163,9 @@ fd_verify_hip_tile_new( fd_ed25519_hip_ctx_t * ctx, ulong max_txn, ulong seed, u
      (integration/fd_verify_tile_hip.patch, verify_hip_seccomp). */
   hipStream_t st = (hipStream_t)fd_ed25519_hip_ctx_stream( ctx );
   for( int k = 0; k < 2; k++ ) {
-    slot_records( t->slot[k], 12ul*max_txn );
+    slot_records( t->slot[k], 12ul*(max_txn + SLOT_SEG_SLACK) );
     hipLaunchKernelGGL( k_tile_results, dim3( 1 ), dim3( 64 ), 0, st, 0ul, t->slot[k].d_tsz, t->slot[k].d_tcode,
-                        t->slot[k].d_tag, (u64 const *)0, (u8 const *)0, t->slot[k].d_counter, (u32 const *)0,
+                        t->slot[k].d_tag, (u64 const *)0, (u8 const *)0, t->slot[k].d_counter, (u32 const *)0, 0u,
                         t->slot[k].d_res );
     TX_CHECK( hipGetLastError() );
   }
@@ -717,9 +1246,18 @@ extern "C" void fd_verify_hip_tile_delete( fd_verify_hip_tile_t * t ) {
 __global__ __launch_bounds__(256)
 void k_tile_results( ulong n, u16 const * __restrict__ tsz, signed char const * __restrict__ tcode,
                      u64 const * __restrict__ tag, u64 const * __restrict__ bid, u8 const * __restrict__ kind,
-                     u32 const * __restrict__ counter, u32 const * __restrict__ flag, u8 * __restrict__ res ) {
+                     u32 const * __restrict__ counter, u32 const * __restrict__ flag, u32 n_seg,
+                     u8 * __restrict__ res ) {
   ulong j = (ulong)blockIdx.x * blockDim.x + threadIdx.x;
-  if( j == 0ul ) { ((u32 *)res)[0] = *counter; ((u32 *)res)[1] = flag ? *flag : 0u; }
+  if( j == 0ul ) {
+    ((u32 *)res)[0] = *counter; ((u32 *)res)[1] = flag ? *flag : 0u;
+    u64 rd = 0ul, wr = 0ul;
+    for( u32 x = 0; x < n_seg; x++ ) {                       /* k_txnm_batch: flag = misc + 1, segments after */
+      u64 b = *(u64 const *)(flag - 1 + 32u + x*FD_HIP_SEG_STRIDE + SEG_BYTES_W);
+      rd += b & 0xffffffffull; wr += b >> 32;
+    }
+    ((u64 *)res)[2] = rd; ((u64 *)res)[3] = wr;
+  }
   if( j >= n ) return;
   tile_res r;
   r.tag = tag[j]; r.bid = bid ? bid[j] : 0ul; r.tsz = tsz[j]; r.tcode = tcode[j]; r.kind = kind ? kind[j] : 0u;
@@ -756,7 +1294,7 @@ static void
 submit_results( tile_slot & s, hipStream_t st, ulong n, uchar const * d_in_kind ) {
   hipLaunchKernelGGL( k_tile_results, dim3( (unsigned)((n + 255)/256) ), dim3( 256 ), 0, st, n, s.d_tsz, s.d_tcode,
                       s.d_tag, s.frags ? s.d_bid : (u64 const *)0, (u8 const *)d_in_kind, s.d_counter,
-                      s.frags ? s.d_flag : (u32 const *)0, s.d_res );
+                      s.frags ? s.d_flag : (u32 const *)0, s.n_seg, s.d_res );
   TX_CHECK( hipGetLastError() );
   TX_CHECK( hipMemcpyAsync( s.h_res, s.d_res, TILE_RES_HDR + 24ul*n, hipMemcpyDeviceToHost, st ) );
 }
@@ -769,7 +1307,7 @@ submit_begin( fd_verify_hip_tile_t * t, ulong n, hipStream_t & st, int & rc ) {
   if( s.busy ) { rc = -2; return 0; }                        /* two batches outstanding */
   st = (hipStream_t)fd_ed25519_hip_ctx_stream( t->ctx );
   TX_CHECK( hipSetDevice( fd_ed25519_hip_ctx_device( t->ctx ) ) );
-  s.n = n; s.nsig = 0; s.busy = 1; s.frags = 0; t->submitted++;
+  s.n = n; s.nsig = 0; s.busy = 1; s.frags = 0; s.ing_timed = 0; s.n_seg = 0; t->submitted++;
   TX_CHECK( hipEventRecord( s.ev_start, st ) );
   return &s;
 }
@@ -804,17 +1342,49 @@ fd_verify_hip_tile_submit_frags( fd_verify_hip_tile_t * t, ulong n, uchar const 
   s.frags = 1;
   if( !n ) { memset( s.h_res, 0, TILE_RES_HDR ); TX_CHECK( hipEventRecord( s.ev_done, st ) ); return 0; }
   dim3 grid( (unsigned)((n + 255)/256) ), blk( 256 );
-  TX_CHECK( hipMemsetAsync( s.d_flag, 0, 4, st ) );
-  /* one wave per frag: up to 4 frags per 256-thread workgroup, grid capped */
-  ulong wgs = (n + 3ul) / 4ul; if( wgs > 8192ul ) wgs = 8192ul;
-  hipLaunchKernelGGL( k_txnm_ingest, dim3( (unsigned)wgs ), blk, 0, st, n, d_in, d_in_chunk, d_in_sz, d_in_kind,
-                      d_out, d_out_chunk, s.d_pay_off, s.d_pay_sz, s.d_tout, s.d_bid, s.d_flag );
-  TX_CHECK( hipGetLastError() );
-  parse_out po = { s.d_tsz, s.d_nsig, s.d_sig_at, s.d_acct_at, s.d_msg_at, s.d_msg_sz, s.d_tag };
-  hipLaunchKernelGGL( k_txn_parse, grid, blk, 0, st, n, (u8 const *)d_out, s.d_pay_off, s.d_pay_sz, (u8 *)0,
-                      (u64)t->seed, po, s.d_tout );
-  TX_CHECK( hipGetLastError() );
-  submit_verify( t, s, st, n, d_out );
+  if( t->ingest_split ) {
+    /* the three-kernel form (ingest copy, one-lane parse, expansion, then
+       k_msg_hist in the verify): kept for A/B runs, FD_VERIFY_HIP_INGEST=split */
+    TX_CHECK( hipMemsetAsync( s.d_flag, 0, 4, st ) );
+    /* one wave per frag: up to 4 frags per 256-thread workgroup, grid capped */
+    ulong wgs = (n + 3ul) / 4ul; if( wgs > 8192ul ) wgs = 8192ul;
+    hipLaunchKernelGGL( k_txnm_ingest, dim3( (unsigned)wgs ), blk, 0, st, n, d_in, d_in_chunk, d_in_sz, d_in_kind,
+                        d_out, d_out_chunk, s.d_pay_off, s.d_pay_sz, s.d_tout, s.d_bid, s.d_flag );
+    TX_CHECK( hipGetLastError() );
+    parse_out po = { s.d_tsz, s.d_nsig, s.d_sig_at, s.d_acct_at, s.d_msg_at, s.d_msg_sz, s.d_tag };
+    hipLaunchKernelGGL( k_txn_parse, grid, blk, 0, st, n, (u8 const *)d_out, s.d_pay_off, s.d_pay_sz, (u8 *)0,
+                        (u64)t->seed, po, s.d_tout );
+    TX_CHECK( hipGetLastError() );
+    submit_verify( t, s, st, n, d_out );
+  } else {
+    /* k_txnm_batch: ingest, parse and record expansion in one pass, the
+       records in n_seg segments of seg_cap (fd_hip_order.h) */
+    ulong F = t->fb == 8 ? 8ul : 16ul, nwg = (n + F - 1ul) / F;
+    u32 n_seg = nwg < FB_SEGS ? (u32)nwg : FB_SEGS;
+    ulong seg_cap = 12ul * F * ((nwg + n_seg - 1ul) / n_seg);
+    ulong need = (ulong)n_seg * seg_cap;                     /* <= 12 x (n + SLOT_SEG_SLACK): sized at tile_new */
+    if( s.rcap < need ) { TX_CHECK( hipStreamSynchronize( st ) ); slot_records( s, need ); }
+    s.n_seg = n_seg;
+    TX_CHECK( hipMemsetAsync( s.d_misc, 0, 4ul*(32ul + (ulong)n_seg*FD_HIP_SEG_STRIDE), st ) );
+    s.ing_timed = t->ingest_timing;
+    if( s.ing_timed ) TX_CHECK( hipEventRecord( s.ev_ing0, st ) );
+    if( F == 8ul )
+      hipLaunchKernelGGL( k_txnm_batch<8>, dim3( (unsigned)nwg ), dim3( 64 ), 0, st, n, d_in,
+                          d_in_chunk, d_in_sz, d_in_kind, d_out, d_out_chunk, (u64)t->seed, s.d_tsz, s.d_tag, s.d_bid,
+                          s.d_first, s.d_cnt, s.d_misc, s.d_rsig, s.d_rpub, s.d_rmoff, s.d_rmsz, n_seg, seg_cap );
+    else
+      hipLaunchKernelGGL( k_txnm_batch<16>, dim3( (unsigned)nwg ), dim3( 64 ), 0, st, n, d_in,
+                          d_in_chunk, d_in_sz, d_in_kind, d_out, d_out_chunk, (u64)t->seed, s.d_tsz, s.d_tag, s.d_bid,
+                          s.d_first, s.d_cnt, s.d_misc, s.d_rsig, s.d_rpub, s.d_rmoff, s.d_rmsz, n_seg, seg_cap );
+    TX_CHECK( hipGetLastError() );
+    if( s.ing_timed ) TX_CHECK( hipEventRecord( s.ev_ing1, st ) );
+    fd_hip_segs_t segs = { s.d_misc + 32u, n_seg, seg_cap, s.d_counter };
+    if( fd_ed25519_hip_verify_segs( t->ctx, segs, s.d_rsig, s.d_rpub, d_out, s.d_rmoff, s.d_rmsz, s.d_rcode, st ) ) {
+      fprintf( stderr, "fd_verify_hip: segmented verify refused (%u x %lu records)\n", n_seg, seg_cap );
+      abort();
+    }
+    fd_ed25519_hip_group_reduce_dev( t->ctx, n, s.d_first, s.d_cnt, s.d_rcode, s.d_tcode, st );
+  }
   submit_results( s, st, n, d_in_kind );
   TX_CHECK( hipEventRecord( s.ev_done, st ) );
   return 0;
@@ -900,6 +1470,17 @@ fd_verify_hip_tile_complete( fd_verify_hip_tile_t * t, ulong const * bundle_id, 
     result[j] = FD_VERIFY_HIP_FRAG_PUBLISH;
   }
   auto h1 = std::chrono::steady_clock::now();
+  if( s.frags && !t->ingest_split ) {
+    float ims = 0.f;
+    if( s.ing_timed && n ) TX_CHECK( hipEventElapsedTime( &ims, s.ev_ing0, s.ev_ing1 ) );
+    u64 const * hb = (u64 const *)s.h_res;
+    double txnt = 0.0;
+    for( ulong j = 0; j < n; j++ ) txnt += (double)R[j].tsz + 2.0;
+    t->last_ingest[0] = (double)ims;
+    t->last_ingest[1] = (double)n;
+    t->last_ingest[2] = n ? (double)hb[2] + (double)hb[3] + txnt + 104.0 * (double)s.nsig + 34.0 * (double)n : 0.0;
+    t->last_ingest[3] = (double)s.nsig;
+  }
   t->m_sigs += s.nsig;
   t->last_gpu_ms  = gpu_ms;
   t->last_host_ms = std::chrono::duration<double, std::milli>( h1 - h0 ).count();
@@ -908,6 +1489,12 @@ fd_verify_hip_tile_complete( fd_verify_hip_tile_t * t, ulong const * bundle_id, 
   hist_sample( t->hist[1], (ulong)std::chrono::duration_cast<std::chrono::nanoseconds>( h1 - h0 ).count() );
   s.busy = 0; t->completed++;
   return 0;
+}
+
+extern "C" void fd_verify_hip_tile_set_ingest_timing( fd_verify_hip_tile_t * t, int on ) { t->ingest_timing = !!on; }
+
+extern "C" void fd_verify_hip_tile_ingest_stats( fd_verify_hip_tile_t const * t, double out[4] ) {
+  for( int k = 0; k < 4; k++ ) out[k] = t->last_ingest[k];
 }
 
 extern "C" void fd_verify_hip_tile_metrics( fd_verify_hip_tile_t const * t, ulong out[6] ) {

@@ -39,6 +39,7 @@ EXPORTS = (
     "fd_verify_hip_tile_metrics", "fd_verify_hip_tile_metrics2", "fd_verify_hip_tile_last_timing", "fd_verify_hip_tile_submit_frags",
     "fd_verify_hip_before_frag", "fd_verify_hip_hist_edges", "fd_verify_hip_tile_hist_init",
     "fd_verify_hip_tile_hist", "fd_verify_hip_tile_poll", "fd_verify_hip_tile_inflight",
+    "fd_verify_hip_tile_set_ingest_timing", "fd_verify_hip_tile_ingest_stats",
 )
 HIST_BUCKET_CNT = 16
 
@@ -86,6 +87,8 @@ def lib():
         L.fd_verify_hip_tile_metrics.argtypes = [vp, vp]
         L.fd_verify_hip_tile_metrics2.argtypes = [vp, vp]
         L.fd_verify_hip_tile_last_timing.argtypes = [vp, vp]
+        L.fd_verify_hip_tile_set_ingest_timing.argtypes = [vp, c.c_int]
+        L.fd_verify_hip_tile_ingest_stats.argtypes = [vp, vp]
         L.fd_verify_hip_tile_submit_frags.restype = c.c_int
         L.fd_verify_hip_tile_submit_frags.argtypes = [vp, u64, vp, vp, vp, vp, vp, vp]
         L.fd_verify_hip_before_frag.restype = c.c_int
@@ -242,6 +245,17 @@ class VerifyTile:
         out = np.zeros(3, np.float64)
         self._lib.fd_verify_hip_tile_last_timing(self.tile, out.ctypes.data)
         return {"gpu_ms": float(out[0]), "host_ms": float(out[1]), "sigs": int(out[2])}
+
+    def set_ingest_timing(self, on=True):
+        """HIP events around each batch's ingest kernel (k_txnm_batch)."""
+        self._lib.fd_verify_hip_tile_set_ingest_timing(self.tile, int(bool(on)))
+
+    def ingest_stats(self):
+        """Last completed frag batch: ingest kernel ms (timing on), frags,
+        algorithmic bytes (include/fd_verify_hip.h), signature records."""
+        out = np.zeros(4, np.float64)
+        self._lib.fd_verify_hip_tile_ingest_stats(self.tile, out.ctypes.data)
+        return {"ms": float(out[0]), "frags": int(out[1]), "bytes": float(out[2]), "records": int(out[3])}
 
     def hist_init(self, min_ns, max_ns):
         """Reset both batch latency histograms with fd_histf edges over [min_ns, max_ns)."""

@@ -247,6 +247,21 @@ void fd_verify_hip_tile_metrics2( fd_verify_hip_tile_t const * tile, ulong out[ 
    signatures in the batch */
 void fd_verify_hip_tile_last_timing( fd_verify_hip_tile_t const * tile, double out[ 3 ] );
 
+/* Frag-ingest kernel accounting (submit_frags batches; the north star's
+   "achieved HBM GB/s on packet ingest").  set_ingest_timing( tile, 1 )
+   brackets each batch's ingest kernel (k_txnm_batch: copy, parse, record
+   expansion) with HIP events on the tile's stream; ingest_stats then
+   reports, for the last completed batch:
+     out[0] kernel time (ms; 0 when timing is off)
+     out[1] frags
+     out[2] algorithmic bytes: in-frag bytes read + out-frag bytes written
+            (during_frag's copy) + fd_txn_t and txn_t_sz written (after_frag)
+            + signature records written (96 B + 8 B of message span each)
+            + per-frag results (23 B)
+     out[3] signature records */
+void fd_verify_hip_tile_set_ingest_timing( fd_verify_hip_tile_t * tile, int on );
+void fd_verify_hip_tile_ingest_stats     ( fd_verify_hip_tile_t const * tile, double out[ 4 ] );
+
 /* Batch latency histograms (SURVEY: the tile's counters plus GPU batch
    latency), laid out as the reference's fd_histf (src/util/hist/fd_histf.h:
    16 buckets: [0,min), roughly geometric integer edges from min to max, and
