@@ -1077,7 +1077,9 @@ struct fd_verify_hip_tile {
   /* bundle state (fd_verify_ctx_t bundle_failed / bundle_id) */
   int        bundle_failed; ulong bundle_id;
   ulong      m_parse, m_verify, m_dedup, m_bundle, m_pub, m_sigs, m_gossip;
-  tile_slot  slot[2];
+  tile_slot  slot[FD_VERIFY_HIP_INFLIGHT_MAX];
+  ulong      nslot;          /* batches in flight at most: the slot ring (fd_verify_hip_tile_set_inflight; 2) */
+  ulong      nalloc;         /* slots allocated */
   ulong      submitted, completed;
   int        ingest_split;   /* FD_VERIFY_HIP_INGEST=split: the three-kernel frag ingest (A/B runs) */
   int        fb;             /* k_txnm_batch frags per workgroup (FD_VERIFY_HIP_FB: 8 or 16) */
@@ -1135,6 +1137,16 @@ void k_tile_results( ulong n, u16 const * __restrict__ tsz, signed char const * 
                      u32 const * __restrict__ counter, u32 const * __restrict__ flag, u32 n_seg,
                      u8 * __restrict__ res );
 
+/* a slot's record buffers at their bound and the results kernel loaded (a
+   tile is created in privileged_init: its sandboxed steady state allocates
+   nothing and loads no code) */
+static void slot_warm( tile_slot & s, ulong max_txn, hipStream_t st ) {
+  slot_records( s, 12ul*(max_txn + SLOT_SEG_SLACK) );
+  hipLaunchKernelGGL( k_tile_results, dim3( 1 ), dim3( 64 ), 0, st, 0ul, s.d_tsz, s.d_tcode, s.d_tag,
+                      (u64 const *)0, (u8 const *)0, s.d_counter, (u32 const *)0, 0u, s.d_res );
+  TX_CHECK( hipGetLastError() );
+}
+
 extern "C" fd_verify_hip_tile_t *
 fd_verify_hip_tile_new( fd_ed25519_hip_ctx_t * ctx, ulong max_txn, ulong seed, ulong depth, ulong map_cnt ) {
   if( !ctx || !max_txn || !depth ) return 0;
@@ -1153,6 +1165,7 @@ fd_verify_hip_tile_new( fd_ed25519_hip_ctx_t * ctx, ulong max_txn, ulong seed, u
   t->own_mem = (ulong *)malloc( sizeof(ulong)*(depth + map_cnt) );
   t->oldest = &t->own_oldest; t->ring = t->own_mem; t->depth = depth; t->map = t->own_mem + depth; t->map_cnt = map_cnt;
   t->own_oldest = fd_verify_hip_tcache_reset( t->ring, depth, t->map, map_cnt );
+  t->nslot = t->nalloc = 2ul;
   slot_alloc( t->slot[0], max_txn ); slot_alloc( t->slot[1], max_txn );
   fd_verify_hip_tile_hist_init( t, 10000ul, 1000000000ul );   /* 10 us .. 1 s */
   /* Everything the batch path would otherwise do lazily, done now: record
@@ -1162,13 +1175,7 @@ fd_verify_hip_tile_new( fd_ed25519_hip_ctx_t * ctx, ulong max_txn, ulong seed, u
      privileged_init, so its sandboxed steady state needs neither
      (integration/fd_verify_tile_hip.patch, verify_hip_seccomp). */
   hipStream_t st = (hipStream_t)fd_ed25519_hip_ctx_stream( ctx );
-  for( int k = 0; k < 2; k++ ) {
-    slot_records( t->slot[k], 12ul*(max_txn + SLOT_SEG_SLACK) );
-    hipLaunchKernelGGL( k_tile_results, dim3( 1 ), dim3( 64 ), 0, st, 0ul, t->slot[k].d_tsz, t->slot[k].d_tcode,
-                        t->slot[k].d_tag, (u64 const *)0, (u8 const *)0, t->slot[k].d_counter, (u32 const *)0, 0u,
-                        t->slot[k].d_res );
-    TX_CHECK( hipGetLastError() );
-  }
+  for( int k = 0; k < 2; k++ ) slot_warm( t->slot[k], max_txn, st );
   TX_CHECK( hipStreamSynchronize( st ) );
   {
     /* one empty-payload frag through the whole batch path (ingest, parse,
@@ -1230,7 +1237,7 @@ extern "C" void fd_verify_hip_tile_delete( fd_verify_hip_tile_t * t ) {
   if( !t ) return;
   (void)hipSetDevice( fd_ed25519_hip_ctx_device( t->ctx ) );
   (void)hipStreamSynchronize( (hipStream_t)fd_ed25519_hip_ctx_stream( t->ctx ) );
-  slot_free( t->slot[0] ); slot_free( t->slot[1] );
+  for( ulong k = 0; k < t->nalloc; k++ ) slot_free( t->slot[k] );
   free( t->own_mem ); free( t );
 }
 
@@ -1303,7 +1310,7 @@ static tile_slot *
 submit_begin( fd_verify_hip_tile_t * t, ulong n, hipStream_t & st, int & rc ) {
   rc = 0;
   if( n > t->max_txn ) { rc = -1; return 0; }
-  tile_slot & s = t->slot[t->submitted & 1];
+  tile_slot & s = t->slot[t->submitted % t->nslot];
   if( s.busy ) { rc = -2; return 0; }                        /* two batches outstanding */
   st = (hipStream_t)fd_ed25519_hip_ctx_stream( t->ctx );
   TX_CHECK( hipSetDevice( fd_ed25519_hip_ctx_device( t->ctx ) ) );
@@ -1393,7 +1400,7 @@ fd_verify_hip_tile_submit_frags( fd_verify_hip_tile_t * t, ulong n, uchar const 
 extern "C" int
 fd_verify_hip_tile_poll( fd_verify_hip_tile_t const * t ) {
   if( t->completed == t->submitted ) return -1;
-  tile_slot const & s = t->slot[t->completed & 1];
+  tile_slot const & s = t->slot[t->completed % t->nslot];
   TX_CHECK( hipSetDevice( fd_ed25519_hip_ctx_device( t->ctx ) ) );
   hipError_t e = hipEventQuery( s.ev_done );
   if( e == hipErrorNotReady ) return 0;
@@ -1405,10 +1412,23 @@ extern "C" ulong
 fd_verify_hip_tile_inflight( fd_verify_hip_tile_t const * t ) { return t->submitted - t->completed; }
 
 extern "C" int
+fd_verify_hip_tile_set_inflight( fd_verify_hip_tile_t * t, ulong k ) {
+  if( k < 1ul || k > FD_VERIFY_HIP_INFLIGHT_MAX || t->submitted != t->completed ) return -1;
+  TX_CHECK( hipSetDevice( fd_ed25519_hip_ctx_device( t->ctx ) ) );
+  hipStream_t st = (hipStream_t)fd_ed25519_hip_ctx_stream( t->ctx );
+  for( ulong j = t->nalloc; j < k; j++ ) { slot_alloc( t->slot[j], t->max_txn ); slot_warm( t->slot[j], t->max_txn, st ); }
+  TX_CHECK( hipStreamSynchronize( st ) );
+  if( k > t->nalloc ) t->nalloc = k;
+  t->nslot = k;
+  t->submitted = t->completed = 0;                        /* batch b takes slot b % nslot */
+  return 0;
+}
+
+extern "C" int
 fd_verify_hip_tile_complete( fd_verify_hip_tile_t * t, ulong const * bundle_id, signed char * result,
                              ulong * tag_out, ushort * txn_t_sz ) {
   if( t->completed == t->submitted ) return -1;
-  tile_slot & s = t->slot[t->completed & 1];
+  tile_slot & s = t->slot[t->completed % t->nslot];
   TX_CHECK( hipSetDevice( fd_ed25519_hip_ctx_device( t->ctx ) ) );
   TX_CHECK( hipEventSynchronize( s.ev_done ) );
   u32 const * hdr = (u32 const *)s.h_res;

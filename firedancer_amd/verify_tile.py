@@ -39,7 +39,7 @@ EXPORTS = (
     "fd_verify_hip_tile_metrics", "fd_verify_hip_tile_metrics2", "fd_verify_hip_tile_last_timing", "fd_verify_hip_tile_submit_frags",
     "fd_verify_hip_before_frag", "fd_verify_hip_hist_edges", "fd_verify_hip_tile_hist_init",
     "fd_verify_hip_tile_hist", "fd_verify_hip_tile_poll", "fd_verify_hip_tile_inflight",
-    "fd_verify_hip_tile_set_ingest_timing", "fd_verify_hip_tile_ingest_stats",
+    "fd_verify_hip_tile_set_ingest_timing", "fd_verify_hip_tile_ingest_stats", "fd_verify_hip_tile_set_inflight",
 )
 HIST_BUCKET_CNT = 16
 
@@ -89,6 +89,8 @@ def lib():
         L.fd_verify_hip_tile_last_timing.argtypes = [vp, vp]
         L.fd_verify_hip_tile_set_ingest_timing.argtypes = [vp, c.c_int]
         L.fd_verify_hip_tile_ingest_stats.argtypes = [vp, vp]
+        L.fd_verify_hip_tile_set_inflight.restype = c.c_int
+        L.fd_verify_hip_tile_set_inflight.argtypes = [vp, u64]
         L.fd_verify_hip_tile_submit_frags.restype = c.c_int
         L.fd_verify_hip_tile_submit_frags.argtypes = [vp, u64, vp, vp, vp, vp, vp, vp]
         L.fd_verify_hip_before_frag.restype = c.c_int
@@ -245,6 +247,11 @@ class VerifyTile:
         out = np.zeros(3, np.float64)
         self._lib.fd_verify_hip_tile_last_timing(self.tile, out.ctypes.data)
         return {"gpu_ms": float(out[0]), "host_ms": float(out[1]), "sigs": int(out[2])}
+
+    def set_inflight(self, k):
+        """Batches kept on the GPU at once (1..4; 2 for a new tile)."""
+        if self._lib.fd_verify_hip_tile_set_inflight(self.tile, int(k)):
+            raise ValueError("set_inflight: k out of range or batches outstanding")
 
     def set_ingest_timing(self, on=True):
         """HIP events around each batch's ingest kernel (k_txnm_batch)."""

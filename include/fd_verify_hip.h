@@ -226,6 +226,14 @@ fd_verify_hip_tile_poll( fd_verify_hip_tile_t const * tile );
 ulong
 fd_verify_hip_tile_inflight( fd_verify_hip_tile_t const * tile );
 
+/* Batches the tile keeps on the GPU at once (1..FD_VERIFY_HIP_INFLIGHT_MAX;
+   2 for a new tile): submit returns -2 while that many are outstanding.
+   Allocates and warms the extra batch slots (call from privileged_init).
+   -1 if k is out of range or batches are outstanding. */
+#define FD_VERIFY_HIP_INFLIGHT_MAX 4
+int
+fd_verify_hip_tile_set_inflight( fd_verify_hip_tile_t * tile, ulong k );
+
 int
 fd_verify_hip_tile_complete( fd_verify_hip_tile_t * tile,
                              ulong const *          bundle_id,   /* host, n entries or NULL */

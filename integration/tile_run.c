@@ -1,0 +1,350 @@
+/* tile_run.c -- the reference's verify tile with integration/fd_verify_tile_hip.patch
+   applied, run and timed in the reference's own run loop.
+
+   Not test infrastructure: this is the north star's operating point, the
+   unchanged tile (src/disco/verify/fd_verify_tile.c + the patch) handing its
+   frags to the engine.  Built by integration/Makefile from the reference's
+   sources where they lie (no copies) against firedancer_amd/libfd_ed25519_hip.so;
+   driven by tools/tile_bench.py.
+
+   The topology is the reference's quic -> verify fan-out
+   (src/app/fdctl/topology.c:90,173): ONE quic_verify link that every verify
+   tile polls, each tile taking seq % tile_cnt == kind_id (before_frag,
+   fd_verify_tile.c:37-58), each with its own verify_dedup out link.
+
+     tile_run produce <shm> <stream.bin> <tile_cnt> <in_depth>
+         The quic side: creates <shm> (a file in /dev/shm), lays every frag
+         of the stream into the quic_verify dcache as fd_txn_m_t frags (the
+         copy the quic tile would have made), prints READY, waits for the
+         tiles, then publishes the frags' mcache lines in seq order, never
+         more than in_depth - 64 ahead of the slowest tile's fseq (the
+         reference link is unreliable and would drop frags past its depth; a
+         throughput bench must not), and prints one JSON line once every
+         tile is done.
+     tile_run tile <shm> <tile_idx>
+         Verify tile tile_idx: the mock topology around the shared in link
+         (tile_drv.c's shape, src/disco/verify/test_verify_tile.c:45-85),
+         privileged_init (HIP context, GPU tile_idx % device count),
+         unprivileged_init, then stem_run1 (src/disco/stem/fd_stem.c) with
+         the patched callbacks until its share of the stream is published
+         or dropped and nothing is left on the GPU.
+
+   Stream file: "FDT1" u64 n, u64 seed, u64 tcache_depth, per frag u64
+   bundle_id, u16 payload_sz, payload bytes (oracle/tile_drv.c's format). */
+
+#define FD_TILE_TEST
+static int drv_should_shutdown( void * ctx );
+#define STEM_CALLBACK_SHOULD_SHUTDOWN( ctx ) drv_should_shutdown( ctx )
+#include TILE_SRC
+#include "../topo/fd_topob.h"
+#include "../metrics/fd_metrics.h"
+#include "../../tango/fseq/fd_fseq.h"
+#include "../../tango/tempo/fd_tempo.h"
+#include "../quic/fd_tpu.h"
+#include <errno.h>
+#include <fcntl.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <sys/mman.h>
+#include <unistd.h>
+
+#if !FD_HAS_HIP
+#error "tile_run drives the patched tile (FD_HAS_HIP)"
+#endif
+
+#if defined(fd_boot)                         /* integration/Makefile renames fd_boot / fd_halt (tile_drv.c) */
+void fd_boot( int * pargc, char *** pargv ) { (void)pargc; (void)pargv; }
+void fd_halt( void ) {}
+#endif
+
+#define RUN_MAGIC     (0xfd7111e5a11ce5ULL)
+#define RUN_TILE_MAX  (16UL)
+#define RUN_OUT_DEPTH (65536UL)              /* verify_dedup mcache: >= FD_VERIFY_HIP_STEM_BURST */
+
+typedef struct {
+  volatile long t_ready, t_end;
+  volatile ulong done, frags, sigs, pub, parse, verify, dedup, bundle;
+  volatile ulong batches;
+  volatile double gpu_ms, host_ms;           /* sums over the tile's batches (fd_verify_hip_tile_hist sums) */
+} run_res_t;
+
+typedef struct {
+  ulong magic;
+  ulong n, tile_cnt, seed, tcache_depth, in_depth;
+  ulong mcache_off, dcache_off, fseq_off;    /* tile t's fseq at fseq_off + t*fseq_stride */
+  ulong fseq_stride, dcache_data_sz, map_sz;
+  volatile ulong ready, start;
+  volatile long  t0;
+  run_res_t res[ RUN_TILE_MAX ];
+} run_hdr_t;
+
+static void * drv_map( char const * path, ulong sz, int create ) {
+  int fd = open( path, create ? (O_RDWR|O_CREAT|O_EXCL) : O_RDWR, 0600 );
+  if( fd<0 ) FD_LOG_ERR(( "open(%s) failed (%i-%s)", path, errno, fd_io_strerror( errno ) ));
+  if( create && ftruncate( fd, (off_t)sz ) ) FD_LOG_ERR(( "ftruncate failed" ));
+  if( !create ) {
+    run_hdr_t h;
+    if( pread( fd, &h, sizeof(h), 0 )!=(long)sizeof(h) || h.magic!=RUN_MAGIC ) FD_LOG_ERR(( "%s: not a tile_run segment", path ));
+    sz = h.map_sz;
+  }
+  void * p = mmap( NULL, sz, PROT_READ|PROT_WRITE, MAP_SHARED, fd, 0 );
+  if( p==MAP_FAILED ) FD_LOG_ERR(( "mmap failed (%i-%s)", errno, fd_io_strerror( errno ) ));
+  close( fd );
+  return p;
+}
+
+static uchar * read_all( char const * path, ulong * sz ) {
+  FILE * f = fopen( path, "rb" ); FD_TEST( f );
+  fseek( f, 0, SEEK_END ); long n = ftell( f ); fseek( f, 0, SEEK_SET );
+  uchar * b = malloc( (ulong)n ); FD_TEST( b );
+  FD_TEST( fread( b, 1, (ulong)n, f )==(ulong)n );
+  fclose( f );
+  *sz = (ulong)n;
+  return b;
+}
+
+/* ---- produce ------------------------------------------------------------ */
+
+static int
+produce( char const * path, char const * stream, ulong tile_cnt, ulong in_depth ) {
+  FD_TEST( tile_cnt>=1UL && tile_cnt<=RUN_TILE_MAX && fd_ulong_is_pow2( in_depth ) );
+  ulong in_sz; uchar * in = read_all( stream, &in_sz );
+  FD_TEST( in_sz>=28UL && !memcmp( in, "FDT1", 4 ) );
+  ulong n, seed, depth;
+  memcpy( &n, in+4, 8 ); memcpy( &seed, in+12, 8 ); memcpy( &depth, in+20, 8 );
+
+  /* frag layout: fd_txn_m_t header + payload, chunk-aligned, back to back */
+  ulong * chunk_rel = malloc( n*sizeof(ulong) ); ushort * fsz = malloc( n*sizeof(ushort) );
+  ulong * poff = malloc( n*sizeof(ulong) );
+  FD_TEST( chunk_rel && fsz && poff );
+  ulong off = 28UL, data = 0UL;
+  for( ulong j=0UL; j<n; j++ ) {
+    ushort psz; memcpy( &psz, in+off+8, 2 );
+    poff[ j ] = off; off += 10UL + psz;
+    FD_TEST( off<=in_sz && psz<=FD_TPU_MTU );
+    fsz[ j ] = (ushort)( sizeof(fd_txn_m_t) + psz );
+    chunk_rel[ j ] = data >> FD_CHUNK_LG_SZ;
+    data += fd_ulong_align_up( fsz[ j ], FD_CHUNK_SZ );
+  }
+  ulong data_sz = data + FD_TPU_REASM_MTU + FD_CHUNK_SZ;         /* the wmark leaves an MTU past the last frag */
+  ulong mc_off  = fd_ulong_align_up( sizeof(run_hdr_t), fd_mcache_align() );
+  ulong fs_off  = fd_ulong_align_up( mc_off + fd_mcache_footprint( in_depth, 0UL ), fd_fseq_align() );
+  ulong fs_strd = fd_ulong_align_up( fd_fseq_footprint(), 128UL );
+  ulong dc_off  = fd_ulong_align_up( fs_off + tile_cnt*fs_strd, fd_dcache_align() );
+  ulong map_sz  = fd_ulong_align_up( dc_off + fd_dcache_footprint( data_sz, 0UL ), 4096UL );
+
+  uchar * base = drv_map( path, map_sz, 1 );
+  run_hdr_t * hdr = (run_hdr_t *)base;
+  memset( hdr, 0, sizeof(run_hdr_t) );
+  fd_frag_meta_t * mcache = fd_mcache_join( fd_mcache_new( base + mc_off, in_depth, 0UL, 0UL ) );
+  for( ulong t=0UL; t<tile_cnt; t++ ) FD_TEST( fd_fseq_join( fd_fseq_new( base + fs_off + t*fs_strd, 0UL ) ) );
+  uchar * dcache = fd_dcache_join( fd_dcache_new( base + dc_off, data_sz, 0UL ) );
+  FD_TEST( mcache && dcache );
+  ulong chunk0 = fd_dcache_compact_chunk0( base, dcache );
+  for( ulong j=0UL; j<n; j++ ) {
+    fd_txn_m_t * m = (fd_txn_m_t *)fd_chunk_to_laddr( base, chunk0 + chunk_rel[ j ] );
+    memset( m, 0, sizeof(fd_txn_m_t) );
+    memcpy( &m->block_engine.bundle_id, in+poff[ j ], 8 );
+    m->payload_sz = (ushort)( fsz[ j ] - sizeof(fd_txn_m_t) );
+    memcpy( fd_txn_m_payload( m ), in+poff[ j ]+10UL, m->payload_sz );
+  }
+  hdr->n = n; hdr->tile_cnt = tile_cnt; hdr->seed = seed; hdr->tcache_depth = depth; hdr->in_depth = in_depth;
+  hdr->mcache_off = mc_off; hdr->dcache_off = dc_off; hdr->fseq_off = fs_off; hdr->fseq_stride = fs_strd;
+  hdr->dcache_data_sz = data_sz; hdr->map_sz = map_sz;
+  FD_COMPILER_MFENCE();
+  hdr->magic = RUN_MAGIC;
+  FD_COMPILER_MFENCE();
+  printf( "READY\n" ); fflush( stdout );
+
+  for( long tw=fd_log_wallclock(); hdr->ready<tile_cnt; FD_SPIN_PAUSE() )
+    if( fd_log_wallclock()-tw > 300L*1000000000L ) FD_LOG_ERR(( "tiles not ready after 300 s (%lu of %lu)", hdr->ready, tile_cnt ));
+
+  ulong const * fseq[ RUN_TILE_MAX ];
+  for( ulong t=0UL; t<tile_cnt; t++ ) fseq[ t ] = fd_fseq_join( base + fs_off + t*fs_strd );
+  long t0 = fd_log_wallclock();
+  hdr->t0 = t0;
+  FD_COMPILER_MFENCE();
+  hdr->start = 1UL;
+  ulong ctl = fd_frag_meta_ctl( 0UL, 1, 1, 0 );
+  ulong lim = 0UL;
+  for( ulong seq=0UL; seq<n; seq++ ) {
+    while( seq>=lim ) {                                        /* flow control against the slowest tile */
+      ulong m = ULONG_MAX;
+      for( ulong t=0UL; t<tile_cnt; t++ ) m = fd_ulong_min( m, fd_fseq_query( fseq[ t ] ) );
+      lim = m + in_depth - 64UL;
+      if( seq>=lim ) FD_SPIN_PAUSE();
+      if( fd_log_wallclock()-t0 > 600L*1000000000L ) FD_LOG_ERR(( "tiles stalled at seq %lu", seq ));
+    }
+    ulong ts = (ulong)fd_frag_meta_ts_comp( fd_tickcount() );
+    fd_mcache_publish( mcache, in_depth, seq, 0UL, chunk0 + chunk_rel[ seq ], fsz[ seq ], ctl, ts, ts );
+  }
+  long t_pub = fd_log_wallclock();
+  ulong done = 0UL;
+  while( done<tile_cnt ) {
+    done = 0UL;
+    for( ulong t=0UL; t<tile_cnt; t++ ) done += hdr->res[ t ].done;
+    if( fd_log_wallclock()-t0 > 900L*1000000000L ) FD_LOG_ERR(( "tiles not done after 900 s" ));
+    FD_SPIN_PAUSE();
+  }
+  long t_end = t0; ulong sigs = 0UL, frags = 0UL, pub = 0UL, batches = 0UL;
+  ulong parse = 0UL, verify = 0UL, dedup = 0UL, bundle = 0UL; double gpu_ms = 0.0, host_ms = 0.0;
+  printf( "{\"tiles\": [" );
+  for( ulong t=0UL; t<tile_cnt; t++ ) {
+    run_res_t * r = &hdr->res[ t ];
+    t_end = fd_long_max( t_end, r->t_end );
+    sigs += r->sigs; frags += r->frags; pub += r->pub; batches += r->batches;
+    parse += r->parse; verify += r->verify; dedup += r->dedup; bundle += r->bundle;
+    gpu_ms += r->gpu_ms; host_ms += r->host_ms;
+    printf( "%s{\"frags\": %lu, \"sigs\": %lu, \"published\": %lu, \"batches\": %lu, \"s\": %.6f, "
+            "\"gpu_ms_per_batch\": %.4f, \"host_ms_per_batch\": %.4f}", t ? ", " : "", r->frags, r->sigs, r->pub,
+            r->batches, (double)( r->t_end - t0 )*1e-9, r->batches ? r->gpu_ms/(double)r->batches : 0.0,
+            r->batches ? r->host_ms/(double)r->batches : 0.0 );
+  }
+  double s = (double)( t_end - t0 )*1e-9;
+  printf( "], \"frags\": %lu, \"sigs\": %lu, \"published\": %lu, \"parse_fail\": %lu, \"verify_fail\": %lu, "
+          "\"dedup\": %lu, \"bundle_peer_fail\": %lu, \"seconds\": %.6f, \"publish_s\": %.6f, "
+          "\"verifies_per_s\": %.1f, \"frags_per_s\": %.1f, \"batches\": %lu, \"gpu_ms_per_batch\": %.4f, "
+          "\"host_ms_per_batch\": %.4f, \"batch_max\": %lu, \"batch_cap\": %lu, \"inflight\": %lu, "
+          "\"flush_ns\": %ld, \"in_depth\": %lu, \"tile_cnt\": %lu}\n",
+          frags, sigs, pub, parse, verify, dedup, bundle, s, (double)( t_pub - t0 )*1e-9, (double)sigs/s,
+          (double)frags/s, batches, batches ? gpu_ms/(double)batches : 0.0, batches ? host_ms/(double)batches : 0.0,
+          FD_VERIFY_HIP_BATCH_MAX, FD_VERIFY_HIP_BATCH_CAP, FD_VERIFY_HIP_INFLIGHT, (long)FD_VERIFY_HIP_FLUSH_NS,
+          in_depth, tile_cnt );
+  fflush( stdout );
+  munmap( base, map_sz );
+  unlink( path );
+  free( in ); free( chunk_rel ); free( fsz ); free( poff );
+  return 0;
+}
+
+/* ---- tile --------------------------------------------------------------- */
+
+static uchar * drv_arena;
+static ulong   drv_arena_sz, drv_arena_used;
+
+static void *
+drv_malloc( ulong align, ulong sz ) {
+  ulong off = fd_ulong_align_up( drv_arena_used, align );
+  FD_TEST( off+sz<=drv_arena_sz );
+  drv_arena_used = off + sz;
+  return drv_arena + off;
+}
+
+static fd_verify_ctx_t * drv_ctx;
+static ulong             drv_share;           /* frags of the stream this tile takes */
+static long              drv_deadline;
+
+static int
+drv_should_shutdown( void * _ctx ) {
+  static ulong calls;                                           /* every stem iteration: look every 64th */
+  if( FD_LIKELY( (++calls) & 63UL ) ) return 0;
+  fd_verify_ctx_t * ctx = (fd_verify_ctx_t *)_ctx;
+  ulong m[ 6 ];
+  fd_verify_hip_tile_metrics( ctx->hip_tile, m );
+  ulong seen = m[0] + m[1] + m[2] + m[3] + m[4];            /* parse, verify, dedup, bundle failures, published */
+  if( FD_UNLIKELY( fd_log_wallclock()>drv_deadline ) ) FD_LOG_ERR(( "tile: %lu of %lu frags after the deadline", seen, drv_share ));
+  return seen>=drv_share && FD_VERIFY_HIP_IDLE( ctx );
+}
+
+static int
+tile( char const * path, ulong t ) {
+  uchar * base = drv_map( path, 0UL, 0 );
+  run_hdr_t * hdr = (run_hdr_t *)base;
+  FD_TEST( t<hdr->tile_cnt );
+  ulong in_depth = hdr->in_depth;
+
+  fd_topo_t * topo = fd_topob_new( aligned_alloc( alignof(fd_topo_t), fd_ulong_align_up( sizeof(fd_topo_t), alignof(fd_topo_t) ) ),
+                                   "verify-run" );
+  fd_topo_wksp_t * qw = fd_topob_wksp( topo, "quic_verify" );   /* the shared segment */
+  fd_topo_wksp_t * tw = fd_topob_wksp( topo, "verify" );        /* this tile's own memory */
+  fd_topo_tile_t * tile = fd_topob_tile( topo, "verify", "verify", "verify", 0UL, 0, 0 );
+  tile->kind_id = t;                                            /* GPU t % devices; round robin index */
+  tile->verify.tcache_depth = hdr->tcache_depth;
+  ulong out_data = fd_dcache_req_data_sz( FD_TPU_PARSED_MTU, RUN_OUT_DEPTH, FD_VERIFY_HIP_STEM_BURST, 1 );
+  drv_arena_sz = 4096UL + scratch_footprint( tile ) + scratch_align() + fd_mcache_footprint( RUN_OUT_DEPTH, 0UL ) +
+                 fd_dcache_footprint( out_data, 0UL ) + fd_mcache_align() + fd_dcache_align() + 4096UL;
+  drv_arena = aligned_alloc( 4096UL, fd_ulong_align_up( drv_arena_sz, 4096UL ) );
+  FD_TEST( drv_arena );
+  memset( drv_arena, 0, drv_arena_sz );
+  drv_arena_used = 4096UL;
+  qw->wksp = (fd_wksp_t *)base;
+  tw->wksp = (fd_wksp_t *)drv_arena;
+  void * scratch = drv_malloc( scratch_align(), scratch_footprint( tile ) );
+  topo->objs[ tile->tile_obj_id ].offset = (ulong)scratch - (ulong)drv_arena;
+
+  fd_topo_link_t * quic = fd_topob_link( topo, "quic_verify", "quic_verify", in_depth, FD_TPU_REASM_MTU, 1UL );
+  quic->mcache = fd_mcache_join( base + hdr->mcache_off );
+  quic->dcache = fd_dcache_join( base + hdr->dcache_off );
+  fd_topo_link_t * out = fd_topob_link( topo, "verify_dedup", "verify", RUN_OUT_DEPTH, FD_TPU_PARSED_MTU,
+                                        FD_VERIFY_HIP_STEM_BURST );
+  out->mcache = fd_mcache_join( fd_mcache_new( drv_malloc( fd_mcache_align(), fd_mcache_footprint( RUN_OUT_DEPTH, 0UL ) ),
+                                               RUN_OUT_DEPTH, 0UL, 0UL ) );
+  out->dcache = fd_dcache_join( fd_dcache_new( drv_malloc( fd_dcache_align(), fd_dcache_footprint( out_data, 0UL ) ),
+                                               out_data, 0UL ) );
+  FD_TEST( quic->mcache && quic->dcache && out->mcache && out->dcache );
+  fd_topob_tile_in ( topo, "verify", 0UL, "verify", "quic_verify", 0UL, FD_TOPOB_UNRELIABLE, FD_TOPOB_POLLED );
+  fd_topob_tile_out( topo, "verify", 0UL, "verify_dedup", 0UL );
+  tile->kind_id = t;
+  quic->mtu = FD_TPU_REASM_MTU; out->mtu = FD_TPU_PARSED_MTU;
+
+  privileged_init( topo, tile );
+  fd_verify_ctx_t * ctx = (fd_verify_ctx_t *)scratch;
+  ctx->hashmap_seed = hdr->seed + t;                            /* fixed per tile: runs are reproducible */
+  unprivileged_init( topo, tile );
+  ctx->round_robin_cnt = hdr->tile_cnt; ctx->round_robin_idx = t;
+  drv_ctx   = ctx;
+  drv_share = hdr->n/hdr->tile_cnt + (t<hdr->n%hdr->tile_cnt ? 1UL : 0UL);
+
+  /* the stem's run loop state (fd_stem.c:207-394): metrics, scratch, the
+     in link's fseq in the shared segment (the producer's flow control), a
+     consumer of the out link that returns every credit (STEM_SHUTDOWN_SEQ) */
+  ulong * metrics = aligned_alloc( FD_METRICS_ALIGN, fd_ulong_align_up( FD_METRICS_FOOTPRINT( 1UL, 1UL ), FD_METRICS_ALIGN ) );
+  fd_metrics_register( fd_metrics_new( metrics, 1UL, 1UL ) );
+  void * stem_scratch = aligned_alloc( FD_STEM_SCRATCH_ALIGN,
+                                       fd_ulong_align_up( stem_scratch_footprint( 1UL, 1UL, 1UL ), FD_STEM_SCRATCH_ALIGN ) );
+  ulong * in_fseq = fd_fseq_join( base + hdr->fseq_off + t*hdr->fseq_stride );
+  uchar cons_mem[ 256 ] __attribute__((aligned(128)));
+  FD_TEST( fd_fseq_footprint()<=sizeof(cons_mem) );
+  ulong * cons_fseq = fd_fseq_join( fd_fseq_new( cons_mem, STEM_SHUTDOWN_SEQ ) );
+  fd_rng_t rng_mem[ 1 ];
+  fd_rng_t * rng = fd_rng_join( fd_rng_new( rng_mem, (uint)(hdr->seed + t), 0UL ) );
+  fd_frag_meta_t const * in_mcache[ 1 ] = { quic->mcache };
+  ulong *                in_fseqs [ 1 ] = { in_fseq };
+  fd_frag_meta_t *       out_mcache[ 1 ] = { out->mcache };
+  ulong                  cons_out[ 1 ] = { 0UL };
+  ulong *                cons_fseqs[ 1 ] = { cons_fseq };
+  (void)fd_tempo_tick_per_ns( NULL );                           /* calibrate before the clock starts */
+
+  hdr->res[ t ].t_ready = fd_log_wallclock();
+  __atomic_fetch_add( &hdr->ready, 1UL, __ATOMIC_SEQ_CST );
+  while( !hdr->start ) FD_SPIN_PAUSE();
+  drv_deadline = fd_log_wallclock() + 600L*1000000000L;
+  stem_run1( 1UL, in_mcache, in_fseqs, 1UL, out_mcache, 1UL, cons_out, cons_fseqs, FD_VERIFY_HIP_STEM_BURST, 0L, rng,
+             stem_scratch, ctx );
+  long t_end = fd_log_wallclock();
+
+  ulong m[ 6 ];
+  fd_verify_hip_tile_metrics( ctx->hip_tile, m );
+  ulong cnt[ 16 ], sum_gpu = 0UL, sum_host = 0UL, nb = 0UL;
+  fd_verify_hip_tile_hist( ctx->hip_tile, 0, cnt, NULL, &sum_gpu );
+  for( ulong k=0UL; k<16UL; k++ ) nb += cnt[ k ];
+  fd_verify_hip_tile_hist( ctx->hip_tile, 1, NULL, NULL, &sum_host );
+  run_res_t * r = &hdr->res[ t ];
+  r->t_end = t_end; r->frags = m[0] + m[1] + m[2] + m[3] + m[4]; r->sigs = m[5]; r->pub = m[4];
+  r->parse = m[0]; r->verify = m[1]; r->dedup = m[2]; r->bundle = m[3];
+  r->batches = nb; r->gpu_ms = (double)sum_gpu*1e-6; r->host_ms = (double)sum_host*1e-6;
+  FD_COMPILER_MFENCE();
+  r->done = 1UL;
+  return 0;
+}
+
+int
+main( int argc, char ** argv ) {
+  fd_boot( &argc, &argv );
+  if( argc>=6 && !strcmp( argv[1], "produce" ) )
+    return produce( argv[2], argv[3], strtoul( argv[4], NULL, 0 ), strtoul( argv[5], NULL, 0 ) );
+  if( argc>=4 && !strcmp( argv[1], "tile" ) )
+    return tile( argv[2], strtoul( argv[3], NULL, 0 ) );
+  fprintf( stderr, "usage: %s produce <shm> <stream.bin> <tile_cnt> <in_depth> | tile <shm> <tile_idx>\n", argv[0] );
+  return 2;
+}

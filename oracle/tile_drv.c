@@ -173,8 +173,8 @@ main( int argc, char ** argv ) {
     struct sigaction sa; memset( &sa, 0, sizeof(sa) );
     sa.sa_sigaction = drv_sigsys; sa.sa_flags = SA_SIGINFO;
     FD_TEST( !sigaction( SIGSYS, &sa, NULL ) );
-    struct sock_filter filter[ 64 ];
-    ulong cnt = verify_hip_seccomp( 64UL, filter, (uint)out_fd );
+    struct sock_filter filter[ 128 ];
+    ulong cnt = verify_hip_seccomp( 128UL, filter, (uint)out_fd, ctx->hip_fd, ctx->hip_fd_cnt );
     struct sock_fprog prog = { .len = (ushort)cnt, .filter = filter };
     FD_TEST( !prctl( PR_SET_NO_NEW_PRIVS, 1, 0, 0, 0 ) );
     FD_TEST( !syscall( SYS_seccomp, SECCOMP_SET_MODE_FILTER, 0, &prog ) );

@@ -1,0 +1,133 @@
+#!/usr/bin/env python3
+"""Time the reference's verify tile patched to use the engine (north star's
+operating point), in the reference's own stem loop, on one GPU.
+
+For each configuration: one producer process (integration/_build/tile_run
+produce: the quic side of the quic_verify link, frags pre-laid in its dcache,
+mcache lines published with flow control) and T verify tile processes
+(tile_run tile: fd_verify_tile.c + integration/fd_verify_tile_hip.patch,
+privileged_init / unprivileged_init / stem_run1), each taking seq % T as the
+reference's verify tiles do.  The tiles are processes, not threads, as in the
+reference; each has its own HIP context and hardware queues.
+
+value = signatures the tiles' GPU batches verified / (last tile done - first
+frag published).  Also reported per configuration: frags/s, per-batch GPU and
+host-pass times, outcome counts (parse / verify / dedup failures, published).
+
+The stream is config C4's generator (firedancer_amd/txn_workload.py, GPU
+signer), --frags frags.  Binaries per (batch_max, inflight) setting are built
+here (integration/Makefile, needs /root/reference) and travel to the GPU box.
+
+usage: python tools/tile_bench.py [--frags N] [--tiles 4,6,8] [--configs b4096i2,b8192i3 ...]
+       python tools/tile_bench.py --build          (build the sweep's binaries; CPU side)
+Prints one JSON line per run and a final summary line."""
+import argparse
+import json
+import os
+import subprocess
+import sys
+import tempfile
+import time
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+sys.path.insert(0, os.path.join(REPO, "tests"))
+BUILD = os.path.join(REPO, "integration", "_build")
+SWEEP = [(b, i) for b in (1024, 2048, 4096, 8192) for i in (2, 3, 4)]
+
+
+def binary(b, i):
+    return os.path.join(BUILD, f"tile_run_b{b}i{i}")
+
+
+def build():
+    for b, i in SWEEP:
+        subprocess.check_call(["make", "-s", "-C", os.path.join(REPO, "integration"), f"VARIANT=_b{b}i{i}",
+                               f"DEFS=-DFD_VERIFY_HIP_BATCH_MAX={b}UL -DFD_VERIFY_HIP_INFLIGHT={i}UL",
+                               f"_build/tile_run_b{b}i{i}"])
+        print(binary(b, i))
+
+
+def make_stream(n, path, seed=0x5eed0004, depth=4194302):
+    import torch  # noqa: F401
+    from firedancer_amd import Verifier
+    from firedancer_amd.txn_workload import gpu_signer, make_txn_stream
+    from tile_io import write_fdt1
+    v = Verifier(device=0, chunk_sigs=1 << 20)
+    s = make_txn_stream(n, gpu_signer(v), seed=seed)
+    v.close()
+    write_fdt1(path, s.pool, s.off, s.sz, np.zeros(s.n, np.uint64), 0x7f4a11, depth)
+    return s
+
+
+def run_one(exe, stream, tiles, in_depth, timeout):
+    shm = f"/dev/shm/fd_tile_bench_{os.getpid()}"
+    if os.path.exists(shm):
+        os.unlink(shm)
+    prod = subprocess.Popen([exe, "produce", shm, stream, str(tiles), str(in_depth)], stdout=subprocess.PIPE,
+                            stderr=subprocess.PIPE, text=True)
+    procs = []
+    try:
+        line = prod.stdout.readline()
+        if line.strip() != "READY":
+            raise RuntimeError(f"producer: {line!r} {prod.stderr.read()[-2000:]}")
+        procs = [subprocess.Popen([exe, "tile", shm, str(t)], stdout=subprocess.DEVNULL, stderr=subprocess.PIPE,
+                                  text=True) for t in range(tiles)]
+        out, err = prod.communicate(timeout=timeout)
+        if prod.returncode:
+            raise RuntimeError(f"producer rc {prod.returncode}: {err[-2000:]}")
+        for p in procs:
+            p.wait(timeout=60)
+            if p.returncode:
+                raise RuntimeError(f"tile rc {p.returncode}: {p.stderr.read()[-2000:]}")
+        return json.loads(out.strip().splitlines()[-1])
+    finally:
+        for p in procs + [prod]:
+            if p.poll() is None:
+                p.kill()
+                p.wait()
+        if os.path.exists(shm):
+            os.unlink(shm)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--build", action="store_true")
+    ap.add_argument("--frags", type=int, default=1 << 21)
+    ap.add_argument("--tiles", default="6")
+    ap.add_argument("--configs", default="b4096i2")
+    ap.add_argument("--in-depth", type=int, default=16384,
+                    help="quic_verify mcache depth (config tiles.verify.receive_buffer_size, default.toml:1153)")
+    ap.add_argument("--repeat", type=int, default=1)
+    ap.add_argument("--timeout", type=float, default=300)
+    args = ap.parse_args()
+    if args.build:
+        build()
+        return
+    with tempfile.TemporaryDirectory() as td:
+        stream = os.path.join(td, "stream.bin")
+        t = time.time()
+        s = make_stream(args.frags, stream)
+        print(f"stream: {s.n} frags, {s.n_records} signatures, {time.time() - t:.1f} s", file=sys.stderr)
+        best = None
+        for cfg in args.configs.split(","):
+            b, i = cfg[1:].split("i")
+            exe = binary(int(b), int(i))
+            for tiles in (int(x) for x in args.tiles.split(",")):
+                for r in range(args.repeat):
+                    res = run_one(exe, stream, tiles, args.in_depth, args.timeout)
+                    res["config"] = cfg
+                    print(json.dumps(res), flush=True)
+                    if best is None or res["verifies_per_s"] > best["verifies_per_s"]:
+                        best = res
+        print(json.dumps({"metric": "ed25519 verifies/sec through the patched reference verify tile (stem_run1, "
+                                    "one GPU)", "value": best["verifies_per_s"], "unit": "verifies/s",
+                          "config": best["config"], "tiles": best["tile_cnt"], "frags": best["frags"],
+                          "sigs": best["sigs"], "in_depth": best["in_depth"],
+                          "workload": "config 4 stream (firedancer_amd/txn_workload.py), GPU-signed"}))
+
+
+if __name__ == "__main__":
+    main()
