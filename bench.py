@@ -61,6 +61,7 @@ PEAK_SLOTS = SIMDS * MAX_CLOCK / 4        # VALU issue slots/s: one quad-cycle p
 PMC_SUMMARY = "r03ag_pmc_summary.json"    # rocprofv3 PMC passes of this kernel build (tools/run_profile.sh)
 ISSUE_SUMMARY = "r03ag_valu_issue_calibration.json"   # VALU issue-slot pass of this build (tools/run_valu_calib.sh)
 ISSUE_SUMMARY_C4 = "r03ag_c4_valu_issue.json"          # the same pass over C4's timing-leg batch (tools/run_c4_issue.sh)
+PMC_SUMMARY_C4 = "r04_c4_pmc_summary.json"             # FETCH/WRITE passes over the C4 bench (tools/c4_pmc_summary.py)
 
 
 def w_total(msg_sz):
@@ -155,6 +156,39 @@ def c4_issue_roofline(dsm_avg_ms, units_per_launch):
         if r and r.get("profile_matches_build") and not r["slots_scaled_from_profiled_units"]:
             return r
     return issue_roofline(dsm_avg_ms, units_per_launch)
+
+
+def ingest_roofline(st):
+    """HBM roofline of the verify tile's frag-ingest kernel (k_txnm_batch:
+    during_frag's copy, after_frag's parse, record expansion) for tile 0's
+    timing-leg batch: algorithmic bytes (fd_verify_hip_tile_ingest_stats,
+    include/fd_verify_hip.h) / kernel time (HIP events) against 8 TB/s; the
+    traffic is the committed PMC pass's FETCH_SIZE x 2 + WRITE_SIZE per
+    launch (profiles/PMC_SUMMARY_C4) when it describes this build's kernel."""
+    if not st or not st["ms"]:
+        return None
+    achieved = st["bytes"] / (st["ms"] * 1e-3) / 1e9
+    r = {"kernel": "k_txnm_batch<16>", "bound": "hbm", "unit": "GB/s", "achieved": round(achieved, 1),
+         "peak": 8000.0, "frac": round(achieved / 8000.0, 4), "avg_launch_ms": round(st["ms"], 4),
+         "algorithmic_bytes_per_launch": st["bytes"], "frags_per_launch": st["frags"], "records": st["records"],
+         "traffic": None}
+    path = os.path.join(REPO, "profiles", PMC_SUMMARY_C4)
+    if os.path.exists(path):
+        with open(path) as f:
+            pm = json.load(f)
+        k = pm.get("kernels", {}).get("k_txnm_batch")
+        have = None
+        try:
+            from firedancer_amd.kernel_hash import engine_kernel_hashes
+            have = engine_kernel_hashes(names=("k_txnm_batch<16>",)).get("k_txnm_batch<16>")
+        except Exception:                          # noqa: BLE001 -- reported as no match
+            pass
+        if k:
+            r["traffic"] = k["hbm_side_bytes_per_launch"]
+            r["traffic_ratio"] = round(k["hbm_side_bytes_per_launch"] / k["algorithmic_bytes_per_launch"], 3)
+            r["traffic_source"] = f"profiles/{PMC_SUMMARY_C4}: FETCH_SIZE*2 + WRITE_SIZE of k_txnm_batch"
+            r["profile_matches_build"] = bool(have) and have == pm.get("kernel_sha", {}).get("k_txnm_batch<16>")
+    return r
 
 
 def prep_issue_util():
@@ -253,6 +287,8 @@ def main():
                     help="c4 PCIe-inclusive leg: timed steps (the pipeline's fill, one copy, and drain, one host "
                          "pass, are paid once per leg; 0: --steps)")
     ap.add_argument("--sigs", type=int, default=None, help="override signatures per GPU per step")
+    ap.add_argument("--no-c4", action="store_true",
+                    help="c2 (default config): skip the config-4 sub-object (the verify-tile path, 'c4' in the line)")
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--cpu-seconds", type=float, default=8.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -262,7 +298,7 @@ def main():
                     help="nccl (RCCL over xGMI, one rank per GPU: the driver's N-GPU runs); gloo rehearses the "
                          "N>1 path with several ranks sharing one GPU (rank r on GPU r %% device_count)")
     args = ap.parse_args()
-    if args.config == "c4":
+    if args.config == "c4" or (args.config == "c2" and not args.no_c4):
         # The reference runs each verify tile as its own process, each with the
         # HIP runtime's own hardware queues; here the tiles are threads of one
         # process, so give that process a queue per tile (HIP default 4).
@@ -486,9 +522,18 @@ def main():
                          "ingest_GBps": round(ingest_gbps, 2), "ingest_bytes_per_sig": ingest_bytes},
             "cpu_baseline": cpu,
         }
-        emit(out)
     for vv in ctxs + [v]:
         vv.close()
+    if cfg == "c2" and not args.no_c4:
+        # config 4, the north star's workload (the verify tile's frags), as a
+        # sub-object of the same line: every rank runs it after the C2 leg
+        c4 = run_c4(args, rank, world, local, dist, emit_line=False)
+        if rank == 0:
+            out["c4"] = {k: c4[k] for k in ("value", "unit", "ms_per_step", "steps", "frags_per_s", "config",
+                                            "frag_outcomes_last_batch", "batch_gpu_ms", "batch_host_ms",
+                                            "roofline", "ingest_roofline", "pcie_inclusive", "cpu_baseline")}
+    if rank == 0:
+        emit(out)
     if dist:
         dist.barrier()
         dist.destroy_process_group()
@@ -523,7 +568,7 @@ def ref_tile_baseline(pool, off, sz, threads, target_s, seed, depth):
                       f"{threads} pinned threads = {threads} verify tiles, tcache depth {depth} each)"}
 
 
-def run_c4(args, rank, world, local, dist):
+def run_c4(args, rank, world, local, dist, emit_line=True):
     """Config 4: synthetic Solana txn stream through the verify tile.
 
     A step is one batch of --txns frags through --tiles GPU verify tiles
@@ -719,9 +764,12 @@ def run_c4(args, rank, world, local, dist):
     gpu_ms = [x for g in gpu_ms for x in g]; host_ms = [x for h in host_ms for x in h]
     # kernel roofline: one extra (untimed) batch of tile 0 with per-kernel HIP-event timing
     v.set_timing(True)
+    tiles[0].set_ingest_timing(frags_mode)
     submit(0); tiles[0].complete()
     prep_ms, dsm_ms, launches = v.get_timing()
     dsm_units = v.get_dsm_units()
+    ing = tiles[0].ingest_stats() if frags_mode else None
+    tiles[0].set_ingest_timing(False)
     v.set_timing(False)
     n_sig_batch = int(my_sigs) // max(args.steps, 1)
     launches = max(launches, 1)
@@ -768,10 +816,12 @@ def run_c4(args, rank, world, local, dist):
                          "prep_ms_per_batch": round(prep_ms, 4),
                          "timing_leg": "one extra batch of tile 0 alone, HIP events around each launch"}),
             "ingest": args.c4_ingest,
+            "ingest_roofline": ingest_roofline(ing),
             "pcie_inclusive": pcie,
             "cpu_baseline": cpu,
         }
-        emit(out)
+        if emit_line:
+            emit(out)
     for tl in tiles:
         tl.close()
     for x in vs:
@@ -780,7 +830,7 @@ def run_c4(args, rank, world, local, dist):
         if "hb" in P:
             P["h_in"] = None
             P["hb"].close()
-    if dist:
+    if dist and emit_line:
         dist.barrier()
         dist.destroy_process_group()
     return out

@@ -1029,6 +1029,8 @@ struct tile_slot {
      header bundle ids, in kinds and the corrupt-frag flag */
   u32 *         d_pay_off; u16 * d_pay_sz; u32 * d_tout; u64 * d_bid; u32 * d_flag;
   u32 *         d_misc;     /* counter, flag, record segments (SLOT_MISC_*) */
+  fd_ed25519_hip_ctx_t * ctx;   /* the verify context (stream and scratch) the slot's batches run on */
+  int           own_ctx;    /* created by set_inflight: batches of different slots run concurrently */
   u32           n_seg;      /* the last batch's record segments (0: not k_txnm_batch) */
   hipEvent_t    ev_ing0, ev_ing1;   /* around the ingest kernel (ingest timing) */
   int           ing_timed;
@@ -1167,6 +1169,7 @@ fd_verify_hip_tile_new( fd_ed25519_hip_ctx_t * ctx, ulong max_txn, ulong seed, u
   t->own_oldest = fd_verify_hip_tcache_reset( t->ring, depth, t->map, map_cnt );
   t->nslot = t->nalloc = 2ul;
   slot_alloc( t->slot[0], max_txn ); slot_alloc( t->slot[1], max_txn );
+  t->slot[0].ctx = t->slot[1].ctx = ctx;                  /* one stream: the two batches run back to back */
   fd_verify_hip_tile_hist_init( t, 10000ul, 1000000000ul );   /* 10 us .. 1 s */
   /* Everything the batch path would otherwise do lazily, done now: record
      buffers at their bound (12 signatures per frag) and this module's code
@@ -1237,7 +1240,11 @@ extern "C" void fd_verify_hip_tile_delete( fd_verify_hip_tile_t * t ) {
   if( !t ) return;
   (void)hipSetDevice( fd_ed25519_hip_ctx_device( t->ctx ) );
   (void)hipStreamSynchronize( (hipStream_t)fd_ed25519_hip_ctx_stream( t->ctx ) );
-  for( ulong k = 0; k < t->nalloc; k++ ) slot_free( t->slot[k] );
+  for( ulong k = 0; k < t->nalloc; k++ ) {
+    if( t->slot[k].own_ctx ) (void)hipStreamSynchronize( (hipStream_t)fd_ed25519_hip_ctx_stream( t->slot[k].ctx ) );
+    slot_free( t->slot[k] );
+    if( t->slot[k].own_ctx ) fd_ed25519_hip_ctx_delete( t->slot[k].ctx );
+  }
   free( t->own_mem ); free( t );
 }
 
@@ -1292,9 +1299,9 @@ submit_verify( fd_verify_hip_tile_t * t, tile_slot & s, hipStream_t st, ulong n,
   TX_CHECK( hipGetLastError() );
   /* the record count stays on the device: no host round trip between the
      expansion and the verify, so submit never waits on the GPU */
-  fd_ed25519_hip_verify_dev_count( t->ctx, need, s.d_counter, s.d_rsig, s.d_rpub, d_pool, s.d_rmoff, s.d_rmsz,
+  fd_ed25519_hip_verify_dev_count( s.ctx, need, s.d_counter, s.d_rsig, s.d_rpub, d_pool, s.d_rmoff, s.d_rmsz,
                                    s.d_rcode, NULL, st );
-  fd_ed25519_hip_group_reduce_dev( t->ctx, n, s.d_first, s.d_cnt, s.d_rcode, s.d_tcode, st );
+  fd_ed25519_hip_group_reduce_dev( s.ctx, n, s.d_first, s.d_cnt, s.d_rcode, s.d_tcode, st );
 }
 
 static void
@@ -1312,8 +1319,8 @@ submit_begin( fd_verify_hip_tile_t * t, ulong n, hipStream_t & st, int & rc ) {
   if( n > t->max_txn ) { rc = -1; return 0; }
   tile_slot & s = t->slot[t->submitted % t->nslot];
   if( s.busy ) { rc = -2; return 0; }                        /* two batches outstanding */
-  st = (hipStream_t)fd_ed25519_hip_ctx_stream( t->ctx );
-  TX_CHECK( hipSetDevice( fd_ed25519_hip_ctx_device( t->ctx ) ) );
+  st = (hipStream_t)fd_ed25519_hip_ctx_stream( s.ctx );
+  TX_CHECK( hipSetDevice( fd_ed25519_hip_ctx_device( s.ctx ) ) );
   s.n = n; s.nsig = 0; s.busy = 1; s.frags = 0; s.ing_timed = 0; s.n_seg = 0; t->submitted++;
   TX_CHECK( hipEventRecord( s.ev_start, st ) );
   return &s;
@@ -1386,11 +1393,11 @@ fd_verify_hip_tile_submit_frags( fd_verify_hip_tile_t * t, ulong n, uchar const 
     TX_CHECK( hipGetLastError() );
     if( s.ing_timed ) TX_CHECK( hipEventRecord( s.ev_ing1, st ) );
     fd_hip_segs_t segs = { s.d_misc + 32u, n_seg, seg_cap, s.d_counter };
-    if( fd_ed25519_hip_verify_segs( t->ctx, segs, s.d_rsig, s.d_rpub, d_out, s.d_rmoff, s.d_rmsz, s.d_rcode, st ) ) {
+    if( fd_ed25519_hip_verify_segs( s.ctx, segs, s.d_rsig, s.d_rpub, d_out, s.d_rmoff, s.d_rmsz, s.d_rcode, st ) ) {
       fprintf( stderr, "fd_verify_hip: segmented verify refused (%u x %lu records)\n", n_seg, seg_cap );
       abort();
     }
-    fd_ed25519_hip_group_reduce_dev( t->ctx, n, s.d_first, s.d_cnt, s.d_rcode, s.d_tcode, st );
+    fd_ed25519_hip_group_reduce_dev( s.ctx, n, s.d_first, s.d_cnt, s.d_rcode, s.d_tcode, st );
   }
   submit_results( s, st, n, d_in_kind );
   TX_CHECK( hipEventRecord( s.ev_done, st ) );
@@ -1414,11 +1421,24 @@ fd_verify_hip_tile_inflight( fd_verify_hip_tile_t const * t ) { return t->submit
 extern "C" int
 fd_verify_hip_tile_set_inflight( fd_verify_hip_tile_t * t, ulong k ) {
   if( k < 1ul || k > FD_VERIFY_HIP_INFLIGHT_MAX || t->submitted != t->completed ) return -1;
-  TX_CHECK( hipSetDevice( fd_ed25519_hip_ctx_device( t->ctx ) ) );
+  int dev = fd_ed25519_hip_ctx_device( t->ctx );
+  TX_CHECK( hipSetDevice( dev ) );
   hipStream_t st = (hipStream_t)fd_ed25519_hip_ctx_stream( t->ctx );
-  for( ulong j = t->nalloc; j < k; j++ ) { slot_alloc( t->slot[j], t->max_txn ); slot_warm( t->slot[j], t->max_txn, st ); }
   TX_CHECK( hipStreamSynchronize( st ) );
+  for( ulong j = t->nalloc; j < k; j++ ) { slot_alloc( t->slot[j], t->max_txn ); slot_warm( t->slot[j], t->max_txn, st ); }
   if( k > t->nalloc ) t->nalloc = k;
+  /* every slot past the first on a context (stream, verify scratch) of its
+     own: a batch's GPU time is nearly independent of its size until it
+     fills the GPU (~1.1 ms per tile batch of 2-16 K frags), so batches that
+     wait on one stream behind each other leave the GPU idle */
+  for( ulong j = 1; j < k; j++ ) {
+    tile_slot & s = t->slot[j];
+    if( s.own_ctx ) continue;
+    s.ctx = fd_ed25519_hip_ctx_new( dev, 12ul*(t->max_txn + SLOT_SEG_SLACK) );
+    if( !s.ctx ) return -1;
+    s.own_ctx = 1;
+  }
+  for( ulong j = 0; j < t->nalloc; j++ ) if( !t->slot[j].ctx ) t->slot[j].ctx = t->ctx;
   t->nslot = k;
   t->submitted = t->completed = 0;                        /* batch b takes slot b % nslot */
   return 0;
@@ -1644,6 +1664,16 @@ fd_replay_hip_txn_verify_dev( fd_replay_hip_t * r, ulong n, uchar const * d_pool
   TX_CHECK( hipEventRecord( r->ev_last, st ) );
   r->ev_used = 1;
   return 0;
+}
+
+extern "C" int
+fd_replay_hip_poll( fd_replay_hip_t const * r ) {
+  if( !r->ev_used ) return -1;
+  TX_CHECK( hipSetDevice( fd_ed25519_hip_ctx_device( r->ctx ) ) );
+  hipError_t e = hipEventQuery( r->ev_last );
+  if( e == hipErrorNotReady ) return 0;
+  TX_CHECK( e );
+  return 1;
 }
 
 extern "C" int

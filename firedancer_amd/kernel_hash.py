@@ -60,18 +60,24 @@ def kernel_hashes(lib_path, names=("k_verify_dsm", "k_verify_prep")):
         syms, secs = _elf_symbols(co)
         for sname, value, size, shndx in syms:
             for k in names:
-                # C++-mangled kernel symbol: _Z<len><name>...; skip the .kd descriptor
-                if f"{len(k)}{k}" in sname and not sname.endswith(".kd") and size and 0 < shndx < len(secs):
+                # C++-mangled kernel symbol: _Z<len><name>...; "name<N>" names the
+                # int-template instance _Z<len><name>ILi<N>E...; skip the .kd descriptor
+                if "<" in k:
+                    base, arg = k[:-1].split("<")
+                    pat = f"{len(base)}{base}ILi{arg}E"
+                else:
+                    pat = f"{len(k)}{k}"
+                if pat in sname and not sname.endswith(".kd") and size and 0 < shndx < len(secs):
                     sec = secs[shndx]
                     start = sec[4] + (value - sec[3])
                     found[k] = hashlib.sha256(co[start:start + size]).hexdigest()[:16]
     return found
 
 
-def engine_kernel_hashes():
+def engine_kernel_hashes(names=("k_verify_dsm", "k_verify_prep")):
     from .ed25519 import LIB
     path = os.environ.get("FD_ED25519_HIP_LIB") or LIB
-    return kernel_hashes(path)
+    return kernel_hashes(path, names)
 
 
 if __name__ == "__main__":

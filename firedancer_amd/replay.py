@@ -28,7 +28,7 @@ FD_RUNTIME_EXECUTE_SUCCESS = 0
 FD_RUNTIME_TXN_ERR_SIGNATURE_FAILURE = -13
 
 # Every symbol include/fd_replay_hip.h declares (checked by tests/test_abi.py).
-EXPORTS = ("fd_replay_hip_new", "fd_replay_hip_delete", "fd_replay_hip_txn_verify_dev",
+EXPORTS = ("fd_replay_hip_new", "fd_replay_hip_delete", "fd_replay_hip_txn_verify_dev", "fd_replay_hip_poll",
            "fd_fec_hip_verify_roots_dev", "fd_precompile_hip_new", "fd_precompile_hip_delete",
            "fd_precompile_hip_ed25519_verify_dev")
 
@@ -68,6 +68,8 @@ def lib():
         L.fd_replay_hip_delete.argtypes = [vp]
         L.fd_replay_hip_txn_verify_dev.restype = c.c_int
         L.fd_replay_hip_txn_verify_dev.argtypes = [vp, u64, vp, vp, vp, vp]
+        L.fd_replay_hip_poll.restype = c.c_int
+        L.fd_replay_hip_poll.argtypes = [vp]
         L.fd_fec_hip_verify_roots_dev.restype = c.c_int
         L.fd_fec_hip_verify_roots_dev.argtypes = [vp, u64, vp, vp, vp, vp, vp]
         L.fd_precompile_hip_new.restype = vp
@@ -113,6 +115,11 @@ class ReplayVerifier:
             rc = self._lib.fd_replay_hip_txn_verify_dev(*args, h)
         if rc:
             raise ValueError(f"fd_replay_hip_txn_verify_dev: n={n} > max_txn={self.max_txn}")
+
+    def poll(self):
+        """fd_replay_hip_poll: 1 when the last txn_verify_dev is done, 0 while
+        it runs, -1 before any call."""
+        return self._lib.fd_replay_hip_poll(self.r)
 
     def close(self):
         if self.r:

@@ -81,6 +81,13 @@ fd_replay_hip_txn_verify_dev( fd_replay_hip_t *         r,
                               int *                     d_result,
                               void *                    stream );
 
+/* Non-blocking completion check of the last fd_replay_hip_txn_verify_dev
+   call (its results are in d_result once this says so): 1 done, 0 still
+   running, -1 no call yet.  For a caller that polls from its run loop (the
+   replay tile's after_credit, integration/fd_replay_hip.patch). */
+int
+fd_replay_hip_poll( fd_replay_hip_t const * r );
+
 /* ---- shred FEC-set roots ----------------------------------------------------
 
    d_codes[i] = fd_ed25519_verify( d_roots + 32*i, 32, d_sigs + 64*i,

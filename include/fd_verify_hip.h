@@ -222,14 +222,19 @@ fd_verify_hip_tile_submit_frags( fd_verify_hip_tile_t * tile,
 int
 fd_verify_hip_tile_poll( fd_verify_hip_tile_t const * tile );
 
-/* batches submitted and not yet completed (0, 1 or 2) */
+/* batches submitted and not yet completed (at most the in-flight limit) */
 ulong
 fd_verify_hip_tile_inflight( fd_verify_hip_tile_t const * tile );
 
 /* Batches the tile keeps on the GPU at once (1..FD_VERIFY_HIP_INFLIGHT_MAX;
-   2 for a new tile): submit returns -2 while that many are outstanding.
-   Allocates and warms the extra batch slots (call from privileged_init).
-   -1 if k is out of range or batches are outstanding. */
+   2 for a new tile, both on ctx's stream, run back to back): submit returns
+   -2 while that many are outstanding.  After set_inflight every slot past
+   the first runs on a verify context (stream and scratch) of its own, on
+   ctx's device, so the batches in flight run concurrently: a batch's GPU
+   time is nearly independent of its size until it fills the GPU.
+   Allocates and warms the slots (call from privileged_init: device memory
+   for 12 records per frag of max_txn in each).  -1 if k is out of range or
+   batches are outstanding.  Results still complete in submission order. */
 #define FD_VERIFY_HIP_INFLIGHT_MAX 4
 int
 fd_verify_hip_tile_set_inflight( fd_verify_hip_tile_t * tile, ulong k );

@@ -59,13 +59,15 @@ void fd_halt( void ) {}
 
 #define RUN_MAGIC     (0xfd7111e5a11ce5ULL)
 #define RUN_TILE_MAX  (16UL)
-#define RUN_OUT_DEPTH (65536UL)              /* verify_dedup mcache: >= FD_VERIFY_HIP_STEM_BURST */
+/* verify_dedup mcache: at least twice FD_VERIFY_HIP_STEM_BURST (fd_stem.c:358) */
+#define RUN_OUT_DEPTH (fd_ulong_max( 65536UL, fd_ulong_pow2_up( 2UL*FD_VERIFY_HIP_STEM_BURST ) ))
 
 typedef struct {
   volatile long t_ready, t_end;
   volatile ulong done, frags, sigs, pub, parse, verify, dedup, bundle;
   volatile ulong batches;
   volatile double gpu_ms, host_ms;           /* sums over the tile's batches (fd_verify_hip_tile_hist sums) */
+  volatile ulong regime[ 8 ];                /* the stem's REGIME_DURATION_NANOS ticks (fd_stem.c:406-712) */
 } run_res_t;
 
 typedef struct {
@@ -113,20 +115,21 @@ produce( char const * path, char const * stream, ulong tile_cnt, ulong in_depth 
   ulong n, seed, depth;
   memcpy( &n, in+4, 8 ); memcpy( &seed, in+12, 8 ); memcpy( &depth, in+20, 8 );
 
-  /* frag layout: fd_txn_m_t header + payload, chunk-aligned, back to back */
-  ulong * chunk_rel = malloc( n*sizeof(ulong) ); ushort * fsz = malloc( n*sizeof(ushort) );
-  ulong * poff = malloc( n*sizeof(ulong) );
-  FD_TEST( chunk_rel && fsz && poff );
-  ulong off = 28UL, data = 0UL;
+  /* the stream's frags, in order (offsets into the file image) */
+  ushort * fsz = malloc( n*sizeof(ushort) ); ulong * poff = malloc( n*sizeof(ulong) );
+  FD_TEST( fsz && poff );
+  ulong off = 28UL;
   for( ulong j=0UL; j<n; j++ ) {
     ushort psz; memcpy( &psz, in+off+8, 2 );
     poff[ j ] = off; off += 10UL + psz;
     FD_TEST( off<=in_sz && psz<=FD_TPU_MTU );
     fsz[ j ] = (ushort)( sizeof(fd_txn_m_t) + psz );
-    chunk_rel[ j ] = data >> FD_CHUNK_LG_SZ;
-    data += fd_ulong_align_up( fsz[ j ], FD_CHUNK_SZ );
   }
-  ulong data_sz = data + FD_TPU_REASM_MTU + FD_CHUNK_SZ;         /* the wmark leaves an MTU past the last frag */
+  /* the quic_verify dcache: a ring of in_depth frags, as the quic tile's
+     (the producer writes each frag into it just before publishing it, so a
+     tile's during_frag copies recently written bytes, as it would behind a
+     quic tile) */
+  ulong data_sz = fd_dcache_req_data_sz( FD_TPU_RAW_MTU, in_depth, 1UL, 1 );
   ulong mc_off  = fd_ulong_align_up( sizeof(run_hdr_t), fd_mcache_align() );
   ulong fs_off  = fd_ulong_align_up( mc_off + fd_mcache_footprint( in_depth, 0UL ), fd_fseq_align() );
   ulong fs_strd = fd_ulong_align_up( fd_fseq_footprint(), 128UL );
@@ -141,13 +144,7 @@ produce( char const * path, char const * stream, ulong tile_cnt, ulong in_depth 
   uchar * dcache = fd_dcache_join( fd_dcache_new( base + dc_off, data_sz, 0UL ) );
   FD_TEST( mcache && dcache );
   ulong chunk0 = fd_dcache_compact_chunk0( base, dcache );
-  for( ulong j=0UL; j<n; j++ ) {
-    fd_txn_m_t * m = (fd_txn_m_t *)fd_chunk_to_laddr( base, chunk0 + chunk_rel[ j ] );
-    memset( m, 0, sizeof(fd_txn_m_t) );
-    memcpy( &m->block_engine.bundle_id, in+poff[ j ], 8 );
-    m->payload_sz = (ushort)( fsz[ j ] - sizeof(fd_txn_m_t) );
-    memcpy( fd_txn_m_payload( m ), in+poff[ j ]+10UL, m->payload_sz );
-  }
+  ulong wmark  = fd_dcache_compact_wmark ( base, dcache, FD_TPU_RAW_MTU );
   hdr->n = n; hdr->tile_cnt = tile_cnt; hdr->seed = seed; hdr->tcache_depth = depth; hdr->in_depth = in_depth;
   hdr->mcache_off = mc_off; hdr->dcache_off = dc_off; hdr->fseq_off = fs_off; hdr->fseq_stride = fs_strd;
   hdr->dcache_data_sz = data_sz; hdr->map_sz = map_sz;
@@ -157,7 +154,7 @@ produce( char const * path, char const * stream, ulong tile_cnt, ulong in_depth 
   printf( "READY\n" ); fflush( stdout );
 
   for( long tw=fd_log_wallclock(); hdr->ready<tile_cnt; FD_SPIN_PAUSE() )
-    if( fd_log_wallclock()-tw > 300L*1000000000L ) FD_LOG_ERR(( "tiles not ready after 300 s (%lu of %lu)", hdr->ready, tile_cnt ));
+    if( fd_log_wallclock()-tw > 120L*1000000000L ) FD_LOG_ERR(( "tiles not ready after 120 s (%lu of %lu)", hdr->ready, tile_cnt ));
 
   ulong const * fseq[ RUN_TILE_MAX ];
   for( ulong t=0UL; t<tile_cnt; t++ ) fseq[ t ] = fd_fseq_join( base + fs_off + t*fs_strd );
@@ -166,7 +163,7 @@ produce( char const * path, char const * stream, ulong tile_cnt, ulong in_depth 
   FD_COMPILER_MFENCE();
   hdr->start = 1UL;
   ulong ctl = fd_frag_meta_ctl( 0UL, 1, 1, 0 );
-  ulong lim = 0UL;
+  ulong lim = 0UL, chunk = chunk0;
   for( ulong seq=0UL; seq<n; seq++ ) {
     while( seq>=lim ) {                                        /* flow control against the slowest tile */
       ulong m = ULONG_MAX;
@@ -175,8 +172,14 @@ produce( char const * path, char const * stream, ulong tile_cnt, ulong in_depth 
       if( seq>=lim ) FD_SPIN_PAUSE();
       if( fd_log_wallclock()-t0 > 600L*1000000000L ) FD_LOG_ERR(( "tiles stalled at seq %lu", seq ));
     }
+    fd_txn_m_t * m = (fd_txn_m_t *)fd_chunk_to_laddr( base, chunk );
+    memset( m, 0, sizeof(fd_txn_m_t) );
+    memcpy( &m->block_engine.bundle_id, in+poff[ seq ], 8 );
+    m->payload_sz = (ushort)( fsz[ seq ] - sizeof(fd_txn_m_t) );
+    memcpy( fd_txn_m_payload( m ), in+poff[ seq ]+10UL, m->payload_sz );
     ulong ts = (ulong)fd_frag_meta_ts_comp( fd_tickcount() );
-    fd_mcache_publish( mcache, in_depth, seq, 0UL, chunk0 + chunk_rel[ seq ], fsz[ seq ], ctl, ts, ts );
+    fd_mcache_publish( mcache, in_depth, seq, 0UL, chunk, fsz[ seq ], ctl, ts, ts );
+    chunk = fd_dcache_compact_next( chunk, fsz[ seq ], chunk0, wmark );
   }
   long t_pub = fd_log_wallclock();
   ulong done = 0UL;
@@ -186,7 +189,7 @@ produce( char const * path, char const * stream, ulong tile_cnt, ulong in_depth 
     if( fd_log_wallclock()-t0 > 900L*1000000000L ) FD_LOG_ERR(( "tiles not done after 900 s" ));
     FD_SPIN_PAUSE();
   }
-  long t_end = t0; ulong sigs = 0UL, frags = 0UL, pub = 0UL, batches = 0UL;
+  long t_end = t0; ulong sigs = 0UL, frags = 0UL, pub = 0UL, batches = 0UL, reg[ 8 ] = { 0UL };
   ulong parse = 0UL, verify = 0UL, dedup = 0UL, bundle = 0UL; double gpu_ms = 0.0, host_ms = 0.0;
   printf( "{\"tiles\": [" );
   for( ulong t=0UL; t<tile_cnt; t++ ) {
@@ -195,13 +198,24 @@ produce( char const * path, char const * stream, ulong tile_cnt, ulong in_depth 
     sigs += r->sigs; frags += r->frags; pub += r->pub; batches += r->batches;
     parse += r->parse; verify += r->verify; dedup += r->dedup; bundle += r->bundle;
     gpu_ms += r->gpu_ms; host_ms += r->host_ms;
+    for( ulong k=0UL; k<8UL; k++ ) reg[ k ] += r->regime[ k ];
     printf( "%s{\"frags\": %lu, \"sigs\": %lu, \"published\": %lu, \"batches\": %lu, \"s\": %.6f, "
             "\"gpu_ms_per_batch\": %.4f, \"host_ms_per_batch\": %.4f}", t ? ", " : "", r->frags, r->sigs, r->pub,
             r->batches, (double)( r->t_end - t0 )*1e-9, r->batches ? r->gpu_ms/(double)r->batches : 0.0,
             r->batches ? r->host_ms/(double)r->batches : 0.0 );
   }
   double s = (double)( t_end - t0 )*1e-9;
-  printf( "], \"frags\": %lu, \"sigs\": %lu, \"published\": %lu, \"parse_fail\": %lu, \"verify_fail\": %lu, "
+  double rt = (double)( reg[0]+reg[1]+reg[2]+reg[3]+reg[4]+reg[5]+reg[6]+reg[7] ) + 1e-9;
+  printf( "], " );
+  /* fd_stem.c's regimes: {housekeeping, prefrag (before/after_credit), postfrag (the frag callbacks)}
+     x {caught up, processing, backpressured} */
+  printf( "\"regime\": {\"caught_up\": %.4f, \"processing\": %.4f, \"backpressure\": %.4f, "
+          "\"hk_caught_up\": %.4f, \"hk_processing\": %.4f, \"pre_caught_up\": %.4f, \"pre_processing\": %.4f, "
+          "\"post_caught_up\": %.4f, \"post_processing\": %.4f}, ",
+          (double)( reg[0]+reg[3]+reg[6] )/rt, (double)( reg[1]+reg[4]+reg[7] )/rt, (double)( reg[2]+reg[5] )/rt,
+          (double)reg[0]/rt, (double)reg[1]/rt, (double)reg[3]/rt, (double)reg[4]/rt, (double)reg[6]/rt,
+          (double)reg[7]/rt );
+  printf( "\"frags\": %lu, \"sigs\": %lu, \"published\": %lu, \"parse_fail\": %lu, \"verify_fail\": %lu, "
           "\"dedup\": %lu, \"bundle_peer_fail\": %lu, \"seconds\": %.6f, \"publish_s\": %.6f, "
           "\"verifies_per_s\": %.1f, \"frags_per_s\": %.1f, \"batches\": %lu, \"gpu_ms_per_batch\": %.4f, "
           "\"host_ms_per_batch\": %.4f, \"batch_max\": %lu, \"batch_cap\": %lu, \"inflight\": %lu, "
@@ -213,7 +227,7 @@ produce( char const * path, char const * stream, ulong tile_cnt, ulong in_depth 
   fflush( stdout );
   munmap( base, map_sz );
   unlink( path );
-  free( in ); free( chunk_rel ); free( fsz ); free( poff );
+  free( in ); free( fsz ); free( poff );
   return 0;
 }
 
@@ -258,7 +272,6 @@ tile( char const * path, ulong t ) {
   fd_topo_wksp_t * qw = fd_topob_wksp( topo, "quic_verify" );   /* the shared segment */
   fd_topo_wksp_t * tw = fd_topob_wksp( topo, "verify" );        /* this tile's own memory */
   fd_topo_tile_t * tile = fd_topob_tile( topo, "verify", "verify", "verify", 0UL, 0, 0 );
-  tile->kind_id = t;                                            /* GPU t % devices; round robin index */
   tile->verify.tcache_depth = hdr->tcache_depth;
   ulong out_data = fd_dcache_req_data_sz( FD_TPU_PARSED_MTU, RUN_OUT_DEPTH, FD_VERIFY_HIP_STEM_BURST, 1 );
   drv_arena_sz = 4096UL + scratch_footprint( tile ) + scratch_align() + fd_mcache_footprint( RUN_OUT_DEPTH, 0UL ) +
@@ -284,7 +297,7 @@ tile( char const * path, ulong t ) {
   FD_TEST( quic->mcache && quic->dcache && out->mcache && out->dcache );
   fd_topob_tile_in ( topo, "verify", 0UL, "verify", "quic_verify", 0UL, FD_TOPOB_UNRELIABLE, FD_TOPOB_POLLED );
   fd_topob_tile_out( topo, "verify", 0UL, "verify_dedup", 0UL );
-  tile->kind_id = t;
+  tile->kind_id = t;                                            /* GPU t % devices; round robin index */
   quic->mtu = FD_TPU_REASM_MTU; out->mtu = FD_TPU_PARSED_MTU;
 
   privileged_init( topo, tile );
@@ -333,6 +346,7 @@ tile( char const * path, ulong t ) {
   r->t_end = t_end; r->frags = m[0] + m[1] + m[2] + m[3] + m[4]; r->sigs = m[5]; r->pub = m[4];
   r->parse = m[0]; r->verify = m[1]; r->dedup = m[2]; r->bundle = m[3];
   r->batches = nb; r->gpu_ms = (double)sum_gpu*1e-6; r->host_ms = (double)sum_host*1e-6;
+  for( ulong k=0UL; k<8UL; k++ ) r->regime[ k ] = fd_metrics_tl[ MIDX( COUNTER, TILE, REGIME_DURATION_NANOS ) + k ];
   FD_COMPILER_MFENCE();
   r->done = 1UL;
   return 0;

@@ -35,19 +35,20 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, REPO)
 sys.path.insert(0, os.path.join(REPO, "tests"))
 BUILD = os.path.join(REPO, "integration", "_build")
-SWEEP = [(b, i) for b in (1024, 2048, 4096, 8192) for i in (2, 3, 4)]
+SWEEP = [(b, i, p) for b in (1024, 2048, 4096, 8192) for i in (2, 3, 4) for p in (2000, 20000)]
 
 
-def binary(b, i):
-    return os.path.join(BUILD, f"tile_run_b{b}i{i}")
+def binary(b, i, p=2000):
+    return os.path.join(BUILD, f"tile_run_b{b}i{i}" + ("" if p == 2000 else f"p{p}"))
 
 
 def build():
-    for b, i in SWEEP:
-        subprocess.check_call(["make", "-s", "-C", os.path.join(REPO, "integration"), f"VARIANT=_b{b}i{i}",
-                               f"DEFS=-DFD_VERIFY_HIP_BATCH_MAX={b}UL -DFD_VERIFY_HIP_INFLIGHT={i}UL",
-                               f"_build/tile_run_b{b}i{i}"])
-        print(binary(b, i))
+    for b, i, p in SWEEP:
+        v = os.path.basename(binary(b, i, p))[len("tile_run"):]
+        subprocess.check_call(["make", "-s", "-C", os.path.join(REPO, "integration"), f"VARIANT={v}",
+                               f"DEFS=-DFD_VERIFY_HIP_BATCH_MAX={b}UL -DFD_VERIFY_HIP_INFLIGHT={i}UL "
+                               f"-DFD_VERIFY_HIP_POLL_NS={p}L", f"_build/tile_run{v}"])
+        print(binary(b, i, p))
 
 
 def make_stream(n, path, seed=0x5eed0004, depth=4194302):
@@ -62,32 +63,52 @@ def make_stream(n, path, seed=0x5eed0004, depth=4194302):
     return s
 
 
-def run_one(exe, stream, tiles, in_depth, timeout):
+def run_one(exe, stream, tiles, in_depth, timeout, logdir):
+    """One producer and `tiles` tile processes; every process's stderr goes to
+    a file in logdir; liveness is checked every second (a tile that dies ends
+    the run at once), with a progress line on stderr."""
     shm = f"/dev/shm/fd_tile_bench_{os.getpid()}"
     if os.path.exists(shm):
         os.unlink(shm)
+    os.makedirs(logdir, exist_ok=True)
+    perr = open(os.path.join(logdir, "producer.err"), "w")
     prod = subprocess.Popen([exe, "produce", shm, stream, str(tiles), str(in_depth)], stdout=subprocess.PIPE,
-                            stderr=subprocess.PIPE, text=True)
-    procs = []
+                            stderr=perr, text=True)
+    procs, terr = [], []
+    t0 = time.time()
     try:
         line = prod.stdout.readline()
         if line.strip() != "READY":
-            raise RuntimeError(f"producer: {line!r} {prod.stderr.read()[-2000:]}")
-        procs = [subprocess.Popen([exe, "tile", shm, str(t)], stdout=subprocess.DEVNULL, stderr=subprocess.PIPE,
-                                  text=True) for t in range(tiles)]
-        out, err = prod.communicate(timeout=timeout)
+            raise RuntimeError(f"producer: {line!r} (see {logdir}/producer.err)")
+        for t in range(tiles):
+            terr.append(open(os.path.join(logdir, f"tile{t}.err"), "w"))
+            procs.append(subprocess.Popen([exe, "tile", shm, str(t)], stdout=subprocess.DEVNULL, stderr=terr[-1]))
+        last = 0.0
+        while prod.poll() is None:
+            dead = [(t, p.returncode) for t, p in enumerate(procs) if p.poll() is not None and p.returncode]
+            if dead:
+                raise RuntimeError(f"tile(s) died: {dead} (see {logdir}/tile*.err)")
+            if time.time() - t0 > timeout:
+                raise RuntimeError(f"timeout after {timeout} s")
+            if time.time() - last >= 10.0:
+                print(f"  run: {time.time() - t0:.0f} s", file=sys.stderr, flush=True)
+                last = time.time()
+            time.sleep(0.2)
+        out = prod.stdout.read()
         if prod.returncode:
-            raise RuntimeError(f"producer rc {prod.returncode}: {err[-2000:]}")
-        for p in procs:
+            raise RuntimeError(f"producer rc {prod.returncode} (see {logdir}/producer.err)")
+        for t, p in enumerate(procs):
             p.wait(timeout=60)
             if p.returncode:
-                raise RuntimeError(f"tile rc {p.returncode}: {p.stderr.read()[-2000:]}")
+                raise RuntimeError(f"tile {t} rc {p.returncode} (see {logdir}/tile{t}.err)")
         return json.loads(out.strip().splitlines()[-1])
     finally:
         for p in procs + [prod]:
             if p.poll() is None:
                 p.kill()
                 p.wait()
+        for f in terr + [perr]:
+            f.close()
         if os.path.exists(shm):
             os.unlink(shm)
 
@@ -97,11 +118,13 @@ def main():
     ap.add_argument("--build", action="store_true")
     ap.add_argument("--frags", type=int, default=1 << 21)
     ap.add_argument("--tiles", default="6")
-    ap.add_argument("--configs", default="b4096i2")
+    ap.add_argument("--configs", default="b4096i2",
+                    help="b<batch_max>i<inflight>[p<poll_ns>], comma-separated (binaries from --build)")
     ap.add_argument("--in-depth", type=int, default=16384,
                     help="quic_verify mcache depth (config tiles.verify.receive_buffer_size, default.toml:1153)")
     ap.add_argument("--repeat", type=int, default=1)
-    ap.add_argument("--timeout", type=float, default=300)
+    ap.add_argument("--timeout", type=float, default=150)
+    ap.add_argument("--logdir", default=os.path.join(REPO, "gpurun_out", "tile_bench_logs"))
     args = ap.parse_args()
     if args.build:
         build()
@@ -110,14 +133,16 @@ def main():
         stream = os.path.join(td, "stream.bin")
         t = time.time()
         s = make_stream(args.frags, stream)
-        print(f"stream: {s.n} frags, {s.n_records} signatures, {time.time() - t:.1f} s", file=sys.stderr)
+        print(f"stream: {s.n} frags, {s.n_records} signatures, {time.time() - t:.1f} s", file=sys.stderr, flush=True)
         best = None
         for cfg in args.configs.split(","):
-            b, i = cfg[1:].split("i")
-            exe = binary(int(b), int(i))
+            b, rest = cfg[1:].split("i")
+            i, p = (rest.split("p") + ["2000"])[:2]
+            exe = binary(int(b), int(i), int(p))
             for tiles in (int(x) for x in args.tiles.split(",")):
                 for r in range(args.repeat):
-                    res = run_one(exe, stream, tiles, args.in_depth, args.timeout)
+                    res = run_one(exe, stream, tiles, args.in_depth, args.timeout,
+                                  os.path.join(args.logdir, f"{cfg}_t{tiles}_{r}"))
                     res["config"] = cfg
                     print(json.dumps(res), flush=True)
                     if best is None or res["verifies_per_s"] > best["verifies_per_s"]:
