@@ -1601,6 +1601,8 @@ struct fd_replay_hip {
   u8 *    d_nsig; u32 * d_sig_at; u32 * d_acct_at; u32 * d_msg_at; u32 * d_msg_sz;
   u32 *   d_first; u8 * d_cnt; signed char * d_tcode; u32 * d_counter; u32 * h_counter;
   u8 *    d_rsig; u8 * d_rpub; u32 * d_rmoff; u32 * d_rmsz; signed char * d_rcode;
+  u8 *    d_hpool; fd_txn_hip_desc_t * d_hdesc; int * d_hres;   /* fd_replay_hip_txn_verify_host staging */
+  ulong   hpool_cap;
   hipEvent_t ev_last; int ev_used;   /* calls on different streams run in call order over this scratch */
 };
 
@@ -1620,6 +1622,11 @@ fd_replay_hip_new( fd_ed25519_hip_ctx_t * ctx, ulong max_txn ) {
   TX_CHECK( hipMalloc( &r->d_rsig, 64*rc ) );   TX_CHECK( hipMalloc( &r->d_rpub, 32*rc ) );
   TX_CHECK( hipMalloc( &r->d_rmoff, 4*rc ) );   TX_CHECK( hipMalloc( &r->d_rmsz, 4*rc ) );
   TX_CHECK( hipMalloc( &r->d_rcode, rc ) );
+  r->hpool_cap = (ulong)FD_REPLAY_HIP_TXN_MTU * n;
+  TX_CHECK( hipMalloc( &r->d_hpool, r->hpool_cap + 16ul ) );
+  TX_CHECK( hipMemset( r->d_hpool, 0, r->hpool_cap + 16ul ) );   /* the 16-byte read-past tail is defined */
+  TX_CHECK( hipMalloc( &r->d_hdesc, sizeof(fd_txn_hip_desc_t)*n ) );
+  TX_CHECK( hipMalloc( &r->d_hres, 4*n ) );
   TX_CHECK( hipEventCreateWithFlags( &r->ev_last, hipEventDisableTiming ) );
   return r;
 }
@@ -1636,6 +1643,7 @@ fd_replay_hip_delete( fd_replay_hip_t * r ) {
   (void)hipFree( r->d_counter ); (void)hipHostFree( r->h_counter );
   (void)hipFree( r->d_rsig ); (void)hipFree( r->d_rpub ); (void)hipFree( r->d_rmoff ); (void)hipFree( r->d_rmsz );
   (void)hipFree( r->d_rcode );
+  (void)hipFree( r->d_hpool ); (void)hipFree( r->d_hdesc ); (void)hipFree( r->d_hres );
   free( r );
 }
 
@@ -1663,6 +1671,33 @@ fd_replay_hip_txn_verify_dev( fd_replay_hip_t * r, ulong n, uchar const * d_pool
   TX_CHECK( hipGetLastError() );
   TX_CHECK( hipEventRecord( r->ev_last, st ) );
   r->ev_used = 1;
+  return 0;
+}
+
+extern "C" int
+fd_replay_hip_txn_verify_host( fd_replay_hip_t * r, ulong n, uchar const * h_pool, ulong pool_sz,
+                               fd_txn_hip_desc_t const * h_desc, int * h_result, void * stream ) {
+  if( n > r->max_txn || pool_sz > r->hpool_cap ) return -1;
+  for( ulong j=0; j<n; j++ )          /* every span inside the staged pool (k_desc_spans trusts them) */
+    if( (ulong)h_desc[j].payload_off + h_desc[j].payload_sz > pool_sz ) return -1;
+  if( !n ) return 0;
+  hipStream_t st = stream ? (hipStream_t)stream : (hipStream_t)fd_ed25519_hip_ctx_stream( r->ctx );
+  TX_CHECK( hipSetDevice( fd_ed25519_hip_ctx_device( r->ctx ) ) );
+  if( r->ev_used ) TX_CHECK( hipStreamWaitEvent( st, r->ev_last, 0 ) );
+  TX_CHECK( hipMemcpyAsync( r->d_hpool, h_pool, pool_sz, hipMemcpyHostToDevice, st ) );
+  TX_CHECK( hipMemcpyAsync( r->d_hdesc, h_desc, sizeof(fd_txn_hip_desc_t)*n, hipMemcpyHostToDevice, st ) );
+  int rc = fd_replay_hip_txn_verify_dev( r, n, r->d_hpool, r->d_hdesc, r->d_hres, st );
+  if( rc ) return rc;
+  TX_CHECK( hipMemcpyAsync( h_result, r->d_hres, 4*n, hipMemcpyDeviceToHost, st ) );
+  TX_CHECK( hipEventRecord( r->ev_last, st ) );
+  return 0;
+}
+
+extern "C" int
+fd_replay_hip_wait( fd_replay_hip_t * r ) {
+  if( !r->ev_used ) return 0;
+  TX_CHECK( hipSetDevice( fd_ed25519_hip_ctx_device( r->ctx ) ) );
+  TX_CHECK( hipEventSynchronize( r->ev_last ) );
   return 0;
 }
 

@@ -29,6 +29,7 @@ FD_RUNTIME_TXN_ERR_SIGNATURE_FAILURE = -13
 
 # Every symbol include/fd_replay_hip.h declares (checked by tests/test_abi.py).
 EXPORTS = ("fd_replay_hip_new", "fd_replay_hip_delete", "fd_replay_hip_txn_verify_dev", "fd_replay_hip_poll",
+           "fd_replay_hip_txn_verify_host", "fd_replay_hip_wait",
            "fd_fec_hip_verify_roots_dev", "fd_precompile_hip_new", "fd_precompile_hip_delete",
            "fd_precompile_hip_ed25519_verify_dev")
 
@@ -70,6 +71,10 @@ def lib():
         L.fd_replay_hip_txn_verify_dev.argtypes = [vp, u64, vp, vp, vp, vp]
         L.fd_replay_hip_poll.restype = c.c_int
         L.fd_replay_hip_poll.argtypes = [vp]
+        L.fd_replay_hip_txn_verify_host.restype = c.c_int
+        L.fd_replay_hip_txn_verify_host.argtypes = [vp, u64, vp, u64, vp, vp, vp]
+        L.fd_replay_hip_wait.restype = c.c_int
+        L.fd_replay_hip_wait.argtypes = [vp]
         L.fd_fec_hip_verify_roots_dev.restype = c.c_int
         L.fd_fec_hip_verify_roots_dev.argtypes = [vp, u64, vp, vp, vp, vp, vp]
         L.fd_precompile_hip_new.restype = vp
@@ -116,10 +121,29 @@ class ReplayVerifier:
         if rc:
             raise ValueError(f"fd_replay_hip_txn_verify_dev: n={n} > max_txn={self.max_txn}")
 
+    def txn_verify_host(self, n, pool, desc, result, stream=None):
+        """fd_replay_hip_txn_verify_host: pool / desc / result are host numpy
+        arrays (uint8, DESC_DTYPE[n], int32[n]) that must stay alive and
+        untouched until poll() == 1 or wait().  Raises on a rejected call."""
+        n = int(n)
+        for a, nm in ((pool, "pool"), (desc, "desc"), (result, "result")):
+            if not (isinstance(a, np.ndarray) and a.flags.c_contiguous):
+                raise TypeError(f"{nm}: contiguous numpy array required")
+        if desc.dtype != DESC_DTYPE or desc.size < n or result.dtype != np.int32 or result.size < n:
+            raise ValueError("desc must be DESC_DTYPE[n], result int32[n]")
+        with self.verifier._stream(stream) as h:
+            rc = self._lib.fd_replay_hip_txn_verify_host(self.r, n, pool.ctypes.data, pool.nbytes, desc.ctypes.data,
+                                                          result.ctypes.data, h)
+        if rc:
+            raise ValueError(f"fd_replay_hip_txn_verify_host rejected n={n} pool_sz={pool.nbytes}")
+
     def poll(self):
-        """fd_replay_hip_poll: 1 when the last txn_verify_dev is done, 0 while
-        it runs, -1 before any call."""
+        """fd_replay_hip_poll: 1 when the last txn_verify_dev / _host is done,
+        0 while it runs, -1 before any call."""
         return self._lib.fd_replay_hip_poll(self.r)
+
+    def wait(self):
+        self._lib.fd_replay_hip_wait(self.r)
 
     def close(self):
         if self.r:

@@ -48,9 +48,9 @@ def _size(n, e, v0, d):
     return 1 + 64 * n + (4 if v0 else 3) + 1 + 32 * (n + e) + 32 + 1 + 1 + 1 + e + len(_cu16(d)) + d + (37 if v0 else 0)
 
 
-def _shape(rng, n, large):
+def _shape(rng, n, large, v0_frac=0.10):
     """(extra accounts e, v0, data size d) for a txn with n signers that fits the MTU."""
-    e, v0, d = 2, bool(rng.random() < 0.10), 9
+    e, v0, d = 2, bool(rng.random() < v0_frac), 9
     while _size(n, e, v0, d) > MTU:
         if v0:
             v0 = False
@@ -74,12 +74,16 @@ def _nsig(rng, k):
                                                                 rng.integers(7, 13, k)))).astype(np.int64)
 
 
-def make_txn_stream(n_txn, signer, seed=0x5eed0004, mix="c2", dup_frac=0.01, graft_frac=0.001, bad_frac=0.005):
-    """Build n_txn frags; signer(prvs[m,32], pool, msg_off, msg_sz) -> (pubs, sigs)."""
+def make_txn_stream(n_txn, signer, seed=0x5eed0004, mix="c2", dup_frac=0.01, graft_frac=0.001, bad_frac=0.005,
+                    v0_frac=0.10):
+    """Build n_txn frags; signer(prvs[m,32], pool, msg_off, msg_sz) -> (pubs, sigs).
+    mix "c2" applies the C2 mutation model, anything else keeps every
+    signature valid; v0_frac is the share of v0 txns (each with one
+    address-table lookup)."""
     rng = np.random.default_rng(seed)
     nsig = _nsig(rng, n_txn)
     large = rng.random(n_txn) < 0.25
-    shapes = [_shape(rng, int(nsig[t]), bool(large[t])) for t in range(n_txn)]
+    shapes = [_shape(rng, int(nsig[t]), bool(large[t]), v0_frac) for t in range(n_txn)]
     keys = np.array([(nsig[t], s[0], int(s[1]), s[2]) for t, s in enumerate(shapes)], np.int64)
     size = np.array([_size(int(k[0]), int(k[1]), bool(k[2]), int(k[3])) for k in keys], np.int64)
     off = np.zeros(n_txn, np.int64)

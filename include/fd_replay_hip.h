@@ -81,12 +81,38 @@ fd_replay_hip_txn_verify_dev( fd_replay_hip_t *         r,
                               int *                     d_result,
                               void *                    stream );
 
-/* Non-blocking completion check of the last fd_replay_hip_txn_verify_dev
-   call (its results are in d_result once this says so): 1 done, 0 still
+/* The same for a caller that holds the transactions in host memory (the
+   replay tile: fd_txn_p_t payloads it packs into h_pool, descriptors into
+   h_desc; integration/fd_replay_hip.patch).  Copies h_pool[0,pool_sz) and
+   h_desc[0,n) into device staging owned by r (pool_sz up to
+   FD_REPLAY_HIP_TXN_MTU * max_txn), verifies, and copies the n results into
+   h_result.  Asynchronous on stream (NULL: ctx's stream): h_pool, h_desc and
+   h_result must stay untouched until fd_replay_hip_poll returns 1 or
+   fd_replay_hip_wait returns; pinned host memory
+   (fd_ed25519_hip_host_alloc / _host_register) makes the copies DMA.
+   Returns 0, or -1 (nothing launched) if n > max_txn, pool_sz is over the
+   staging, or a descriptor's payload runs past pool_sz. */
+#define FD_REPLAY_HIP_TXN_MTU (1232UL)   /* FD_TXN_MTU, fd_txn.h:65 */
+
+int
+fd_replay_hip_txn_verify_host( fd_replay_hip_t *         r,
+                               ulong                     n,
+                               uchar const *             h_pool,
+                               ulong                     pool_sz,
+                               fd_txn_hip_desc_t const * h_desc,
+                               int *                     h_result,
+                               void *                    stream );
+
+/* Non-blocking completion check of the last fd_replay_hip_txn_verify_dev /
+   _host call (its results are in place once this says so): 1 done, 0 still
    running, -1 no call yet.  For a caller that polls from its run loop (the
-   replay tile's after_credit, integration/fd_replay_hip.patch). */
+   replay tile's after_credit). */
 int
 fd_replay_hip_poll( fd_replay_hip_t const * r );
+
+/* Blocks until the last call is done.  Returns 0. */
+int
+fd_replay_hip_wait( fd_replay_hip_t * r );
 
 /* ---- shred FEC-set roots ----------------------------------------------------
 

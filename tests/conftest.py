@@ -25,6 +25,7 @@ def pytest_sessionstart(session):
         subprocess.check_call(["make", "-s", "-j8", "-C", os.path.join(REPO, "oracle"), "oracle", "ref"])
         if os.path.exists(os.path.join(REPO, "firedancer_amd", "libfd_ed25519_hip.so")):
             subprocess.check_call(["make", "-s", "-j8", "-C", os.path.join(REPO, "oracle"), "tile"])
+            subprocess.check_call(["make", "-s", "-j8", "-C", os.path.join(REPO, "integration"), "all"])
 
 
 @pytest.fixture(scope="session")

@@ -1,0 +1,79 @@
+"""Block files for integration/sched_run.c (the reference's replay scheduler
+with integration/fd_replay_hip.patch) and its output.
+
+A block is the reference's entry-batch stream (fd_sched.c:1380-1420): each
+batch is a u64 microblock count, then per microblock an fd_microblock_hdr_t
+(src/ballet/block/fd_microblock.h:9-21: hash_cnt u64, hash[32], txn_cnt u64,
+packed, 48 bytes) followed by txn_cnt serialized transactions.  A batch is
+cut into FEC sets (fd_store_fec_t payloads) of at most fec_max bytes; a
+batch's last FEC set carries is_last_in_batch."""
+import os
+import struct
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+BUILD = os.path.join(os.path.dirname(HERE), "integration", "_build")
+REC_DTYPE = np.dtype([("sig0", "u1", (64,)), ("result", "<i4"), ("source", "u1"), ("_pad", "u1", (3,))])
+assert REC_DTYPE.itemsize == 72
+
+
+def block_fecs(pool, off, sz, txn_per_mblk=48, mblk_per_batch=16, fec_max=31840, seed=5):
+    """[(bytes, last_in_batch)] for the txns pool[off[i]:off[i]+sz[i]] in order."""
+    rng = np.random.default_rng(seed)
+    n, i, fecs = len(off), 0, []
+    while i < n:
+        parts, mb = [], 0
+        while i < n and mb < mblk_per_batch:
+            k = min(n - i, txn_per_mblk)
+            parts.append(struct.pack("<Q", int(rng.integers(1, 12500))) + rng.bytes(32) + struct.pack("<Q", k))
+            parts.extend(pool[int(off[j]):int(off[j]) + int(sz[j])].tobytes() for j in range(i, i + k))
+            i, mb = i + k, mb + 1
+        batch = struct.pack("<Q", mb) + b"".join(parts)
+        cuts = list(range(0, len(batch), fec_max))
+        for c in cuts:
+            fecs.append((batch[c:c + fec_max], c == cuts[-1]))
+    return fecs
+
+
+def write_block(path, fecs):
+    with open(path, "wb") as f:
+        f.write(b"FDB1" + struct.pack("<Q", len(fecs)))
+        for data, last in fecs:
+            f.write(struct.pack("<IB", len(data), int(last)) + data)
+
+
+def read_records(path):
+    with open(path, "rb") as f:
+        assert f.read(4) == b"FDR1"
+        (n,) = struct.unpack("<Q", f.read(8))
+        return np.frombuffer(f.read(n * REC_DTYPE.itemsize), REC_DTYPE)
+
+
+def run_sched(exe, jobs, tmp_dir, timeout=900):
+    """Runs sched_run over jobs (dicts: block, mode, and optionally exec_cnt,
+    record, batch_max, batch_min) in ONE process (the scheduler's memory is
+    set up once); returns [(JSON summary, sigverify records)] in job order."""
+    import json
+    lines, outs = [], []
+    for k, j in enumerate(jobs):
+        out = os.path.join(str(tmp_dir), f"job{k}.bin")
+        outs.append(out)
+        lines.append(" ".join(str(x) for x in (j["block"], j["mode"], j.get("exec_cnt", 4), int(j.get("record", 0)), out,
+                                               j.get("batch_max", 16384), j.get("batch_min", 256))))
+    jf = os.path.join(str(tmp_dir), "jobs.txt")
+    with open(jf, "w") as f:
+        f.write("\n".join(lines) + "\n")
+    r = subprocess.run([os.path.join(BUILD, exe), jf], capture_output=True, text=True, timeout=timeout)
+    assert r.returncode == 0, (r.returncode, r.stdout[-2000:], r.stderr[-4000:])
+    infos = [json.loads(l) for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(infos) == len(jobs), r.stdout[-2000:]
+    return [(i, read_records(o)) for i, o in zip(infos, outs)]
+
+
+def results_by_sig0(recs):
+    """{sig0 bytes: result} (the blocks' sig0 are unique)."""
+    d = {bytes(r["sig0"]): int(r["result"]) for r in recs}
+    assert len(d) == len(recs), "duplicate sig0 in the records"
+    return d

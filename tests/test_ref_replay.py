@@ -1,0 +1,124 @@
+"""CPU: integration/fd_replay_hip.patch against the reference's replay path.
+
+The patch gives the reference's scheduler (src/discof/replay/fd_sched.c) a
+bulk sigverify claim (fd_sched_sigverify_claim / _claim_done) and the replay
+tile (fd_replay_tile.c) an after_credit step that sends claimed
+transactions to the GPU in one batch (fd_replay_hip_txn_verify_host)
+instead of one FD_SCHED_TT_TXN_SIGVERIFY task per transaction to the exec
+tiles (fd_exec_tile.c:161 -> fd_executor_txn_verify, fd_executor.c:1607-1623).
+
+- The patched fd_replay_tile.c compiles against the reference headers with
+  FD_HAS_HIP 0 and 1 (-Wall -Wextra -Werror; integration/Makefile), and only
+  the FD_HAS_HIP object calls into the engine.
+- integration/sched_run.c drives the patched scheduler over one generated
+  block (FEC sets of entry batches, fd_sched_fec_ingest) with emulated exec
+  tiles: in "exec" mode sigverify runs as the reference runs it, in "claim"
+  mode through the patch's bulk claims, each transaction verified by the
+  reference's own fd_ed25519_verify_batch_single_msg (linked from its
+  sources).  Every transaction's result equals the oracle's restatement of
+  fd_executor_txn_verify, the block reaches its end with every counter
+  balanced, and a block with one bad signature is marked dead, abandoned and
+  drained (the scheduler's invariant checks abort the driver otherwise).
+The GPU half ("hip" mode, >= 10K-txn blocks) is tests/test_gpu_replay_block.py."""
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+import oracle_lib as O
+import txn_lib as T
+from replay_io import BUILD, block_fecs, results_by_sig0, run_sched, write_block
+
+pytestmark = pytest.mark.skipif(not os.path.exists(os.path.join(BUILD, "sched_run_ref")),
+                                reason="the replay drivers need /root/reference (built by build())")
+
+
+def expected_exec(pool, off, sz):
+    """{sig0: fd_executor_txn_verify result} restated on the oracle."""
+    from firedancer_amd.replay import descs_from_txn_t
+    tsz, out = T.oracle_parse_many(pool, off, sz)
+    assert (tsz > 0).all()
+    desc = descs_from_txn_t(out, off, sz)
+    exp = {}
+    for d in desc:
+        p = pool[int(d["payload_off"]):int(d["payload_off"]) + int(d["payload_sz"])]
+        so, mo, ao, cnt = int(d["signature_off"]), int(d["message_off"]), int(d["acct_addr_off"]), int(d["signature_cnt"])
+        code = O.verify_batch_single_msg(p[mo:].tobytes(), p[so:so + 64 * cnt].tobytes(), p[ao:ao + 32 * cnt].tobytes(),
+                                         cnt, errmode=O.ERRMODE_REF)
+        exp[p[so:so + 64].tobytes()] = 0 if code == 0 else -13
+    return exp
+
+
+def make_block(tmp_path, n, mix, seed, bad_at=None):
+    from firedancer_amd.txn_workload import make_txn_stream
+    s = make_txn_stream(n, T.oracle_signer, seed=seed, mix=mix, dup_frac=0.0, graft_frac=0.0, bad_frac=0.0,
+                        v0_frac=0.0)
+    pool = s.pool.copy()
+    if bad_at is not None:
+        pool[int(s.off[bad_at]) + 1 + 7] ^= 0x04          # signature 0's R
+    path = str(tmp_path / f"block_{seed}.bin")
+    write_block(path, block_fecs(pool, s.off, s.sz))
+    return path, pool, s
+
+
+@pytest.fixture(scope="module")
+def runs(tmp_path_factory):
+    """Every scenario in one driver process (fd_sched_new touches ~28 GiB)."""
+    d = tmp_path_factory.mktemp("replay")
+    mixed, mpool, ms = make_block(d, 1500, "c2", 0x7e91)           # ~40% of txns fail sigverify
+    valid, _, _ = make_block(d, 700, "none", 0x7e92)
+    bad, bpool, bs = make_block(d, 900, "none", 0x7e93, bad_at=450)
+    jobs = {("mixed", "exec"): dict(block=mixed, mode="exec", record=1, batch_max=256, batch_min=32),
+            ("mixed", "claim"): dict(block=mixed, mode="claim", record=1, batch_max=256, batch_min=32)}
+    for e in (1, 3, 8):
+        jobs[("valid", e)] = dict(block=valid, mode="claim", exec_cnt=e, batch_max=128, batch_min=16)
+    for m in ("exec", "claim"):
+        jobs[("bad", m)] = dict(block=bad, mode=m, batch_max=64, batch_min=8)
+    res = run_sched("sched_run_ref", list(jobs.values()), d)
+    out = dict(zip(jobs, res))
+    out["mixed_exp"] = expected_exec(mpool, ms.off, ms.sz)
+    out["mixed_stream"] = ms
+    out["bad_sig0"] = bpool[int(bs.off[450]) + 1:int(bs.off[450]) + 65].tobytes()
+    return out
+
+
+def test_patched_replay_tile_compiles_both_ways():
+    ref, hip = os.path.join(BUILD, "replay_tile_ref.o"), os.path.join(BUILD, "replay_tile_hip.o")
+    assert os.path.exists(ref) and os.path.exists(hip)
+    und = lambda o: subprocess.run(["nm", "-u", o], capture_output=True, text=True, check=True).stdout  # noqa: E731
+    u_ref, u_hip = und(ref), und(hip)
+    assert "fd_replay_hip" not in u_ref and "fd_sched_sigverify_claim" not in u_ref
+    for s in ("fd_replay_hip_new", "fd_replay_hip_txn_verify_host", "fd_replay_hip_poll", "fd_sched_sigverify_claim",
+              "fd_sched_sigverify_claim_done", "fd_ed25519_hip_host_alloc"):
+        assert s in u_hip, s
+
+
+@pytest.mark.parametrize("mode", ["exec", "claim"])
+def test_every_txn_equals_reference(runs, mode):
+    info, recs = runs[("mixed", mode)]
+    exp, s = runs["mixed_exp"], runs["mixed_stream"]
+    assert info["block_ended"] == 1 and info["dead"] == 0 and info["refcnt"] == 0, info
+    assert results_by_sig0(recs) == exp
+    assert 0.3 < np.mean([v == 0 for v in exp.values()]) < 0.9
+    if mode == "claim":
+        assert info["bulk_batches"] >= 1500 // 256 and info["sigs_bulk"] > 0.5 * s.n_records, info
+    else:
+        assert info["bulk_batches"] == 0 and info["sigs_exec"] == s.n_records, info
+
+
+@pytest.mark.parametrize("exec_cnt", [1, 3, 8])
+def test_valid_block_completes_through_claims(runs, exec_cnt):
+    info, recs = runs[("valid", exec_cnt)]
+    assert info["block_ended"] == 1 and info["dead"] == 0 and info["refcnt"] == 0, info
+    assert info["sigverified"] == 700 and (recs["result"] == 0).all()
+    assert info["fec_ingested"] == info["fec_cnt"] and info["bulk_batches"] > 0
+
+
+@pytest.mark.parametrize("mode", ["exec", "claim"])
+def test_bad_signature_kills_the_block(runs, mode):
+    info, recs = runs[("bad", mode)]
+    assert info["dead"] == 1 and info["block_ended"] == 0, info
+    got = results_by_sig0(recs)
+    assert got.get(runs["bad_sig0"]) == -13
+    assert sum(v != 0 for v in got.values()) == 1
