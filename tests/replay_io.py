@@ -37,6 +37,35 @@ def block_fecs(pool, off, sz, txn_per_mblk=48, mblk_per_batch=16, fec_max=31840,
     return fecs
 
 
+def distinct_accounts(pool, off, sz):
+    """Mask of the legacy txns whose account addresses are pairwise distinct.
+    The C2 mutation model can give two signers of one txn the same
+    small-order key; a txn that names an account twice never sanitizes on
+    chain, and the reference's dispatcher (fd_rdisp) waits on itself for it,
+    so such txns stay out of generated blocks."""
+    keep = np.ones(len(off), bool)
+    for i, (o, z) in enumerate(zip(off, sz)):
+        p = pool[int(o):int(o) + int(z)]
+        n = int(p[0])
+        cnt = int(p[1 + 64 * n + 3])
+        a = p[1 + 64 * n + 4:1 + 64 * n + 4 + 32 * cnt].reshape(cnt, 32)
+        keep[i] = len(np.unique(a, axis=0)) == cnt
+    return keep
+
+
+def block_stream(n, signer, seed, mix, bad_at=None):
+    """(pool, off, sz, signatures): n generated legacy txns (1-12 signers,
+    mix "c2" or all valid) minus those naming an account twice, in block
+    order; bad_at flips a bit of that txn's first signature."""
+    from firedancer_amd.txn_workload import make_txn_stream
+    s = make_txn_stream(n, signer, seed=seed, mix=mix, dup_frac=0.0, graft_frac=0.0, bad_frac=0.0, v0_frac=0.0)
+    keep = distinct_accounts(s.pool, s.off, s.sz)
+    off, sz, pool = s.off[keep], s.sz[keep], s.pool.copy()
+    if bad_at is not None:
+        pool[int(off[bad_at]) + 1 + 7] ^= 0x04
+    return pool, off, sz, int(pool[off.astype(np.int64)].astype(np.int64).sum())
+
+
 def write_block(path, fecs):
     with open(path, "wb") as f:
         f.write(b"FDB1" + struct.pack("<Q", len(fecs)))

@@ -79,14 +79,13 @@ def main():
         out["fail_frac"] = float((h_res != 0).mean())
         rv.close()
         if args.sched:
-            from replay_io import block_fecs, run_sched, write_block
+            from replay_io import block_fecs, block_stream, run_sched, write_block
             with tempfile.TemporaryDirectory() as td:
-                s2 = make_txn_stream(n, gpu_signer(v), seed=0x7e70 + n, mix="none", dup_frac=0.0, graft_frac=0.0,
-                                     bad_frac=0.0, v0_frac=0.0)
+                pool2, off2, sz2, sigs2 = block_stream(n, gpu_signer(v), 0x7e70 + n, "none")
                 bp = os.path.join(td, "block.bin")
-                write_block(bp, block_fecs(s2.pool, s2.off, s2.sz))
+                write_block(bp, block_fecs(pool2, off2, sz2))
                 (info, _), = run_sched("sched_run_hip", [dict(block=bp, mode="hip", exec_cnt=8)], td)
-                out["sched"] = {"seconds": info["seconds"], "sig_per_s": s2.n_records / info["seconds"],
+                out["sched"] = {"txns": len(off2), "seconds": info["seconds"], "sig_per_s": sigs2 / info["seconds"],
                                 "bulk_batches": info["bulk_batches"], "bulk_max": info["bulk_max"],
                                 "sigs_bulk": info["sigs_bulk"], "sigs_exec": info["sigs_exec"],
                                 "block_ended": info["block_ended"]}
