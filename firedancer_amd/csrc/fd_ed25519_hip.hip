@@ -964,20 +964,18 @@ DEV void lat_chain( ge_p3 & P, u32 const * tab, u32 const * ident, u32 kd[8], u3
   }
 }
 
-/* the XCD (XCC) this workgroup runs on: hwreg(HW_REG_XCC_ID, 0, 4) */
-DEV u32 xcc_id( void ) { return (u32)__builtin_amdgcn_s_getreg( (3 << 11) | (0 << 6) | 20 ); }
-
-
-/* copies > 1: each signature gets that many consecutive workgroups, which the
-   dispatcher deals to different XCDs, all computing the same verdict; the
-   first to finish writes the code and tags done[i] with this call's seq, and
-   the others stop at their next window.  A lone call's time depends on
-   where the dispatcher places it (measured 415-1068 us per call, repeating
-   with period 8 as single-workgroup launches rotate over the XCDs; the shader
-   clock is the same 2.39 GHz on every launch, tools/xcd_clock); racing one
-   copy per XCD takes the fastest.  Every copy writes the same code, so a tie
-   is harmless, and done[] is only an early-exit hint: the host reads the
-   codes after the whole launch. */
+/* copies > 1: each signature gets that many consecutive workgroups (the
+   dispatcher deals consecutive workgroups to the XCDs in turn, so they land
+   on different CUs), all computing the same verdict; the first to finish
+   writes the code and tags done[i] with this call's seq, and the others stop
+   at their next window.  A lone workgroup is fast or slow by the state of
+   the CU it lands on (415-1068 us per call for one copy; the shader clock is
+   the same 2.39 GHz on every launch, tools/xcd_clock; profiles/r03k, r03x),
+   so racing copies takes the fastest: up to ctx->lat_copies
+   (LAT_COPIES_MAX, 16) per signature, at most one workgroup per CU over the
+   whole call and within the context's lat_cus budget (verify_impl).  Every
+   copy writes the same code, so a tie is harmless, and done[] is only an
+   early-exit hint: the host reads the codes after the whole launch. */
 __global__ __launch_bounds__(LAT_WG)
 void k_verify_lat( ulong n, uchar const * __restrict__ sigs, uchar const * __restrict__ pubs,
                    uchar const * __restrict__ pool, uint const * __restrict__ moff, uint const * __restrict__ msz,
@@ -1505,8 +1503,8 @@ verify_impl( fd_ed25519_hip_ctx_t * ctx, ulong n, uchar const * d_sigs, uchar co
   if( ctx->ev_used ) FD_CHECK( hipStreamWaitEvent( s, ctx->ev_last, 0 ) );   /* previous call's scratch use */
   if( !d_n && n <= ctx->lat_max && n <= ctx->chunk && !ctx->timing ) {
     /* small batch: one workgroup per signature (k_verify_lat), racing as
-       many copies as the context's workgroup-slot budget holds, up to one
-       per XCD */
+       many copies as the context's workgroup-slot budget holds, up to
+       lat_copies and one workgroup per CU */
     u32 copies = 1u;
     {
       ulong c = ctx->lat_cus / n;
@@ -1850,7 +1848,12 @@ static void slots_setup( void ) {
     char const * lc = getenv( "FD_ED25519_HIP_DROPIN_LAT_CUS" );   /* A/B override of the share */
     c->lat_cus = lc ? (ulong)atol( lc ) : c->lat_cus / (ulong)g_slots;
     if( !c->lat_cus ) c->lat_cus = 1ul;
-    c->lat_max = c->lat_cus < LAT_MAX_N ? c->lat_cus : LAT_MAX_N;
+    /* combined drop-in batches of up to lat_cus records (256 on a 256-CU
+       part with 4 slots) take the latency path; FD_ED25519_HIP_DROPIN_LAT_MAX
+       overrides (A/B against LAT_DEFAULT_N: INTEGRATION.md §1) */
+    char const * lm = getenv( "FD_ED25519_HIP_DROPIN_LAT_MAX" );
+    c->lat_max = lm ? (ulong)atol( lm ) : c->lat_cus;
+    if( c->lat_max > LAT_MAX_N ) c->lat_max = LAT_MAX_N;
     g_slot_ctx[j] = c;
   }
 }
@@ -1934,10 +1937,14 @@ dropin_run( uchar const * msg, ulong msg_sz, uchar const * sigs, uchar const * p
       g_open = f;
     }
     b = &g_stage[g_open];
-    if( b->n + n <= DROPIN_REC_MAX && STAGE_MSG + b->pool + need <= b->cap ) break;
+    /* the records' message offsets are 32-bit (off[] below): a block's pool
+       stays under 2^32 bytes, and a caller that would pass it closes the
+       block (an empty block always fits: need <= DROPIN_MSG_MAX + 31) */
+    if( b->n + n <= DROPIN_REC_MAX && STAGE_MSG + b->pool + need <= b->cap && b->pool + need <= (ulong)UINT32_MAX ) break;
     if( !b->n ) {                                          /* empty and too small: grow it */
-      ulong cap = STAGE_MSG + need;
-      stage_grow( ctx, b, cap > 2ul*b->cap ? cap : 2ul*b->cap );
+      ulong cap = STAGE_MSG + need, dbl = 2ul*b->cap;
+      if( dbl > STAGE_MSG + (ulong)UINT32_MAX ) dbl = STAGE_MSG + (ulong)UINT32_MAX;
+      stage_grow( ctx, b, cap > dbl ? cap : dbl );
       break;
     }
     /* full: it runs as soon as a slot is free (one of its callers starts

@@ -146,9 +146,10 @@ void                   fd_ed25519_hip_set_halfsize( fd_ed25519_hip_ctx_t * ctx, 
 /* Calls of at most max_n records (default 32, at most 256) whose count is
    known on the host run on the latency path: one workgroup of three waves per
    signature (the A and R decodes, the hash, and the [k1]A, [k2]R and B terms
-   run side by side; each signature races copies on other XCDs as far as the
-   context's budget, fd_ed25519_hip_set_lat_cus, allows), instead of one lane
-   per signature through k_verify_prep / k_verify_dsm.  Same verdicts and
+   run side by side; each signature races copies on other CUs, up to 16 and
+   one workgroup per CU over the call, as far as the context's budget,
+   fd_ed25519_hip_set_lat_cus, allows), instead of one lane per signature
+   through k_verify_prep / k_verify_dsm.  Same verdicts and
    codes; 0 sends every call to the bulk kernels.  The drop-in entry points
    run on their own batch-slot contexts.  A latency call's n x copies
    workgroups each hold a quarter of a CU until they end (a 32-record call
@@ -159,14 +160,19 @@ void                   fd_ed25519_hip_set_small_batch( fd_ed25519_hip_ctx_t * ct
 
 /* k_verify_lat workgroup slots a latency-path call may fill with racing
    copies (default: all of them, 4 per CU; the drop-in's batch slots each get
-   1/slots): a call of n records runs min(slots / n, one per XCD) copies of
-   each signature, at least one. */
+   1/slots, and take calls of up to that many records, at most 256, on the
+   latency path): a call of n records runs min(cus / n, 16, CUs / n) copies
+   of each signature, at least one. */
 void                   fd_ed25519_hip_set_lat_cus( fd_ed25519_hip_ctx_t * ctx, ulong cus );
 
 /* Recreates the context's stream restricted to the CUs whose bits are set in
    mask[0..words) (hipExtStreamCreateWithCUMask numbering; words 0: all CUs
    again).  Work already queued on the old stream is drained first.  Returns
-   0, or -1 if the runtime refused the mask. */
+   0, or -1 if the runtime refused the mask.  A masked stream is a BLOCKING
+   stream (hipExtStreamCreateWithCUMask takes no flags): unlike the default
+   non-blocking context stream it synchronises with work on the null stream
+   (e.g. torch's legacy default stream), so keep such work off the null
+   stream while a masked context is busy. */
 int                    fd_ed25519_hip_ctx_set_cu_mask( fd_ed25519_hip_ctx_t * ctx, uint const * mask, uint words );
 
 /* k_verify_dsm runs a persistent grid sized to every resident workgroup

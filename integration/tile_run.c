@@ -21,13 +21,20 @@
          reference link is unreliable and would drop frags past its depth; a
          throughput bench must not), and prints one JSON line once every
          tile is done.
-     tile_run tile <shm> <tile_idx>
+     tile_run tile <shm> <tile_idx>      (TILE_RUN_WALK=1: walk mode, below)
          Verify tile tile_idx: the mock topology around the shared in link
          (tile_drv.c's shape, src/disco/verify/test_verify_tile.c:45-85),
          privileged_init (HIP context, GPU tile_idx % device count),
          unprivileged_init, then stem_run1 (src/disco/stem/fd_stem.c) with
          the patched callbacks until its share of the stream is published
          or dropped and nothing is left on the GPU.
+
+   Walk mode (environment TILE_RUN_WALK=1 on the tiles): each tile's round
+   robin count is set past every seq, so before_frag filters every frag and
+   the tile only walks the link (mcache poll, before_frag, fseq updates)
+   until its in-link fseq reaches the stream's end: the rate at which ONE
+   consumer can walk the shared quic_verify link, which bounds every verify
+   tile of the fan-out (each walks all frags of the link).
 
    Stream file: "FDT1" u64 n, u64 seed, u64 tcache_depth, per frag u64
    bundle_id, u16 payload_sz, payload bytes (oracle/tile_drv.c's format). */
@@ -36,6 +43,9 @@
 static int drv_should_shutdown( void * ctx );
 #define STEM_CALLBACK_SHOULD_SHUTDOWN( ctx ) drv_should_shutdown( ctx )
 #include TILE_SRC
+static int     drv_walk;            /* TILE_RUN_WALK: filter every frag, shut down at the link's end */
+static ulong * drv_in_fseq;
+static ulong   drv_n;
 #include "../topo/fd_topob.h"
 #include "../metrics/fd_metrics.h"
 #include "../../tango/fseq/fd_fseq.h"
@@ -253,6 +263,10 @@ drv_should_shutdown( void * _ctx ) {
   static ulong calls;                                           /* every stem iteration: look every 64th */
   if( FD_LIKELY( (++calls) & 63UL ) ) return 0;
   fd_verify_ctx_t * ctx = (fd_verify_ctx_t *)_ctx;
+  if( drv_walk ) {
+    if( FD_UNLIKELY( fd_log_wallclock()>drv_deadline ) ) FD_LOG_ERR(( "walk: not at the end after the deadline" ));
+    return fd_fseq_query( drv_in_fseq )>=drv_n;
+  }
   ulong m[ 6 ];
   fd_verify_hip_tile_metrics( ctx->hip_tile, m );
   ulong seen = m[0] + m[1] + m[2] + m[3] + m[4];            /* parse, verify, dedup, bundle failures, published */
@@ -305,6 +319,8 @@ tile( char const * path, ulong t ) {
   ctx->hashmap_seed = hdr->seed + t;                            /* fixed per tile: runs are reproducible */
   unprivileged_init( topo, tile );
   ctx->round_robin_cnt = hdr->tile_cnt; ctx->round_robin_idx = t;
+  drv_walk = !!getenv( "TILE_RUN_WALK" );
+  if( drv_walk ) ctx->round_robin_cnt = ULONG_MAX;              /* seq % cnt == seq: only seq t would pass, t < tile_cnt */
   drv_ctx   = ctx;
   drv_share = hdr->n/hdr->tile_cnt + (t<hdr->n%hdr->tile_cnt ? 1UL : 0UL);
 
@@ -316,6 +332,7 @@ tile( char const * path, ulong t ) {
   void * stem_scratch = aligned_alloc( FD_STEM_SCRATCH_ALIGN,
                                        fd_ulong_align_up( stem_scratch_footprint( 1UL, 1UL, 1UL ), FD_STEM_SCRATCH_ALIGN ) );
   ulong * in_fseq = fd_fseq_join( base + hdr->fseq_off + t*hdr->fseq_stride );
+  drv_in_fseq = in_fseq; drv_n = hdr->n;
   uchar cons_mem[ 256 ] __attribute__((aligned(128)));
   FD_TEST( fd_fseq_footprint()<=sizeof(cons_mem) );
   ulong * cons_fseq = fd_fseq_join( fd_fseq_new( cons_mem, STEM_SHUTDOWN_SEQ ) );

@@ -107,10 +107,28 @@ def test_mismatched_prototype_is_rejected(tmp_path):
     assert r.returncode != 0 and "conflicting types" in r.stderr, r.stderr
 
 
-def test_with_hip_mk_present():
-    """The build-side plug a maintainer drops into config/extra/ (INTEGRATION.md 1)."""
-    mk = open(os.path.join(REPO, "integration", "with-hip.mk")).read()
-    assert "FD_HAS_HIP" in mk and "-lfd_ed25519_hip" in mk
+def _plug_flags(mode):
+    """CPPFLAGS integration/with-hip.mk sets for FD_HIP_PLUG=mode (make -p of a
+    Makefile that includes it)."""
+    mk = os.path.join(REPO, "integration", "with-hip.mk")
+    r = subprocess.run(["make", "-s", "-f", "-", f"FD_HIP_PLUG={mode}", "FD_HIP_ENGINE=" + REPO, "show"],
+                       input=f"include {mk}\nshow:\n\t@echo $(CPPFLAGS)\n", capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr
+    return r.stdout.split()
+
+
+def test_with_hip_mk_modes():
+    """The build-side plug a maintainer drops into config/extra/ (INTEGRATION.md 1):
+    selective by default (batch callers only), full on request, anything
+    else refused."""
+    sel, full = _plug_flags("selective"), _plug_flags("full")
+    assert "-DFD_HAS_HIP=1" in sel and not any("DROPIN" in f for f in sel)
+    assert "-DFD_HAS_HIP=1" in full and "-DFD_HAS_HIP_DROPIN=1" in full
+    mk = os.path.join(REPO, "integration", "with-hip.mk")
+    r = subprocess.run(["make", "-s", "-f", "-", "FD_HIP_PLUG=bogus", "show"],
+                       input=f"include {mk}\nshow:\n\t@echo $(CPPFLAGS)\n", capture_output=True, text=True)
+    assert r.returncode != 0 and "FD_HIP_PLUG" in r.stderr
+    assert "-lfd_ed25519_hip" in open(mk).read()
 
 
 PLUG_MAIN = r"""
@@ -141,38 +159,94 @@ REF_OBJS = ["ballet/ed25519/fd_curve25519.o", "ballet/ed25519/fd_curve25519_scal
             "ballet/sha512/fd_sha512_core_avx2.o"]
 
 
-def test_patched_reference_links_engine(tmp_path):
-    """integration/fd_ed25519_user_hip.patch applied to a temporary copy of the
-    reference's fd_ed25519_user.c, compiled with -DFD_HAS_HIP=1 next to the
-    reference's other verify-path objects (oracle/Makefile's build of the
-    reference sources): the program links with no duplicate or missing symbol,
-    the reference's CPU signer runs, and fd_ed25519_verify / strerror resolve
-    to libfd_ed25519_hip.so."""
-    ref_o = os.path.join(REPO, "oracle", "_ref", "avx512")
-    if not all(os.path.exists(os.path.join(ref_o, o)) for o in REF_OBJS):
-        pytest.skip("oracle/_ref reference objects not built")
-    build()
+PLUG_SELECTIVE = r"""
+#define _GNU_SOURCE
+#include "ballet/ed25519/fd_ed25519.h"
+#include "fd_replay_hip.h"
+#include <dlfcn.h>
+#include <stdio.h>
+#include <string.h>
+int
+main( void ) {
+  /* the reference's CPU verify stays in the program and answers the
+     latency-bound callers ... */
+  uchar prv[32], pub[32], sig[64], msg[3] = { 1, 2, 3 };
+  fd_sha512_t sha[1];
+  memset( prv, 7, 32 );
+  fd_ed25519_public_from_private( pub, prv, sha );
+  fd_ed25519_sign( sig, msg, 3, pub, prv, sha );
+  int ok  = fd_ed25519_verify( msg, 3, sig, pub, sha );
+  sig[5] ^= 1;
+  int bad = fd_ed25519_verify( msg, 3, sig, pub, sha );
+  /* ... while the batch callers' entry points come from the engine */
+  Dl_info a, b;
+  if( !dladdr( (void *)fd_ed25519_verify, &a ) || !dladdr( (void *)fd_replay_hip_txn_verify_host, &b ) ) return 2;
+  char const * an = strrchr( a.dli_fname, '/' ), * bn = strrchr( b.dli_fname, '/' );
+  printf( "%s|%s|%d|%d\n", an ? an+1 : a.dli_fname, bn ? bn+1 : b.dli_fname, ok, bad );
+  return 0;
+}
+"""
+
+
+def _patched_user_o(tmp_path, defs):
     src_dir = tmp_path / "src" / "ballet" / "ed25519"
-    src_dir.mkdir(parents=True)
+    src_dir.mkdir(parents=True, exist_ok=True)
     user_c = src_dir / "fd_ed25519_user.c"
     user_c.write_text(open(os.path.join(REF_SRC, "ballet", "ed25519", "fd_ed25519_user.c")).read())
     subprocess.check_call(["patch", "-s", "-p1", "-d", str(tmp_path), "-i",
                            os.path.join(REPO, "integration", "fd_ed25519_user_hip.patch")])
-    flags = ["-O2", "-ffunction-sections", "-fdata-sections"] + MACHINE + ["-DFD_HAS_HIP=1", "-w", "-I", REF_SRC,
-                                                                          "-I", str(src_dir)]
+    flags = ["-O2", "-ffunction-sections", "-fdata-sections"] + MACHINE + defs + ["-w", "-I", REF_SRC, "-I", str(src_dir)]
     # the patched file includes its siblings by relative path: compile it from the reference tree's view
     obj = tmp_path / "user.o"
     subprocess.check_call(["gcc"] + flags + ["-iquote", os.path.join(REF_SRC, "ballet", "ed25519"), "-c",
                                              str(user_c), "-o", str(obj)])
+    return flags, obj
+
+
+def _link_run(tmp_path, flags, obj, main_src, ref_o):
     main_c = tmp_path / "main.c"
-    main_c.write_text(PLUG_MAIN)
+    main_c.write_text(main_src)
     exe = tmp_path / "plug"
     libdir = os.path.dirname(LIB)
-    r = subprocess.run(["gcc"] + flags + [str(main_c), str(obj)] + [os.path.join(ref_o, o) for o in REF_OBJS] +
+    r = subprocess.run(["gcc"] + flags + ["-I", os.path.join(REPO, "include"), str(main_c), str(obj)] +
+                       [os.path.join(ref_o, o) for o in REF_OBJS] +
                        ["-Wl,--gc-sections",   # as oracle/Makefile: drop the unreferenced fd_log users
                         "-L", libdir, "-lfd_ed25519_hip", "-ldl", "-Wl,-rpath-link,/opt/rocm/lib",
                         "-Wl,-rpath," + libdir, "-o", str(exe)], capture_output=True, text=True)
     assert r.returncode == 0, r.stderr
-    out = subprocess.check_output([str(exe)]).decode().strip().split("|")
+    return subprocess.check_output([str(exe)]).decode().strip().split("|")
+
+
+def test_patched_reference_links_engine(tmp_path):
+    """Full plug (FD_HIP_PLUG=full: -DFD_HAS_HIP=1 -DFD_HAS_HIP_DROPIN=1):
+    integration/fd_ed25519_user_hip.patch applied to a temporary copy of the
+    reference's fd_ed25519_user.c, compiled next to the reference's other
+    verify-path objects (oracle/Makefile's build of the reference sources):
+    the program links with no duplicate or missing symbol, the reference's
+    CPU signer runs, and fd_ed25519_verify / strerror resolve to
+    libfd_ed25519_hip.so."""
+    ref_o = os.path.join(REPO, "oracle", "_ref", "avx512")
+    if not all(os.path.exists(os.path.join(ref_o, o)) for o in REF_OBJS):
+        pytest.skip("oracle/_ref reference objects not built")
+    build()
+    flags, obj = _patched_user_o(tmp_path, ["-DFD_HAS_HIP=1", "-DFD_HAS_HIP_DROPIN=1"])
+    out = _link_run(tmp_path, flags, obj, PLUG_MAIN, ref_o)
     assert out[0] == "libfd_ed25519_hip.so" and out[1] == "libfd_ed25519_hip.so", out
     assert out[2] == "bad signature"
+
+
+def test_selective_plug_keeps_cpu_verify(tmp_path):
+    """Selective plug (the default, FD_HIP_PLUG=selective: -DFD_HAS_HIP=1
+    alone): the same patched file keeps the reference's fd_ed25519_verify,
+    which the program resolves to itself and which verifies on the CPU
+    (SUCCESS, then ERR_MSG for a flipped signature bit, fd_ed25519.h:29-32),
+    while the batch callers' engine entry points resolve to
+    libfd_ed25519_hip.so; no GPU call is made."""
+    ref_o = os.path.join(REPO, "oracle", "_ref", "avx512")
+    if not all(os.path.exists(os.path.join(ref_o, o)) for o in REF_OBJS):
+        pytest.skip("oracle/_ref reference objects not built")
+    build()
+    flags, obj = _patched_user_o(tmp_path, ["-DFD_HAS_HIP=1"])
+    out = _link_run(tmp_path, flags, obj, PLUG_SELECTIVE, ref_o)
+    assert out[0] == "plug" and out[1] == "libfd_ed25519_hip.so", out
+    assert out[2] == "0" and int(out[3]) < 0, out

@@ -16,7 +16,10 @@
 #                      SQ group, FETCH_SIZE, WRITE_SIZE, TCC/GRBM (one pass each)
 #   c4pmc[:args]       VALU issue + FETCH_SIZE + WRITE_SIZE passes over the C4 bench
 #   tile[:args]        python tools/tile_bench.py <args>        -> tile_<n>.json
+#   replay[:args]      python tools/replay_block_bench.py <args> -> replay_<n>.json
 #   smoke              __graft_entry__.smoke()
+# (It replaces the round-3 per-session scripts tools/run_r03*.sh and the
+# one-off A/B runners; they are in git history before this file's commit.)
 # Every GPU step runs under its own timeout; a failure ends the session.
 set -o pipefail
 export TMPDIR=/tmp
@@ -58,7 +61,7 @@ for step in "$@"; do
       python3 -c "import json; d=json.load(open('$O/ab_$n.json')); print('ab [$a]', d['value'], d.get('batch_gpu_ms'))" ;;
     stats)
       timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d $O/stats_$n -o run -- \
-          python3 bench.py --contexts 1 $a > $O/stats_$n.json 2> $O/stats_$n.err || fail stats $? $O/stats_$n.err
+          python3 bench.py --contexts 1 --no-c4 $a > $O/stats_$n.json 2> $O/stats_$n.err || fail stats $? $O/stats_$n.err
       echo "stats ok" ;;
     c4stats)
       timeout -k 10 900 rocprofv3 --kernel-trace --stats --output-format csv -d $O/c4stats_$n -o run -- \
@@ -66,7 +69,7 @@ for step in "$@"; do
           > $O/c4stats_$n.json 2> $O/c4stats_$n.err || fail c4stats $? $O/c4stats_$n.err
       echo "c4stats ok" ;;
     pmc)
-      B="python3 bench.py --contexts 1 --no-cpu-baseline --steps 2 --warmup 1"
+      B="python3 bench.py --contexts 1 --no-c4 --no-cpu-baseline --steps 2 --warmup 1"
       pmc_pass pmc_valu "$VALU_G" $B
       pmc_pass pmc_sq "$SQ_G" $B
       pmc_pass pmc_fetch "FETCH_SIZE" $B
@@ -80,6 +83,10 @@ for step in "$@"; do
     tile)
       timeout -k 10 900 python3 tools/tile_bench.py $a > $O/tile_$n.json 2> $O/tile_$n.err || fail tile $? $O/tile_$n.err
       tail -c 600 $O/tile_$n.json ;;
+    replay)
+      timeout -k 10 600 python3 -u tools/replay_block_bench.py $a > $O/replay_$n.json 2> $O/replay_$n.err \
+          || fail replay $? $O/replay_$n.err
+      cut -c1-600 $O/replay_$n.json ;;
     smoke)
       timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.txt 2>&1 || fail smoke $? $O/smoke.txt
       tail -2 $O/smoke.txt ;;

@@ -17,7 +17,7 @@ for f in sorted(glob.glob(os.path.join(d, "p*", "**", "*counter_collection.csv")
     for r in csv.DictReader(open(f)):
         k = r["Kernel_Name"].split("(")[0]
         acc[k][r["Counter_Name"]].append(float(r["Counter_Value"]))
-res = {"source": "rocprofv3 --pmc (one counter group per run) on: python3 bench.py --contexts 1 --no-cpu-baseline --steps 2 "
+res = {"source": "rocprofv3 --pmc (one counter group per run) on: python3 bench.py --contexts 1 --no-c4 --no-cpu-baseline --steps 2 "
                  "--warmup 1; values are means per dispatch", "kernels": {}}
 for k in ("k_verify_prep", "k_verify_dsm"):
     if k not in acc:

@@ -63,7 +63,7 @@ def make_stream(n, path, seed=0x5eed0004, depth=4194302):
     return s
 
 
-def run_one(exe, stream, tiles, in_depth, timeout, logdir):
+def run_one(exe, stream, tiles, in_depth, timeout, logdir, walk=False):
     """One producer and `tiles` tile processes; every process's stderr goes to
     a file in logdir; liveness is checked every second (a tile that dies ends
     the run at once), with a progress line on stderr."""
@@ -82,7 +82,8 @@ def run_one(exe, stream, tiles, in_depth, timeout, logdir):
             raise RuntimeError(f"producer: {line!r} (see {logdir}/producer.err)")
         for t in range(tiles):
             terr.append(open(os.path.join(logdir, f"tile{t}.err"), "w"))
-            procs.append(subprocess.Popen([exe, "tile", shm, str(t)], stdout=subprocess.DEVNULL, stderr=terr[-1]))
+            env = dict(os.environ, TILE_RUN_WALK="1") if walk else None
+            procs.append(subprocess.Popen([exe, "tile", shm, str(t)], stdout=subprocess.DEVNULL, stderr=terr[-1], env=env))
         last = 0.0
         while prod.poll() is None:
             dead = [(t, p.returncode) for t, p in enumerate(procs) if p.poll() is not None and p.returncode]
@@ -123,6 +124,8 @@ def main():
     ap.add_argument("--in-depth", type=int, default=16384,
                     help="quic_verify mcache depth (config tiles.verify.receive_buffer_size, default.toml:1153)")
     ap.add_argument("--repeat", type=int, default=1)
+    ap.add_argument("--walk", action="store_true",
+                    help="also time walk mode per tile count: tiles filter every frag (tile_run.c), the link-walk bound")
     ap.add_argument("--timeout", type=float, default=150)
     ap.add_argument("--logdir", default=os.path.join(REPO, "gpurun_out", "tile_bench_logs"))
     args = ap.parse_args()
@@ -135,6 +138,14 @@ def main():
         s = make_stream(args.frags, stream)
         print(f"stream: {s.n} frags, {s.n_records} signatures, {time.time() - t:.1f} s", file=sys.stderr, flush=True)
         best = None
+        if args.walk:
+            exe = binary(4096, 2)
+            for tiles in (int(x) for x in args.tiles.split(",")):
+                res = run_one(exe, stream, tiles, args.in_depth, args.timeout,
+                              os.path.join(args.logdir, f"walk_t{tiles}"), walk=True)
+                print(json.dumps({"walk": True, "tile_cnt": tiles, "frags": s.n, "seconds": res["seconds"],
+                                  "frags_walked_per_s": s.n / res["seconds"], "regime": res.get("regime"),
+                                  "in_depth": args.in_depth}), flush=True)
         for cfg in args.configs.split(","):
             b, rest = cfg[1:].split("i")
             i, p = (rest.split("p") + ["2000"])[:2]
