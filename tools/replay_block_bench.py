@@ -12,7 +12,10 @@ mutation model, GPU-signed), one JSON line each:
   sched      (--sched) the whole block through the reference's scheduler
              with integration/fd_replay_hip.patch (integration/sched_run.c,
              hip mode): FEC ingest, parse, claims, packing, GPU batches,
-             retirement -- one host thread, as the replay tile
+             retirement -- one host thread, as the replay tile; skip_seconds
+             is the same loop with claimed txns passed unverified (the
+             scheduler's own cost), so seconds - skip_seconds is what GPU
+             sigverify adds to the replay thread
 sig/s = signatures in the block / seconds (median over --reps).
 usage: python tools/replay_block_bench.py [--txns 16384,98039] [--reps 20] [--sched]"""
 import argparse
@@ -84,8 +87,10 @@ def main():
                 pool2, off2, sz2, sigs2 = block_stream(n, gpu_signer(v), 0x7e70 + n, "none")
                 bp = os.path.join(td, "block.bin")
                 write_block(bp, block_fecs(pool2, off2, sz2))
-                (info, _), = run_sched("sched_run_hip", [dict(block=bp, mode="hip", exec_cnt=8)], td)
-                out["sched"] = {"txns": len(off2), "seconds": info["seconds"], "sig_per_s": sigs2 / info["seconds"],
+                (skip, _), (info, _) = run_sched("sched_run_hip", [dict(block=bp, mode="skip", exec_cnt=8),
+                                                                   dict(block=bp, mode="hip", exec_cnt=8)], td)
+                out["sched"] = {"txns": len(off2), "sigs": sigs2, "seconds": info["seconds"],
+                                "sig_per_s": sigs2 / info["seconds"], "skip_seconds": skip["seconds"],
                                 "bulk_batches": info["bulk_batches"], "bulk_max": info["bulk_max"],
                                 "sigs_bulk": info["sigs_bulk"], "sigs_exec": info["sigs_exec"],
                                 "block_ended": info["block_ended"]}
