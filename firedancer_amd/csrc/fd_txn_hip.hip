@@ -399,10 +399,10 @@ void k_txnm_ingest( ulong n, u8 const * in, u32 const * __restrict__ in_chunk,
   u32 lane = threadIdx.x & 63u;
   ulong w = ((ulong)blockIdx.x * blockDim.x + threadIdx.x) >> 6, nw = ((ulong)gridDim.x * blockDim.x) >> 6;
   for( ulong j = w; j < n; j += nw ) {
-    u8 const * src = in + 64ul * in_chunk[j];
     u32 ob = 64u * out_chunk[j];
     u8 * dst = out + ob;
     u32 sz = in_sz[j], kind = in_kind[j], psz = 0u, bad = 0u;
+    u8 const * src = (kind & FD_VERIFY_HIP_IN_HOSTCOPY) ? dst : in + 64ul * in_chunk[j];   /* host did during_frag */
     u64 b = 0ul;
     if( kind == FD_VERIFY_HIP_IN_GOSSIP ) {
       u64 tsz = *(u64 const *)(src + FD_VERIFY_HIP_GOSSIP_VOTE_TXN_SZ_OFF);
@@ -711,9 +711,11 @@ void k_txnm_batch( ulong n, u8 const * in, u32 const * __restrict__ in_chunk, u1
   bool const fl = lane < nf;
   ulong const j = j0 + lane;
   u32 ic = 0u, oc = 0u, sz = 0u, kind = 0u;
-  if( fl ) { ic = in_chunk[j]; oc = out_chunk[j]; sz = in_sz[j]; kind = in_kind[j]; }
-  u8 const * src = in + 64ul * ic;
+  if( fl ) { oc = out_chunk[j]; sz = in_sz[j]; kind = in_kind[j]; }
+  if( fl && !(kind & FD_VERIFY_HIP_IN_HOSTCOPY) ) ic = in_chunk[j];
   u8 *       dst = out + 64ul * oc;
+  u8 const * src = (kind & FD_VERIFY_HIP_IN_HOSTCOPY) ? (u8 const *)dst : in + 64ul * ic;   /* host did during_frag */
+  u32 const src_lo = (u32)(u64)src, src_hi = (u32)((u64)src >> 32);
   bool const gossip = fl && kind == FD_VERIFY_HIP_IN_GOSSIP;
   u32 tsz_g = 0u;
   if( __ballot( gossip ) && gossip ) {
@@ -761,12 +763,12 @@ void k_txnm_batch( ulong n, u8 const * in, u32 const * __restrict__ in_chunk, u1
     for( int r = 0; r < FB_LB; r++ ) {
       u32 q = q0 + 64u * (u32)r + lane;
       u32 f = group_of<F>( excl, q < tot ? q : 0u );
-      u32 fic = __shfl( ic, (int)f ), foc = __shfl( oc, (int)f ), flo = __shfl( lo, (int)f );
-      u32 fce = __shfl( cend, (int)f ), fex = __shfl( excl, (int)f );
+      u32 fsl = __shfl( src_lo, (int)f ), fsh = __shfl( src_hi, (int)f ), foc = __shfl( oc, (int)f );
+      u32 flo = __shfl( lo, (int)f ), fce = __shfl( cend, (int)f ), fex = __shfl( excl, (int)f );
       u32 b = flo + 16u * (q - fex);                                         /* byte offset in the frag */
       da[r] = out + 64ul * foc + b;
       ce[r] = q < tot ? (fce > b ? fce - b : 0u) : 0u;                       /* bytes of this piece to copy */
-      if( q < tot ) v[r] = *(uint4 const *)(in + 64ul * fic + b);
+      if( q < tot ) v[r] = *(uint4 const *)((u8 const *)(((u64)fsh << 32) | (u64)fsl) + b);
     }
     #pragma unroll
     for( int r = 0; r < FB_LB; r++ ) {
@@ -1137,7 +1139,7 @@ __global__ __launch_bounds__(256)
 void k_tile_results( ulong n, u16 const * __restrict__ tsz, signed char const * __restrict__ tcode,
                      u64 const * __restrict__ tag, u64 const * __restrict__ bid, u8 const * __restrict__ kind,
                      u32 const * __restrict__ counter, u32 const * __restrict__ flag, u32 n_seg,
-                     u8 * __restrict__ res );
+                     u8 const * __restrict__ out, u32 const * __restrict__ out_chunk, u8 * __restrict__ res );
 
 /* a slot's record buffers at their bound and the results kernel loaded (a
    tile is created in privileged_init: its sandboxed steady state allocates
@@ -1145,7 +1147,8 @@ void k_tile_results( ulong n, u16 const * __restrict__ tsz, signed char const * 
 static void slot_warm( tile_slot & s, ulong max_txn, hipStream_t st ) {
   slot_records( s, 12ul*(max_txn + SLOT_SEG_SLACK) );
   hipLaunchKernelGGL( k_tile_results, dim3( 1 ), dim3( 64 ), 0, st, 0ul, s.d_tsz, s.d_tcode, s.d_tag,
-                      (u64 const *)0, (u8 const *)0, s.d_counter, (u32 const *)0, 0u, s.d_res );
+                      (u64 const *)0, (u8 const *)0, s.d_counter, (u32 const *)0, 0u, (u8 const *)0,
+                      (u32 const *)0, s.d_res );
   TX_CHECK( hipGetLastError() );
 }
 
@@ -1261,7 +1264,7 @@ __global__ __launch_bounds__(256)
 void k_tile_results( ulong n, u16 const * __restrict__ tsz, signed char const * __restrict__ tcode,
                      u64 const * __restrict__ tag, u64 const * __restrict__ bid, u8 const * __restrict__ kind,
                      u32 const * __restrict__ counter, u32 const * __restrict__ flag, u32 n_seg,
-                     u8 * __restrict__ res ) {
+                     u8 const * __restrict__ out, u32 const * __restrict__ out_chunk, u8 * __restrict__ res ) {
   ulong j = (ulong)blockIdx.x * blockDim.x + threadIdx.x;
   if( j == 0ul ) {
     ((u32 *)res)[0] = *counter; ((u32 *)res)[1] = flag ? *flag : 0u;
@@ -1275,7 +1278,9 @@ void k_tile_results( ulong n, u16 const * __restrict__ tsz, signed char const * 
   if( j >= n ) return;
   tile_res r;
   r.tag = tag[j]; r.bid = bid ? bid[j] : 0ul; r.tsz = tsz[j]; r.tcode = tcode[j]; r.kind = kind ? kind[j] : 0u;
-  r.pad = 0u;
+  /* frag mode: the out header's payload_sz (after the GPU's own during_frag),
+     for the caller's fd_txn_m_realized_footprint */
+  r.pad = out ? (u32)*(u16 const *)(out + 64ul*out_chunk[j] + FD_VERIFY_HIP_TXNM_PAYLOAD_SZ_OFF) : 0u;
   *(tile_res *)(res + TILE_RES_HDR + 24ul*j) = r;
 }
 
@@ -1305,10 +1310,12 @@ submit_verify( fd_verify_hip_tile_t * t, tile_slot & s, hipStream_t st, ulong n,
 }
 
 static void
-submit_results( tile_slot & s, hipStream_t st, ulong n, uchar const * d_in_kind ) {
+submit_results( tile_slot & s, hipStream_t st, ulong n, uchar const * d_in_kind, uchar const * d_out = 0,
+                uint const * d_out_chunk = 0 ) {
   hipLaunchKernelGGL( k_tile_results, dim3( (unsigned)((n + 255)/256) ), dim3( 256 ), 0, st, n, s.d_tsz, s.d_tcode,
                       s.d_tag, s.frags ? s.d_bid : (u64 const *)0, (u8 const *)d_in_kind, s.d_counter,
-                      s.frags ? s.d_flag : (u32 const *)0, s.n_seg, s.d_res );
+                      s.frags ? s.d_flag : (u32 const *)0, s.n_seg, (u8 const *)d_out, (u32 const *)d_out_chunk,
+                      s.d_res );
   TX_CHECK( hipGetLastError() );
   TX_CHECK( hipMemcpyAsync( s.h_res, s.d_res, TILE_RES_HDR + 24ul*n, hipMemcpyDeviceToHost, st ) );
 }
@@ -1399,7 +1406,7 @@ fd_verify_hip_tile_submit_frags( fd_verify_hip_tile_t * t, ulong n, uchar const 
     }
     fd_ed25519_hip_group_reduce_dev( s.ctx, n, s.d_first, s.d_cnt, s.d_rcode, s.d_tcode, st );
   }
-  submit_results( s, st, n, d_in_kind );
+  submit_results( s, st, n, d_in_kind, d_out, d_out_chunk );
   TX_CHECK( hipEventRecord( s.ev_done, st ) );
   return 0;
 }
@@ -1444,16 +1451,18 @@ fd_verify_hip_tile_set_inflight( fd_verify_hip_tile_t * t, ulong k ) {
   return 0;
 }
 
-extern "C" int
-fd_verify_hip_tile_complete( fd_verify_hip_tile_t * t, ulong const * bundle_id, signed char * result,
-                             ulong * tag_out, ushort * txn_t_sz ) {
+static int
+tile_complete( fd_verify_hip_tile_t * t, ulong const * bundle_id, uchar const * skip, signed char * result,
+               ulong * tag_out, ushort * txn_t_sz, ushort * payload_sz = 0 ) {
   if( t->completed == t->submitted ) return -1;
   tile_slot & s = t->slot[t->completed % t->nslot];
   TX_CHECK( hipSetDevice( fd_ed25519_hip_ctx_device( t->ctx ) ) );
   TX_CHECK( hipEventSynchronize( s.ev_done ) );
   u32 const * hdr = (u32 const *)s.h_res;
   tile_res const * R = (tile_res const *)(s.h_res + TILE_RES_HDR);
-  if( s.frags && s.n && hdr[1] ) {
+  int skipped = 0;
+  if( skip ) for( ulong j = 0; j < s.n; j++ ) skipped |= !!skip[j];
+  if( s.frags && s.n && hdr[1] && !skipped ) {
     /* during_frag's FD_LOG_ERR (fd_verify_tile.c:75-85): a corrupt frag kills the tile */
     fprintf( stderr, "fd_verify_hip: corrupt frag in batch (size beyond FD_TPU_RAW_MTU / 2048 or payload_sz "
                      "beyond FD_TPU_MTU)\n" );
@@ -1472,8 +1481,15 @@ fd_verify_hip_tile_complete( fd_verify_hip_tile_t * t, ulong const * bundle_id, 
   const ulong PF = 8;
   for( ulong j = 0; j < n && j < PF; j++ ) __builtin_prefetch( map + (R[j].tag & mask) );
   for( ulong j = 0; j < n; j++ ) {
+    if( payload_sz ) payload_sz[j] = (ushort)R[j].pad;
+    if( skip && skip[j] ) {                                  /* overrun: the stem never calls after_frag */
+      if( txn_t_sz ) txn_t_sz[j] = 0;
+      if( tag_out ) tag_out[j] = 0;
+      result[j] = FD_VERIFY_HIP_FRAG_OVERRUN;
+      continue;
+    }
     if( s.frags ) {                                          /* after_frag's first statement (:112) */
-      u32 k = R[j].kind;
+      u32 k = R[j].kind & ~FD_VERIFY_HIP_IN_HOSTCOPY;
       t->m_gossip += (k == FD_VERIFY_HIP_IN_GOSSIP) | (k == FD_VERIFY_HIP_IN_SEND);
     }
     if( j + PF < n ) {
@@ -1529,6 +1545,19 @@ fd_verify_hip_tile_complete( fd_verify_hip_tile_t * t, ulong const * bundle_id, 
   hist_sample( t->hist[1], (ulong)std::chrono::duration_cast<std::chrono::nanoseconds>( h1 - h0 ).count() );
   s.busy = 0; t->completed++;
   return 0;
+}
+
+extern "C" int
+fd_verify_hip_tile_complete( fd_verify_hip_tile_t * t, ulong const * bundle_id, signed char * result,
+                             ulong * tag_out, ushort * txn_t_sz ) {
+  return tile_complete( t, bundle_id, NULL, result, tag_out, txn_t_sz );
+}
+
+extern "C" int
+fd_verify_hip_tile_complete_skip( fd_verify_hip_tile_t * t, uchar const * skip, signed char * result,
+                                  ulong * tag_out, ushort * txn_t_sz, ushort * payload_sz ) {
+  if( !t->slot[t->completed % t->nslot].frags && t->completed != t->submitted ) return -1;   /* frag batches only */
+  return tile_complete( t, NULL, skip, result, tag_out, txn_t_sz, payload_sz );
 }
 
 extern "C" void fd_verify_hip_tile_set_ingest_timing( fd_verify_hip_tile_t * t, int on ) { t->ingest_timing = !!on; }

@@ -36,6 +36,7 @@ EXPORTS = (
     "fd_verify_hip_tcache_reset", "fd_verify_hip_tcache_query", "fd_verify_hip_tcache_insert",
     "fd_verify_hip_tile_new", "fd_verify_hip_tile_join_tcache", "fd_verify_hip_tile_tcache_reset",
     "fd_verify_hip_tile_delete", "fd_verify_hip_tile_set_seed", "fd_verify_hip_tile_submit", "fd_verify_hip_tile_complete",
+    "fd_verify_hip_tile_complete_skip",
     "fd_verify_hip_tile_metrics", "fd_verify_hip_tile_metrics2", "fd_verify_hip_tile_last_timing", "fd_verify_hip_tile_submit_frags",
     "fd_verify_hip_before_frag", "fd_verify_hip_hist_edges", "fd_verify_hip_tile_hist_init",
     "fd_verify_hip_tile_hist", "fd_verify_hip_tile_poll", "fd_verify_hip_tile_inflight",
@@ -48,6 +49,8 @@ TXNM_SZ, TXNM_PAYLOAD_SZ_OFF, TXNM_TXN_T_SZ_OFF, TXNM_SRC_IPV4_OFF, TXNM_SRC_TPU
 TPU_RAW_MTU, TPU_SOURCE_GOSSIP = 1312, 3
 GOSSIP_UPDATE_TAG_VOTE, GOSSIP_VOTE_ADDR_OFF, GOSSIP_VOTE_TXN_SZ_OFF, GOSSIP_VOTE_TXN_OFF = 3, 56, 72, 80
 IN_QUIC, IN_BUNDLE, IN_GOSSIP, IN_SEND = 0, 1, 2, 3
+IN_HOSTCOPY = 0x80      # or'd into a kind: the host did during_frag's copy into the out chunk
+FRAG_OVERRUN = -5       # complete_skip's result for a skipped (overrun) frag
 
 _bound = False
 
@@ -84,6 +87,8 @@ def lib():
         L.fd_verify_hip_tile_inflight.restype = u64
         L.fd_verify_hip_tile_inflight.argtypes = [vp]
         L.fd_verify_hip_tile_complete.argtypes = [vp, vp, vp, vp, vp]
+        L.fd_verify_hip_tile_complete_skip.restype = c.c_int
+        L.fd_verify_hip_tile_complete_skip.argtypes = [vp, vp, vp, vp, vp, vp]
         L.fd_verify_hip_tile_metrics.argtypes = [vp, vp]
         L.fd_verify_hip_tile_metrics2.argtypes = [vp, vp]
         L.fd_verify_hip_tile_last_timing.argtypes = [vp, vp]
@@ -230,6 +235,22 @@ class VerifyTile:
                                                    result.ctypes.data, tag.ctypes.data, tsz.ctypes.data)
         if rc:
             raise RuntimeError(f"fd_verify_hip_tile_complete: {rc}")
+        return result, tag, tsz
+
+    def complete_skip(self, skip):
+        """complete() with skip[j] != 0 frags treated as overrun (FRAG_OVERRUN)."""
+        n, _keep = self._pending.pop(0)
+        skip = np.ascontiguousarray(skip, np.uint8)
+        assert skip.size >= n
+        result = np.zeros(n, np.int8)
+        tag = np.zeros(n, np.uint64)
+        tsz = np.zeros(n, np.uint16)
+        psz = np.zeros(n, np.uint16)
+        rc = self._lib.fd_verify_hip_tile_complete_skip(self.tile, skip.ctypes.data, result.ctypes.data,
+                                                        tag.ctypes.data, tsz.ctypes.data, psz.ctypes.data)
+        if rc:
+            raise RuntimeError(f"fd_verify_hip_tile_complete_skip: {rc}")
+        self.last_payload_sz = psz
         return result, tag, tsz
 
     def after_frags(self, n, pool, txn_off, txn_sz, bundle_id=None, txn_out=None):

@@ -61,6 +61,7 @@ typedef unsigned short ushort;
 #define FD_VERIFY_HIP_FRAG_DEDUP        (-2)   /* metrics.dedup_fail_cnt       */
 #define FD_VERIFY_HIP_FRAG_PARSE_FAIL   (-3)   /* metrics.parse_fail_cnt       */
 #define FD_VERIFY_HIP_FRAG_BUNDLE_PEER  (-4)   /* metrics.bundle_peer_fail_cnt */
+#define FD_VERIFY_HIP_FRAG_OVERRUN      (-5)   /* skipped by complete_skip: the stem's overrun (no after_frag) */
 
 /* ---- verify-tile frag formats (x86-64 layouts of the reference structs;
    tests/test_ref_layout.py checks every offset against the reference headers
@@ -90,6 +91,12 @@ typedef unsigned short ushort;
 #define FD_VERIFY_HIP_IN_BUNDLE 1u
 #define FD_VERIFY_HIP_IN_GOSSIP 2u
 #define FD_VERIFY_HIP_IN_SEND   3u
+/* or'd into a QUIC / BUNDLE / SEND kind: the host tile did during_frag's
+   copy into the frag's out chunk itself (a frag of a link the GPU does not
+   map); d_in_chunk[j] is ignored and the frag is parsed in place (GOSSIP |
+   HOSTCOPY: the host converted the vote into an fd_txn_m_t already; it
+   still counts as a gossiped vote). */
+#define FD_VERIFY_HIP_IN_HOSTCOPY 0x80u
 
 /* before_frag (fd_verify_tile.c:37-58) on the host: 1 = this tile skips
    the frag (round robin over verify tiles by seq; bundles to tile 0;
@@ -196,9 +203,11 @@ fd_verify_hip_tile_submit( fd_verify_hip_tile_t * tile,
    fd_txn_t at fd_txn_m_txn_t and txn_t_sz into the header.  bundle_id comes
    from each header (complete's bundle_id argument is ignored for such a
    batch) and GOSSIP/SEND frags count into gossiped_votes_cnt (:112).
-   A QUIC/BUNDLE/SEND frag whose in and out addresses are the same is parsed
-   in place (no copy): a host tile that keeps during_frag's copy into its out
-   dcache passes in = out.
+   A QUIC/BUNDLE/SEND frag whose in and out addresses are the same, or whose
+   kind carries FD_VERIFY_HIP_IN_HOSTCOPY, is parsed in place (no copy): a
+   host tile that keeps during_frag's copy into its out dcache passes in =
+   out, or the flag for the frags it copied while the GPU copies the others
+   from d_in (integration/fd_verify_tile_hip.patch, FD_VERIFY_HIP_GPU_COPY).
    A corrupt frag (sz > FD_TPU_RAW_MTU, or > 2048 for gossip; payload_sz >
    FD_TPU_MTU) aborts the process in complete(), as the reference's
    FD_LOG_ERR ends the tile.  All pointers are device-visible (HBM, or
@@ -245,6 +254,28 @@ fd_verify_hip_tile_complete( fd_verify_hip_tile_t * tile,
                              signed char *          result,      /* host, n */
                              ulong *                tag,         /* host, n or NULL */
                              ushort *               txn_t_sz );  /* host, n or NULL */
+
+/* complete() for a frag batch of which the caller found some frags overrun
+   after the GPU read them (skip[j] != 0: the in-link's mcache line of the
+   frag's seq was overwritten by then, so its bytes may be a later frag's --
+   the GPU-copy form of the stem's overrun check after during_frag,
+   integration/fd_verify_tile_hip.patch FD_VERIFY_HIP_GPU_COPY).  A skipped
+   frag gets FD_VERIFY_HIP_FRAG_OVERRUN and is invisible to the ordered pass
+   (no tcache query or insert, no bundle state, no metric), as a frag the
+   stem drops never reaches after_frag.  A batch with a skipped frag does
+   not abort on the corrupt-frag flag (the corrupt bytes may be the
+   overrun's; a corrupt frag that is not skipped parses as a parse failure
+   and is not published).  payload_sz[j] is the frag's out header
+   payload_sz after the GPU's during_frag (for fd_txn_m_realized_footprint
+   without reading the header back).  Frag batches only: -1 for a
+   fd_verify_hip_tile_submit batch. */
+int
+fd_verify_hip_tile_complete_skip( fd_verify_hip_tile_t * tile,
+                                  uchar const *          skip,         /* host, n (NULL: none skipped) */
+                                  signed char *          result,       /* host, n */
+                                  ulong *                tag,          /* host, n or NULL */
+                                  ushort *               txn_t_sz,     /* host, n or NULL */
+                                  ushort *               payload_sz ); /* host, n or NULL */
 
 /* metrics (cumulative): out[0..3] = parse_fail, verify_fail, dedup_fail,
    bundle_peer_fail (fd_verify_tile.h:51-57); out[4] = published,

@@ -10,6 +10,9 @@
      claim  the patch's bulk path (fd_sched_sigverify_claim / _claim_done),
             each claimed batch verified by the same reference CPU function:
             checks the scheduler half of the patch without a GPU
+     skip   the bulk path with every claimed transaction passed unverified:
+            the scheduler and driver loop alone (the cost the other modes
+            add to the replay thread is theirs minus this)
      hip    the patch's bulk path as the replay tile runs it
             (replay_hip_sigverify in fd_replay_tile.c): claimed batches
             packed into pinned buffers and verified by
@@ -22,7 +25,7 @@
    abandon) unless the run is in record mode, which keeps verifying so that
    every transaction's result can be compared.
 
-   usage: sched_run <fecs.bin> <exec|claim|hip> <exec_cnt> <record 0|1> <out.bin> [batch_max] [batch_min]
+   usage: sched_run <fecs.bin> <exec|claim|skip|hip> <exec_cnt> <record 0|1> <out.bin> [batch_max] [batch_min]
    fecs.bin : "FDB1" u64 fec_cnt, then per FEC set: u32 data_sz, u8 last_in_batch, data
               (one block, bank 1 on the snapshot root bank 0; the last FEC
               set is the block's last)
@@ -52,6 +55,7 @@ void fd_halt( void ) {}
 #define MODE_EXEC  0
 #define MODE_CLAIM 1
 #define MODE_HIP   2
+#define MODE_SKIP  3
 
 typedef struct { uchar sig0[ 64 ]; int result; uchar source; uchar pad[ 3 ]; } rec_t;
 FD_STATIC_ASSERT( sizeof(rec_t)==72UL, rec_layout );
@@ -141,6 +145,8 @@ bulk_sigverify( fd_sched_t * sched, bulk_t * b, int mode, ulong batch_min, ulong
   sigs_bulk += sigs; batches_bulk++; bulk_max = fd_ulong_max( bulk_max, cnt );
   if( mode==MODE_CLAIM ) {
     for( ulong j=0UL; j<cnt; j++ ) b->result[ j ] = txn_verify_ref( fd_sched_get_txn( sched, b->txn_idx[ j ] ) );
+  } else if( mode==MODE_SKIP ) {
+    for( ulong j=0UL; j<cnt; j++ ) b->result[ j ] = FD_RUNTIME_EXECUTE_SUCCESS;
   } else {
 #if FD_HAS_HIP
     ulong pool_sz = 0UL;
@@ -173,9 +179,9 @@ static void * sched_mem;
 
 static int
 run_job( char ** argv, int argc ) {
-  if( argc<5 ) { fprintf( stderr, "job: fecs.bin exec|claim|hip exec_cnt record out.bin [batch_max] [batch_min]\n" ); return 2; }
+  if( argc<5 ) { fprintf( stderr, "job: fecs.bin exec|claim|skip|hip exec_cnt record out.bin [batch_max] [batch_min]\n" ); return 2; }
   int mode = !strcmp( argv[1], "exec" ) ? MODE_EXEC : !strcmp( argv[1], "claim" ) ? MODE_CLAIM :
-             !strcmp( argv[1], "hip" ) ? MODE_HIP : -1;
+             !strcmp( argv[1], "hip" ) ? MODE_HIP : !strcmp( argv[1], "skip" ) ? MODE_SKIP : -1;
   FD_TEST( mode>=0 );
   ulong exec_cnt  = strtoul( argv[2], NULL, 0 );
   record_mode     = atoi( argv[3] );
@@ -345,7 +351,7 @@ int
 main( int argc, char ** argv ) {
   fd_boot( &argc, &argv );
   if( argc!=2 && argc<6 ) {
-    fprintf( stderr, "usage: %s fecs.bin exec|claim|hip exec_cnt record out.bin [batch_max] [batch_min]\n"
+    fprintf( stderr, "usage: %s fecs.bin exec|claim|skip|hip exec_cnt record out.bin [batch_max] [batch_min]\n"
                      "       %s jobs.txt   (one job per line, same fields)\n", argv[0], argv[0] );
     return 2;
   }

@@ -74,7 +74,7 @@ void fd_halt( void ) {}
 
 typedef struct {
   volatile long t_ready, t_end;
-  volatile ulong done, frags, sigs, pub, parse, verify, dedup, bundle;
+  volatile ulong done, frags, sigs, pub, parse, verify, dedup, bundle, overrun;
   volatile ulong batches;
   volatile double gpu_ms, host_ms;           /* sums over the tile's batches (fd_verify_hip_tile_hist sums) */
   volatile ulong regime[ 8 ];                /* the stem's REGIME_DURATION_NANOS ticks (fd_stem.c:406-712) */
@@ -200,13 +200,13 @@ produce( char const * path, char const * stream, ulong tile_cnt, ulong in_depth 
     FD_SPIN_PAUSE();
   }
   long t_end = t0; ulong sigs = 0UL, frags = 0UL, pub = 0UL, batches = 0UL, reg[ 8 ] = { 0UL };
-  ulong parse = 0UL, verify = 0UL, dedup = 0UL, bundle = 0UL; double gpu_ms = 0.0, host_ms = 0.0;
+  ulong parse = 0UL, verify = 0UL, dedup = 0UL, bundle = 0UL, overrun = 0UL; double gpu_ms = 0.0, host_ms = 0.0;
   printf( "{\"tiles\": [" );
   for( ulong t=0UL; t<tile_cnt; t++ ) {
     run_res_t * r = &hdr->res[ t ];
     t_end = fd_long_max( t_end, r->t_end );
     sigs += r->sigs; frags += r->frags; pub += r->pub; batches += r->batches;
-    parse += r->parse; verify += r->verify; dedup += r->dedup; bundle += r->bundle;
+    parse += r->parse; verify += r->verify; dedup += r->dedup; bundle += r->bundle; overrun += r->overrun;
     gpu_ms += r->gpu_ms; host_ms += r->host_ms;
     for( ulong k=0UL; k<8UL; k++ ) reg[ k ] += r->regime[ k ];
     printf( "%s{\"frags\": %lu, \"sigs\": %lu, \"published\": %lu, \"batches\": %lu, \"s\": %.6f, "
@@ -229,11 +229,11 @@ produce( char const * path, char const * stream, ulong tile_cnt, ulong in_depth 
           "\"dedup\": %lu, \"bundle_peer_fail\": %lu, \"seconds\": %.6f, \"publish_s\": %.6f, "
           "\"verifies_per_s\": %.1f, \"frags_per_s\": %.1f, \"batches\": %lu, \"gpu_ms_per_batch\": %.4f, "
           "\"host_ms_per_batch\": %.4f, \"batch_max\": %lu, \"batch_cap\": %lu, \"inflight\": %lu, "
-          "\"flush_ns\": %ld, \"in_depth\": %lu, \"tile_cnt\": %lu}\n",
+          "\"flush_ns\": %ld, \"in_depth\": %lu, \"tile_cnt\": %lu, \"overrun\": %lu, \"gpu_copy\": %d}\n",
           frags, sigs, pub, parse, verify, dedup, bundle, s, (double)( t_pub - t0 )*1e-9, (double)sigs/s,
           (double)frags/s, batches, batches ? gpu_ms/(double)batches : 0.0, batches ? host_ms/(double)batches : 0.0,
           FD_VERIFY_HIP_BATCH_MAX, FD_VERIFY_HIP_BATCH_CAP, FD_VERIFY_HIP_INFLIGHT, (long)FD_VERIFY_HIP_FLUSH_NS,
-          in_depth, tile_cnt );
+          in_depth, tile_cnt, overrun, (int)FD_VERIFY_HIP_GPU_COPY );
   fflush( stdout );
   munmap( base, map_sz );
   unlink( path );
@@ -269,7 +269,8 @@ drv_should_shutdown( void * _ctx ) {
   }
   ulong m[ 6 ];
   fd_verify_hip_tile_metrics( ctx->hip_tile, m );
-  ulong seen = m[0] + m[1] + m[2] + m[3] + m[4];            /* parse, verify, dedup, bundle failures, published */
+  ulong seen = m[0] + m[1] + m[2] + m[3] + m[4]             /* parse, verify, dedup, bundle failures, published */
+             + ctx->hip_overrun_cnt;                        /* and frags dropped as overrun after the GPU's read */
   if( FD_UNLIKELY( fd_log_wallclock()>drv_deadline ) ) FD_LOG_ERR(( "tile: %lu of %lu frags after the deadline", seen, drv_share ));
   return seen>=drv_share && FD_VERIFY_HIP_IDLE( ctx );
 }
@@ -361,7 +362,7 @@ tile( char const * path, ulong t ) {
   fd_verify_hip_tile_hist( ctx->hip_tile, 1, NULL, NULL, &sum_host );
   run_res_t * r = &hdr->res[ t ];
   r->t_end = t_end; r->frags = m[0] + m[1] + m[2] + m[3] + m[4]; r->sigs = m[5]; r->pub = m[4];
-  r->parse = m[0]; r->verify = m[1]; r->dedup = m[2]; r->bundle = m[3];
+  r->parse = m[0]; r->verify = m[1]; r->dedup = m[2]; r->bundle = m[3]; r->overrun = ctx->hip_overrun_cnt;
   r->batches = nb; r->gpu_ms = (double)sum_gpu*1e-6; r->host_ms = (double)sum_host*1e-6;
   for( ulong k=0UL; k<8UL; k++ ) r->regime[ k ] = fd_metrics_tl[ MIDX( COUNTER, TILE, REGIME_DURATION_NANOS ) + k ];
   FD_COMPILER_MFENCE();

@@ -265,6 +265,83 @@ def test_in_place_frags(stream):
     check(*r, exp_out, payloads, bids, spans, 13, 128, buf)
 
 
+def test_host_copied_and_gpu_copied_frags(stream):
+    """A batch mixing the two sources the patched tile uses with
+    FD_VERIFY_HIP_GPU_COPY: frags the host tile's during_frag already copied
+    into their out chunks (kind | FD_VERIFY_HIP_IN_HOSTCOPY, in chunk
+    garbage) and frags the GPU copies from the in dcache, gossip votes and
+    lying headers among them, against the restated reference, every group
+    size and the split form byte-equal."""
+    rng = np.random.default_rng(12)
+    s = stream
+    pays = _payloads(s)[:2000]
+    n = len(pays)
+    bid = np.zeros(n, np.uint64)
+    gossip = rng.random(n) < 0.1
+    hdr_psz = [min(1232, p.size + int(rng.integers(1, 100))) if j % 9 == 0 and not gossip[j] else None
+               for j, p in enumerate(pays)]
+    region, in_chunk, in_sz, kinds = frag_region(pays, bid, gossip, rng, hdr_psz)
+    out_chunk = (rng.permutation(n) * PARSED_CHUNKS).astype(np.uint32)
+    out_init = stale_out(rng, PARSED_CHUNKS * (n + 1), out_chunk)
+    exp_out, payloads, bids, spans = emulate(region, in_chunk, in_sz, kinds, out_init, out_chunk)
+    host = (rng.random(n) < 0.5) & (kinds != V.IN_GOSSIP)
+    pre = out_init.copy()                      # the host tile's during_frag for those frags
+    for j in np.nonzero(host)[0]:
+        a, o, z = 64 * int(in_chunk[j]), 64 * int(out_chunk[j]), int(in_sz[j])
+        pre[o:o + z] = region[a:a + z]
+    k2 = kinds.copy()
+    k2[host] |= V.IN_HOSTCOPY
+    ic2 = in_chunk.copy()
+    ic2[host] = 0xFFFFFFF0                     # never read
+    outs = []
+    for env in ({}, {"FD_VERIFY_HIP_FB": "8"}, {"FD_VERIFY_HIP_INGEST": "split"}):
+        r = run_tile(region, ic2, in_sz, k2, pre, out_chunk, 91, 4096, env=env)
+        check(*r, exp_out, payloads, bids, spans, 91, 4096, pre)
+        outs.append(r[4])
+    assert np.array_equal(outs[0], outs[1]) and np.array_equal(outs[0], outs[2])
+    assert host.sum() > 0.3 * n and r[3]["gossiped_votes_cnt"] == int(gossip.sum())
+
+
+def test_overrun_skip_is_invisible(stream):
+    """complete_skip: frags the caller found overrun (the GPU-copy tile's
+    post-read mcache check) get FRAG_OVERRUN and leave no trace in the
+    ordered pass -- the others' results, tags, metrics and tcache equal the
+    reference run over the stream without them (the stream's resends make a
+    leaked tcache insert visible as an extra dedup)."""
+    import torch
+    rng = np.random.default_rng(13)
+    pays = _payloads(stream)[:1500]
+    n = len(pays)
+    bid = np.zeros(n, np.uint64)
+    for start in rng.choice(n - 8, 20, replace=False):
+        bid[start:start + int(rng.integers(1, 6))] = int(rng.integers(1, 2**40))
+    region, in_chunk, in_sz, kinds = frag_region(pays, bid, np.zeros(n, bool), rng)
+    out_chunk = (np.arange(n) * PARSED_CHUNKS).astype(np.uint32)
+    out_init = stale_out(rng, PARSED_CHUNKS * (n + 1), out_chunk)
+    skip = rng.random(n) < 0.2
+    keep = ~skip
+    _, payloads, bids, _ = emulate(region, in_chunk[keep], in_sz[keep], kinds[keep], out_init, out_chunk[keep])
+    tile = V.VerifyTile(None, max_txn=n, hashmap_seed=5, tcache_depth=512, chunk_sigs=1 << 16)
+    tile.submit_frags(n, _dev(region), _dev(in_chunk, np.int32), _dev(in_sz, np.int16), _dev(kinds), _dev(out_init),
+                      _dev(out_chunk, np.int32))
+    res, tag, tsz = tile.complete_skip(skip.astype(np.uint8))
+    psz = tile.last_payload_sz
+    m = tile.metrics()
+    tile.close()
+    tile.verifier.close()
+    torch.cuda.synchronize()
+    pool = np.concatenate(payloads + [np.zeros(1, np.uint8)])
+    off = np.cumsum([0] + [p.size for p in payloads[:-1]]).astype(np.uint32)
+    sz = np.array([p.size for p in payloads], np.uint16)
+    o = T.OracleTile(seed=5, depth=512)
+    eres, etag, etsz = o.run(pool, off, sz, bids)
+    assert (res[skip] == V.FRAG_OVERRUN).all() and (tag[skip] == 0).all()
+    assert np.array_equal(res[keep], eres) and np.array_equal(tag[keep], etag) and np.array_equal(tsz[keep], etsz)
+    assert {k: m[k] for k in o.metrics()} == o.metrics()
+    assert o.metrics()["dedup_fail_cnt"] > 0
+    assert np.array_equal(psz[keep], [p.size for p in payloads])    # the out headers' payload_sz
+
+
 def test_large_batch_records_and_order(stream):
     """A 2^16-frag batch (the generated stream tiled, each frag re-keyed so no
     resend is a dedup of another copy's): every signature gets a record

@@ -35,20 +35,29 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, REPO)
 sys.path.insert(0, os.path.join(REPO, "tests"))
 BUILD = os.path.join(REPO, "integration", "_build")
-SWEEP = [(b, i, p) for b in (1024, 2048, 4096, 8192) for i in (2, 3, 4) for p in (2000, 20000)]
+# (batch_max, inflight, gpu_copy): the patch's FD_VERIFY_HIP_* settings; gpu_copy 0 is the host
+# during_frag copy ("h" suffix)
+SWEEP = [(b, i, g) for b in (1024, 2048, 4096, 8192) for i in (2, 3, 4) for g in (1, 0)]
 
 
-def binary(b, i, p=2000):
-    return os.path.join(BUILD, f"tile_run_b{b}i{i}" + ("" if p == 2000 else f"p{p}"))
+def binary(b, i, g=1):
+    return os.path.join(BUILD, f"tile_run_b{b}i{i}" + ("" if g else "h"))
+
+
+def parse_config(cfg):
+    """b<batch_max>i<inflight>[h] -> (batch_max, inflight, gpu_copy)"""
+    g = 0 if cfg.endswith("h") else 1
+    b, i = cfg.rstrip("h")[1:].split("i")
+    return int(b), int(i), g
 
 
 def build():
-    for b, i, p in SWEEP:
-        v = os.path.basename(binary(b, i, p))[len("tile_run"):]
+    for b, i, g in SWEEP:
+        v = os.path.basename(binary(b, i, g))[len("tile_run"):]
         subprocess.check_call(["make", "-s", "-C", os.path.join(REPO, "integration"), f"VARIANT={v}",
                                f"DEFS=-DFD_VERIFY_HIP_BATCH_MAX={b}UL -DFD_VERIFY_HIP_INFLIGHT={i}UL "
-                               f"-DFD_VERIFY_HIP_POLL_NS={p}L", f"_build/tile_run{v}"])
-        print(binary(b, i, p))
+                               f"-DFD_VERIFY_HIP_GPU_COPY={g}", f"_build/tile_run{v}"])
+        print(binary(b, i, g))
 
 
 def make_stream(n, path, seed=0x5eed0004, depth=4194302):
@@ -120,7 +129,7 @@ def main():
     ap.add_argument("--frags", type=int, default=1 << 21)
     ap.add_argument("--tiles", default="6")
     ap.add_argument("--configs", default="b4096i2",
-                    help="b<batch_max>i<inflight>[p<poll_ns>], comma-separated (binaries from --build)")
+                    help="b<batch_max>i<inflight>[h], comma-separated (binaries from --build; h: host during_frag copy)")
     ap.add_argument("--in-depth", type=int, default=16384,
                     help="quic_verify mcache depth (config tiles.verify.receive_buffer_size, default.toml:1153)")
     ap.add_argument("--repeat", type=int, default=1)
@@ -139,7 +148,7 @@ def main():
         print(f"stream: {s.n} frags, {s.n_records} signatures, {time.time() - t:.1f} s", file=sys.stderr, flush=True)
         best = None
         if args.walk:
-            exe = binary(4096, 2)
+            exe = binary(4096, 2, 0)
             for tiles in (int(x) for x in args.tiles.split(",")):
                 res = run_one(exe, stream, tiles, args.in_depth, args.timeout,
                               os.path.join(args.logdir, f"walk_t{tiles}"), walk=True)
@@ -147,9 +156,7 @@ def main():
                                   "frags_walked_per_s": s.n / res["seconds"], "regime": res.get("regime"),
                                   "in_depth": args.in_depth}), flush=True)
         for cfg in args.configs.split(","):
-            b, rest = cfg[1:].split("i")
-            i, p = (rest.split("p") + ["2000"])[:2]
-            exe = binary(int(b), int(i), int(p))
+            exe = binary(*parse_config(cfg))
             for tiles in (int(x) for x in args.tiles.split(",")):
                 for r in range(args.repeat):
                     res = run_one(exe, stream, tiles, args.in_depth, args.timeout,
