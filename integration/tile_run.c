@@ -17,7 +17,8 @@
          of the stream into the quic_verify dcache as fd_txn_m_t frags (the
          copy the quic tile would have made), prints READY, waits for the
          tiles, then publishes the frags' mcache lines in seq order, never
-         more than in_depth - 64 ahead of the slowest tile's fseq (the
+         more than in_depth - 64 (less the frags a GPU-copy tile holds
+         unread, RING x BATCH_CAP) ahead of the slowest tile's fseq (the
          reference link is unreliable and would drop frags past its depth; a
          throughput bench must not), and prints one JSON line once every
          tile is done.
@@ -173,12 +174,17 @@ produce( char const * path, char const * stream, ulong tile_cnt, ulong in_depth 
   FD_COMPILER_MFENCE();
   hdr->start = 1UL;
   ulong ctl = fd_frag_meta_ctl( 0UL, 1, 1, 0 );
+  /* a tile with the GPU-side during_frag holds up to RING x BATCH_CAP frags
+     between the stem consuming them (its fseq) and the GPU reading them:
+     the producer stays that much further behind, so nothing is overrun */
+  ulong const hold = FD_VERIFY_HIP_GPU_COPY ? FD_VERIFY_HIP_RING*FD_VERIFY_HIP_BATCH_CAP : 0UL;
+  if( FD_UNLIKELY( in_depth<hold+128UL ) ) FD_LOG_ERR(( "in_depth %lu too small for the GPU copy's %lu held frags", in_depth, hold ));
   ulong lim = 0UL, chunk = chunk0;
   for( ulong seq=0UL; seq<n; seq++ ) {
     while( seq>=lim ) {                                        /* flow control against the slowest tile */
       ulong m = ULONG_MAX;
       for( ulong t=0UL; t<tile_cnt; t++ ) m = fd_ulong_min( m, fd_fseq_query( fseq[ t ] ) );
-      lim = m + in_depth - 64UL;
+      lim = m + in_depth - 64UL - hold;
       if( seq>=lim ) FD_SPIN_PAUSE();
       if( fd_log_wallclock()-t0 > 600L*1000000000L ) FD_LOG_ERR(( "tiles stalled at seq %lu", seq ));
     }
