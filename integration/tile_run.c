@@ -176,8 +176,10 @@ produce( char const * path, char const * stream, ulong tile_cnt, ulong in_depth 
   ulong ctl = fd_frag_meta_ctl( 0UL, 1, 1, 0 );
   /* a tile with the GPU-side during_frag holds up to RING x BATCH_CAP frags
      between the stem consuming them (its fseq) and the GPU reading them:
-     the producer stays that much further behind, so nothing is overrun */
-  ulong const hold = FD_VERIFY_HIP_GPU_COPY ? FD_VERIFY_HIP_RING*FD_VERIFY_HIP_BATCH_CAP : 0UL;
+     the producer stays that much (times the tile count: each tile takes
+     every T-th seq) further behind, so nothing is overrun */
+  ulong const hold = FD_VERIFY_HIP_GPU_COPY ? FD_VERIFY_HIP_RING*FD_VERIFY_HIP_BATCH_CAP*tile_cnt : 0UL;   /* seq % T: a
+                                                                 tile's held frags span T times as many seqs */
   if( FD_UNLIKELY( in_depth<hold+128UL ) ) FD_LOG_ERR(( "in_depth %lu too small for the GPU copy's %lu held frags", in_depth, hold ));
   ulong lim = 0UL, chunk = chunk0;
   for( ulong seq=0UL; seq<n; seq++ ) {

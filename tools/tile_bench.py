@@ -157,12 +157,20 @@ def main():
                                   "in_depth": args.in_depth}), flush=True)
         for cfg in args.configs.split(","):
             exe = binary(*parse_config(cfg))
+            b, i, g = parse_config(cfg)
             for tiles in (int(x) for x in args.tiles.split(",")):
+                # a GPU-copy tile holds (i + 1) x 2b frags between consuming and the GPU's read, every
+                # tiles-th seq: the link must be deeper than that (tile_run.c's producer keeps out of it)
+                depth = args.in_depth
+                while g and depth < (i + 1) * 2 * b * tiles + 16384:
+                    depth *= 2
                 for r in range(args.repeat):
-                    res = run_one(exe, stream, tiles, args.in_depth, args.timeout,
+                    res = run_one(exe, stream, tiles, depth, args.timeout,
                                   os.path.join(args.logdir, f"{cfg}_t{tiles}_{r}"))
                     res["config"] = cfg
                     print(json.dumps(res), flush=True)
+                    if res.get("overrun"):          # dropped frags: not a valid throughput
+                        continue
                     if best is None or res["verifies_per_s"] > best["verifies_per_s"]:
                         best = res
         print(json.dumps({"metric": "ed25519 verifies/sec through the patched reference verify tile (stem_run1, "
