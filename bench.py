@@ -289,6 +289,9 @@ def main():
     ap.add_argument("--sigs", type=int, default=None, help="override signatures per GPU per step")
     ap.add_argument("--no-c4", action="store_true",
                     help="c2 (default config): skip the config-4 sub-object (the verify-tile path, 'c4' in the line)")
+    ap.add_argument("--no-tile", action="store_true",
+                    help="skip the patched reference verify tile leg (out['tile'], rank 0 at N=1)")
+    ap.add_argument("--tile-frags", type=int, default=1 << 21)
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--cpu-seconds", type=float, default=8.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -532,12 +535,53 @@ def main():
             out["c4"] = {k: c4[k] for k in ("value", "unit", "ms_per_step", "steps", "frags_per_s", "config",
                                             "frag_outcomes_last_batch", "batch_gpu_ms", "batch_host_ms",
                                             "roofline", "ingest_roofline", "pcie_inclusive", "cpu_baseline")}
+    if cfg == "c2" and not args.no_tile and rank == 0 and world == 1:
+        out["tile"] = run_tile_leg(args)
     if rank == 0:
         emit(out)
     if dist:
         dist.barrier()
         dist.destroy_process_group()
     return out
+
+
+def run_tile_leg(args):
+    """The north star's operating point: the reference's verify tile with
+    integration/fd_verify_tile_hip.patch (defaults: GPU-side during_frag,
+    8192-frag batches, 3 in flight) in the reference's stem_run1 loop, one
+    tile process fed by a producer process over a quic_verify link
+    (integration/tile_run.c, tools/tile_bench.py), over --tile-frags frags of
+    the C4 stream; then the same link walked by a tile that filters every
+    frag (the fan-out's bound).  Binaries are built from the reference
+    sources in the build container (integration/_build); without them the
+    leg reports why and the line goes on."""
+    sys.path.insert(0, os.path.join(REPO, "tools"))
+    try:
+        import tempfile
+        import tile_bench as TB
+        exe = os.path.join(TB.BUILD, "tile_run")
+        if not os.path.exists(exe):
+            return {"value": None, "error": "integration/_build/tile_run missing (build() with /root/reference)"}
+        with tempfile.TemporaryDirectory() as td:
+            stream = os.path.join(td, "stream.bin")
+            s = TB.make_stream(args.tile_frags, stream)
+            logdir = os.path.join(td, "logs")
+            r = TB.run_one(exe, stream, 1, 131072, 120, os.path.join(logdir, "tile"))
+            w = TB.run_one(exe, stream, 1, 131072, 120, os.path.join(logdir, "walk"), walk=True)
+        ok = not r.get("overrun")
+        return {"value": r["verifies_per_s"] if ok else None, "unit": "verifies/s",
+                "frags_per_s": r["frags_per_s"], "frags": r["frags"], "sigs": r["sigs"],
+                "published": r["published"], "overrun": r.get("overrun"), "seconds": r["seconds"],
+                "gpu_ms_per_batch": r["gpu_ms_per_batch"], "host_ms_per_batch": r["host_ms_per_batch"],
+                "regime": r["regime"], "walk_bound_frags_per_s": round(s.n / w["seconds"], 1),
+                "walk_bound_verifies_per_s": round(s.n_records / w["seconds"], 1),
+                "config": {"tiles": 1, "batch_max": r["batch_max"], "inflight": r["inflight"],
+                           "gpu_copy": r.get("gpu_copy"), "in_depth": r["in_depth"],
+                           "workload": f"config 4 stream, {s.n} frags ({s.n_records} signatures), GPU-signed"},
+                "what": "integration/fd_verify_tile_hip.patch'd fd_verify_tile.c in stem_run1 (tile_run.c), "
+                        "producer process -> 1 tile process; value = signatures / (last publish - first frag)"}
+    except Exception as e:                   # the tile leg never fails the bench line
+        return {"value": None, "error": f"{type(e).__name__}: {e}"}
 
 
 def ref_tile_baseline(pool, off, sz, threads, target_s, seed, depth):
