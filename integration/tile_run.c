@@ -178,8 +178,9 @@ produce( char const * path, char const * stream, ulong tile_cnt, ulong in_depth 
      between the stem consuming them (its fseq) and the GPU reading them:
      the producer stays that much (times the tile count: each tile takes
      every T-th seq) further behind, so nothing is overrun */
-  ulong const hold = FD_VERIFY_HIP_GPU_COPY ? FD_VERIFY_HIP_RING*FD_VERIFY_HIP_BATCH_CAP*tile_cnt : 0UL;   /* seq % T: a
-                                                                 tile's held frags span T times as many seqs */
+  ulong const hold = ( FD_VERIFY_HIP_GPU_COPY && !getenv( "TILE_RUN_NO_MARGIN" ) )   /* the env: overrun tests */
+                     ? FD_VERIFY_HIP_RING*FD_VERIFY_HIP_BATCH_CAP*tile_cnt : 0UL;  /* seq % T: a tile's held frags
+                                                                                     span T times as many seqs */
   if( FD_UNLIKELY( in_depth<hold+128UL ) ) FD_LOG_ERR(( "in_depth %lu too small for the GPU copy's %lu held frags", in_depth, hold ));
   ulong lim = 0UL, chunk = chunk0;
   for( ulong seq=0UL; seq<n; seq++ ) {

@@ -1,0 +1,61 @@
+"""GPU: the patched reference verify tile in the reference's own run loop
+(integration/tile_run.c: fd_verify_tile.c + integration/fd_verify_tile_hip.patch
+in stem_run1, a producer process on the quic_verify link), as the bench's
+tile leg runs it.
+
+- The GPU-side during_frag (the patch's default) and the reference's host
+  copy (FD_VERIFY_HIP_GPU_COPY 0) give the same outcome counts -- published,
+  parse / verify / dedup / bundle failures and signatures -- over a C4
+  stream (one tile: arrival order, and so the tcache's dedup decisions, is
+  the link's seq order in both).
+- With the producer allowed to run a whole link depth past the tile's
+  consumption (TILE_RUN_NO_MARGIN) and a link shallower than the frags the
+  GPU-copy tile holds unread, frags are overwritten before the GPU reads
+  them: the tile drops them as overruns (fd_verify_hip_tile_complete_skip)
+  and keeps running -- every frag is either an outcome or an overrun, and
+  nothing aborts on the overwritten bytes.
+The full-byte equality of the patched tile with the reference tile is
+tests/test_gpu_tile_hip.py (mock topology, both copy forms via the kernel
+tests in tests/test_gpu_txn_batch.py)."""
+import os
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(os.path.dirname(HERE), "tools"))
+
+
+@pytest.fixture(scope="module")
+def stream(tmp_path_factory, verifier):
+    import tile_bench as TB
+    assert os.path.exists(os.path.join(TB.BUILD, "tile_run")), "integration/_build missing: run build()"
+    p = str(tmp_path_factory.mktemp("tile_run") / "stream.bin")
+    s = TB.make_stream(1 << 18, p, seed=0x7e60)
+    return p, s
+
+
+def _outcomes(r):
+    return {k: r[k] for k in ("frags", "sigs", "published", "parse_fail", "verify_fail", "dedup", "bundle_peer_fail")}
+
+
+def test_gpu_copy_equals_host_copy(stream, tmp_path):
+    import tile_bench as TB
+    path, s = stream
+    g = TB.run_one(os.path.join(TB.BUILD, "tile_run"), path, 1, 131072, 120, str(tmp_path / "gpu"))
+    h = TB.run_one(os.path.join(TB.BUILD, "tile_run_hostcopy"), path, 1, 131072, 120, str(tmp_path / "host"))
+    assert g["gpu_copy"] == 1 and h["gpu_copy"] == 0
+    assert g["overrun"] == 0 and h["overrun"] == 0
+    assert _outcomes(g) == _outcomes(h)
+    assert g["frags"] == s.n and g["published"] > 0.5 * s.n and g["dedup"] > 0
+
+
+def test_overruns_are_dropped_not_fatal(stream, tmp_path, monkeypatch):
+    import tile_bench as TB
+    path, s = stream
+    monkeypatch.setenv("TILE_RUN_NO_MARGIN", "1")
+    r = TB.run_one(os.path.join(TB.BUILD, "tile_run"), path, 1, 16384, 120, str(tmp_path / "ovr"))
+    assert r["overrun"] > 0, r
+    assert r["frags"] + r["overrun"] == s.n
