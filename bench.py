@@ -184,9 +184,15 @@ def ingest_roofline(st):
         except Exception:                          # noqa: BLE001 -- reported as no match
             pass
         if k:
-            r["traffic"] = k["hbm_side_bytes_per_launch"]
-            r["traffic_ratio"] = round(k["hbm_side_bytes_per_launch"] / k["algorithmic_bytes_per_launch"], 3)
-            r["traffic_source"] = f"profiles/{PMC_SUMMARY_C4}: FETCH_SIZE*2 + WRITE_SIZE of k_txnm_batch"
+            # the PMC pass profiles whole 2^20-frag launches (one tile); this
+            # leg's launch is one tile's share of a step, so the traffic is
+            # that pass's bytes per algorithmic byte times this launch's
+            ratio = k["hbm_side_bytes_per_launch"] / k["algorithmic_bytes_per_launch"]
+            r["traffic"] = round(ratio * st["bytes"], 1)
+            r["traffic_ratio"] = round(ratio, 3)
+            r["traffic_source"] = (f"profiles/{PMC_SUMMARY_C4}: FETCH_SIZE*2 + WRITE_SIZE of k_txnm_batch over "
+                                   f"{k.get('frags_per_launch')}-frag launches ({k['hbm_side_bytes_per_launch']:.0f} B "
+                                   f"per launch), scaled to this launch by bytes per algorithmic byte")
             r["profile_matches_build"] = bool(have) and have == pm.get("kernel_sha", {}).get("k_txnm_batch<16>")
     return r
 
