@@ -17,7 +17,15 @@
 #   c4pmc[:args]       VALU issue + FETCH_SIZE + WRITE_SIZE passes over the C4 bench
 #   tile[:args]        python tools/tile_bench.py <args>        -> tile_<n>.json
 #   replay[:args]      python tools/replay_block_bench.py <args> -> replay_<n>.json
+#   profile            the profile set bench.py prices its rooflines with, for this build:
+#                      tools/run_profile.sh, run_valu_calib.sh and run_c4_issue.sh (tag <tag>),
+#                      then the c4pmc and c4stats steps; summarise with tools/pmc_summary.py,
+#                      valu_calib_summary.py, c4_issue_summary.py, txnm_pmc_summary.py
 #   smoke              __graft_entry__.smoke()
+# Round-4 sessions, as steps: replay/tile tests + tile sweep (r04n) =
+#   tests:tests/test_gpu_replay_block.py,tests/test_gpu_replay.py,tests/test_gpu_txn_batch.py,tests/test_gpu_tile_hip.py
+#   replay:--txns,16384,98039,--sched  tile:--frags,2097152,--tiles,1,2,4,--configs,b8192i4,b8192i4h
+# the link-walk bound (r04o): tile:--walk,--tiles,1,2,4,--configs,b8192i4
 # (It replaces the round-3 per-session scripts tools/run_r03*.sh and the
 # one-off A/B runners; they are in git history before this file's commit.)
 # Every GPU step runs under its own timeout; a failure ends the session.
@@ -87,6 +95,18 @@ for step in "$@"; do
       timeout -k 10 600 python3 -u tools/replay_block_bench.py $a > $O/replay_$n.json 2> $O/replay_$n.err \
           || fail replay $? $O/replay_$n.err
       cut -c1-600 $O/replay_$n.json ;;
+    profile)
+      bash tools/run_profile.sh $T || fail profile $?
+      bash tools/run_valu_calib.sh $T || fail valu $?
+      bash tools/run_c4_issue.sh $T || fail c4issue $?
+      B="python3 bench.py --config c4 --tiles 1 --no-cpu-baseline --steps 2 --warmup 1 --c4-pcie-steps 1"
+      pmc_pass c4pmc_valu "$VALU_G" $B
+      pmc_pass c4pmc_fetch "FETCH_SIZE" $B
+      pmc_pass c4pmc_write "WRITE_SIZE" $B
+      timeout -k 10 900 rocprofv3 --kernel-trace --stats --output-format csv -d $O/c4stats_$n -o run -- \
+          python3 bench.py --config c4 --tiles 1 --no-cpu-baseline --steps 3 --warmup 1 --c4-pcie-steps 1 \
+          > $O/c4stats_$n.json 2> $O/c4stats_$n.err || fail c4stats $? $O/c4stats_$n.err
+      echo "profile set ok" ;;
     smoke)
       timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.txt 2>&1 || fail smoke $? $O/smoke.txt
       tail -2 $O/smoke.txt ;;
