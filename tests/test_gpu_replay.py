@@ -101,6 +101,29 @@ def test_replay_max_txn_guard(verifier):
     assert DESC_DTYPE.itemsize == 16
 
 
+def test_replay_host_entry_rejects_bad_spans(verifier):
+    """fd_replay_hip_txn_verify_host refuses (nothing launched) a descriptor
+    whose payload runs past pool_sz, n over max_txn, and a pool over its
+    staging; a good call after them still verifies."""
+    from firedancer_amd.replay import DESC_DTYPE, ReplayVerifier
+    rv = ReplayVerifier(verifier, 4)
+    pool = np.zeros(300, np.uint8)
+    desc = np.zeros(2, DESC_DTYPE)
+    desc["payload_off"], desc["payload_sz"], desc["signature_cnt"] = [0, 200], [150, 150], 1
+    res = np.zeros(2, np.int32)
+    with pytest.raises(ValueError):
+        rv.txn_verify_host(2, pool, desc, res)                       # 200 + 150 > 300
+    with pytest.raises(ValueError):
+        rv.txn_verify_host(5, np.zeros(5 * 1232, np.uint8), np.zeros(5, DESC_DTYPE), np.zeros(5, np.int32))
+    with pytest.raises(ValueError):
+        rv.txn_verify_host(1, np.zeros(4 * 1232 + 1, np.uint8), desc[:1], res[:1])
+    desc["payload_off"][1] = 150
+    rv.txn_verify_host(2, pool, desc, res)
+    rv.wait()
+    assert (res == -13).all()                                       # zero signatures over zero keys
+    rv.close()
+
+
 def test_fec_roots_vs_oracle(verifier):
     """5000 FEC-set roots signed by 4 leaders, C2 mutations, through the
     fixed-size-message path; codes equal the oracle's fd_ed25519_verify."""
