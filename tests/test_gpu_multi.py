@@ -61,6 +61,25 @@ def test_two_ranks_shard_and_gather(tmp_path):
 
 
 @pytest.mark.gpu
+def test_bench_world2_default_line_gloo():
+    """The default bench line (C2 leg + the c4 sub-object) at world 2, as the
+    driver's scaling runs launch it (gloo here: two ranks on one GPU):
+    one JSON line, both legs' values present, the c4 leg's signatures
+    summed over the ranks."""
+    port = _free_port()
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), "bench.py", "--gpus", "2",
+           "--sigs", str(1 << 18), "--txns", str(1 << 16), "--steps", "2", "--warmup", "1",
+           "--c4-pcie-steps", "1", "--dist-backend", "gloo", "--no-cpu-baseline", "--no-tile"]
+    r = subprocess.run(cmd, cwd=REPO, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [x for x in r.stdout.splitlines() if x.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["value"] > 0 and "tile" not in d
+    assert d["c4"]["value"] > 0 and d["c4"]["config"]["frags_per_gpu"] == 1 << 16
+
+
 def test_bench_world2_c5_gloo(tmp_path):
     port = _free_port()
     """bench.py's N>1 path at world 2 (gloo: RCCL refuses two ranks on one
