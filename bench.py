@@ -574,6 +574,8 @@ def run_tile_leg(args):
             logdir = os.path.join(td, "logs")
             r = TB.run_one(exe, stream, 1, 131072, 120, os.path.join(logdir, "tile"))
             w = TB.run_one(exe, stream, 1, 131072, 120, os.path.join(logdir, "walk"), walk=True)
+            hexe = os.path.join(TB.BUILD, "tile_run_hostcopy")      # the reference's own during_frag copy
+            h = TB.run_one(hexe, stream, 1, 131072, 120, os.path.join(logdir, "host")) if os.path.exists(hexe) else None
         ok = not r.get("overrun")
         return {"value": r["verifies_per_s"] if ok else None, "unit": "verifies/s",
                 "frags_per_s": r["frags_per_s"], "frags": r["frags"], "sigs": r["sigs"],
@@ -581,11 +583,15 @@ def run_tile_leg(args):
                 "gpu_ms_per_batch": r["gpu_ms_per_batch"], "host_ms_per_batch": r["host_ms_per_batch"],
                 "regime": r["regime"], "walk_bound_frags_per_s": round(s.n / w["seconds"], 1),
                 "walk_bound_verifies_per_s": round(s.n_records / w["seconds"], 1),
+                "host_copy_value": h["verifies_per_s"] if h and not h.get("overrun") else None,
+                "host_copy_frags_per_s": h["frags_per_s"] if h else None,
                 "config": {"tiles": 1, "batch_max": r["batch_max"], "inflight": r["inflight"],
                            "gpu_copy": r.get("gpu_copy"), "in_depth": r["in_depth"],
                            "workload": f"config 4 stream, {s.n} frags ({s.n_records} signatures), GPU-signed"},
                 "what": "integration/fd_verify_tile_hip.patch'd fd_verify_tile.c in stem_run1 (tile_run.c), "
-                        "producer process -> 1 tile process; value = signatures / (last publish - first frag)"}
+                        "producer process -> 1 tile process; value = signatures / (last publish - first frag); "
+                        "host_copy_value: the same with the reference's during_frag copy on the host "
+                        "(FD_VERIFY_HIP_GPU_COPY 0); walk_bound: a tile that filters every frag"}
     except Exception as e:                   # the tile leg never fails the bench line
         return {"value": None, "error": f"{type(e).__name__}: {e}"}
 
