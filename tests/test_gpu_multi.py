@@ -80,12 +80,13 @@ def test_bench_world2_default_line_gloo():
     assert d["c4"]["value"] > 0 and d["c4"]["config"]["frags_per_gpu"] == 1 << 16
 
 
+@pytest.mark.gpu
 def test_bench_world2_c5_gloo(tmp_path):
-    port = _free_port()
     """bench.py's N>1 path at world 2 (gloo: RCCL refuses two ranks on one
     GPU): the JSON line carries the CPU baseline, and the two ranks'
     verdicts -- each rank generates and verifies only its shard of the one
     global C5 set -- equal a one-process pass over the whole set."""
+    port = _free_port()
     import numpy as np
     import torch
 
