@@ -1031,6 +1031,10 @@ struct tile_slot {
      header bundle ids, in kinds and the corrupt-frag flag */
   u32 *         d_pay_off; u16 * d_pay_sz; u32 * d_tout; u64 * d_bid; u32 * d_flag;
   u32 *         d_misc;     /* counter, flag, record segments (SLOT_MISC_*) */
+  /* mcache range mode (submit_range): the frag list k_range_gather builds
+     from the in link's mcache lines, and each frag's tsorig (device, host) */
+  u32 *         d_rin; u16 * d_rsz; u8 * d_rkind; u32 * d_tso; u32 * h_tso;
+  int           range;
   fd_ed25519_hip_ctx_t * ctx;   /* the verify context (stream and scratch) the slot's batches run on */
   int           own_ctx;    /* created by set_inflight: batches of different slots run concurrently */
   u32           n_seg;      /* the last batch's record segments (0: not k_txnm_batch) */
@@ -1106,6 +1110,9 @@ static void slot_alloc( tile_slot & s, ulong n ) {
   TX_CHECK( hipMalloc( &s.d_res, TILE_RES_HDR + 24*n ) );  TX_CHECK( hipHostMalloc( &s.h_res, TILE_RES_HDR + 24*n, 0 ) );
   TX_CHECK( hipMalloc( &s.d_pay_off, 4*n ) );     TX_CHECK( hipMalloc( &s.d_pay_sz, 2*n ) );
   TX_CHECK( hipMalloc( &s.d_tout, 4*n ) );        TX_CHECK( hipMalloc( &s.d_bid, 8*n ) );
+  TX_CHECK( hipMalloc( &s.d_rin, 4*n ) );         TX_CHECK( hipMalloc( &s.d_rsz, 2*n ) );
+  TX_CHECK( hipMalloc( &s.d_rkind, n ) );         TX_CHECK( hipMalloc( &s.d_tso, 4*n ) );
+  TX_CHECK( hipHostMalloc( &s.h_tso, 4*n, 0 ) );
   TX_CHECK( hipEventCreate( &s.ev_start ) ); TX_CHECK( hipEventCreate( &s.ev_done ) );
   TX_CHECK( hipEventCreate( &s.ev_ing0 ) ); TX_CHECK( hipEventCreate( &s.ev_ing1 ) );
 }
@@ -1130,6 +1137,8 @@ static void slot_free( tile_slot & s ) {
   (void)hipFree( s.d_cnt ); (void)hipFree( s.d_tcode ); (void)hipFree( s.d_misc );
   (void)hipFree( s.d_res ); (void)hipHostFree( s.h_res );
   (void)hipFree( s.d_pay_off ); (void)hipFree( s.d_pay_sz ); (void)hipFree( s.d_tout ); (void)hipFree( s.d_bid );
+  (void)hipFree( s.d_rin ); (void)hipFree( s.d_rsz ); (void)hipFree( s.d_rkind ); (void)hipFree( s.d_tso );
+  (void)hipHostFree( s.h_tso );
   (void)hipEventDestroy( s.ev_start ); (void)hipEventDestroy( s.ev_done );
   (void)hipEventDestroy( s.ev_ing0 ); (void)hipEventDestroy( s.ev_ing1 );
   slot_free_records( s );
@@ -1328,7 +1337,7 @@ submit_begin( fd_verify_hip_tile_t * t, ulong n, hipStream_t & st, int & rc ) {
   if( s.busy ) { rc = -2; return 0; }                        /* two batches outstanding */
   st = (hipStream_t)fd_ed25519_hip_ctx_stream( s.ctx );
   TX_CHECK( hipSetDevice( fd_ed25519_hip_ctx_device( s.ctx ) ) );
-  s.n = n; s.nsig = 0; s.busy = 1; s.frags = 0; s.ing_timed = 0; s.n_seg = 0; t->submitted++;
+  s.n = n; s.nsig = 0; s.busy = 1; s.frags = 0; s.range = 0; s.ing_timed = 0; s.n_seg = 0; t->submitted++;
   TX_CHECK( hipEventRecord( s.ev_start, st ) );
   return &s;
 }
@@ -1352,16 +1361,12 @@ fd_verify_hip_tile_submit( fd_verify_hip_tile_t * t, ulong n, uchar const * d_po
   return 0;
 }
 
-extern "C" int
-fd_verify_hip_tile_submit_frags( fd_verify_hip_tile_t * t, ulong n, uchar const * d_in, uint const * d_in_chunk,
-                                 ushort const * d_in_sz, uchar const * d_in_kind, uchar * d_out,
-                                 uint const * d_out_chunk ) {
-  hipStream_t st; int rc;
-  tile_slot * sp = submit_begin( t, n, st, rc );
-  if( !sp ) return rc;
-  tile_slot & s = *sp;
-  s.frags = 1;
-  if( !n ) { memset( s.h_res, 0, TILE_RES_HDR ); TX_CHECK( hipEventRecord( s.ev_done, st ) ); return 0; }
+/* a frag batch after submit_begin, n > 0: ingest (copy, parse, records),
+   verify, per-txn reduce and the results D2H on the slot's stream */
+static void
+submit_frags_body( fd_verify_hip_tile_t * t, tile_slot & s, hipStream_t st, ulong n, uchar const * d_in,
+                   uint const * d_in_chunk, ushort const * d_in_sz, uchar const * d_in_kind, uchar * d_out,
+                   uint const * d_out_chunk ) {
   dim3 grid( (unsigned)((n + 255)/256) ), blk( 256 );
   if( t->ingest_split ) {
     /* the three-kernel form (ingest copy, one-lane parse, expansion, then
@@ -1407,6 +1412,84 @@ fd_verify_hip_tile_submit_frags( fd_verify_hip_tile_t * t, ulong n, uchar const 
     fd_ed25519_hip_group_reduce_dev( s.ctx, n, s.d_first, s.d_cnt, s.d_rcode, s.d_tcode, st );
   }
   submit_results( s, st, n, d_in_kind, d_out, d_out_chunk );
+}
+
+extern "C" int
+fd_verify_hip_tile_submit_frags( fd_verify_hip_tile_t * t, ulong n, uchar const * d_in, uint const * d_in_chunk,
+                                 ushort const * d_in_sz, uchar const * d_in_kind, uchar * d_out,
+                                 uint const * d_out_chunk ) {
+  hipStream_t st; int rc;
+  tile_slot * sp = submit_begin( t, n, st, rc );
+  if( !sp ) return rc;
+  tile_slot & s = *sp;
+  s.frags = 1;
+  if( !n ) { memset( s.h_res, 0, TILE_RES_HDR ); TX_CHECK( hipEventRecord( s.ev_done, st ) ); return 0; }
+  submit_frags_body( t, s, st, n, d_in, d_in_chunk, d_in_sz, d_in_kind, d_out, d_out_chunk );
+  TX_CHECK( hipEventRecord( s.ev_done, st ) );
+  return 0;
+}
+
+/* mcache range mode.  The stem reads a polled link one mcache line at a
+   time on the tile's core (fd_stem.c: the line's seq, before_frag, the
+   fields, during_frag, the seq again) -- for the quic_verify fan-out every
+   verify tile reads every line of the link, a cross-core miss each, which
+   bounds the stage at ~15-20 M frags/s on the GPU box whatever the tile
+   count.  A tile whose quic_verify link is unpolled
+   (FD_TOPOB_UNPOLLED, integration/fd_verify_topo_hip.patch) hands the GPU
+   whole published seq ranges of it instead: k_range_gather reads the lines
+   (32 B each, from the registered mcache), keeps the tile's round-robin
+   share (before_frag, fd_verify_tile.c:37-58), checks each as the stem and
+   during_frag do, and writes the frag list k_txnm_batch ingests.
+
+   Per kept seq j (seq = first + j*rr_cnt): the line must still hold seq
+   and a chunk in [chunk0, wmark] with sz <= FD_TPU_RAW_MTU; a line that
+   does not (overwritten by a producer that lapped the tile, or corrupt) is
+   given sz 0xffff, which k_txnm_batch flags as a corrupt frag without
+   reading it -- the caller's overrun check after the batch (the oldest
+   line, then per frag) tells the two apart: an overrun frag is skipped
+   (complete_skip/complete_range), a corrupt one ends the tile as
+   during_frag's FD_LOG_ERR does.  The line's fields are read only after
+   the caller saw the line hold seq (the producer writes seq last,
+   fd_mcache_publish), so they are that frag's unless the line was reused
+   since, which the same overrun check catches. */
+__global__ __launch_bounds__(256)
+void k_range_gather( ulong n, u8 const * __restrict__ mcache, ulong line_mask, ulong first, ulong stride,
+                     ulong chunk_off, ulong chunk0, ulong wmark, u32 * __restrict__ in_chunk,
+                     u16 * __restrict__ in_sz, u8 * __restrict__ in_kind, u32 * __restrict__ tso ) {
+  ulong j = (ulong)blockIdx.x * blockDim.x + threadIdx.x;
+  if( j >= n ) return;
+  ulong const seq = first + j * stride;
+  u8 const * line = mcache + 32ul * (seq & line_mask);
+  uint4 const w1 = *(uint4 const *)(line + 16);                              /* chunk, sz, ctl, tsorig, tspub */
+  u64 const found = *(u64 const *)line;
+  u32 const chunk = w1.x, sz = w1.y & 0xffffu;
+  bool ok = found == seq && (ulong)chunk >= chunk0 && (ulong)chunk <= wmark && sz <= FD_VERIFY_HIP_TPU_RAW_MTU;
+  in_chunk[j] = ok ? (u32)((ulong)chunk - chunk_off) : 0u;
+  in_sz[j]    = ok ? (u16)sz : (u16)0xffffu;
+  in_kind[j]  = (u8)FD_VERIFY_HIP_IN_QUIC;
+  tso[j]      = ok ? w1.z : 0u;
+}
+
+extern "C" int
+fd_verify_hip_tile_submit_range( fd_verify_hip_tile_t * t, fd_verify_hip_range_t const * r, uchar const * d_in,
+                                 uchar * d_out, uint const * d_out_chunk ) {
+  if( !r || !r->mcache || !d_in || !d_out || !d_out_chunk ) return -1;
+  if( !r->depth || (r->depth & (r->depth - 1ul)) || r->seq_cnt > r->depth || !r->rr_cnt || r->rr_idx >= r->rr_cnt ||
+      r->chunk0 < r->chunk_off || r->chunk0 > r->wmark || r->wmark - r->chunk_off > 0xffffffffull ) return -1;
+  ulong const n = fd_verify_hip_range_frag_cnt( r->seq0, r->seq_cnt, r->rr_cnt, r->rr_idx );
+  hipStream_t st; int rc;
+  tile_slot * sp = submit_begin( t, n, st, rc );
+  if( !sp ) return rc;
+  tile_slot & s = *sp;
+  s.frags = 1; s.range = 1;
+  if( !n ) { memset( s.h_res, 0, TILE_RES_HDR ); TX_CHECK( hipEventRecord( s.ev_done, st ) ); return 0; }
+  ulong const first = r->seq0 + (r->rr_idx + r->rr_cnt - r->seq0 % r->rr_cnt) % r->rr_cnt;
+  hipLaunchKernelGGL( k_range_gather, dim3( (unsigned)((n + 255ul)/256ul) ), dim3( 256 ), 0, st, n,
+                      (u8 const *)r->mcache, r->depth - 1ul, first, r->rr_cnt, r->chunk_off, r->chunk0, r->wmark,
+                      s.d_rin, s.d_rsz, s.d_rkind, s.d_tso );
+  TX_CHECK( hipGetLastError() );
+  submit_frags_body( t, s, st, n, d_in, s.d_rin, s.d_rsz, s.d_rkind, d_out, d_out_chunk );
+  TX_CHECK( hipMemcpyAsync( s.h_tso, s.d_tso, 4ul*n, hipMemcpyDeviceToHost, st ) );
   TX_CHECK( hipEventRecord( s.ev_done, st ) );
   return 0;
 }
@@ -1453,9 +1536,10 @@ fd_verify_hip_tile_set_inflight( fd_verify_hip_tile_t * t, ulong k ) {
 
 static int
 tile_complete( fd_verify_hip_tile_t * t, ulong const * bundle_id, uchar const * skip, signed char * result,
-               ulong * tag_out, ushort * txn_t_sz, ushort * payload_sz = 0 ) {
+               ulong * tag_out, ushort * txn_t_sz, ushort * payload_sz = 0, uint * tsorig = 0 ) {
   if( t->completed == t->submitted ) return -1;
   tile_slot & s = t->slot[t->completed % t->nslot];
+  if( tsorig && !s.range ) return -1;                       /* a range batch's lines only */
   TX_CHECK( hipSetDevice( fd_ed25519_hip_ctx_device( t->ctx ) ) );
   TX_CHECK( hipEventSynchronize( s.ev_done ) );
   u32 const * hdr = (u32 const *)s.h_res;
@@ -1469,6 +1553,7 @@ tile_complete( fd_verify_hip_tile_t * t, ulong const * bundle_id, uchar const * 
     abort();
   }
   s.nsig = s.n ? hdr[0] : 0u;
+  if( tsorig && s.n ) memcpy( tsorig, s.h_tso, 4ul*s.n );
   float gpu_ms = 0.f;
   TX_CHECK( hipEventElapsedTime( &gpu_ms, s.ev_start, s.ev_done ) );
   auto h0 = std::chrono::steady_clock::now();
@@ -1558,6 +1643,14 @@ fd_verify_hip_tile_complete_skip( fd_verify_hip_tile_t * t, uchar const * skip, 
                                   ulong * tag_out, ushort * txn_t_sz, ushort * payload_sz ) {
   if( !t->slot[t->completed % t->nslot].frags && t->completed != t->submitted ) return -1;   /* frag batches only */
   return tile_complete( t, NULL, skip, result, tag_out, txn_t_sz, payload_sz );
+}
+
+extern "C" int
+fd_verify_hip_tile_complete_range( fd_verify_hip_tile_t * t, uchar const * skip, signed char * result,
+                                   ushort * txn_t_sz, ushort * payload_sz, uint * tsorig ) {
+  if( !result ) return -1;
+  if( t->completed != t->submitted && !t->slot[t->completed % t->nslot].frags ) return -1;
+  return tile_complete( t, NULL, skip, result, NULL, txn_t_sz, payload_sz, tsorig );
 }
 
 extern "C" void fd_verify_hip_tile_set_ingest_timing( fd_verify_hip_tile_t * t, int on ) { t->ingest_timing = !!on; }

@@ -36,7 +36,7 @@ EXPORTS = (
     "fd_verify_hip_tcache_reset", "fd_verify_hip_tcache_query", "fd_verify_hip_tcache_insert",
     "fd_verify_hip_tile_new", "fd_verify_hip_tile_join_tcache", "fd_verify_hip_tile_tcache_reset",
     "fd_verify_hip_tile_delete", "fd_verify_hip_tile_set_seed", "fd_verify_hip_tile_submit", "fd_verify_hip_tile_complete",
-    "fd_verify_hip_tile_complete_skip",
+    "fd_verify_hip_tile_complete_skip", "fd_verify_hip_tile_submit_range", "fd_verify_hip_tile_complete_range",
     "fd_verify_hip_tile_metrics", "fd_verify_hip_tile_metrics2", "fd_verify_hip_tile_last_timing", "fd_verify_hip_tile_submit_frags",
     "fd_verify_hip_before_frag", "fd_verify_hip_hist_edges", "fd_verify_hip_tile_hist_init",
     "fd_verify_hip_tile_hist", "fd_verify_hip_tile_poll", "fd_verify_hip_tile_inflight",
@@ -51,6 +51,22 @@ GOSSIP_UPDATE_TAG_VOTE, GOSSIP_VOTE_ADDR_OFF, GOSSIP_VOTE_TXN_SZ_OFF, GOSSIP_VOT
 IN_QUIC, IN_BUNDLE, IN_GOSSIP, IN_SEND = 0, 1, 2, 3
 IN_HOSTCOPY = 0x80      # or'd into a kind: the host did during_frag's copy into the out chunk
 FRAG_OVERRUN = -5       # complete_skip's result for a skipped (overrun) frag
+
+
+class Range(ctypes.Structure):
+    """fd_verify_hip_range_t: a published seq range of an unpolled in link's mcache."""
+    _fields_ = [("mcache", ctypes.c_void_p), ("depth", ctypes.c_ulong), ("seq0", ctypes.c_ulong),
+                ("seq_cnt", ctypes.c_ulong), ("rr_cnt", ctypes.c_ulong), ("rr_idx", ctypes.c_ulong),
+                ("chunk_off", ctypes.c_ulong), ("chunk0", ctypes.c_ulong), ("wmark", ctypes.c_ulong)]
+
+
+def range_frag_cnt(seq0, seq_cnt, rr_cnt, rr_idx):
+    """fd_verify_hip_range_frag_cnt: seqs of [seq0, seq0+seq_cnt) with seq % rr_cnt == rr_idx."""
+    if not seq_cnt or not rr_cnt or rr_idx >= rr_cnt:
+        return 0
+    first = seq0 + (rr_idx + rr_cnt - seq0 % rr_cnt) % rr_cnt
+    end = seq0 + seq_cnt
+    return (end - 1 - first) // rr_cnt + 1 if first < end else 0
 
 _bound = False
 
@@ -98,6 +114,10 @@ def lib():
         L.fd_verify_hip_tile_set_inflight.argtypes = [vp, u64]
         L.fd_verify_hip_tile_submit_frags.restype = c.c_int
         L.fd_verify_hip_tile_submit_frags.argtypes = [vp, u64, vp, vp, vp, vp, vp, vp]
+        L.fd_verify_hip_tile_submit_range.restype = c.c_int
+        L.fd_verify_hip_tile_submit_range.argtypes = [vp, c.POINTER(Range), vp, vp, vp]
+        L.fd_verify_hip_tile_complete_range.restype = c.c_int
+        L.fd_verify_hip_tile_complete_range.argtypes = [vp, vp, vp, vp, vp, vp]
         L.fd_verify_hip_before_frag.restype = c.c_int
         L.fd_verify_hip_before_frag.argtypes = [c.c_uint, u64, u64, u64, u64]
         L.fd_verify_hip_hist_edges.restype = c.c_int
@@ -214,6 +234,40 @@ class VerifyTile:
         if rc:
             raise RuntimeError(f"fd_verify_hip_tile_submit_frags: {rc}")
         self._pending.append((n, (d_in, in_chunk, in_sz, in_kind, d_out, out_chunk)))
+
+    def submit_range(self, mcache, depth, seq0, seq_cnt, rr_cnt, rr_idx, chunk_off, chunk0, wmark, d_in, d_out,
+                     out_chunk):
+        """fd_verify_hip_tile_submit_range: the GPU reads mcache lines [seq0, seq0+seq_cnt)
+        (device tensor of depth 32-byte fd_frag_meta_t lines), keeps seq % rr_cnt == rr_idx
+        and ingests those frags from d_in + 64*(chunk - chunk_off) into d_out + 64*out_chunk[j]."""
+        dev = self.verifier.device
+        n = range_frag_cnt(int(seq0), int(seq_cnt), int(rr_cnt), int(rr_idx))
+        r = Range(_ptr(mcache, 32 * int(depth), "mcache", dev), int(depth), int(seq0), int(seq_cnt), int(rr_cnt),
+                  int(rr_idx), int(chunk_off), int(chunk0), int(wmark))
+        rc = self._lib.fd_verify_hip_tile_submit_range(self.tile, ctypes.byref(r), _ptr(d_in, 1, "d_in", dev),
+                                                       _ptr(d_out, 1, "d_out", dev),
+                                                       _ptr(out_chunk, 4 * max(n, 1), "out_chunk", dev))
+        if rc:
+            raise RuntimeError(f"fd_verify_hip_tile_submit_range: {rc}")
+        self._pending.append((n, (mcache, d_in, d_out, out_chunk)))
+        return n
+
+    def complete_range(self, skip=None):
+        """complete_skip plus each kept frag's mcache tsorig (range batches):
+        (result, txn_t_sz, payload_sz, tsorig)."""
+        n, _keep = self._pending.pop(0)
+        sk = None if skip is None else np.ascontiguousarray(skip, np.uint8)
+        assert sk is None or sk.size >= n
+        result = np.zeros(max(n, 1), np.int8)
+        tsz = np.zeros(max(n, 1), np.uint16)
+        psz = np.zeros(max(n, 1), np.uint16)
+        tso = np.zeros(max(n, 1), np.uint32)
+        rc = self._lib.fd_verify_hip_tile_complete_range(self.tile, None if sk is None else sk.ctypes.data,
+                                                         result.ctypes.data, tsz.ctypes.data, psz.ctypes.data,
+                                                         tso.ctypes.data)
+        if rc:
+            raise RuntimeError(f"fd_verify_hip_tile_complete_range: {rc}")
+        return result[:n], tsz[:n], psz[:n], tso[:n]
 
     def poll(self):
         """fd_verify_hip_tile_poll: 1 oldest batch done, 0 running, -1 none (never blocks)."""

@@ -223,6 +223,66 @@ fd_verify_hip_tile_submit_frags( fd_verify_hip_tile_t * tile,
                                  uchar *                d_out,
                                  uint const *           d_out_chunk );
 
+/* mcache range mode: the tile reads an unpolled quic_verify link
+   (FD_TOPOB_UNPOLLED; integration/fd_verify_topo_hip.patch) by whole
+   published seq ranges instead of one stem frag at a time.  The GPU reads
+   the link's mcache lines [seq0, seq0+seq_cnt) (fd_frag_meta_t, 32 B:
+   seq, sig, chunk, sz, ctl, tsorig, tspub), keeps before_frag's round
+   robin share (seq % rr_cnt == rr_idx, fd_verify_tile.c:37-58), checks
+   each as the stem and during_frag do (the line still holds seq; chunk in
+   [chunk0, wmark]; sz <= FD_TPU_RAW_MTU, :74-76) and ingests the kept
+   frags as submit_frags does, from d_in + 64*(chunk - chunk_off).  Kept
+   frag j (seq first + j*rr_cnt) goes to out chunk d_out_chunk[j]
+   (fd_verify_hip_range_frag_cnt of them).
+
+   The caller submits only seqs it saw published (the line of the range's
+   last seq holding that seq), and after the batch does the stem's overrun
+   check: if the line of the range's first kept seq no longer holds it,
+   each kept frag whose line was reused is skipped (complete_range's skip).
+   A line the GPU found reused or corrupt flags the batch corrupt; with no
+   frag skipped that aborts in complete, as during_frag's FD_LOG_ERR ends
+   the tile.  mcache and d_in are device-visible (the link's mcache and
+   dcache registered with fd_ed25519_hip_host_register).  -1 for a bad
+   range (depth not a power of 2, seq_cnt > depth, rr_idx >= rr_cnt,
+   chunk0 outside [chunk_off, wmark]), -2 while every slot is busy, -1 if
+   the share exceeds the tile's max_txn. */
+typedef struct {
+  void const * mcache;          /* device address of line 0 */
+  ulong        depth;           /* lines (power of 2) */
+  ulong        seq0, seq_cnt;   /* the range */
+  ulong        rr_cnt, rr_idx;  /* before_frag's round robin */
+  ulong        chunk_off;       /* link chunk of d_in's first byte (64-byte units from the link's wksp) */
+  ulong        chunk0, wmark;   /* during_frag's chunk range (fd_dcache_compact_chunk0 / _wmark) */
+} fd_verify_hip_range_t;
+
+/* kept seqs of [seq0, seq0+seq_cnt): seq % rr_cnt == rr_idx */
+static inline ulong
+fd_verify_hip_range_frag_cnt( ulong seq0, ulong seq_cnt, ulong rr_cnt, ulong rr_idx ) {
+  if( !seq_cnt || !rr_cnt || rr_idx>=rr_cnt ) return 0UL;
+  ulong first = seq0 + ( rr_idx + rr_cnt - seq0 % rr_cnt ) % rr_cnt;
+  ulong end   = seq0 + seq_cnt;
+  return first<end ? ( end - 1UL - first )/rr_cnt + 1UL : 0UL;
+}
+
+int
+fd_verify_hip_tile_submit_range( fd_verify_hip_tile_t *        tile,
+                                 fd_verify_hip_range_t const * range,
+                                 uchar const *                 d_in,
+                                 uchar *                       d_out,
+                                 uint const *                  d_out_chunk );
+
+/* complete_skip for any frag batch, and for a range batch each kept
+   frag's mcache tsorig (NULL: not wanted; -1 if wanted from a batch that
+   is not a range).  txn_t_sz / payload_sz as in complete_skip (NULL: not
+   wanted). */
+int
+fd_verify_hip_tile_complete_range( fd_verify_hip_tile_t * tile,
+                                   uchar const *          skip,         /* host, n (NULL: none skipped) */
+                                   signed char *          result,       /* host, n */
+                                   ushort *               txn_t_sz,     /* host, n or NULL */
+                                   ushort *               payload_sz,   /* host, n or NULL */
+                                   uint *                 tsorig );     /* host, n or NULL */
+
 /* Non-blocking: 1 if the oldest outstanding batch has finished on the GPU
    (complete() will not wait), 0 if it is still running, -1 if no batch is
    outstanding.  A stem loop polls from after_credit and calls complete()

@@ -30,6 +30,15 @@
          the patched callbacks until its share of the stream is published
          or dropped and nothing is left on the GPU.
 
+   Range mode (environment TILE_RUN_RANGE=1 on the producer and the tiles):
+   the tiles' quic_verify in link is FD_TOPOB_UNPOLLED (as
+   integration/fd_verify_topo_hip.patch makes it in the reference's
+   topologies), so the stem polls no in link and the patched tile reads the
+   link by published seq ranges from after_credit, the GPU reading the
+   mcache lines (fd_verify_hip_tile_submit_range).  Such a tile moves its
+   fseq only once the GPU has read a range, so the producer needs no margin
+   for frags a tile holds unread.
+
    Walk mode (environment TILE_RUN_WALK=1 on the tiles): each tile's round
    robin count is set past every seq, so before_frag filters every frag and
    the tile only walks the link (mcache poll, before_frag, fseq updates)
@@ -45,6 +54,7 @@ static int drv_should_shutdown( void * ctx );
 #define STEM_CALLBACK_SHOULD_SHUTDOWN( ctx ) drv_should_shutdown( ctx )
 #include TILE_SRC
 static int     drv_walk;            /* TILE_RUN_WALK: filter every frag, shut down at the link's end */
+static int     drv_range;           /* TILE_RUN_RANGE: the in link unpolled, read by range */
 static ulong * drv_in_fseq;
 static ulong   drv_n;
 #include "../topo/fd_topob.h"
@@ -178,11 +188,14 @@ produce( char const * path, char const * stream, ulong tile_cnt, ulong in_depth 
      between the stem consuming them (its fseq) and the GPU reading them:
      the producer stays that much (times the tile count: each tile takes
      every T-th seq) further behind, so nothing is overrun */
-  ulong const hold = ( FD_VERIFY_HIP_GPU_COPY && !getenv( "TILE_RUN_NO_MARGIN" ) )   /* the env: overrun tests */
+  ulong const hold = ( FD_VERIFY_HIP_GPU_COPY && !getenv( "TILE_RUN_NO_MARGIN" )    /* the env: overrun tests */
+                       && !getenv( "TILE_RUN_RANGE" ) )                           /* range tiles hold none */
                      ? FD_VERIFY_HIP_RING*FD_VERIFY_HIP_BATCH_CAP*tile_cnt : 0UL;  /* seq % T: a tile's held frags
                                                                                      span T times as many seqs */
   if( FD_UNLIKELY( in_depth<hold+128UL ) ) FD_LOG_ERR(( "in_depth %lu too small for the GPU copy's %lu held frags", in_depth, hold ));
-  ulong lim = 0UL, chunk = chunk0;
+  ulong lim = getenv( "TILE_RUN_NO_FLOW" ) ? ULONG_MAX : 0UL;  /* the env: the reference's unreliable link, no
+                                                                  flow control at all (overrun tests) */
+  ulong chunk = chunk0;
   for( ulong seq=0UL; seq<n; seq++ ) {
     while( seq>=lim ) {                                        /* flow control against the slowest tile */
       ulong m = ULONG_MAX;
@@ -238,11 +251,12 @@ produce( char const * path, char const * stream, ulong tile_cnt, ulong in_depth 
           "\"dedup\": %lu, \"bundle_peer_fail\": %lu, \"seconds\": %.6f, \"publish_s\": %.6f, "
           "\"verifies_per_s\": %.1f, \"frags_per_s\": %.1f, \"batches\": %lu, \"gpu_ms_per_batch\": %.4f, "
           "\"host_ms_per_batch\": %.4f, \"batch_max\": %lu, \"batch_cap\": %lu, \"inflight\": %lu, "
-          "\"flush_ns\": %ld, \"in_depth\": %lu, \"tile_cnt\": %lu, \"overrun\": %lu, \"gpu_copy\": %d}\n",
+          "\"flush_ns\": %ld, \"in_depth\": %lu, \"tile_cnt\": %lu, \"overrun\": %lu, \"gpu_copy\": %d, "
+          "\"range\": %d}\n",
           frags, sigs, pub, parse, verify, dedup, bundle, s, (double)( t_pub - t0 )*1e-9, (double)sigs/s,
           (double)frags/s, batches, batches ? gpu_ms/(double)batches : 0.0, batches ? host_ms/(double)batches : 0.0,
           FD_VERIFY_HIP_BATCH_MAX, FD_VERIFY_HIP_BATCH_CAP, FD_VERIFY_HIP_INFLIGHT, (long)FD_VERIFY_HIP_FLUSH_NS,
-          in_depth, tile_cnt, overrun, (int)FD_VERIFY_HIP_GPU_COPY );
+          in_depth, tile_cnt, overrun, (int)FD_VERIFY_HIP_GPU_COPY, !!getenv( "TILE_RUN_RANGE" ) );
   fflush( stdout );
   munmap( base, map_sz );
   unlink( path );
@@ -319,10 +333,14 @@ tile( char const * path, ulong t ) {
   out->dcache = fd_dcache_join( fd_dcache_new( drv_malloc( fd_dcache_align(), fd_dcache_footprint( out_data, 0UL ) ),
                                                out_data, 0UL ) );
   FD_TEST( quic->mcache && quic->dcache && out->mcache && out->dcache );
-  fd_topob_tile_in ( topo, "verify", 0UL, "verify", "quic_verify", 0UL, FD_TOPOB_UNRELIABLE, FD_TOPOB_POLLED );
+  drv_range = !!getenv( "TILE_RUN_RANGE" );
+  fd_topob_tile_in ( topo, "verify", 0UL, "verify", "quic_verify", 0UL, FD_TOPOB_UNRELIABLE,
+                     drv_range ? FD_TOPOB_UNPOLLED : FD_TOPOB_POLLED );
   fd_topob_tile_out( topo, "verify", 0UL, "verify_dedup", 0UL );
   tile->kind_id = t;                                            /* GPU t % devices; round robin index */
   quic->mtu = FD_TPU_REASM_MTU; out->mtu = FD_TPU_PARSED_MTU;
+  ulong * in_fseq = fd_fseq_join( base + hdr->fseq_off + t*hdr->fseq_stride );
+  tile->in_link_fseq[ 0 ] = in_fseq;                            /* fd_topo_fill_tile's: the range tile moves it */
 
   privileged_init( topo, tile );
   fd_verify_ctx_t * ctx = (fd_verify_ctx_t *)scratch;
@@ -341,7 +359,6 @@ tile( char const * path, ulong t ) {
   fd_metrics_register( fd_metrics_new( metrics, 1UL, 1UL ) );
   void * stem_scratch = aligned_alloc( FD_STEM_SCRATCH_ALIGN,
                                        fd_ulong_align_up( stem_scratch_footprint( 1UL, 1UL, 1UL ), FD_STEM_SCRATCH_ALIGN ) );
-  ulong * in_fseq = fd_fseq_join( base + hdr->fseq_off + t*hdr->fseq_stride );
   drv_in_fseq = in_fseq; drv_n = hdr->n;
   uchar cons_mem[ 256 ] __attribute__((aligned(128)));
   FD_TEST( fd_fseq_footprint()<=sizeof(cons_mem) );
@@ -359,7 +376,7 @@ tile( char const * path, ulong t ) {
   __atomic_fetch_add( &hdr->ready, 1UL, __ATOMIC_SEQ_CST );
   while( !hdr->start ) FD_SPIN_PAUSE();
   drv_deadline = fd_log_wallclock() + 600L*1000000000L;
-  stem_run1( 1UL, in_mcache, in_fseqs, 1UL, out_mcache, 1UL, cons_out, cons_fseqs, FD_VERIFY_HIP_STEM_BURST, 0L, rng,
+  stem_run1( drv_range ? 0UL : 1UL, in_mcache, in_fseqs, 1UL, out_mcache, 1UL, cons_out, cons_fseqs, FD_VERIFY_HIP_STEM_BURST, 0L, rng,
              stem_scratch, ctx );
   long t_end = fd_log_wallclock();
 

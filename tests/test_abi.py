@@ -15,7 +15,8 @@ def declared_functions(header="fd_ed25519_hip.h"):
     hdr = open(os.path.join(REPO, "include", header)).read()
     hdr = re.sub(r"/\*.*?\*/", "", hdr, flags=re.S)
     names = set(re.findall(r"\b(fd_\w*)\s*\(", hdr))
-    return names
+    inline = set(re.findall(r"static\s+inline\s+\w+\s+(fd_\w+)\s*\(", hdr))   # header-only helpers
+    return names - inline
 
 
 def test_build_and_exports():
@@ -87,3 +88,27 @@ def test_kernel_hashes_found():
     h = engine_kernel_hashes()
     assert set(h) == {"k_verify_dsm", "k_verify_prep"}, h
     assert all(len(v) == 16 and int(v, 16) >= 0 for v in h.values())
+
+
+def test_range_frag_cnt_matches(tmp_path):
+    """fd_verify_hip_range_frag_cnt (include/fd_verify_hip.h, the patched
+    tile's count of its round robin share of a seq range) against its Python
+    mirror and a brute-force count, seqs near 0 and near 2^40."""
+    import itertools
+    grid = [(s0, cnt, rr, idx) for s0, cnt, rr in itertools.product((0, 1, 5, 2**40 + 3), (0, 1, 2, 7, 64, 1000),
+                                                                      (1, 2, 3, 6, 16))
+            for idx in (0, rr - 1, rr // 2, rr)]                     # idx == rr: an out of range index (0)
+    src = ['#include <stdio.h>', '#include "fd_verify_hip.h"', 'static const unsigned long g[][4] = {']
+    src += ['  { %dUL, %dUL, %dUL, %dUL },' % t for t in grid]
+    src += ['};', 'int main( void ) {', '  for( unsigned long i=0; i<sizeof(g)/sizeof(g[0]); i++ )',
+            '    printf( "%lu\\n", fd_verify_hip_range_frag_cnt( g[i][0], g[i][1], g[i][2], g[i][3] ) );',
+            '  return 0;', '}']
+    c = tmp_path / "rc.c"
+    c.write_text("\n".join(src) + "\n")
+    exe = tmp_path / "rc"
+    subprocess.check_call(["gcc", "-std=c11", "-Wall", "-Wextra", "-Werror", "-I", os.path.join(REPO, "include"),
+                           str(c), "-o", str(exe)])
+    got = [int(x) for x in subprocess.check_output([str(exe)]).decode().split()]
+    for (s0, cnt, rr, idx), g in zip(grid, got):
+        brute = sum(1 for q in range(s0, s0 + cnt) if q % rr == idx) if idx < rr else 0
+        assert g == brute == verify_tile.range_frag_cnt(s0, cnt, rr, idx), (s0, cnt, rr, idx, g, brute)

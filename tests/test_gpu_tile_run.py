@@ -14,6 +14,12 @@ tile leg runs it.
   them: the tile drops them as overruns (fd_verify_hip_tile_complete_skip)
   and keeps running -- every frag is either an outcome or an overrun, and
   nothing aborts on the overwritten bytes.
+- Range mode (TILE_RUN_RANGE: the tiles' quic_verify link unpolled, read by
+  published seq ranges the GPU gathers, fd_verify_hip_tile_submit_range)
+  gives the host copy's outcome counts at one and two tiles; with a
+  producer under no flow control at all (TILE_RUN_NO_FLOW: the reference's
+  unreliable link) on a shallow link, the tile is lapped, drops the lost
+  frags as the stem drops an overrun, and keeps running.
 The full-byte equality of the patched tile with the reference tile is
 tests/test_gpu_tile_hip.py (mock topology, both copy forms via the kernel
 tests in tests/test_gpu_txn_batch.py)."""
@@ -57,5 +63,27 @@ def test_overruns_are_dropped_not_fatal(stream, tmp_path, monkeypatch):
     path, s = stream
     monkeypatch.setenv("TILE_RUN_NO_MARGIN", "1")
     r = TB.run_one(os.path.join(TB.BUILD, "tile_run"), path, 1, 16384, 120, str(tmp_path / "ovr"))
+    assert r["overrun"] > 0, r
+    assert r["frags"] + r["overrun"] == s.n
+
+
+@pytest.mark.parametrize("tiles", [1, 2])
+def test_range_mode_equals_host_copy(stream, tmp_path, tiles):
+    import tile_bench as TB
+    path, s = stream
+    r = TB.run_one(os.path.join(TB.BUILD, "tile_run"), path, tiles, 131072, 120, str(tmp_path / "range"),
+                   range_mode=True)
+    h = TB.run_one(os.path.join(TB.BUILD, "tile_run_hostcopy"), path, tiles, 131072, 120, str(tmp_path / "host"))
+    assert r["range"] == 1 and h["range"] == 0
+    assert r["overrun"] == 0 and h["overrun"] == 0
+    assert _outcomes(r) == _outcomes(h)
+    assert r["frags"] == s.n
+
+
+def test_range_mode_overrun_is_dropped(stream, tmp_path, monkeypatch):
+    import tile_bench as TB
+    path, s = stream
+    monkeypatch.setenv("TILE_RUN_NO_FLOW", "1")
+    r = TB.run_one(os.path.join(TB.BUILD, "tile_run"), path, 1, 4096, 120, str(tmp_path / "rovr"), range_mode=True)
     assert r["overrun"] > 0, r
     assert r["frags"] + r["overrun"] == s.n

@@ -14,7 +14,11 @@ stream (tests/golden/c4_stream_2048.npz).
   pins that diagnosis: its map holds values that are not tags in its ring,
   and it misses dedups the fixed tile catches.
 - The GPU tile (FD_HAS_HIP) compiles and links against the engine; it runs
-  in tests/test_gpu_tile_hip.py."""
+  in tests/test_gpu_tile_hip.py.
+- integration/fd_verify_topo_hip.patch applies to both of the reference's
+  topologies and changes exactly one thing in each: the verify tiles'
+  quic_verify in link is FD_TOPOB_UNPOLLED when FD_HAS_HIP (range mode,
+  tests/test_gpu_tile_run.py), FD_TOPOB_POLLED otherwise."""
 import os
 import subprocess
 
@@ -69,3 +73,40 @@ def test_gpu_tile_links_against_engine():
     for s in ("fd_verify_hip_tile_poll", "fd_verify_hip_tile_submit_frags", "fd_verify_hip_tile_complete",
               "fd_ed25519_hip_host_register"):
         assert s in syms, s
+
+
+REF = "/root/reference"
+
+
+@pytest.mark.skipif(not os.path.isdir(REF), reason="needs /root/reference")
+def test_topology_patch_applies_and_only_unpolls_quic_verify(tmp_path):
+    import shutil
+    files = ["src/app/fdctl/topology.c", "src/app/firedancer/topology.c"]
+    for f in files:
+        os.makedirs(tmp_path / os.path.dirname(f), exist_ok=True)
+        shutil.copy(os.path.join(REF, f), tmp_path / f)
+    patch = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "integration",
+                         "fd_verify_topo_hip.patch")
+    subprocess.check_call(["patch", "-s", "-p1", "-i", patch], cwd=tmp_path)
+    for f in files:
+        old = open(os.path.join(REF, f)).read().splitlines()
+        new = open(tmp_path / f).read().splitlines()
+        changed = [(a, b) for a, b in zip([x for x in old if "quic_verify" in x and "verify\"," in x],
+                                          [x for x in new if "quic_verify" in x and "verify\"," in x])]
+        tile_in = [(a, b) for a, b in changed if "fd_topob_tile_in" in a]
+        assert len(tile_in) == 1 and tile_in[0][1] == tile_in[0][0].replace("FD_TOPOB_POLLED", "FD_VERIFY_QUIC_POLL")
+        body = "\n".join(new)
+        assert "#define FD_VERIFY_QUIC_POLL FD_TOPOB_UNPOLLED" in body and "#define FD_VERIFY_QUIC_POLL FD_TOPOB_POLLED" in body
+        # every other line is the reference's
+        extra = [x for x in new if x not in old]
+        assert all("FD_VERIFY_QUIC_POLL" in x or x.startswith(("/*", "   ", "#if", "#else", "#endif")) or not x.strip()
+                   for x in extra), extra
+
+
+def test_tile_run_uses_range_entry_points():
+    exe = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "integration", "_build", "tile_run")
+    if not os.path.exists(exe):
+        pytest.skip("integration/_build missing")
+    syms = subprocess.run(["nm", "-u", exe], capture_output=True, text=True).stdout
+    for s_ in ("fd_verify_hip_tile_submit_range", "fd_verify_hip_tile_complete_range"):
+        assert s_ in syms, s_

@@ -45,10 +45,15 @@ def binary(b, i, g=1):
 
 
 def parse_config(cfg):
-    """b<batch_max>i<inflight>[h] -> (batch_max, inflight, gpu_copy)"""
+    """b<batch_max>i<inflight>[h|r] -> (batch_max, inflight, gpu_copy); h: the host during_frag
+    copy, r: range mode (the GPU-copy binary with the quic_verify link unpolled, is_range())"""
     g = 0 if cfg.endswith("h") else 1
-    b, i = cfg.rstrip("h")[1:].split("i")
+    b, i = cfg.rstrip("hr")[1:].split("i")
     return int(b), int(i), g
+
+
+def is_range(cfg):
+    return cfg.endswith("r")
 
 
 def build():
@@ -72,17 +77,19 @@ def make_stream(n, path, seed=0x5eed0004, depth=4194302):
     return s
 
 
-def run_one(exe, stream, tiles, in_depth, timeout, logdir, walk=False):
+def run_one(exe, stream, tiles, in_depth, timeout, logdir, walk=False, range_mode=False):
     """One producer and `tiles` tile processes; every process's stderr goes to
     a file in logdir; liveness is checked every second (a tile that dies ends
-    the run at once), with a progress line on stderr."""
+    the run at once), with a progress line on stderr.  range_mode: the tiles
+    read the link by range (TILE_RUN_RANGE, tile_run.c)."""
     shm = f"/dev/shm/fd_tile_bench_{os.getpid()}"
     if os.path.exists(shm):
         os.unlink(shm)
     os.makedirs(logdir, exist_ok=True)
     perr = open(os.path.join(logdir, "producer.err"), "w")
+    renv = dict(os.environ, TILE_RUN_RANGE="1") if range_mode else None
     prod = subprocess.Popen([exe, "produce", shm, stream, str(tiles), str(in_depth)], stdout=subprocess.PIPE,
-                            stderr=perr, text=True)
+                            stderr=perr, text=True, env=renv)
     procs, terr = [], []
     t0 = time.time()
     try:
@@ -91,7 +98,7 @@ def run_one(exe, stream, tiles, in_depth, timeout, logdir, walk=False):
             raise RuntimeError(f"producer: {line!r} (see {logdir}/producer.err)")
         for t in range(tiles):
             terr.append(open(os.path.join(logdir, f"tile{t}.err"), "w"))
-            env = dict(os.environ, TILE_RUN_WALK="1") if walk else None
+            env = dict(os.environ, TILE_RUN_WALK="1") if walk else renv
             procs.append(subprocess.Popen([exe, "tile", shm, str(t)], stdout=subprocess.DEVNULL, stderr=terr[-1], env=env))
         last = 0.0
         while prod.poll() is None:
@@ -129,7 +136,8 @@ def main():
     ap.add_argument("--frags", type=int, default=1 << 21)
     ap.add_argument("--tiles", default="6")
     ap.add_argument("--configs", default="b4096i2",
-                    help="b<batch_max>i<inflight>[h], comma-separated (binaries from --build; h: host during_frag copy)")
+                    help="b<batch_max>i<inflight>[h|r], comma-separated (binaries from --build; h: host during_frag "
+                         "copy; r: range mode, the quic_verify link unpolled)")
     ap.add_argument("--in-depth", type=int, default=16384,
                     help="quic_verify mcache depth (config tiles.verify.receive_buffer_size, default.toml:1153)")
     ap.add_argument("--repeat", type=int, default=1)
@@ -166,7 +174,7 @@ def main():
                     depth *= 2
                 for r in range(args.repeat):
                     res = run_one(exe, stream, tiles, depth, args.timeout,
-                                  os.path.join(args.logdir, f"{cfg}_t{tiles}_{r}"))
+                                  os.path.join(args.logdir, f"{cfg}_t{tiles}_{r}"), range_mode=is_range(cfg))
                     res["config"] = cfg
                     print(json.dumps(res), flush=True)
                     if res.get("overrun"):          # dropped frags: not a valid throughput
