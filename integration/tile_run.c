@@ -39,6 +39,12 @@
    fseq only once the GPU has read a range, so the producer needs no margin
    for frags a tile holds unread.
 
+   Prelay (environment TILE_RUN_PRELAY=1 on the producer): the dcache holds
+   the whole stream (in_depth >= the frag count) and every frag is laid into
+   it before READY, so the timed loop only publishes mcache lines: the rate
+   is the verify stage's, not one producer core's copy (~15-20 M frags/s of
+   C4 frags on the GPU box).
+
    Walk mode (environment TILE_RUN_WALK=1 on the tiles): each tile's round
    robin count is set past every seq, so before_frag filters every frag and
    the tile only walks the link (mcache poll, before_frag, fseq updates)
@@ -150,7 +156,14 @@ produce( char const * path, char const * stream, ulong tile_cnt, ulong in_depth 
      (the producer writes each frag into it just before publishing it, so a
      tile's during_frag copies recently written bytes, as it would behind a
      quic tile) */
+  int const prelay = !!getenv( "TILE_RUN_PRELAY" );
+  if( FD_UNLIKELY( prelay && in_depth<n ) ) FD_LOG_ERR(( "prelay: in_depth %lu < %lu frags", in_depth, n ));
   ulong data_sz = fd_dcache_req_data_sz( FD_TPU_RAW_MTU, in_depth, 1UL, 1 );
+  if( prelay ) {                                             /* every frag at its own place: no wrap */
+    data_sz = 2UL*FD_TPU_RAW_MTU + 4096UL;
+    for( ulong j=0UL; j<n; j++ ) data_sz += fd_ulong_align_up( fsz[ j ], 2UL*FD_CHUNK_SZ );
+    data_sz = fd_ulong_align_up( data_sz, 4096UL );
+  }
   ulong mc_off  = fd_ulong_align_up( sizeof(run_hdr_t), fd_mcache_align() );
   ulong fs_off  = fd_ulong_align_up( mc_off + fd_mcache_footprint( in_depth, 0UL ), fd_fseq_align() );
   ulong fs_strd = fd_ulong_align_up( fd_fseq_footprint(), 128UL );
@@ -169,6 +182,22 @@ produce( char const * path, char const * stream, ulong tile_cnt, ulong in_depth 
   hdr->n = n; hdr->tile_cnt = tile_cnt; hdr->seed = seed; hdr->tcache_depth = depth; hdr->in_depth = in_depth;
   hdr->mcache_off = mc_off; hdr->dcache_off = dc_off; hdr->fseq_off = fs_off; hdr->fseq_stride = fs_strd;
   hdr->dcache_data_sz = data_sz; hdr->map_sz = map_sz;
+  ulong * pchunk = NULL;
+  if( prelay ) {
+    pchunk = malloc( n*sizeof(ulong) ); FD_TEST( pchunk );
+    ulong c = chunk0;
+    for( ulong j=0UL; j<n; j++ ) {
+      fd_txn_m_t * m = (fd_txn_m_t *)fd_chunk_to_laddr( base, c );
+      memset( m, 0, sizeof(fd_txn_m_t) );
+      memcpy( &m->block_engine.bundle_id, in+poff[ j ], 8 );
+      m->payload_sz = (ushort)( fsz[ j ] - sizeof(fd_txn_m_t) );
+      memcpy( fd_txn_m_payload( m ), in+poff[ j ]+10UL, m->payload_sz );
+      pchunk[ j ] = c;
+      ulong nc = fd_dcache_compact_next( c, fsz[ j ], chunk0, wmark );
+      if( FD_UNLIKELY( nc<c && j+1UL<n ) ) FD_LOG_ERR(( "prelay: dcache wrapped at frag %lu", j ));
+      c = nc;
+    }
+  }
   FD_COMPILER_MFENCE();
   hdr->magic = RUN_MAGIC;
   FD_COMPILER_MFENCE();
@@ -204,14 +233,17 @@ produce( char const * path, char const * stream, ulong tile_cnt, ulong in_depth 
       if( seq>=lim ) FD_SPIN_PAUSE();
       if( fd_log_wallclock()-t0 > 600L*1000000000L ) FD_LOG_ERR(( "tiles stalled at seq %lu", seq ));
     }
-    fd_txn_m_t * m = (fd_txn_m_t *)fd_chunk_to_laddr( base, chunk );
-    memset( m, 0, sizeof(fd_txn_m_t) );
-    memcpy( &m->block_engine.bundle_id, in+poff[ seq ], 8 );
-    m->payload_sz = (ushort)( fsz[ seq ] - sizeof(fd_txn_m_t) );
-    memcpy( fd_txn_m_payload( m ), in+poff[ seq ]+10UL, m->payload_sz );
+    if( prelay ) chunk = pchunk[ seq ];
+    else {
+      fd_txn_m_t * m = (fd_txn_m_t *)fd_chunk_to_laddr( base, chunk );
+      memset( m, 0, sizeof(fd_txn_m_t) );
+      memcpy( &m->block_engine.bundle_id, in+poff[ seq ], 8 );
+      m->payload_sz = (ushort)( fsz[ seq ] - sizeof(fd_txn_m_t) );
+      memcpy( fd_txn_m_payload( m ), in+poff[ seq ]+10UL, m->payload_sz );
+    }
     ulong ts = (ulong)fd_frag_meta_ts_comp( fd_tickcount() );
     fd_mcache_publish( mcache, in_depth, seq, 0UL, chunk, fsz[ seq ], ctl, ts, ts );
-    chunk = fd_dcache_compact_next( chunk, fsz[ seq ], chunk0, wmark );
+    if( !prelay ) chunk = fd_dcache_compact_next( chunk, fsz[ seq ], chunk0, wmark );
   }
   long t_pub = fd_log_wallclock();
   ulong done = 0UL;
@@ -260,7 +292,7 @@ produce( char const * path, char const * stream, ulong tile_cnt, ulong in_depth 
   fflush( stdout );
   munmap( base, map_sz );
   unlink( path );
-  free( in ); free( fsz ); free( poff );
+  free( in ); free( fsz ); free( poff ); free( pchunk );
   return 0;
 }
 

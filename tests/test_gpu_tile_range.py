@@ -138,7 +138,7 @@ def test_bad_ranges_refused(stream):
     m, _ = mcache_lines(256, 0, in_chunk, in_sz, rng)
     tile = V.VerifyTile(None, max_txn=64, hashmap_seed=1, tcache_depth=64, chunk_sigs=1 << 16)
     d_m, d_in = _dev(m.view(np.uint8)), _dev(region)
-    d_out, oc = _dev(np.zeros(64 * PARSED_CHUNKS * 65, np.uint8)), _dev(np.arange(64, dtype=np.uint32) * 34, np.int32)
+    d_out, oc = _dev(np.zeros(64 * PARSED_CHUNKS * 65, np.uint8)), _dev(np.zeros(512, np.uint32), np.int32)
     wm = CHUNK_OFF + region.size // 64 - 40
     for depth, seq_cnt, rr_cnt, rr_idx, c0, chunk_off in [
             (255, 64, 1, 0, CHUNK_OFF, CHUNK_OFF),       # depth not a power of 2

@@ -5,7 +5,8 @@
 # Usage: bash tools/gpu_session.sh <tag> <step> [<step> ...]
 #   -> gpurun_out/<tag>/...   (stops at the first failing step)
 #
-# Steps (arguments after ':' are passed on, ',' separates them):
+# Steps (arguments after ':' are passed on, ',' separates them, '+' stands for
+# a ',' inside one argument: --tiles,1+2+4 is --tiles 1,2,4):
 #   tests[:files]      pytest -m gpu on the given test files (default: all)
 #   bench[:args]       python bench.py <args>                  -> bench_<n>.json
 #   c4[:args]          python bench.py --config c4 <args>       -> c4_<n>.json
@@ -24,8 +25,9 @@
 #   smoke              __graft_entry__.smoke()
 # Round-4 sessions, as steps: replay/tile tests + tile sweep (r04n) =
 #   tests:tests/test_gpu_replay_block.py,tests/test_gpu_replay.py,tests/test_gpu_txn_batch.py,tests/test_gpu_tile_hip.py
-#   replay:--txns,16384,98039,--sched  tile:--frags,2097152,--tiles,1,2,4,--configs,b8192i4,b8192i4h
-# the link-walk bound (r04o): tile:--walk,--tiles,1,2,4,--configs,b8192i4
+#   replay:--txns,16384+98039,--sched  tile:--frags,2097152,--tiles,1+2+4,--configs,b8192i4+b8192i4h
+# the link-walk bound (r04o): tile:--walk,--tiles,1+2+4,--configs,b8192i4
+# range mode (r04w): tile:--frags,2097152,--tiles,1+2+4,--configs,b8192i3r+b8192i3+b4096i3r
 # (It replaces the round-3 per-session scripts tools/run_r03*.sh and the
 # one-off A/B runners; they are in git history before this file's commit.)
 # Every GPU step runs under its own timeout; a failure ends the session.
@@ -40,7 +42,7 @@ VALU_G="SQ_INSTS_VALU SQ_THREAD_CYCLES_VALU SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_V
 SQ_G="SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_ANY"
 
 fail() { echo "step $1 failed (rc=$2)"; [ -n "$3" ] && tail -40 "$3"; exit $2; }
-args_of() { local a="${1#*:}"; [ "$a" = "$1" ] && a=""; echo "${a//,/ }"; }
+args_of() { local a="${1#*:}"; [ "$a" = "$1" ] && a=""; a="${a//,/ }"; echo "${a//+/,}"; }
 
 pmc_pass() {   # <name> <counters> <cmd...>
   local name=$1 ctr=$2; shift 2

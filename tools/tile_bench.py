@@ -37,7 +37,8 @@ sys.path.insert(0, os.path.join(REPO, "tests"))
 BUILD = os.path.join(REPO, "integration", "_build")
 # (batch_max, inflight, gpu_copy): the patch's FD_VERIFY_HIP_* settings; gpu_copy 0 is the host
 # during_frag copy ("h" suffix)
-SWEEP = [(b, i, g) for b in (1024, 2048, 4096, 8192) for i in (2, 3, 4) for g in (1, 0)]
+SWEEP = [(b, i, g) for b in (1024, 2048, 4096, 8192) for i in (2, 3, 4) for g in (1, 0)] + \
+        [(b, i, 1) for b in (16384, 32768) for i in (3, 4)]     # range mode: few host cycles per frag
 
 
 def binary(b, i, g=1):
@@ -77,7 +78,7 @@ def make_stream(n, path, seed=0x5eed0004, depth=4194302):
     return s
 
 
-def run_one(exe, stream, tiles, in_depth, timeout, logdir, walk=False, range_mode=False):
+def run_one(exe, stream, tiles, in_depth, timeout, logdir, walk=False, range_mode=False, prelay=False):
     """One producer and `tiles` tile processes; every process's stderr goes to
     a file in logdir; liveness is checked every second (a tile that dies ends
     the run at once), with a progress line on stderr.  range_mode: the tiles
@@ -88,8 +89,9 @@ def run_one(exe, stream, tiles, in_depth, timeout, logdir, walk=False, range_mod
     os.makedirs(logdir, exist_ok=True)
     perr = open(os.path.join(logdir, "producer.err"), "w")
     renv = dict(os.environ, TILE_RUN_RANGE="1") if range_mode else None
+    penv = dict(renv or os.environ, TILE_RUN_PRELAY="1") if prelay else renv
     prod = subprocess.Popen([exe, "produce", shm, stream, str(tiles), str(in_depth)], stdout=subprocess.PIPE,
-                            stderr=perr, text=True, env=renv)
+                            stderr=perr, text=True, env=penv)
     procs, terr = [], []
     t0 = time.time()
     try:
@@ -141,6 +143,10 @@ def main():
     ap.add_argument("--in-depth", type=int, default=16384,
                     help="quic_verify mcache depth (config tiles.verify.receive_buffer_size, default.toml:1153)")
     ap.add_argument("--repeat", type=int, default=1)
+    ap.add_argument("--prelay", action="store_true",
+                    help="the producer lays the whole stream into a dcache that holds it before the clock starts "
+                         "(tile_run.c TILE_RUN_PRELAY; link depth = the frag count): the stage's rate, not one "
+                         "producer core's copy")
     ap.add_argument("--walk", action="store_true",
                     help="also time walk mode per tile count: tiles filter every frag (tile_run.c), the link-walk bound")
     ap.add_argument("--timeout", type=float, default=150)
@@ -158,11 +164,12 @@ def main():
         if args.walk:
             exe = binary(4096, 2, 0)
             for tiles in (int(x) for x in args.tiles.split(",")):
-                res = run_one(exe, stream, tiles, args.in_depth, args.timeout,
-                              os.path.join(args.logdir, f"walk_t{tiles}"), walk=True)
+                depth = 1 << (s.n - 1).bit_length() if args.prelay else args.in_depth
+                res = run_one(exe, stream, tiles, depth, args.timeout,
+                              os.path.join(args.logdir, f"walk_t{tiles}"), walk=True, prelay=args.prelay)
                 print(json.dumps({"walk": True, "tile_cnt": tiles, "frags": s.n, "seconds": res["seconds"],
                                   "frags_walked_per_s": s.n / res["seconds"], "regime": res.get("regime"),
-                                  "in_depth": args.in_depth}), flush=True)
+                                  "in_depth": depth, "prelay": args.prelay}), flush=True)
         for cfg in args.configs.split(","):
             exe = binary(*parse_config(cfg))
             b, i, g = parse_config(cfg)
@@ -172,10 +179,14 @@ def main():
                 depth = args.in_depth
                 while g and depth < (i + 1) * 2 * b * tiles + 16384:
                     depth *= 2
+                if args.prelay:
+                    depth = max(depth, 1 << (s.n - 1).bit_length())
                 for r in range(args.repeat):
                     res = run_one(exe, stream, tiles, depth, args.timeout,
-                                  os.path.join(args.logdir, f"{cfg}_t{tiles}_{r}"), range_mode=is_range(cfg))
+                                  os.path.join(args.logdir, f"{cfg}_t{tiles}_{r}"), range_mode=is_range(cfg),
+                                  prelay=args.prelay)
                     res["config"] = cfg
+                    res["prelay"] = args.prelay
                     print(json.dumps(res), flush=True)
                     if res.get("overrun"):          # dropped frags: not a valid throughput
                         continue
@@ -184,7 +195,7 @@ def main():
         print(json.dumps({"metric": "ed25519 verifies/sec through the patched reference verify tile (stem_run1, "
                                     "one GPU)", "value": best["verifies_per_s"], "unit": "verifies/s",
                           "config": best["config"], "tiles": best["tile_cnt"], "frags": best["frags"],
-                          "sigs": best["sigs"], "in_depth": best["in_depth"],
+                          "sigs": best["sigs"], "in_depth": best["in_depth"], "prelay": args.prelay,
                           "workload": "config 4 stream (firedancer_amd/txn_workload.py), GPU-signed"}))
 
 
