@@ -687,6 +687,16 @@ struct pay_view {                                          /* the payload: frag 
   DEVI u32 operator[]( u32 i ) const { return f[FD_VERIFY_HIP_TXNM_SZ + i]; }
 };
 
+/* Out staging (hout != 0, fd_verify_hip_tile_set_staging): out / out_chunk
+   are a staging area in HBM and hout / hout_chunk the caller's out dcache
+   (pinned host memory).  The kernel then works on HBM only -- the copy, the
+   fd_txn_t and the signature records' messages (which the verify reads)
+   land in the staging frag -- and k_out_flush copies to the out dcache
+   exactly the bytes the reference writes there (fdesc[j]: the copy's end,
+   payload_sz, txn_t_sz, gossip, corrupt).  Bytes after_frag reads but
+   during_frag did not copy (a frag shorter than its header or its
+   payload_sz: the out dcache's own bytes) are read from the out dcache, and
+   a host-copied frag (FD_VERIFY_HIP_IN_HOSTCOPY) is read from it too. */
 template<int F>
 __global__ __launch_bounds__(64)
 void k_txnm_batch( ulong n, u8 const * in, u32 const * __restrict__ in_chunk, u16 const * __restrict__ in_sz,
@@ -694,7 +704,8 @@ void k_txnm_batch( ulong n, u8 const * in, u32 const * __restrict__ in_chunk, u1
                    u16 * __restrict__ tsz_o, u64 * __restrict__ tag_o, u64 * __restrict__ bid_o,
                    u32 * __restrict__ first_o, u8 * __restrict__ cnt_o, u32 * __restrict__ misc,
                    u8 * __restrict__ rsig, u8 * __restrict__ rpub, u32 * __restrict__ rmoff,
-                   u32 * __restrict__ rmsz, u32 n_seg, ulong seg_cap ) {
+                   u32 * __restrict__ rmsz, u32 n_seg, ulong seg_cap, u8 const * hout,
+                   u32 const * __restrict__ hout_chunk, u64 * __restrict__ fdesc ) {
   constexpr u32 BUDGET = FB_PIECES_PER_FRAG * (u32)F;                        /* staged pieces per group */
   __shared__ __attribute__((aligned(16))) u8 lds[16u * BUDGET + 32u];       /* + over-read of the last piece */
   /* this group's record segment (fd_hip_order.h): claims, histogram and
@@ -710,11 +721,13 @@ void k_txnm_batch( ulong n, u8 const * in, u32 const * __restrict__ in_chunk, u1
   /* per-frag metadata on lanes [0, nf) */
   bool const fl = lane < nf;
   ulong const j = j0 + lane;
-  u32 ic = 0u, oc = 0u, sz = 0u, kind = 0u;
+  u32 ic = 0u, oc = 0u, sz = 0u, kind = 0u, hoc = 0u;
   if( fl ) { oc = out_chunk[j]; sz = in_sz[j]; kind = in_kind[j]; }
   if( fl && !(kind & FD_VERIFY_HIP_IN_HOSTCOPY) ) ic = in_chunk[j];
+  if( fl && hout ) hoc = hout_chunk[j];
   u8 *       dst = out + 64ul * oc;
-  u8 const * src = (kind & FD_VERIFY_HIP_IN_HOSTCOPY) ? (u8 const *)dst : in + 64ul * ic;   /* host did during_frag */
+  u8 const * hdst = hout ? hout + 64ul * hoc : (u8 const *)dst;              /* the out dcache's frag */
+  u8 const * src = (kind & FD_VERIFY_HIP_IN_HOSTCOPY) ? hdst : in + 64ul * ic;  /* host did during_frag */
   u32 const src_lo = (u32)(u64)src, src_hi = (u32)((u64)src >> 32);
   bool const gossip = fl && kind == FD_VERIFY_HIP_IN_GOSSIP;
   u32 tsz_g = 0u;
@@ -734,7 +747,7 @@ void k_txnm_batch( ulong n, u8 const * in, u32 const * __restrict__ in_chunk, u1
       bad = sz > FD_VERIFY_HIP_TPU_RAW_MTU;
       if( !bad ) {
         hi = sz > FD_VERIFY_HIP_TXNM_SZ ? sz : FD_VERIFY_HIP_TXNM_SZ;       /* with the whole header */
-        cend = src == dst ? 0u : sz;                                        /* in place: copied by the host tile */
+        cend = src == (u8 const *)dst ? 0u : sz;                            /* in place: copied by the host tile */
       }
     }
   }
@@ -787,7 +800,7 @@ void k_txnm_batch( ulong n, u8 const * in, u32 const * __restrict__ in_chunk, u1
      a payload_sz past the frag) those are the out dcache's own bytes.  A
      group with such a frag, or one whose pieces overflow the LDS budget,
      parses through frag_view from global memory instead of LDS. */
-  frag_view const fv = { src, dst, cend };
+  frag_view const fv = { src, hdst, cend };
   u32 const hb = 16u * excl;                                                /* the frag's first staged byte in LDS */
   u32 psz = 0u, tsz = 0u, nsig = 0u, side = 0u;
   u64 bid = 0ul, tag = 0ul;
@@ -796,7 +809,7 @@ void k_txnm_batch( ulong n, u8 const * in, u32 const * __restrict__ in_chunk, u1
     if( gossip ) {
       psz = bad ? 0u : tsz_g;
     } else if( !bad ) {
-      bool short_hdr = src != dst && sz < FD_VERIFY_HIP_TXNM_SZ;
+      bool short_hdr = src != (u8 const *)dst && sz < FD_VERIFY_HIP_TXNM_SZ;
       if( packed && !short_hdr ) {
         psz = *(u16 const *)(lds + hb + FD_VERIFY_HIP_TXNM_PAYLOAD_SZ_OFF);
         bid = *(u64 const *)(lds + hb + FD_VERIFY_HIP_TXNM_BUNDLE_ID_OFF);
@@ -806,8 +819,13 @@ void k_txnm_batch( ulong n, u8 const * in, u32 const * __restrict__ in_chunk, u1
         for( u32 k = 0; k < 8u; k++ ) bid |= (u64)fv[FD_VERIFY_HIP_TXNM_BUNDLE_ID_OFF + k] << (8u*k);
       }
       if( psz > FD_TXN_HIP_MTU ) { bad = 1u; psz = 0u; }
-      u32 have = src == dst ? ((hi + 15u) & ~15u) : sz;                     /* bytes of the out frag staged */
+      u32 have = src == (u8 const *)dst ? ((hi + 15u) & ~15u) : sz;         /* bytes of the out frag staged */
       side = short_hdr || FD_VERIFY_HIP_TXNM_SZ + psz > have;               /* parse reads bytes not staged */
+      /* out staging: the payload bytes past the copy are the out dcache's
+         (stale) bytes, and the verify hashes the message from the staging
+         frag -- bring them over (a frag shorter than its payload_sz only) */
+      if( hout && !bad )
+        for( u32 x = cend; x < FD_VERIFY_HIP_TXNM_SZ + psz; x++ ) dst[x] = hdst[x];
     }
     if( bad ) atomicOr( flag, 1u );
   }
@@ -834,6 +852,7 @@ void k_txnm_batch( ulong n, u8 const * in, u32 const * __restrict__ in_chunk, u1
     tsz = glob ? txn_parse( pv, psz_p, tout, sp ) : txn_parse_lds( lds + pb, psz_p, tout, sp );
     *(u16 *)(dst + FD_VERIFY_HIP_TXNM_TXN_T_SZ_OFF) = (u16)tsz;
     nsig = tsz ? sp.nsig : 0u;
+    if( fdesc ) fdesc[j] = (u64)cend | ((u64)psz << 12) | ((u64)tsz << 23) | ((u64)gossip << 33) | ((u64)bad << 34);
   }
   TXTR( 4 );
 
@@ -889,8 +908,10 @@ void k_txnm_batch( ulong n, u8 const * in, u32 const * __restrict__ in_chunk, u1
     bool live = q < 6u * rtot && k < flc;                                   /* k >= flc: a capped frag */
     uint4 v;
     if( glob ) {
-      u32 fic = __shfl( ic, (int)f ), foc = __shfl( oc, (int)f ), fce = __shfl( cend, (int)f );
-      pay_view const fp = { { in + 64ul * fic, out + 64ul * foc, fce } };
+      u32 fsl = __shfl( src_lo, (int)f ), fsh = __shfl( src_hi, (int)f ), fce = __shfl( cend, (int)f );
+      u32 fhl = __shfl( (u32)(u64)hdst, (int)f ), fhh = __shfl( (u32)((u64)hdst >> 32), (int)f );
+      pay_view const fp = { { (u8 const *)(((u64)fsh << 32) | (u64)fsl), (u8 const *)(((u64)fhh << 32) | (u64)fhl),
+                              fce } };
       u32 w[4] = { 0u, 0u, 0u, 0u };
       if( live )
         for( u32 x = 0; x < 16u; x++ ) w[x >> 2] |= fp[at + x] << (8u*(x & 3u));
@@ -940,6 +961,56 @@ void k_txnm_batch( ulong n, u8 const * in, u32 const * __restrict__ in_chunk, u1
     acc += (u64)(u32)__builtin_amdgcn_readlane( (int)rd, g ) | ((u64)(u32)__builtin_amdgcn_readlane( (int)wr, g ) << 32);
   if( lane == 0u ) atomicAdd( (unsigned long long *)(seg + SEG_BYTES_W), (unsigned long long)acc );
   TXTR( 7 );
+}
+
+/* Out staging's last step: frag j's staging bytes to the out dcache, only
+   those the reference writes there (fd_verify_tile.c:64-99 and :118-120):
+   during_frag's copy [0, cend) -- for a gossip vote the header fields and
+   the payload [80, 80 + payload_sz) -- txn_t_sz, and the fd_txn_t at
+   fd_txn_m_txn_t; every other byte of the out chunk keeps its value.  One
+   wave per frag, a 16-byte piece per lane: whole pieces as one store
+   (coalesced across the wave), the edge pieces by dword and byte. */
+DEVI u32 piece_mask( u32 p0, u32 a, u32 b ) {               /* bytes of [p0, p0+16) in [a, b), as a 16-bit mask */
+  u32 lo = a > p0 ? a - p0 : 0u, hi = b < p0 + 16u ? (b > p0 ? b - p0 : 0u) : 16u;
+  return hi > lo ? ((0xffffu >> (16u - (hi - lo))) << lo) & 0xffffu : 0u;
+}
+
+__global__ __launch_bounds__(256)
+void k_out_flush( ulong n, u8 const * __restrict__ stage, u32 const * __restrict__ stage_chunk, u8 * hout,
+                  u32 const * __restrict__ hout_chunk, u64 const * __restrict__ fdesc ) {
+  ulong const j = (ulong)blockIdx.x * 4ul + (threadIdx.x >> 6);
+  u32 const lane = threadIdx.x & 63u;
+  if( j >= n ) return;
+  u64 const d = fdesc[j];
+  u32 const cend = (u32)(d & 0xfffu), psz = (u32)((d >> 12) & 0x7ffu), tsz = (u32)((d >> 23) & 0x3ffu);
+  bool const gossip = (d >> 33) & 1u, bad = (d >> 34) & 1u;
+  if( bad ) return;                                          /* the tile aborts on it (or skips it as overrun) */
+  u32 const to = (FD_VERIFY_HIP_TXNM_SZ + psz + (FD_VERIFY_HIP_TXN_ALIGN - 1u)) & ~(FD_VERIFY_HIP_TXN_ALIGN - 1u);
+  u32 const end = max( max( cend, 12u ), tsz ? to + tsz : 0u );
+  u8 const * s = stage + 64ul * stage_chunk[j];
+  u8 *       h = hout  + 64ul * hout_chunk[j];
+  for( u32 p0 = 16u * lane; p0 < end; p0 += 1024u ) {
+    u32 m = piece_mask( p0, FD_VERIFY_HIP_TXNM_PAYLOAD_SZ_OFF + 2u, FD_VERIFY_HIP_TXNM_TXN_T_SZ_OFF + 2u );  /* txn_t_sz */
+    if( gossip ) {
+      m |= piece_mask( p0, FD_VERIFY_HIP_TXNM_PAYLOAD_SZ_OFF, FD_VERIFY_HIP_TXNM_SRC_TPU_OFF + 1u );   /* psz .. source_tpu */
+      m |= piece_mask( p0, FD_VERIFY_HIP_TXNM_BUNDLE_ID_OFF, FD_VERIFY_HIP_TXNM_BUNDLE_ID_OFF + 8u );
+      m |= piece_mask( p0, FD_VERIFY_HIP_TXNM_SZ, cend );
+    } else {
+      m |= piece_mask( p0, 0u, cend );
+    }
+    if( tsz ) m |= piece_mask( p0, to, to + tsz );
+    if( !m ) continue;
+    uint4 const v = *(uint4 const *)(s + p0);
+    if( m == 0xffffu ) { *(uint4 *)(h + p0) = v; continue; }
+    u32 const w[4] = { v.x, v.y, v.z, v.w };
+    #pragma unroll
+    for( u32 k = 0; k < 4u; k++ ) {
+      u32 mk = (m >> (4u*k)) & 0xfu;
+      if( mk == 0xfu ) { *(u32 *)(h + p0 + 4u*k) = w[k]; continue; }
+      #pragma unroll
+      for( u32 b = 0; b < 4u; b++ ) if( (mk >> b) & 1u ) h[p0 + 4u*k + b] = (u8)(w[k] >> (8u*b));
+    }
+  }
 }
 
 extern "C" int
@@ -1035,6 +1106,9 @@ struct tile_slot {
      from the in link's mcache lines, and each frag's tsorig (device, host) */
   u32 *         d_rin; u16 * d_rsz; u8 * d_rkind; u32 * d_tso; u32 * h_tso;
   int           range;
+  /* out staging (set_staging): staging frags (STAGE_CHUNKS 64-B chunks
+     each, frag j at chunk STAGE_CHUNKS*j) and k_out_flush's descriptors */
+  u8 *          d_stage; u32 * d_stage_chunk; u64 * d_fdesc;
   fd_ed25519_hip_ctx_t * ctx;   /* the verify context (stream and scratch) the slot's batches run on */
   int           own_ctx;    /* created by set_inflight: batches of different slots run concurrently */
   u32           n_seg;      /* the last batch's record segments (0: not k_txnm_batch) */
@@ -1092,6 +1166,7 @@ struct fd_verify_hip_tile {
   int        ingest_split;   /* FD_VERIFY_HIP_INGEST=split: the three-kernel frag ingest (A/B runs) */
   int        fb;             /* k_txnm_batch frags per workgroup (FD_VERIFY_HIP_FB: 8 or 16) */
   int        ingest_timing;  /* fd_verify_hip_tile_set_ingest_timing */
+  int        staging;        /* fd_verify_hip_tile_set_staging */
   double     last_ingest[4]; /* fd_verify_hip_tile_ingest_stats */
   double     last_gpu_ms, last_host_ms, last_sigs;
   lat_hist   hist[2];        /* batch latency: GPU, host pass (ns) */
@@ -1131,7 +1206,21 @@ static void slot_records( tile_slot & s, ulong need ) {   /* (re)size the per-si
   s.rcap = need;
 }
 
+#define STAGE_CHUNKS 34ul   /* FD_TPU_PARSED_MTU (2168 B) in 64-B chunks */
+
+static void slot_stage_alloc( tile_slot & s, ulong n ) {
+  if( s.d_stage ) return;
+  TX_CHECK( hipMalloc( &s.d_stage, 64ul*STAGE_CHUNKS*n ) );
+  TX_CHECK( hipMalloc( &s.d_stage_chunk, 4ul*n ) );
+  TX_CHECK( hipMalloc( &s.d_fdesc, 8ul*n ) );
+  u32 * h = (u32 *)malloc( 4ul*n );
+  for( ulong j = 0; j < n; j++ ) h[j] = (u32)(STAGE_CHUNKS*j);
+  TX_CHECK( hipMemcpy( s.d_stage_chunk, h, 4ul*n, hipMemcpyHostToDevice ) );
+  free( h );
+}
+
 static void slot_free( tile_slot & s ) {
+  (void)hipFree( s.d_stage ); (void)hipFree( s.d_stage_chunk ); (void)hipFree( s.d_fdesc );
   (void)hipFree( s.d_tsz ); (void)hipFree( s.d_nsig ); (void)hipFree( s.d_sig_at ); (void)hipFree( s.d_acct_at );
   (void)hipFree( s.d_msg_at ); (void)hipFree( s.d_msg_sz ); (void)hipFree( s.d_tag ); (void)hipFree( s.d_first );
   (void)hipFree( s.d_cnt ); (void)hipFree( s.d_tcode ); (void)hipFree( s.d_misc );
@@ -1148,7 +1237,8 @@ __global__ __launch_bounds__(256)
 void k_tile_results( ulong n, u16 const * __restrict__ tsz, signed char const * __restrict__ tcode,
                      u64 const * __restrict__ tag, u64 const * __restrict__ bid, u8 const * __restrict__ kind,
                      u32 const * __restrict__ counter, u32 const * __restrict__ flag, u32 n_seg,
-                     u8 const * __restrict__ out, u32 const * __restrict__ out_chunk, u8 * __restrict__ res );
+                     u8 const * __restrict__ out, u32 const * __restrict__ out_chunk, u64 const * __restrict__ fdesc,
+                     u8 * __restrict__ res );
 
 /* a slot's record buffers at their bound and the results kernel loaded (a
    tile is created in privileged_init: its sandboxed steady state allocates
@@ -1157,7 +1247,7 @@ static void slot_warm( tile_slot & s, ulong max_txn, hipStream_t st ) {
   slot_records( s, 12ul*(max_txn + SLOT_SEG_SLACK) );
   hipLaunchKernelGGL( k_tile_results, dim3( 1 ), dim3( 64 ), 0, st, 0ul, s.d_tsz, s.d_tcode, s.d_tag,
                       (u64 const *)0, (u8 const *)0, s.d_counter, (u32 const *)0, 0u, (u8 const *)0,
-                      (u32 const *)0, s.d_res );
+                      (u32 const *)0, (u64 const *)0, s.d_res );
   TX_CHECK( hipGetLastError() );
 }
 
@@ -1273,7 +1363,8 @@ __global__ __launch_bounds__(256)
 void k_tile_results( ulong n, u16 const * __restrict__ tsz, signed char const * __restrict__ tcode,
                      u64 const * __restrict__ tag, u64 const * __restrict__ bid, u8 const * __restrict__ kind,
                      u32 const * __restrict__ counter, u32 const * __restrict__ flag, u32 n_seg,
-                     u8 const * __restrict__ out, u32 const * __restrict__ out_chunk, u8 * __restrict__ res ) {
+                     u8 const * __restrict__ out, u32 const * __restrict__ out_chunk, u64 const * __restrict__ fdesc,
+                     u8 * __restrict__ res ) {
   ulong j = (ulong)blockIdx.x * blockDim.x + threadIdx.x;
   if( j == 0ul ) {
     ((u32 *)res)[0] = *counter; ((u32 *)res)[1] = flag ? *flag : 0u;
@@ -1289,7 +1380,8 @@ void k_tile_results( ulong n, u16 const * __restrict__ tsz, signed char const * 
   r.tag = tag[j]; r.bid = bid ? bid[j] : 0ul; r.tsz = tsz[j]; r.tcode = tcode[j]; r.kind = kind ? kind[j] : 0u;
   /* frag mode: the out header's payload_sz (after the GPU's own during_frag),
      for the caller's fd_txn_m_realized_footprint */
-  r.pad = out ? (u32)*(u16 const *)(out + 64ul*out_chunk[j] + FD_VERIFY_HIP_TXNM_PAYLOAD_SZ_OFF) : 0u;
+  r.pad = fdesc ? (u32)((fdesc[j] >> 12) & 0x7ffu)
+        : out   ? (u32)*(u16 const *)(out + 64ul*out_chunk[j] + FD_VERIFY_HIP_TXNM_PAYLOAD_SZ_OFF) : 0u;
   *(tile_res *)(res + TILE_RES_HDR + 24ul*j) = r;
 }
 
@@ -1320,11 +1412,11 @@ submit_verify( fd_verify_hip_tile_t * t, tile_slot & s, hipStream_t st, ulong n,
 
 static void
 submit_results( tile_slot & s, hipStream_t st, ulong n, uchar const * d_in_kind, uchar const * d_out = 0,
-                uint const * d_out_chunk = 0 ) {
+                uint const * d_out_chunk = 0, u64 const * fdesc = 0 ) {
   hipLaunchKernelGGL( k_tile_results, dim3( (unsigned)((n + 255)/256) ), dim3( 256 ), 0, st, n, s.d_tsz, s.d_tcode,
                       s.d_tag, s.frags ? s.d_bid : (u64 const *)0, (u8 const *)d_in_kind, s.d_counter,
                       s.frags ? s.d_flag : (u32 const *)0, s.n_seg, (u8 const *)d_out, (u32 const *)d_out_chunk,
-                      s.d_res );
+                      fdesc, s.d_res );
   TX_CHECK( hipGetLastError() );
   TX_CHECK( hipMemcpyAsync( s.h_res, s.d_res, TILE_RES_HDR + 24ul*n, hipMemcpyDeviceToHost, st ) );
 }
@@ -1394,22 +1486,39 @@ submit_frags_body( fd_verify_hip_tile_t * t, tile_slot & s, hipStream_t st, ulon
     TX_CHECK( hipMemsetAsync( s.d_misc, 0, 4ul*(32ul + (ulong)n_seg*FD_HIP_SEG_STRIDE), st ) );
     s.ing_timed = t->ingest_timing;
     if( s.ing_timed ) TX_CHECK( hipEventRecord( s.ev_ing0, st ) );
+    /* out staging: the batch works on HBM staging frags, then k_out_flush
+       writes the out dcache (pinned host memory) with coalesced stores */
+    bool const stg = t->staging;
+    uchar *        k_out   = stg ? s.d_stage : d_out;
+    uint const *   k_chunk = stg ? s.d_stage_chunk : d_out_chunk;
+    u8 const *     h_out   = stg ? (u8 const *)d_out : (u8 const *)0;
+    u32 const *    h_chunk = stg ? (u32 const *)d_out_chunk : (u32 const *)0;
+    u64 *          fdesc   = stg ? s.d_fdesc : (u64 *)0;
     if( F == 8ul )
       hipLaunchKernelGGL( k_txnm_batch<8>, dim3( (unsigned)nwg ), dim3( 64 ), 0, st, n, d_in,
-                          d_in_chunk, d_in_sz, d_in_kind, d_out, d_out_chunk, (u64)t->seed, s.d_tsz, s.d_tag, s.d_bid,
-                          s.d_first, s.d_cnt, s.d_misc, s.d_rsig, s.d_rpub, s.d_rmoff, s.d_rmsz, n_seg, seg_cap );
+                          d_in_chunk, d_in_sz, d_in_kind, k_out, k_chunk, (u64)t->seed, s.d_tsz, s.d_tag, s.d_bid,
+                          s.d_first, s.d_cnt, s.d_misc, s.d_rsig, s.d_rpub, s.d_rmoff, s.d_rmsz, n_seg, seg_cap,
+                          h_out, h_chunk, fdesc );
     else
       hipLaunchKernelGGL( k_txnm_batch<16>, dim3( (unsigned)nwg ), dim3( 64 ), 0, st, n, d_in,
-                          d_in_chunk, d_in_sz, d_in_kind, d_out, d_out_chunk, (u64)t->seed, s.d_tsz, s.d_tag, s.d_bid,
-                          s.d_first, s.d_cnt, s.d_misc, s.d_rsig, s.d_rpub, s.d_rmoff, s.d_rmsz, n_seg, seg_cap );
+                          d_in_chunk, d_in_sz, d_in_kind, k_out, k_chunk, (u64)t->seed, s.d_tsz, s.d_tag, s.d_bid,
+                          s.d_first, s.d_cnt, s.d_misc, s.d_rsig, s.d_rpub, s.d_rmoff, s.d_rmsz, n_seg, seg_cap,
+                          h_out, h_chunk, fdesc );
     TX_CHECK( hipGetLastError() );
     if( s.ing_timed ) TX_CHECK( hipEventRecord( s.ev_ing1, st ) );
+    if( stg ) {
+      hipLaunchKernelGGL( k_out_flush, dim3( (unsigned)((n + 3ul)/4ul) ), dim3( 256 ), 0, st, n, (u8 const *)k_out,
+                          (u32 const *)k_chunk, (u8 *)d_out, (u32 const *)d_out_chunk, (u64 const *)fdesc );
+      TX_CHECK( hipGetLastError() );
+    }
     fd_hip_segs_t segs = { s.d_misc + 32u, n_seg, seg_cap, s.d_counter };
-    if( fd_ed25519_hip_verify_segs( s.ctx, segs, s.d_rsig, s.d_rpub, d_out, s.d_rmoff, s.d_rmsz, s.d_rcode, st ) ) {
+    if( fd_ed25519_hip_verify_segs( s.ctx, segs, s.d_rsig, s.d_rpub, k_out, s.d_rmoff, s.d_rmsz, s.d_rcode, st ) ) {
       fprintf( stderr, "fd_verify_hip: segmented verify refused (%u x %lu records)\n", n_seg, seg_cap );
       abort();
     }
     fd_ed25519_hip_group_reduce_dev( s.ctx, n, s.d_first, s.d_cnt, s.d_rcode, s.d_tcode, st );
+    submit_results( s, st, n, d_in_kind, k_out, k_chunk, fdesc );
+    return;
   }
   submit_results( s, st, n, d_in_kind, d_out, d_out_chunk );
 }
@@ -1515,7 +1624,10 @@ fd_verify_hip_tile_set_inflight( fd_verify_hip_tile_t * t, ulong k ) {
   TX_CHECK( hipSetDevice( dev ) );
   hipStream_t st = (hipStream_t)fd_ed25519_hip_ctx_stream( t->ctx );
   TX_CHECK( hipStreamSynchronize( st ) );
-  for( ulong j = t->nalloc; j < k; j++ ) { slot_alloc( t->slot[j], t->max_txn ); slot_warm( t->slot[j], t->max_txn, st ); }
+  for( ulong j = t->nalloc; j < k; j++ ) {
+    slot_alloc( t->slot[j], t->max_txn ); slot_warm( t->slot[j], t->max_txn, st );
+    if( t->staging ) slot_stage_alloc( t->slot[j], t->max_txn );
+  }
   if( k > t->nalloc ) t->nalloc = k;
   /* every slot past the first on a context (stream, verify scratch) of its
      own: a batch's GPU time is nearly independent of its size until it
@@ -1651,6 +1763,15 @@ fd_verify_hip_tile_complete_range( fd_verify_hip_tile_t * t, uchar const * skip,
   if( !result ) return -1;
   if( t->completed != t->submitted && !t->slot[t->completed % t->nslot].frags ) return -1;
   return tile_complete( t, NULL, skip, result, NULL, txn_t_sz, payload_sz, tsorig );
+}
+
+extern "C" int
+fd_verify_hip_tile_set_staging( fd_verify_hip_tile_t * t, int on ) {
+  if( t->submitted != t->completed || (on && t->ingest_split) ) return -1;
+  TX_CHECK( hipSetDevice( fd_ed25519_hip_ctx_device( t->ctx ) ) );
+  if( on ) for( ulong j = 0; j < t->nalloc; j++ ) slot_stage_alloc( t->slot[j], t->max_txn );
+  t->staging = !!on;
+  return 0;
 }
 
 extern "C" void fd_verify_hip_tile_set_ingest_timing( fd_verify_hip_tile_t * t, int on ) { t->ingest_timing = !!on; }

@@ -37,6 +37,7 @@ EXPORTS = (
     "fd_verify_hip_tile_new", "fd_verify_hip_tile_join_tcache", "fd_verify_hip_tile_tcache_reset",
     "fd_verify_hip_tile_delete", "fd_verify_hip_tile_set_seed", "fd_verify_hip_tile_submit", "fd_verify_hip_tile_complete",
     "fd_verify_hip_tile_complete_skip", "fd_verify_hip_tile_submit_range", "fd_verify_hip_tile_complete_range",
+    "fd_verify_hip_tile_set_staging",
     "fd_verify_hip_tile_metrics", "fd_verify_hip_tile_metrics2", "fd_verify_hip_tile_last_timing", "fd_verify_hip_tile_submit_frags",
     "fd_verify_hip_before_frag", "fd_verify_hip_hist_edges", "fd_verify_hip_tile_hist_init",
     "fd_verify_hip_tile_hist", "fd_verify_hip_tile_poll", "fd_verify_hip_tile_inflight",
@@ -117,6 +118,8 @@ def lib():
         L.fd_verify_hip_tile_submit_range.restype = c.c_int
         L.fd_verify_hip_tile_submit_range.argtypes = [vp, c.POINTER(Range), vp, vp, vp]
         L.fd_verify_hip_tile_complete_range.restype = c.c_int
+        L.fd_verify_hip_tile_set_staging.restype = c.c_int
+        L.fd_verify_hip_tile_set_staging.argtypes = [vp, c.c_int]
         L.fd_verify_hip_tile_complete_range.argtypes = [vp, vp, vp, vp, vp, vp]
         L.fd_verify_hip_before_frag.restype = c.c_int
         L.fd_verify_hip_before_frag.argtypes = [c.c_uint, u64, u64, u64, u64]
@@ -327,6 +330,12 @@ class VerifyTile:
         """Batches kept on the GPU at once (1..4; 2 for a new tile)."""
         if self._lib.fd_verify_hip_tile_set_inflight(self.tile, int(k)):
             raise ValueError("set_inflight: k out of range or batches outstanding")
+
+    def set_staging(self, on=True):
+        """Out staging (fd_verify_hip_tile_set_staging): batches work on HBM staging frags and
+        write the out dcache at the end, only the bytes the reference writes."""
+        if self._lib.fd_verify_hip_tile_set_staging(self.tile, int(bool(on))):
+            raise ValueError("set_staging: batches outstanding or the split ingest")
 
     def set_ingest_timing(self, on=True):
         """HIP events around each batch's ingest kernel (k_txnm_batch)."""

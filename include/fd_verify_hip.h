@@ -308,6 +308,20 @@ fd_verify_hip_tile_inflight( fd_verify_hip_tile_t const * tile );
 int
 fd_verify_hip_tile_set_inflight( fd_verify_hip_tile_t * tile, ulong k );
 
+/* Out staging, for an out dcache in pinned host memory (the tile's
+   verify_dedup link).  With it on, a frag batch's kernels work on staging
+   frags in HBM -- during_frag's copy, the fd_txn_t, the messages the verify
+   hashes -- and one kernel then writes the out dcache with coalesced
+   stores, exactly the bytes the reference writes there (the copy,
+   txn_t_sz and the fd_txn_t; for a gossip vote its header fields and
+   payload); every other out byte keeps its value.  Without it the kernels
+   read and write the out dcache in place: over PCIe that is a small write
+   per fd_txn_t field and a small read per message piece.  Allocates
+   max_txn x 2176 B of HBM per slot (call from privileged_init).  -1 with
+   batches outstanding, or to turn it on under FD_VERIFY_HIP_INGEST=split. */
+int
+fd_verify_hip_tile_set_staging( fd_verify_hip_tile_t * tile, int on );
+
 int
 fd_verify_hip_tile_complete( fd_verify_hip_tile_t * tile,
                              ulong const *          bundle_id,   /* host, n entries or NULL */

@@ -14,7 +14,9 @@ restated here from src/disco/verify/fd_verify_tile.c:64-161:
                 reference build by tests/test_ref_fixture.py).
 and checks per-frag results, tags, metrics and the out dcache's bytes, and
 that the split three-kernel form (FD_VERIFY_HIP_INGEST=split) and both group
-sizes (FD_VERIFY_HIP_FB=8/16) write the same out dcache byte for byte."""
+sizes (FD_VERIFY_HIP_FB=8/16) write the same out dcache byte for byte, as
+does out staging (fd_verify_hip_tile_set_staging: the batch on HBM staging
+frags, then only the bytes the reference writes copied to the out dcache)."""
 import os
 
 import numpy as np
@@ -88,13 +90,16 @@ def emulate(region_in, in_chunk, in_sz, kinds, out_init, out_chunk, in_place=Fal
     return out, payloads, np.array(bids, np.uint64), spans
 
 
-def run_tile(region_in, in_chunk, in_sz, kinds, out_init, out_chunk, seed, depth, in_place=False, env=None):
+def run_tile(region_in, in_chunk, in_sz, kinds, out_init, out_chunk, seed, depth, in_place=False, env=None,
+             staging=False):
     import torch
     old = {k: os.environ.get(k) for k in (env or {})}
     os.environ.update(env or {})
     try:
         n = in_chunk.size
         tile = V.VerifyTile(None, max_txn=max(n, 1), hashmap_seed=seed, tcache_depth=depth, chunk_sigs=1 << 16)
+        if staging:
+            tile.set_staging(True)
         d_out = _dev(out_init)
         d_in = d_out if in_place else _dev(region_in)
         tile.submit_frags(n, d_in, _dev(in_chunk, np.int32), _dev(in_sz, np.int16), _dev(kinds), d_out,
@@ -210,10 +215,13 @@ def test_ragged_batches(stream, n):
     check(*r, exp_out, payloads, bids, spans, 5, 64, out_init)
 
 
-def test_lying_headers_and_short_frags(stream):
+@pytest.mark.parametrize("staging", [False, True])
+def test_lying_headers_and_short_frags(stream, staging):
     """Headers whose payload_sz is below or above the frag's bytes (the parse
     then reads stale out-dcache bytes, as after_frag does), frags shorter
-    than their 80-B header, and a header-only frag."""
+    than their 80-B header, and a header-only frag; in place and with out
+    staging (whose verify then hashes those stale bytes from the staging
+    frag)."""
     rng = np.random.default_rng(3)
     pays = _payloads(stream)[:400]
     n = len(pays)
@@ -239,7 +247,7 @@ def test_lying_headers_and_short_frags(stream):
     exp_out, payloads, bids, spans = emulate(region, in_chunk, in_sz, kinds, out_init, out_chunk)
     # the stale-byte cases are exercised: some frags parse bytes the copy never wrote
     assert sum(1 for j in range(n) if payloads[j].size + 80 > int(in_sz[j])) >= 100
-    r = run_tile(region, in_chunk, in_sz, kinds, out_init, out_chunk, 9, 256)
+    r = run_tile(region, in_chunk, in_sz, kinds, out_init, out_chunk, 9, 256, staging=staging)
     check(*r, exp_out, payloads, bids, spans, 9, 256, out_init)
     assert (r[0] == V.FRAG_PUBLISH).sum() > 50 and (r[0] == V.FRAG_PARSE_FAIL).sum() > 50
 
@@ -389,3 +397,75 @@ def test_groups_over_the_lds_budget(stream):
     check(*r, exp_out, payloads, bids, spans, 31, 512, out_init)
     s = run_tile(region, in_chunk, in_sz, kinds, out_init, out_chunk, 31, 512, env={"FD_VERIFY_HIP_INGEST": "split"})
     assert np.array_equal(r[4], s[4])
+
+
+def test_out_staging_writes_the_same_bytes(stream):
+    """Out staging against the in-place form on every frag shape the other
+    tests use -- gossip votes, bundles, host-copied frags, headers whose
+    payload_sz runs past the frag, frags shorter than their header, groups
+    over the LDS budget -- in one batch: results, tags, metrics and the out
+    dcache are equal byte for byte (the flush writes exactly the reference's
+    bytes; a staging frag's payload past the copy comes from the out dcache's
+    own bytes), and both equal the restated reference.  One exception, never
+    published: a failed parse leaves the fields it wrote before failing in
+    the in-place out dcache (as fd_txn_parse.c:133-180 does in the
+    reference's), and staging does not flush a failed parse's fd_txn_t."""
+    rng = np.random.default_rng(14)
+    pays = _payloads(stream)[:3000]
+    big = [p for p in pays if p.size >= 700][:64]
+    pays = pays[:1500] + big + pays[1500:2900]
+    n = len(pays)
+    bid = np.zeros(n, np.uint64)
+    for start in rng.choice(n - 8, 40, replace=False):
+        bid[start:start + int(rng.integers(1, 6))] = int(rng.integers(1, 2**40))
+    gossip = (bid == 0) & (rng.random(n) < 0.1)
+    hdr_psz = [min(1232, p.size + int(rng.integers(1, 100))) if j % 11 == 0 and not gossip[j] else None
+               for j, p in enumerate(pays)]
+    frag_sz = [int(rng.integers(1, 80)) if j % 97 == 5 and not gossip[j] else None for j in range(n)]
+    region, in_chunk, in_sz, kinds = frag_region(pays, bid, gossip, rng, hdr_psz, frag_sz)
+    out_chunk = (rng.permutation(n) * PARSED_CHUNKS).astype(np.uint32)
+    out_init = stale_out(rng, PARSED_CHUNKS * (n + 1), out_chunk)
+    exp_out, payloads, bids, spans = emulate(region, in_chunk, in_sz, kinds, out_init, out_chunk)
+    host = (rng.random(n) < 0.3) & (kinds != V.IN_GOSSIP)
+    pre = out_init.copy()
+    for j in np.nonzero(host)[0]:
+        a, o, z = 64 * int(in_chunk[j]), 64 * int(out_chunk[j]), int(in_sz[j])
+        pre[o:o + z] = region[a:a + z]
+    k2 = kinds.copy()
+    k2[host] |= V.IN_HOSTCOPY
+    ic2 = in_chunk.copy()
+    ic2[host] = 0xFFFFFFF0
+    a = run_tile(region, ic2, in_sz, k2, pre, out_chunk, 93, 4096)
+    b = run_tile(region, ic2, in_sz, k2, pre, out_chunk, 93, 4096, staging=True)
+    for x, y in zip(a[:3], b[:3]):
+        assert np.array_equal(x, y)
+    assert a[3] == b[3]
+    keep = np.ones(a[4].size, bool)
+    for j in np.nonzero(a[2] == 0)[0]:                  # a failed parse's partial fd_txn_t
+        t = 64 * int(out_chunk[j]) + (80 + payloads[j].size + 1) // 2 * 2
+        keep[t:t + 852] = False
+    assert np.array_equal(a[4][keep], b[4][keep])
+    assert (~keep).sum() > 0 and keep.sum() > 0.9 * keep.size
+    check(*b, exp_out, payloads, bids, spans, 93, 4096, pre)
+    assert a[3]["parse_fail_cnt"] > 0 and a[3]["gossiped_votes_cnt"] == int(gossip.sum())
+
+
+def test_out_staging_refused_under_split(stream):
+    tile = V.VerifyTile(None, max_txn=16, hashmap_seed=1, tcache_depth=64, chunk_sigs=1 << 16)
+    tile.set_staging(True)
+    tile.set_staging(False)
+    tile.close()
+    tile.verifier.close()
+    old = os.environ.get("FD_VERIFY_HIP_INGEST")
+    os.environ["FD_VERIFY_HIP_INGEST"] = "split"
+    try:
+        tile = V.VerifyTile(None, max_txn=16, hashmap_seed=1, tcache_depth=64, chunk_sigs=1 << 16)
+        with pytest.raises(ValueError):
+            tile.set_staging(True)
+        tile.close()
+        tile.verifier.close()
+    finally:
+        if old is None:
+            os.environ.pop("FD_VERIFY_HIP_INGEST", None)
+        else:
+            os.environ["FD_VERIFY_HIP_INGEST"] = old

@@ -78,7 +78,8 @@ def make_stream(n, path, seed=0x5eed0004, depth=4194302):
     return s
 
 
-def run_one(exe, stream, tiles, in_depth, timeout, logdir, walk=False, range_mode=False, prelay=False):
+def run_one(exe, stream, tiles, in_depth, timeout, logdir, walk=False, range_mode=False, prelay=False,
+            rocprof=None):
     """One producer and `tiles` tile processes; every process's stderr goes to
     a file in logdir; liveness is checked every second (a tile that dies ends
     the run at once), with a progress line on stderr.  range_mode: the tiles
@@ -101,7 +102,11 @@ def run_one(exe, stream, tiles, in_depth, timeout, logdir, walk=False, range_mod
         for t in range(tiles):
             terr.append(open(os.path.join(logdir, f"tile{t}.err"), "w"))
             env = dict(os.environ, TILE_RUN_WALK="1") if walk else renv
-            procs.append(subprocess.Popen([exe, "tile", shm, str(t)], stdout=subprocess.DEVNULL, stderr=terr[-1], env=env))
+            cmd = [exe, "tile", shm, str(t)]
+            if rocprof:                       # each tile under its own kernel trace (the program itself after --)
+                cmd = ["rocprofv3", "--kernel-trace", "--stats", "--output-format", "csv", "-d", rocprof,
+                       "-o", f"tile{t}", "--"] + cmd
+            procs.append(subprocess.Popen(cmd, stdout=subprocess.DEVNULL, stderr=terr[-1], env=env))
         last = 0.0
         while prod.poll() is None:
             dead = [(t, p.returncode) for t, p in enumerate(procs) if p.poll() is not None and p.returncode]
@@ -147,6 +152,8 @@ def main():
                     help="the producer lays the whole stream into a dcache that holds it before the clock starts "
                          "(tile_run.c TILE_RUN_PRELAY; link depth = the frag count): the stage's rate, not one "
                          "producer core's copy")
+    ap.add_argument("--rocprof", default=None,
+                    help="run every tile under rocprofv3 --kernel-trace --stats into this directory")
     ap.add_argument("--walk", action="store_true",
                     help="also time walk mode per tile count: tiles filter every frag (tile_run.c), the link-walk bound")
     ap.add_argument("--timeout", type=float, default=150)
@@ -184,7 +191,8 @@ def main():
                 for r in range(args.repeat):
                     res = run_one(exe, stream, tiles, depth, args.timeout,
                                   os.path.join(args.logdir, f"{cfg}_t{tiles}_{r}"), range_mode=is_range(cfg),
-                                  prelay=args.prelay)
+                                  prelay=args.prelay,
+                                  rocprof=os.path.join(args.rocprof, f"{cfg}_t{tiles}_{r}") if args.rocprof else None)
                     res["config"] = cfg
                     res["prelay"] = args.prelay
                     print(json.dumps(res), flush=True)
