@@ -553,14 +553,20 @@ def main():
 
 def run_tile_leg(args):
     """The north star's operating point: the reference's verify tile with
-    integration/fd_verify_tile_hip.patch (defaults: GPU-side during_frag,
-    8192-frag batches, 3 in flight) in the reference's stem_run1 loop, one
-    tile process fed by a producer process over a quic_verify link
-    (integration/tile_run.c, tools/tile_bench.py), over --tile-frags frags of
-    the C4 stream; then the same link walked by a tile that filters every
-    frag (the fan-out's bound).  Binaries are built from the reference
-    sources in the build container (integration/_build); without them the
-    leg reports why and the line goes on."""
+    integration/fd_verify_tile_hip.patch in the reference's stem_run1 loop,
+    fed by a producer process over a quic_verify link (integration/
+    tile_run.c, tools/tile_bench.py), over --tile-frags frags of the C4
+    stream.  value: range mode (the link unpolled, as
+    integration/fd_verify_topo_hip.patch makes it; the tile hands the GPU
+    published seq ranges), the better of one and two tile processes.  Beside
+    it, one tile with every link polled by the stem -- the GPU-side
+    during_frag (polled_value) and the reference's host copy
+    (host_copy_value) -- and the link walked by a tile that filters every
+    frag.  The producer lays the stream into a dcache that holds all of it
+    before the clock starts (prelay): one producer core copying frags runs at
+    ~15-20 M frags/s and would be the bound.  Binaries are built from the
+    reference sources in the build container (integration/_build); without
+    them the leg reports why and the line goes on."""
     sys.path.insert(0, os.path.join(REPO, "tools"))
     try:
         import tempfile
@@ -572,26 +578,33 @@ def run_tile_leg(args):
             stream = os.path.join(td, "stream.bin")
             s = TB.make_stream(args.tile_frags, stream)
             logdir = os.path.join(td, "logs")
-            r = TB.run_one(exe, stream, 1, 131072, 120, os.path.join(logdir, "tile"))
-            w = TB.run_one(exe, stream, 1, 131072, 120, os.path.join(logdir, "walk"), walk=True)
+            depth = 1 << (s.n - 1).bit_length()
+            rng = [TB.run_one(exe, stream, t, depth, 120, os.path.join(logdir, f"range{t}"), range_mode=True,
+                              prelay=True) for t in (1, 2)]
+            r = max((x for x in rng if not x.get("overrun")), key=lambda x: x["verifies_per_s"], default=rng[0])
+            p = TB.run_one(exe, stream, 1, depth, 120, os.path.join(logdir, "polled"), prelay=True)
+            w = TB.run_one(exe, stream, 1, depth, 120, os.path.join(logdir, "walk"), walk=True, prelay=True)
             hexe = os.path.join(TB.BUILD, "tile_run_hostcopy")      # the reference's own during_frag copy
-            h = TB.run_one(hexe, stream, 1, 131072, 120, os.path.join(logdir, "host")) if os.path.exists(hexe) else None
+            h = TB.run_one(hexe, stream, 1, depth, 120, os.path.join(logdir, "host"), prelay=True) \
+                if os.path.exists(hexe) else None
         ok = not r.get("overrun")
         return {"value": r["verifies_per_s"] if ok else None, "unit": "verifies/s",
                 "frags_per_s": r["frags_per_s"], "frags": r["frags"], "sigs": r["sigs"],
                 "published": r["published"], "overrun": r.get("overrun"), "seconds": r["seconds"],
                 "gpu_ms_per_batch": r["gpu_ms_per_batch"], "host_ms_per_batch": r["host_ms_per_batch"],
-                "regime": r["regime"], "walk_bound_frags_per_s": round(s.n / w["seconds"], 1),
-                "walk_bound_verifies_per_s": round(s.n_records / w["seconds"], 1),
+                "regime": r["regime"], "by_tiles": {str(x["tile_cnt"]): x["verifies_per_s"] for x in rng},
+                "polled_value": p["verifies_per_s"] if not p.get("overrun") else None,
                 "host_copy_value": h["verifies_per_s"] if h and not h.get("overrun") else None,
-                "host_copy_frags_per_s": h["frags_per_s"] if h else None,
-                "config": {"tiles": 1, "batch_max": r["batch_max"], "inflight": r["inflight"],
-                           "gpu_copy": r.get("gpu_copy"), "in_depth": r["in_depth"],
+                "walk_frags_per_s": round(s.n / w["seconds"], 1),
+                "config": {"tiles": r["tile_cnt"], "range_batch_max": r.get("range_batch_max"),
+                           "batch_max": r["batch_max"], "inflight": r["inflight"], "in_depth": r["in_depth"],
+                           "prelay": True,
                            "workload": f"config 4 stream, {s.n} frags ({s.n_records} signatures), GPU-signed"},
                 "what": "integration/fd_verify_tile_hip.patch'd fd_verify_tile.c in stem_run1 (tile_run.c), "
-                        "producer process -> 1 tile process; value = signatures / (last publish - first frag); "
-                        "host_copy_value: the same with the reference's during_frag copy on the host "
-                        "(FD_VERIFY_HIP_GPU_COPY 0); walk_bound: a tile that filters every frag"}
+                        "producer process -> tile processes; value = signatures / (last publish - first frag), "
+                        "range mode (quic_verify unpolled, fd_verify_topo_hip.patch); polled_value: the stem "
+                        "polls the link (GPU-side during_frag); host_copy_value: the reference's during_frag "
+                        "copy (FD_VERIFY_HIP_GPU_COPY 0); walk: a tile that filters every frag"}
     except Exception as e:                   # the tile leg never fails the bench line
         return {"value": None, "error": f"{type(e).__name__}: {e}"}
 

@@ -327,7 +327,7 @@ class VerifyTile:
         return {"gpu_ms": float(out[0]), "host_ms": float(out[1]), "sigs": int(out[2])}
 
     def set_inflight(self, k):
-        """Batches kept on the GPU at once (1..4; 2 for a new tile)."""
+        """Batches kept on the GPU at once (1..8; 2 for a new tile)."""
         if self._lib.fd_verify_hip_tile_set_inflight(self.tile, int(k)):
             raise ValueError("set_inflight: k out of range or batches outstanding")
 

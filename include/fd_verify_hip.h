@@ -304,7 +304,7 @@ fd_verify_hip_tile_inflight( fd_verify_hip_tile_t const * tile );
    Allocates and warms the slots (call from privileged_init: device memory
    for 12 records per frag of max_txn in each).  -1 if k is out of range or
    batches are outstanding.  Results still complete in submission order. */
-#define FD_VERIFY_HIP_INFLIGHT_MAX 4
+#define FD_VERIFY_HIP_INFLIGHT_MAX 8
 int
 fd_verify_hip_tile_set_inflight( fd_verify_hip_tile_t * tile, ulong k );
 

@@ -284,11 +284,12 @@ produce( char const * path, char const * stream, ulong tile_cnt, ulong in_depth 
           "\"verifies_per_s\": %.1f, \"frags_per_s\": %.1f, \"batches\": %lu, \"gpu_ms_per_batch\": %.4f, "
           "\"host_ms_per_batch\": %.4f, \"batch_max\": %lu, \"batch_cap\": %lu, \"inflight\": %lu, "
           "\"flush_ns\": %ld, \"in_depth\": %lu, \"tile_cnt\": %lu, \"overrun\": %lu, \"gpu_copy\": %d, "
-          "\"range\": %d}\n",
+          "\"range\": %d, \"range_batch_max\": %lu}\n",
           frags, sigs, pub, parse, verify, dedup, bundle, s, (double)( t_pub - t0 )*1e-9, (double)sigs/s,
           (double)frags/s, batches, batches ? gpu_ms/(double)batches : 0.0, batches ? host_ms/(double)batches : 0.0,
           FD_VERIFY_HIP_BATCH_MAX, FD_VERIFY_HIP_BATCH_CAP, FD_VERIFY_HIP_INFLIGHT, (long)FD_VERIFY_HIP_FLUSH_NS,
-          in_depth, tile_cnt, overrun, (int)FD_VERIFY_HIP_GPU_COPY, !!getenv( "TILE_RUN_RANGE" ) );
+          in_depth, tile_cnt, overrun, (int)FD_VERIFY_HIP_GPU_COPY, !!getenv( "TILE_RUN_RANGE" ),
+          FD_VERIFY_HIP_RANGE_BATCH_MAX );
   fflush( stdout );
   munmap( base, map_sz );
   unlink( path );

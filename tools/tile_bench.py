@@ -38,7 +38,9 @@ BUILD = os.path.join(REPO, "integration", "_build")
 # (batch_max, inflight, gpu_copy): the patch's FD_VERIFY_HIP_* settings; gpu_copy 0 is the host
 # during_frag copy ("h" suffix)
 SWEEP = [(b, i, g) for b in (1024, 2048, 4096, 8192) for i in (2, 3, 4) for g in (1, 0)] + \
-        [(b, i, 1) for b in (16384, 32768) for i in (3, 4)]     # range mode: few host cycles per frag
+        [(b, i, 1) for b in (16384, 32768, 65536) for i in (2, 3, 4)] + \
+        [(b, i, 1) for b in (16384, 32768) for i in (6, 8)] + \
+        [(131072, i, 1) for i in (2, 3)]                                # range mode: few host cycles per frag
 
 
 def binary(b, i, g=1):
@@ -62,6 +64,7 @@ def build():
         v = os.path.basename(binary(b, i, g))[len("tile_run"):]
         subprocess.check_call(["make", "-s", "-C", os.path.join(REPO, "integration"), f"VARIANT={v}",
                                f"DEFS=-DFD_VERIFY_HIP_BATCH_MAX={b}UL -DFD_VERIFY_HIP_INFLIGHT={i}UL "
+                               f"-DFD_VERIFY_HIP_RANGE_BATCH_MAX={b}UL "
                                f"-DFD_VERIFY_HIP_GPU_COPY={g}", f"_build/tile_run{v}"])
         print(binary(b, i, g))
 
@@ -79,7 +82,7 @@ def make_stream(n, path, seed=0x5eed0004, depth=4194302):
 
 
 def run_one(exe, stream, tiles, in_depth, timeout, logdir, walk=False, range_mode=False, prelay=False,
-            rocprof=None):
+            rocprof=None, hw_queues=None):
     """One producer and `tiles` tile processes; every process's stderr goes to
     a file in logdir; liveness is checked every second (a tile that dies ends
     the run at once), with a progress line on stderr.  range_mode: the tiles
@@ -102,6 +105,8 @@ def run_one(exe, stream, tiles, in_depth, timeout, logdir, walk=False, range_mod
         for t in range(tiles):
             terr.append(open(os.path.join(logdir, f"tile{t}.err"), "w"))
             env = dict(os.environ, TILE_RUN_WALK="1") if walk else renv
+            if hw_queues:                     # HIP hardware queues per tile process (one per in-flight slot)
+                env = dict(env or os.environ, GPU_MAX_HW_QUEUES=str(hw_queues))
             cmd = [exe, "tile", shm, str(t)]
             if rocprof:                       # each tile under its own kernel trace (the program itself after --)
                 cmd = ["rocprofv3", "--kernel-trace", "--stats", "--output-format", "csv", "-d", rocprof,
@@ -152,6 +157,8 @@ def main():
                     help="the producer lays the whole stream into a dcache that holds it before the clock starts "
                          "(tile_run.c TILE_RUN_PRELAY; link depth = the frag count): the stage's rate, not one "
                          "producer core's copy")
+    ap.add_argument("--hw-queues", type=int, default=None,
+                    help="GPU_MAX_HW_QUEUES for the tile processes (default: the environment's; at most 32)")
     ap.add_argument("--rocprof", default=None,
                     help="run every tile under rocprofv3 --kernel-trace --stats into this directory")
     ap.add_argument("--walk", action="store_true",
@@ -191,7 +198,7 @@ def main():
                 for r in range(args.repeat):
                     res = run_one(exe, stream, tiles, depth, args.timeout,
                                   os.path.join(args.logdir, f"{cfg}_t{tiles}_{r}"), range_mode=is_range(cfg),
-                                  prelay=args.prelay,
+                                  prelay=args.prelay, hw_queues=args.hw_queues,
                                   rocprof=os.path.join(args.rocprof, f"{cfg}_t{tiles}_{r}") if args.rocprof else None)
                     res["config"] = cfg
                     res["prelay"] = args.prelay
