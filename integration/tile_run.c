@@ -18,7 +18,7 @@
          copy the quic tile would have made), prints READY, waits for the
          tiles, then publishes the frags' mcache lines in seq order, never
          more than in_depth - 64 (less the frags a GPU-copy tile holds
-         unread, RING x BATCH_CAP) ahead of the slowest tile's fseq (the
+         unread, RING x 2 x BATCH_MAX) ahead of the slowest tile's fseq (the
          reference link is unreliable and would drop frags past its depth; a
          throughput bench must not), and prints one JSON line once every
          tile is done.
@@ -213,14 +213,14 @@ produce( char const * path, char const * stream, ulong tile_cnt, ulong in_depth 
   FD_COMPILER_MFENCE();
   hdr->start = 1UL;
   ulong ctl = fd_frag_meta_ctl( 0UL, 1, 1, 0 );
-  /* a tile with the GPU-side during_frag holds up to RING x BATCH_CAP frags
+  /* a tile with the GPU-side during_frag holds up to RING x 2 x BATCH_MAX frags
      between the stem consuming them (its fseq) and the GPU reading them:
      the producer stays that much (times the tile count: each tile takes
      every T-th seq) further behind, so nothing is overrun */
   ulong const hold = ( FD_VERIFY_HIP_GPU_COPY && !getenv( "TILE_RUN_NO_MARGIN" )    /* the env: overrun tests */
                        && !getenv( "TILE_RUN_RANGE" ) )                           /* range tiles hold none */
-                     ? FD_VERIFY_HIP_RING*FD_VERIFY_HIP_BATCH_CAP*tile_cnt : 0UL;  /* seq % T: a tile's held frags
-                                                                                     span T times as many seqs */
+                     ? FD_VERIFY_HIP_RING*2UL*FD_VERIFY_HIP_BATCH_MAX*tile_cnt : 0UL;  /* seq % T: held frags
+                                                                                          span T x the seqs */
   if( FD_UNLIKELY( in_depth<hold+128UL ) ) FD_LOG_ERR(( "in_depth %lu too small for the GPU copy's %lu held frags", in_depth, hold ));
   ulong lim = getenv( "TILE_RUN_NO_FLOW" ) ? ULONG_MAX : 0UL;  /* the env: the reference's unreliable link, no
                                                                   flow control at all (overrun tests) */
