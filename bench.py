@@ -297,7 +297,7 @@ def main():
                     help="c2 (default config): skip the config-4 sub-object (the verify-tile path, 'c4' in the line)")
     ap.add_argument("--no-tile", action="store_true",
                     help="skip the patched reference verify tile leg (out['tile'], rank 0 at N=1)")
-    ap.add_argument("--tile-frags", type=int, default=1 << 21)
+    ap.add_argument("--tile-frags", type=int, default=1 << 22)
     ap.add_argument("--cpu-threads", type=int, default=16)
     ap.add_argument("--cpu-seconds", type=float, default=8.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -579,13 +579,14 @@ def run_tile_leg(args):
             s = TB.make_stream(args.tile_frags, stream)
             logdir = os.path.join(td, "logs")
             depth = 1 << (s.n - 1).bit_length()
+            hq = 8                                                  # a HIP stream per in-flight batch
             rng = [TB.run_one(exe, stream, t, depth, 120, os.path.join(logdir, f"range{t}"), range_mode=True,
-                              prelay=True) for t in (1, 2)]
+                              prelay=True, hw_queues=hq) for t in (1, 2)]
             r = max((x for x in rng if not x.get("overrun")), key=lambda x: x["verifies_per_s"], default=rng[0])
-            p = TB.run_one(exe, stream, 1, depth, 120, os.path.join(logdir, "polled"), prelay=True)
+            p = TB.run_one(exe, stream, 1, depth, 120, os.path.join(logdir, "polled"), prelay=True, hw_queues=hq)
             w = TB.run_one(exe, stream, 1, depth, 120, os.path.join(logdir, "walk"), walk=True, prelay=True)
             hexe = os.path.join(TB.BUILD, "tile_run_hostcopy")      # the reference's own during_frag copy
-            h = TB.run_one(hexe, stream, 1, depth, 120, os.path.join(logdir, "host"), prelay=True) \
+            h = TB.run_one(hexe, stream, 1, depth, 120, os.path.join(logdir, "host"), prelay=True, hw_queues=hq) \
                 if os.path.exists(hexe) else None
         ok = not r.get("overrun")
         return {"value": r["verifies_per_s"] if ok else None, "unit": "verifies/s",
@@ -596,7 +597,7 @@ def run_tile_leg(args):
                 "polled_value": p["verifies_per_s"] if not p.get("overrun") else None,
                 "host_copy_value": h["verifies_per_s"] if h and not h.get("overrun") else None,
                 "walk_frags_per_s": round(s.n / w["seconds"], 1),
-                "config": {"tiles": r["tile_cnt"], "range_batch_max": r.get("range_batch_max"),
+                "config": {"tiles": r["tile_cnt"], "range_batch_max": r.get("range_batch_max"), "gpu_max_hw_queues": hq,
                            "batch_max": r["batch_max"], "inflight": r["inflight"], "in_depth": r["in_depth"],
                            "prelay": True,
                            "workload": f"config 4 stream, {s.n} frags ({s.n_records} signatures), GPU-signed"},

@@ -50,8 +50,8 @@ def _outcomes(r):
 def test_gpu_copy_equals_host_copy(stream, tmp_path):
     import tile_bench as TB
     path, s = stream
-    g = TB.run_one(os.path.join(TB.BUILD, "tile_run"), path, 1, 131072, 120, str(tmp_path / "gpu"))
-    h = TB.run_one(os.path.join(TB.BUILD, "tile_run_hostcopy"), path, 1, 131072, 120, str(tmp_path / "host"))
+    g = TB.run_one(os.path.join(TB.BUILD, "tile_run"), path, 1, 262144, 120, str(tmp_path / "gpu"))
+    h = TB.run_one(os.path.join(TB.BUILD, "tile_run_hostcopy"), path, 1, 262144, 120, str(tmp_path / "host"))
     assert g["gpu_copy"] == 1 and h["gpu_copy"] == 0
     assert g["overrun"] == 0 and h["overrun"] == 0
     assert _outcomes(g) == _outcomes(h)
