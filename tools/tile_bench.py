@@ -39,7 +39,7 @@ BUILD = os.path.join(REPO, "integration", "_build")
 # during_frag copy ("h" suffix)
 SWEEP = [(b, i, g) for b in (1024, 2048, 4096, 8192) for i in (2, 3, 4) for g in (1, 0)] + \
         [(b, i, 1) for b in (16384, 32768, 65536) for i in (2, 3, 4)] + \
-        [(b, i, 1) for b in (16384, 32768) for i in (6, 8)] + \
+        [(b, i, 1) for b in (16384, 32768, 65536) for i in (6, 8)] + \
         [(131072, i, 1) for i in (2, 3)]                                # range mode: few host cycles per frag
 
 
