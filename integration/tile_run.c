@@ -45,7 +45,12 @@
    is the verify stage's, not one producer core's copy (~15-20 M frags/s of
    C4 frags on the GPU box).
 
-   Walk mode (environment TILE_RUN_WALK=1 on the tiles): each tile's round
+   Links (environment TILE_RUN_LINKS=L on the producer, 1..4): L quic_verify
+   links, as with L quic tiles (topology.c:90,173: every verify tile reads
+   every quic_verify link); frag j of the stream goes to link j % L as that
+   link's seq j / L.  Each tile takes seq % T of every link.
+
+   Walk mode (environment TILE_RUN_WALK=1 on the tiles, one link): each tile's round
    robin count is set past every seq, so before_frag filters every frag and
    the tile only walks the link (mcache poll, before_frag, fseq updates)
    until its in-link fseq reaches the stream's end: the rate at which ONE
@@ -86,6 +91,7 @@ void fd_halt( void ) {}
 
 #define RUN_MAGIC     (0xfd7111e5a11ce5ULL)
 #define RUN_TILE_MAX  (16UL)
+#define RUN_LINK_MAX  (4UL)
 /* verify_dedup mcache: at least twice FD_VERIFY_HIP_STEM_BURST (fd_stem.c:358) */
 #define RUN_OUT_DEPTH (fd_ulong_max( 65536UL, fd_ulong_pow2_up( 2UL*FD_VERIFY_HIP_STEM_BURST ) ))
 
@@ -99,8 +105,9 @@ typedef struct {
 
 typedef struct {
   ulong magic;
-  ulong n, tile_cnt, seed, tcache_depth, in_depth;
-  ulong mcache_off, dcache_off, fseq_off;    /* tile t's fseq at fseq_off + t*fseq_stride */
+  ulong n, tile_cnt, seed, tcache_depth, in_depth, link_cnt;
+  ulong mcache_off[ RUN_LINK_MAX ], dcache_off[ RUN_LINK_MAX ];
+  ulong fseq_off[ RUN_LINK_MAX ];            /* link l, tile t's fseq at fseq_off[l] + t*fseq_stride */
   ulong fseq_stride, dcache_data_sz, map_sz;
   volatile ulong ready, start;
   volatile long  t0;
@@ -156,46 +163,65 @@ produce( char const * path, char const * stream, ulong tile_cnt, ulong in_depth 
      (the producer writes each frag into it just before publishing it, so a
      tile's during_frag copies recently written bytes, as it would behind a
      quic tile) */
+  char const * le = getenv( "TILE_RUN_LINKS" );
+  ulong const L = le ? strtoul( le, NULL, 0 ) : 1UL;
+  if( FD_UNLIKELY( L<1UL || L>RUN_LINK_MAX ) ) FD_LOG_ERR(( "TILE_RUN_LINKS %lu not in [1,%lu]", L, RUN_LINK_MAX ));
   int const prelay = !!getenv( "TILE_RUN_PRELAY" );
-  if( FD_UNLIKELY( prelay && in_depth<n ) ) FD_LOG_ERR(( "prelay: in_depth %lu < %lu frags", in_depth, n ));
+  if( FD_UNLIKELY( prelay && in_depth<(n+L-1UL)/L ) ) FD_LOG_ERR(( "prelay: in_depth %lu < %lu frags", in_depth, n ));
   ulong data_sz = fd_dcache_req_data_sz( FD_TPU_RAW_MTU, in_depth, 1UL, 1 );
   if( prelay ) {                                             /* every frag at its own place: no wrap */
-    data_sz = 2UL*FD_TPU_RAW_MTU + 4096UL;
-    for( ulong j=0UL; j<n; j++ ) data_sz += fd_ulong_align_up( fsz[ j ], 2UL*FD_CHUNK_SZ );
-    data_sz = fd_ulong_align_up( data_sz, 4096UL );
+    ulong most = 0UL;
+    for( ulong l=0UL; l<L; l++ ) {
+      ulong sz_l = 2UL*FD_TPU_RAW_MTU + 4096UL;
+      for( ulong j=l; j<n; j+=L ) sz_l += fd_ulong_align_up( fsz[ j ], 2UL*FD_CHUNK_SZ );
+      most = fd_ulong_max( most, sz_l );
+    }
+    data_sz = fd_ulong_align_up( most, 4096UL );
   }
-  ulong mc_off  = fd_ulong_align_up( sizeof(run_hdr_t), fd_mcache_align() );
-  ulong fs_off  = fd_ulong_align_up( mc_off + fd_mcache_footprint( in_depth, 0UL ), fd_fseq_align() );
   ulong fs_strd = fd_ulong_align_up( fd_fseq_footprint(), 128UL );
-  ulong dc_off  = fd_ulong_align_up( fs_off + tile_cnt*fs_strd, fd_dcache_align() );
-  ulong map_sz  = fd_ulong_align_up( dc_off + fd_dcache_footprint( data_sz, 0UL ), 4096UL );
+  ulong mc_off[ RUN_LINK_MAX ], fs_off[ RUN_LINK_MAX ], dc_off[ RUN_LINK_MAX ];
+  ulong at = sizeof(run_hdr_t);
+  for( ulong l=0UL; l<L; l++ ) {
+    /* page-aligned: a range tile maps each link's mcache and dcache for the GPU */
+    mc_off[ l ] = fd_ulong_align_up( at, 4096UL );
+    fs_off[ l ] = fd_ulong_align_up( mc_off[ l ] + fd_mcache_footprint( in_depth, 0UL ), 4096UL );
+    dc_off[ l ] = fd_ulong_align_up( fs_off[ l ] + tile_cnt*fs_strd, 4096UL );
+    at          = dc_off[ l ] + fd_dcache_footprint( data_sz, 0UL );
+  }
+  ulong map_sz  = fd_ulong_align_up( at, 4096UL );
 
   uchar * base = drv_map( path, map_sz, 1 );
   run_hdr_t * hdr = (run_hdr_t *)base;
   memset( hdr, 0, sizeof(run_hdr_t) );
-  fd_frag_meta_t * mcache = fd_mcache_join( fd_mcache_new( base + mc_off, in_depth, 0UL, 0UL ) );
-  for( ulong t=0UL; t<tile_cnt; t++ ) FD_TEST( fd_fseq_join( fd_fseq_new( base + fs_off + t*fs_strd, 0UL ) ) );
-  uchar * dcache = fd_dcache_join( fd_dcache_new( base + dc_off, data_sz, 0UL ) );
-  FD_TEST( mcache && dcache );
-  ulong chunk0 = fd_dcache_compact_chunk0( base, dcache );
-  ulong wmark  = fd_dcache_compact_wmark ( base, dcache, FD_TPU_RAW_MTU );
+  fd_frag_meta_t * mcache[ RUN_LINK_MAX ];
+  ulong chunk0[ RUN_LINK_MAX ], wmark[ RUN_LINK_MAX ];
+  for( ulong l=0UL; l<L; l++ ) {
+    mcache[ l ] = fd_mcache_join( fd_mcache_new( base + mc_off[ l ], in_depth, 0UL, 0UL ) );
+    for( ulong t=0UL; t<tile_cnt; t++ ) FD_TEST( fd_fseq_join( fd_fseq_new( base + fs_off[ l ] + t*fs_strd, 0UL ) ) );
+    uchar * dcache = fd_dcache_join( fd_dcache_new( base + dc_off[ l ], data_sz, 0UL ) );
+    FD_TEST( mcache[ l ] && dcache );
+    chunk0[ l ] = fd_dcache_compact_chunk0( base, dcache );
+    wmark [ l ] = fd_dcache_compact_wmark ( base, dcache, FD_TPU_RAW_MTU );
+    hdr->mcache_off[ l ] = mc_off[ l ]; hdr->dcache_off[ l ] = dc_off[ l ]; hdr->fseq_off[ l ] = fs_off[ l ];
+  }
   hdr->n = n; hdr->tile_cnt = tile_cnt; hdr->seed = seed; hdr->tcache_depth = depth; hdr->in_depth = in_depth;
-  hdr->mcache_off = mc_off; hdr->dcache_off = dc_off; hdr->fseq_off = fs_off; hdr->fseq_stride = fs_strd;
-  hdr->dcache_data_sz = data_sz; hdr->map_sz = map_sz;
+  hdr->link_cnt = L; hdr->fseq_stride = fs_strd; hdr->dcache_data_sz = data_sz; hdr->map_sz = map_sz;
   ulong * pchunk = NULL;
   if( prelay ) {
     pchunk = malloc( n*sizeof(ulong) ); FD_TEST( pchunk );
-    ulong c = chunk0;
-    for( ulong j=0UL; j<n; j++ ) {
-      fd_txn_m_t * m = (fd_txn_m_t *)fd_chunk_to_laddr( base, c );
-      memset( m, 0, sizeof(fd_txn_m_t) );
-      memcpy( &m->block_engine.bundle_id, in+poff[ j ], 8 );
-      m->payload_sz = (ushort)( fsz[ j ] - sizeof(fd_txn_m_t) );
-      memcpy( fd_txn_m_payload( m ), in+poff[ j ]+10UL, m->payload_sz );
-      pchunk[ j ] = c;
-      ulong nc = fd_dcache_compact_next( c, fsz[ j ], chunk0, wmark );
-      if( FD_UNLIKELY( nc<c && j+1UL<n ) ) FD_LOG_ERR(( "prelay: dcache wrapped at frag %lu", j ));
-      c = nc;
+    for( ulong l=0UL; l<L; l++ ) {
+      ulong c = chunk0[ l ];
+      for( ulong j=l; j<n; j+=L ) {
+        fd_txn_m_t * m = (fd_txn_m_t *)fd_chunk_to_laddr( base, c );
+        memset( m, 0, sizeof(fd_txn_m_t) );
+        memcpy( &m->block_engine.bundle_id, in+poff[ j ], 8 );
+        m->payload_sz = (ushort)( fsz[ j ] - sizeof(fd_txn_m_t) );
+        memcpy( fd_txn_m_payload( m ), in+poff[ j ]+10UL, m->payload_sz );
+        pchunk[ j ] = c;
+        ulong nc = fd_dcache_compact_next( c, fsz[ j ], chunk0[ l ], wmark[ l ] );
+        if( FD_UNLIKELY( nc<c && j+L<n ) ) FD_LOG_ERR(( "prelay: dcache wrapped at frag %lu", j ));
+        c = nc;
+      }
     }
   }
   FD_COMPILER_MFENCE();
@@ -206,8 +232,9 @@ produce( char const * path, char const * stream, ulong tile_cnt, ulong in_depth 
   for( long tw=fd_log_wallclock(); hdr->ready<tile_cnt; FD_SPIN_PAUSE() )
     if( fd_log_wallclock()-tw > 120L*1000000000L ) FD_LOG_ERR(( "tiles not ready after 120 s (%lu of %lu)", hdr->ready, tile_cnt ));
 
-  ulong const * fseq[ RUN_TILE_MAX ];
-  for( ulong t=0UL; t<tile_cnt; t++ ) fseq[ t ] = fd_fseq_join( base + fs_off + t*fs_strd );
+  ulong const * fseq[ RUN_LINK_MAX ][ RUN_TILE_MAX ];
+  for( ulong l=0UL; l<L; l++ )
+    for( ulong t=0UL; t<tile_cnt; t++ ) fseq[ l ][ t ] = fd_fseq_join( base + fs_off[ l ] + t*fs_strd );
   long t0 = fd_log_wallclock();
   hdr->t0 = t0;
   FD_COMPILER_MFENCE();
@@ -222,28 +249,32 @@ produce( char const * path, char const * stream, ulong tile_cnt, ulong in_depth 
                      ? FD_VERIFY_HIP_RING*2UL*FD_VERIFY_HIP_BATCH_MAX*tile_cnt : 0UL;  /* seq % T: held frags
                                                                                           span T x the seqs */
   if( FD_UNLIKELY( in_depth<hold+128UL ) ) FD_LOG_ERR(( "in_depth %lu too small for the GPU copy's %lu held frags", in_depth, hold ));
-  ulong lim = getenv( "TILE_RUN_NO_FLOW" ) ? ULONG_MAX : 0UL;  /* the env: the reference's unreliable link, no
-                                                                  flow control at all (overrun tests) */
-  ulong chunk = chunk0;
-  for( ulong seq=0UL; seq<n; seq++ ) {
-    while( seq>=lim ) {                                        /* flow control against the slowest tile */
+  ulong lim[ RUN_LINK_MAX ], chunk[ RUN_LINK_MAX ];
+  for( ulong l=0UL; l<L; l++ ) {
+    lim  [ l ] = getenv( "TILE_RUN_NO_FLOW" ) ? ULONG_MAX : 0UL;   /* the env: the reference's unreliable link, no
+                                                                     flow control at all (overrun tests) */
+    chunk[ l ] = chunk0[ l ];
+  }
+  for( ulong j=0UL; j<n; j++ ) {
+    ulong l = j % L, seq = j / L;                              /* frag j: link j % L, its seq j / L */
+    while( seq>=lim[ l ] ) {                                   /* flow control against the slowest tile */
       ulong m = ULONG_MAX;
-      for( ulong t=0UL; t<tile_cnt; t++ ) m = fd_ulong_min( m, fd_fseq_query( fseq[ t ] ) );
-      lim = m + in_depth - 64UL - hold;
-      if( seq>=lim ) FD_SPIN_PAUSE();
-      if( fd_log_wallclock()-t0 > 600L*1000000000L ) FD_LOG_ERR(( "tiles stalled at seq %lu", seq ));
+      for( ulong t=0UL; t<tile_cnt; t++ ) m = fd_ulong_min( m, fd_fseq_query( fseq[ l ][ t ] ) );
+      lim[ l ] = m + in_depth - 64UL - hold;
+      if( seq>=lim[ l ] ) FD_SPIN_PAUSE();
+      if( fd_log_wallclock()-t0 > 600L*1000000000L ) FD_LOG_ERR(( "tiles stalled at link %lu seq %lu", l, seq ));
     }
-    if( prelay ) chunk = pchunk[ seq ];
+    if( prelay ) chunk[ l ] = pchunk[ j ];
     else {
-      fd_txn_m_t * m = (fd_txn_m_t *)fd_chunk_to_laddr( base, chunk );
+      fd_txn_m_t * m = (fd_txn_m_t *)fd_chunk_to_laddr( base, chunk[ l ] );
       memset( m, 0, sizeof(fd_txn_m_t) );
-      memcpy( &m->block_engine.bundle_id, in+poff[ seq ], 8 );
-      m->payload_sz = (ushort)( fsz[ seq ] - sizeof(fd_txn_m_t) );
-      memcpy( fd_txn_m_payload( m ), in+poff[ seq ]+10UL, m->payload_sz );
+      memcpy( &m->block_engine.bundle_id, in+poff[ j ], 8 );
+      m->payload_sz = (ushort)( fsz[ j ] - sizeof(fd_txn_m_t) );
+      memcpy( fd_txn_m_payload( m ), in+poff[ j ]+10UL, m->payload_sz );
     }
     ulong ts = (ulong)fd_frag_meta_ts_comp( fd_tickcount() );
-    fd_mcache_publish( mcache, in_depth, seq, 0UL, chunk, fsz[ seq ], ctl, ts, ts );
-    if( !prelay ) chunk = fd_dcache_compact_next( chunk, fsz[ seq ], chunk0, wmark );
+    fd_mcache_publish( mcache[ l ], in_depth, seq, 0UL, chunk[ l ], fsz[ j ], ctl, ts, ts );
+    if( !prelay ) chunk[ l ] = fd_dcache_compact_next( chunk[ l ], fsz[ j ], chunk0[ l ], wmark[ l ] );
   }
   long t_pub = fd_log_wallclock();
   ulong done = 0UL;
@@ -284,12 +315,12 @@ produce( char const * path, char const * stream, ulong tile_cnt, ulong in_depth 
           "\"verifies_per_s\": %.1f, \"frags_per_s\": %.1f, \"batches\": %lu, \"gpu_ms_per_batch\": %.4f, "
           "\"host_ms_per_batch\": %.4f, \"batch_max\": %lu, \"batch_cap\": %lu, \"inflight\": %lu, "
           "\"flush_ns\": %ld, \"in_depth\": %lu, \"tile_cnt\": %lu, \"overrun\": %lu, \"gpu_copy\": %d, "
-          "\"range\": %d, \"range_batch_max\": %lu}\n",
+          "\"range\": %d, \"range_batch_max\": %lu, \"links\": %lu}\n",
           frags, sigs, pub, parse, verify, dedup, bundle, s, (double)( t_pub - t0 )*1e-9, (double)sigs/s,
           (double)frags/s, batches, batches ? gpu_ms/(double)batches : 0.0, batches ? host_ms/(double)batches : 0.0,
           FD_VERIFY_HIP_BATCH_MAX, FD_VERIFY_HIP_BATCH_CAP, FD_VERIFY_HIP_INFLIGHT, (long)FD_VERIFY_HIP_FLUSH_NS,
           in_depth, tile_cnt, overrun, (int)FD_VERIFY_HIP_GPU_COPY, !!getenv( "TILE_RUN_RANGE" ),
-          FD_VERIFY_HIP_RANGE_BATCH_MAX );
+          FD_VERIFY_HIP_RANGE_BATCH_MAX, L );
   fflush( stdout );
   munmap( base, map_sz );
   unlink( path );
@@ -356,24 +387,33 @@ tile( char const * path, ulong t ) {
   void * scratch = drv_malloc( scratch_align(), scratch_footprint( tile ) );
   topo->objs[ tile->tile_obj_id ].offset = (ulong)scratch - (ulong)drv_arena;
 
-  fd_topo_link_t * quic = fd_topob_link( topo, "quic_verify", "quic_verify", in_depth, FD_TPU_REASM_MTU, 1UL );
-  quic->mcache = fd_mcache_join( base + hdr->mcache_off );
-  quic->dcache = fd_dcache_join( base + hdr->dcache_off );
+  ulong const L = hdr->link_cnt;
+  fd_topo_link_t * quic[ RUN_LINK_MAX ];
+  for( ulong l=0UL; l<L; l++ ) {
+    quic[ l ] = fd_topob_link( topo, "quic_verify", "quic_verify", in_depth, FD_TPU_REASM_MTU, 1UL );
+    quic[ l ]->mcache = fd_mcache_join( base + hdr->mcache_off[ l ] );
+    quic[ l ]->dcache = fd_dcache_join( base + hdr->dcache_off[ l ] );
+    FD_TEST( quic[ l ]->mcache && quic[ l ]->dcache );
+    quic[ l ]->mtu = FD_TPU_REASM_MTU;
+  }
   fd_topo_link_t * out = fd_topob_link( topo, "verify_dedup", "verify", RUN_OUT_DEPTH, FD_TPU_PARSED_MTU,
                                         FD_VERIFY_HIP_STEM_BURST );
   out->mcache = fd_mcache_join( fd_mcache_new( drv_malloc( fd_mcache_align(), fd_mcache_footprint( RUN_OUT_DEPTH, 0UL ) ),
                                                RUN_OUT_DEPTH, 0UL, 0UL ) );
   out->dcache = fd_dcache_join( fd_dcache_new( drv_malloc( fd_dcache_align(), fd_dcache_footprint( out_data, 0UL ) ),
                                                out_data, 0UL ) );
-  FD_TEST( quic->mcache && quic->dcache && out->mcache && out->dcache );
+  FD_TEST( out->mcache && out->dcache );
   drv_range = !!getenv( "TILE_RUN_RANGE" );
-  fd_topob_tile_in ( topo, "verify", 0UL, "verify", "quic_verify", 0UL, FD_TOPOB_UNRELIABLE,
-                     drv_range ? FD_TOPOB_UNPOLLED : FD_TOPOB_POLLED );
+  ulong * in_fseq[ RUN_LINK_MAX ];
+  for( ulong l=0UL; l<L; l++ ) {
+    fd_topob_tile_in( topo, "verify", 0UL, "verify", "quic_verify", l, FD_TOPOB_UNRELIABLE,
+                      drv_range ? FD_TOPOB_UNPOLLED : FD_TOPOB_POLLED );
+    in_fseq[ l ] = fd_fseq_join( base + hdr->fseq_off[ l ] + t*hdr->fseq_stride );
+    tile->in_link_fseq[ l ] = in_fseq[ l ];                     /* fd_topo_fill_tile's: the range tile moves it */
+  }
   fd_topob_tile_out( topo, "verify", 0UL, "verify_dedup", 0UL );
   tile->kind_id = t;                                            /* GPU t % devices; round robin index */
-  quic->mtu = FD_TPU_REASM_MTU; out->mtu = FD_TPU_PARSED_MTU;
-  ulong * in_fseq = fd_fseq_join( base + hdr->fseq_off + t*hdr->fseq_stride );
-  tile->in_link_fseq[ 0 ] = in_fseq;                            /* fd_topo_fill_tile's: the range tile moves it */
+  out->mtu = FD_TPU_PARSED_MTU;
 
   privileged_init( topo, tile );
   fd_verify_ctx_t * ctx = (fd_verify_ctx_t *)scratch;
@@ -383,23 +423,29 @@ tile( char const * path, ulong t ) {
   drv_walk = !!getenv( "TILE_RUN_WALK" );
   if( drv_walk ) ctx->round_robin_cnt = ULONG_MAX;              /* seq % cnt == seq: only seq t would pass, t < tile_cnt */
   drv_ctx   = ctx;
-  drv_share = hdr->n/hdr->tile_cnt + (t<hdr->n%hdr->tile_cnt ? 1UL : 0UL);
+  drv_share = 0UL;                                              /* seq % T of every link */
+  for( ulong l=0UL; l<L; l++ ) {
+    ulong nl = ( hdr->n + L - 1UL - l )/L;                      /* frags on link l */
+    drv_share += nl/hdr->tile_cnt + ( t<nl%hdr->tile_cnt ? 1UL : 0UL );
+  }
 
   /* the stem's run loop state (fd_stem.c:207-394): metrics, scratch, the
      in link's fseq in the shared segment (the producer's flow control), a
      consumer of the out link that returns every credit (STEM_SHUTDOWN_SEQ) */
-  ulong * metrics = aligned_alloc( FD_METRICS_ALIGN, fd_ulong_align_up( FD_METRICS_FOOTPRINT( 1UL, 1UL ), FD_METRICS_ALIGN ) );
-  fd_metrics_register( fd_metrics_new( metrics, 1UL, 1UL ) );
+  ulong * metrics = aligned_alloc( FD_METRICS_ALIGN, fd_ulong_align_up( FD_METRICS_FOOTPRINT( L, 1UL ), FD_METRICS_ALIGN ) );
+  fd_metrics_register( fd_metrics_new( metrics, L, 1UL ) );
   void * stem_scratch = aligned_alloc( FD_STEM_SCRATCH_ALIGN,
-                                       fd_ulong_align_up( stem_scratch_footprint( 1UL, 1UL, 1UL ), FD_STEM_SCRATCH_ALIGN ) );
-  drv_in_fseq = in_fseq; drv_n = hdr->n;
+                                       fd_ulong_align_up( stem_scratch_footprint( L, 1UL, 1UL ), FD_STEM_SCRATCH_ALIGN ) );
+  if( FD_UNLIKELY( drv_walk && L!=1UL ) ) FD_LOG_ERR(( "walk mode takes one link" ));
+  drv_in_fseq = in_fseq[ 0 ]; drv_n = hdr->n;
   uchar cons_mem[ 256 ] __attribute__((aligned(128)));
   FD_TEST( fd_fseq_footprint()<=sizeof(cons_mem) );
   ulong * cons_fseq = fd_fseq_join( fd_fseq_new( cons_mem, STEM_SHUTDOWN_SEQ ) );
   fd_rng_t rng_mem[ 1 ];
   fd_rng_t * rng = fd_rng_join( fd_rng_new( rng_mem, (uint)(hdr->seed + t), 0UL ) );
-  fd_frag_meta_t const * in_mcache[ 1 ] = { quic->mcache };
-  ulong *                in_fseqs [ 1 ] = { in_fseq };
+  fd_frag_meta_t const * in_mcache[ RUN_LINK_MAX ];
+  ulong *                in_fseqs [ RUN_LINK_MAX ];
+  for( ulong l=0UL; l<L; l++ ) { in_mcache[ l ] = quic[ l ]->mcache; in_fseqs[ l ] = in_fseq[ l ]; }
   fd_frag_meta_t *       out_mcache[ 1 ] = { out->mcache };
   ulong                  cons_out[ 1 ] = { 0UL };
   ulong *                cons_fseqs[ 1 ] = { cons_fseq };
@@ -409,7 +455,7 @@ tile( char const * path, ulong t ) {
   __atomic_fetch_add( &hdr->ready, 1UL, __ATOMIC_SEQ_CST );
   while( !hdr->start ) FD_SPIN_PAUSE();
   drv_deadline = fd_log_wallclock() + 600L*1000000000L;
-  stem_run1( drv_range ? 0UL : 1UL, in_mcache, in_fseqs, 1UL, out_mcache, 1UL, cons_out, cons_fseqs, FD_VERIFY_HIP_STEM_BURST, 0L, rng,
+  stem_run1( drv_range ? 0UL : L, in_mcache, in_fseqs, 1UL, out_mcache, 1UL, cons_out, cons_fseqs, FD_VERIFY_HIP_STEM_BURST, 0L, rng,
              stem_scratch, ctx );
   long t_end = fd_log_wallclock();
 

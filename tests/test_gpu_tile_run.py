@@ -20,6 +20,13 @@ tile leg runs it.
   producer under no flow control at all (TILE_RUN_NO_FLOW: the reference's
   unreliable link) on a shallow link, the tile is lapped, drops the lost
   frags as the stem drops an overrun, and keeps running.
+- Two quic_verify links (as with two quic tiles; every verify tile reads
+  every link): range mode (two range links, round robin) and the stem's
+  polling (the first link GPU-copied, the second host-copied) at one and
+  two tiles.  Arrival order across links differs between the two forms,
+  so the counts compared are those the order cannot change: frags,
+  signatures, parse failures, published, and published + dedup + verify
+  failures.
 The full-byte equality of the patched tile with the reference tile is
 tests/test_gpu_tile_hip.py (mock topology, both copy forms via the kernel
 tests in tests/test_gpu_txn_batch.py)."""
@@ -87,3 +94,18 @@ def test_range_mode_overrun_is_dropped(stream, tmp_path, monkeypatch):
     r = TB.run_one(os.path.join(TB.BUILD, "tile_run"), path, 1, 4096, 120, str(tmp_path / "rovr"), range_mode=True)
     assert r["overrun"] > 0, r
     assert r["frags"] + r["overrun"] == s.n
+
+
+@pytest.mark.parametrize("tiles", [1, 2])
+def test_two_links_range_and_polled(stream, tmp_path, tiles):
+    import tile_bench as TB
+    path, s = stream
+    exe = os.path.join(TB.BUILD, "tile_run")
+    r = TB.run_one(exe, path, tiles, 262144, 120, str(tmp_path / "range"), range_mode=True, links=2)
+    p = TB.run_one(exe, path, tiles, 262144, 120, str(tmp_path / "polled"), links=2)
+    assert r["links"] == 2 and p["links"] == 2 and r["range"] == 1 and p["range"] == 0
+    assert r["overrun"] == 0 and p["overrun"] == 0
+    for k in ("frags", "sigs", "parse_fail", "published"):
+        assert r[k] == p[k], (k, r[k], p[k])
+    assert r["frags"] == s.n
+    assert r["published"] + r["dedup"] + r["verify_fail"] == p["published"] + p["dedup"] + p["verify_fail"]

@@ -82,7 +82,7 @@ def make_stream(n, path, seed=0x5eed0004, depth=4194302):
 
 
 def run_one(exe, stream, tiles, in_depth, timeout, logdir, walk=False, range_mode=False, prelay=False,
-            rocprof=None, hw_queues=None):
+            rocprof=None, hw_queues=None, links=1):
     """One producer and `tiles` tile processes; every process's stderr goes to
     a file in logdir; liveness is checked every second (a tile that dies ends
     the run at once), with a progress line on stderr.  range_mode: the tiles
@@ -94,6 +94,8 @@ def run_one(exe, stream, tiles, in_depth, timeout, logdir, walk=False, range_mod
     perr = open(os.path.join(logdir, "producer.err"), "w")
     renv = dict(os.environ, TILE_RUN_RANGE="1") if range_mode else None
     penv = dict(renv or os.environ, TILE_RUN_PRELAY="1") if prelay else renv
+    if links != 1:                            # quic_verify links, as with that many quic tiles
+        penv = dict(penv or os.environ, TILE_RUN_LINKS=str(links))
     prod = subprocess.Popen([exe, "produce", shm, stream, str(tiles), str(in_depth)], stdout=subprocess.PIPE,
                             stderr=perr, text=True, env=penv)
     procs, terr = [], []
