@@ -101,8 +101,9 @@ def test_two_links_range_and_polled(stream, tmp_path, tiles):
     import tile_bench as TB
     path, s = stream
     exe = os.path.join(TB.BUILD, "tile_run")
-    r = TB.run_one(exe, path, tiles, 262144, 120, str(tmp_path / "range"), range_mode=True, links=2)
-    p = TB.run_one(exe, path, tiles, 262144, 120, str(tmp_path / "polled"), links=2)
+    depth = 262144 * tiles                  # the polled tiles hold (INFLIGHT+1) x 2 x BATCH_MAX frags each
+    r = TB.run_one(exe, path, tiles, depth, 120, str(tmp_path / "range"), range_mode=True, links=2)
+    p = TB.run_one(exe, path, tiles, depth, 120, str(tmp_path / "polled"), links=2)
     assert r["links"] == 2 and p["links"] == 2 and r["range"] == 1 and p["range"] == 0
     assert r["overrun"] == 0 and p["overrun"] == 0
     for k in ("frags", "sigs", "parse_fail", "published"):
