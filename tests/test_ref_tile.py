@@ -110,3 +110,18 @@ def test_tile_run_uses_range_entry_points():
     syms = subprocess.run(["nm", "-u", exe], capture_output=True, text=True).stdout
     for s_ in ("fd_verify_hip_tile_submit_range", "fd_verify_hip_tile_complete_range"):
         assert s_ in syms, s_
+
+
+def test_patched_tile_compiles_warning_free():
+    """integration/Makefile's tile_run_strict.o: the patched fd_verify_tile.c
+    (both patches' tile side, range mode included) and tile_run.c under
+    -Wall -Wextra -Werror (the populate_allowed_* hooks excepted: tile_run
+    drives the callbacks itself)."""
+    obj = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "integration", "_build",
+                       "tile_run_strict.o")
+    if not os.path.exists(obj):
+        pytest.skip("integration/_build missing")
+    syms = subprocess.run(["nm", obj], capture_output=True, text=True).stdout
+    for s_ in ("fd_verify_hip_tile_submit_range", "fd_verify_hip_tile_complete_range",
+               "fd_verify_hip_tile_set_staging", "fd_verify_hip_tile_submit_frags"):
+        assert s_ in syms, s_                  # the range, staging and stem paths are compiled in
