@@ -1766,6 +1766,18 @@ fd_verify_hip_tile_complete_range( fd_verify_hip_tile_t * t, uchar const * skip,
 }
 
 extern "C" int
+fd_verify_hip_tile_set_cu_mask( fd_verify_hip_tile_t * t, uint const * mask, uint words ) {
+  if( t->submitted != t->completed ) return -1;
+  for( ulong j = 0; j < t->nalloc; j++ ) {
+    fd_ed25519_hip_ctx_t * c = t->slot[j].ctx;
+    bool seen = false;                                       /* slots sharing the tile's context: once */
+    for( ulong k = 0; k < j; k++ ) seen |= t->slot[k].ctx == c;
+    if( !seen && fd_ed25519_hip_ctx_set_cu_mask( c, mask, words ) ) return -1;
+  }
+  return 0;
+}
+
+extern "C" int
 fd_verify_hip_tile_set_staging( fd_verify_hip_tile_t * t, int on ) {
   if( t->submitted != t->completed || (on && t->ingest_split) ) return -1;
   TX_CHECK( hipSetDevice( fd_ed25519_hip_ctx_device( t->ctx ) ) );

@@ -37,7 +37,7 @@ EXPORTS = (
     "fd_verify_hip_tile_new", "fd_verify_hip_tile_join_tcache", "fd_verify_hip_tile_tcache_reset",
     "fd_verify_hip_tile_delete", "fd_verify_hip_tile_set_seed", "fd_verify_hip_tile_submit", "fd_verify_hip_tile_complete",
     "fd_verify_hip_tile_complete_skip", "fd_verify_hip_tile_submit_range", "fd_verify_hip_tile_complete_range",
-    "fd_verify_hip_tile_set_staging",
+    "fd_verify_hip_tile_set_staging", "fd_verify_hip_tile_set_cu_mask",
     "fd_verify_hip_tile_metrics", "fd_verify_hip_tile_metrics2", "fd_verify_hip_tile_last_timing", "fd_verify_hip_tile_submit_frags",
     "fd_verify_hip_before_frag", "fd_verify_hip_hist_edges", "fd_verify_hip_tile_hist_init",
     "fd_verify_hip_tile_hist", "fd_verify_hip_tile_poll", "fd_verify_hip_tile_inflight",
@@ -120,6 +120,8 @@ def lib():
         L.fd_verify_hip_tile_complete_range.restype = c.c_int
         L.fd_verify_hip_tile_set_staging.restype = c.c_int
         L.fd_verify_hip_tile_set_staging.argtypes = [vp, c.c_int]
+        L.fd_verify_hip_tile_set_cu_mask.restype = c.c_int
+        L.fd_verify_hip_tile_set_cu_mask.argtypes = [vp, vp, c.c_uint]
         L.fd_verify_hip_tile_complete_range.argtypes = [vp, vp, vp, vp, vp, vp]
         L.fd_verify_hip_before_frag.restype = c.c_int
         L.fd_verify_hip_before_frag.argtypes = [c.c_uint, u64, u64, u64, u64]

@@ -322,6 +322,14 @@ fd_verify_hip_tile_set_inflight( fd_verify_hip_tile_t * tile, ulong k );
 int
 fd_verify_hip_tile_set_staging( fd_verify_hip_tile_t * tile, int on );
 
+/* fd_ed25519_hip_ctx_set_cu_mask on every slot context of the tile: its
+   batches run on the CUs the mask names (words = 0: all of them again).
+   For tiles that share a GPU, each on its own CUs.  -1 with batches
+   outstanding or if the runtime refuses the mask.  A masked stream is a
+   blocking stream (fd_ed25519_hip.h). */
+int
+fd_verify_hip_tile_set_cu_mask( fd_verify_hip_tile_t * tile, uint const * mask, uint words );
+
 int
 fd_verify_hip_tile_complete( fd_verify_hip_tile_t * tile,
                              ulong const *          bundle_id,   /* host, n entries or NULL */

@@ -417,6 +417,14 @@ tile( char const * path, ulong t ) {
 
   privileged_init( topo, tile );
   fd_verify_ctx_t * ctx = (fd_verify_ctx_t *)scratch;
+  if( getenv( "TILE_RUN_CU_SPLIT" ) ) {                         /* A/B: tile t on CUs [t, t+1) x cus/T */
+    uint cus = (uint)strtoul( getenv( "TILE_RUN_CU_SPLIT" ), NULL, 0 ), mask[ 16 ] = { 0U };
+    uint lo = (uint)( t*cus/hdr->tile_cnt ), hi = (uint)( (t+1UL)*cus/hdr->tile_cnt );
+    FD_TEST( cus>0U && cus<=512U );
+    for( uint c=lo; c<hi; c++ ) mask[ c>>5 ] |= 1U<<( c&31U );
+    if( FD_UNLIKELY( fd_verify_hip_tile_set_cu_mask( ctx->hip_tile, mask, (cus+31U)/32U ) ) )
+      FD_LOG_ERR(( "fd_verify_hip_tile_set_cu_mask failed" ));
+  }
   ctx->hashmap_seed = hdr->seed + t;                            /* fixed per tile: runs are reproducible */
   unprivileged_init( topo, tile );
   ctx->round_robin_cnt = hdr->tile_cnt; ctx->round_robin_idx = t;
