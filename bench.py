@@ -543,6 +543,10 @@ def main():
                                             "roofline", "ingest_roofline", "pcie_inclusive", "cpu_baseline")}
     if cfg == "c2" and not args.no_tile and rank == 0 and world == 1:
         out["tile"] = run_tile_leg(args)
+        cb = (out.get("c4") or {}).get("cpu_baseline")
+        if cb and cb.get("value"):               # the same C4 workload through the reference's own CPU tile
+            out["tile"]["cpu_baseline"] = dict(cb, note="the c4 leg's: the reference's verify tile on host cores, "
+                                                        "over the same C4 stream shape")
     if rank == 0:
         emit(out)
     if dist:
