@@ -132,7 +132,7 @@ main( int argc, char ** argv ) {
   fd_topo_wksp_t * wksp = fd_topob_wksp( topo, "wksp" );
   fd_topo_tile_t * tile = fd_topob_tile( topo, "verify", "wksp", "wksp", 0UL, 0, 0 );
   tile->verify.tcache_depth = depth;
-  drv_arena_sz = 4096UL + scratch_footprint( tile ) + scratch_align() +
+  drv_arena_sz = 4096UL + scratch_footprint( tile ) + scratch_align() + fd_fseq_footprint() + fd_fseq_align() +
                  drv_link_footprint( link_depth, FD_TPU_RAW_MTU, 1UL ) +
                  drv_link_footprint( link_depth, FD_TPU_PARSED_MTU, DRV_OUT_BURST );
   drv_arena = aligned_alloc( 4096UL, fd_ulong_align_up( drv_arena_sz, 4096UL ) );
@@ -144,9 +144,16 @@ main( int argc, char ** argv ) {
   topo->objs[ tile->tile_obj_id ].offset = (ulong)scratch - (ulong)drv_arena;
   fd_topo_link_t * quic = drv_link( topo, "quic_verify", link_depth, FD_TPU_RAW_MTU, 1UL );
   fd_topo_link_t * out  = drv_link( topo, "verify_dedup", link_depth, FD_TPU_PARSED_MTU, DRV_OUT_BURST );
-  fd_topob_tile_in ( topo, "verify", 0UL, "wksp", "quic_verify", 0UL, 0, 1 );
+  /* TILE_DRV_RANGE (patched tile, FD_HAS_HIP): the quic link unpolled, as
+     integration/fd_verify_topo_hip.patch makes it -- the driver only
+     publishes the frags and the tile reads them by range from after_credit */
+  int const range = !!getenv( "TILE_DRV_RANGE" );
+  fd_topob_tile_in ( topo, "verify", 0UL, "wksp", "quic_verify", 0UL, 0, !range );
   fd_topob_tile_out( topo, "verify", 0UL, "verify_dedup", 0UL );
   quic->mtu = FD_TPU_RAW_MTU; out->mtu = FD_TPU_PARSED_MTU;
+  ulong * in_fseq = fd_fseq_join( fd_fseq_new( drv_malloc( fd_fseq_align(), fd_fseq_footprint() ), 0UL ) );
+  FD_TEST( in_fseq );
+  tile->in_link_fseq[ 0 ] = in_fseq;
 
   privileged_init( topo, tile );
   fd_verify_ctx_t * ctx = (fd_verify_ctx_t *)scratch;
@@ -183,7 +190,9 @@ main( int argc, char ** argv ) {
 #endif
   (void)sandboxed;
 
-  ulong   in_chunk = ctx->in[0].chunk0;
+  ulong const in_chunk0 = fd_dcache_compact_chunk0( drv_arena, quic->dcache );   /* = ctx->in[0] when polled */
+  ulong const in_wmark  = fd_dcache_compact_wmark ( drv_arena, quic->dcache, quic->mtu );
+  ulong   in_chunk = in_chunk0;
   ulong   off = 28UL;
   for( ulong j=0UL; j<n; j++ ) {
 #if FD_HAS_HIP
@@ -192,18 +201,18 @@ main( int argc, char ** argv ) {
     ulong bid; ushort psz;
     memcpy( &bid, in+off, 8 ); memcpy( &psz, in+off+8, 2 ); off += 10UL;
     FD_TEST( off+psz<=in_sz );
-    uchar * frag = fd_chunk_to_laddr( ctx->in[0].mem, in_chunk );
+    uchar * frag = fd_chunk_to_laddr( drv_arena, in_chunk );
     fd_txn_m_t * m = (fd_txn_m_t *)frag;
     memset( m, 0, sizeof(fd_txn_m_t) );
     m->payload_sz = psz; m->block_engine.bundle_id = bid;
     memcpy( fd_txn_m_payload( m ), in+off, psz ); off += psz;
     ulong sz = sizeof(fd_txn_m_t) + psz;
     fd_mcache_publish( quic->mcache, link_depth, j, 0UL, in_chunk, sz, 0UL, j, j );
-    if( !before_frag( ctx, 0UL, j, 0UL ) ) {
+    if( !range && !before_frag( ctx, 0UL, j, 0UL ) ) {
       during_frag( ctx, 0UL, j, 0UL, in_chunk, sz, 0UL );
       after_frag( ctx, 0UL, j, 0UL, sz, j, j, &stem );
     }
-    in_chunk = fd_dcache_compact_next( in_chunk, sz, ctx->in[0].chunk0, ctx->in[0].wmark );
+    in_chunk = fd_dcache_compact_next( in_chunk, sz, in_chunk0, in_wmark );
   }
 #if FD_HAS_HIP
   /* drain: the tile flushes a partial batch after its timeout and
