@@ -217,12 +217,16 @@ main( int argc, char ** argv ) {
 #if FD_HAS_HIP
   /* drain: the tile flushes a partial batch after its timeout and
      publishes completed batches from after_credit */
+  /* range mode: idle is not enough, the tile must also have read the link
+     to its end (it reads ranges only from after_credit) */
+#define DRV_DONE( ctx ) ( FD_VERIFY_HIP_IDLE( ctx ) && ( !range || (ctx)->hip_rlink[ 0 ].seq>=n ) )
   for( long t0 = fd_log_wallclock(); fd_log_wallclock()-t0 < 30L*1000L*1000L*1000L; ) {
     int poll_in = 1, busy = 0;
     after_credit( ctx, &stem, &poll_in, &busy );
-    if( FD_VERIFY_HIP_IDLE( ctx ) ) break;
+    if( DRV_DONE( ctx ) ) break;
   }
-  FD_TEST( FD_VERIFY_HIP_IDLE( ctx ) );
+  FD_TEST( DRV_DONE( ctx ) );
+#undef DRV_DONE
 #endif
 
   ulong pub = out_seq[0];
