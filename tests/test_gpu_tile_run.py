@@ -87,11 +87,13 @@ def test_range_mode_equals_host_copy(stream, tmp_path, tiles):
     assert r["frags"] == s.n
 
 
-def test_range_mode_overrun_is_dropped(stream, tmp_path, monkeypatch):
+@pytest.mark.parametrize("tiles", [1, 2])
+def test_range_mode_overrun_is_dropped(stream, tmp_path, monkeypatch, tiles):
     import tile_bench as TB
     path, s = stream
     monkeypatch.setenv("TILE_RUN_NO_FLOW", "1")
-    r = TB.run_one(os.path.join(TB.BUILD, "tile_run"), path, 1, 4096, 120, str(tmp_path / "rovr"), range_mode=True)
+    r = TB.run_one(os.path.join(TB.BUILD, "tile_run"), path, tiles, 4096, 120, str(tmp_path / "rovr"),
+                   range_mode=True)
     assert r["overrun"] > 0, r
     assert r["frags"] + r["overrun"] == s.n
 
