@@ -1262,6 +1262,9 @@ fd_ed25519_hip_ctx_new( int device, ulong chunk_sigs ) {
     FD_CHECK( hipDeviceGetAttribute( &ncu_, hipDeviceAttributeMultiprocessorCount, device ) );
     ctx->lat_copies = LAT_COPIES_MAX;
     { char const * lc = getenv( "FD_ED25519_HIP_LAT_COPIES" ); if( lc && atoi( lc ) > 0 ) ctx->lat_copies = (u32)atoi( lc ); }
+    /* A/B: every context's DSM grid 1/share of the resident slots (contexts sharing the GPU;
+       fd_ed25519_hip_set_dsm_share sets it per context) */
+    { char const * ds = getenv( "FD_ED25519_HIP_DSM_SHARE" ); if( ds && atoi( ds ) > 0 ) ctx->dsm_share = (ulong)atoi( ds ); }
     ctx->ncu = (ulong)(ncu_ > 0 ? ncu_ : 1);
     FD_CHECK( hipMalloc( (void **)&ctx->d_lat_done, LAT_MAX_N * sizeof(ulong) ) );
     FD_CHECK( hipMemsetAsync( ctx->d_lat_done, 0, LAT_MAX_N * sizeof(ulong), ctx->stream ) );
