@@ -1116,6 +1116,9 @@ struct tile_slot {
   int           ing_timed;
   int           frags;
   hipEvent_t    ev_start, ev_done;
+  /* out staging: k_out_flush runs on a stream of its own beside the verify
+     (it needs only k_txnm_batch's staging frags), joined before ev_done */
+  hipStream_t   st_flush; hipEvent_t ev_fork, ev_join;
   int           busy;
 };
 
@@ -1190,6 +1193,9 @@ static void slot_alloc( tile_slot & s, ulong n ) {
   TX_CHECK( hipHostMalloc( &s.h_tso, 4*n, 0 ) );
   TX_CHECK( hipEventCreate( &s.ev_start ) ); TX_CHECK( hipEventCreate( &s.ev_done ) );
   TX_CHECK( hipEventCreate( &s.ev_ing0 ) ); TX_CHECK( hipEventCreate( &s.ev_ing1 ) );
+  TX_CHECK( hipStreamCreateWithFlags( &s.st_flush, hipStreamNonBlocking ) );
+  TX_CHECK( hipEventCreateWithFlags( &s.ev_fork, hipEventDisableTiming ) );
+  TX_CHECK( hipEventCreateWithFlags( &s.ev_join, hipEventDisableTiming ) );
 }
 
 static void slot_free_records( tile_slot & s ) {
@@ -1230,6 +1236,8 @@ static void slot_free( tile_slot & s ) {
   (void)hipHostFree( s.h_tso );
   (void)hipEventDestroy( s.ev_start ); (void)hipEventDestroy( s.ev_done );
   (void)hipEventDestroy( s.ev_ing0 ); (void)hipEventDestroy( s.ev_ing1 );
+  (void)hipStreamSynchronize( s.st_flush ); (void)hipStreamDestroy( s.st_flush );
+  (void)hipEventDestroy( s.ev_fork ); (void)hipEventDestroy( s.ev_join );
   slot_free_records( s );
 }
 
@@ -1506,10 +1514,14 @@ submit_frags_body( fd_verify_hip_tile_t * t, tile_slot & s, hipStream_t st, ulon
                           h_out, h_chunk, fdesc );
     TX_CHECK( hipGetLastError() );
     if( s.ing_timed ) TX_CHECK( hipEventRecord( s.ev_ing1, st ) );
-    if( stg ) {
-      hipLaunchKernelGGL( k_out_flush, dim3( (unsigned)((n + 3ul)/4ul) ), dim3( 256 ), 0, st, n, (u8 const *)k_out,
-                          (u32 const *)k_chunk, (u8 *)d_out, (u32 const *)d_out_chunk, (u64 const *)fdesc );
+    if( stg ) {                                              /* off the verify's critical path */
+      TX_CHECK( hipEventRecord( s.ev_fork, st ) );
+      TX_CHECK( hipStreamWaitEvent( s.st_flush, s.ev_fork, 0 ) );
+      hipLaunchKernelGGL( k_out_flush, dim3( (unsigned)((n + 3ul)/4ul) ), dim3( 256 ), 0, s.st_flush, n,
+                          (u8 const *)k_out, (u32 const *)k_chunk, (u8 *)d_out, (u32 const *)d_out_chunk,
+                          (u64 const *)fdesc );
       TX_CHECK( hipGetLastError() );
+      TX_CHECK( hipEventRecord( s.ev_join, s.st_flush ) );
     }
     fd_hip_segs_t segs = { s.d_misc + 32u, n_seg, seg_cap, s.d_counter };
     if( fd_ed25519_hip_verify_segs( s.ctx, segs, s.d_rsig, s.d_rpub, k_out, s.d_rmoff, s.d_rmsz, s.d_rcode, st ) ) {
@@ -1518,6 +1530,7 @@ submit_frags_body( fd_verify_hip_tile_t * t, tile_slot & s, hipStream_t st, ulon
     }
     fd_ed25519_hip_group_reduce_dev( s.ctx, n, s.d_first, s.d_cnt, s.d_rcode, s.d_tcode, st );
     submit_results( s, st, n, d_in_kind, k_out, k_chunk, fdesc );
+    if( stg ) TX_CHECK( hipStreamWaitEvent( st, s.ev_join, 0 ) );   /* ev_done covers the out dcache writes */
     return;
   }
   submit_results( s, st, n, d_in_kind, d_out, d_out_chunk );
