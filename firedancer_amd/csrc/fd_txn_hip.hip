@@ -1466,7 +1466,7 @@ fd_verify_hip_tile_submit( fd_verify_hip_tile_t * t, ulong n, uchar const * d_po
 static void
 submit_frags_body( fd_verify_hip_tile_t * t, tile_slot & s, hipStream_t st, ulong n, uchar const * d_in,
                    uint const * d_in_chunk, ushort const * d_in_sz, uchar const * d_in_kind, uchar * d_out,
-                   uint const * d_out_chunk ) {
+                   uint const * d_out_chunk, int misc_zeroed = 0 ) {
   dim3 grid( (unsigned)((n + 255)/256) ), blk( 256 );
   if( t->ingest_split ) {
     /* the three-kernel form (ingest copy, one-lane parse, expansion, then
@@ -1491,7 +1491,8 @@ submit_frags_body( fd_verify_hip_tile_t * t, tile_slot & s, hipStream_t st, ulon
     ulong need = (ulong)n_seg * seg_cap;                     /* <= 12 x (n + SLOT_SEG_SLACK): sized at tile_new */
     if( s.rcap < need ) { TX_CHECK( hipStreamSynchronize( st ) ); slot_records( s, need ); }
     s.n_seg = n_seg;
-    TX_CHECK( hipMemsetAsync( s.d_misc, 0, 4ul*(32ul + (ulong)n_seg*FD_HIP_SEG_STRIDE), st ) );
+    if( !misc_zeroed )                                       /* submit_range: k_range_gather zeroed it */
+      TX_CHECK( hipMemsetAsync( s.d_misc, 0, 4ul*(32ul + (ulong)n_seg*FD_HIP_SEG_STRIDE), st ) );
     s.ing_timed = t->ingest_timing;
     if( s.ing_timed ) TX_CHECK( hipEventRecord( s.ev_ing0, st ) );
     /* out staging: the batch works on HBM staging frags, then k_out_flush
@@ -1575,10 +1576,13 @@ fd_verify_hip_tile_submit_frags( fd_verify_hip_tile_t * t, ulong n, uchar const 
    fd_mcache_publish), so they are that frag's unless the line was reused
    since, which the same overrun check catches. */
 __global__ __launch_bounds__(256)
-void k_range_gather( ulong n, u8 const * __restrict__ mcache, ulong line_mask, ulong first, ulong stride,
+void k_range_gather( u32 * __restrict__ misc, u32 misc_words,
+                     ulong n, u8 const * __restrict__ mcache, ulong line_mask, ulong first, ulong stride,
                      ulong chunk_off, ulong chunk0, ulong wmark, u32 * __restrict__ in_chunk,
                      u16 * __restrict__ in_sz, u8 * __restrict__ in_kind, u32 * __restrict__ tso ) {
   ulong j = (ulong)blockIdx.x * blockDim.x + threadIdx.x;
+  /* the slot's misc block for k_txnm_batch (one dispatch fewer on the batch's path) */
+  for( ulong w = j; w < (ulong)misc_words; w += (ulong)gridDim.x * blockDim.x ) misc[w] = 0u;
   if( j >= n ) return;
   ulong const seq = first + j * stride;
   u8 const * line = mcache + 32ul * (seq & line_mask);
@@ -1606,11 +1610,14 @@ fd_verify_hip_tile_submit_range( fd_verify_hip_tile_t * t, fd_verify_hip_range_t
   s.frags = 1; s.range = 1;
   if( !n ) { memset( s.h_res, 0, TILE_RES_HDR ); TX_CHECK( hipEventRecord( s.ev_done, st ) ); return 0; }
   ulong const first = r->seq0 + (r->rr_idx + r->rr_cnt - r->seq0 % r->rr_cnt) % r->rr_cnt;
-  hipLaunchKernelGGL( k_range_gather, dim3( (unsigned)((n + 255ul)/256ul) ), dim3( 256 ), 0, st, n,
+  int const fold = !t->ingest_split;                        /* the fused ingest's misc block, zeroed here */
+  ulong const F = t->fb == 8 ? 8ul : 16ul, nwg = (n + F - 1ul) / F;
+  u32 const misc_words = fold ? 32u + (nwg < FB_SEGS ? (u32)nwg : FB_SEGS) * FD_HIP_SEG_STRIDE : 0u;
+  hipLaunchKernelGGL( k_range_gather, dim3( (unsigned)((n + 255ul)/256ul) ), dim3( 256 ), 0, st, s.d_misc, misc_words, n,
                       (u8 const *)r->mcache, r->depth - 1ul, first, r->rr_cnt, r->chunk_off, r->chunk0, r->wmark,
                       s.d_rin, s.d_rsz, s.d_rkind, s.d_tso );
   TX_CHECK( hipGetLastError() );
-  submit_frags_body( t, s, st, n, d_in, s.d_rin, s.d_rsz, s.d_rkind, d_out, d_out_chunk );
+  submit_frags_body( t, s, st, n, d_in, s.d_rin, s.d_rsz, s.d_rkind, d_out, d_out_chunk, fold );
   TX_CHECK( hipMemcpyAsync( s.h_tso, s.d_tso, 4ul*n, hipMemcpyDeviceToHost, st ) );
   TX_CHECK( hipEventRecord( s.ev_done, st ) );
   return 0;
