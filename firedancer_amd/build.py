@@ -12,8 +12,9 @@ PKG = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(PKG, "csrc")
 LIB = os.path.join(PKG, "libfd_ed25519_hip.so")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
-SOURCES = ["fd_ed25519_hip.hip", "fd_ed25519_dev.h", "fd_hip_order.h", "fd_txn_hip.hip", "fd_sha512_hip.hip"]
-UNITS = ["fd_ed25519_hip.hip", "fd_txn_hip.hip", "fd_sha512_hip.hip"]
+SOURCES = ["fd_ed25519_hip.hip", "fd_ed25519_dev.h", "fd_hip_order.h", "fd_txn_hip.hip", "fd_txn_hip_int.h", "fd_sha512_hip.hip",
+           "fd_verify_svc.hip"]
+UNITS = ["fd_ed25519_hip.hip", "fd_txn_hip.hip", "fd_sha512_hip.hip", "fd_verify_svc.hip"]
 
 
 def _stale(target, deps):
@@ -31,7 +32,7 @@ def build(force=False, verbose=False, variant=None, defines=()):
     """Build the library (or an experimental variant with extra -D defines,
     loaded when FD_ED25519_HIP_LIB names it)."""
     lib_path = variant_path(variant)
-    deps = [os.path.join(CSRC, s) for s in SOURCES] + [os.path.join(PKG, "..", "include", h) for h in ("fd_ed25519_hip.h", "fd_verify_hip.h", "fd_replay_hip.h", "fd_sha512_hip.h")]
+    deps = [os.path.join(CSRC, s) for s in SOURCES] + [os.path.join(PKG, "..", "include", h) for h in ("fd_ed25519_hip.h", "fd_verify_hip.h", "fd_replay_hip.h", "fd_sha512_hip.h", "fd_verify_svc.h")]
     if force or _stale(lib_path, deps):
         extra = os.environ.get("FD_HIPCC_EXTRA", "").split() if variant else []   # variants only: A/B flags
         cmd = [HIPCC, "--offload-arch=gfx950", "-O3", "-fPIC", "-shared", "-std=c++17"] + extra + \

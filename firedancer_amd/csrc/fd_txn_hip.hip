@@ -25,6 +25,7 @@
 #include "../../include/fd_verify_hip.h"
 #include "../../include/fd_replay_hip.h"
 #include "fd_hip_order.h"
+#include "fd_txn_hip_int.h"
 
 #include <hip/hip_runtime.h>
 #include <chrono>
@@ -705,7 +706,8 @@ void k_txnm_batch( ulong n, u8 const * in, u32 const * __restrict__ in_chunk, u1
                    u32 * __restrict__ first_o, u8 * __restrict__ cnt_o, u32 * __restrict__ misc,
                    u8 * __restrict__ rsig, u8 * __restrict__ rpub, u32 * __restrict__ rmoff,
                    u32 * __restrict__ rmsz, u32 n_seg, ulong seg_cap, u8 const * hout,
-                   u32 const * __restrict__ hout_chunk, u64 * __restrict__ fdesc ) {
+                   u32 const * __restrict__ hout_chunk, u64 * __restrict__ fdesc,
+                   u64 const * __restrict__ seedv ) {
   constexpr u32 BUDGET = FB_PIECES_PER_FRAG * (u32)F;                        /* staged pieces per group */
   __shared__ __attribute__((aligned(16))) u8 lds[16u * BUDGET + 32u];       /* + over-read of the last piece */
   /* this group's record segment (fd_hip_order.h): claims, histogram and
@@ -883,7 +885,7 @@ void k_txnm_batch( ulong n, u8 const * in, u32 const * __restrict__ in_chunk, u1
       for( int q = 0; q < 8; q++ )
         w[q] = (u64)lds_ld4( lds, pb + sp.sig_at + 8u*q ) | ((u64)lds_ld4( lds, pb + sp.sig_at + 8u*q + 4u ) << 32);
     }
-    tag = xh_hash64( seed, w );
+    tag = xh_hash64( seedv ? seedv[j] : seed, w );                         /* seedv: the service's per-frag seeds */
   }
   base = (u32)__builtin_amdgcn_readfirstlane( (int)base );
   TXTR( 5 );
@@ -1507,12 +1509,12 @@ submit_frags_body( fd_verify_hip_tile_t * t, tile_slot & s, hipStream_t st, ulon
       hipLaunchKernelGGL( k_txnm_batch<8>, dim3( (unsigned)nwg ), dim3( 64 ), 0, st, n, d_in,
                           d_in_chunk, d_in_sz, d_in_kind, k_out, k_chunk, (u64)t->seed, s.d_tsz, s.d_tag, s.d_bid,
                           s.d_first, s.d_cnt, s.d_misc, s.d_rsig, s.d_rpub, s.d_rmoff, s.d_rmsz, n_seg, seg_cap,
-                          h_out, h_chunk, fdesc );
+                          h_out, h_chunk, fdesc, (u64 const *)0 );
     else
       hipLaunchKernelGGL( k_txnm_batch<16>, dim3( (unsigned)nwg ), dim3( 64 ), 0, st, n, d_in,
                           d_in_chunk, d_in_sz, d_in_kind, k_out, k_chunk, (u64)t->seed, s.d_tsz, s.d_tag, s.d_bid,
                           s.d_first, s.d_cnt, s.d_misc, s.d_rsig, s.d_rpub, s.d_rmoff, s.d_rmsz, n_seg, seg_cap,
-                          h_out, h_chunk, fdesc );
+                          h_out, h_chunk, fdesc, (u64 const *)0 );
     TX_CHECK( hipGetLastError() );
     if( s.ing_timed ) TX_CHECK( hipEventRecord( s.ev_ing1, st ) );
     if( stg ) {                                              /* off the verify's critical path */
@@ -1535,6 +1537,42 @@ submit_frags_body( fd_verify_hip_tile_t * t, tile_slot & s, hipStream_t st, ulon
     return;
   }
   submit_results( s, st, n, d_in_kind, d_out, d_out_chunk );
+}
+
+/* the frag-batch core for the verify service (fd_txn_hip_int.h): the same
+   k_txnm_batch<16> / verify_segs / reduce sequence as submit_frags_body's
+   fused path, with per-frag seeds and no host out dcache (the service's
+   staging frags are flushed later, fd_verify_svc.hip) */
+extern "C" __attribute__((visibility("hidden"))) ulong fd_txn_hip_record_cap( ulong n ) {
+  return 12ul * (n + SLOT_SEG_SLACK);
+}
+extern "C" __attribute__((visibility("hidden"))) ulong fd_txn_hip_misc_bytes( void ) { return SLOT_MISC_BYTES; }
+
+extern "C" __attribute__((visibility("hidden"))) void
+fd_txn_hip_batch_core( fd_ed25519_hip_ctx_t * ctx, hipStream_t st, ulong n, u8 const * in, u32 const * in_chunk,
+                       u16 const * in_sz, u8 const * in_kind, u8 * out, u32 const * out_chunk, u64 const * seedv,
+                       u16 * tsz, u64 * tag, u64 * bid, u32 * first, u8 * cnt, u32 * misc, u8 * rsig, u8 * rpub,
+                       u32 * rmoff, u32 * rmsz, ulong rcap, signed char * rcode, signed char * tcode, u64 * fdesc ) {
+  if( !n ) return;
+  ulong const F = 16ul, nwg = (n + F - 1ul) / F;
+  u32 const n_seg = nwg < FB_SEGS ? (u32)nwg : FB_SEGS;
+  ulong const seg_cap = 12ul * F * ((nwg + n_seg - 1ul) / n_seg);
+  if( (ulong)n_seg * seg_cap > rcap ) {
+    fprintf( stderr, "fd_verify_hip: batch core: %lu frags need %lu records, %lu allocated\n", n,
+             (ulong)n_seg * seg_cap, rcap );
+    abort();
+  }
+  TX_CHECK( hipMemsetAsync( misc, 0, 4ul*(32ul + (ulong)n_seg*FD_HIP_SEG_STRIDE), st ) );
+  hipLaunchKernelGGL( k_txnm_batch<16>, dim3( (unsigned)nwg ), dim3( 64 ), 0, st, n, in, in_chunk, in_sz, in_kind,
+                      out, out_chunk, (u64)0, tsz, tag, bid, first, cnt, misc, rsig, rpub, rmoff, rmsz, n_seg, seg_cap,
+                      (u8 const *)0, (u32 const *)0, fdesc, seedv );
+  TX_CHECK( hipGetLastError() );
+  fd_hip_segs_t segs = { misc + 32u, n_seg, seg_cap, misc };
+  if( fd_ed25519_hip_verify_segs( ctx, segs, rsig, rpub, out, rmoff, rmsz, rcode, st ) ) {
+    fprintf( stderr, "fd_verify_hip: segmented verify refused (%u x %lu records)\n", n_seg, seg_cap );
+    abort();
+  }
+  fd_ed25519_hip_group_reduce_dev( ctx, n, first, cnt, rcode, tcode, st );
 }
 
 extern "C" int

@@ -1,0 +1,578 @@
+/* fd_verify_svc.hip -- the per-GPU verify service (include/fd_verify_svc.h):
+   the GPU tile's side of the shared-memory protocol.
+
+   One process per GPU owns the HIP context.  Every verify tile it serves
+   posts requests (a seq range of an unpolled quic_verify link, or frags it
+   copied from a polled link) into its slots of the segment.  The service
+   merges the posted requests of all tiles into one launch (up to batch_max
+   frags), so a launch is C4-sized whatever the tile count:
+
+     k_svc_gather   one wave per frag: before_frag's share (range requests
+                    name only the kept seqs: seq0 + i x rr_cnt), the mcache
+                    line (seq still there, chunk in [chunk0, wmark], sz <=
+                    FD_TPU_RAW_MTU: fd_stem.c and during_frag's checks,
+                    fd_verify_tile.c:74-76), and the frag's bytes from the
+                    link's dcache (pinned host memory) into an HBM ingest
+                    frag -- the PCIe read leaves the CU as soon as it lands,
+                    before the LDS-heavy parse holds it
+     fd_txn_hip_batch_core
+                    k_txnm_batch<16> (during_frag's copy into the request's
+                    HBM staging frags, fd_txn_parse, the sig0 tag with each
+                    tile's seed, the signature records), the verify, the
+                    per-txn fd_ed25519_verify_batch_single_msg reduce
+     k_svc_results  32-B result records; one DMA copy per request into its
+                    slot's result array, then the slot goes to RESULTS
+
+   The out frags stay in HBM.  After its ordered pass (tcache, bundles) the
+   tile posts flushes: out entries (frag, chunk, realized size) of the frags
+   it publishes, chunks assigned as after_frag assigns them.  A flush copies
+   those staging frags into an HBM mirror of the tile's out dcache at the
+   same offsets (k_svc_compact) and DMAs the covered spans -- one or two per
+   flush, contiguous because the chunks are -- into the host out dcache.  Only
+   published frags cross PCIe, and no CU waits on a PCIe write.
+
+   Flushes of a tile run in order on the tile's own stream; requests and
+   flushes of different tiles are independent.  Every HIP failure aborts
+   (the reference's FD_LOG_ERR ends a tile; a device error is never turned
+   into a verdict). */
+
+#include "../../include/fd_verify_svc.h"
+#include "../../include/fd_verify_hip.h"
+#include "fd_txn_hip_int.h"
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <time.h>
+
+#define SV_CHECK( x ) do {                                                            \
+    hipError_t e_ = (x);                                                               \
+    if( e_ != hipSuccess ) {                                                           \
+      fprintf( stderr, "fd_verify_svc: %s failed at %s:%d: %s\n", #x, __FILE__,      \
+               __LINE__, hipGetErrorString( e_ ) );                                    \
+      abort();                                                                         \
+    }                                                                                  \
+  } while( 0 )
+
+typedef uint8_t  u8;
+typedef uint16_t u16;
+typedef uint32_t u32;
+typedef uint64_t u64;
+
+#define SVC_INGEST_CHUNKS 32ul   /* an ingest frag: 2048 B (a gossip message's bound, the RAW_MTU's 1312 below it) */
+#define SVC_REQ_MAX       64u    /* requests per launch */
+#define SVC_LAUNCH_MAX    8ul
+#define SVC_FLUSH_Q       64ul   /* flushes in flight per tile */
+#define SVC_REGION_MAX    64ul
+
+static long svc_now_ns( void ) {
+  struct timespec ts;
+  clock_gettime( CLOCK_MONOTONIC, &ts );
+  return (long)ts.tv_sec * 1000000000L + (long)ts.tv_nsec;
+}
+
+/* one request of a launch, as the gather kernel reads it (128 B) */
+struct __attribute__((aligned(16))) svc_desc {
+  u64 base;        /* the request's first frag in the launch */
+  u64 n;
+  u64 kind;        /* FD_VERIFY_SVC_REQ_* */
+  u64 src;         /* RANGE: the mcache's line 0; FRAGS: the frag area (device addresses) */
+  u64 aux0;        /* RANGE: the link's chunk base; FRAGS: the sizes */
+  u64 aux1;        /* FRAGS: the kinds */
+  u64 first;       /* RANGE: the first kept seq */
+  u64 stride;      /* RANGE: rr_cnt */
+  u64 line_mask;   /* RANGE: depth - 1 */
+  u64 chunk0, wmark;
+  u64 seed;
+  u64 stage0;      /* staging chunk of the request's frag 0 */
+  u64 rsv[3];
+};
+static_assert( sizeof(svc_desc) == 128, "svc_desc layout" );
+
+/**********************************************************************/
+/* kernels                                                             */
+
+__global__ __launch_bounds__(256)
+void k_svc_gather( svc_desc const * __restrict__ desc, u32 nreq, ulong n, u8 * __restrict__ ingest,
+                   u8 * __restrict__ stage, u32 * __restrict__ in_chunk, u16 * __restrict__ in_sz,
+                   u8 * __restrict__ in_kind, u32 * __restrict__ tso, u64 * __restrict__ seedv,
+                   u32 * __restrict__ stage_chunk ) {
+  __shared__ u64 sbase[SVC_REQ_MAX];
+  for( u32 i = threadIdx.x; i < nreq; i += blockDim.x ) sbase[i] = desc[i].base;
+  __syncthreads();
+  ulong const j = (ulong)blockIdx.x * 4ul + (threadIdx.x >> 6);
+  u32 const lane = threadIdx.x & 63u;
+  if( j >= n ) return;
+  u32 lo = 0u, hi = nreq;                                   /* sbase[lo] <= j < sbase[hi] */
+  while( hi - lo > 1u ) { u32 mid = (lo + hi) >> 1; if( sbase[mid] <= j ) lo = mid; else hi = mid; }
+  svc_desc const * d = desc + lo;
+  ulong const i = j - d->base;
+  u32 sz = 0u, kind = FD_VERIFY_HIP_IN_QUIC, tsv = 0u;
+  bool ok;
+  u8 const * src;
+  if( d->kind == FD_VERIFY_SVC_REQ_RANGE ) {
+    ulong const seq = d->first + i * d->stride;
+    u8 const * line = (u8 const *)d->src + 32ul * (seq & d->line_mask);
+    /* lanes 0 and 1 read the line's two halves (seq, sig | chunk, sz,
+       ctl, tsorig, tspub) with vector loads, every lane takes them */
+    uint4 v = make_uint4( 0u, 0u, 0u, 0u );
+    if( lane < 2u ) v = *(uint4 const *)(line + 16u * lane);
+    u64 const found = (u64)(u32)__shfl( (int)v.x, 0 ) | ((u64)(u32)__shfl( (int)v.y, 0 ) << 32);
+    u32 const chunk = (u32)__shfl( (int)v.x, 1 );
+    sz  = (u32)__shfl( (int)v.y, 1 ) & 0xffffu;
+    tsv = (u32)__shfl( (int)v.z, 1 );
+    ok  = found == seq && (ulong)chunk >= d->chunk0 && (ulong)chunk <= d->wmark && sz <= FD_VERIFY_HIP_TPU_RAW_MTU;
+    src = (u8 const *)d->aux0 + 64ul * chunk;
+  } else {
+    src  = (u8 const *)d->src + FD_VERIFY_SVC_FRAG_STRIDE * i;
+    sz   = ((u16 const *)d->aux0)[i];
+    kind = ((u8 const *)d->aux1)[i];
+    ok   = sz <= FD_VERIFY_SVC_FRAG_STRIDE;
+  }
+  u8 * dst = ingest + 64ul * SVC_INGEST_CHUNKS * j;
+  if( ok ) for( u32 p = 16u * lane; p < sz; p += 1024u ) *(uint4 *)(dst + p) = *(uint4 const *)(src + p);
+  u32 const sc = (u32)(d->stage0 + FD_TXN_HIP_STAGE_CHUNKS * i);
+  /* a gossip vote's out header: the reference writes four fields into the
+     out chunk's stale header (fd_verify_tile.c:90-93); here the rest is 0 */
+  if( kind == FD_VERIFY_HIP_IN_GOSSIP && lane < 5u ) *(uint4 *)(stage + 64ul * sc + 16u * lane) = make_uint4( 0u, 0u, 0u, 0u );
+  if( lane == 0u ) {
+    in_chunk[j] = (u32)(SVC_INGEST_CHUNKS * j); in_sz[j] = ok ? (u16)sz : (u16)0xffffu; in_kind[j] = (u8)kind;
+    tso[j] = tsv; seedv[j] = d->seed; stage_chunk[j] = sc;
+  }
+}
+
+__global__ __launch_bounds__(256)
+void k_svc_results( ulong n, u16 const * __restrict__ tsz, u64 const * __restrict__ tag, u64 const * __restrict__ bid,
+                    u8 const * __restrict__ cnt, signed char const * __restrict__ tcode, u64 const * __restrict__ fdesc,
+                    u32 const * __restrict__ tso, fd_verify_svc_res_t * __restrict__ res ) {
+  ulong const j = (ulong)blockIdx.x * blockDim.x + threadIdx.x;
+  if( j >= n ) return;
+  u64 const d = fdesc[j];
+  u32 const cend = (u32)(d & 0xfffu), psz = (u32)((d >> 12) & 0x7ffu);
+  bool const gossip = (d >> 33) & 1u, bad = (d >> 34) & 1u;
+  fd_verify_svc_res_t r;
+  r.tag = tag[j]; r.bundle_id = bid[j]; r.txn_t_sz = tsz[j]; r.payload_sz = (u16)psz; r.code = tcode[j];
+  r.flags = bad ? (u8)FD_VERIFY_SVC_RES_BAD
+                : (!gossip && cend < FD_VERIFY_HIP_TXNM_SZ + psz) ? (u8)FD_VERIFY_SVC_RES_HOST : (u8)0;
+  r.sig_cnt = cnt[j]; r.rsv0 = 0u; r.tsorig = tso[j]; r.rsv1 = 0u;
+  res[j] = r;
+}
+
+/* a flush: out entry e's staging frag (its realized bytes, in whole 64-B
+   chunks) to the tile's HBM mirror at the entry's chunk; one wave per entry */
+__global__ __launch_bounds__(256)
+void k_svc_compact( fd_verify_svc_out_t const * __restrict__ out, ulong m, u8 const * __restrict__ stage,
+                    ulong stage0, u8 * __restrict__ mirror, long delta ) {
+  ulong const e = (ulong)blockIdx.x * 4ul + (threadIdx.x >> 6);
+  u32 const lane = threadIdx.x & 63u;
+  if( e >= m ) return;
+  fd_verify_svc_out_t const o = out[e];
+  if( o.flags & FD_VERIFY_SVC_OUT_HOSTWRITTEN ) return;
+  u32 const len = ((u32)o.sz + 63u) & ~63u;
+  u8 const * s = stage + 64ul * (stage0 + FD_TXN_HIP_STAGE_CHUNKS * (ulong)o.idx);
+  u8 *       d = mirror + (long)(64ul * (ulong)o.chunk) + delta;
+  for( u32 p = 16u * lane; p < len; p += 1024u ) *(uint4 *)(d + p) = *(uint4 const *)(s + p);
+}
+
+/**********************************************************************/
+/* service                                                             */
+
+struct svc_launch {
+  int                    busy;
+  fd_ed25519_hip_ctx_t * ctx;
+  hipStream_t            st;
+  hipEvent_t             ev0, ev1;
+  u8 *  d_ingest; u32 * d_in_chunk; u16 * d_in_sz; u8 * d_in_kind; u32 * d_tso; u64 * d_seed; u32 * d_stage_chunk;
+  u16 * d_tsz; u64 * d_tag; u64 * d_bid; u32 * d_first; u8 * d_cnt; signed char * d_tcode; u32 * d_misc;
+  u8 *  d_rsig; u8 * d_rpub; u32 * d_rmoff; u32 * d_rmsz; signed char * d_rcode; ulong rcap; u64 * d_fdesc;
+  fd_verify_svc_res_t * d_res;
+  svc_desc * h_desc; svc_desc * d_desc;
+  ulong nreq, n;
+  struct { ulong t, slot; } req[SVC_REQ_MAX];
+};
+
+struct svc_tile {
+  int          set;
+  u8 *         h_out;          /* the out dcache (host) */
+  ulong        out_sz;
+  u8 const *   chunk_base;     /* host address of out chunk 0 */
+  u8 *         d_mirror;       /* HBM, out_sz bytes */
+  hipStream_t  st;
+  hipEvent_t   ev[SVC_FLUSH_Q];
+  ulong        take;           /* next request id to take */
+  ulong        flush_take;     /* next flush to start */
+  ulong        flush_fin;      /* flushes retired */
+};
+
+struct svc_pend { ulong t, slot, n; long seen; };
+
+struct fd_verify_svc {
+  fd_verify_svc_seg_t * seg;
+  int      dev;
+  ulong    batch_max, inflight;
+  ulong    merge_min; long merge_wait_ns;
+  struct { u8 * h; ulong sz; u8 * d; } reg[SVC_REGION_MAX];
+  ulong    nreg;
+  struct { int set; u8 const * d_mcache; ulong depth; u8 const * d_base; ulong chunk0, wmark; } link[FD_VERIFY_SVC_LINK_MAX];
+  svc_tile tile[FD_VERIFY_SVC_TILE_MAX];
+  u8 *     d_stage;            /* staging: tile x slot x slot_cap frags of FD_TXN_HIP_STAGE_CHUNKS */
+  svc_launch L[SVC_LAUNCH_MAX];
+  svc_pend * pend; ulong pend_cap, pend_head, pend_tail, pend_frags;
+  ulong    stat[8];            /* launches, frags, requests, flushes, flushed frags, flushed bytes, spans, gpu ns */
+  int      running;
+};
+
+static u8 * svc_dev( fd_verify_svc_t * s, void const * h, ulong sz ) {
+  u8 const * p = (u8 const *)h;
+  for( ulong k = 0; k < s->nreg; k++ )
+    if( p >= s->reg[k].h && p + sz <= s->reg[k].h + s->reg[k].sz ) return s->reg[k].d + (p - s->reg[k].h);
+  fprintf( stderr, "fd_verify_svc: %p (+%lu) is in no mapped region\n", h, sz );
+  abort();
+}
+
+static ulong svc_stage0( fd_verify_svc_t const * s, ulong t, ulong slot ) {
+  return (t * s->seg->req_depth + slot) * s->seg->slot_cap * FD_TXN_HIP_STAGE_CHUNKS;
+}
+
+static void launch_alloc( svc_launch & L, int dev, ulong nmax ) {
+  memset( &L, 0, sizeof(L) );
+  L.rcap = fd_txn_hip_record_cap( nmax );
+  L.ctx  = fd_ed25519_hip_ctx_new( dev, L.rcap );
+  if( !L.ctx ) { fprintf( stderr, "fd_verify_svc: context creation failed\n" ); abort(); }
+  L.st = (hipStream_t)fd_ed25519_hip_ctx_stream( L.ctx );
+  SV_CHECK( hipMalloc( &L.d_ingest, 64ul * SVC_INGEST_CHUNKS * nmax ) );
+  SV_CHECK( hipMalloc( &L.d_in_chunk, 4ul * nmax ) ); SV_CHECK( hipMalloc( &L.d_in_sz, 2ul * nmax ) );
+  SV_CHECK( hipMalloc( &L.d_in_kind, nmax ) );        SV_CHECK( hipMalloc( &L.d_tso, 4ul * nmax ) );
+  SV_CHECK( hipMalloc( &L.d_seed, 8ul * nmax ) );     SV_CHECK( hipMalloc( &L.d_stage_chunk, 4ul * nmax ) );
+  SV_CHECK( hipMalloc( &L.d_tsz, 2ul * nmax ) );      SV_CHECK( hipMalloc( &L.d_tag, 8ul * nmax ) );
+  SV_CHECK( hipMalloc( &L.d_bid, 8ul * nmax ) );      SV_CHECK( hipMalloc( &L.d_first, 4ul * nmax ) );
+  SV_CHECK( hipMalloc( &L.d_cnt, nmax ) );            SV_CHECK( hipMalloc( &L.d_tcode, nmax ) );
+  SV_CHECK( hipMalloc( &L.d_misc, fd_txn_hip_misc_bytes() ) );
+  SV_CHECK( hipMalloc( &L.d_rsig, 64ul * L.rcap ) );  SV_CHECK( hipMalloc( &L.d_rpub, 32ul * L.rcap ) );
+  SV_CHECK( hipMalloc( &L.d_rmoff, 4ul * L.rcap ) );  SV_CHECK( hipMalloc( &L.d_rmsz, 4ul * L.rcap ) );
+  SV_CHECK( hipMalloc( &L.d_rcode, L.rcap ) );        SV_CHECK( hipMalloc( &L.d_fdesc, 8ul * nmax ) );
+  SV_CHECK( hipMalloc( &L.d_res, sizeof(fd_verify_svc_res_t) * nmax ) );
+  SV_CHECK( hipHostMalloc( &L.h_desc, sizeof(svc_desc) * SVC_REQ_MAX, 0 ) );
+  SV_CHECK( hipMalloc( &L.d_desc, sizeof(svc_desc) * SVC_REQ_MAX ) );
+  SV_CHECK( hipEventCreate( &L.ev0 ) ); SV_CHECK( hipEventCreate( &L.ev1 ) );
+}
+
+static void launch_free( svc_launch & L ) {
+  if( !L.ctx ) return;
+  (void)hipStreamSynchronize( L.st );
+  (void)hipFree( L.d_ingest ); (void)hipFree( L.d_in_chunk ); (void)hipFree( L.d_in_sz ); (void)hipFree( L.d_in_kind );
+  (void)hipFree( L.d_tso ); (void)hipFree( L.d_seed ); (void)hipFree( L.d_stage_chunk ); (void)hipFree( L.d_tsz );
+  (void)hipFree( L.d_tag ); (void)hipFree( L.d_bid ); (void)hipFree( L.d_first ); (void)hipFree( L.d_cnt );
+  (void)hipFree( L.d_tcode ); (void)hipFree( L.d_misc ); (void)hipFree( L.d_rsig ); (void)hipFree( L.d_rpub );
+  (void)hipFree( L.d_rmoff ); (void)hipFree( L.d_rmsz ); (void)hipFree( L.d_rcode ); (void)hipFree( L.d_fdesc );
+  (void)hipFree( L.d_res ); (void)hipHostFree( L.h_desc ); (void)hipFree( L.d_desc );
+  (void)hipEventDestroy( L.ev0 ); (void)hipEventDestroy( L.ev1 );
+  fd_ed25519_hip_ctx_delete( L.ctx );
+  L.ctx = 0;
+}
+
+extern "C" fd_verify_svc_t *
+fd_verify_svc_boot( void * seg_mem, int device, ulong batch_max, ulong inflight ) {
+  fd_verify_svc_seg_t * seg = fd_verify_svc_join( seg_mem );
+  if( !seg || inflight < 1ul || inflight > SVC_LAUNCH_MAX || batch_max < seg->slot_cap ) return 0;
+  /* staging messages are addressed by 32-bit byte offsets (the verify's
+     msg_off): the whole staging area stays below 4 GiB */
+  ulong stage_sz = seg->tile_cnt * seg->req_depth * seg->slot_cap * FD_TXN_HIP_STAGE_CHUNKS * 64ul;
+  if( stage_sz + 4096ul >= (1ul << 32) ) {
+    fprintf( stderr, "fd_verify_svc: staging %lu B over 4 GiB (tiles x req_depth x slot_cap too large)\n", stage_sz );
+    return 0;
+  }
+  SV_CHECK( hipSetDevice( device ) );
+  fd_verify_svc_t * s = (fd_verify_svc_t *)calloc( 1, sizeof(fd_verify_svc_t) );
+  s->seg = seg; s->dev = device; s->batch_max = batch_max; s->inflight = inflight;
+  s->merge_min = batch_max / 2ul; s->merge_wait_ns = 100000L;
+  SV_CHECK( hipMalloc( &s->d_stage, stage_sz + 4096ul ) );
+  for( ulong k = 0; k < inflight; k++ ) launch_alloc( s->L[k], device, batch_max );
+  s->pend_cap = seg->tile_cnt * seg->req_depth;
+  s->pend = (svc_pend *)calloc( s->pend_cap, sizeof(svc_pend) );
+  SV_CHECK( hipDeviceSynchronize() );
+  return s;
+}
+
+extern "C" int
+fd_verify_svc_map( fd_verify_svc_t * s, void * host, ulong sz ) {
+  if( !s || !host || !sz || s->nreg >= SVC_REGION_MAX ) return -1;
+  ulong a = (ulong)host & ~4095ul, e = ((ulong)host + sz + 4095ul) & ~4095ul;
+  SV_CHECK( hipSetDevice( s->dev ) );
+  if( hipHostRegister( (void *)a, e - a, hipHostRegisterMapped | hipHostRegisterPortable ) != hipSuccess ) return -1;
+  void * d = 0;
+  SV_CHECK( hipHostGetDevicePointer( &d, (void *)a, 0 ) );
+  s->reg[s->nreg].h = (u8 *)a; s->reg[s->nreg].sz = e - a; s->reg[s->nreg].d = (u8 *)d;
+  s->nreg++;
+  return 0;
+}
+
+extern "C" int
+fd_verify_svc_set_link( fd_verify_svc_t * s, ulong link, void const * mcache, ulong depth, void const * chunk_base,
+                        ulong chunk0, ulong wmark ) {
+  if( !s || link >= FD_VERIFY_SVC_LINK_MAX || !mcache || !depth || (depth & (depth - 1ul)) || chunk0 > wmark ||
+      wmark > 0xffffffffull ) return -1;
+  s->link[link].d_mcache = svc_dev( s, mcache, 32ul * depth );
+  s->link[link].depth    = depth;
+  s->link[link].d_base   = svc_dev( s, (u8 const *)chunk_base + 64ul * chunk0, 64ul * (wmark - chunk0) + 2048ul ) -
+                           64ul * chunk0;
+  s->link[link].chunk0   = chunk0; s->link[link].wmark = wmark;
+  s->link[link].set      = 1;
+  return 0;
+}
+
+extern "C" int
+fd_verify_svc_set_tile( fd_verify_svc_t * s, ulong t, void * out_dcache, ulong out_sz, void const * chunk_base ) {
+  if( !s || t >= s->seg->tile_cnt || !out_dcache || !out_sz || s->tile[t].set ) return -1;
+  svc_tile & T = s->tile[t];
+  (void)svc_dev( s, out_dcache, out_sz );                   /* mapped, for the DMA copies */
+  (void)svc_dev( s, fd_verify_svc_tile( s->seg, t ), s->seg->tile_sz );   /* the tile's part of the segment */
+  SV_CHECK( hipSetDevice( s->dev ) );
+  T.h_out = (u8 *)out_dcache; T.out_sz = out_sz; T.chunk_base = (u8 const *)chunk_base;
+  SV_CHECK( hipMalloc( &T.d_mirror, out_sz + 4096ul ) );
+  SV_CHECK( hipStreamCreateWithFlags( &T.st, hipStreamNonBlocking ) );
+  for( ulong k = 0; k < SVC_FLUSH_Q; k++ ) SV_CHECK( hipEventCreateWithFlags( &T.ev[k], hipEventDisableTiming ) );
+  T.set = 1;
+  return 0;
+}
+
+extern "C" void
+fd_verify_svc_set_merge( fd_verify_svc_t * s, ulong min_frags, ulong wait_ns ) {
+  s->merge_min = min_frags; s->merge_wait_ns = (long)wait_ns;
+}
+
+extern "C" int
+fd_verify_svc_run( fd_verify_svc_t * s ) {
+  for( ulong t = 0; t < s->seg->tile_cnt; t++ ) if( !s->tile[t].set ) return -1;
+  /* the kernels' code objects loaded and every buffer touched once before
+     the first request (the steady state loads nothing) */
+  for( ulong k = 0; k < s->inflight; k++ ) {
+    svc_launch & L = s->L[k];
+    hipLaunchKernelGGL( k_svc_gather, dim3( 1 ), dim3( 256 ), 0, L.st, L.d_desc, 0u, 0ul, L.d_ingest, s->d_stage,
+                        L.d_in_chunk, L.d_in_sz, L.d_in_kind, L.d_tso, L.d_seed, L.d_stage_chunk );
+    hipLaunchKernelGGL( k_svc_results, dim3( 1 ), dim3( 256 ), 0, L.st, 0ul, L.d_tsz, L.d_tag, L.d_bid, L.d_cnt,
+                        L.d_tcode, L.d_fdesc, L.d_tso, L.d_res );
+    SV_CHECK( hipGetLastError() );
+  }
+  for( ulong t = 0; t < s->seg->tile_cnt; t++ ) {
+    hipLaunchKernelGGL( k_svc_compact, dim3( 1 ), dim3( 256 ), 0, s->tile[t].st, (fd_verify_svc_out_t const *)0, 0ul,
+                        (u8 const *)s->d_stage, 0ul, s->tile[t].d_mirror, 0L );
+    SV_CHECK( hipGetLastError() );
+  }
+  SV_CHECK( hipDeviceSynchronize() );
+  s->running = 1;
+  fd_verify_svc_st( &s->seg->svc_state, FD_VERIFY_SVC_SVC_RUNNING );
+  return 0;
+}
+
+/* validate a posted request and write its launch descriptor */
+static void
+svc_desc_of( fd_verify_svc_t * s, ulong t, ulong slot, ulong base, svc_desc & d ) {
+  fd_verify_svc_seg_t * g = s->seg;
+  fd_verify_svc_req_t const * r = fd_verify_svc_req( g, t, slot );
+  memset( &d, 0, sizeof(d) );
+  d.base = base; d.n = r->n; d.kind = r->kind; d.seed = r->seed; d.stage0 = svc_stage0( s, t, slot );
+  if( r->kind == FD_VERIFY_SVC_REQ_RANGE ) {
+    if( r->link >= FD_VERIFY_SVC_LINK_MAX || !s->link[r->link].set || !r->rr_cnt || r->rr_idx >= r->rr_cnt ||
+        r->seq_cnt > s->link[r->link].depth ||
+        r->n != fd_verify_svc_range_cnt( r->seq0, r->seq_cnt, r->rr_cnt, r->rr_idx ) || r->n > g->slot_cap ) {
+      fprintf( stderr, "fd_verify_svc: tile %lu slot %lu: bad range request (link %lu seq0 %lu cnt %lu rr %lu/%lu n %lu)\n",
+               t, slot, r->link, r->seq0, r->seq_cnt, r->rr_idx, r->rr_cnt, r->n );
+      abort();
+    }
+    d.src = (u64)s->link[r->link].d_mcache; d.aux0 = (u64)s->link[r->link].d_base;
+    d.first = fd_verify_svc_range_first( r->seq0, r->rr_cnt, r->rr_idx ); d.stride = r->rr_cnt;
+    d.line_mask = s->link[r->link].depth - 1ul; d.chunk0 = s->link[r->link].chunk0; d.wmark = s->link[r->link].wmark;
+  } else if( r->kind == FD_VERIFY_SVC_REQ_FRAGS ) {
+    if( r->n > g->frag_cap ) {
+      fprintf( stderr, "fd_verify_svc: tile %lu slot %lu: %lu frags over the frag area's %lu\n", t, slot, r->n, g->frag_cap );
+      abort();
+    }
+    d.src  = (u64)svc_dev( s, fd_verify_svc_frag( g, t, slot ), r->n * FD_VERIFY_SVC_FRAG_STRIDE );
+    d.aux0 = (u64)svc_dev( s, fd_verify_svc_frag_sz( g, t, slot ), 2ul * r->n );
+    d.aux1 = (u64)svc_dev( s, fd_verify_svc_frag_kind( g, t, slot ), r->n );
+  } else {
+    fprintf( stderr, "fd_verify_svc: tile %lu slot %lu: request kind %lu\n", t, slot, r->kind );
+    abort();
+  }
+}
+
+static void
+svc_launch_start( fd_verify_svc_t * s, svc_launch & L ) {
+  fd_verify_svc_seg_t * g = s->seg;
+  ulong n = 0;
+  L.nreq = 0;
+  while( s->pend_head != s->pend_tail && L.nreq < SVC_REQ_MAX ) {
+    svc_pend const & p = s->pend[s->pend_head % s->pend_cap];
+    if( n + p.n > s->batch_max ) break;
+    svc_desc_of( s, p.t, p.slot, n, L.h_desc[L.nreq] );
+    L.req[L.nreq].t = p.t; L.req[L.nreq].slot = p.slot;
+    L.nreq++; n += p.n;
+    s->pend_frags -= p.n; s->pend_head++;
+  }
+  L.n = n; L.busy = 1;
+  SV_CHECK( hipSetDevice( s->dev ) );
+  SV_CHECK( hipEventRecord( L.ev0, L.st ) );
+  SV_CHECK( hipMemcpyAsync( L.d_desc, L.h_desc, sizeof(svc_desc) * L.nreq, hipMemcpyHostToDevice, L.st ) );
+  hipLaunchKernelGGL( k_svc_gather, dim3( (unsigned)((n + 3ul) / 4ul) ), dim3( 256 ), 0, L.st, L.d_desc, (u32)L.nreq, n,
+                      L.d_ingest, s->d_stage, L.d_in_chunk, L.d_in_sz, L.d_in_kind, L.d_tso, L.d_seed, L.d_stage_chunk );
+  SV_CHECK( hipGetLastError() );
+  fd_txn_hip_batch_core( L.ctx, L.st, n, L.d_ingest, L.d_in_chunk, L.d_in_sz, L.d_in_kind, s->d_stage, L.d_stage_chunk,
+                         L.d_seed, L.d_tsz, L.d_tag, L.d_bid, L.d_first, L.d_cnt, L.d_misc, L.d_rsig, L.d_rpub,
+                         L.d_rmoff, L.d_rmsz, L.rcap, L.d_rcode, L.d_tcode, L.d_fdesc );
+  hipLaunchKernelGGL( k_svc_results, dim3( (unsigned)((n + 255ul) / 256ul) ), dim3( 256 ), 0, L.st, n, L.d_tsz, L.d_tag,
+                      L.d_bid, L.d_cnt, L.d_tcode, L.d_fdesc, L.d_tso, L.d_res );
+  SV_CHECK( hipGetLastError() );
+  for( ulong k = 0; k < L.nreq; k++ ) {
+    svc_desc const & d = L.h_desc[k];
+    SV_CHECK( hipMemcpyAsync( fd_verify_svc_res( g, L.req[k].t, L.req[k].slot ), L.d_res + d.base,
+                              sizeof(fd_verify_svc_res_t) * d.n, hipMemcpyDeviceToHost, L.st ) );
+  }
+  SV_CHECK( hipEventRecord( L.ev1, L.st ) );
+  s->stat[0]++; s->stat[1] += n; s->stat[2] += L.nreq;
+}
+
+static void
+svc_flush_start( fd_verify_svc_t * s, ulong t, fd_verify_svc_flush_t const * f ) {
+  fd_verify_svc_seg_t * g = s->seg;
+  svc_tile & T = s->tile[t];
+  if( f->slot >= g->req_depth || f->lo > f->hi || f->hi > g->slot_cap ) {
+    fprintf( stderr, "fd_verify_svc: tile %lu: bad flush (slot %lu [%lu,%lu))\n", t, f->slot, f->lo, f->hi );
+    abort();
+  }
+  ulong const m = f->hi - f->lo;
+  fd_verify_svc_out_t const * out = fd_verify_svc_out( g, t, f->slot ) + f->lo;
+  long const delta = (long)(T.chunk_base - T.h_out);              /* mirror offset of chunk c: 64 c + delta */
+  SV_CHECK( hipSetDevice( s->dev ) );
+  if( m ) {
+    hipLaunchKernelGGL( k_svc_compact, dim3( (unsigned)((m + 3ul) / 4ul) ), dim3( 256 ), 0, T.st,
+                        (fd_verify_svc_out_t const *)svc_dev( s, out, m * sizeof(fd_verify_svc_out_t) ), m,
+                        (u8 const *)s->d_stage, svc_stage0( s, t, f->slot ), T.d_mirror, delta );
+    SV_CHECK( hipGetLastError() );
+  }
+  /* the covered spans: maximal runs of entries whose chunks follow each
+     other (a wrap or a frag the tile wrote itself ends a run) */
+  long s0 = -1, s1 = -1;
+  for( ulong e = 0; e <= m; e++ ) {
+    long a = -1, b = -1;
+    if( e < m && !(out[e].flags & FD_VERIFY_SVC_OUT_HOSTWRITTEN) ) {
+      a = (long)(64ul * (ulong)out[e].chunk) + delta;
+      b = a + (long)(((ulong)out[e].sz + 63ul) & ~63ul);
+      if( a < 0 || b > (long)T.out_sz ) {
+        fprintf( stderr, "fd_verify_svc: tile %lu: out chunk %u (+%u) outside the out dcache\n", t, out[e].chunk, out[e].sz );
+        abort();
+      }
+      if( a == s1 ) { s1 = b; continue; }
+    }
+    if( s0 >= 0 && s1 > s0 ) {
+      SV_CHECK( hipMemcpyAsync( T.h_out + s0, T.d_mirror + s0, (ulong)(s1 - s0), hipMemcpyDeviceToHost, T.st ) );
+      s->stat[5] += (ulong)(s1 - s0); s->stat[6]++;
+    }
+    s0 = a; s1 = b;
+  }
+  SV_CHECK( hipEventRecord( T.ev[T.flush_take % SVC_FLUSH_Q], T.st ) );
+  s->stat[3]++; s->stat[4] += m;
+}
+
+extern "C" int
+fd_verify_svc_poll( fd_verify_svc_t * s ) {
+  fd_verify_svc_seg_t * g = s->seg;
+  int did = 0;
+  SV_CHECK( hipSetDevice( s->dev ) );
+  g->svc_heartbeat++;
+  /* 1. finished launches: their slots' results are in the segment */
+  ulong busy = 0;
+  for( ulong k = 0; k < s->inflight; k++ ) {
+    svc_launch & L = s->L[k];
+    if( !L.busy ) continue;
+    hipError_t e = hipEventQuery( L.ev1 );
+    if( e == hipErrorNotReady ) { busy++; continue; }
+    SV_CHECK( e );
+    float ms = 0.f;
+    SV_CHECK( hipEventElapsedTime( &ms, L.ev0, L.ev1 ) );
+    s->stat[7] += (ulong)((double)ms * 1e6);
+    for( ulong r = 0; r < L.nreq; r++ ) {
+      fd_verify_svc_req_t * q = fd_verify_svc_req( g, L.req[r].t, L.req[r].slot );
+      q->batch_frags = L.n;
+      fd_verify_svc_st( &q->state, FD_VERIFY_SVC_RESULTS );
+    }
+    L.busy = 0; did = 1;
+  }
+  /* 2. flushes: retire in order, start the newly posted */
+  for( ulong t = 0; t < g->tile_cnt; t++ ) {
+    svc_tile & T = s->tile[t];
+    fd_verify_svc_tile_t * b = fd_verify_svc_tile( g, t );
+    while( T.flush_fin < T.flush_take ) {
+      hipError_t e = hipEventQuery( T.ev[T.flush_fin % SVC_FLUSH_Q] );
+      if( e == hipErrorNotReady ) break;
+      SV_CHECK( e );
+      T.flush_fin++; did = 1;
+      fd_verify_svc_st( &b->flush_done, T.flush_fin );
+    }
+    ulong post = fd_verify_svc_ld( &b->flush_post );
+    while( T.flush_take < post && T.flush_take - T.flush_fin < SVC_FLUSH_Q ) {
+      svc_flush_start( s, t, &b->flush[T.flush_take % FD_VERIFY_SVC_FLUSH_DEPTH] );
+      T.flush_take++; did = 1;
+    }
+  }
+  /* 3. posted requests, in each tile's ring order */
+  long const now = svc_now_ns();
+  for( ulong t = 0; t < g->tile_cnt; t++ ) {
+    svc_tile & T = s->tile[t];
+    while( s->pend_tail - s->pend_head < s->pend_cap ) {
+      ulong slot = T.take & (g->req_depth - 1ul);
+      fd_verify_svc_req_t * q = fd_verify_svc_req( g, t, slot );
+      if( fd_verify_svc_ld( &q->state ) != FD_VERIFY_SVC_POSTED ) break;
+      if( q->id != T.take ) {
+        fprintf( stderr, "fd_verify_svc: tile %lu posted request %lu in slot %lu, expected %lu\n", t, q->id, slot, T.take );
+        abort();
+      }
+      T.take++; did = 1;
+      if( !q->n ) {                                          /* nothing to verify: results at once */
+        q->batch_frags = 0; fd_verify_svc_st( &q->state, FD_VERIFY_SVC_RESULTS );
+        continue;
+      }
+      svc_pend & p = s->pend[s->pend_tail % s->pend_cap];
+      p.t = t; p.slot = slot; p.n = q->n; p.seen = now;
+      s->pend_tail++; s->pend_frags += q->n;
+    }
+  }
+  /* 4. a launch: when the posted frags fill its merge target, or the GPU
+     would otherwise idle, or the oldest has waited merge_wait_ns */
+  while( s->pend_head != s->pend_tail && busy < s->inflight ) {
+    bool ready = s->pend_frags >= s->merge_min || !busy || now - s->pend[s->pend_head % s->pend_cap].seen >= s->merge_wait_ns;
+    if( !ready ) break;
+    ulong k = 0;
+    while( s->L[k].busy ) k++;
+    svc_launch_start( s, s->L[k] );
+    busy++; did = 1;
+  }
+  return did;
+}
+
+extern "C" void
+fd_verify_svc_stats( fd_verify_svc_t const * s, ulong out[8] ) {
+  for( int k = 0; k < 8; k++ ) out[k] = s->stat[k];
+}
+
+extern "C" void
+fd_verify_svc_delete( fd_verify_svc_t * s ) {
+  if( !s ) return;
+  (void)hipSetDevice( s->dev );
+  (void)hipDeviceSynchronize();
+  for( ulong k = 0; k < SVC_LAUNCH_MAX; k++ ) launch_free( s->L[k] );
+  for( ulong t = 0; t < FD_VERIFY_SVC_TILE_MAX; t++ ) {
+    svc_tile & T = s->tile[t];
+    if( !T.set ) continue;
+    (void)hipStreamDestroy( T.st );
+    for( ulong k = 0; k < SVC_FLUSH_Q; k++ ) (void)hipEventDestroy( T.ev[k] );
+    (void)hipFree( T.d_mirror );
+  }
+  (void)hipFree( s->d_stage );
+  for( ulong k = 0; k < s->nreg; k++ ) (void)hipHostUnregister( s->reg[k].h );
+  fd_verify_svc_st( &s->seg->svc_state, FD_VERIFY_SVC_SVC_STOPPED );
+  free( s->pend );
+  free( s );
+}

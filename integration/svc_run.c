@@ -1,0 +1,88 @@
+/* svc_run.c -- the GPU tile of the service-mode verify stage run
+   (integration/svc_tile_run.c, integration/svc_run.h): one process that
+   owns the HIP context and serves every verify tile of the run through the
+   segment of include/fd_verify_svc.h.
+
+     svc_run <shm> <gpu>
+
+   Maps the run's shared file, registers it for the GPU once (every link's
+   mcache and dcache, the tiles' verify_dedup dcaches and the segment lie
+   in it), names the quic_verify links (service link l = link kind_id l)
+   and the tiles' out dcaches, then polls until the producer sets shutdown.
+   Environment: SVC_BATCH_MAX (frags per merged launch, default 131072),
+   SVC_INFLIGHT (launches at once, default 4), SVC_MERGE_MIN (frags that
+   start a launch at once, default batch_max / 2), SVC_MERGE_WAIT_NS
+   (default 100000).
+
+   The integration's GPU tile (integration/fd_verify_gpu_tile.c) does the
+   same from the topology's objects. */
+
+#include "../../tango/mcache/fd_mcache.h"
+#include "../../tango/dcache/fd_dcache.h"
+#include "../quic/fd_tpu.h"
+#include "fd_verify_svc.h"
+#include "svc_run.h"
+#include <errno.h>
+#include <fcntl.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <sys/mman.h>
+#include <unistd.h>
+
+#if defined(fd_boot)
+void fd_boot( int * pargc, char *** pargv ) { (void)pargc; (void)pargv; }
+void fd_halt( void ) {}
+#endif
+
+static ulong env_ulong( char const * k, ulong def ) { char const * v = getenv( k ); return v ? strtoul( v, NULL, 0 ) : def; }
+
+int
+main( int argc, char ** argv ) {
+  fd_boot( &argc, &argv );
+  if( argc<3 ) { fprintf( stderr, "usage: %s <shm> <gpu>\n", argv[0] ); return 2; }
+  int fd = open( argv[1], O_RDWR );
+  if( fd<0 ) FD_LOG_ERR(( "open(%s) failed (%i-%s)", argv[1], errno, fd_io_strerror( errno ) ));
+  svc_run_hdr_t h;
+  if( pread( fd, &h, sizeof(h), 0 )!=(long)sizeof(h) || h.magic!=SVC_RUN_MAGIC ) FD_LOG_ERR(( "%s: not a svc_run segment", argv[1] ));
+  uchar * base = mmap( NULL, h.map_sz, PROT_READ|PROT_WRITE, MAP_SHARED, fd, 0 );
+  if( base==MAP_FAILED ) FD_LOG_ERR(( "mmap failed (%i-%s)", errno, fd_io_strerror( errno ) ));
+  close( fd );
+  svc_run_hdr_t * hdr = (svc_run_hdr_t *)base;
+
+  ulong batch_max = env_ulong( "SVC_BATCH_MAX", 131072UL );
+  ulong inflight  = env_ulong( "SVC_INFLIGHT", 4UL );
+  fd_verify_svc_t * svc = fd_verify_svc_boot( base + hdr->svc_off, (int)strtol( argv[2], NULL, 0 ), batch_max, inflight );
+  if( !svc ) FD_LOG_ERR(( "fd_verify_svc_boot failed (batch_max %lu, inflight %lu)", batch_max, inflight ));
+  fd_verify_svc_set_merge( svc, env_ulong( "SVC_MERGE_MIN", batch_max/2UL ), env_ulong( "SVC_MERGE_WAIT_NS", 100000UL ) );
+  if( fd_verify_svc_map( svc, base, hdr->map_sz ) ) FD_LOG_ERR(( "registering %lu B for the GPU failed", hdr->map_sz ));
+  for( ulong l=0UL; l<hdr->link_cnt; l++ ) {
+    fd_frag_meta_t const * mcache = fd_mcache_join( base + hdr->mcache_off[ l ] );
+    uchar const *          dcache = fd_dcache_join( base + hdr->dcache_off[ l ] );
+    if( !mcache || !dcache ) FD_LOG_ERR(( "link %lu: join failed", l ));
+    /* during_frag's range, from the link's mtu as the tile sees it (svc_tile_run.c: FD_TPU_REASM_MTU) */
+    if( fd_verify_svc_set_link( svc, l, mcache, fd_mcache_depth( mcache ), base, fd_dcache_compact_chunk0( base, dcache ),
+                                fd_dcache_compact_wmark( base, dcache, FD_TPU_REASM_MTU ) ) )
+      FD_LOG_ERR(( "fd_verify_svc_set_link %lu failed", l ));
+  }
+  for( ulong t=0UL; t<hdr->tile_cnt; t++ ) {
+    uchar * dcache = fd_dcache_join( base + hdr->out_dcache_off[ t ] );
+    if( !dcache || fd_verify_svc_set_tile( svc, t, dcache, fd_dcache_data_sz( dcache ), base ) )
+      FD_LOG_ERR(( "fd_verify_svc_set_tile %lu failed", t ));
+  }
+  if( fd_verify_svc_run( svc ) ) FD_LOG_ERR(( "fd_verify_svc_run failed" ));
+  FD_COMPILER_MFENCE();
+  hdr->svc_ready = 1UL;
+  long deadline = fd_log_wallclock() + 1200L*1000000000L;
+  for( ulong it=0UL; !hdr->shutdown; it++ ) {
+    if( !fd_verify_svc_poll( svc ) ) FD_SPIN_PAUSE();
+    if( !( it & 0xffffUL ) && fd_log_wallclock()>deadline ) FD_LOG_ERR(( "service: no shutdown after 1200 s" ));
+  }
+  ulong st[ 8 ];
+  fd_verify_svc_stats( svc, st );
+  for( ulong k=0UL; k<8UL; k++ ) hdr->svc_stats[ k ] = st[ k ];
+  fd_verify_svc_delete( svc );
+  FD_COMPILER_MFENCE();
+  hdr->svc_done = 1UL;
+  munmap( base, h.map_sz );
+  return 0;
+}

@@ -1,0 +1,153 @@
+#!/usr/bin/env python3
+"""Run and time the verify stage in service mode (north star's operating
+point): the reference's verify tiles patched with
+integration/fd_verify_tile_svc.patch (no HIP in the tile processes) served
+by one GPU tile (integration/svc_run.c, fd_verify_svc_* in the engine),
+between a quic_verify producer and one reliable verify_dedup consumer per
+tile (integration/svc_tile_run.c).
+
+Per run: one producer, one GPU-tile process, T tile processes and T
+consumer processes, all on one shared file in /dev/shm.
+
+value = signatures the GPU verified for the tiles / (last tile done - first
+frag published).  Also: frags/s, outcome counts, per-frag latency (tspub -
+tsorig) percentiles, overruns, the service's launch statistics, each
+tile's thread count and device fds after privileged_init, and each tile's
+published-payload digest (the reference tile's run gives the same digest,
+tests/test_gpu_svc_run.py).
+
+usage: python tools/svc_bench.py [--frags N] [--tiles 1,2] [--repeat R] [--rate R,...] [--in-depth D]
+       [--gpu-env KEY=VAL,...]
+Prints one JSON line per run and a final summary line."""
+import argparse
+import json
+import os
+import subprocess
+import sys
+import tempfile
+import time
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+sys.path.insert(0, os.path.join(REPO, "tests"))
+sys.path.insert(0, os.path.join(REPO, "tools"))
+BUILD = os.path.join(REPO, "integration", "_build")
+EXE = os.path.join(BUILD, "svc_tile_run")
+SVC = os.path.join(BUILD, "svc_run")
+
+
+def run_one(stream, tiles, in_depth, timeout, logdir, env=None, svc_env=None, svc_exe=None, gpu=0):
+    """One producer, the GPU tile, `tiles` tile processes and `tiles`
+    consumers.  env: the SVC_RUN_* settings (every process); svc_env: the
+    GPU tile's (SVC_BATCH_MAX, SVC_INFLIGHT, ...).  Liveness is checked every
+    0.2 s: a process that dies ends the run at once."""
+    shm = f"/dev/shm/fd_svc_bench_{os.getpid()}"
+    if os.path.exists(shm):
+        os.unlink(shm)
+    os.makedirs(logdir, exist_ok=True)
+    e = dict(os.environ)
+    e.update(env or {})
+    errs, procs = [], []
+
+    def spawn(cmd, name, extra=None):
+        f = open(os.path.join(logdir, name + ".err"), "w")
+        errs.append(f)
+        ee = dict(e)
+        ee.update(extra or {})
+        p = subprocess.Popen(cmd, stdout=subprocess.DEVNULL, stderr=f, env=ee)
+        procs.append((name, p))
+        return p
+
+    perr = open(os.path.join(logdir, "producer.err"), "w")
+    errs.append(perr)
+    prod = subprocess.Popen([EXE, "produce", shm, stream, str(tiles), str(in_depth)], stdout=subprocess.PIPE,
+                            stderr=perr, text=True, env=e)
+    t0 = time.time()
+    try:
+        line = prod.stdout.readline()
+        if line.strip() != "READY":
+            raise RuntimeError(f"producer: {line!r} (see {logdir}/producer.err)")
+        spawn([svc_exe or SVC, shm, str(gpu)], "svc", svc_env)
+        for t in range(tiles):
+            spawn([EXE, "consume", shm, str(t)], f"cons{t}")
+            spawn([EXE, "tile", shm, str(t)], f"tile{t}")
+        last = 0.0
+        while prod.poll() is None:
+            dead = [(n, p.returncode) for n, p in procs if p.poll() is not None and p.returncode]
+            if dead:
+                raise RuntimeError(f"died: {dead} (see {logdir}/*.err)")
+            if time.time() - t0 > timeout:
+                raise RuntimeError(f"timeout after {timeout} s")
+            if time.time() - last >= 10.0:
+                print(f"  run: {time.time() - t0:.0f} s", file=sys.stderr, flush=True)
+                last = time.time()
+            time.sleep(0.2)
+        out = prod.stdout.read()
+        if prod.returncode:
+            raise RuntimeError(f"producer rc {prod.returncode} (see {logdir}/producer.err)")
+        for n, p in procs:
+            p.wait(timeout=60)
+            if p.returncode:
+                raise RuntimeError(f"{n} rc {p.returncode} (see {logdir}/{n}.err)")
+        return json.loads(out.strip().splitlines()[-1])
+    finally:
+        for _, p in procs + [("producer", prod)]:
+            if p.poll() is None:
+                p.kill()
+                p.wait()
+        for f in errs:
+            f.close()
+        if os.path.exists(shm):
+            os.unlink(shm)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--frags", type=int, default=1 << 21)
+    ap.add_argument("--tiles", default="2")
+    ap.add_argument("--repeat", type=int, default=1)
+    ap.add_argument("--in-depth", type=int, default=0,
+                    help="quic_verify depth (0: the stream's frag count rounded up, with --prelay)")
+    ap.add_argument("--prelay", action="store_true")
+    ap.add_argument("--rate", default="0", help="offered rates in frags/s, no flow control (0: flow-controlled)")
+    ap.add_argument("--env", default="", help="KEY=VAL,... for every process (SVC_RUN_*)")
+    ap.add_argument("--svc-env", default="", help="KEY=VAL,... for the GPU tile (SVC_BATCH_MAX, SVC_INFLIGHT, ...)")
+    ap.add_argument("--timeout", type=float, default=300)
+    ap.add_argument("--logdir", default=os.path.join(REPO, "gpurun_out", "svc_bench_logs"))
+    args = ap.parse_args()
+    import tile_bench as TB
+
+    def kv(s):
+        return dict(x.split("=", 1) for x in s.split(",") if x)
+    with tempfile.TemporaryDirectory() as td:
+        stream = os.path.join(td, "stream.bin")
+        t = time.time()
+        s = TB.make_stream(args.frags, stream)
+        print(f"stream: {s.n} frags, {s.n_records} signatures, {time.time() - t:.1f} s", file=sys.stderr, flush=True)
+        best = None
+        for rate in (int(x) for x in args.rate.split(",")):
+            for tiles in (int(x) for x in args.tiles.split(",")):
+                depth = args.in_depth or (1 << (s.n - 1).bit_length())
+                env = kv(args.env)
+                if args.prelay:
+                    env["SVC_RUN_PRELAY"] = "1"
+                    depth = max(depth, 1 << (s.n - 1).bit_length())
+                if rate:
+                    env["SVC_RUN_RATE"] = str(rate)
+                for r in range(args.repeat):
+                    res = run_one(stream, tiles, depth, args.timeout, os.path.join(args.logdir, f"t{tiles}_r{rate}_{r}"),
+                                  env=env, svc_env=kv(args.svc_env))
+                    res["rep"] = r
+                    print(json.dumps(res), flush=True)
+                    if res.get("overrun") or res.get("lapped"):
+                        continue
+                    if best is None or res["verifies_per_s"] > best["verifies_per_s"]:
+                        best = res
+        if best:
+            print(json.dumps({"metric": "ed25519 verifies/sec through the service-mode verify stage (one GPU)",
+                              "value": best["verifies_per_s"], "tiles": best["tile_cnt"], "frags": best["frags"],
+                              "sigs": best["sigs"], "latency": best["latency"]}))
+
+
+if __name__ == "__main__":
+    main()
