@@ -240,6 +240,7 @@ DEVI u32 txn_parse( P const & p, u32 sz, u8 * out, txn_span & sp ) {
 struct __attribute__((packed)) tile_res { u64 tag; u64 bid; u16 tsz; signed char tcode; u8 kind; u32 pad; };
 static_assert( sizeof(tile_res) == 24, "tile_res layout" );
 #define TILE_RES_HDR 32ul   /* u32 record count, u32 flag, u64 pad, u64 ingest bytes read, written */
+#define TILE_RES_BAD 0x40u  /* or'd into tile_res.kind: the frag itself is corrupt (known per frag with out staging) */
 
 /* per-frag SoA scratch written by k_txn_parse */
 struct parse_out {
@@ -1388,6 +1389,7 @@ void k_tile_results( ulong n, u16 const * __restrict__ tsz, signed char const * 
   if( j >= n ) return;
   tile_res r;
   r.tag = tag[j]; r.bid = bid ? bid[j] : 0ul; r.tsz = tsz[j]; r.tcode = tcode[j]; r.kind = kind ? kind[j] : 0u;
+  if( fdesc && ((fdesc[j] >> 34) & 1u) ) r.kind |= (u8)TILE_RES_BAD;   /* this frag is corrupt (out staging) */
   /* frag mode: the out header's payload_sz (after the GPU's own during_frag),
      for the caller's fd_txn_m_realized_footprint */
   r.pad = fdesc ? (u32)((fdesc[j] >> 12) & 0x7ffu)
@@ -1716,8 +1718,15 @@ tile_complete( fd_verify_hip_tile_t * t, ulong const * bundle_id, uchar const * 
   tile_res const * R = (tile_res const *)(s.h_res + TILE_RES_HDR);
   int skipped = 0;
   if( skip ) for( ulong j = 0; j < s.n; j++ ) skipped |= !!skip[j];
-  if( s.frags && s.n && hdr[1] && !skipped ) {
-    /* during_frag's FD_LOG_ERR (fd_verify_tile.c:75-85): a corrupt frag kills the tile */
+  /* during_frag's FD_LOG_ERR (fd_verify_tile.c:75-85): a corrupt frag kills
+     the tile.  With frags skipped as overruns the flag may be theirs: the
+     per-frag bit (out staging) still finds a corrupt frag that was not
+     skipped; without staging only the batch flag exists and a skipped
+     frag's corruption cannot be told from another's */
+  bool corrupt = s.frags && s.n && hdr[1] && !skipped;
+  if( s.frags && s.n && hdr[1] && skipped )
+    for( ulong j = 0; j < s.n; j++ ) corrupt |= !skip[j] && (R[j].kind & TILE_RES_BAD);
+  if( corrupt ) {
     fprintf( stderr, "fd_verify_hip: corrupt frag in batch (size beyond FD_TPU_RAW_MTU / 2048 or payload_sz "
                      "beyond FD_TPU_MTU)\n" );
     abort();
@@ -1744,7 +1753,7 @@ tile_complete( fd_verify_hip_tile_t * t, ulong const * bundle_id, uchar const * 
       continue;
     }
     if( s.frags ) {                                          /* after_frag's first statement (:112) */
-      u32 k = R[j].kind & ~FD_VERIFY_HIP_IN_HOSTCOPY;
+      u32 k = R[j].kind & ~(FD_VERIFY_HIP_IN_HOSTCOPY | TILE_RES_BAD);
       t->m_gossip += (k == FD_VERIFY_HIP_IN_GOSSIP) | (k == FD_VERIFY_HIP_IN_SEND);
     }
     if( j + PF < n ) {
@@ -1831,6 +1840,12 @@ fd_verify_hip_tile_set_cu_mask( fd_verify_hip_tile_t * t, uint const * mask, uin
     bool seen = false;                                       /* slots sharing the tile's context: once */
     for( ulong k = 0; k < j; k++ ) seen |= t->slot[k].ctx == c;
     if( !seen && fd_ed25519_hip_ctx_set_cu_mask( c, mask, words ) ) return -1;
+    /* the slot's out-flush stream runs on the same CUs */
+    tile_slot & s = t->slot[j];
+    TX_CHECK( hipStreamSynchronize( s.st_flush ) );
+    TX_CHECK( hipStreamDestroy( s.st_flush ) );
+    if( words ) { if( hipExtStreamCreateWithCUMask( &s.st_flush, words, mask ) != hipSuccess ) return -1; }
+    else        TX_CHECK( hipStreamCreateWithFlags( &s.st_flush, hipStreamNonBlocking ) );
   }
   return 0;
 }
@@ -1991,8 +2006,14 @@ extern "C" int
 fd_replay_hip_txn_verify_host( fd_replay_hip_t * r, ulong n, uchar const * h_pool, ulong pool_sz,
                                fd_txn_hip_desc_t const * h_desc, int * h_result, void * stream ) {
   if( n > r->max_txn || pool_sz > r->hpool_cap ) return -1;
-  for( ulong j=0; j<n; j++ )          /* every span inside the staged pool (k_desc_spans trusts them) */
-    if( (ulong)h_desc[j].payload_off + h_desc[j].payload_sz > pool_sz ) return -1;
+  for( ulong j=0; j<n; j++ ) {        /* every span inside the staged pool (k_desc_spans trusts them) */
+    fd_txn_hip_desc_t const * d = h_desc + j;
+    if( (ulong)d->payload_off + d->payload_sz > pool_sz ) return -1;
+    ulong c = d->signature_cnt;
+    if( c >= 1ul && c <= 16ul &&        /* the records read: signatures, pubkeys, the message (cnt 0 or > 16 read nothing) */
+        ( (ulong)d->signature_off + 64ul*c > d->payload_sz || (ulong)d->acct_addr_off + 32ul*c > d->payload_sz ||
+          (ulong)d->message_off > d->payload_sz ) ) return -1;
+  }
   if( !n ) return 0;
   hipStream_t st = stream ? (hipStream_t)stream : (hipStream_t)fd_ed25519_hip_ctx_stream( r->ctx );
   TX_CHECK( hipSetDevice( fd_ed25519_hip_ctx_device( r->ctx ) ) );

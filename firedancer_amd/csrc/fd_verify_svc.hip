@@ -525,6 +525,7 @@ fd_verify_svc_poll( fd_verify_svc_t * s ) {
       ulong slot = T.take & (g->req_depth - 1ul);
       fd_verify_svc_req_t * q = fd_verify_svc_req( g, t, slot );
       if( fd_verify_svc_ld( &q->state ) != FD_VERIFY_SVC_POSTED ) break;
+      if( q->id + g->req_depth == T.take ) break;            /* the slot's previous request, still on the GPU */
       if( q->id != T.take ) {
         fprintf( stderr, "fd_verify_svc: tile %lu posted request %lu in slot %lu, expected %lu\n", t, q->id, slot, T.take );
         abort();

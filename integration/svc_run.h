@@ -29,6 +29,7 @@ typedef struct {
   volatile ulong link_consumed, link_filtered, link_ovr_poll, link_ovr_poll_frags, link_ovr_read, link_ovr_read_frags;
   volatile ulong metrics_ok;                   /* the link-in metric slots hold the tile's counts */
   volatile ulong threads, dev_fds;             /* after privileged_init: /proc/self/task entries, /dev/kfd|dri fds */
+  volatile ulong sandboxed;                    /* the tile ran inside fd_sandbox_enter (SVC_RUN_SANDBOX) */
 } svc_run_tile_res_t;
 
 typedef struct {

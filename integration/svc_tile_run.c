@@ -60,6 +60,7 @@ static int drv_should_shutdown( void * ctx );
 #include "../../tango/tempo/fd_tempo.h"
 #include "../../util/pod/fd_pod_format.h"
 #include "../quic/fd_tpu.h"
+#include "../../util/sandbox/fd_sandbox.h"
 #include "svc_run.h"
 #include <dirent.h>
 #include <errno.h>
@@ -309,11 +310,11 @@ produce( char const * path, char const * stream, ulong tile_cnt, ulong in_depth 
     for( ulong k=0UL; k<SVC_RUN_LAT_B; k++ ) { lat[ k ] += c->lat[ k ]; latq[ k ] += c->lat_q[ k ]; }
     printf( "%s{\"frags\": %lu, \"sigs\": %lu, \"published\": %lu, \"parse_fail\": %lu, \"verify_fail\": %lu, "
             "\"dedup\": %lu, \"bundle_peer_fail\": %lu, \"overrun\": %lu, \"lapped\": %lu, \"s\": %.6f, "
-            "\"consumed\": %lu, \"digest\": \"%016lx\", \"threads\": %lu, \"dev_fds\": %lu, \"metrics_ok\": %lu, "
+            "\"consumed\": %lu, \"digest\": \"%016lx\", \"threads\": %lu, \"dev_fds\": %lu, \"metrics_ok\": %lu, \"sandboxed\": %lu, "
             "\"link\": {\"consumed\": %lu, \"filtered\": %lu, \"overrun_polling\": %lu, \"overrun_polling_frags\": %lu, "
             "\"overrun_reading\": %lu, \"overrun_reading_frags\": %lu}}",
             t ? ", " : "", r->frags, r->sigs, r->pub, r->parse, r->verify, r->dedup, r->bundle, r->overrun, r->lapped,
-            (double)( r->t_end - t0 )*1e-9, c->frags, c->digest, r->threads, r->dev_fds, r->metrics_ok,
+            (double)( r->t_end - t0 )*1e-9, c->frags, c->digest, r->threads, r->dev_fds, r->metrics_ok, r->sandboxed,
             r->link_consumed, r->link_filtered, r->link_ovr_poll, r->link_ovr_poll_frags, r->link_ovr_read,
             r->link_ovr_read_frags );
   }
@@ -459,19 +460,8 @@ tile( char const * path, ulong t ) {
   FD_TEST( fd_pod_insert_ulong( topo->props, "verify_svc.gpu_cnt", 1UL ) );
   FD_TEST( fd_pod_insertf_ulong( topo->props, svc->id, "verify_svc.%lu", 0UL ) );
 
-  privileged_init( topo, tile );
-  drv_res = &hdr->tile[ t ];
-  { ulong th, fds; drv_process_census( &th, &fds ); drv_res->threads = th; drv_res->dev_fds = fds; }
-  fd_verify_ctx_t * ctx = (fd_verify_ctx_t *)scratch;
-  ctx->hashmap_seed = hdr->seed + t;                            /* fixed per tile: runs are reproducible */
-  unprivileged_init( topo, tile );
-  ctx->round_robin_cnt = hdr->tile_cnt; ctx->round_robin_idx = t;
-  drv_share = 0UL;                                              /* seq % T of every link */
-  for( ulong l=0UL; l<L; l++ ) {
-    ulong nl = ( hdr->n + L - 1UL - l )/L;
-    drv_share += nl/hdr->tile_cnt + ( t<nl%hdr->tile_cnt ? 1UL : 0UL );
-  }
-
+  /* everything the run loop uses, allocated before the sandbox (which
+     leaves no address space to map) */
   ulong * metrics = aligned_alloc( FD_METRICS_ALIGN, fd_ulong_align_up( FD_METRICS_FOOTPRINT( L, 1UL ), FD_METRICS_ALIGN ) );
   fd_metrics_register( fd_metrics_new( metrics, L, 1UL ) );
   ulong polled_cnt = polled ? L : 0UL;
@@ -486,6 +476,44 @@ tile( char const * path, ulong t ) {
   ulong                  cons_out[ 1 ] = { 0UL };
   ulong *                cons_fseqs[ 1 ] = { fd_fseq_join( base + hdr->cons_fseq_off[ t ] ) };
   (void)fd_tempo_tick_per_ns( NULL );                           /* calibrate before the clock starts */
+
+  privileged_init( topo, tile );
+  drv_res = &hdr->tile[ t ];
+  { ulong th, fds; drv_process_census( &th, &fds ); drv_res->threads = th; drv_res->dev_fds = fds; }
+  fd_verify_ctx_t * ctx = (fd_verify_ctx_t *)scratch;
+  ctx->hashmap_seed = hdr->seed + t;                            /* fixed per tile: runs are reproducible */
+
+  /* SVC_RUN_SANDBOX=1: the reference's sandbox, entered where
+     fd_topo_run_tile enters it (src/disco/topo/fd_topo_run.c:86-135: after
+     privileged_init, with the tile's own populate_allowed_fds and
+     populate_allowed_seccomp -- the reference's policy, write and fsync
+     only): a user namespace, pivot_root, landlock, rlimits, no
+     capabilities, seccomp.  The process keeps only stderr (fdctl's boot
+     closes the rest; here the driver does).  The loop's exit is not in the
+     policy: the tile dies of SIGSYS after reporting, as a reference tile
+     never returns. */
+  drv_res->sandboxed = 0UL;
+  if( getenv( "SVC_RUN_SANDBOX" ) ) {
+    int   fds[ 256 ];
+    ulong fd_cnt = populate_allowed_fds( topo, tile, 256UL, fds );
+    struct sock_filter filter[ 256 ];
+    ulong filter_cnt = populate_allowed_seccomp( topo, tile, 256UL, filter );
+    for( int f=0; f<1024; f++ ) {
+      int keep = 0;
+      for( ulong k=0UL; k<fd_cnt; k++ ) keep |= fds[ k ]==f;
+      if( !keep ) close( f );
+    }
+    fd_sandbox_enter( (uint)getuid(), (uint)getgid(), 0, 0, 0, 1, 0, 0UL, 0UL, 0UL, fd_cnt, fds, filter_cnt, filter );
+    drv_res->sandboxed = 1UL;
+  }
+
+  unprivileged_init( topo, tile );
+  ctx->round_robin_cnt = hdr->tile_cnt; ctx->round_robin_idx = t;
+  drv_share = 0UL;                                              /* seq % T of every link */
+  for( ulong l=0UL; l<L; l++ ) {
+    ulong nl = ( hdr->n + L - 1UL - l )/L;
+    drv_share += nl/hdr->tile_cnt + ( t<nl%hdr->tile_cnt ? 1UL : 0UL );
+  }
 
   __atomic_fetch_add( &hdr->tiles_ready, 1UL, __ATOMIC_SEQ_CST );
   while( !hdr->start ) FD_SPIN_PAUSE();

@@ -112,3 +112,21 @@ def test_unreliable_producer_overruns_are_dropped(tmp_path, verifier):
     assert r["overrun"] + r["lapped"] > 0, r
     assert r["frags"] + r["overrun"] + r["lapped"] == s.n
     assert r["consumer_bad"] == 0 and r["tile_threads_max"] == 1 and r["metrics_ok"] == 1
+
+
+def test_sandboxed_tiles_with_the_gpu_tile(stream, tmp_path):
+    """the tiles inside the reference's fd_sandbox_enter (user namespace,
+    pivot_root, landlock, the reference's seccomp policy) while the GPU tile
+    serves them; skipped where user namespaces are refused"""
+    import subprocess
+    if subprocess.run(["unshare", "-U", "true"], capture_output=True).returncode:
+        pytest.skip("user namespaces refused on this box")
+    r = S.run(stream["path"], 2, 1 << 14, str(tmp_path / "run"), env=dict(SMALL, SVC_RUN_SANDBOX="1"))
+    _check(r, stream["s"].n)
+    assert all(x["sandboxed"] == 1 for x in r["tiles"])
+    for t in range(2):
+        p = str(tmp_path / f"share{t}.bin")
+        S.share_stream(p, stream["s"], stream["bid"], t, 2, SEED, DEPTH)
+        run_driver("ref", p, str(tmp_path / f"ref{t}.bin"))
+        assert S.tile_counts(r["tiles"][t]) == S.reference_digest(read_fdo1(str(tmp_path / f"ref{t}.bin"), DEPTH)), t
+

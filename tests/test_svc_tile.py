@@ -147,3 +147,23 @@ def test_svc_patch_compiles_strict():
     """the patched tile and svc_tile_run.c under -Wall -Wextra -Werror
     (integration/Makefile svc_tile_strict.o)"""
     assert os.path.exists(os.path.join(S.BUILD, "svc_tile_strict.o"))
+
+
+def test_tiles_run_inside_the_reference_sandbox(stream, tmp_path):
+    """SVC_RUN_SANDBOX=1: each tile enters the reference's fd_sandbox_enter
+    after privileged_init (src/disco/topo/fd_topo_run.c:86-135) with its own
+    populate_allowed_fds / populate_allowed_seccomp -- the reference's
+    verify policy (write and fsync only), a user namespace, pivot_root,
+    landlock, rlimits -- and still gives the reference's sequence.  Skipped
+    where the container refuses user namespaces."""
+    if subprocess.run(["unshare", "-U", "true"], capture_output=True).returncode:
+        pytest.skip("user namespaces refused here")
+    r = S.run(stream["path"], 2, 1 << 14, str(tmp_path / "run"), env=dict(SMALL, SVC_RUN_SANDBOX="1"), mock=True)
+    _check_run(r, stream["s"].n)
+    assert all(x["sandboxed"] == 1 for x in r["tiles"])
+    for t in range(2):
+        p = str(tmp_path / f"share{t}.bin")
+        S.share_stream(p, stream["s"], stream["bid"], t, 2, SEED, DEPTH)
+        run_driver("ref", p, str(tmp_path / f"ref{t}.bin"))
+        assert S.tile_counts(r["tiles"][t]) == S.reference_digest(read_fdo1(str(tmp_path / f"ref{t}.bin"), DEPTH)), t
+
