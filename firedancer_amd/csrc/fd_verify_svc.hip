@@ -459,7 +459,7 @@ svc_flush_start( fd_verify_svc_t * s, ulong t, fd_verify_svc_flush_t const * f )
     long a = -1, b = -1;
     if( e < m && !(out[e].flags & FD_VERIFY_SVC_OUT_HOSTWRITTEN) ) {
       a = (long)(64ul * (ulong)out[e].chunk) + delta;
-      b = a + (long)(((ulong)out[e].sz + 63ul) & ~63ul);
+      b = a + (long)(((ulong)out[e].sz + 127ul) & ~127ul);  /* fd_dcache_compact_next advances by chunk pairs */
       if( a < 0 || b > (long)T.out_sz ) {
         fprintf( stderr, "fd_verify_svc: tile %lu: out chunk %u (+%u) outside the out dcache\n", t, out[e].chunk, out[e].sz );
         abort();

@@ -1,0 +1,150 @@
+/* fd_verify_gpu_tile.c -- the GPU tile of the service-mode verify stage, for
+   the reference's topology.  It goes in the reference tree as
+   src/disco/verify/fd_verify_gpu_tile.c (config/extra/with-hip.mk adds it to
+   the build with FD_HAS_HIP_SVC; integration/fd_verify_topo_hip.patch adds
+   the tiles, the verify_svc objects and the registrations).
+
+   One "vgpu" tile per GPU (kind_id = the HIP device).  It owns the GPU's
+   HIP context -- the only multithreaded tile, so the only one the sandbox
+   cannot take (fd_sandbox_enter's unshare( CLONE_NEWUSER ) refuses a
+   threaded process, src/util/sandbox/fd_sandbox.c:649; the topology patch
+   runs it unsandboxed, as Frankendancer runs Agave) -- and serves the verify
+   tiles with kind_id % gpu_cnt == kind_id through its verify_svc object
+   (include/fd_verify_svc.h): every quic_verify link's mcache and dcache and
+   its tiles' verify_dedup dcaches are registered for the GPU in
+   privileged_init, then the stem loop calls fd_verify_svc_poll from
+   after_credit.  The verify tiles stay the reference's single-threaded,
+   sandboxed processes (integration/fd_verify_tile_svc.patch).
+
+   The same steps, on a run's shared file instead of the topology's
+   workspaces, are integration/svc_run.c (what the tests and the bench run).
+
+   Properties (topo->props, set by the topology patch):
+     verify_svc.gpu_cnt            GPU tiles (verify tile kind_id % gpu_cnt picks one)
+     verify_svc.<g>                obj id of GPU g's segment
+     obj.<id>.{tile_cnt,req_depth,slot_cap,frag_cap}   the segment's shape
+     verify_svc.batch_max, verify_svc.inflight         launch size and count */
+
+#include "../topo/fd_topo.h"
+#include "../../util/pod/fd_pod_format.h"
+#include "../../tango/mcache/fd_mcache.h"
+#include "../../tango/dcache/fd_dcache.h"
+#include "fd_verify_svc.h"
+
+#define VAL(name) (__extension__({                                                             \
+  ulong __x = fd_pod_queryf_ulong( topo->props, ULONG_MAX, "obj.%lu.%s", obj->id, name );      \
+  if( FD_UNLIKELY( __x==ULONG_MAX ) ) FD_LOG_ERR(( "obj.%lu.%s was not set", obj->id, name )); \
+  __x; }))
+
+/* ---- the verify_svc object (fd_topo_obj_callbacks_t, as src/app/shared/fd_obj_callbacks.c) ---- */
+
+static ulong
+verify_svc_footprint( fd_topo_t const * topo, fd_topo_obj_t const * obj ) {
+  ulong fp = fd_verify_svc_footprint( VAL("tile_cnt"), VAL("req_depth"), VAL("slot_cap"), VAL("frag_cap") );
+  if( FD_UNLIKELY( !fp ) ) FD_LOG_ERR(( "obj.%lu: bad verify_svc shape", obj->id ));
+  return fp;
+}
+
+static ulong
+verify_svc_align( fd_topo_t const * topo FD_FN_UNUSED, fd_topo_obj_t const * obj FD_FN_UNUSED ) {
+  return FD_VERIFY_SVC_ALIGN;
+}
+
+static void
+verify_svc_new( fd_topo_t const * topo, fd_topo_obj_t const * obj ) {
+  FD_TEST( fd_verify_svc_new( fd_topo_obj_laddr( topo, obj->id ), VAL("tile_cnt"), VAL("req_depth"), VAL("slot_cap"),
+                              VAL("frag_cap") ) );
+}
+
+fd_topo_obj_callbacks_t fd_obj_cb_verify_svc = {
+  .name      = "verify_svc",
+  .footprint = verify_svc_footprint,
+  .align     = verify_svc_align,
+  .new       = verify_svc_new,
+};
+
+/* ---- the tile ---------------------------------------------------------------------------- */
+
+typedef struct {
+  fd_verify_svc_t * svc;
+  ulong             mapped[ FD_TOPO_MAX_WKSPS ];   /* workspaces registered for the GPU */
+} fd_vgpu_ctx_t;
+
+FD_FN_CONST static inline ulong scratch_align( void ) { return 128UL; }
+FD_FN_PURE  static inline ulong scratch_footprint( fd_topo_tile_t const * tile ) { (void)tile; return sizeof(fd_vgpu_ctx_t); }
+
+/* register a workspace for the GPU once (all of it: links' mcaches,
+   dcaches and the segment are addressed inside it) */
+static void
+vgpu_map( fd_vgpu_ctx_t * ctx, fd_topo_t const * topo, ulong wksp_id ) {
+  if( ctx->mapped[ wksp_id ] ) return;
+  fd_topo_wksp_t const * w = &topo->workspaces[ wksp_id ];
+  if( FD_UNLIKELY( fd_verify_svc_map( ctx->svc, w->wksp, w->page_sz*w->page_cnt ) ) )
+    FD_LOG_ERR(( "registering workspace %s (%lu B) for the GPU failed", w->name, w->page_sz*w->page_cnt ));
+  ctx->mapped[ wksp_id ] = 1UL;
+}
+
+static void
+privileged_init( fd_topo_t * topo, fd_topo_tile_t * tile ) {
+  fd_vgpu_ctx_t * ctx = (fd_vgpu_ctx_t *)fd_topo_obj_laddr( topo, tile->tile_obj_id );
+  memset( ctx, 0, sizeof(fd_vgpu_ctx_t) );
+  ulong gpu     = tile->kind_id;
+  ulong gpu_cnt = fd_pod_query_ulong( topo->props, "verify_svc.gpu_cnt", 0UL );
+  ulong obj_id  = fd_pod_queryf_ulong( topo->props, ULONG_MAX, "verify_svc.%lu", gpu );
+  if( FD_UNLIKELY( !gpu_cnt || gpu>=gpu_cnt || obj_id==ULONG_MAX ) ) FD_LOG_ERR(( "no verify_svc object for GPU %lu", gpu ));
+  ulong batch_max = fd_pod_query_ulong( topo->props, "verify_svc.batch_max", 131072UL );
+  ulong inflight  = fd_pod_query_ulong( topo->props, "verify_svc.inflight",  4UL      );
+  ctx->svc = fd_verify_svc_boot( fd_topo_obj_laddr( topo, obj_id ), (int)gpu, batch_max, inflight );
+  if( FD_UNLIKELY( !ctx->svc ) ) FD_LOG_ERR(( "fd_verify_svc_boot failed on GPU %lu", gpu ));
+  vgpu_map( ctx, topo, topo->objs[ obj_id ].wksp_id );
+
+  /* every quic_verify link (service link l = its kind_id) */
+  for( ulong i=0UL; i<topo->link_cnt; i++ ) {
+    fd_topo_link_t const * l = &topo->links[ i ];
+    if( strcmp( l->name, "quic_verify" ) ) continue;
+    ulong dw = topo->objs[ l->dcache_obj_id ].wksp_id;
+    vgpu_map( ctx, topo, topo->objs[ l->mcache_obj_id ].wksp_id );
+    vgpu_map( ctx, topo, dw );
+    void * base = topo->workspaces[ dw ].wksp;
+    if( FD_UNLIKELY( fd_verify_svc_set_link( ctx->svc, l->kind_id, l->mcache, fd_mcache_depth( l->mcache ), base,
+                                             fd_dcache_compact_chunk0( base, l->dcache ),
+                                             fd_dcache_compact_wmark ( base, l->dcache, l->mtu ) ) ) )
+      FD_LOG_ERR(( "quic_verify link %lu: fd_verify_svc_set_link failed", l->kind_id ));
+  }
+  /* the verify tiles this GPU serves: their verify_dedup dcaches */
+  for( ulong i=0UL; i<topo->tile_cnt; i++ ) {
+    fd_topo_tile_t const * v = &topo->tiles[ i ];
+    if( strcmp( v->name, "verify" ) || fd_verify_svc_gpu_of( v->kind_id, gpu_cnt )!=gpu ) continue;
+    fd_topo_link_t const * out = &topo->links[ v->out_link_id[ 0 ] ];
+    ulong dw = topo->objs[ out->dcache_obj_id ].wksp_id;
+    vgpu_map( ctx, topo, dw );
+    if( FD_UNLIKELY( fd_verify_svc_set_tile( ctx->svc, fd_verify_svc_slot_of( v->kind_id, gpu_cnt ), out->dcache,
+                                             fd_dcache_data_sz( out->dcache ), topo->workspaces[ dw ].wksp ) ) )
+      FD_LOG_ERR(( "verify tile %lu: fd_verify_svc_set_tile failed", v->kind_id ));
+  }
+  if( FD_UNLIKELY( fd_verify_svc_run( ctx->svc ) ) ) FD_LOG_ERR(( "fd_verify_svc_run failed (a verify tile not set?)" ));
+}
+
+static inline void
+after_credit( fd_vgpu_ctx_t *     ctx,
+              fd_stem_context_t * stem,
+              int *               opt_poll_in,
+              int *               charge_busy ) {
+  (void)stem; (void)opt_poll_in;
+  *charge_busy = fd_verify_svc_poll( ctx->svc );
+}
+
+#define STEM_BURST                  (1UL)
+#define STEM_CALLBACK_CONTEXT_TYPE  fd_vgpu_ctx_t
+#define STEM_CALLBACK_CONTEXT_ALIGN 128UL
+#define STEM_CALLBACK_AFTER_CREDIT  after_credit
+
+#include "../stem/fd_stem.c"
+
+fd_topo_run_tile_t fd_tile_verify_gpu = {
+  .name                     = "vgpu",
+  .scratch_align            = scratch_align,
+  .scratch_footprint        = scratch_footprint,
+  .privileged_init          = privileged_init,
+  .run                      = stem_run,
+};

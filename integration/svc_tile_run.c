@@ -330,11 +330,11 @@ produce( char const * path, char const * stream, ulong tile_cnt, ulong in_depth 
           hdr->svc_stats[5], hdr->svc_stats[6], (double)hdr->svc_stats[7]*1e-9 );
   printf( "\"frags\": %lu, \"sigs\": %lu, \"published\": %lu, \"parse_fail\": %lu, \"verify_fail\": %lu, "
           "\"dedup\": %lu, \"bundle_peer_fail\": %lu, \"overrun\": %lu, \"lapped\": %lu, \"host_redone\": %lu, "
-          "\"consumed\": %lu, \"consumer_bad\": %lu, \"metrics_ok\": %lu, \"tile_threads_max\": %lu, \"tile_dev_fds\": %lu, "
+          "\"consumed\": %lu, \"consumer_bad\": %lu, \"digest_on\": %d, \"metrics_ok\": %lu, \"tile_threads_max\": %lu, \"tile_dev_fds\": %lu, "
           "\"seconds\": %.6f, \"publish_s\": %.6f, \"consumer_s\": %.6f, \"verifies_per_s\": %.1f, \"frags_per_s\": %.1f, "
           "\"offered_rate\": %lu, \"in_depth\": %lu, \"out_depth\": %lu, \"tile_cnt\": %lu, \"links\": %lu, \"prelay\": %d, "
           "\"polled\": %d, \"req_depth\": %lu, \"slot_cap\": %lu, \"range_max\": %lu, \"stream_frags\": %lu}\n",
-          frags, sigs, pub, parse, verify, dedup, bundle, ovr, lapped, host, cons_frags, cons_bad, metrics_ok, threads_max,
+          frags, sigs, pub, parse, verify, dedup, bundle, ovr, lapped, host, cons_frags, cons_bad, !!getenv( "SVC_RUN_DIGEST" ), metrics_ok, threads_max,
           dev_fds, s, (double)( t_pub - t0 )*1e-9, (double)( t_last - t0 )*1e-9, (double)sigs/s, (double)frags/s, rate,
           in_depth, out_depth, tile_cnt, L, prelay, !!getenv( "SVC_RUN_POLLED" ), req_depth, slot_cap,
           (ulong)FD_VERIFY_SVC_RANGE_MAX, n );
@@ -568,6 +568,12 @@ consume( char const * path, ulong t ) {
   FD_TEST( mcache && fseq );
   double tick_per_ns = fd_tempo_tick_per_ns( NULL );
   ulong stall_ms = env_ulong( "SVC_RUN_CONS_STALL_MS", 0UL );
+  /* SVC_RUN_DIGEST=1: read every frag's bytes (size checks, the payload
+     digest); otherwise only the mcache lines (the credits and the latency):
+     a consumer that reads ~700 B per frag is ~100-200 ns a frag, as the
+     reference's dedup tile's copy is, and would bound a bench of the
+     verify stage at its own rate */
+  int const digest_on = !!getenv( "SVC_RUN_DIGEST" );
   svc_run_cons_res_t * c = &hdr->cons[ t ];
   __atomic_fetch_add( &hdr->cons_ready, 1UL, __ATOMIC_SEQ_CST );
   while( !hdr->start ) FD_SPIN_PAUSE();
@@ -589,14 +595,18 @@ consume( char const * path, ulong t ) {
     if( FD_UNLIKELY( diff>0L ) ) { ovr += (ulong)diff; seq = found; continue; }   /* a reliable consumer never sees this */
     FD_COMPILER_MFENCE();
     ulong chunk = line->chunk, sz = line->sz, tsorig = line->tsorig, tspub = line->tspub;
-    uchar const * frag = (uchar const *)fd_chunk_to_laddr_const( base, chunk );
-    fd_txn_m_t const * m = (fd_txn_m_t const *)frag;
-    ulong psz = m->payload_sz, tsz = m->txn_t_sz;
-    ulong want = fd_ulong_align_up( sizeof(fd_txn_m_t) + psz, fd_txn_align() ) + tsz;
-    ulong d2 = fd_hash( digest, fd_txn_m_payload_const( m ), psz );
+    ulong d2 = digest, b2 = 0UL;
+    if( digest_on ) {
+      uchar const * frag = (uchar const *)fd_chunk_to_laddr_const( base, chunk );
+      fd_txn_m_t const * m = (fd_txn_m_t const *)frag;
+      ulong psz = m->payload_sz, tsz = m->txn_t_sz;
+      ulong want = fd_ulong_align_up( sizeof(fd_txn_m_t) + psz, fd_txn_align() ) + tsz;
+      d2 = fd_hash( digest, fd_txn_m_payload_const( m ), psz );
+      b2 = ( want!=sz || !tsz || psz>FD_TPU_MTU );
+    }
     FD_COMPILER_MFENCE();
     if( FD_UNLIKELY( fd_frag_meta_seq_query( line )!=seq ) ) { ovr++; continue; }
-    bad    += ( want!=sz || !tsz || psz>FD_TPU_MTU );
+    bad    += b2;
     digest  = d2;
     bytes  += sz;
     long now = fd_tickcount();

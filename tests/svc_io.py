@@ -54,5 +54,6 @@ def share_stream(path, s, bid, t, tiles, seed, depth):
 def run(stream, tiles, in_depth, logdir, env=None, svc_env=None, mock=False, timeout=240):
     import svc_bench as SB
     assert os.path.exists(SB.EXE), "integration/_build/svc_tile_run missing: run build() with /root/reference"
+    env = dict(env or {}, SVC_RUN_DIGEST="1")                 # the consumers read and digest every frag
     return SB.run_one(stream, tiles, in_depth, timeout, logdir, env=env, svc_env=svc_env,
                       svc_exe=MOCK if mock else None)

@@ -78,19 +78,42 @@ def test_gpu_tile_links_against_engine():
 REF = "/root/reference"
 
 
+def _strip_svc(lines):
+    """the lines outside #if FD_HAS_HIP_SVC ... #endif blocks (the service
+    mode's additions, checked separately)"""
+    out, depth = [], 0
+    for x in lines:
+        if depth:
+            depth += x.startswith("#if")
+            depth -= x.startswith("#endif")
+            continue
+        if x.startswith("#if FD_HAS_HIP_SVC"):
+            depth = 1
+            continue
+        out.append(x)
+    return out
+
+
 @pytest.mark.skipif(not os.path.isdir(REF), reason="needs /root/reference")
 def test_topology_patch_applies_and_only_unpolls_quic_verify(tmp_path):
+    """integration/fd_verify_topo_hip.patch: both topologies' quic_verify in
+    links unpolled with FD_HAS_HIP or FD_HAS_HIP_SVC; everything else it
+    adds sits in FD_HAS_HIP_SVC blocks (the GPU tiles, their verify_svc
+    objects and registrations, the GPU tile's sandbox opt-out), and the
+    patched fdctl files compile with FD_HAS_HIP_SVC against the reference's
+    headers."""
     import shutil
-    files = ["src/app/fdctl/topology.c", "src/app/firedancer/topology.c"]
-    for f in files:
+    topos = ["src/app/fdctl/topology.c", "src/app/firedancer/topology.c"]
+    others = ["src/app/fdctl/main.c", "src/disco/topo/fd_topo_run.c"]
+    for f in topos + others:
         os.makedirs(tmp_path / os.path.dirname(f), exist_ok=True)
         shutil.copy(os.path.join(REF, f), tmp_path / f)
     patch = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "integration",
                          "fd_verify_topo_hip.patch")
     subprocess.check_call(["patch", "-s", "-p1", "-i", patch], cwd=tmp_path)
-    for f in files:
+    for f in topos:
         old = open(os.path.join(REF, f)).read().splitlines()
-        new = open(tmp_path / f).read().splitlines()
+        new = _strip_svc(open(tmp_path / f).read().splitlines())
         changed = [(a, b) for a, b in zip([x for x in old if "quic_verify" in x and "verify\"," in x],
                                           [x for x in new if "quic_verify" in x and "verify\"," in x])]
         tile_in = [(a, b) for a, b in changed if "fd_topob_tile_in" in a]
@@ -101,6 +124,30 @@ def test_topology_patch_applies_and_only_unpolls_quic_verify(tmp_path):
         extra = [x for x in new if x not in old]
         assert all("FD_VERIFY_QUIC_POLL" in x or x.startswith(("/*", "   ", "#if", "#else", "#endif")) or not x.strip()
                    for x in extra), extra
+    for f in others:
+        assert _strip_svc(open(tmp_path / f).read().splitlines()) == open(os.path.join(REF, f)).read().splitlines(), f
+    fd = open(tmp_path / "src/app/fdctl/topology.c").read()
+    assert '"vgpu"' in fd and "fd_verify_svc_tiles_on" in fd and "verify_svc.gpu_cnt" in fd
+    for f in ["src/app/fdctl/topology.c", "src/app/fdctl/main.c", "src/disco/topo/fd_topo_run.c"]:
+        subprocess.check_call(["gcc", "-std=c17", "-DFD_HAS_HOSTED=1", "-DFD_HAS_INT128=1", "-DFD_HAS_DOUBLE=1",
+                               "-DFD_HAS_ALLOCA=1", "-DFD_HAS_X86=1", "-DFD_HAS_ATOMIC=1", "-DFD_HAS_THREADS=1",
+                               "-DFD_HAS_HIP_SVC=1", "-fsyntax-only", "-Wall", "-Werror"] +
+                              ([] if f.endswith("fd_topo_run.c") else ["-D_GNU_SOURCE"]) + [
+                               "-I" + os.path.join(REF, os.path.dirname(f)),
+                               "-I" + os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "include"),
+                               str(tmp_path / f)])
+
+
+def test_gpu_tile_compiles_against_reference_headers():
+    """integration/fd_verify_gpu_tile.c (the topology's vgpu tile and the
+    verify_svc object callbacks) under -Wall -Wextra -Werror"""
+    obj = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "integration", "_build",
+                       "verify_gpu_tile.o")
+    if not os.path.exists(obj):
+        pytest.skip("integration/_build missing")
+    syms = subprocess.run(["nm", obj], capture_output=True, text=True).stdout
+    for s_ in ("fd_tile_verify_gpu", "fd_obj_cb_verify_svc", "fd_verify_svc_boot", "fd_verify_svc_poll"):
+        assert s_ in syms, s_
 
 
 def test_tile_run_uses_range_entry_points():
