@@ -30,6 +30,7 @@ typedef struct {
   volatile ulong metrics_ok;                   /* the link-in metric slots hold the tile's counts */
   volatile ulong threads, dev_fds;             /* after privileged_init: /proc/self/task entries, /dev/kfd|dri fds */
   volatile ulong sandboxed;                    /* the tile ran inside fd_sandbox_enter (SVC_RUN_SANDBOX) */
+  volatile double sec_pub, sec_pass, sec_flush, sec_post;   /* the tile's time in before_credit's steps */
 } svc_run_tile_res_t;
 
 typedef struct {

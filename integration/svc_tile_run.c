@@ -22,7 +22,9 @@
            SVC_RUN_LINKS=L      quic_verify links (frag j: link j % L, seq j / L)
            SVC_RUN_PRELAY=1     the dcache holds the whole stream, laid in
                                 before the clock starts (the stage's rate,
-                                not one producer core's copy)
+                                not one producer core's copy); the mcache
+                                keeps in_depth lines, so a producer that
+                                laps a tile still overruns it
            SVC_RUN_RATE=R       offered rate, frags/s, with NO flow control
                                 (the reference's unreliable link,
                                 topology.c:173): frags the tiles do not read
@@ -156,7 +158,6 @@ produce( char const * path, char const * stream, ulong tile_cnt, ulong in_depth 
   ulong const slot_cap  = env_ulong( "SVC_RUN_SLOT_CAP", 32768UL );
   ulong const frag_cap  = env_ulong( "SVC_RUN_FRAG_CAP", getenv( "SVC_RUN_POLLED" ) ? 4096UL : 0UL );
   if( FD_UNLIKELY( L<1UL || L>SVC_RUN_LINK_MAX ) ) FD_LOG_ERR(( "SVC_RUN_LINKS %lu not in [1,%lu]", L, SVC_RUN_LINK_MAX ));
-  if( FD_UNLIKELY( prelay && in_depth<(n+L-1UL)/L ) ) FD_LOG_ERR(( "prelay: in_depth %lu < %lu frags", in_depth, n ));
   if( FD_UNLIKELY( !fd_ulong_is_pow2( out_depth ) ) ) FD_LOG_ERR(( "SVC_RUN_OUT_DEPTH %lu not a power of 2", out_depth ));
   ulong svc_sz = fd_verify_svc_footprint( tile_cnt, req_depth, slot_cap, frag_cap );
   if( FD_UNLIKELY( !svc_sz ) ) FD_LOG_ERR(( "bad service segment parameters" ));
@@ -312,11 +313,12 @@ produce( char const * path, char const * stream, ulong tile_cnt, ulong in_depth 
             "\"dedup\": %lu, \"bundle_peer_fail\": %lu, \"overrun\": %lu, \"lapped\": %lu, \"s\": %.6f, "
             "\"consumed\": %lu, \"digest\": \"%016lx\", \"threads\": %lu, \"dev_fds\": %lu, \"metrics_ok\": %lu, \"sandboxed\": %lu, "
             "\"link\": {\"consumed\": %lu, \"filtered\": %lu, \"overrun_polling\": %lu, \"overrun_polling_frags\": %lu, "
-            "\"overrun_reading\": %lu, \"overrun_reading_frags\": %lu}}",
+            "\"overrun_reading\": %lu, \"overrun_reading_frags\": %lu}, "
+            "\"busy_s\": {\"publish\": %.4f, \"pass\": %.4f, \"flush\": %.4f, \"post\": %.4f}}",
             t ? ", " : "", r->frags, r->sigs, r->pub, r->parse, r->verify, r->dedup, r->bundle, r->overrun, r->lapped,
             (double)( r->t_end - t0 )*1e-9, c->frags, c->digest, r->threads, r->dev_fds, r->metrics_ok, r->sandboxed,
             r->link_consumed, r->link_filtered, r->link_ovr_poll, r->link_ovr_poll_frags, r->link_ovr_read,
-            r->link_ovr_read_frags );
+            r->link_ovr_read_frags, r->sec_pub, r->sec_pass, r->sec_flush, r->sec_post );
   }
   double s  = (double)( t_end - t0 )*1e-9;
   double rt = (double)( reg[0]+reg[1]+reg[2]+reg[3]+reg[4]+reg[5]+reg[6]+reg[7] ) + 1e-9;
@@ -549,6 +551,9 @@ tile( char const * path, ulong t ) {
           m[ FD_METRICS_COUNTER_LINK_OVERRUN_READING_FRAG_COUNT_OFF ]==rl->overrun_reading_frag_cnt;
   }
   r->metrics_ok = ok;
+  double tpn = fd_tempo_tick_per_ns( NULL );
+  r->sec_pub  = (double)ctx->svc_ticks[ 0 ]/tpn*1e-9; r->sec_pass = (double)ctx->svc_ticks[ 1 ]/tpn*1e-9;
+  r->sec_flush = (double)ctx->svc_ticks[ 2 ]/tpn*1e-9; r->sec_post = (double)ctx->svc_ticks[ 3 ]/tpn*1e-9;
   for( ulong k=0UL; k<8UL; k++ ) r->regime[ k ] = fd_metrics_tl[ MIDX( COUNTER, TILE, REGIME_DURATION_NANOS ) + k ];
   FD_COMPILER_MFENCE();
   r->done = 1UL;

@@ -14,7 +14,11 @@
      ref_verify_tile_run     sequential after_frag over a frag array
      ref_verify_tile_bench   T verify "tiles" on T pinned threads, frags
                              round-robined by seq (before_frag,
-                             fd_verify_tile.c:38-58), timed */
+                             fd_verify_tile.c:38-58), timed
+     ref_verify_tile_digest  one tile's round robin share: the published
+                             sequence's payload digest and the outcome
+                             counts (the service-mode bench's parity,
+                             tools/svc_bench.py) */
 
 #define _GNU_SOURCE
 #include "disco/verify/fd_verify_tile.h"
@@ -153,4 +157,99 @@ void ref_verify_tile_bench( int threads, int first_cpu, ulong repeat, ulong seed
   ulong sigs = 0, pub = 0;
   for( int i=0;i<threads;i++ ) { pthread_join( th[i], NULL ); sigs += jb[i].sigs; pub += jb[i].published; }
   out[0] = now_s() - t0; out[1] = (double)(n*(repeat ? repeat : 1)); out[2] = (double)sigs; out[3] = (double)pub;
+}
+
+/* ---- a tile's published sequence, for the service-mode stage's parity ----
+
+   Tile t of T over one quic_verify link (seq = frag index): the frags
+   j % T == t in order through after_frag.  fd_txn_verify's signature check
+   is a pure function of the frag, so it runs first over the share on
+   `threads` threads (the reference's fd_txn_parse and
+   fd_ed25519_verify_batch_single_msg, the AVX-512 build); the order-dependent
+   rest -- bundle state, tcache query, verdict, tcache insert
+   (fd_verify_tile.h:61-111 with FD_TCACHE_QUERY / FD_TCACHE_INSERT) -- then
+   runs in arrival order.  digest chains fd_hash( digest, payload,
+   payload_sz ) over the published frags from 0x5eedd16e57, as
+   integration/svc_tile_run.c's consumer does.  out: digest, published,
+   parse, verify, dedup, bundle_peer, signatures of parsed frags. */
+
+typedef struct {
+  ulong t, tiles, n, lo, hi; uchar const * pool; uint const * off; ushort const * sz;
+  signed char * code; ushort * tsz; uchar * nsig;
+} digest_job_t;
+
+static void * digest_worker( void * arg ) {
+  digest_job_t * j = (digest_job_t *)arg;
+  fd_sha512_t shas[FD_TXN_ACTUAL_SIG_MAX] __attribute__((aligned(FD_SHA512_ALIGN)));
+  fd_sha512_t * sp[FD_TXN_ACTUAL_SIG_MAX];
+  for( ulong i=0; i<FD_TXN_ACTUAL_SIG_MAX; i++ ) sp[i] = fd_sha512_join( fd_sha512_new( shas + i ) );
+  uchar txn_buf[FD_TXN_MAX_SZ] __attribute__((aligned(8)));
+  for( ulong k=j->lo; k<j->hi; k++ ) {
+    ulong s = j->t + k*j->tiles;
+    uchar const * pay = j->pool + j->off[s];
+    fd_txn_t * txn = (fd_txn_t *)txn_buf;
+    ushort tsz = (ushort)fd_txn_parse( pay, j->sz[s], txn, NULL );
+    j->tsz[k] = tsz; j->code[k] = 0; j->nsig[k] = 0;
+    if( !tsz ) continue;
+    j->nsig[k] = txn->signature_cnt;
+    j->code[k] = (signed char)fd_ed25519_verify_batch_single_msg( pay + txn->message_off, (ulong)j->sz[s] - txn->message_off,
+                                                                  pay + txn->signature_off, pay + txn->acct_addr_off, sp,
+                                                                  txn->signature_cnt );
+  }
+  return NULL;
+}
+
+void ref_verify_tile_digest( ulong tiles, ulong t, ulong seed, ulong depth, ulong n, uchar const * pool,
+                             uint const * off, ushort const * sz, ulong const * bundle_id, int threads, ulong * out ) {
+  ulong m = t<n ? ( n - 1UL - t )/tiles + 1UL : 0UL;
+  signed char * code = (signed char *)malloc( m + 1UL );
+  ushort *      tsz  = (ushort *)malloc( 2UL*m + 2UL );
+  uchar *       nsig = (uchar *)malloc( m + 1UL );
+  if( threads < 1 ) threads = 1;
+  if( threads > 256 ) threads = 256;
+  pthread_t th[256]; digest_job_t jb[256];
+  for( int i=0; i<threads; i++ ) {
+    jb[i] = (digest_job_t){ .t=t, .tiles=tiles, .n=n, .lo=m*(ulong)i/(ulong)threads, .hi=m*(ulong)(i+1)/(ulong)threads,
+                            .pool=pool, .off=off, .sz=sz, .code=code, .tsz=tsz, .nsig=nsig };
+    pthread_create( &th[i], NULL, digest_worker, &jb[i] );
+  }
+  for( int i=0; i<threads; i++ ) pthread_join( th[i], NULL );
+  ref_tile_t * rt = tile_new( seed, depth, 0 );
+  fd_verify_ctx_t * ctx = &rt->ctx;
+  ulong digest = 0x5eedd16e57UL, pub = 0UL, sigs = 0UL;
+  for( ulong k=0; k<m; k++ ) {
+    ulong s = t + k*tiles;
+    uchar const * pay = pool + off[s];
+    ulong bid = bundle_id ? bundle_id[s] : 0UL;
+    int is_bundle = !!bid;
+    if( is_bundle & (bid!=ctx->bundle_id) ) { ctx->bundle_failed = 0; ctx->bundle_id = bid; }
+    if( is_bundle & (!!ctx->bundle_failed) ) { ctx->metrics.bundle_peer_fail_cnt++; continue; }
+    if( !tsz[k] ) { if( is_bundle ) ctx->bundle_failed = 1; ctx->metrics.parse_fail_cnt++; continue; }
+    sigs += nsig[k];
+    uchar txn_buf[FD_TXN_MAX_SZ] __attribute__((aligned(8)));
+    fd_txn_t * txn = (fd_txn_t *)txn_buf;
+    fd_txn_parse( pay, sz[s], txn, NULL );
+    ulong tag = fd_hash( ctx->hashmap_seed, pay + txn->signature_off, 64UL );
+    int res = FD_TXN_VERIFY_SUCCESS, ha_dup = 0;
+    if( !is_bundle ) {
+      FD_FN_UNUSED ulong map_idx = 0;
+      FD_TCACHE_QUERY( ha_dup, map_idx, ctx->tcache_map, ctx->tcache_map_cnt, tag );
+      if( ha_dup ) res = FD_TXN_VERIFY_DEDUP;
+    }
+    if( res==FD_TXN_VERIFY_SUCCESS && code[k]!=FD_ED25519_SUCCESS ) res = FD_TXN_VERIFY_FAILED;
+    if( res==FD_TXN_VERIFY_SUCCESS && !is_bundle ) {
+      FD_TCACHE_INSERT( ha_dup, *ctx->tcache_sync, ctx->tcache_ring, ctx->tcache_depth, ctx->tcache_map, ctx->tcache_map_cnt, tag );
+      if( ha_dup ) res = FD_TXN_VERIFY_DEDUP;
+    }
+    if( res!=FD_TXN_VERIFY_SUCCESS ) {
+      if( is_bundle ) ctx->bundle_failed = 1;
+      if( res==FD_TXN_VERIFY_DEDUP ) ctx->metrics.dedup_fail_cnt++; else ctx->metrics.verify_fail_cnt++;
+      continue;
+    }
+    digest = fd_hash( digest, pay, sz[s] );
+    pub++;
+  }
+  out[0] = digest; out[1] = pub; out[2] = ctx->metrics.parse_fail_cnt; out[3] = ctx->metrics.verify_fail_cnt;
+  out[4] = ctx->metrics.dedup_fail_cnt; out[5] = ctx->metrics.bundle_peer_fail_cnt; out[6] = sigs;
+  tile_delete( rt ); free( code ); free( tsz ); free( nsig );
 }

@@ -57,3 +57,26 @@ def run(stream, tiles, in_depth, logdir, env=None, svc_env=None, mock=False, tim
     env = dict(env or {}, SVC_RUN_DIGEST="1")                 # the consumers read and digest every frag
     return SB.run_one(stream, tiles, in_depth, timeout, logdir, env=env, svc_env=svc_env,
                       svc_exe=MOCK if mock else None)
+
+
+def ref_share_digests(pool, off, sz, bid, tiles, seed, depth, threads=8, seed_step=1):
+    """each tile's published sequence (digest, counts) from the reference's
+    own parse and AVX-512 verify (oracle/_ref/libfdref_txn.so
+    ref_verify_tile_digest): tile t's share of one link, tile seed
+    seed + t*seed_step (svc_tile_run.c seeds tile t with the stream's seed + t)"""
+    import ctypes as c
+    L = c.CDLL(os.path.join(REPO, "oracle", "_ref", "libfdref_txn.so"))
+    u64, vp = c.c_uint64, c.c_void_p
+    L.ref_verify_tile_digest.argtypes = [u64, u64, u64, u64, u64, vp, vp, vp, vp, c.c_int, vp]
+    pool = np.ascontiguousarray(pool, np.uint8)
+    off = np.ascontiguousarray(off, np.uint32)
+    sz = np.ascontiguousarray(sz, np.uint16)
+    bid = np.ascontiguousarray(bid, np.uint64) if bid is not None else None
+    res = []
+    for t in range(tiles):
+        out = np.zeros(8, np.uint64)
+        L.ref_verify_tile_digest(tiles, t, seed + t * seed_step, depth, len(off), pool.ctypes.data, off.ctypes.data,
+                                 sz.ctypes.data, bid.ctypes.data if bid is not None else None, threads, out.ctypes.data)
+        res.append(dict(digest=int(out[0]), published=int(out[1]), parse_fail=int(out[2]), verify_fail=int(out[3]),
+                        dedup=int(out[4]), bundle_peer_fail=int(out[5]), sigs=int(out[6])))
+    return res
