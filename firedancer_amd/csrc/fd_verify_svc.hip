@@ -220,7 +220,9 @@ struct fd_verify_svc {
   u8 *     d_stage;            /* staging: tile x slot x slot_cap frags of FD_TXN_HIP_STAGE_CHUNKS */
   svc_launch L[SVC_LAUNCH_MAX];
   svc_pend * pend; ulong pend_cap, pend_head, pend_tail, pend_frags;
-  ulong    stat[8];            /* launches, frags, requests, flushes, flushed frags, flushed bytes, spans, gpu ns */
+  ulong    stat[16];           /* launches, frags, requests, flushes, flushed frags, flushed bytes, spans, gpu ns;
+                                  host ns starting launches, starting flushes, retiring, polls */
+  long     merge_idle_ns;      /* a launch on an idle GPU once the oldest request has waited this long */
   int      running;
 };
 
@@ -287,7 +289,7 @@ fd_verify_svc_boot( void * seg_mem, int device, ulong batch_max, ulong inflight 
   SV_CHECK( hipSetDevice( device ) );
   fd_verify_svc_t * s = (fd_verify_svc_t *)calloc( 1, sizeof(fd_verify_svc_t) );
   s->seg = seg; s->dev = device; s->batch_max = batch_max; s->inflight = inflight;
-  s->merge_min = batch_max / 2ul; s->merge_wait_ns = 100000L;
+  s->merge_min = batch_max / 2ul; s->merge_wait_ns = 400000L; s->merge_idle_ns = 20000L;
   SV_CHECK( hipMalloc( &s->d_stage, stage_sz + 4096ul ) );
   for( ulong k = 0; k < inflight; k++ ) launch_alloc( s->L[k], device, batch_max );
   s->pend_cap = seg->tile_cnt * seg->req_depth;
@@ -339,8 +341,8 @@ fd_verify_svc_set_tile( fd_verify_svc_t * s, ulong t, void * out_dcache, ulong o
 }
 
 extern "C" void
-fd_verify_svc_set_merge( fd_verify_svc_t * s, ulong min_frags, ulong wait_ns ) {
-  s->merge_min = min_frags; s->merge_wait_ns = (long)wait_ns;
+fd_verify_svc_set_merge( fd_verify_svc_t * s, ulong min_frags, ulong wait_ns, ulong idle_ns ) {
+  s->merge_min = min_frags; s->merge_wait_ns = (long)wait_ns; s->merge_idle_ns = (long)idle_ns;
 }
 
 extern "C" int
@@ -480,8 +482,10 @@ extern "C" int
 fd_verify_svc_poll( fd_verify_svc_t * s ) {
   fd_verify_svc_seg_t * g = s->seg;
   int did = 0;
+  long const p0 = svc_now_ns();
   SV_CHECK( hipSetDevice( s->dev ) );
   g->svc_heartbeat++;
+  s->stat[11]++;
   /* 1. finished launches: their slots' results are in the segment */
   ulong busy = 0;
   for( ulong k = 0; k < s->inflight; k++ ) {
@@ -511,12 +515,19 @@ fd_verify_svc_poll( fd_verify_svc_t * s ) {
       T.flush_fin++; did = 1;
       fd_verify_svc_st( &b->flush_done, T.flush_fin );
     }
+  }
+  long const p1 = svc_now_ns();
+  s->stat[10] += (ulong)(p1 - p0);
+  for( ulong t = 0; t < g->tile_cnt; t++ ) {
+    svc_tile & T = s->tile[t];
+    fd_verify_svc_tile_t * b = fd_verify_svc_tile( g, t );
     ulong post = fd_verify_svc_ld( &b->flush_post );
     while( T.flush_take < post && T.flush_take - T.flush_fin < SVC_FLUSH_Q ) {
       svc_flush_start( s, t, &b->flush[T.flush_take % FD_VERIFY_SVC_FLUSH_DEPTH] );
       T.flush_take++; did = 1;
     }
   }
+  s->stat[9] += (ulong)(svc_now_ns() - p1);
   /* 3. posted requests, in each tile's ring order */
   long const now = svc_now_ns();
   for( ulong t = 0; t < g->tile_cnt; t++ ) {
@@ -540,22 +551,28 @@ fd_verify_svc_poll( fd_verify_svc_t * s ) {
       s->pend_tail++; s->pend_frags += q->n;
     }
   }
-  /* 4. a launch: when the posted frags fill its merge target, or the GPU
-     would otherwise idle, or the oldest has waited merge_wait_ns */
+  /* 4. a launch: when the posted frags fill its merge target, or the
+     oldest has waited merge_wait_ns, or (the GPU idle) merge_idle_ns --
+     large launches while the GPU is busy (a 55 K-signature launch runs ~one
+     wave per SIMD and costs 3x per signature), little added
+     latency while it is not */
   while( s->pend_head != s->pend_tail && busy < s->inflight ) {
-    bool ready = s->pend_frags >= s->merge_min || !busy || now - s->pend[s->pend_head % s->pend_cap].seen >= s->merge_wait_ns;
+    long waited = now - s->pend[s->pend_head % s->pend_cap].seen;
+    bool ready = s->pend_frags >= s->merge_min || waited >= s->merge_wait_ns || ( !busy && waited >= s->merge_idle_ns );
     if( !ready ) break;
     ulong k = 0;
     while( s->L[k].busy ) k++;
+    long const l0 = svc_now_ns();
     svc_launch_start( s, s->L[k] );
+    s->stat[8] += (ulong)(svc_now_ns() - l0);
     busy++; did = 1;
   }
   return did;
 }
 
 extern "C" void
-fd_verify_svc_stats( fd_verify_svc_t const * s, ulong out[8] ) {
-  for( int k = 0; k < 8; k++ ) out[k] = s->stat[k];
+fd_verify_svc_stats( fd_verify_svc_t const * s, ulong out[12] ) {
+  for( int k = 0; k < 12; k++ ) out[k] = s->stat[k];
 }
 
 extern "C" void

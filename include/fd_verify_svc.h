@@ -366,11 +366,14 @@ static inline ulong fd_verify_svc_tiles_on( ulong gpu, ulong verify_cnt, ulong g
    fd_verify_svc_poll( svc ): one iteration of the service loop (retire
      finished launches and flushes, start flushes, merge posted requests into
      a launch); 1 if it did anything.  Never blocks.
-   fd_verify_svc_set_merge( svc, min_frags, wait_ns ): a launch starts once
-     the posted requests hold min_frags frags, or the oldest has waited
-     wait_ns, or the GPU has no launch in flight.
-   fd_verify_svc_stats( svc, out[ 8 ] ): launches, frags, signatures,
-     flushes, flushed frags, flushed bytes, copy spans, requests.
+   fd_verify_svc_set_merge( svc, min_frags, wait_ns, idle_ns ): a launch
+     starts once the posted requests hold min_frags frags, or the oldest has
+     waited wait_ns, or -- no launch in flight -- idle_ns (defaults
+     batch_max / 2, 400 us, 20 us).
+   fd_verify_svc_stats( svc, out[ 12 ] ): launches, frags, requests,
+     flushes, flushed frags, flushed bytes, copy spans, GPU ns (summed over
+     launches), host ns starting launches, host ns starting flushes, host ns
+     polling events, polls.
    fd_verify_svc_delete( svc ): waits for the GPU and frees everything. */
 
 typedef struct fd_verify_svc fd_verify_svc_t;
@@ -381,10 +384,10 @@ int               fd_verify_svc_set_link( fd_verify_svc_t * svc, ulong link, voi
                                           void const * chunk_base, ulong chunk0, ulong wmark );
 int               fd_verify_svc_set_tile( fd_verify_svc_t * svc, ulong t, void * out_dcache, ulong out_dcache_sz,
                                           void const * out_chunk_base );
-void              fd_verify_svc_set_merge( fd_verify_svc_t * svc, ulong min_frags, ulong wait_ns );
+void              fd_verify_svc_set_merge( fd_verify_svc_t * svc, ulong min_frags, ulong wait_ns, ulong idle_ns );
 int               fd_verify_svc_run     ( fd_verify_svc_t * svc );
 int               fd_verify_svc_poll    ( fd_verify_svc_t * svc );
-void              fd_verify_svc_stats   ( fd_verify_svc_t const * svc, ulong out[ 8 ] );
+void              fd_verify_svc_stats   ( fd_verify_svc_t const * svc, ulong out[ 12 ] );
 void              fd_verify_svc_delete  ( fd_verify_svc_t * svc );
 
 #ifdef __cplusplus

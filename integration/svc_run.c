@@ -9,10 +9,11 @@
    mcache and dcache, the tiles' verify_dedup dcaches and the segment lie
    in it), names the quic_verify links (service link l = link kind_id l)
    and the tiles' out dcaches, then polls until the producer sets shutdown.
-   Environment: SVC_BATCH_MAX (frags per merged launch, default 131072),
+   Environment: SVC_BATCH_MAX (frags per merged launch, default 262144),
    SVC_INFLIGHT (launches at once, default 4), SVC_MERGE_MIN (frags that
    start a launch at once, default batch_max / 2), SVC_MERGE_WAIT_NS
-   (default 100000).
+   (default 400000), SVC_MERGE_IDLE_NS (the wait with no launch in flight,
+   default 20000).
 
    The integration's GPU tile (integration/fd_verify_gpu_tile.c) does the
    same from the topology's objects. */
@@ -49,11 +50,12 @@ main( int argc, char ** argv ) {
   close( fd );
   svc_run_hdr_t * hdr = (svc_run_hdr_t *)base;
 
-  ulong batch_max = env_ulong( "SVC_BATCH_MAX", 131072UL );
+  ulong batch_max = env_ulong( "SVC_BATCH_MAX", 262144UL );
   ulong inflight  = env_ulong( "SVC_INFLIGHT", 4UL );
   fd_verify_svc_t * svc = fd_verify_svc_boot( base + hdr->svc_off, (int)strtol( argv[2], NULL, 0 ), batch_max, inflight );
   if( !svc ) FD_LOG_ERR(( "fd_verify_svc_boot failed (batch_max %lu, inflight %lu)", batch_max, inflight ));
-  fd_verify_svc_set_merge( svc, env_ulong( "SVC_MERGE_MIN", batch_max/2UL ), env_ulong( "SVC_MERGE_WAIT_NS", 100000UL ) );
+  fd_verify_svc_set_merge( svc, env_ulong( "SVC_MERGE_MIN", batch_max/2UL ), env_ulong( "SVC_MERGE_WAIT_NS", 400000UL ),
+                           env_ulong( "SVC_MERGE_IDLE_NS", 20000UL ) );
   if( fd_verify_svc_map( svc, base, hdr->map_sz ) ) FD_LOG_ERR(( "registering %lu B for the GPU failed", hdr->map_sz ));
   for( ulong l=0UL; l<hdr->link_cnt; l++ ) {
     fd_frag_meta_t const * mcache = fd_mcache_join( base + hdr->mcache_off[ l ] );
@@ -77,9 +79,9 @@ main( int argc, char ** argv ) {
     if( !fd_verify_svc_poll( svc ) ) FD_SPIN_PAUSE();
     if( !( it & 0xffffUL ) && fd_log_wallclock()>deadline ) FD_LOG_ERR(( "service: no shutdown after 1200 s" ));
   }
-  ulong st[ 8 ];
+  ulong st[ 12 ];
   fd_verify_svc_stats( svc, st );
-  for( ulong k=0UL; k<8UL; k++ ) hdr->svc_stats[ k ] = st[ k ];
+  for( ulong k=0UL; k<12UL; k++ ) hdr->svc_stats[ k ] = st[ k ];
   fd_verify_svc_delete( svc );
   FD_COMPILER_MFENCE();
   hdr->svc_done = 1UL;

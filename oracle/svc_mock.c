@@ -157,7 +157,7 @@ main( int argc, char ** argv ) {
     }
     if( !did ) FD_SPIN_PAUSE();
   }
-  for( ulong k=0UL; k<8UL; k++ ) hdr->svc_stats[ k ] = st[ k ];
+  for( ulong k=0UL; k<8UL; k++ ) hdr->svc_stats[ k ] = st[ k ];   /* no host-time stats */
   FD_COMPILER_MFENCE();
   hdr->svc_done = 1UL;
   return 0;
