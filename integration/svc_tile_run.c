@@ -33,7 +33,10 @@
                                 tile's fseq, nothing dropped
            SVC_RUN_OUT_DEPTH    verify_dedup depth (default 16384)
            SVC_RUN_POLLED=1     the quic_verify links polled by the stem (frag
-                                requests through the frag area)
+                                requests through the frag area); =m (m > 1):
+                                a bit mask, link l polled if bit l is set,
+                                the others read by range (both kinds of in
+                                link on one tile)
            SVC_RUN_REQ_DEPTH, SVC_RUN_SLOT_CAP, SVC_RUN_FRAG_CAP   the segment
      svc_tile_run tile <shm> <t>
          Verify tile t: the mock topology around the shared links (the shape
@@ -417,7 +420,8 @@ tile( char const * path, ulong t ) {
   svc_run_hdr_t * hdr = (svc_run_hdr_t *)base;
   FD_TEST( t<hdr->tile_cnt );
   ulong in_depth = hdr->in_depth;
-  int const polled = !!getenv( "SVC_RUN_POLLED" );
+  ulong const pmask = env_ulong( "SVC_RUN_POLLED", 0UL );
+  ulong const polled_mask = pmask==1UL ? ~0UL : pmask;          /* 1: every link; m > 1: the links of mask m */
 
   fd_topo_t * topo = fd_topob_new( aligned_alloc( alignof(fd_topo_t), fd_ulong_align_up( sizeof(fd_topo_t), alignof(fd_topo_t) ) ),
                                    "verify-svc-run" );
@@ -452,7 +456,7 @@ tile( char const * path, ulong t ) {
   ulong * in_fseq[ SVC_RUN_LINK_MAX ];
   for( ulong l=0UL; l<L; l++ ) {
     fd_topob_tile_in( topo, "verify", 0UL, "verify", "quic_verify", l, FD_TOPOB_UNRELIABLE,
-                      polled ? FD_TOPOB_POLLED : FD_TOPOB_UNPOLLED );
+                      ( polled_mask>>l )&1UL ? FD_TOPOB_POLLED : FD_TOPOB_UNPOLLED );
     in_fseq[ l ] = fd_fseq_join( base + hdr->fseq_off[ l ] + t*hdr->fseq_stride );
     tile->in_link_fseq[ l ] = in_fseq[ l ];
   }
@@ -468,14 +472,15 @@ tile( char const * path, ulong t ) {
      leaves no address space to map) */
   ulong * metrics = aligned_alloc( FD_METRICS_ALIGN, fd_ulong_align_up( FD_METRICS_FOOTPRINT( L, 1UL ), FD_METRICS_ALIGN ) );
   fd_metrics_register( fd_metrics_new( metrics, L, 1UL ) );
-  ulong polled_cnt = polled ? L : 0UL;
+  ulong polled_cnt = 0UL;
+  fd_frag_meta_t const * in_mcache[ SVC_RUN_LINK_MAX ];
+  ulong *                in_fseqs [ SVC_RUN_LINK_MAX ];
+  for( ulong l=0UL; l<L; l++ )                                  /* the stem's ins: the polled links, in link order */
+    if( ( polled_mask>>l )&1UL ) { in_mcache[ polled_cnt ] = quic[ l ]->mcache; in_fseqs[ polled_cnt ] = in_fseq[ l ]; polled_cnt++; }
   void * stem_scratch = aligned_alloc( FD_STEM_SCRATCH_ALIGN,
                                        fd_ulong_align_up( stem_scratch_footprint( polled_cnt, 1UL, 1UL ), FD_STEM_SCRATCH_ALIGN ) );
   fd_rng_t rng_mem[ 1 ];
   fd_rng_t * rng = fd_rng_join( fd_rng_new( rng_mem, (uint)(hdr->seed + t), 0UL ) );
-  fd_frag_meta_t const * in_mcache[ SVC_RUN_LINK_MAX ];
-  ulong *                in_fseqs [ SVC_RUN_LINK_MAX ];
-  for( ulong l=0UL; l<L; l++ ) { in_mcache[ l ] = quic[ l ]->mcache; in_fseqs[ l ] = in_fseq[ l ]; }
   fd_frag_meta_t *       out_mcache[ 1 ] = { out->mcache };
   ulong                  cons_out[ 1 ] = { 0UL };
   ulong *                cons_fseqs[ 1 ] = { fd_fseq_join( base + hdr->cons_fseq_off[ t ] ) };

@@ -130,3 +130,26 @@ def test_sandboxed_tiles_with_the_gpu_tile(stream, tmp_path):
         run_driver("ref", p, str(tmp_path / f"ref{t}.bin"))
         assert S.tile_counts(r["tiles"][t]) == S.reference_digest(read_fdo1(str(tmp_path / f"ref{t}.bin"), DEPTH)), t
 
+
+@pytest.mark.parametrize("tiles", [1, 2])
+def test_range_link_beside_a_polled_link(stream, tmp_path, tiles):
+    """two quic_verify links, link 0 read by range and link 1 polled by the
+    stem (frag requests): the order-free counts equal the reference's over
+    each tile's share and the all-range run's (tests/test_svc_tile.py has
+    the CPU stand-in's run of the same)"""
+    s = stream["s"]
+    p = str(tmp_path / "nobundle.bin")
+    write_fdt1(p, s.pool, s.off, s.sz, np.zeros(s.n, np.uint64), SEED, 1 << 14)
+    env = dict(SMALL, SVC_RUN_LINKS="2", SVC_RUN_FRAG_CAP="512")
+    mixed = S.run(p, tiles, 1 << 14, str(tmp_path / "mixed"), env=dict(env, SVC_RUN_POLLED="2"))
+    rng = S.run(p, tiles, 1 << 14, str(tmp_path / "range"), env=env)
+    _check(mixed, s.n)
+    _check(rng, s.n)
+
+    def order_free(x):
+        return (x["published"], x["parse_fail"], x["published"] + x["dedup"] + x["verify_fail"])
+    for t in range(tiles):
+        idx = np.array([j for j in range(s.n) if (j // 2) % tiles == t])
+        ref = S.ref_share_digests(s.pool, s.off[idx], s.sz[idx], None, 1, SEED + t, 1 << 14)[0]
+        assert order_free(mixed["tiles"][t]) == order_free(ref) == order_free(rng["tiles"][t]), t
+

@@ -167,3 +167,36 @@ def test_tiles_run_inside_the_reference_sandbox(stream, tmp_path):
         run_driver("ref", p, str(tmp_path / f"ref{t}.bin"))
         assert S.tile_counts(r["tiles"][t]) == S.reference_digest(read_fdo1(str(tmp_path / f"ref{t}.bin"), DEPTH)), t
 
+
+def _order_free(x):
+    """counts no arrival order between links can change (a resend and its
+    original on different links: which one publishes, and whether the other
+    is a dedup or -- a grafted sig0 -- a verify failure, depends on the
+    order; how many publish, and the sum, do not)"""
+    return (x["published"], x["parse_fail"], x["published"] + x["dedup"] + x["verify_fail"])
+
+
+@pytest.mark.parametrize("tiles", [1, 2])
+def test_range_link_beside_a_polled_link(stream, tmp_path, tiles):
+    """two quic_verify links on every tile, link 0 unpolled (range requests)
+    and link 1 polled by the stem (frag requests through the frag area):
+    per tile the order-free counts equal the reference's over the tile's
+    share (seq % T of both links), and the all-range run's"""
+    s = stream["s"]
+    # no bundles (a bundle's frags split over two links are order-bound), and a
+    # tcache that holds the whole stream (with 777 entries whether a resend is
+    # caught depends on how far apart the two links put it and its original)
+    p = str(tmp_path / "nobundle.bin")
+    write_fdt1(p, s.pool, s.off, s.sz, np.zeros(s.n, np.uint64), SEED, 1 << 14)
+    env = dict(SMALL, SVC_RUN_LINKS="2", SVC_RUN_FRAG_CAP="512")
+    mixed = S.run(p, tiles, 1 << 14, str(tmp_path / "mixed"), env=dict(env, SVC_RUN_POLLED="2"), mock=True)
+    rng = S.run(p, tiles, 1 << 14, str(tmp_path / "range"), env=env, mock=True)
+    _check_run(mixed, s.n)
+    _check_run(rng, s.n)
+    for t in range(tiles):
+        idx = np.array([j for j in range(s.n) if (j // 2) % tiles == t])   # frag j: link j % 2, seq j // 2
+        ref = S.ref_share_digests(s.pool, s.off[idx], s.sz[idx], None, 1, SEED + t, 1 << 14)[0]
+        assert _order_free(mixed["tiles"][t]) == _order_free(ref) == _order_free(rng["tiles"][t]), t
+        assert mixed["tiles"][t]["sigs"] == rng["tiles"][t]["sigs"]
+        assert mixed["tiles"][t]["link"]["consumed"] == len(range(t, (s.n + 1) // 2, tiles))   # the range link's share
+
