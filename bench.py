@@ -595,7 +595,8 @@ def run_tile_leg(args):
             pre = {"SVC_RUN_PRELAY": "1"}
             runs = {}
             for t in (1, 2):
-                runs[t] = [SB.run_one(stream, t, depth, 180, os.path.join(logdir, f"t{t}_{k}"), env=pre) for k in range(3)]
+                runs[t] = [SB.run_one(stream, t, depth, 180, os.path.join(logdir, f"t{t}_{k}"), env=pre, pin="auto")
+                           for k in range(3)]
 
             def med(xs):
                 v = sorted(x["verifies_per_s"] for x in xs)
@@ -604,13 +605,15 @@ def run_tile_leg(args):
             best = sorted(runs[tb], key=lambda x: x["verifies_per_s"])[1]
             ok = not any(x.get("overrun") or x.get("lapped") for x in runs[tb])
             # parity against the reference's code, per tile
-            d = SB.run_one(stream, tb, depth, 180, os.path.join(logdir, "digest"), env=dict(pre, SVC_RUN_DIGEST="1"))
+            d = SB.run_one(stream, tb, depth, 180, os.path.join(logdir, "digest"), env=dict(pre, SVC_RUN_DIGEST="1"),
+                          pin="auto")
             ref = SI.ref_share_digests(s.pool, s.off, s.sz, None, tb, 0x7f4a11, 4194302, threads=16)
             got = [SI.tile_counts(x) for x in d["tiles"]]
             equal = all(g == {k: r[k] for k in g} for g, r in zip(got, ref)) and d["consumer_bad"] == 0
             # latency at the reference's link depth, paced below the measured rate
             rate = int(0.8 * best["frags_per_s"])
-            lat = SB.run_one(stream, tb, 16384, 180, os.path.join(logdir, "paced"), env=dict(pre, SVC_RUN_RATE=str(rate)))
+            lat = SB.run_one(stream, tb, 16384, 180, os.path.join(logdir, "paced"), env=dict(pre, SVC_RUN_RATE=str(rate)),
+                            pin="auto")
         return {"value": best["verifies_per_s"] if ok else None, "unit": "verifies/s",
                 "frags_per_s": best["frags_per_s"], "frags": best["frags"], "sigs": best["sigs"],
                 "published": best["published"], "overrun": best["overrun"], "seconds": best["seconds"],

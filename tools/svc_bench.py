@@ -37,7 +37,43 @@ EXE = os.path.join(BUILD, "svc_tile_run")
 SVC = os.path.join(BUILD, "svc_run")
 
 
-def run_one(stream, tiles, in_depth, timeout, logdir, env=None, svc_env=None, svc_exe=None, gpu=0):
+def gpu_numa_node(gpu=0):
+    """the NUMA node of the gpu-th AMD GPU (PCI vendor 0x1002, display class), -1 if unknown"""
+    try:
+        nodes = []
+        for d in sorted(os.listdir("/sys/bus/pci/devices")):
+            base = os.path.join("/sys/bus/pci/devices", d)
+            if open(os.path.join(base, "vendor")).read().strip() == "0x1002" and \
+               open(os.path.join(base, "class")).read().strip().startswith(("0x0380", "0x0300", "0x1200")):
+                nodes.append(int(open(os.path.join(base, "numa_node")).read().strip()))
+        return nodes[gpu] if gpu < len(nodes) else -1
+    except (OSError, ValueError):
+        return -1
+
+
+def pick_cpus(count, node=-1):
+    """count CPUs of distinct physical cores (one hardware thread each), on
+    NUMA node `node` first, among the CPUs this process may use"""
+    allowed = sorted(os.sched_getaffinity(0))
+    def sib(c):
+        try:
+            return open(f"/sys/devices/system/cpu/cpu{c}/topology/thread_siblings_list").read().strip()
+        except OSError:
+            return str(c)
+    def on_node(c):
+        return node < 0 or os.path.exists(f"/sys/devices/system/cpu/cpu{c}/node{node}")
+    seen, first, rest = set(), [], []
+    for c in allowed:
+        k = sib(c)
+        if k in seen:
+            continue
+        seen.add(k)
+        (first if on_node(c) else rest).append(c)
+    cpus = (first + rest)[:count]
+    return cpus if len(cpus) == count else None
+
+
+def run_one(stream, tiles, in_depth, timeout, logdir, env=None, svc_env=None, svc_exe=None, gpu=0, pin=None):
     """One producer, the GPU tile, `tiles` tile processes and `tiles`
     consumers.  env: the SVC_RUN_* settings (every process); svc_env: the
     GPU tile's (SVC_BATCH_MAX, SVC_INFLIGHT, ...).  Liveness is checked every
@@ -49,20 +85,32 @@ def run_one(stream, tiles, in_depth, timeout, logdir, env=None, svc_env=None, sv
     e = dict(os.environ)
     e.update(env or {})
     errs, procs = [], []
+    # pin: one core each for the producer, the GPU tile, the tiles and the consumers, on the GPU's NUMA node
+    # (the reference pins every tile to a core, [layout.affinity]); "auto" picks them, or a list of CPUs
+    if pin == "auto":
+        pin = pick_cpus(2 + 2 * tiles, gpu_numa_node(gpu))
+    cpu_of = {}
+    if pin:
+        names = ["producer", "svc"] + [f"tile{t}" for t in range(tiles)] + [f"cons{t}" for t in range(tiles)]
+        cpu_of = dict(zip(names, pin))
+
+    def pre(name):
+        c = cpu_of.get(name)
+        return (lambda: os.sched_setaffinity(0, {c})) if c is not None else None
 
     def spawn(cmd, name, extra=None):
         f = open(os.path.join(logdir, name + ".err"), "w")
         errs.append(f)
         ee = dict(e)
         ee.update(extra or {})
-        p = subprocess.Popen(cmd, stdout=subprocess.DEVNULL, stderr=f, env=ee)
+        p = subprocess.Popen(cmd, stdout=subprocess.DEVNULL, stderr=f, env=ee, preexec_fn=pre(name))
         procs.append((name, p))
         return p
 
     perr = open(os.path.join(logdir, "producer.err"), "w")
     errs.append(perr)
     prod = subprocess.Popen([EXE, "produce", shm, stream, str(tiles), str(in_depth)], stdout=subprocess.PIPE,
-                            stderr=perr, text=True, env=e)
+                            stderr=perr, text=True, env=e, preexec_fn=pre("producer"))
     t0 = time.time()
     try:
         line = prod.stdout.readline()
@@ -96,7 +144,9 @@ def run_one(stream, tiles, in_depth, timeout, logdir, env=None, svc_env=None, sv
             p.wait(timeout=60)
             if bad(n, p.returncode):
                 raise RuntimeError(f"{n} rc {p.returncode} (see {logdir}/{n}.err)")
-        return json.loads(out.strip().splitlines()[-1])
+        res = json.loads(out.strip().splitlines()[-1])
+        res["pinned"] = cpu_of or None
+        return res
     finally:
         for _, p in procs + [("producer", prod)]:
             if p.poll() is None:
@@ -119,6 +169,7 @@ def main():
     ap.add_argument("--rate", default="0", help="offered rates in frags/s, no flow control (0: flow-controlled)")
     ap.add_argument("--env", default="", help="KEY=VAL,... for every process (SVC_RUN_*)")
     ap.add_argument("--svc-env", default="", help="KEY=VAL,... for the GPU tile (SVC_BATCH_MAX, SVC_INFLIGHT, ...)")
+    ap.add_argument("--pin", default="auto", help="auto (one core each on the GPU's NUMA node), none, or c0,c1,...")
     ap.add_argument("--timeout", type=float, default=300)
     ap.add_argument("--logdir", default=os.path.join(REPO, "gpurun_out", "svc_bench_logs"))
     args = ap.parse_args()
@@ -142,8 +193,9 @@ def main():
                 if rate:
                     env["SVC_RUN_RATE"] = str(rate)
                 for r in range(args.repeat):
+                    pin = None if args.pin == "none" else args.pin if args.pin == "auto" else [int(x) for x in args.pin.split(",")]
                     res = run_one(stream, tiles, depth, args.timeout, os.path.join(args.logdir, f"t{tiles}_r{rate}_{r}"),
-                                  env=env, svc_env=kv(args.svc_env))
+                                  env=env, svc_env=kv(args.svc_env), pin=pin)
                     res["rep"] = r
                     print(json.dumps(res), flush=True)
                     if res.get("overrun") or res.get("lapped"):
