@@ -32,6 +32,12 @@
                                 default 0: flow control against the slowest
                                 tile's fseq, nothing dropped
            SVC_RUN_OUT_DEPTH    verify_dedup depth (default 16384)
+           SVC_RUN_LIE=k        every k-th frag's mcache sz is 8 bytes short
+                                of its header's payload_sz (no reference
+                                producer does this, fd_tpu_reasm.c:278):
+                                after_frag parses stale out-dcache bytes,
+                                which the tile redoes on its core
+                                (FD_VERIFY_SVC_RES_HOST)
            SVC_RUN_POLLED=1     the quic_verify links polled by the stem (frag
                                 requests through the frag area); =m (m > 1):
                                 a bit mask, link l polled if bit l is set,
@@ -156,6 +162,7 @@ produce( char const * path, char const * stream, ulong tile_cnt, ulong in_depth 
   ulong const L         = env_ulong( "SVC_RUN_LINKS", 1UL );
   int   const prelay    = !!getenv( "SVC_RUN_PRELAY" );
   ulong const rate      = env_ulong( "SVC_RUN_RATE", 0UL );
+  ulong const lie       = env_ulong( "SVC_RUN_LIE", 0UL );
   ulong const out_depth = env_ulong( "SVC_RUN_OUT_DEPTH", 16384UL );
   ulong const req_depth = env_ulong( "SVC_RUN_REQ_DEPTH", 16UL );
   ulong const slot_cap  = env_ulong( "SVC_RUN_SLOT_CAP", 32768UL );
@@ -280,7 +287,8 @@ produce( char const * path, char const * stream, ulong tile_cnt, ulong in_depth 
       memcpy( fd_txn_m_payload( m ), in+poff[ j ]+10UL, m->payload_sz );
     }
     ulong ts = (ulong)fd_frag_meta_ts_comp( fd_tickcount() );
-    fd_mcache_publish( mcache[ l ], in_depth, seq, 0UL, chunk[ l ], fsz[ j ], ctl, ts, ts );
+    ulong psz_lie = lie && j%lie==lie-1UL && fsz[ j ]>=sizeof(fd_txn_m_t)+8UL ? 8UL : 0UL;
+    fd_mcache_publish( mcache[ l ], in_depth, seq, 0UL, chunk[ l ], fsz[ j ]-psz_lie, ctl, ts, ts );
     if( !prelay ) chunk[ l ] = fd_dcache_compact_next( chunk[ l ], fsz[ j ], chunk0[ l ], wmark[ l ] );
   }
   long t_pub = fd_log_wallclock();

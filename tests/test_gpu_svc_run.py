@@ -153,3 +153,12 @@ def test_range_link_beside_a_polled_link(stream, tmp_path, tiles):
         ref = S.ref_share_digests(s.pool, s.off[idx], s.sz[idx], None, 1, SEED + t, 1 << 14)[0]
         assert order_free(mixed["tiles"][t]) == order_free(ref) == order_free(rng["tiles"][t]), t
 
+
+def test_frags_shorter_than_their_payload_are_redone_on_the_tile(stream, tmp_path):
+    """every 97th frag's mcache sz short of 80 + payload_sz: the GPU flags
+    them (FD_VERIFY_SVC_RES_HOST) and the tile redoes them on its core, in
+    order between the GPU's frags, on a 256-frag out link"""
+    r = S.run(stream["path"], 1, 1 << 14, str(tmp_path / "run"), env=dict(SMALL, SVC_RUN_LIE="97", SVC_RUN_OUT_DEPTH="256"))
+    _check(r, stream["s"].n)
+    assert r["host_redone"] == len(range(96, stream["s"].n, 97))
+

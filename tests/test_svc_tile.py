@@ -200,3 +200,16 @@ def test_range_link_beside_a_polled_link(stream, tmp_path, tiles):
         assert mixed["tiles"][t]["sigs"] == rng["tiles"][t]["sigs"]
         assert mixed["tiles"][t]["link"]["consumed"] == len(range(t, (s.n + 1) // 2, tiles))   # the range link's share
 
+
+def test_frags_shorter_than_their_payload_are_redone_on_the_tile(stream, tmp_path):
+    """every 97th frag's mcache sz 8 bytes short of 80 + payload_sz
+    (SVC_RUN_LIE): after_frag would parse 8 stale out-dcache bytes, so the
+    tile redoes those frags as the reference tile does (FD_VERIFY_SVC_RES_HOST:
+    its own copy, parse and CPU verify, published in order between the GPU's
+    frags); every frag is accounted for, nothing read is torn, and the tile
+    does not stall on its credits (a 256-frag out link)"""
+    env = dict(SMALL, SVC_RUN_LIE="97", SVC_RUN_OUT_DEPTH="256")
+    r = S.run(stream["path"], 1, 1 << 14, str(tmp_path / "run"), env=env, mock=True)
+    _check_run(r, stream["s"].n)
+    assert r["host_redone"] == len(range(96, stream["s"].n, 97))
+
