@@ -74,6 +74,7 @@ static ulong   drv_n;
 #include "../../tango/tempo/fd_tempo.h"
 #include "../quic/fd_tpu.h"
 #include <errno.h>
+#include <pthread.h>
 #include <fcntl.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -92,8 +93,15 @@ void fd_halt( void ) {}
 #define RUN_MAGIC     (0xfd7111e5a11ce5ULL)
 #define RUN_TILE_MAX  (16UL)
 #define RUN_LINK_MAX  (4UL)
-/* verify_dedup mcache: at least twice FD_VERIFY_HIP_STEM_BURST (fd_stem.c:358) */
-#define RUN_OUT_DEPTH (fd_ulong_max( 65536UL, fd_ulong_pow2_up( 2UL*FD_VERIFY_HIP_STEM_BURST ) ))
+/* verify_dedup depth: deep enough that the out chunk ring never holds back a
+   throughput run (the tile's frags on the GPU hold chunks: verify_hip_room);
+   TILE_RUN_OUT_DEPTH sets it (the reference's default is 16384,
+   tiles.verify.receive_buffer_size) */
+static ulong run_out_depth( void ) {
+  char const * v = getenv( "TILE_RUN_OUT_DEPTH" );
+  return v ? fd_ulong_pow2_up( strtoul( v, NULL, 0 ) ) : (1UL<<20);
+}
+#define RUN_OUT_DEPTH run_out_depth()
 
 typedef struct {
   volatile long t_ready, t_end;
@@ -101,6 +109,7 @@ typedef struct {
   volatile ulong batches;
   volatile double gpu_ms, host_ms;           /* sums over the tile's batches (fd_verify_hip_tile_hist sums) */
   volatile ulong regime[ 8 ];                /* the stem's REGIME_DURATION_NANOS ticks (fd_stem.c:406-712) */
+  volatile ulong cons_digest, cons_cnt, cons_bad;   /* TILE_RUN_CONS: the out link's consumer */
 } run_res_t;
 
 typedef struct {
@@ -295,9 +304,12 @@ produce( char const * path, char const * stream, ulong tile_cnt, ulong in_depth 
     gpu_ms += r->gpu_ms; host_ms += r->host_ms;
     for( ulong k=0UL; k<8UL; k++ ) reg[ k ] += r->regime[ k ];
     printf( "%s{\"frags\": %lu, \"sigs\": %lu, \"published\": %lu, \"batches\": %lu, \"s\": %.6f, "
-            "\"gpu_ms_per_batch\": %.4f, \"host_ms_per_batch\": %.4f}", t ? ", " : "", r->frags, r->sigs, r->pub,
+            "\"gpu_ms_per_batch\": %.4f, \"host_ms_per_batch\": %.4f, \"parse_fail\": %lu, \"verify_fail\": %lu, "
+            "\"dedup\": %lu, \"bundle_peer_fail\": %lu, \"cons_digest\": \"%016lx\", \"consumed\": %lu, "
+            "\"cons_bad\": %lu}", t ? ", " : "", r->frags, r->sigs, r->pub,
             r->batches, (double)( r->t_end - t0 )*1e-9, r->batches ? r->gpu_ms/(double)r->batches : 0.0,
-            r->batches ? r->host_ms/(double)r->batches : 0.0 );
+            r->batches ? r->host_ms/(double)r->batches : 0.0, r->parse, r->verify, r->dedup, r->bundle,
+            r->cons_digest, r->cons_cnt, r->cons_bad );
   }
   double s = (double)( t_end - t0 )*1e-9;
   double rt = (double)( reg[0]+reg[1]+reg[2]+reg[3]+reg[4]+reg[5]+reg[6]+reg[7] ) + 1e-9;
@@ -344,6 +356,49 @@ drv_malloc( ulong align, ulong sz ) {
 static fd_verify_ctx_t * drv_ctx;
 static ulong             drv_share;           /* frags of the stream this tile takes */
 static long              drv_deadline;
+
+/* TILE_RUN_CONS: a reliable consumer of the tile's verify_dedup link (as
+   the dedup tile), on a thread of the tile process.  It stalls
+   TILE_RUN_CONS_STALL_MS first, then reads every frag in seq order, checks
+   the line still holds the seq after reading (an overwritten frag counts in
+   cons_bad), chains the payloads into a digest (tests/svc_io.py digest_of:
+   fd_hash from 0x5eedd16e57) and returns credits through its fseq. */
+typedef struct {
+  fd_frag_meta_t const * mcache;
+  ulong                  depth;
+  void const *           mem;                 /* the out dcache's chunk base */
+  ulong *                fseq;
+  long                   stall_ns;
+  volatile ulong         target;              /* ULONG_MAX until the tile is done: then its published count */
+  ulong                  digest, cnt, bad;
+} drv_cons_t;
+
+static void *
+drv_cons( void * _c ) {
+  drv_cons_t * c = (drv_cons_t *)_c;
+  for( long t = fd_log_wallclock(); fd_log_wallclock()-t < c->stall_ns; ) FD_SPIN_PAUSE();
+  ulong seq = 0UL, digest = 0x5eedd16e57UL;
+  while( seq<c->target ) {
+    fd_frag_meta_t const * line = c->mcache + fd_mcache_line_idx( seq, c->depth );
+    ulong found = fd_frag_meta_seq_query( line );
+    long  diff  = fd_seq_diff( found, seq );
+    if( diff<0L ) { fd_fseq_update( c->fseq, seq ); FD_SPIN_PAUSE(); continue; }
+    if( FD_UNLIKELY( diff>0L ) ) { c->bad++; seq = found; continue; }   /* lapped: cannot happen to a reliable consumer */
+    FD_COMPILER_MFENCE();
+    ulong chunk = (ulong)line->chunk;
+    FD_COMPILER_MFENCE();
+    fd_txn_m_t const * m = (fd_txn_m_t const *)fd_chunk_to_laddr_const( c->mem, chunk );
+    ulong d = fd_hash( digest, fd_txn_m_payload_const( m ), m->payload_sz );
+    FD_COMPILER_MFENCE();
+    if( FD_UNLIKELY( fd_frag_meta_seq_query( line )!=seq ) ) c->bad++;
+    digest = d;
+    seq++;
+    if( !( seq & 63UL ) ) fd_fseq_update( c->fseq, seq );
+  }
+  fd_fseq_update( c->fseq, seq );
+  c->digest = digest; c->cnt = seq;
+  return NULL;
+}
 
 static int
 drv_should_shutdown( void * _ctx ) {
@@ -448,7 +503,15 @@ tile( char const * path, ulong t ) {
   drv_in_fseq = in_fseq[ 0 ]; drv_n = hdr->n;
   uchar cons_mem[ 256 ] __attribute__((aligned(128)));
   FD_TEST( fd_fseq_footprint()<=sizeof(cons_mem) );
-  ulong * cons_fseq = fd_fseq_join( fd_fseq_new( cons_mem, STEM_SHUTDOWN_SEQ ) );
+  int const with_cons = !!getenv( "TILE_RUN_CONS" );
+  ulong * cons_fseq = fd_fseq_join( fd_fseq_new( cons_mem, with_cons ? 0UL : STEM_SHUTDOWN_SEQ ) );
+  static drv_cons_t cons;
+  pthread_t cons_thread;
+  if( with_cons ) {
+    char const * st = getenv( "TILE_RUN_CONS_STALL_MS" );
+    cons = (drv_cons_t){ .mcache = out->mcache, .depth = fd_mcache_depth( out->mcache ), .mem = ctx->out_mem,
+                         .fseq = cons_fseq, .stall_ns = st ? 1000000L*strtol( st, NULL, 0 ) : 0L, .target = ULONG_MAX };
+  }
   fd_rng_t rng_mem[ 1 ];
   fd_rng_t * rng = fd_rng_join( fd_rng_new( rng_mem, (uint)(hdr->seed + t), 0UL ) );
   fd_frag_meta_t const * in_mcache[ RUN_LINK_MAX ];
@@ -462,6 +525,7 @@ tile( char const * path, ulong t ) {
   hdr->res[ t ].t_ready = fd_log_wallclock();
   __atomic_fetch_add( &hdr->ready, 1UL, __ATOMIC_SEQ_CST );
   while( !hdr->start ) FD_SPIN_PAUSE();
+  if( with_cons ) FD_TEST( !pthread_create( &cons_thread, NULL, drv_cons, &cons ) );
   drv_deadline = fd_log_wallclock() + 600L*1000000000L;
   stem_run1( drv_range ? 0UL : L, in_mcache, in_fseqs, 1UL, out_mcache, 1UL, cons_out, cons_fseqs, FD_VERIFY_HIP_STEM_BURST, 0L, rng,
              stem_scratch, ctx );
@@ -478,6 +542,11 @@ tile( char const * path, ulong t ) {
   r->parse = m[0]; r->verify = m[1]; r->dedup = m[2]; r->bundle = m[3]; r->overrun = ctx->hip_overrun_cnt;
   r->batches = nb; r->gpu_ms = (double)sum_gpu*1e-6; r->host_ms = (double)sum_host*1e-6;
   for( ulong k=0UL; k<8UL; k++ ) r->regime[ k ] = fd_metrics_tl[ MIDX( COUNTER, TILE, REGIME_DURATION_NANOS ) + k ];
+  if( with_cons ) {
+    cons.target = m[4];
+    FD_TEST( !pthread_join( cons_thread, NULL ) );
+    r->cons_digest = cons.digest; r->cons_cnt = cons.cnt; r->cons_bad = cons.bad;
+  }
   FD_COMPILER_MFENCE();
   r->done = 1UL;
   return 0;

@@ -64,8 +64,8 @@ void fd_boot( int * pargc, char *** pargv ) { (void)pargc; (void)pargv; }
 void fd_halt( void ) {}
 #endif
 
-/* the patched tile publishes up to a batch from after_credit, so its out
-   link carries that burst (fd_verify_tile.h, FD_HAS_HIP) */
+/* the out link's burst: the patched tile's (fd_verify_tile.h, FD_HAS_HIP:
+   the reference's 1, its publishes stay within the stem's credits) */
 #if FD_HAS_HIP
 #define DRV_OUT_BURST FD_VERIFY_HIP_STEM_BURST
 #else
@@ -196,7 +196,13 @@ main( int argc, char ** argv ) {
   ulong   off = 28UL;
   for( ulong j=0UL; j<n; j++ ) {
 #if FD_HAS_HIP
-    { int poll_in = 1, busy = 0; after_credit( ctx, &stem, &poll_in, &busy ); }
+    /* as the stem: after_credit until it lets the next frag in (fd_stem.c:545-550) */
+    for( long t0 = fd_log_wallclock();; ) {
+      int poll_in = 1, busy = 0;
+      after_credit( ctx, &stem, &poll_in, &busy );
+      if( poll_in ) break;
+      if( FD_UNLIKELY( fd_log_wallclock()-t0 > 30L*1000L*1000L*1000L ) ) FD_LOG_ERR(( "frag %lu: after_credit never let it in", j ));
+    }
 #endif
     ulong bid; ushort psz;
     memcpy( &bid, in+off, 8 ); memcpy( &psz, in+off+8, 2 ); off += 10UL;

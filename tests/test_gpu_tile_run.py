@@ -112,3 +112,37 @@ def test_two_links_range_and_polled(stream, tmp_path, tiles):
         assert r[k] == p[k], (k, r[k], p[k])
     assert r["frags"] == s.n
     assert r["published"] + r["dedup"] + r["verify_fail"] == p["published"] + p["dedup"] + p["verify_fail"]
+
+
+@pytest.mark.parametrize("range_mode", [False, True])
+@pytest.mark.parametrize("out_depth", [256, 16384])
+def test_stalled_consumer_reads_the_reference_sequence(tmp_path, monkeypatch, range_mode, out_depth):
+    """a reliable consumer of the out link (TILE_RUN_CONS: tile_run.c's
+    drv_cons) that stalls 300 ms while a third of the frags are dropped
+    (parse / verify / dedup): the tile's frags on the GPU and the dropped
+    ones hold out chunks without credits, so only the chunk ring check
+    (verify_hip_room) keeps the tile from overwriting a frag the consumer
+    has not read.  The consumer's digest of every payload it reads, in
+    order, equals the reference tile's over the same stream, at the
+    reference's default out depth (16384) and a shallow one (256), with the
+    reference's stem burst of 1."""
+    import numpy as np
+    import svc_io as S
+    import tile_bench as TB
+    import txn_lib as T
+    from firedancer_amd.txn_workload import make_txn_stream
+    from tile_io import read_fdo1, run_driver, write_fdt1
+    s = make_txn_stream(3000, T.oracle_signer, seed=0x7e6a, dup_frac=0.15, graft_frac=0.02, bad_frac=0.2)
+    p = str(tmp_path / "s.bin")
+    write_fdt1(p, s.pool, s.off, s.sz, np.zeros(s.n, np.uint64), 0x5eed7117, 777)
+    run_driver("ref", p, str(tmp_path / "ref.bin"))
+    ref = S.reference_digest(read_fdo1(str(tmp_path / "ref.bin"), 777))
+    monkeypatch.setenv("TILE_RUN_CONS", "1")
+    monkeypatch.setenv("TILE_RUN_CONS_STALL_MS", "300")
+    monkeypatch.setenv("TILE_RUN_OUT_DEPTH", str(out_depth))
+    r = TB.run_one(os.path.join(TB.BUILD, "tile_run"), p, 1, 16384, 120, str(tmp_path / "run"), range_mode=range_mode)
+    t = r["tiles"][0]
+    assert r["overrun"] == 0 and t["cons_bad"] == 0, r
+    assert t["consumed"] == t["published"] == ref["published"]
+    assert int(t["cons_digest"], 16) == ref["digest"]
+    assert (t["parse_fail"], t["verify_fail"], t["dedup"]) == (ref["parse_fail"], ref["verify_fail"], ref["dedup"])
