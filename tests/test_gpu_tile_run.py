@@ -140,7 +140,7 @@ def test_stalled_consumer_reads_the_reference_sequence(tmp_path, monkeypatch, ra
     monkeypatch.setenv("TILE_RUN_CONS", "1")
     monkeypatch.setenv("TILE_RUN_CONS_STALL_MS", "300")
     monkeypatch.setenv("TILE_RUN_OUT_DEPTH", str(out_depth))
-    r = TB.run_one(os.path.join(TB.BUILD, "tile_run"), p, 1, 16384, 120, str(tmp_path / "run"), range_mode=range_mode)
+    r = TB.run_one(os.path.join(TB.BUILD, "tile_run"), p, 1, 262144, 120, str(tmp_path / "run"), range_mode=range_mode)
     t = r["tiles"][0]
     assert r["overrun"] == 0 and t["cons_bad"] == 0, r
     assert t["consumed"] == t["published"] == ref["published"]
