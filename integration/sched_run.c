@@ -66,6 +66,7 @@ static ulong   bank_refcnt[ BANK_CNT ];
 static int     bank_dead  [ BANK_CNT ];
 static int     record_mode;
 static ulong   sigs_exec, sigs_bulk, batches_bulk, bulk_max;
+static double  t_ingest, t_bulk, t_sv_last, t_start;   /* ingest calls, bulk_sigverify calls, last sigverify done */
 static fd_sha512_t * shas[ FD_TXN_ACTUAL_SIG_MAX ];
 
 static double now( void ) { struct timespec t; clock_gettime( CLOCK_MONOTONIC, &t ); return (double)t.tv_sec + 1e-9*(double)t.tv_nsec; }
@@ -133,6 +134,7 @@ bulk_sigverify( fd_sched_t * sched, bulk_t * b, int mode, ulong batch_min, ulong
       fd_sched_sigverify_claim_done( sched, b->bank_idx, b->txn_idx[ j ] );
     }
     b->cnt = 0UL;
+    t_sv_last = now() - t_start;
     return 1;
   }
   ulong bank_idx;
@@ -244,6 +246,7 @@ run_job( char ** argv, int argc ) {
   ulong tasks_exec = 0UL, tasks_sigverify = 0UL;
   int block_started = 0, block_ended = 0;
   double t0 = now();
+  t_start = t0; t_ingest = t_bulk = t_sv_last = 0.0;
   for(;;) {
     int progress = 0;
     if( fec_i<fec_cnt && !bank_dead[ 1 ] ) {
@@ -259,12 +262,14 @@ run_job( char ** argv, int argc ) {
       fec->is_last_in_block  = fec_i==fec_cnt-1UL ? 1U : 0U;
       fec->is_first_in_block = fec_i==0UL ? 1U : 0U;
       if( fd_sched_fec_can_ingest( sched, fec ) ) {
+        double ti = now();
         FD_TEST( fd_sched_fec_ingest( sched, fec ) );
+        t_ingest += now() - ti;
         fec_i++;
         progress = 1;
       }
     }
-    if( mode!=MODE_EXEC ) progress |= bulk_sigverify( sched, bulk, mode, batch_min, batch_max );
+    if( mode!=MODE_EXEC ) { double tb = now(); progress |= bulk_sigverify( sched, bulk, mode, batch_min, batch_max ); t_bulk += now() - tb; }
 
     fd_sched_task_t task[ 1 ];
     if( fd_sched_task_next_ready( sched, task ) ) {
@@ -310,6 +315,7 @@ run_job( char ** argv, int argc ) {
           sigs_exec += TXN( txn_p )->signature_cnt;
           record( sched, txn_idx, res, 1 );
           sigverify_failed( sched, 1UL, res );
+          t_sv_last = now() - t_start;
         }
         fd_sched_task_done( sched, type, txn_idx, k );
         break;
@@ -332,9 +338,11 @@ run_job( char ** argv, int argc ) {
   printf( "{\"mode\": \"%s\", \"record\": %d, \"exec_cnt\": %lu, \"fec_cnt\": %lu, \"fec_ingested\": %lu, "
           "\"sigverified\": %lu, \"tasks_exec\": %lu, \"tasks_sigverify\": %lu, \"bulk_batches\": %lu, "
           "\"bulk_max\": %lu, \"sigs_exec\": %lu, \"sigs_bulk\": %lu, \"block_started\": %d, \"block_ended\": %d, "
-          "\"dead\": %d, \"refcnt\": %lu, \"seconds\": %.6f, \"batch_max\": %lu, \"batch_min\": %lu}\n",
+          "\"dead\": %d, \"refcnt\": %lu, \"seconds\": %.6f, \"batch_max\": %lu, \"batch_min\": %lu, "
+          "\"ingest_s\": %.6f, \"bulk_s\": %.6f, \"sigverify_done_s\": %.6f}\n",
           argv[1], record_mode, exec_cnt, fec_cnt, fec_i, rec_cnt, tasks_exec, tasks_sigverify, batches_bulk, bulk_max,
-          sigs_exec, sigs_bulk, block_started, block_ended, bank_dead[ 1 ], bank_refcnt[ 1 ], dt, batch_max, batch_min );
+          sigs_exec, sigs_bulk, block_started, block_ended, bank_dead[ 1 ], bank_refcnt[ 1 ], dt, batch_max, batch_min,
+          t_ingest, t_bulk, t_sv_last );
   fflush( stdout );
 #if FD_HAS_HIP
   if( hip ) {

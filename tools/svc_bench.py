@@ -73,11 +73,14 @@ def pick_cpus(count, node=-1):
     return cpus if len(cpus) == count else None
 
 
-def run_one(stream, tiles, in_depth, timeout, logdir, env=None, svc_env=None, svc_exe=None, gpu=0, pin=None):
+def run_one(stream, tiles, in_depth, timeout, logdir, env=None, svc_env=None, svc_exe=None, gpu=0, pin=None,
+            rocprof=None):
     """One producer, the GPU tile, `tiles` tile processes and `tiles`
     consumers.  env: the SVC_RUN_* settings (every process); svc_env: the
     GPU tile's (SVC_BATCH_MAX, SVC_INFLIGHT, ...).  Liveness is checked every
-    0.2 s: a process that dies ends the run at once."""
+    0.2 s: a process that dies ends the run at once.  rocprof: a directory;
+    the GPU tile runs under rocprofv3 --kernel-trace --memory-copy-trace
+    --stats there (the program itself after --)."""
     shm = f"/dev/shm/fd_svc_bench_{os.getpid()}"
     if os.path.exists(shm):
         os.unlink(shm)
@@ -116,7 +119,11 @@ def run_one(stream, tiles, in_depth, timeout, logdir, env=None, svc_env=None, sv
         line = prod.stdout.readline()
         if line.strip() != "READY":
             raise RuntimeError(f"producer: {line!r} (see {logdir}/producer.err)")
-        spawn([svc_exe or SVC, shm, str(gpu)], "svc", svc_env)
+        svc_cmd = [svc_exe or SVC, shm, str(gpu)]
+        if rocprof:
+            svc_cmd = ["rocprofv3", "--kernel-trace", "--memory-copy-trace", "--stats", "--output-format", "csv",
+                       "-d", rocprof, "-o", "svc", "--"] + svc_cmd
+        spawn(svc_cmd, "svc", svc_env)
         for t in range(tiles):
             spawn([EXE, "consume", shm, str(t)], f"cons{t}")
             spawn([EXE, "tile", shm, str(t)], f"tile{t}")
@@ -171,6 +178,7 @@ def main():
     ap.add_argument("--svc-env", default="", help="KEY=VAL,... for the GPU tile (SVC_BATCH_MAX, SVC_INFLIGHT, ...)")
     ap.add_argument("--pin", default="auto", help="auto (one core each on the GPU's NUMA node), none, or c0,c1,...")
     ap.add_argument("--timeout", type=float, default=300)
+    ap.add_argument("--rocprof", default=None, help="directory: the GPU tile under rocprofv3 kernel / copy traces")
     ap.add_argument("--logdir", default=os.path.join(REPO, "gpurun_out", "svc_bench_logs"))
     args = ap.parse_args()
     import tile_bench as TB
@@ -195,7 +203,8 @@ def main():
                 for r in range(args.repeat):
                     pin = None if args.pin == "none" else args.pin if args.pin == "auto" else [int(x) for x in args.pin.split(",")]
                     res = run_one(stream, tiles, depth, args.timeout, os.path.join(args.logdir, f"t{tiles}_r{rate}_{r}"),
-                                  env=env, svc_env=kv(args.svc_env), pin=pin)
+                                  env=env, svc_env=kv(args.svc_env), pin=pin,
+                                  rocprof=os.path.join(args.rocprof, f"t{tiles}_{r}") if args.rocprof else None)
                     res["rep"] = r
                     print(json.dumps(res), flush=True)
                     if res.get("overrun") or res.get("lapped"):
