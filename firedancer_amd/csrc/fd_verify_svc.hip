@@ -4,17 +4,23 @@
    One process per GPU owns the HIP context.  Every verify tile it serves
    posts requests (a seq range of an unpolled quic_verify link, or frags it
    copied from a polled link) into its slots of the segment.  The service
-   merges the posted requests of all tiles into one launch (up to batch_max
-   frags), so a launch is C4-sized whatever the tile count:
+   copies each newly posted request's frags into HBM at once, then merges
+   the ingested requests of all tiles into one verify launch (up to
+   batch_max frags), so a launch is C4-sized whatever the tile count:
 
-     k_svc_gather   one wave per frag: before_frag's share (range requests
-                    name only the kept seqs: seq0 + i x rr_cnt), the mcache
-                    line (seq still there, chunk in [chunk0, wmark], sz <=
-                    FD_TPU_RAW_MTU: fd_stem.c and during_frag's checks,
-                    fd_verify_tile.c:74-76), and the frag's bytes from the
-                    link's dcache (pinned host memory) into an HBM ingest
-                    frag -- the PCIe read leaves the CU as soon as it lands,
-                    before the LDS-heavy parse holds it
+     k_svc_gather   (the ingest, on its own stream, as soon as a request is
+                    posted) one wave per frag: before_frag's share (range
+                    requests name only the kept seqs: seq0 + i x rr_cnt),
+                    the mcache line (seq still there, chunk in [chunk0,
+                    wmark], sz <= FD_TPU_RAW_MTU: fd_stem.c and during_frag's
+                    checks, fd_verify_tile.c:74-76), and the frag's bytes
+                    from the link's dcache (pinned host memory) into the
+                    request slot's HBM ingest frags.  Then the slot goes to
+                    INGESTED: the tile checks for overruns and returns the
+                    link's credits right away, so the link holds a frag for
+                    the PCIe copy only, not for the merge and the verify
+     k_svc_assemble the verify launch's per-frag arrays from its requests'
+                    ingest frags
      fd_txn_hip_batch_core
                     k_txnm_batch<16> (during_frag's copy into the request's
                     HBM staging frags, fd_txn_parse, the sig0 tag with each
@@ -66,6 +72,7 @@ typedef uint64_t u64;
 #define SVC_LAUNCH_MAX    8ul
 #define SVC_FLUSH_Q       64ul   /* flushes in flight per tile */
 #define SVC_REGION_MAX    64ul
+#define SVC_ING_MAX       8ul    /* ingest batches in flight */
 
 static long svc_now_ns( void ) {
   struct timespec ts;
@@ -87,7 +94,8 @@ struct __attribute__((aligned(16))) svc_desc {
   u64 chunk0, wmark;
   u64 seed;
   u64 stage0;      /* staging chunk of the request's frag 0 */
-  u64 rsv[3];
+  u64 ibase;       /* ingest frag of the request's frag 0 (slot (t, s): (t x req_depth + s) x slot_cap) */
+  u64 rsv[2];
 };
 static_assert( sizeof(svc_desc) == 128, "svc_desc layout" );
 
@@ -95,10 +103,9 @@ static_assert( sizeof(svc_desc) == 128, "svc_desc layout" );
 /* kernels                                                             */
 
 __global__ __launch_bounds__(256)
-void k_svc_gather( svc_desc const * __restrict__ desc, u32 nreq, ulong n, u8 * __restrict__ ingest,
-                   u8 * __restrict__ stage, u32 * __restrict__ in_chunk, u16 * __restrict__ in_sz,
-                   u8 * __restrict__ in_kind, u32 * __restrict__ tso, u64 * __restrict__ seedv,
-                   u32 * __restrict__ stage_chunk ) {
+void k_svc_gather( svc_desc const * __restrict__ desc, u32 nreq, ulong n, u8 * __restrict__ ing,
+                   u16 * __restrict__ ing_sz, u8 * __restrict__ ing_kind, u32 * __restrict__ ing_tso,
+                   u8 * __restrict__ stage ) {
   __shared__ u64 sbase[SVC_REQ_MAX];
   for( u32 i = threadIdx.x; i < nreq; i += blockDim.x ) sbase[i] = desc[i].base;
   __syncthreads();
@@ -131,16 +138,34 @@ void k_svc_gather( svc_desc const * __restrict__ desc, u32 nreq, ulong n, u8 * _
     kind = ((u8 const *)d->aux1)[i];
     ok   = sz <= FD_VERIFY_SVC_FRAG_STRIDE;
   }
-  u8 * dst = ingest + 64ul * SVC_INGEST_CHUNKS * j;
+  ulong const f = d->ibase + i;
+  u8 * dst = ing + 64ul * SVC_INGEST_CHUNKS * f;
   if( ok ) for( u32 p = 16u * lane; p < sz; p += 1024u ) *(uint4 *)(dst + p) = *(uint4 const *)(src + p);
-  u32 const sc = (u32)(d->stage0 + FD_TXN_HIP_STAGE_CHUNKS * i);
   /* a gossip vote's out header: the reference writes four fields into the
      out chunk's stale header (fd_verify_tile.c:90-93); here the rest is 0 */
-  if( kind == FD_VERIFY_HIP_IN_GOSSIP && lane < 5u ) *(uint4 *)(stage + 64ul * sc + 16u * lane) = make_uint4( 0u, 0u, 0u, 0u );
-  if( lane == 0u ) {
-    in_chunk[j] = (u32)(SVC_INGEST_CHUNKS * j); in_sz[j] = ok ? (u16)sz : (u16)0xffffu; in_kind[j] = (u8)kind;
-    tso[j] = tsv; seedv[j] = d->seed; stage_chunk[j] = sc;
-  }
+  if( kind == FD_VERIFY_HIP_IN_GOSSIP && lane < 5u )
+    *(uint4 *)(stage + 64ul * (d->stage0 + FD_TXN_HIP_STAGE_CHUNKS * i) + 16u * lane) = make_uint4( 0u, 0u, 0u, 0u );
+  if( lane == 0u ) { ing_sz[f] = ok ? (u16)sz : (u16)0xffffu; ing_kind[f] = (u8)kind; ing_tso[f] = tsv; }
+}
+
+/* a verify launch's per-frag arrays (launch frag j = frag i of request d)
+   from the requests' ingest frags: one thread per frag */
+__global__ __launch_bounds__(256)
+void k_svc_assemble( svc_desc const * __restrict__ desc, u32 nreq, ulong n, u16 const * __restrict__ ing_sz,
+                     u8 const * __restrict__ ing_kind, u32 const * __restrict__ ing_tso, u32 * __restrict__ in_chunk,
+                     u16 * __restrict__ in_sz, u8 * __restrict__ in_kind, u32 * __restrict__ tso, u64 * __restrict__ seedv,
+                     u32 * __restrict__ stage_chunk ) {
+  __shared__ u64 sbase[SVC_REQ_MAX];
+  for( u32 i = threadIdx.x; i < nreq; i += blockDim.x ) sbase[i] = desc[i].base;
+  __syncthreads();
+  ulong const j = (ulong)blockIdx.x * blockDim.x + threadIdx.x;
+  if( j >= n ) return;
+  u32 lo = 0u, hi = nreq;
+  while( hi - lo > 1u ) { u32 mid = (lo + hi) >> 1; if( sbase[mid] <= j ) lo = mid; else hi = mid; }
+  svc_desc const * d = desc + lo;
+  ulong const i = j - d->base, f = d->ibase + i;
+  in_chunk[j] = (u32)(SVC_INGEST_CHUNKS * f); in_sz[j] = ing_sz[f]; in_kind[j] = ing_kind[f]; tso[j] = ing_tso[f];
+  seedv[j] = d->seed; stage_chunk[j] = (u32)(d->stage0 + FD_TXN_HIP_STAGE_CHUNKS * i);
 }
 
 __global__ __launch_bounds__(256)
@@ -184,7 +209,7 @@ struct svc_launch {
   fd_ed25519_hip_ctx_t * ctx;
   hipStream_t            st;
   hipEvent_t             ev0, ev1;
-  u8 *  d_ingest; u32 * d_in_chunk; u16 * d_in_sz; u8 * d_in_kind; u32 * d_tso; u64 * d_seed; u32 * d_stage_chunk;
+  u32 * d_in_chunk; u16 * d_in_sz; u8 * d_in_kind; u32 * d_tso; u64 * d_seed; u32 * d_stage_chunk;
   u16 * d_tsz; u64 * d_tag; u64 * d_bid; u32 * d_first; u8 * d_cnt; signed char * d_tcode; u32 * d_misc;
   u8 *  d_rsig; u8 * d_rpub; u32 * d_rmoff; u32 * d_rmsz; signed char * d_rcode; ulong rcap; u64 * d_fdesc;
   fd_verify_svc_res_t * d_res;
@@ -208,6 +233,15 @@ struct svc_tile {
 
 struct svc_pend { ulong t, slot, n; long seen; };
 
+/* an ingest batch: the gather of newly posted requests, on the ingest stream */
+struct svc_ingest {
+  int         busy;
+  hipEvent_t  ev0, ev1;
+  svc_desc *  h_desc; svc_desc * d_desc;
+  ulong       nreq, n;
+  struct { ulong t, slot; } req[SVC_REQ_MAX];
+};
+
 struct fd_verify_svc {
   fd_verify_svc_seg_t * seg;
   int      dev;
@@ -218,10 +252,17 @@ struct fd_verify_svc {
   struct { int set; u8 const * d_mcache; ulong depth; u8 const * d_base; ulong chunk0, wmark; } link[FD_VERIFY_SVC_LINK_MAX];
   svc_tile tile[FD_VERIFY_SVC_TILE_MAX];
   u8 *     d_stage;            /* staging: tile x slot x slot_cap frags of FD_TXN_HIP_STAGE_CHUNKS */
+  u8 *     d_ing;              /* ingest: tile x slot x slot_cap frags of SVC_INGEST_CHUNKS */
+  u16 *    d_ing_sz; u8 * d_ing_kind; u32 * d_ing_tso;   /* per ingest frag */
+  hipStream_t st_ing;
+  svc_ingest ING[SVC_ING_MAX];
+  ulong    ing_take, ing_fin;  /* ingest batches started / retired (ring order) */
+  svc_desc * sdesc;            /* per (tile, slot): the request's descriptor, made at ingest */
   svc_launch L[SVC_LAUNCH_MAX];
   svc_pend * pend; ulong pend_cap, pend_head, pend_tail, pend_frags;
   ulong    stat[16];           /* launches, frags, requests, flushes, flushed frags, flushed bytes, spans, gpu ns;
-                                  host ns starting launches, starting flushes, retiring, polls */
+                                  host ns starting launches, starting flushes, retiring, polls; ingests, ingest
+                                  gpu ns, host ns starting ingests, the largest launch */
   long     merge_idle_ns;      /* a launch on an idle GPU once the oldest request has waited this long */
   int      running;
 };
@@ -244,7 +285,6 @@ static void launch_alloc( svc_launch & L, int dev, ulong nmax ) {
   L.ctx  = fd_ed25519_hip_ctx_new( dev, L.rcap );
   if( !L.ctx ) { fprintf( stderr, "fd_verify_svc: context creation failed\n" ); abort(); }
   L.st = (hipStream_t)fd_ed25519_hip_ctx_stream( L.ctx );
-  SV_CHECK( hipMalloc( &L.d_ingest, 64ul * SVC_INGEST_CHUNKS * nmax ) );
   SV_CHECK( hipMalloc( &L.d_in_chunk, 4ul * nmax ) ); SV_CHECK( hipMalloc( &L.d_in_sz, 2ul * nmax ) );
   SV_CHECK( hipMalloc( &L.d_in_kind, nmax ) );        SV_CHECK( hipMalloc( &L.d_tso, 4ul * nmax ) );
   SV_CHECK( hipMalloc( &L.d_seed, 8ul * nmax ) );     SV_CHECK( hipMalloc( &L.d_stage_chunk, 4ul * nmax ) );
@@ -264,7 +304,7 @@ static void launch_alloc( svc_launch & L, int dev, ulong nmax ) {
 static void launch_free( svc_launch & L ) {
   if( !L.ctx ) return;
   (void)hipStreamSynchronize( L.st );
-  (void)hipFree( L.d_ingest ); (void)hipFree( L.d_in_chunk ); (void)hipFree( L.d_in_sz ); (void)hipFree( L.d_in_kind );
+  (void)hipFree( L.d_in_chunk ); (void)hipFree( L.d_in_sz ); (void)hipFree( L.d_in_kind );
   (void)hipFree( L.d_tso ); (void)hipFree( L.d_seed ); (void)hipFree( L.d_stage_chunk ); (void)hipFree( L.d_tsz );
   (void)hipFree( L.d_tag ); (void)hipFree( L.d_bid ); (void)hipFree( L.d_first ); (void)hipFree( L.d_cnt );
   (void)hipFree( L.d_tcode ); (void)hipFree( L.d_misc ); (void)hipFree( L.d_rsig ); (void)hipFree( L.d_rpub );
@@ -286,11 +326,28 @@ fd_verify_svc_boot( void * seg_mem, int device, ulong batch_max, ulong inflight 
     fprintf( stderr, "fd_verify_svc: staging %lu B over 4 GiB (tiles x req_depth x slot_cap too large)\n", stage_sz );
     return 0;
   }
+  /* ingest frags are addressed by 32-bit chunk indices (the parse's in_chunk) */
+  ulong const ing_cnt = seg->tile_cnt * seg->req_depth * seg->slot_cap;
+  if( SVC_INGEST_CHUNKS * ing_cnt >= (1ul << 32) ) {
+    fprintf( stderr, "fd_verify_svc: %lu ingest frags over the 32-bit chunk index\n", ing_cnt );
+    return 0;
+  }
   SV_CHECK( hipSetDevice( device ) );
   fd_verify_svc_t * s = (fd_verify_svc_t *)calloc( 1, sizeof(fd_verify_svc_t) );
   s->seg = seg; s->dev = device; s->batch_max = batch_max; s->inflight = inflight;
   s->merge_min = batch_max / 2ul; s->merge_wait_ns = 400000L; s->merge_idle_ns = 20000L;
   SV_CHECK( hipMalloc( &s->d_stage, stage_sz + 4096ul ) );
+  SV_CHECK( hipMalloc( &s->d_ing, 64ul * SVC_INGEST_CHUNKS * ing_cnt + 4096ul ) );
+  SV_CHECK( hipMalloc( &s->d_ing_sz, 2ul * ing_cnt ) ); SV_CHECK( hipMalloc( &s->d_ing_kind, ing_cnt ) );
+  SV_CHECK( hipMalloc( &s->d_ing_tso, 4ul * ing_cnt ) );
+  SV_CHECK( hipStreamCreateWithFlags( &s->st_ing, hipStreamNonBlocking ) );
+  for( ulong k = 0; k < SVC_ING_MAX; k++ ) {
+    svc_ingest & I = s->ING[k];
+    SV_CHECK( hipHostMalloc( &I.h_desc, sizeof(svc_desc) * SVC_REQ_MAX, 0 ) );
+    SV_CHECK( hipMalloc( &I.d_desc, sizeof(svc_desc) * SVC_REQ_MAX ) );
+    SV_CHECK( hipEventCreate( &I.ev0 ) ); SV_CHECK( hipEventCreate( &I.ev1 ) );
+  }
+  s->sdesc = (svc_desc *)calloc( seg->tile_cnt * seg->req_depth, sizeof(svc_desc) );
   for( ulong k = 0; k < inflight; k++ ) launch_alloc( s->L[k], device, batch_max );
   s->pend_cap = seg->tile_cnt * seg->req_depth;
   s->pend = (svc_pend *)calloc( s->pend_cap, sizeof(svc_pend) );
@@ -352,12 +409,15 @@ fd_verify_svc_run( fd_verify_svc_t * s ) {
      the first request (the steady state loads nothing) */
   for( ulong k = 0; k < s->inflight; k++ ) {
     svc_launch & L = s->L[k];
-    hipLaunchKernelGGL( k_svc_gather, dim3( 1 ), dim3( 256 ), 0, L.st, L.d_desc, 0u, 0ul, L.d_ingest, s->d_stage,
-                        L.d_in_chunk, L.d_in_sz, L.d_in_kind, L.d_tso, L.d_seed, L.d_stage_chunk );
+    hipLaunchKernelGGL( k_svc_assemble, dim3( 1 ), dim3( 256 ), 0, L.st, L.d_desc, 0u, 0ul, s->d_ing_sz, s->d_ing_kind,
+                        s->d_ing_tso, L.d_in_chunk, L.d_in_sz, L.d_in_kind, L.d_tso, L.d_seed, L.d_stage_chunk );
     hipLaunchKernelGGL( k_svc_results, dim3( 1 ), dim3( 256 ), 0, L.st, 0ul, L.d_tsz, L.d_tag, L.d_bid, L.d_cnt,
                         L.d_tcode, L.d_fdesc, L.d_tso, L.d_res );
     SV_CHECK( hipGetLastError() );
   }
+  hipLaunchKernelGGL( k_svc_gather, dim3( 1 ), dim3( 256 ), 0, s->st_ing, s->ING[0].d_desc, 0u, 0ul, s->d_ing, s->d_ing_sz,
+                      s->d_ing_kind, s->d_ing_tso, s->d_stage );
+  SV_CHECK( hipGetLastError() );
   for( ulong t = 0; t < s->seg->tile_cnt; t++ ) {
     hipLaunchKernelGGL( k_svc_compact, dim3( 1 ), dim3( 256 ), 0, s->tile[t].st, (fd_verify_svc_out_t const *)0, 0ul,
                         (u8 const *)s->d_stage, 0ul, s->tile[t].d_mirror, 0L );
@@ -376,6 +436,7 @@ svc_desc_of( fd_verify_svc_t * s, ulong t, ulong slot, ulong base, svc_desc & d 
   fd_verify_svc_req_t const * r = fd_verify_svc_req( g, t, slot );
   memset( &d, 0, sizeof(d) );
   d.base = base; d.n = r->n; d.kind = r->kind; d.seed = r->seed; d.stage0 = svc_stage0( s, t, slot );
+  d.ibase = (t * g->req_depth + slot) * g->slot_cap;
   if( r->kind == FD_VERIFY_SVC_REQ_RANGE ) {
     if( r->link >= FD_VERIFY_SVC_LINK_MAX || !s->link[r->link].set || !r->rr_cnt || r->rr_idx >= r->rr_cnt ||
         r->seq_cnt > s->link[r->link].depth ||
@@ -401,6 +462,7 @@ svc_desc_of( fd_verify_svc_t * s, ulong t, ulong slot, ulong base, svc_desc & d 
   }
 }
 
+/* a verify launch over ingested requests (their descriptors were made at ingest) */
 static void
 svc_launch_start( fd_verify_svc_t * s, svc_launch & L ) {
   fd_verify_svc_seg_t * g = s->seg;
@@ -409,7 +471,8 @@ svc_launch_start( fd_verify_svc_t * s, svc_launch & L ) {
   while( s->pend_head != s->pend_tail && L.nreq < SVC_REQ_MAX ) {
     svc_pend const & p = s->pend[s->pend_head % s->pend_cap];
     if( n + p.n > s->batch_max ) break;
-    svc_desc_of( s, p.t, p.slot, n, L.h_desc[L.nreq] );
+    L.h_desc[L.nreq] = s->sdesc[p.t * g->req_depth + p.slot];
+    L.h_desc[L.nreq].base = n;
     L.req[L.nreq].t = p.t; L.req[L.nreq].slot = p.slot;
     L.nreq++; n += p.n;
     s->pend_frags -= p.n; s->pend_head++;
@@ -418,10 +481,11 @@ svc_launch_start( fd_verify_svc_t * s, svc_launch & L ) {
   SV_CHECK( hipSetDevice( s->dev ) );
   SV_CHECK( hipEventRecord( L.ev0, L.st ) );
   SV_CHECK( hipMemcpyAsync( L.d_desc, L.h_desc, sizeof(svc_desc) * L.nreq, hipMemcpyHostToDevice, L.st ) );
-  hipLaunchKernelGGL( k_svc_gather, dim3( (unsigned)((n + 3ul) / 4ul) ), dim3( 256 ), 0, L.st, L.d_desc, (u32)L.nreq, n,
-                      L.d_ingest, s->d_stage, L.d_in_chunk, L.d_in_sz, L.d_in_kind, L.d_tso, L.d_seed, L.d_stage_chunk );
+  hipLaunchKernelGGL( k_svc_assemble, dim3( (unsigned)((n + 255ul) / 256ul) ), dim3( 256 ), 0, L.st, L.d_desc, (u32)L.nreq,
+                      n, s->d_ing_sz, s->d_ing_kind, s->d_ing_tso, L.d_in_chunk, L.d_in_sz, L.d_in_kind, L.d_tso, L.d_seed,
+                      L.d_stage_chunk );
   SV_CHECK( hipGetLastError() );
-  fd_txn_hip_batch_core( L.ctx, L.st, n, L.d_ingest, L.d_in_chunk, L.d_in_sz, L.d_in_kind, s->d_stage, L.d_stage_chunk,
+  fd_txn_hip_batch_core( L.ctx, L.st, n, s->d_ing, L.d_in_chunk, L.d_in_sz, L.d_in_kind, s->d_stage, L.d_stage_chunk,
                          L.d_seed, L.d_tsz, L.d_tag, L.d_bid, L.d_first, L.d_cnt, L.d_misc, L.d_rsig, L.d_rpub,
                          L.d_rmoff, L.d_rmsz, L.rcap, L.d_rcode, L.d_tcode, L.d_fdesc );
   hipLaunchKernelGGL( k_svc_results, dim3( (unsigned)((n + 255ul) / 256ul) ), dim3( 256 ), 0, L.st, n, L.d_tsz, L.d_tag,
@@ -434,6 +498,22 @@ svc_launch_start( fd_verify_svc_t * s, svc_launch & L ) {
   }
   SV_CHECK( hipEventRecord( L.ev1, L.st ) );
   s->stat[0]++; s->stat[1] += n; s->stat[2] += L.nreq;
+  if( n > s->stat[15] ) s->stat[15] = n;
+}
+
+/* the gather of the newly posted requests in I (their frags into the slots'
+   HBM ingest frags), on the ingest stream */
+static void
+svc_ingest_start( fd_verify_svc_t * s, svc_ingest & I ) {
+  SV_CHECK( hipSetDevice( s->dev ) );
+  SV_CHECK( hipEventRecord( I.ev0, s->st_ing ) );
+  SV_CHECK( hipMemcpyAsync( I.d_desc, I.h_desc, sizeof(svc_desc) * I.nreq, hipMemcpyHostToDevice, s->st_ing ) );
+  hipLaunchKernelGGL( k_svc_gather, dim3( (unsigned)((I.n + 3ul) / 4ul) ), dim3( 256 ), 0, s->st_ing, I.d_desc,
+                      (u32)I.nreq, I.n, s->d_ing, s->d_ing_sz, s->d_ing_kind, s->d_ing_tso, s->d_stage );
+  SV_CHECK( hipGetLastError() );
+  SV_CHECK( hipEventRecord( I.ev1, s->st_ing ) );
+  I.busy = 1;
+  s->stat[12]++;
 }
 
 static void
@@ -486,7 +566,7 @@ fd_verify_svc_poll( fd_verify_svc_t * s ) {
   SV_CHECK( hipSetDevice( s->dev ) );
   g->svc_heartbeat++;
   s->stat[11]++;
-  /* 1. finished launches: their slots' results are in the segment */
+  /* 1. finished verify launches: their slots' results are in the segment */
   ulong busy = 0;
   for( ulong k = 0; k < s->inflight; k++ ) {
     svc_launch & L = s->L[k];
@@ -503,6 +583,25 @@ fd_verify_svc_poll( fd_verify_svc_t * s ) {
       fd_verify_svc_st( &q->state, FD_VERIFY_SVC_RESULTS );
     }
     L.busy = 0; did = 1;
+  }
+  /* 1b. finished ingests, in order: their requests' frags are in HBM (the
+     tiles may reuse the link space) and wait for a verify launch */
+  long const now0 = svc_now_ns();
+  while( s->ing_fin < s->ing_take ) {
+    svc_ingest & I = s->ING[s->ing_fin % SVC_ING_MAX];
+    hipError_t e = hipEventQuery( I.ev1 );
+    if( e == hipErrorNotReady ) break;
+    SV_CHECK( e );
+    float ms = 0.f;
+    SV_CHECK( hipEventElapsedTime( &ms, I.ev0, I.ev1 ) );
+    s->stat[13] += (ulong)((double)ms * 1e6);
+    for( ulong r = 0; r < I.nreq; r++ ) {
+      fd_verify_svc_st( &fd_verify_svc_req( g, I.req[r].t, I.req[r].slot )->state, FD_VERIFY_SVC_INGESTED );
+      svc_pend & p = s->pend[s->pend_tail % s->pend_cap];
+      p.t = I.req[r].t; p.slot = I.req[r].slot; p.n = I.h_desc[r].n; p.seen = now0;
+      s->pend_tail++; s->pend_frags += p.n;
+    }
+    I.busy = 0; s->ing_fin++; did = 1;
   }
   /* 2. flushes: retire in order, start the newly posted */
   for( ulong t = 0; t < g->tile_cnt; t++ ) {
@@ -527,32 +626,42 @@ fd_verify_svc_poll( fd_verify_svc_t * s ) {
       T.flush_take++; did = 1;
     }
   }
-  s->stat[9] += (ulong)(svc_now_ns() - p1);
-  /* 3. posted requests, in each tile's ring order */
-  long const now = svc_now_ns();
-  for( ulong t = 0; t < g->tile_cnt; t++ ) {
-    svc_tile & T = s->tile[t];
-    while( s->pend_tail - s->pend_head < s->pend_cap ) {
-      ulong slot = T.take & (g->req_depth - 1ul);
-      fd_verify_svc_req_t * q = fd_verify_svc_req( g, t, slot );
-      if( fd_verify_svc_ld( &q->state ) != FD_VERIFY_SVC_POSTED ) break;
-      if( q->id + g->req_depth == T.take ) break;            /* the slot's previous request, still on the GPU */
-      if( q->id != T.take ) {
-        fprintf( stderr, "fd_verify_svc: tile %lu posted request %lu in slot %lu, expected %lu\n", t, q->id, slot, T.take );
-        abort();
+  long const p2 = svc_now_ns();
+  s->stat[9] += (ulong)(p2 - p1);
+  /* 3. posted requests, in each tile's ring order, into one ingest batch
+     (a request waits while every ingest slot is busy) */
+  if( s->ing_take - s->ing_fin < SVC_ING_MAX ) {
+    svc_ingest & I = s->ING[s->ing_take % SVC_ING_MAX];
+    I.nreq = 0; I.n = 0;
+    for( ulong t = 0; t < g->tile_cnt && I.nreq < SVC_REQ_MAX; t++ ) {
+      svc_tile & T = s->tile[t];
+      while( I.nreq < SVC_REQ_MAX ) {
+        ulong slot = T.take & (g->req_depth - 1ul);
+        fd_verify_svc_req_t * q = fd_verify_svc_req( g, t, slot );
+        if( fd_verify_svc_ld( &q->state ) != FD_VERIFY_SVC_POSTED ) break;
+        if( q->id + g->req_depth == T.take ) break;          /* the slot's previous request, still on the GPU */
+        if( q->id != T.take ) {
+          fprintf( stderr, "fd_verify_svc: tile %lu posted request %lu in slot %lu, expected %lu\n", t, q->id, slot, T.take );
+          abort();
+        }
+        T.take++; did = 1;
+        if( !q->n ) {                                        /* nothing to verify: results at once */
+          q->batch_frags = 0; fd_verify_svc_st( &q->state, FD_VERIFY_SVC_RESULTS );
+          continue;
+        }
+        svc_desc & d = s->sdesc[t * g->req_depth + slot];
+        svc_desc_of( s, t, slot, I.n, d );
+        I.h_desc[I.nreq] = d;
+        I.req[I.nreq].t = t; I.req[I.nreq].slot = slot;
+        I.nreq++; I.n += q->n;
       }
-      T.take++; did = 1;
-      if( !q->n ) {                                          /* nothing to verify: results at once */
-        q->batch_frags = 0; fd_verify_svc_st( &q->state, FD_VERIFY_SVC_RESULTS );
-        continue;
-      }
-      svc_pend & p = s->pend[s->pend_tail % s->pend_cap];
-      p.t = t; p.slot = slot; p.n = q->n; p.seen = now;
-      s->pend_tail++; s->pend_frags += q->n;
     }
+    if( I.nreq ) { svc_ingest_start( s, I ); s->ing_take++; }
   }
-  /* 4. a launch: when the posted frags fill its merge target, or the
-     oldest has waited merge_wait_ns, or (the GPU idle) merge_idle_ns --
+  long const now = svc_now_ns();
+  s->stat[14] += (ulong)(now - p2);
+  /* 4. a verify launch: when the ingested frags fill its merge target, or
+     the oldest has waited merge_wait_ns, or (the GPU idle) merge_idle_ns --
      large launches while the GPU is busy (a 55 K-signature launch runs ~one
      wave per SIMD and costs 3x per signature), little added
      latency while it is not */
@@ -571,8 +680,8 @@ fd_verify_svc_poll( fd_verify_svc_t * s ) {
 }
 
 extern "C" void
-fd_verify_svc_stats( fd_verify_svc_t const * s, ulong out[12] ) {
-  for( int k = 0; k < 12; k++ ) out[k] = s->stat[k];
+fd_verify_svc_stats( fd_verify_svc_t const * s, ulong out[16] ) {
+  for( int k = 0; k < 16; k++ ) out[k] = s->stat[k];
 }
 
 extern "C" void
@@ -589,6 +698,14 @@ fd_verify_svc_delete( fd_verify_svc_t * s ) {
     (void)hipFree( T.d_mirror );
   }
   (void)hipFree( s->d_stage );
+  (void)hipFree( s->d_ing ); (void)hipFree( s->d_ing_sz ); (void)hipFree( s->d_ing_kind ); (void)hipFree( s->d_ing_tso );
+  for( ulong k = 0; k < SVC_ING_MAX; k++ ) {
+    svc_ingest & I = s->ING[k];
+    if( !I.h_desc ) continue;
+    (void)hipHostFree( I.h_desc ); (void)hipFree( I.d_desc ); (void)hipEventDestroy( I.ev0 ); (void)hipEventDestroy( I.ev1 );
+  }
+  if( s->st_ing ) (void)hipStreamDestroy( s->st_ing );
+  free( s->sdesc );
   for( ulong k = 0; k < s->nreg; k++ ) (void)hipHostUnregister( s->reg[k].h );
   fd_verify_svc_st( &s->seg->svc_state, FD_VERIFY_SVC_SVC_STOPPED );
   free( s->pend );

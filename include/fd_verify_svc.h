@@ -50,9 +50,15 @@
                                    FD_VERIFY_SVC_FRAG_STRIDE bytes, their
                                    sizes and kinds (tile writes; polled links)
    Protocol, per tile, single producer / single consumer, no locks:
-     slot state  FREE -(tile posts)-> POSTED -(service, results written)->
-                 RESULTS -(tile, once every published frag of the slot is
-                 out)-> FREE.  Slots are posted and consumed in ring order.
+     slot state  FREE -(tile posts)-> POSTED -(service: the GPU has read
+                 the request's frags into HBM)-> INGESTED -(service, results
+                 written)-> RESULTS -(tile, once every published frag of the
+                 slot is out)-> FREE.  Slots are posted and consumed in ring
+                 order.  INGESTED is when a range request's link lines and
+                 bytes may be reused: the tile runs the stem's overrun check
+                 and moves its fseq then, not after the verify, so the link
+                 holds a frag only for the copy (a service may go straight to
+                 RESULTS, which implies INGESTED).
      flush ring  the tile appends { slot, lo, hi } (out entries [lo, hi) of
                  the slot) and advances flush_post; the service completes
                  flushes in order and advances flush_done.
@@ -94,6 +100,9 @@ typedef unsigned long  ulong;
 #define FD_VERIFY_SVC_FREE         (0UL)
 #define FD_VERIFY_SVC_POSTED       (1UL)
 #define FD_VERIFY_SVC_RESULTS      (2UL)
+#define FD_VERIFY_SVC_INGESTED     (3UL)
+
+static inline int fd_verify_svc_state_ingested( unsigned long state ) { return state==3UL || state==2UL; }
 
 /* service states (fd_verify_svc_seg_t.svc_state) */
 #define FD_VERIFY_SVC_SVC_NONE     (0UL)
@@ -142,7 +151,7 @@ typedef struct {
    sig_cnt and batch_frags before posting; the service writes sig_cnt and
    batch_frags before RESULTS. */
 typedef struct {
-  ulong state;                          /* FD_VERIFY_SVC_{FREE,POSTED,RESULTS}: atomics only */
+  ulong state;                          /* FD_VERIFY_SVC_{FREE,POSTED,INGESTED,RESULTS}: atomics only */
   ulong kind;                           /* FD_VERIFY_SVC_REQ_* */
   ulong link;                           /* RANGE: index into the service's link table */
   ulong seq0, seq_cnt, rr_cnt, rr_idx;  /* RANGE: lines [seq0, seq0+seq_cnt), kept seq % rr_cnt == rr_idx */
@@ -364,16 +373,18 @@ static inline ulong fd_verify_svc_tiles_on( ulong gpu, ulong verify_cnt, ulong g
      tile t's verify_dedup dcache (flush target) and its chunk base.
    fd_verify_svc_run( svc ): marks the service running; then
    fd_verify_svc_poll( svc ): one iteration of the service loop (retire
-     finished launches and flushes, start flushes, merge posted requests into
-     a launch); 1 if it did anything.  Never blocks.
-   fd_verify_svc_set_merge( svc, min_frags, wait_ns, idle_ns ): a launch
-     starts once the posted requests hold min_frags frags, or the oldest has
-     waited wait_ns, or -- no launch in flight -- idle_ns (defaults
-     batch_max / 2, 400 us, 20 us).
-   fd_verify_svc_stats( svc, out[ 12 ] ): launches, frags, requests,
+     finished launches, ingests and flushes, start flushes, copy newly
+     posted requests' frags into HBM at once, merge ingested requests into a
+     verify launch); 1 if it did anything.  Never blocks.
+   fd_verify_svc_set_merge( svc, min_frags, wait_ns, idle_ns ): a verify
+     launch starts once the ingested requests hold min_frags frags, or the
+     oldest has waited wait_ns, or -- no launch in flight -- idle_ns
+     (defaults batch_max / 2, 400 us, 20 us).
+   fd_verify_svc_stats( svc, out[ 16 ] ): launches, frags, requests,
      flushes, flushed frags, flushed bytes, copy spans, GPU ns (summed over
-     launches), host ns starting launches, host ns starting flushes, host ns
-     polling events, polls.
+     verify launches), host ns starting launches, host ns starting flushes,
+     host ns polling events, polls, ingests, ingest GPU ns, host ns starting
+     ingests, the largest launch's frags.
    fd_verify_svc_delete( svc ): waits for the GPU and frees everything. */
 
 typedef struct fd_verify_svc fd_verify_svc_t;
@@ -387,7 +398,7 @@ int               fd_verify_svc_set_tile( fd_verify_svc_t * svc, ulong t, void *
 void              fd_verify_svc_set_merge( fd_verify_svc_t * svc, ulong min_frags, ulong wait_ns, ulong idle_ns );
 int               fd_verify_svc_run     ( fd_verify_svc_t * svc );
 int               fd_verify_svc_poll    ( fd_verify_svc_t * svc );
-void              fd_verify_svc_stats   ( fd_verify_svc_t const * svc, ulong out[ 12 ] );
+void              fd_verify_svc_stats   ( fd_verify_svc_t const * svc, ulong out[ 16 ] );
 void              fd_verify_svc_delete  ( fd_verify_svc_t * svc );
 
 #ifdef __cplusplus

@@ -79,9 +79,9 @@ main( int argc, char ** argv ) {
     if( !fd_verify_svc_poll( svc ) ) FD_SPIN_PAUSE();
     if( !( it & 0xffffUL ) && fd_log_wallclock()>deadline ) FD_LOG_ERR(( "service: no shutdown after 1200 s" ));
   }
-  ulong st[ 12 ];
+  ulong st[ 16 ];
   fd_verify_svc_stats( svc, st );
-  for( ulong k=0UL; k<12UL; k++ ) hdr->svc_stats[ k ] = st[ k ];
+  for( ulong k=0UL; k<16UL; k++ ) hdr->svc_stats[ k ] = st[ k ];
   fd_verify_svc_delete( svc );
   FD_COMPILER_MFENCE();
   hdr->svc_done = 1UL;

@@ -339,10 +339,12 @@ produce( char const * path, char const * stream, ulong tile_cnt, ulong in_depth 
   print_lat( "latency_to_consumer", latq ); printf( ", " );
   printf( "\"svc\": {\"launches\": %lu, \"frags\": %lu, \"requests\": %lu, \"flushes\": %lu, \"flushed_frags\": %lu, "
           "\"flushed_bytes\": %lu, \"spans\": %lu, \"gpu_s\": %.6f, \"host_launch_s\": %.6f, \"host_flush_s\": %.6f, "
-          "\"host_poll_s\": %.6f, \"polls\": %lu}, ",
+          "\"host_poll_s\": %.6f, \"polls\": %lu, \"ingests\": %lu, \"ingest_gpu_s\": %.6f, \"host_ingest_s\": %.6f, "
+          "\"launch_max\": %lu}, ",
           hdr->svc_stats[0], hdr->svc_stats[1], hdr->svc_stats[2], hdr->svc_stats[3], hdr->svc_stats[4],
           hdr->svc_stats[5], hdr->svc_stats[6], (double)hdr->svc_stats[7]*1e-9, (double)hdr->svc_stats[8]*1e-9,
-          (double)hdr->svc_stats[9]*1e-9, (double)hdr->svc_stats[10]*1e-9, hdr->svc_stats[11] );
+          (double)hdr->svc_stats[9]*1e-9, (double)hdr->svc_stats[10]*1e-9, hdr->svc_stats[11], hdr->svc_stats[12],
+          (double)hdr->svc_stats[13]*1e-9, (double)hdr->svc_stats[14]*1e-9, hdr->svc_stats[15] );
   printf( "\"frags\": %lu, \"sigs\": %lu, \"published\": %lu, \"parse_fail\": %lu, \"verify_fail\": %lu, "
           "\"dedup\": %lu, \"bundle_peer_fail\": %lu, \"overrun\": %lu, \"lapped\": %lu, \"host_redone\": %lu, "
           "\"consumed\": %lu, \"consumer_bad\": %lu, \"digest_on\": %d, \"metrics_ok\": %lu, \"tile_threads_max\": %lu, \"tile_dev_fds\": %lu, "
