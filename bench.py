@@ -573,9 +573,10 @@ def run_tile_leg(args):
     published frag, each tile's digest and counts against the reference's
     own parse and AVX-512 verify over that tile's share
     (oracle/_ref/libfdref_txn.so ref_verify_tile_digest).  latency: a paced
-    producer at 80% of the measured frag rate, no flow control, on the
-    reference's default quic_verify depth (16384): tspub - tsorig
-    percentiles and the overruns.  Binaries are built from the reference
+    producer with no flow control on the reference's default quic_verify
+    depth (16384), at the highest of 80/50/30/15/8% of the measured frag
+    rate that loses no frag: tspub - tsorig percentiles and the overruns
+    (every rate tried is listed).  Binaries are built from the reference
     sources in the build container (integration/_build); without them the
     leg reports why and the line goes on."""
     sys.path.insert(0, os.path.join(REPO, "tools"))
@@ -610,10 +611,17 @@ def run_tile_leg(args):
             ref = SI.ref_share_digests(s.pool, s.off, s.sz, None, tb, 0x7f4a11, 4194302, threads=16)
             got = [SI.tile_counts(x) for x in d["tiles"]]
             equal = all(g == {k: r[k] for k in g} for g, r in zip(got, ref)) and d["consumer_bad"] == 0
-            # latency at the reference's link depth, paced below the measured rate
-            rate = int(0.8 * best["frags_per_s"])
-            lat = SB.run_one(stream, tb, 16384, 180, os.path.join(logdir, "paced"), env=dict(pre, SVC_RUN_RATE=str(rate)),
-                            pin="auto")
+            # latency at the reference's link depth: a paced producer with no flow control, at the
+            # highest of a few fractions of the measured rate that loses no frag
+            tried = []
+            for frac in (0.8, 0.5, 0.3, 0.15, 0.08):
+                rate = int(frac * best["frags_per_s"])
+                lat = SB.run_one(stream, tb, 16384, 180, os.path.join(logdir, f"paced{frac}"),
+                                 env=dict(pre, SVC_RUN_RATE=str(rate)), pin="auto")
+                tried.append({"offered_frags_per_s": rate, "lost": lat["overrun"] + lat["lapped"],
+                              "p50_us": lat["latency"]["p50_us"], "p99_us": lat["latency"]["p99_us"]})
+                if not lat["overrun"] and not lat["lapped"]:
+                    break
         return {"value": best["verifies_per_s"] if ok else None, "unit": "verifies/s",
                 "frags_per_s": best["frags_per_s"], "frags": best["frags"], "sigs": best["sigs"],
                 "published": best["published"], "overrun": best["overrun"], "seconds": best["seconds"],
@@ -627,7 +635,7 @@ def run_tile_leg(args):
                 "latency_us": {"p50": lat["latency"]["p50_us"], "p99": lat["latency"]["p99_us"],
                                "p999": lat["latency"]["p999_us"], "offered_frags_per_s": rate,
                                "in_depth": 16384, "overrun": lat["overrun"], "lapped": lat["lapped"],
-                               "achieved_verifies_per_s": lat["verifies_per_s"]},
+                               "achieved_verifies_per_s": lat["verifies_per_s"], "tried": tried},
                 "config": {"tiles": tb, "gpus": 1, "range_max": best["range_max"], "slot_cap": best["slot_cap"],
                            "req_depth": best["req_depth"], "out_depth": best["out_depth"], "in_depth": depth,
                            "prelay": True,

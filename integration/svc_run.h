@@ -24,7 +24,7 @@
 
 typedef struct {
   volatile long  t_end;
-  volatile ulong done, frags, sigs, pub, parse, verify, dedup, bundle, overrun, lapped, host;
+  volatile ulong done, frags, sigs, pub, parse, verify, dedup, bundle, overrun, lapped, host, early;
   volatile ulong regime[ 8 ];                  /* the stem's REGIME_DURATION_NANOS ticks (fd_stem.c:406-712) */
   volatile ulong link_consumed, link_filtered, link_ovr_poll, link_ovr_poll_frags, link_ovr_read, link_ovr_read_frags;
   volatile ulong metrics_ok;                   /* the link-in metric slots hold the tile's counts */

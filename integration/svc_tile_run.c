@@ -325,11 +325,11 @@ produce( char const * path, char const * stream, ulong tile_cnt, ulong in_depth 
             "\"consumed\": %lu, \"digest\": \"%016lx\", \"threads\": %lu, \"dev_fds\": %lu, \"metrics_ok\": %lu, \"sandboxed\": %lu, "
             "\"link\": {\"consumed\": %lu, \"filtered\": %lu, \"overrun_polling\": %lu, \"overrun_polling_frags\": %lu, "
             "\"overrun_reading\": %lu, \"overrun_reading_frags\": %lu}, "
-            "\"busy_s\": {\"publish\": %.4f, \"pass\": %.4f, \"flush\": %.4f, \"post\": %.4f}}",
+            "\"busy_s\": {\"publish\": %.4f, \"pass\": %.4f, \"flush\": %.4f, \"post\": %.4f}, \"early_credits\": %lu}",
             t ? ", " : "", r->frags, r->sigs, r->pub, r->parse, r->verify, r->dedup, r->bundle, r->overrun, r->lapped,
             (double)( r->t_end - t0 )*1e-9, c->frags, c->digest, r->threads, r->dev_fds, r->metrics_ok, r->sandboxed,
             r->link_consumed, r->link_filtered, r->link_ovr_poll, r->link_ovr_poll_frags, r->link_ovr_read,
-            r->link_ovr_read_frags, r->sec_pub, r->sec_pass, r->sec_flush, r->sec_post );
+            r->link_ovr_read_frags, r->sec_pub, r->sec_pass, r->sec_flush, r->sec_post, r->early );
   }
   double s  = (double)( t_end - t0 )*1e-9;
   double rt = (double)( reg[0]+reg[1]+reg[2]+reg[3]+reg[4]+reg[5]+reg[6]+reg[7] ) + 1e-9;
@@ -553,7 +553,7 @@ tile( char const * path, ulong t ) {
   r->parse  = ctx->metrics.parse_fail_cnt; r->verify = ctx->metrics.verify_fail_cnt; r->dedup = ctx->metrics.dedup_fail_cnt;
   r->bundle = ctx->metrics.bundle_peer_fail_cnt;
   r->frags  = r->pub + r->parse + r->verify + r->dedup + r->bundle;
-  r->sigs   = ctx->svc_sig_cnt; r->overrun = lrf; r->lapped = lpf; r->host = ctx->svc_host_cnt;
+  r->sigs   = ctx->svc_sig_cnt; r->overrun = lrf; r->lapped = lpf; r->host = ctx->svc_host_cnt; r->early = ctx->svc_early_cnt;
   r->link_consumed = lc; r->link_filtered = lfl; r->link_ovr_poll = lp; r->link_ovr_poll_frags = lpf;
   r->link_ovr_read = lr; r->link_ovr_read_frags = lrf;
   /* the link-in metric slots after the polled ones hold the range links' counts (metrics_write) */

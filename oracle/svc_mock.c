@@ -12,7 +12,13 @@
    the overrun checks) without a GPU; the product's GPU tile is
    firedancer_amd/csrc/fd_verify_svc.hip, which never uses this file.
 
-     svc_mock <shm> <gpu (ignored)>       (same command line as svc_run) */
+     svc_mock <shm> <gpu (ignored)>       (same command line as svc_run)
+
+   SVC_MOCK_INGEST=us: answer in two steps as the GPU tile does -- copy a
+   posted request's frags (the link's bytes) into staging and mark it
+   INGESTED, then, at least `us` microseconds later, parse and verify from
+   staging only and mark it RESULTS (the tile returns the link's credits in
+   between); default: both at once, straight to RESULTS. */
 
 #include "../../tango/mcache/fd_mcache.h"
 #include "../../tango/dcache/fd_dcache.h"
@@ -39,29 +45,33 @@ void fd_halt( void ) {}
 
 static uchar * stage;                          /* tile x slot x slot_cap staging frags */
 static fd_sha512_t * shas[ 16 ];
+typedef struct { uchar flags; uchar kind; uint tsorig; } meta_t;
+static meta_t * meta;                          /* per staging frag: what the ingest saw */
 
 static uchar *
 stage_of( fd_verify_svc_seg_t * s, ulong t, ulong slot, ulong j ) {
   return stage + ( ( t*s->req_depth + slot )*s->slot_cap + j )*STAGE_SZ;
 }
 
+/* the ingest: before_frag's share, during_frag's checks and copy (or a
+   gossip vote's conversion) into staging; nothing after this reads the link */
 static void
-answer( svc_run_hdr_t * hdr, uchar * base, fd_verify_svc_seg_t * s, ulong t, ulong slot ) {
-  fd_verify_svc_req_t * q   = fd_verify_svc_req( s, t, slot );
-  fd_verify_svc_res_t * res = fd_verify_svc_res( s, t, slot );
+ingest( svc_run_hdr_t * hdr, uchar * base, fd_verify_svc_seg_t * s, ulong t, ulong slot ) {
+  fd_verify_svc_req_t * q = fd_verify_svc_req( s, t, slot );
   for( ulong j=0UL; j<q->n; j++ ) {
-    fd_verify_svc_res_t r; memset( &r, 0, sizeof(r) );
+    meta_t * m = &meta[ ( t*s->req_depth + slot )*s->slot_cap + j ];
     uchar * dst = stage_of( s, t, slot, j );
     ulong sz = 0UL, kind = 0UL;                                  /* FD_VERIFY_HIP_IN_QUIC */
     int   ok = 1;
     uchar const * src = NULL;
+    m->flags = 0; m->tsorig = 0U;
     if( q->kind==FD_VERIFY_SVC_REQ_RANGE ) {
       ulong first = fd_verify_svc_range_first( q->seq0, q->rr_cnt, q->rr_idx ), seq = first + j*q->rr_cnt;
       fd_frag_meta_t const * mc   = fd_mcache_join( base + hdr->mcache_off[ q->link ] );
       ulong                  dpth = fd_mcache_depth( mc );
       fd_frag_meta_t const * line = mc + fd_mcache_line_idx( seq, dpth );
       uchar const *          dc   = fd_dcache_join( base + hdr->dcache_off[ q->link ] );
-      ulong chunk = line->chunk; sz = line->sz; r.tsorig = line->tsorig;
+      ulong chunk = line->chunk; sz = line->sz; m->tsorig = line->tsorig;
       ok  = line->seq==seq && chunk>=fd_dcache_compact_chunk0( base, dc ) &&
             chunk<=fd_dcache_compact_wmark( base, dc, FD_TPU_REASM_MTU ) && sz<=FD_TPU_RAW_MTU;
       src = (uchar const *)fd_chunk_to_laddr_const( base, chunk );
@@ -71,21 +81,37 @@ answer( svc_run_hdr_t * hdr, uchar * base, fd_verify_svc_seg_t * s, ulong t, ulo
       kind = fd_verify_svc_frag_kind( s, t, slot )[ j ];
       ok   = sz<=( kind==2UL ? 2048UL : FD_TPU_RAW_MTU );
     }
-    if( !ok ) { r.flags = FD_VERIFY_SVC_RES_BAD; res[ j ] = r; continue; }
+    m->kind = (uchar)kind;
+    if( !ok ) { m->flags = FD_VERIFY_SVC_RES_BAD; continue; }
     fd_txn_m_t * txnm = (fd_txn_m_t *)dst;
     if( kind==2UL ) {                                            /* during_frag's vote conversion, fd_verify_tile.c:86-97 */
       fd_gossip_update_message_t const * msg = (fd_gossip_update_message_t const *)src;
       memset( dst, 0, sizeof(fd_txn_m_t) );
-      if( msg->vote.txn_sz>FD_TPU_MTU ) { r.flags = FD_VERIFY_SVC_RES_BAD; res[ j ] = r; continue; }
+      if( msg->vote.txn_sz>FD_TPU_MTU ) { m->flags = FD_VERIFY_SVC_RES_BAD; continue; }
       txnm->payload_sz = (ushort)msg->vote.txn_sz; txnm->block_engine.bundle_id = 0UL;
       txnm->source_ipv4 = msg->vote.socket.addr; txnm->source_tpu = FD_TXN_M_TPU_SOURCE_GOSSIP;
       memcpy( fd_txn_m_payload( txnm ), msg->vote.txn, msg->vote.txn_sz );
     } else {
       memset( dst, 0, STAGE_SZ );
       memcpy( dst, src, sz );
-      if( txnm->payload_sz>FD_TPU_MTU ) { r.flags = FD_VERIFY_SVC_RES_BAD; res[ j ] = r; continue; }
-      if( sz<sizeof(fd_txn_m_t) + txnm->payload_sz ) r.flags = FD_VERIFY_SVC_RES_HOST;
+      if( txnm->payload_sz>FD_TPU_MTU ) { m->flags = FD_VERIFY_SVC_RES_BAD; continue; }
+      if( sz<sizeof(fd_txn_m_t) + txnm->payload_sz ) m->flags = FD_VERIFY_SVC_RES_HOST;
     }
+  }
+}
+
+/* the verify, from staging: fd_txn_parse, the sig0 tag, the reference's
+   fd_ed25519_verify_batch_single_msg */
+static void
+answer( fd_verify_svc_seg_t * s, ulong t, ulong slot ) {
+  fd_verify_svc_req_t * q   = fd_verify_svc_req( s, t, slot );
+  fd_verify_svc_res_t * res = fd_verify_svc_res( s, t, slot );
+  for( ulong j=0UL; j<q->n; j++ ) {
+    meta_t const * m = &meta[ ( t*s->req_depth + slot )*s->slot_cap + j ];
+    fd_verify_svc_res_t r; memset( &r, 0, sizeof(r) );
+    r.flags = m->flags; r.tsorig = m->tsorig;
+    if( m->flags & FD_VERIFY_SVC_RES_BAD ) { res[ j ] = r; continue; }
+    fd_txn_m_t * txnm = (fd_txn_m_t *)stage_of( s, t, slot, j );
     fd_txn_t * txnt = fd_txn_m_txn_t( txnm );
     txnm->txn_t_sz = (ushort)fd_txn_parse( fd_txn_m_payload( txnm ), txnm->payload_sz, txnt, NULL );
     r.txn_t_sz = txnm->txn_t_sz; r.payload_sz = txnm->payload_sz; r.bundle_id = txnm->block_engine.bundle_id;
@@ -118,7 +144,12 @@ main( int argc, char ** argv ) {
   fd_verify_svc_seg_t * s = fd_verify_svc_join( base + hdr->svc_off );
   FD_TEST( s );
   stage = malloc( s->tile_cnt*s->req_depth*s->slot_cap*STAGE_SZ );
-  FD_TEST( stage );
+  meta  = malloc( s->tile_cnt*s->req_depth*s->slot_cap*sizeof(meta_t) );
+  FD_TEST( stage && meta );
+  char const * ing_env = getenv( "SVC_MOCK_INGEST" );
+  long const   ing_ns  = ing_env ? 1000L*strtol( ing_env, NULL, 0 ) : -1L;   /* -1: straight to RESULTS */
+  ulong vtake[ FD_VERIFY_SVC_TILE_MAX ] = { 0UL };                  /* requests verified (ingest mode) */
+  long  ing_at[ FD_VERIFY_SVC_TILE_MAX ][ 256 ];                    /* when each slot was ingested */
   for( ulong k=0UL; k<16UL; k++ ) shas[ k ] = fd_sha512_join( fd_sha512_new( aligned_alloc( FD_SHA512_ALIGN, FD_SHA512_FOOTPRINT ) ) );
   ulong take[ FD_VERIFY_SVC_TILE_MAX ] = { 0UL }, ftake[ FD_VERIFY_SVC_TILE_MAX ] = { 0UL };
   ulong st[ 8 ] = { 0UL };
@@ -131,10 +162,19 @@ main( int argc, char ** argv ) {
         ulong slot = take[ t ] & ( s->req_depth-1UL );
         fd_verify_svc_req_t * q = fd_verify_svc_req( s, t, slot );
         if( fd_verify_svc_ld( &q->state )!=FD_VERIFY_SVC_POSTED ) break;
+        if( q->id+s->req_depth==take[ t ] ) break;               /* the slot's previous request, not yet verified */
         FD_TEST( q->id==take[ t ] );
-        answer( hdr, base, s, t, slot );
+        ingest( hdr, base, s, t, slot );
+        if( ing_ns<0L ) { answer( s, t, slot ); vtake[ t ]++; }
+        else { fd_verify_svc_st( &q->state, FD_VERIFY_SVC_INGESTED ); ing_at[ t ][ slot ] = fd_log_wallclock(); }
         st[ 0 ]++; st[ 1 ] += q->n; st[ 2 ]++;
         take[ t ]++; did = 1;
+      }
+      while( vtake[ t ]<take[ t ] ) {                            /* ingest mode: verify after the delay, in order */
+        ulong slot = vtake[ t ] & ( s->req_depth-1UL );
+        if( fd_log_wallclock()-ing_at[ t ][ slot ]<ing_ns ) break;
+        answer( s, t, slot );
+        vtake[ t ]++; did = 1;
       }
       fd_verify_svc_tile_t * b = fd_verify_svc_tile( s, t );
       ulong post = fd_verify_svc_ld( &b->flush_post );

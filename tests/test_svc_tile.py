@@ -86,6 +86,24 @@ def test_two_tiles_equal_reference_shares(stream, tmp_path):
         assert S.tile_counts(r["tiles"][t]) == S.reference_digest(read_fdo1(str(tmp_path / f"ref{t}.bin"), DEPTH)), t
 
 
+def test_credits_return_at_ingest(stream, tmp_path):
+    """the stand-in answers in two steps as the GPU tile does (ingest ->
+    INGESTED, verify 2 ms later -> RESULTS): each tile moves its link fseq at
+    INGESTED, before the results (early_credits counts those ranges), and the
+    published sequences are still the reference's; answering in one step,
+    no range returns its credits early"""
+    r = S.run(stream["path"], 2, 1 << 14, str(tmp_path / "run"), env=dict(SMALL, SVC_MOCK_INGEST="2000"), mock=True)
+    _check_run(r, stream["s"].n)
+    assert all(x["early_credits"] > 0 for x in r["tiles"])
+    for t in range(2):
+        p = str(tmp_path / f"share{t}.bin")
+        S.share_stream(p, stream["s"], stream["bid"], t, 2, SEED, DEPTH)
+        run_driver("ref", p, str(tmp_path / f"ref{t}.bin"))
+        assert S.tile_counts(r["tiles"][t]) == S.reference_digest(read_fdo1(str(tmp_path / f"ref{t}.bin"), DEPTH)), t
+    r1 = S.run(stream["path"], 2, 1 << 14, str(tmp_path / "run1"), env=SMALL, mock=True)
+    assert all(x["early_credits"] == 0 for x in r1["tiles"])
+
+
 def test_stalled_consumer_and_drops(tmp_path):
     """a third of the frags dropped (bad payloads, resends), the consumer
     stalled behind a 128-frag verify_dedup link: nothing overwritten"""
