@@ -26,16 +26,24 @@
                     HBM staging frags, fd_txn_parse, the sig0 tag with each
                     tile's seed, the signature records), the verify, the
                     per-txn fd_ed25519_verify_batch_single_msg reduce
-     k_svc_results  32-B result records; one DMA copy per request into its
-                    slot's result array, then the slot goes to RESULTS
+     k_svc_results  32-B result records, written straight into each
+                    request slot's result array in the segment (registered
+                    host memory); then the slot goes to RESULTS
 
    The out frags stay in HBM.  After its ordered pass (tcache, bundles) the
    tile posts flushes: out entries (frag, chunk, realized size) of the frags
-   it publishes, chunks assigned as after_frag assigns them.  A flush copies
-   those staging frags into an HBM mirror of the tile's out dcache at the
-   same offsets (k_svc_compact) and DMAs the covered spans -- one or two per
-   flush, contiguous because the chunks are -- into the host out dcache.  Only
-   published frags cross PCIe, and no CU waits on a PCIe write.
+   it publishes, chunks assigned as after_frag assigns them.  A flush is one
+   kernel (k_svc_compact) that writes those staging frags straight into the
+   tile's out dcache (registered host memory) at their chunks: whole 64-B
+   chunks in 16-B stores, each frag contiguous, so the PCIe writes are full
+   lines.  Only published frags cross PCIe.
+
+   Host work per step is a few HIP calls (the service thread is the one
+   core that drives every tile's GPU work): descriptors live in mapped
+   pinned memory the kernels read in place, and results and flushed frags
+   are written by kernels, not copied -- no hipMemcpy on the steady-state
+   path.  A flush costs one launch and one event, an ingest one launch and
+   two events, a verify launch its kernels and two events.
 
    Flushes of a tile run in order on the tile's own stream; requests and
    flushes of different tiles are independent.  Every HIP failure aborts
@@ -95,7 +103,8 @@ struct __attribute__((aligned(16))) svc_desc {
   u64 seed;
   u64 stage0;      /* staging chunk of the request's frag 0 */
   u64 ibase;       /* ingest frag of the request's frag 0 (slot (t, s): (t x req_depth + s) x slot_cap) */
-  u64 rsv[2];
+  u64 res;         /* the slot's result array in the segment (device address; verify launches) */
+  u64 rsv[1];
 };
 static_assert( sizeof(svc_desc) == 128, "svc_desc layout" );
 
@@ -169,11 +178,16 @@ void k_svc_assemble( svc_desc const * __restrict__ desc, u32 nreq, ulong n, u16 
 }
 
 __global__ __launch_bounds__(256)
-void k_svc_results( ulong n, u16 const * __restrict__ tsz, u64 const * __restrict__ tag, u64 const * __restrict__ bid,
-                    u8 const * __restrict__ cnt, signed char const * __restrict__ tcode, u64 const * __restrict__ fdesc,
-                    u32 const * __restrict__ tso, fd_verify_svc_res_t * __restrict__ res ) {
+void k_svc_results( svc_desc const * __restrict__ desc, u32 nreq, ulong n, u16 const * __restrict__ tsz,
+                    u64 const * __restrict__ tag, u64 const * __restrict__ bid, u8 const * __restrict__ cnt,
+                    signed char const * __restrict__ tcode, u64 const * __restrict__ fdesc, u32 const * __restrict__ tso ) {
+  __shared__ u64 sbase[SVC_REQ_MAX];
+  for( u32 i = threadIdx.x; i < nreq; i += blockDim.x ) sbase[i] = desc[i].base;
+  __syncthreads();
   ulong const j = (ulong)blockIdx.x * blockDim.x + threadIdx.x;
   if( j >= n ) return;
+  u32 lo = 0u, hi = nreq;
+  while( hi - lo > 1u ) { u32 mid = (lo + hi) >> 1; if( sbase[mid] <= j ) lo = mid; else hi = mid; }
   u64 const d = fdesc[j];
   u32 const cend = (u32)(d & 0xfffu), psz = (u32)((d >> 12) & 0x7ffu);
   bool const gossip = (d >> 33) & 1u, bad = (d >> 34) & 1u;
@@ -182,14 +196,17 @@ void k_svc_results( ulong n, u16 const * __restrict__ tsz, u64 const * __restric
   r.flags = bad ? (u8)FD_VERIFY_SVC_RES_BAD
                 : (!gossip && cend < FD_VERIFY_HIP_TXNM_SZ + psz) ? (u8)FD_VERIFY_SVC_RES_HOST : (u8)0;
   r.sig_cnt = cnt[j]; r.rsv0 = 0u; r.tsorig = tso[j]; r.rsv1 = 0u;
-  res[j] = r;
+  /* straight into the slot's result array in the (registered) segment: a
+     wave writes 2 KB contiguous */
+  ((fd_verify_svc_res_t *)desc[lo].res)[j - sbase[lo]] = r;
 }
 
 /* a flush: out entry e's staging frag (its realized bytes, in whole 64-B
-   chunks) to the tile's HBM mirror at the entry's chunk; one wave per entry */
+   chunks) straight into the tile's out dcache (registered host memory) at the
+   entry's chunk; one wave per entry, 16-B stores, a frag's bytes contiguous */
 __global__ __launch_bounds__(256)
 void k_svc_compact( fd_verify_svc_out_t const * __restrict__ out, ulong m, u8 const * __restrict__ stage,
-                    ulong stage0, u8 * __restrict__ mirror, long delta ) {
+                    ulong stage0, u8 * __restrict__ dcache, long delta ) {
   ulong const e = (ulong)blockIdx.x * 4ul + (threadIdx.x >> 6);
   u32 const lane = threadIdx.x & 63u;
   if( e >= m ) return;
@@ -197,7 +214,7 @@ void k_svc_compact( fd_verify_svc_out_t const * __restrict__ out, ulong m, u8 co
   if( o.flags & FD_VERIFY_SVC_OUT_HOSTWRITTEN ) return;
   u32 const len = ((u32)o.sz + 63u) & ~63u;
   u8 const * s = stage + 64ul * (stage0 + FD_TXN_HIP_STAGE_CHUNKS * (ulong)o.idx);
-  u8 *       d = mirror + (long)(64ul * (ulong)o.chunk) + delta;
+  u8 *       d = dcache + (long)(64ul * (ulong)o.chunk) + delta;
   for( u32 p = 16u * lane; p < len; p += 1024u ) *(uint4 *)(d + p) = *(uint4 const *)(s + p);
 }
 
@@ -212,8 +229,7 @@ struct svc_launch {
   u32 * d_in_chunk; u16 * d_in_sz; u8 * d_in_kind; u32 * d_tso; u64 * d_seed; u32 * d_stage_chunk;
   u16 * d_tsz; u64 * d_tag; u64 * d_bid; u32 * d_first; u8 * d_cnt; signed char * d_tcode; u32 * d_misc;
   u8 *  d_rsig; u8 * d_rpub; u32 * d_rmoff; u32 * d_rmsz; signed char * d_rcode; ulong rcap; u64 * d_fdesc;
-  fd_verify_svc_res_t * d_res;
-  svc_desc * h_desc; svc_desc * d_desc;
+  svc_desc * h_desc; svc_desc * d_desc;   /* mapped pinned memory: the kernels read h_desc at d_desc */
   ulong nreq, n;
   struct { ulong t, slot; } req[SVC_REQ_MAX];
 };
@@ -223,7 +239,7 @@ struct svc_tile {
   u8 *         h_out;          /* the out dcache (host) */
   ulong        out_sz;
   u8 const *   chunk_base;     /* host address of out chunk 0 */
-  u8 *         d_mirror;       /* HBM, out_sz bytes */
+  u8 *         d_out;          /* the out dcache's device address (registered) */
   hipStream_t  st;
   hipEvent_t   ev[SVC_FLUSH_Q];
   ulong        take;           /* next request id to take */
@@ -237,7 +253,7 @@ struct svc_pend { ulong t, slot, n; long seen; };
 struct svc_ingest {
   int         busy;
   hipEvent_t  ev0, ev1;
-  svc_desc *  h_desc; svc_desc * d_desc;
+  svc_desc *  h_desc; svc_desc * d_desc;   /* mapped pinned memory */
   ulong       nreq, n;
   struct { ulong t, slot; } req[SVC_REQ_MAX];
 };
@@ -260,7 +276,7 @@ struct fd_verify_svc {
   svc_desc * sdesc;            /* per (tile, slot): the request's descriptor, made at ingest */
   svc_launch L[SVC_LAUNCH_MAX];
   svc_pend * pend; ulong pend_cap, pend_head, pend_tail, pend_frags;
-  ulong    stat[16];           /* launches, frags, requests, flushes, flushed frags, flushed bytes, spans, gpu ns;
+  ulong    stat[16];           /* launches, frags, requests, flushes, flushed frags, flushed bytes, flush kernels, gpu ns;
                                   host ns starting launches, starting flushes, retiring, polls; ingests, ingest
                                   gpu ns, host ns starting ingests, the largest launch */
   long     merge_idle_ns;      /* a launch on an idle GPU once the oldest request has waited this long */
@@ -295,9 +311,8 @@ static void launch_alloc( svc_launch & L, int dev, ulong nmax ) {
   SV_CHECK( hipMalloc( &L.d_rsig, 64ul * L.rcap ) );  SV_CHECK( hipMalloc( &L.d_rpub, 32ul * L.rcap ) );
   SV_CHECK( hipMalloc( &L.d_rmoff, 4ul * L.rcap ) );  SV_CHECK( hipMalloc( &L.d_rmsz, 4ul * L.rcap ) );
   SV_CHECK( hipMalloc( &L.d_rcode, L.rcap ) );        SV_CHECK( hipMalloc( &L.d_fdesc, 8ul * nmax ) );
-  SV_CHECK( hipMalloc( &L.d_res, sizeof(fd_verify_svc_res_t) * nmax ) );
-  SV_CHECK( hipHostMalloc( &L.h_desc, sizeof(svc_desc) * SVC_REQ_MAX, 0 ) );
-  SV_CHECK( hipMalloc( &L.d_desc, sizeof(svc_desc) * SVC_REQ_MAX ) );
+  SV_CHECK( hipHostMalloc( &L.h_desc, sizeof(svc_desc) * SVC_REQ_MAX, hipHostMallocMapped ) );
+  SV_CHECK( hipHostGetDevicePointer( (void **)&L.d_desc, L.h_desc, 0 ) );
   SV_CHECK( hipEventCreate( &L.ev0 ) ); SV_CHECK( hipEventCreate( &L.ev1 ) );
 }
 
@@ -309,7 +324,7 @@ static void launch_free( svc_launch & L ) {
   (void)hipFree( L.d_tag ); (void)hipFree( L.d_bid ); (void)hipFree( L.d_first ); (void)hipFree( L.d_cnt );
   (void)hipFree( L.d_tcode ); (void)hipFree( L.d_misc ); (void)hipFree( L.d_rsig ); (void)hipFree( L.d_rpub );
   (void)hipFree( L.d_rmoff ); (void)hipFree( L.d_rmsz ); (void)hipFree( L.d_rcode ); (void)hipFree( L.d_fdesc );
-  (void)hipFree( L.d_res ); (void)hipHostFree( L.h_desc ); (void)hipFree( L.d_desc );
+  (void)hipHostFree( L.h_desc );
   (void)hipEventDestroy( L.ev0 ); (void)hipEventDestroy( L.ev1 );
   fd_ed25519_hip_ctx_delete( L.ctx );
   L.ctx = 0;
@@ -343,8 +358,8 @@ fd_verify_svc_boot( void * seg_mem, int device, ulong batch_max, ulong inflight 
   SV_CHECK( hipStreamCreateWithFlags( &s->st_ing, hipStreamNonBlocking ) );
   for( ulong k = 0; k < SVC_ING_MAX; k++ ) {
     svc_ingest & I = s->ING[k];
-    SV_CHECK( hipHostMalloc( &I.h_desc, sizeof(svc_desc) * SVC_REQ_MAX, 0 ) );
-    SV_CHECK( hipMalloc( &I.d_desc, sizeof(svc_desc) * SVC_REQ_MAX ) );
+    SV_CHECK( hipHostMalloc( &I.h_desc, sizeof(svc_desc) * SVC_REQ_MAX, hipHostMallocMapped ) );
+    SV_CHECK( hipHostGetDevicePointer( (void **)&I.d_desc, I.h_desc, 0 ) );
     SV_CHECK( hipEventCreate( &I.ev0 ) ); SV_CHECK( hipEventCreate( &I.ev1 ) );
   }
   s->sdesc = (svc_desc *)calloc( seg->tile_cnt * seg->req_depth, sizeof(svc_desc) );
@@ -386,11 +401,10 @@ extern "C" int
 fd_verify_svc_set_tile( fd_verify_svc_t * s, ulong t, void * out_dcache, ulong out_sz, void const * chunk_base ) {
   if( !s || t >= s->seg->tile_cnt || !out_dcache || !out_sz || s->tile[t].set ) return -1;
   svc_tile & T = s->tile[t];
-  (void)svc_dev( s, out_dcache, out_sz );                   /* mapped, for the DMA copies */
+  T.d_out = svc_dev( s, out_dcache, out_sz );               /* mapped: the flush kernel writes it */
   (void)svc_dev( s, fd_verify_svc_tile( s->seg, t ), s->seg->tile_sz );   /* the tile's part of the segment */
   SV_CHECK( hipSetDevice( s->dev ) );
   T.h_out = (u8 *)out_dcache; T.out_sz = out_sz; T.chunk_base = (u8 const *)chunk_base;
-  SV_CHECK( hipMalloc( &T.d_mirror, out_sz + 4096ul ) );
   SV_CHECK( hipStreamCreateWithFlags( &T.st, hipStreamNonBlocking ) );
   for( ulong k = 0; k < SVC_FLUSH_Q; k++ ) SV_CHECK( hipEventCreateWithFlags( &T.ev[k], hipEventDisableTiming ) );
   T.set = 1;
@@ -411,8 +425,8 @@ fd_verify_svc_run( fd_verify_svc_t * s ) {
     svc_launch & L = s->L[k];
     hipLaunchKernelGGL( k_svc_assemble, dim3( 1 ), dim3( 256 ), 0, L.st, L.d_desc, 0u, 0ul, s->d_ing_sz, s->d_ing_kind,
                         s->d_ing_tso, L.d_in_chunk, L.d_in_sz, L.d_in_kind, L.d_tso, L.d_seed, L.d_stage_chunk );
-    hipLaunchKernelGGL( k_svc_results, dim3( 1 ), dim3( 256 ), 0, L.st, 0ul, L.d_tsz, L.d_tag, L.d_bid, L.d_cnt,
-                        L.d_tcode, L.d_fdesc, L.d_tso, L.d_res );
+    hipLaunchKernelGGL( k_svc_results, dim3( 1 ), dim3( 256 ), 0, L.st, L.d_desc, 0u, 0ul, L.d_tsz, L.d_tag, L.d_bid,
+                        L.d_cnt, L.d_tcode, L.d_fdesc, L.d_tso );
     SV_CHECK( hipGetLastError() );
   }
   hipLaunchKernelGGL( k_svc_gather, dim3( 1 ), dim3( 256 ), 0, s->st_ing, s->ING[0].d_desc, 0u, 0ul, s->d_ing, s->d_ing_sz,
@@ -420,7 +434,7 @@ fd_verify_svc_run( fd_verify_svc_t * s ) {
   SV_CHECK( hipGetLastError() );
   for( ulong t = 0; t < s->seg->tile_cnt; t++ ) {
     hipLaunchKernelGGL( k_svc_compact, dim3( 1 ), dim3( 256 ), 0, s->tile[t].st, (fd_verify_svc_out_t const *)0, 0ul,
-                        (u8 const *)s->d_stage, 0ul, s->tile[t].d_mirror, 0L );
+                        (u8 const *)s->d_stage, 0ul, s->tile[t].d_out, 0L );
     SV_CHECK( hipGetLastError() );
   }
   SV_CHECK( hipDeviceSynchronize() );
@@ -473,6 +487,7 @@ svc_launch_start( fd_verify_svc_t * s, svc_launch & L ) {
     if( n + p.n > s->batch_max ) break;
     L.h_desc[L.nreq] = s->sdesc[p.t * g->req_depth + p.slot];
     L.h_desc[L.nreq].base = n;
+    L.h_desc[L.nreq].res  = (u64)svc_dev( s, fd_verify_svc_res( g, p.t, p.slot ), sizeof(fd_verify_svc_res_t) * p.n );
     L.req[L.nreq].t = p.t; L.req[L.nreq].slot = p.slot;
     L.nreq++; n += p.n;
     s->pend_frags -= p.n; s->pend_head++;
@@ -480,7 +495,6 @@ svc_launch_start( fd_verify_svc_t * s, svc_launch & L ) {
   L.n = n; L.busy = 1;
   SV_CHECK( hipSetDevice( s->dev ) );
   SV_CHECK( hipEventRecord( L.ev0, L.st ) );
-  SV_CHECK( hipMemcpyAsync( L.d_desc, L.h_desc, sizeof(svc_desc) * L.nreq, hipMemcpyHostToDevice, L.st ) );
   hipLaunchKernelGGL( k_svc_assemble, dim3( (unsigned)((n + 255ul) / 256ul) ), dim3( 256 ), 0, L.st, L.d_desc, (u32)L.nreq,
                       n, s->d_ing_sz, s->d_ing_kind, s->d_ing_tso, L.d_in_chunk, L.d_in_sz, L.d_in_kind, L.d_tso, L.d_seed,
                       L.d_stage_chunk );
@@ -488,14 +502,9 @@ svc_launch_start( fd_verify_svc_t * s, svc_launch & L ) {
   fd_txn_hip_batch_core( L.ctx, L.st, n, s->d_ing, L.d_in_chunk, L.d_in_sz, L.d_in_kind, s->d_stage, L.d_stage_chunk,
                          L.d_seed, L.d_tsz, L.d_tag, L.d_bid, L.d_first, L.d_cnt, L.d_misc, L.d_rsig, L.d_rpub,
                          L.d_rmoff, L.d_rmsz, L.rcap, L.d_rcode, L.d_tcode, L.d_fdesc );
-  hipLaunchKernelGGL( k_svc_results, dim3( (unsigned)((n + 255ul) / 256ul) ), dim3( 256 ), 0, L.st, n, L.d_tsz, L.d_tag,
-                      L.d_bid, L.d_cnt, L.d_tcode, L.d_fdesc, L.d_tso, L.d_res );
+  hipLaunchKernelGGL( k_svc_results, dim3( (unsigned)((n + 255ul) / 256ul) ), dim3( 256 ), 0, L.st, L.d_desc, (u32)L.nreq, n,
+                      L.d_tsz, L.d_tag, L.d_bid, L.d_cnt, L.d_tcode, L.d_fdesc, L.d_tso );
   SV_CHECK( hipGetLastError() );
-  for( ulong k = 0; k < L.nreq; k++ ) {
-    svc_desc const & d = L.h_desc[k];
-    SV_CHECK( hipMemcpyAsync( fd_verify_svc_res( g, L.req[k].t, L.req[k].slot ), L.d_res + d.base,
-                              sizeof(fd_verify_svc_res_t) * d.n, hipMemcpyDeviceToHost, L.st ) );
-  }
   SV_CHECK( hipEventRecord( L.ev1, L.st ) );
   s->stat[0]++; s->stat[1] += n; s->stat[2] += L.nreq;
   if( n > s->stat[15] ) s->stat[15] = n;
@@ -507,7 +516,6 @@ static void
 svc_ingest_start( fd_verify_svc_t * s, svc_ingest & I ) {
   SV_CHECK( hipSetDevice( s->dev ) );
   SV_CHECK( hipEventRecord( I.ev0, s->st_ing ) );
-  SV_CHECK( hipMemcpyAsync( I.d_desc, I.h_desc, sizeof(svc_desc) * I.nreq, hipMemcpyHostToDevice, s->st_ing ) );
   hipLaunchKernelGGL( k_svc_gather, dim3( (unsigned)((I.n + 3ul) / 4ul) ), dim3( 256 ), 0, s->st_ing, I.d_desc,
                       (u32)I.nreq, I.n, s->d_ing, s->d_ing_sz, s->d_ing_kind, s->d_ing_tso, s->d_stage );
   SV_CHECK( hipGetLastError() );
@@ -526,36 +534,28 @@ svc_flush_start( fd_verify_svc_t * s, ulong t, fd_verify_svc_flush_t const * f )
   }
   ulong const m = f->hi - f->lo;
   fd_verify_svc_out_t const * out = fd_verify_svc_out( g, t, f->slot ) + f->lo;
-  long const delta = (long)(T.chunk_base - T.h_out);              /* mirror offset of chunk c: 64 c + delta */
+  long const delta = (long)(T.chunk_base - T.h_out);              /* dcache offset of chunk c: 64 c + delta */
+  /* every entry's chunks inside the out dcache before the kernel writes them */
+  ulong bytes = 0;
+  for( ulong e = 0; e < m; e++ ) {
+    if( out[e].flags & FD_VERIFY_SVC_OUT_HOSTWRITTEN ) continue;
+    long a = (long)(64ul * (ulong)out[e].chunk) + delta, b = a + (long)(((ulong)out[e].sz + 63ul) & ~63ul);
+    if( a < 0 || b > (long)T.out_sz ) {
+      fprintf( stderr, "fd_verify_svc: tile %lu: out chunk %u (+%u) outside the out dcache\n", t, out[e].chunk, out[e].sz );
+      abort();
+    }
+    bytes += (ulong)(b - a);
+  }
   SV_CHECK( hipSetDevice( s->dev ) );
   if( m ) {
     hipLaunchKernelGGL( k_svc_compact, dim3( (unsigned)((m + 3ul) / 4ul) ), dim3( 256 ), 0, T.st,
                         (fd_verify_svc_out_t const *)svc_dev( s, out, m * sizeof(fd_verify_svc_out_t) ), m,
-                        (u8 const *)s->d_stage, svc_stage0( s, t, f->slot ), T.d_mirror, delta );
+                        (u8 const *)s->d_stage, svc_stage0( s, t, f->slot ), T.d_out, delta );
     SV_CHECK( hipGetLastError() );
-  }
-  /* the covered spans: maximal runs of entries whose chunks follow each
-     other (a wrap or a frag the tile wrote itself ends a run) */
-  long s0 = -1, s1 = -1;
-  for( ulong e = 0; e <= m; e++ ) {
-    long a = -1, b = -1;
-    if( e < m && !(out[e].flags & FD_VERIFY_SVC_OUT_HOSTWRITTEN) ) {
-      a = (long)(64ul * (ulong)out[e].chunk) + delta;
-      b = a + (long)(((ulong)out[e].sz + 127ul) & ~127ul);  /* fd_dcache_compact_next advances by chunk pairs */
-      if( a < 0 || b > (long)T.out_sz ) {
-        fprintf( stderr, "fd_verify_svc: tile %lu: out chunk %u (+%u) outside the out dcache\n", t, out[e].chunk, out[e].sz );
-        abort();
-      }
-      if( a == s1 ) { s1 = b; continue; }
-    }
-    if( s0 >= 0 && s1 > s0 ) {
-      SV_CHECK( hipMemcpyAsync( T.h_out + s0, T.d_mirror + s0, (ulong)(s1 - s0), hipMemcpyDeviceToHost, T.st ) );
-      s->stat[5] += (ulong)(s1 - s0); s->stat[6]++;
-    }
-    s0 = a; s1 = b;
+    s->stat[6]++;
   }
   SV_CHECK( hipEventRecord( T.ev[T.flush_take % SVC_FLUSH_Q], T.st ) );
-  s->stat[3]++; s->stat[4] += m;
+  s->stat[3]++; s->stat[4] += m; s->stat[5] += bytes;
 }
 
 extern "C" int
@@ -695,14 +695,13 @@ fd_verify_svc_delete( fd_verify_svc_t * s ) {
     if( !T.set ) continue;
     (void)hipStreamDestroy( T.st );
     for( ulong k = 0; k < SVC_FLUSH_Q; k++ ) (void)hipEventDestroy( T.ev[k] );
-    (void)hipFree( T.d_mirror );
   }
   (void)hipFree( s->d_stage );
   (void)hipFree( s->d_ing ); (void)hipFree( s->d_ing_sz ); (void)hipFree( s->d_ing_kind ); (void)hipFree( s->d_ing_tso );
   for( ulong k = 0; k < SVC_ING_MAX; k++ ) {
     svc_ingest & I = s->ING[k];
     if( !I.h_desc ) continue;
-    (void)hipHostFree( I.h_desc ); (void)hipFree( I.d_desc ); (void)hipEventDestroy( I.ev0 ); (void)hipEventDestroy( I.ev1 );
+    (void)hipHostFree( I.h_desc ); (void)hipEventDestroy( I.ev0 ); (void)hipEventDestroy( I.ev1 );
   }
   if( s->st_ing ) (void)hipStreamDestroy( s->st_ing );
   free( s->sdesc );

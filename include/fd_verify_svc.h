@@ -37,7 +37,7 @@
    (fd_hash( seed, sig0, 64 )) and fd_ed25519_verify_batch_single_msg.
    The out frags wait in HBM (staging) until the tile has decided which are
    published; a flush then writes exactly those, at the chunks the tile
-   assigned, with DMA copies of contiguous spans.
+   assigned, with one kernel storing into the registered out dcache.
 
    Shared memory (one segment per GPU, in the topology a workspace object
    both tile kinds join):
@@ -381,7 +381,7 @@ static inline ulong fd_verify_svc_tiles_on( ulong gpu, ulong verify_cnt, ulong g
      oldest has waited wait_ns, or -- no launch in flight -- idle_ns
      (defaults batch_max / 2, 400 us, 20 us).
    fd_verify_svc_stats( svc, out[ 16 ] ): launches, frags, requests,
-     flushes, flushed frags, flushed bytes, copy spans, GPU ns (summed over
+     flushes, flushed frags, flushed bytes, flush kernels, GPU ns (summed over
      verify launches), host ns starting launches, host ns starting flushes,
      host ns polling events, polls, ingests, ingest GPU ns, host ns starting
      ingests, the largest launch's frags.

@@ -80,7 +80,8 @@ def run_one(stream, tiles, in_depth, timeout, logdir, env=None, svc_env=None, sv
     GPU tile's (SVC_BATCH_MAX, SVC_INFLIGHT, ...).  Liveness is checked every
     0.2 s: a process that dies ends the run at once.  rocprof: a directory;
     the GPU tile runs under rocprofv3 --kernel-trace --memory-copy-trace
-    --stats there (the program itself after --)."""
+    --stats there (the program itself after --); SVC_BENCH_HIP_TRACE=1 adds
+    --hip-trace (the HIP API calls' host durations)."""
     shm = f"/dev/shm/fd_svc_bench_{os.getpid()}"
     if os.path.exists(shm):
         os.unlink(shm)
@@ -121,7 +122,8 @@ def run_one(stream, tiles, in_depth, timeout, logdir, env=None, svc_env=None, sv
             raise RuntimeError(f"producer: {line!r} (see {logdir}/producer.err)")
         svc_cmd = [svc_exe or SVC, shm, str(gpu)]
         if rocprof:
-            svc_cmd = ["rocprofv3", "--kernel-trace", "--memory-copy-trace", "--stats", "--output-format", "csv",
+            api = ["--hip-trace"] if os.environ.get("SVC_BENCH_HIP_TRACE") else []
+            svc_cmd = ["rocprofv3", "--kernel-trace", "--memory-copy-trace"] + api + ["--stats", "--output-format", "csv",
                        "-d", rocprof, "-o", "svc", "--"] + svc_cmd
         spawn(svc_cmd, "svc", svc_env)
         for t in range(tiles):
