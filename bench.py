@@ -595,7 +595,7 @@ def run_tile_leg(args):
             depth = 1 << (s.n - 1).bit_length()
             pre = {"SVC_RUN_PRELAY": "1"}
             runs = {}
-            for t in (1, 2):
+            for t in (1, 2, 3):
                 runs[t] = [SB.run_one(stream, t, depth, 180, os.path.join(logdir, f"t{t}_{k}"), env=pre, pin="auto")
                            for k in range(3)]
 

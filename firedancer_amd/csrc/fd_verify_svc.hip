@@ -82,6 +82,13 @@ typedef uint64_t u64;
 #define SVC_REGION_MAX    64ul
 #define SVC_ING_MAX       8ul    /* ingest batches in flight */
 
+/* the device current on the calling thread (the service runs on one
+   thread; hipSetDevice only when it changes) */
+static __thread int svc_cur_dev = -1;
+static void svc_device( int dev ) {
+  if( svc_cur_dev != dev ) { SV_CHECK( hipSetDevice( dev ) ); svc_cur_dev = dev; }
+}
+
 static long svc_now_ns( void ) {
   struct timespec ts;
   clock_gettime( CLOCK_MONOTONIC, &ts );
@@ -206,16 +213,31 @@ void k_svc_results( svc_desc const * __restrict__ desc, u32 nreq, ulong n, u16 c
    entry's chunk; one wave per entry, 16-B stores, a frag's bytes contiguous */
 __global__ __launch_bounds__(256)
 void k_svc_compact( fd_verify_svc_out_t const * __restrict__ out, ulong m, u8 const * __restrict__ stage,
-                    ulong stage0, u8 * __restrict__ dcache, long delta ) {
+                    ulong stage0, u8 * __restrict__ dcache, long delta, ulong out_sz, u32 * __restrict__ err,
+                    u64 * __restrict__ bytes ) {
+  __shared__ u32 wg_bytes;
+  if( threadIdx.x == 0u ) wg_bytes = 0u;
+  __syncthreads();
   ulong const e = (ulong)blockIdx.x * 4ul + (threadIdx.x >> 6);
   u32 const lane = threadIdx.x & 63u;
-  if( e >= m ) return;
-  fd_verify_svc_out_t const o = out[e];
-  if( o.flags & FD_VERIFY_SVC_OUT_HOSTWRITTEN ) return;
-  u32 const len = ((u32)o.sz + 63u) & ~63u;
-  u8 const * s = stage + 64ul * (stage0 + FD_TXN_HIP_STAGE_CHUNKS * (ulong)o.idx);
-  u8 *       d = dcache + (long)(64ul * (ulong)o.chunk) + delta;
-  for( u32 p = 16u * lane; p < len; p += 1024u ) *(uint4 *)(d + p) = *(uint4 const *)(s + p);
+  if( e < m ) {
+    fd_verify_svc_out_t const o = out[e];
+    if( !(o.flags & FD_VERIFY_SVC_OUT_HOSTWRITTEN) ) {
+      u32 const len = ((u32)o.sz + 63u) & ~63u;
+      long const at = (long)(64ul * (ulong)o.chunk) + delta;
+      /* the tile's chunk must lie inside its out dcache: a bad entry is
+         reported (the service aborts at the flush's retirement), never written */
+      if( at < 0 || at + (long)len > (long)out_sz ) { if( lane == 0u ) *(volatile u32 *)err = 1u; }
+      else {
+        u8 const * s = stage + 64ul * (stage0 + FD_TXN_HIP_STAGE_CHUNKS * (ulong)o.idx);
+        u8 *       d = dcache + at;
+        for( u32 p = 16u * lane; p < len; p += 1024u ) *(uint4 *)(d + p) = *(uint4 const *)(s + p);
+        if( lane == 0u ) atomicAdd( &wg_bytes, len );
+      }
+    }
+  }
+  __syncthreads();
+  if( threadIdx.x == 0u && wg_bytes ) atomicAdd( (unsigned long long *)bytes, (unsigned long long)wg_bytes );
 }
 
 /**********************************************************************/
@@ -240,6 +262,8 @@ struct svc_tile {
   ulong        out_sz;
   u8 const *   chunk_base;     /* host address of out chunk 0 */
   u8 *         d_out;          /* the out dcache's device address (registered) */
+  u32 *        h_err;          /* mapped pinned: a flush found an entry outside the out dcache */
+  u32 *        d_err;
   hipStream_t  st;
   hipEvent_t   ev[SVC_FLUSH_Q];
   ulong        take;           /* next request id to take */
@@ -280,6 +304,7 @@ struct fd_verify_svc {
                                   host ns starting launches, starting flushes, retiring, polls; ingests, ingest
                                   gpu ns, host ns starting ingests, the largest launch */
   long     merge_idle_ns;      /* a launch on an idle GPU once the oldest request has waited this long */
+  u64 *    d_flush_bytes;      /* HBM: bytes the flush kernels wrote (stat 5, read by fd_verify_svc_stats) */
   int      running;
 };
 
@@ -352,6 +377,7 @@ fd_verify_svc_boot( void * seg_mem, int device, ulong batch_max, ulong inflight 
   s->seg = seg; s->dev = device; s->batch_max = batch_max; s->inflight = inflight;
   s->merge_min = batch_max / 2ul; s->merge_wait_ns = 400000L; s->merge_idle_ns = 20000L;
   SV_CHECK( hipMalloc( &s->d_stage, stage_sz + 4096ul ) );
+  SV_CHECK( hipMalloc( &s->d_flush_bytes, 64 ) ); SV_CHECK( hipMemset( s->d_flush_bytes, 0, 64 ) );
   SV_CHECK( hipMalloc( &s->d_ing, 64ul * SVC_INGEST_CHUNKS * ing_cnt + 4096ul ) );
   SV_CHECK( hipMalloc( &s->d_ing_sz, 2ul * ing_cnt ) ); SV_CHECK( hipMalloc( &s->d_ing_kind, ing_cnt ) );
   SV_CHECK( hipMalloc( &s->d_ing_tso, 4ul * ing_cnt ) );
@@ -402,6 +428,9 @@ fd_verify_svc_set_tile( fd_verify_svc_t * s, ulong t, void * out_dcache, ulong o
   if( !s || t >= s->seg->tile_cnt || !out_dcache || !out_sz || s->tile[t].set ) return -1;
   svc_tile & T = s->tile[t];
   T.d_out = svc_dev( s, out_dcache, out_sz );               /* mapped: the flush kernel writes it */
+  SV_CHECK( hipHostMalloc( &T.h_err, 64, hipHostMallocMapped ) );
+  SV_CHECK( hipHostGetDevicePointer( (void **)&T.d_err, T.h_err, 0 ) );
+  *T.h_err = 0u;
   (void)svc_dev( s, fd_verify_svc_tile( s->seg, t ), s->seg->tile_sz );   /* the tile's part of the segment */
   SV_CHECK( hipSetDevice( s->dev ) );
   T.h_out = (u8 *)out_dcache; T.out_sz = out_sz; T.chunk_base = (u8 const *)chunk_base;
@@ -419,6 +448,7 @@ fd_verify_svc_set_merge( fd_verify_svc_t * s, ulong min_frags, ulong wait_ns, ul
 extern "C" int
 fd_verify_svc_run( fd_verify_svc_t * s ) {
   for( ulong t = 0; t < s->seg->tile_cnt; t++ ) if( !s->tile[t].set ) return -1;
+  svc_device( s->dev );
   /* the kernels' code objects loaded and every buffer touched once before
      the first request (the steady state loads nothing) */
   for( ulong k = 0; k < s->inflight; k++ ) {
@@ -434,7 +464,7 @@ fd_verify_svc_run( fd_verify_svc_t * s ) {
   SV_CHECK( hipGetLastError() );
   for( ulong t = 0; t < s->seg->tile_cnt; t++ ) {
     hipLaunchKernelGGL( k_svc_compact, dim3( 1 ), dim3( 256 ), 0, s->tile[t].st, (fd_verify_svc_out_t const *)0, 0ul,
-                        (u8 const *)s->d_stage, 0ul, s->tile[t].d_out, 0L );
+                        (u8 const *)s->d_stage, 0ul, s->tile[t].d_out, 0L, 0ul, s->tile[t].d_err, s->d_flush_bytes );
     SV_CHECK( hipGetLastError() );
   }
   SV_CHECK( hipDeviceSynchronize() );
@@ -493,7 +523,7 @@ svc_launch_start( fd_verify_svc_t * s, svc_launch & L ) {
     s->pend_frags -= p.n; s->pend_head++;
   }
   L.n = n; L.busy = 1;
-  SV_CHECK( hipSetDevice( s->dev ) );
+  svc_device( s->dev );
   SV_CHECK( hipEventRecord( L.ev0, L.st ) );
   hipLaunchKernelGGL( k_svc_assemble, dim3( (unsigned)((n + 255ul) / 256ul) ), dim3( 256 ), 0, L.st, L.d_desc, (u32)L.nreq,
                       n, s->d_ing_sz, s->d_ing_kind, s->d_ing_tso, L.d_in_chunk, L.d_in_sz, L.d_in_kind, L.d_tso, L.d_seed,
@@ -514,7 +544,7 @@ svc_launch_start( fd_verify_svc_t * s, svc_launch & L ) {
    HBM ingest frags), on the ingest stream */
 static void
 svc_ingest_start( fd_verify_svc_t * s, svc_ingest & I ) {
-  SV_CHECK( hipSetDevice( s->dev ) );
+  svc_device( s->dev );
   SV_CHECK( hipEventRecord( I.ev0, s->st_ing ) );
   hipLaunchKernelGGL( k_svc_gather, dim3( (unsigned)((I.n + 3ul) / 4ul) ), dim3( 256 ), 0, s->st_ing, I.d_desc,
                       (u32)I.nreq, I.n, s->d_ing, s->d_ing_sz, s->d_ing_kind, s->d_ing_tso, s->d_stage );
@@ -535,27 +565,18 @@ svc_flush_start( fd_verify_svc_t * s, ulong t, fd_verify_svc_flush_t const * f )
   ulong const m = f->hi - f->lo;
   fd_verify_svc_out_t const * out = fd_verify_svc_out( g, t, f->slot ) + f->lo;
   long const delta = (long)(T.chunk_base - T.h_out);              /* dcache offset of chunk c: 64 c + delta */
-  /* every entry's chunks inside the out dcache before the kernel writes them */
-  ulong bytes = 0;
-  for( ulong e = 0; e < m; e++ ) {
-    if( out[e].flags & FD_VERIFY_SVC_OUT_HOSTWRITTEN ) continue;
-    long a = (long)(64ul * (ulong)out[e].chunk) + delta, b = a + (long)(((ulong)out[e].sz + 63ul) & ~63ul);
-    if( a < 0 || b > (long)T.out_sz ) {
-      fprintf( stderr, "fd_verify_svc: tile %lu: out chunk %u (+%u) outside the out dcache\n", t, out[e].chunk, out[e].sz );
-      abort();
-    }
-    bytes += (ulong)(b - a);
-  }
-  SV_CHECK( hipSetDevice( s->dev ) );
   if( m ) {
+    /* the kernel checks every entry's chunks against the out dcache (the
+       host does not walk the entries: the service thread drives every tile) */
     hipLaunchKernelGGL( k_svc_compact, dim3( (unsigned)((m + 3ul) / 4ul) ), dim3( 256 ), 0, T.st,
                         (fd_verify_svc_out_t const *)svc_dev( s, out, m * sizeof(fd_verify_svc_out_t) ), m,
-                        (u8 const *)s->d_stage, svc_stage0( s, t, f->slot ), T.d_out, delta );
+                        (u8 const *)s->d_stage, svc_stage0( s, t, f->slot ), T.d_out, delta, T.out_sz, T.d_err,
+                        s->d_flush_bytes );
     SV_CHECK( hipGetLastError() );
     s->stat[6]++;
   }
   SV_CHECK( hipEventRecord( T.ev[T.flush_take % SVC_FLUSH_Q], T.st ) );
-  s->stat[3]++; s->stat[4] += m; s->stat[5] += bytes;
+  s->stat[3]++; s->stat[4] += m;
 }
 
 extern "C" int
@@ -563,7 +584,7 @@ fd_verify_svc_poll( fd_verify_svc_t * s ) {
   fd_verify_svc_seg_t * g = s->seg;
   int did = 0;
   long const p0 = svc_now_ns();
-  SV_CHECK( hipSetDevice( s->dev ) );
+  svc_device( s->dev );
   g->svc_heartbeat++;
   s->stat[11]++;
   /* 1. finished verify launches: their slots' results are in the segment */
@@ -611,6 +632,10 @@ fd_verify_svc_poll( fd_verify_svc_t * s ) {
       hipError_t e = hipEventQuery( T.ev[T.flush_fin % SVC_FLUSH_Q] );
       if( e == hipErrorNotReady ) break;
       SV_CHECK( e );
+      if( *(volatile u32 *)T.h_err ) {
+        fprintf( stderr, "fd_verify_svc: tile %lu: a flush entry's chunks lie outside the out dcache\n", t );
+        abort();
+      }
       T.flush_fin++; did = 1;
       fd_verify_svc_st( &b->flush_done, T.flush_fin );
     }
@@ -682,6 +707,8 @@ fd_verify_svc_poll( fd_verify_svc_t * s ) {
 extern "C" void
 fd_verify_svc_stats( fd_verify_svc_t const * s, ulong out[16] ) {
   for( int k = 0; k < 16; k++ ) out[k] = s->stat[k];
+  u64 b = 0;
+  if( hipMemcpy( &b, s->d_flush_bytes, 8, hipMemcpyDeviceToHost ) == hipSuccess ) out[5] = b;
 }
 
 extern "C" void
@@ -694,9 +721,10 @@ fd_verify_svc_delete( fd_verify_svc_t * s ) {
     svc_tile & T = s->tile[t];
     if( !T.set ) continue;
     (void)hipStreamDestroy( T.st );
+    (void)hipHostFree( T.h_err );
     for( ulong k = 0; k < SVC_FLUSH_Q; k++ ) (void)hipEventDestroy( T.ev[k] );
   }
-  (void)hipFree( s->d_stage );
+  (void)hipFree( s->d_stage ); (void)hipFree( s->d_flush_bytes );
   (void)hipFree( s->d_ing ); (void)hipFree( s->d_ing_sz ); (void)hipFree( s->d_ing_kind ); (void)hipFree( s->d_ing_tso );
   for( ulong k = 0; k < SVC_ING_MAX; k++ ) {
     svc_ingest & I = s->ING[k];
