@@ -305,6 +305,7 @@ struct fd_verify_svc {
                                   gpu ns, host ns starting ingests, the largest launch */
   long     merge_idle_ns;      /* a launch on an idle GPU once the oldest request has waited this long */
   u64 *    d_flush_bytes;      /* HBM: bytes the flush kernels wrote (stat 5, read by fd_verify_svc_stats) */
+  ulong    io_cus;             /* CUs kept for the PCIe kernels (ingest, flush), the rest for the verify (0: shared) */
   int      running;
 };
 
@@ -446,9 +447,46 @@ fd_verify_svc_set_merge( fd_verify_svc_t * s, ulong min_frags, ulong wait_ns, ul
 }
 
 extern "C" int
+fd_verify_svc_set_io_cus( fd_verify_svc_t * s, ulong cus ) {
+  if( !s || s->running ) return -1;
+  s->io_cus = cus;
+  return 0;
+}
+
+/* io_cus > 0: the ingest and flush streams on CUs [0, io_cus), the verify
+   launches' streams on the others.  The PCIe kernels spend their time
+   waiting on host memory; on their own CUs they neither hold wave slots
+   the persistent DSM grid wants nor wait behind it. */
+static int
+svc_split_cus( fd_verify_svc_t * s ) {
+  hipDeviceProp_t prop;
+  SV_CHECK( hipGetDeviceProperties( &prop, s->dev ) );
+  ulong const cus = (ulong)prop.multiProcessorCount;
+  if( s->io_cus >= cus || cus > 32ul * 16ul ) return -1;
+  uint io[16] = { 0u }, vf[16] = { 0u };
+  uint const words = (uint)((cus + 31ul) / 32ul);
+  for( ulong c = 0; c < cus; c++ ) {
+    if( c < s->io_cus ) io[c >> 5] |= 1u << (c & 31ul);
+    else                vf[c >> 5] |= 1u << (c & 31ul);
+  }
+  SV_CHECK( hipStreamDestroy( s->st_ing ) );
+  SV_CHECK( hipExtStreamCreateWithCUMask( &s->st_ing, words, io ) );
+  for( ulong t = 0; t < s->seg->tile_cnt; t++ ) {
+    SV_CHECK( hipStreamDestroy( s->tile[t].st ) );
+    SV_CHECK( hipExtStreamCreateWithCUMask( &s->tile[t].st, words, io ) );
+  }
+  for( ulong k = 0; k < s->inflight; k++ ) {
+    if( fd_ed25519_hip_ctx_set_cu_mask( s->L[k].ctx, vf, words ) ) return -1;
+    s->L[k].st = (hipStream_t)fd_ed25519_hip_ctx_stream( s->L[k].ctx );
+  }
+  return 0;
+}
+
+extern "C" int
 fd_verify_svc_run( fd_verify_svc_t * s ) {
   for( ulong t = 0; t < s->seg->tile_cnt; t++ ) if( !s->tile[t].set ) return -1;
   svc_device( s->dev );
+  if( s->io_cus && svc_split_cus( s ) ) return -1;
   /* the kernels' code objects loaded and every buffer touched once before
      the first request (the steady state loads nothing) */
   for( ulong k = 0; k < s->inflight; k++ ) {

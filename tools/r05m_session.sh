@@ -1,5 +1,5 @@
 #!/bin/bash
-# round 5 session m: in-kernel flush checks, one hipSetDevice -- GPU tests, policy sweep, kernel profile
+# round 5 session m: in-kernel flush checks, one hipSetDevice, CUs split for the PCIe kernels -- GPU tests, policy sweep, kernel profile
 out=gpurun_out/r05m; mkdir -p $out
 export TMPDIR=/tmp
 timeout -k 10 500 python -u -m pytest -x -v --timeout 200 --timeout-method thread tests/test_gpu_svc_run.py > $out/pytest.txt 2>&1 || exit $?
@@ -12,6 +12,9 @@ run w2i2 1,2,3,4 "SVC_RUN_REQ_DEPTH=8" "SVC_MERGE_WAIT_NS=2000000,SVC_INFLIGHT=2
 run w2i3 2,3 "SVC_RUN_REQ_DEPTH=8" "SVC_MERGE_WAIT_NS=2000000,SVC_INFLIGHT=3" || exit $?
 run w1i2 2,3 "SVC_RUN_REQ_DEPTH=8" "SVC_MERGE_WAIT_NS=1000000,SVC_INFLIGHT=2" || exit $?
 run w4i2 2,3 "SVC_RUN_REQ_DEPTH=16" "SVC_MERGE_WAIT_NS=4000000,SVC_INFLIGHT=2" || exit $?
+run io16 2,3 "SVC_RUN_REQ_DEPTH=8" "SVC_MERGE_WAIT_NS=2000000,SVC_INFLIGHT=2,SVC_IO_CUS=16" || exit $?
+run io32 2,3 "SVC_RUN_REQ_DEPTH=8" "SVC_MERGE_WAIT_NS=2000000,SVC_INFLIGHT=2,SVC_IO_CUS=32" || exit $?
+run io64 2,3 "SVC_RUN_REQ_DEPTH=8" "SVC_MERGE_WAIT_NS=2000000,SVC_INFLIGHT=2,SVC_IO_CUS=64" || exit $?
 timeout -k 10 240 python -u tools/svc_bench.py --frags 4194304 --tiles 2 --prelay --env SVC_RUN_REQ_DEPTH=8 \
   --svc-env SVC_MERGE_WAIT_NS=2000000,SVC_INFLIGHT=2 --rocprof $out/prof --timeout 200 --logdir $out/logsp > $out/prof.jsonl 2> $out/prof.err
 find $out/prof -name "*trace*.csv" -delete
