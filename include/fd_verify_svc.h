@@ -382,7 +382,8 @@ static inline ulong fd_verify_svc_tiles_on( ulong gpu, ulong verify_cnt, ulong g
    fd_verify_svc_set_merge( svc, min_frags, wait_ns, idle_ns ): a verify
      launch starts once the ingested requests hold min_frags frags, or the
      oldest has waited wait_ns, or -- no launch in flight -- idle_ns
-     (defaults batch_max / 2, 400 us, 20 us).
+     (defaults batch_max / 2, 2 ms, 20 us; two launches in flight measure
+     best on one MI355X).
    fd_verify_svc_stats( svc, out[ 16 ] ): launches, frags, requests,
      flushes, flushed frags, flushed bytes, flush kernels, GPU ns (summed over
      verify launches), host ns starting launches, host ns starting flushes,

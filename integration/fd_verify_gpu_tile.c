@@ -23,7 +23,17 @@
      verify_svc.gpu_cnt            GPU tiles (verify tile kind_id % gpu_cnt picks one)
      verify_svc.<g>                obj id of GPU g's segment
      obj.<id>.{tile_cnt,req_depth,slot_cap,frag_cap}   the segment's shape
-     verify_svc.batch_max, verify_svc.inflight         launch size and count */
+     verify_svc.batch_max, verify_svc.inflight         launch size and count
+     verify_svc.merge_min, .merge_wait_ns, .merge_idle_ns   the merge policy (fd_verify_svc_set_merge)
+     verify_svc.io_cus                                 CUs for the PCIe kernels (fd_verify_svc_set_io_cus)
+   Defaults: the measured best on one MI355X, the
+   same as integration/svc_run.c's. */
+
+#define SVC_BATCH_MAX_DEFAULT     (262144UL)
+#define SVC_INFLIGHT_DEFAULT      (2UL)
+#define SVC_MERGE_WAIT_NS_DEFAULT (2000000UL)
+#define SVC_MERGE_IDLE_NS_DEFAULT (20000UL)
+#define SVC_IO_CUS_DEFAULT        (0UL)
 
 #include "../topo/fd_topo.h"
 #include "../../util/pod/fd_pod_format.h"
@@ -92,10 +102,16 @@ privileged_init( fd_topo_t * topo, fd_topo_tile_t * tile ) {
   ulong gpu_cnt = fd_pod_query_ulong( topo->props, "verify_svc.gpu_cnt", 0UL );
   ulong obj_id  = fd_pod_queryf_ulong( topo->props, ULONG_MAX, "verify_svc.%lu", gpu );
   if( FD_UNLIKELY( !gpu_cnt || gpu>=gpu_cnt || obj_id==ULONG_MAX ) ) FD_LOG_ERR(( "no verify_svc object for GPU %lu", gpu ));
-  ulong batch_max = fd_pod_query_ulong( topo->props, "verify_svc.batch_max", 131072UL );
-  ulong inflight  = fd_pod_query_ulong( topo->props, "verify_svc.inflight",  4UL      );
+  ulong batch_max = fd_pod_query_ulong( topo->props, "verify_svc.batch_max", SVC_BATCH_MAX_DEFAULT );
+  ulong inflight  = fd_pod_query_ulong( topo->props, "verify_svc.inflight",  SVC_INFLIGHT_DEFAULT  );
   ctx->svc = fd_verify_svc_boot( fd_topo_obj_laddr( topo, obj_id ), (int)gpu, batch_max, inflight );
   if( FD_UNLIKELY( !ctx->svc ) ) FD_LOG_ERR(( "fd_verify_svc_boot failed on GPU %lu", gpu ));
+  fd_verify_svc_set_merge( ctx->svc, fd_pod_query_ulong( topo->props, "verify_svc.merge_min", batch_max/2UL ),
+                           fd_pod_query_ulong( topo->props, "verify_svc.merge_wait_ns", SVC_MERGE_WAIT_NS_DEFAULT ),
+                           fd_pod_query_ulong( topo->props, "verify_svc.merge_idle_ns", SVC_MERGE_IDLE_NS_DEFAULT ) );
+  if( FD_UNLIKELY( fd_verify_svc_set_io_cus( ctx->svc, fd_pod_query_ulong( topo->props, "verify_svc.io_cus",
+                                                                            SVC_IO_CUS_DEFAULT ) ) ) )
+    FD_LOG_ERR(( "fd_verify_svc_set_io_cus failed on GPU %lu", gpu ));
   vgpu_map( ctx, topo, topo->objs[ obj_id ].wksp_id );
 
   /* every quic_verify link (service link l = its kind_id) */

@@ -10,9 +10,9 @@
    in it), names the quic_verify links (service link l = link kind_id l)
    and the tiles' out dcaches, then polls until the producer sets shutdown.
    Environment: SVC_BATCH_MAX (frags per merged launch, default 262144),
-   SVC_INFLIGHT (launches at once, default 4), SVC_MERGE_MIN (frags that
+   SVC_INFLIGHT (launches at once, default 2), SVC_MERGE_MIN (frags that
    start a launch at once, default batch_max / 2), SVC_MERGE_WAIT_NS
-   (default 400000), SVC_MERGE_IDLE_NS (the wait with no launch in flight,
+   (default 2000000), SVC_MERGE_IDLE_NS (the wait with no launch in flight,
    default 20000), SVC_IO_CUS (CUs for the ingest and flush kernels, the
    rest for the verify; default 0: shared).
 
@@ -52,10 +52,10 @@ main( int argc, char ** argv ) {
   svc_run_hdr_t * hdr = (svc_run_hdr_t *)base;
 
   ulong batch_max = env_ulong( "SVC_BATCH_MAX", 262144UL );
-  ulong inflight  = env_ulong( "SVC_INFLIGHT", 4UL );
+  ulong inflight  = env_ulong( "SVC_INFLIGHT", 2UL );
   fd_verify_svc_t * svc = fd_verify_svc_boot( base + hdr->svc_off, (int)strtol( argv[2], NULL, 0 ), batch_max, inflight );
   if( !svc ) FD_LOG_ERR(( "fd_verify_svc_boot failed (batch_max %lu, inflight %lu)", batch_max, inflight ));
-  fd_verify_svc_set_merge( svc, env_ulong( "SVC_MERGE_MIN", batch_max/2UL ), env_ulong( "SVC_MERGE_WAIT_NS", 400000UL ),
+  fd_verify_svc_set_merge( svc, env_ulong( "SVC_MERGE_MIN", batch_max/2UL ), env_ulong( "SVC_MERGE_WAIT_NS", 2000000UL ),
                            env_ulong( "SVC_MERGE_IDLE_NS", 20000UL ) );
   if( fd_verify_svc_map( svc, base, hdr->map_sz ) ) FD_LOG_ERR(( "registering %lu B for the GPU failed", hdr->map_sz ));
   for( ulong l=0UL; l<hdr->link_cnt; l++ ) {
