@@ -45,6 +45,7 @@ def main():
     ap.add_argument("--steps", type=int, default=5, help="bisection steps per depth")
     ap.add_argument("--lo", type=float, default=2e6, help="lowest offered rate, frags/s")
     ap.add_argument("--env", default="", help="KEY=VAL,... for every process (SVC_RUN_*)")
+    ap.add_argument("--svc-env", default="", help="KEY=VAL,... for the GPU tile only")
     ap.add_argument("--pin", default="auto")
     ap.add_argument("--timeout", type=float, default=120)
     ap.add_argument("--mock", action="store_true", help="the CPU stand-in for the GPU tile (oracle/_ref/svc_mock)")
@@ -53,6 +54,7 @@ def main():
     import tile_bench as TB
     base_env = dict(x.split("=", 1) for x in args.env.split(",") if x)
     base_env["SVC_RUN_PRELAY"] = "1"
+    svc_env = dict(x.split("=", 1) for x in args.svc_env.split(",") if x)
     pin = None if args.pin == "none" else "auto"
     runs = [0]
 
@@ -62,7 +64,7 @@ def main():
             env["SVC_RUN_RATE"] = str(int(rate))
         runs[0] += 1
         r = SB.run_one(stream, args.tiles, depth, args.timeout, os.path.join(args.logdir, f"run{runs[0]}"),
-                       env=env, pin=pin, svc_exe=os.path.join(SB.REPO, "oracle", "_ref", "svc_mock") if args.mock else None)
+                       env=env, svc_env=svc_env, pin=pin, svc_exe=os.path.join(SB.REPO, "oracle", "_ref", "svc_mock") if args.mock else None)
         line = {k: r[k] for k in ("in_depth", "offered_rate", "frags", "overrun", "lapped", "verifies_per_s",
                                   "frags_per_s", "latency", "latency_to_consumer")}
         line["stream_frags"] = r["stream_frags"]
