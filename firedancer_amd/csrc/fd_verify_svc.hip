@@ -213,31 +213,20 @@ void k_svc_results( svc_desc const * __restrict__ desc, u32 nreq, ulong n, u16 c
    entry's chunk; one wave per entry, 16-B stores, a frag's bytes contiguous */
 __global__ __launch_bounds__(256)
 void k_svc_compact( fd_verify_svc_out_t const * __restrict__ out, ulong m, u8 const * __restrict__ stage,
-                    ulong stage0, u8 * __restrict__ dcache, long delta, ulong out_sz, u32 * __restrict__ err,
-                    u64 * __restrict__ bytes ) {
-  __shared__ u32 wg_bytes;
-  if( threadIdx.x == 0u ) wg_bytes = 0u;
-  __syncthreads();
+                    ulong stage0, u8 * __restrict__ dcache, long delta, ulong out_sz, u32 * __restrict__ err ) {
   ulong const e = (ulong)blockIdx.x * 4ul + (threadIdx.x >> 6);
   u32 const lane = threadIdx.x & 63u;
-  if( e < m ) {
-    fd_verify_svc_out_t const o = out[e];
-    if( !(o.flags & FD_VERIFY_SVC_OUT_HOSTWRITTEN) ) {
-      u32 const len = ((u32)o.sz + 63u) & ~63u;
-      long const at = (long)(64ul * (ulong)o.chunk) + delta;
-      /* the tile's chunk must lie inside its out dcache: a bad entry is
-         reported (the service aborts at the flush's retirement), never written */
-      if( at < 0 || at + (long)len > (long)out_sz ) { if( lane == 0u ) *(volatile u32 *)err = 1u; }
-      else {
-        u8 const * s = stage + 64ul * (stage0 + FD_TXN_HIP_STAGE_CHUNKS * (ulong)o.idx);
-        u8 *       d = dcache + at;
-        for( u32 p = 16u * lane; p < len; p += 1024u ) *(uint4 *)(d + p) = *(uint4 const *)(s + p);
-        if( lane == 0u ) atomicAdd( &wg_bytes, len );
-      }
-    }
-  }
-  __syncthreads();
-  if( threadIdx.x == 0u && wg_bytes ) atomicAdd( (unsigned long long *)bytes, (unsigned long long)wg_bytes );
+  if( e >= m ) return;
+  fd_verify_svc_out_t const o = out[e];
+  if( o.flags & FD_VERIFY_SVC_OUT_HOSTWRITTEN ) return;
+  u32 const len = ((u32)o.sz + 63u) & ~63u;
+  long const at = (long)(64ul * (ulong)o.chunk) + delta;
+  /* the tile's chunk must lie inside its out dcache: a bad entry is
+     reported (the service aborts at the flush's retirement), never written */
+  if( at < 0 || at + (long)len > (long)out_sz ) { if( lane == 0u ) *(volatile u32 *)err = 1u; return; }
+  u8 const * src = stage + 64ul * (stage0 + FD_TXN_HIP_STAGE_CHUNKS * (ulong)o.idx);
+  u8 *       dst = dcache + at;
+  for( u32 p = 16u * lane; p < len; p += 1024u ) *(uint4 *)(dst + p) = *(uint4 const *)(src + p);
 }
 
 /**********************************************************************/
@@ -304,8 +293,6 @@ struct fd_verify_svc {
                                   host ns starting launches, starting flushes, retiring, polls; ingests, ingest
                                   gpu ns, host ns starting ingests, the largest launch */
   long     merge_idle_ns;      /* a launch on an idle GPU once the oldest request has waited this long */
-  u64 *    d_flush_bytes;      /* HBM: bytes the flush kernels wrote (stat 5, read by fd_verify_svc_stats) */
-  ulong    io_cus;             /* CUs kept for the PCIe kernels (ingest, flush), the rest for the verify (0: shared) */
   int      running;
 };
 
@@ -378,7 +365,6 @@ fd_verify_svc_boot( void * seg_mem, int device, ulong batch_max, ulong inflight 
   s->seg = seg; s->dev = device; s->batch_max = batch_max; s->inflight = inflight;
   s->merge_min = batch_max / 2ul; s->merge_wait_ns = 2000000L; s->merge_idle_ns = 20000L;
   SV_CHECK( hipMalloc( &s->d_stage, stage_sz + 4096ul ) );
-  SV_CHECK( hipMalloc( &s->d_flush_bytes, 64 ) ); SV_CHECK( hipMemset( s->d_flush_bytes, 0, 64 ) );
   SV_CHECK( hipMalloc( &s->d_ing, 64ul * SVC_INGEST_CHUNKS * ing_cnt + 4096ul ) );
   SV_CHECK( hipMalloc( &s->d_ing_sz, 2ul * ing_cnt ) ); SV_CHECK( hipMalloc( &s->d_ing_kind, ing_cnt ) );
   SV_CHECK( hipMalloc( &s->d_ing_tso, 4ul * ing_cnt ) );
@@ -447,46 +433,9 @@ fd_verify_svc_set_merge( fd_verify_svc_t * s, ulong min_frags, ulong wait_ns, ul
 }
 
 extern "C" int
-fd_verify_svc_set_io_cus( fd_verify_svc_t * s, ulong cus ) {
-  if( !s || s->running ) return -1;
-  s->io_cus = cus;
-  return 0;
-}
-
-/* io_cus > 0: the ingest and flush streams on CUs [0, io_cus), the verify
-   launches' streams on the others.  The PCIe kernels spend their time
-   waiting on host memory; on their own CUs they neither hold wave slots
-   the persistent DSM grid wants nor wait behind it. */
-static int
-svc_split_cus( fd_verify_svc_t * s ) {
-  hipDeviceProp_t prop;
-  SV_CHECK( hipGetDeviceProperties( &prop, s->dev ) );
-  ulong const cus = (ulong)prop.multiProcessorCount;
-  if( s->io_cus >= cus || cus > 32ul * 16ul ) return -1;
-  uint io[16] = { 0u }, vf[16] = { 0u };
-  uint const words = (uint)((cus + 31ul) / 32ul);
-  for( ulong c = 0; c < cus; c++ ) {
-    if( c < s->io_cus ) io[c >> 5] |= 1u << (c & 31ul);
-    else                vf[c >> 5] |= 1u << (c & 31ul);
-  }
-  SV_CHECK( hipStreamDestroy( s->st_ing ) );
-  SV_CHECK( hipExtStreamCreateWithCUMask( &s->st_ing, words, io ) );
-  for( ulong t = 0; t < s->seg->tile_cnt; t++ ) {
-    SV_CHECK( hipStreamDestroy( s->tile[t].st ) );
-    SV_CHECK( hipExtStreamCreateWithCUMask( &s->tile[t].st, words, io ) );
-  }
-  for( ulong k = 0; k < s->inflight; k++ ) {
-    if( fd_ed25519_hip_ctx_set_cu_mask( s->L[k].ctx, vf, words ) ) return -1;
-    s->L[k].st = (hipStream_t)fd_ed25519_hip_ctx_stream( s->L[k].ctx );
-  }
-  return 0;
-}
-
-extern "C" int
 fd_verify_svc_run( fd_verify_svc_t * s ) {
   for( ulong t = 0; t < s->seg->tile_cnt; t++ ) if( !s->tile[t].set ) return -1;
   svc_device( s->dev );
-  if( s->io_cus && svc_split_cus( s ) ) return -1;
   /* the kernels' code objects loaded and every buffer touched once before
      the first request (the steady state loads nothing) */
   for( ulong k = 0; k < s->inflight; k++ ) {
@@ -502,7 +451,7 @@ fd_verify_svc_run( fd_verify_svc_t * s ) {
   SV_CHECK( hipGetLastError() );
   for( ulong t = 0; t < s->seg->tile_cnt; t++ ) {
     hipLaunchKernelGGL( k_svc_compact, dim3( 1 ), dim3( 256 ), 0, s->tile[t].st, (fd_verify_svc_out_t const *)0, 0ul,
-                        (u8 const *)s->d_stage, 0ul, s->tile[t].d_out, 0L, 0ul, s->tile[t].d_err, s->d_flush_bytes );
+                        (u8 const *)s->d_stage, 0ul, s->tile[t].d_out, 0L, 0ul, s->tile[t].d_err );
     SV_CHECK( hipGetLastError() );
   }
   SV_CHECK( hipDeviceSynchronize() );
@@ -608,8 +557,7 @@ svc_flush_start( fd_verify_svc_t * s, ulong t, fd_verify_svc_flush_t const * f )
        host does not walk the entries: the service thread drives every tile) */
     hipLaunchKernelGGL( k_svc_compact, dim3( (unsigned)((m + 3ul) / 4ul) ), dim3( 256 ), 0, T.st,
                         (fd_verify_svc_out_t const *)svc_dev( s, out, m * sizeof(fd_verify_svc_out_t) ), m,
-                        (u8 const *)s->d_stage, svc_stage0( s, t, f->slot ), T.d_out, delta, T.out_sz, T.d_err,
-                        s->d_flush_bytes );
+                        (u8 const *)s->d_stage, svc_stage0( s, t, f->slot ), T.d_out, delta, T.out_sz, T.d_err );
     SV_CHECK( hipGetLastError() );
     s->stat[6]++;
   }
@@ -745,8 +693,6 @@ fd_verify_svc_poll( fd_verify_svc_t * s ) {
 extern "C" void
 fd_verify_svc_stats( fd_verify_svc_t const * s, ulong out[16] ) {
   for( int k = 0; k < 16; k++ ) out[k] = s->stat[k];
-  u64 b = 0;
-  if( hipMemcpy( &b, s->d_flush_bytes, 8, hipMemcpyDeviceToHost ) == hipSuccess ) out[5] = b;
 }
 
 extern "C" void
@@ -762,7 +708,7 @@ fd_verify_svc_delete( fd_verify_svc_t * s ) {
     (void)hipHostFree( T.h_err );
     for( ulong k = 0; k < SVC_FLUSH_Q; k++ ) (void)hipEventDestroy( T.ev[k] );
   }
-  (void)hipFree( s->d_stage ); (void)hipFree( s->d_flush_bytes );
+  (void)hipFree( s->d_stage );
   (void)hipFree( s->d_ing ); (void)hipFree( s->d_ing_sz ); (void)hipFree( s->d_ing_kind ); (void)hipFree( s->d_ing_tso );
   for( ulong k = 0; k < SVC_ING_MAX; k++ ) {
     svc_ingest & I = s->ING[k];

@@ -371,9 +371,6 @@ static inline ulong fd_verify_svc_tiles_on( ulong gpu, ulong verify_cnt, ulong g
      _wmark).
    fd_verify_svc_set_tile( svc, t, out_dcache, out_dcache_sz, out_chunk_base ):
      tile t's verify_dedup dcache (flush target) and its chunk base.
-   fd_verify_svc_set_io_cus( svc, cus ): before run -- the ingest and
-     flush kernels (PCIe-bound) on CUs [0, cus) of the device, the verify
-     launches on the rest (default 0: all kernels on all CUs).
    fd_verify_svc_run( svc ): marks the service running; then
    fd_verify_svc_poll( svc ): one iteration of the service loop (retire
      finished launches, ingests and flushes, start flushes, copy newly
@@ -385,7 +382,7 @@ static inline ulong fd_verify_svc_tiles_on( ulong gpu, ulong verify_cnt, ulong g
      (defaults batch_max / 2, 2 ms, 20 us; two launches in flight measure
      best on one MI355X).
    fd_verify_svc_stats( svc, out[ 16 ] ): launches, frags, requests,
-     flushes, flushed frags, flushed bytes, flush kernels, GPU ns (summed over
+     flushes, flushed frags, 0 (unused), flush kernels, GPU ns (summed over
      verify launches), host ns starting launches, host ns starting flushes,
      host ns polling events, polls, ingests, ingest GPU ns, host ns starting
      ingests, the largest launch's frags.
@@ -400,7 +397,6 @@ int               fd_verify_svc_set_link( fd_verify_svc_t * svc, ulong link, voi
 int               fd_verify_svc_set_tile( fd_verify_svc_t * svc, ulong t, void * out_dcache, ulong out_dcache_sz,
                                           void const * out_chunk_base );
 void              fd_verify_svc_set_merge( fd_verify_svc_t * svc, ulong min_frags, ulong wait_ns, ulong idle_ns );
-int               fd_verify_svc_set_io_cus( fd_verify_svc_t * svc, ulong cus );
 int               fd_verify_svc_run     ( fd_verify_svc_t * svc );
 int               fd_verify_svc_poll    ( fd_verify_svc_t * svc );
 void              fd_verify_svc_stats   ( fd_verify_svc_t const * svc, ulong out[ 16 ] );

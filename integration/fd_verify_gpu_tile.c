@@ -25,7 +25,6 @@
      obj.<id>.{tile_cnt,req_depth,slot_cap,frag_cap}   the segment's shape
      verify_svc.batch_max, verify_svc.inflight         launch size and count
      verify_svc.merge_min, .merge_wait_ns, .merge_idle_ns   the merge policy (fd_verify_svc_set_merge)
-     verify_svc.io_cus                                 CUs for the PCIe kernels (fd_verify_svc_set_io_cus)
    Defaults: the measured best on one MI355X, the
    same as integration/svc_run.c's. */
 
@@ -33,7 +32,6 @@
 #define SVC_INFLIGHT_DEFAULT      (2UL)
 #define SVC_MERGE_WAIT_NS_DEFAULT (2000000UL)
 #define SVC_MERGE_IDLE_NS_DEFAULT (20000UL)
-#define SVC_IO_CUS_DEFAULT        (0UL)
 
 #include "../topo/fd_topo.h"
 #include "../../util/pod/fd_pod_format.h"
@@ -109,9 +107,6 @@ privileged_init( fd_topo_t * topo, fd_topo_tile_t * tile ) {
   fd_verify_svc_set_merge( ctx->svc, fd_pod_query_ulong( topo->props, "verify_svc.merge_min", batch_max/2UL ),
                            fd_pod_query_ulong( topo->props, "verify_svc.merge_wait_ns", SVC_MERGE_WAIT_NS_DEFAULT ),
                            fd_pod_query_ulong( topo->props, "verify_svc.merge_idle_ns", SVC_MERGE_IDLE_NS_DEFAULT ) );
-  if( FD_UNLIKELY( fd_verify_svc_set_io_cus( ctx->svc, fd_pod_query_ulong( topo->props, "verify_svc.io_cus",
-                                                                            SVC_IO_CUS_DEFAULT ) ) ) )
-    FD_LOG_ERR(( "fd_verify_svc_set_io_cus failed on GPU %lu", gpu ));
   vgpu_map( ctx, topo, topo->objs[ obj_id ].wksp_id );
 
   /* every quic_verify link (service link l = its kind_id) */

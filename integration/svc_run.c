@@ -13,8 +13,7 @@
    SVC_INFLIGHT (launches at once, default 2), SVC_MERGE_MIN (frags that
    start a launch at once, default batch_max / 2), SVC_MERGE_WAIT_NS
    (default 2000000), SVC_MERGE_IDLE_NS (the wait with no launch in flight,
-   default 20000), SVC_IO_CUS (CUs for the ingest and flush kernels, the
-   rest for the verify; default 0: shared).
+   default 20000).
 
    The integration's GPU tile (integration/fd_verify_gpu_tile.c) does the
    same from the topology's objects. */
@@ -72,7 +71,6 @@ main( int argc, char ** argv ) {
     if( !dcache || fd_verify_svc_set_tile( svc, t, dcache, fd_dcache_data_sz( dcache ), base ) )
       FD_LOG_ERR(( "fd_verify_svc_set_tile %lu failed", t ));
   }
-  if( fd_verify_svc_set_io_cus( svc, env_ulong( "SVC_IO_CUS", 0UL ) ) ) FD_LOG_ERR(( "fd_verify_svc_set_io_cus failed" ));
   if( fd_verify_svc_run( svc ) ) FD_LOG_ERR(( "fd_verify_svc_run failed" ));
   FD_COMPILER_MFENCE();
   hdr->svc_ready = 1UL;
