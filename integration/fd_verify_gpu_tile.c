@@ -33,6 +33,7 @@
 #define SVC_MERGE_WAIT_NS_DEFAULT (2000000UL)
 #define SVC_MERGE_IDLE_NS_DEFAULT (20000UL)
 
+#include <stdlib.h>                           /* setenv */
 #include "../topo/fd_topo.h"
 #include "../../util/pod/fd_pod_format.h"
 #include "../../tango/mcache/fd_mcache.h"
@@ -100,6 +101,10 @@ privileged_init( fd_topo_t * topo, fd_topo_tile_t * tile ) {
   ulong gpu_cnt = fd_pod_query_ulong( topo->props, "verify_svc.gpu_cnt", 0UL );
   ulong obj_id  = fd_pod_queryf_ulong( topo->props, ULONG_MAX, "verify_svc.%lu", gpu );
   if( FD_UNLIKELY( !gpu_cnt || gpu>=gpu_cnt || obj_id==ULONG_MAX ) ) FD_LOG_ERR(( "no verify_svc object for GPU %lu", gpu ));
+  /* before the first HIP call: hardware queues for the ingest, flush and
+     launch streams (HIP's default 4 makes the ingest and flush streams wait
+     behind verify launches in shared queues) */
+  setenv( "GPU_MAX_HW_QUEUES", "16", 0 );
   ulong batch_max = fd_pod_query_ulong( topo->props, "verify_svc.batch_max", SVC_BATCH_MAX_DEFAULT );
   ulong inflight  = fd_pod_query_ulong( topo->props, "verify_svc.inflight",  SVC_INFLIGHT_DEFAULT  );
   ctx->svc = fd_verify_svc_boot( fd_topo_obj_laddr( topo, obj_id ), (int)gpu, batch_max, inflight );
