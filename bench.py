@@ -614,10 +614,12 @@ def run_tile_leg(args):
             # latency at the reference's link depth: a paced producer with no flow control, at the
             # highest of a few fractions of the measured rate that loses no frag
             tried = []
+            # a shallow link wants more, smaller request slots
+            PACED_SLOTS = {"SVC_RUN_REQ_DEPTH": "64", "SVC_RUN_SLOT_CAP": "8192"}
             for frac in (0.8, 0.5, 0.3, 0.15, 0.08):
                 rate = int(frac * best["frags_per_s"])
                 lat = SB.run_one(stream, tb, 16384, 180, os.path.join(logdir, f"paced{frac}"),
-                                 env=dict(pre, SVC_RUN_RATE=str(rate)), pin="auto")
+                                 env=dict(pre, SVC_RUN_RATE=str(rate), **PACED_SLOTS), pin="auto")
                 tried.append({"offered_frags_per_s": rate, "lost": lat["overrun"] + lat["lapped"],
                               "p50_us": lat["latency"]["p50_us"], "p99_us": lat["latency"]["p99_us"]})
                 if not lat["overrun"] and not lat["lapped"]:
@@ -634,7 +636,8 @@ def run_tile_leg(args):
                                       "over each tile's share, tcache and bundle pass in arrival order"},
                 "latency_us": {"p50": lat["latency"]["p50_us"], "p99": lat["latency"]["p99_us"],
                                "p999": lat["latency"]["p999_us"], "offered_frags_per_s": rate,
-                               "in_depth": 16384, "overrun": lat["overrun"], "lapped": lat["lapped"],
+                               "in_depth": 16384, "req_depth": 64, "slot_cap": 8192,
+                               "overrun": lat["overrun"], "lapped": lat["lapped"],
                                "achieved_verifies_per_s": lat["verifies_per_s"], "tried": tried},
                 "config": {"tiles": tb, "gpus": 1, "range_max": best["range_max"], "slot_cap": best["slot_cap"],
                            "req_depth": best["req_depth"], "out_depth": best["out_depth"], "in_depth": depth,
