@@ -91,16 +91,21 @@ def run_one(stream, tiles, in_depth, timeout, logdir, env=None, svc_env=None, sv
     errs, procs = [], []
     # pin: one core each for the producer, the GPU tile, the tiles and the consumers, on the GPU's NUMA node
     # (the reference pins every tile to a core, [layout.affinity]); "auto" picks them, or a list of CPUs
+    # the GPU tile gets SVC_CORES cores: the HIP runtime's own threads (the
+    # process's signal / callback threads) inherit its affinity, and on one
+    # core they take turns with the service loop
+    svc_cores = int(os.environ.get("SVC_BENCH_SVC_CORES", "3"))
     if pin == "auto":
-        pin = pick_cpus(2 + 2 * tiles, gpu_numa_node(gpu))
+        pin = pick_cpus(1 + svc_cores + 2 * tiles, gpu_numa_node(gpu))
     cpu_of = {}
     if pin:
-        names = ["producer", "svc"] + [f"tile{t}" for t in range(tiles)] + [f"cons{t}" for t in range(tiles)]
-        cpu_of = dict(zip(names, pin))
+        names = ["producer"] + [f"tile{t}" for t in range(tiles)] + [f"cons{t}" for t in range(tiles)]
+        cpu_of = {n: {c} for n, c in zip(names, pin)}
+        cpu_of["svc"] = set(pin[1 + 2 * tiles:1 + 2 * tiles + svc_cores])
 
     def pre(name):
         c = cpu_of.get(name)
-        return (lambda: os.sched_setaffinity(0, {c})) if c is not None else None
+        return (lambda: os.sched_setaffinity(0, c)) if c else None
 
     def spawn(cmd, name, extra=None):
         f = open(os.path.join(logdir, name + ".err"), "w")
@@ -154,7 +159,7 @@ def run_one(stream, tiles, in_depth, timeout, logdir, env=None, svc_env=None, sv
             if bad(n, p.returncode):
                 raise RuntimeError(f"{n} rc {p.returncode} (see {logdir}/{n}.err)")
         res = json.loads(out.strip().splitlines()[-1])
-        res["pinned"] = cpu_of or None
+        res["pinned"] = {k: sorted(v) for k, v in cpu_of.items()} or None
         return res
     finally:
         for _, p in procs + [("producer", prod)]:
