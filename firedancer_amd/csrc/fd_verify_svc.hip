@@ -118,10 +118,6 @@ static_assert( sizeof(svc_desc) == 128, "svc_desc layout" );
 /**********************************************************************/
 /* kernels                                                             */
 
-/* LPF lanes per frag (64: a wave per frag; 16: four frags per wave, each
-   lane moving more bytes -- fewer waves holding CU slots while they wait
-   on PCIe) */
-template<int LPF>
 __global__ __launch_bounds__(256)
 void k_svc_gather( svc_desc const * __restrict__ desc, u32 nreq, ulong n, u8 * __restrict__ ing,
                    u16 * __restrict__ ing_sz, u8 * __restrict__ ing_kind, u32 * __restrict__ ing_tso,
@@ -129,8 +125,8 @@ void k_svc_gather( svc_desc const * __restrict__ desc, u32 nreq, ulong n, u8 * _
   __shared__ u64 sbase[SVC_REQ_MAX];
   for( u32 i = threadIdx.x; i < nreq; i += blockDim.x ) sbase[i] = desc[i].base;
   __syncthreads();
-  ulong const j = (ulong)blockIdx.x * (256ul / LPF) + (threadIdx.x / LPF);
-  u32 const lane = threadIdx.x % LPF, lane0 = (threadIdx.x & 63u) - lane;   /* the frag's first lane in the wave */
+  ulong const j = (ulong)blockIdx.x * 4ul + (threadIdx.x >> 6);
+  u32 const lane = threadIdx.x & 63u;
   if( j >= n ) return;
   u32 lo = 0u, hi = nreq;                                   /* sbase[lo] <= j < sbase[hi] */
   while( hi - lo > 1u ) { u32 mid = (lo + hi) >> 1; if( sbase[mid] <= j ) lo = mid; else hi = mid; }
@@ -146,10 +142,10 @@ void k_svc_gather( svc_desc const * __restrict__ desc, u32 nreq, ulong n, u8 * _
        ctl, tsorig, tspub) with vector loads, every lane takes them */
     uint4 v = make_uint4( 0u, 0u, 0u, 0u );
     if( lane < 2u ) v = *(uint4 const *)(line + 16u * lane);
-    u64 const found = (u64)(u32)__shfl( (int)v.x, (int)lane0 ) | ((u64)(u32)__shfl( (int)v.y, (int)lane0 ) << 32);
-    u32 const chunk = (u32)__shfl( (int)v.x, (int)lane0 + 1 );
-    sz  = (u32)__shfl( (int)v.y, (int)lane0 + 1 ) & 0xffffu;
-    tsv = (u32)__shfl( (int)v.z, (int)lane0 + 1 );
+    u64 const found = (u64)(u32)__shfl( (int)v.x, 0 ) | ((u64)(u32)__shfl( (int)v.y, 0 ) << 32);
+    u32 const chunk = (u32)__shfl( (int)v.x, 1 );
+    sz  = (u32)__shfl( (int)v.y, 1 ) & 0xffffu;
+    tsv = (u32)__shfl( (int)v.z, 1 );
     ok  = found == seq && (ulong)chunk >= d->chunk0 && (ulong)chunk <= d->wmark && sz <= FD_VERIFY_HIP_TPU_RAW_MTU;
     src = (u8 const *)d->aux0 + 64ul * chunk;
   } else {
@@ -160,7 +156,7 @@ void k_svc_gather( svc_desc const * __restrict__ desc, u32 nreq, ulong n, u8 * _
   }
   ulong const f = d->ibase + i;
   u8 * dst = ing + 64ul * SVC_INGEST_CHUNKS * f;
-  if( ok ) for( u32 p = 16u * lane; p < sz; p += 16u * LPF ) *(uint4 *)(dst + p) = *(uint4 const *)(src + p);
+  if( ok ) for( u32 p = 16u * lane; p < sz; p += 1024u ) *(uint4 *)(dst + p) = *(uint4 const *)(src + p);
   /* a gossip vote's out header: the reference writes four fields into the
      out chunk's stale header (fd_verify_tile.c:90-93); here the rest is 0 */
   if( kind == FD_VERIFY_HIP_IN_GOSSIP && lane < 5u )
@@ -215,12 +211,11 @@ void k_svc_results( svc_desc const * __restrict__ desc, u32 nreq, ulong n, u16 c
 /* a flush: out entry e's staging frag (its realized bytes, in whole 64-B
    chunks) straight into the tile's out dcache (registered host memory) at the
    entry's chunk; one wave per entry, 16-B stores, a frag's bytes contiguous */
-template<int LPF>
 __global__ __launch_bounds__(256)
 void k_svc_compact( fd_verify_svc_out_t const * __restrict__ out, ulong m, u8 const * __restrict__ stage,
                     ulong stage0, u8 * __restrict__ dcache, long delta, ulong out_sz, u32 * __restrict__ err ) {
-  ulong const e = (ulong)blockIdx.x * (256ul / LPF) + (threadIdx.x / LPF);
-  u32 const lane = threadIdx.x % LPF;
+  ulong const e = (ulong)blockIdx.x * 4ul + (threadIdx.x >> 6);
+  u32 const lane = threadIdx.x & 63u;
   if( e >= m ) return;
   fd_verify_svc_out_t const o = out[e];
   if( o.flags & FD_VERIFY_SVC_OUT_HOSTWRITTEN ) return;
@@ -231,7 +226,7 @@ void k_svc_compact( fd_verify_svc_out_t const * __restrict__ out, ulong m, u8 co
   if( at < 0 || at + (long)len > (long)out_sz ) { if( lane == 0u ) *(volatile u32 *)err = 1u; return; }
   u8 const * src = stage + 64ul * (stage0 + FD_TXN_HIP_STAGE_CHUNKS * (ulong)o.idx);
   u8 *       dst = dcache + at;
-  for( u32 p = 16u * lane; p < len; p += 16u * LPF ) *(uint4 *)(dst + p) = *(uint4 const *)(src + p);
+  for( u32 p = 16u * lane; p < len; p += 1024u ) *(uint4 *)(dst + p) = *(uint4 const *)(src + p);
 }
 
 /**********************************************************************/
@@ -298,7 +293,6 @@ struct fd_verify_svc {
                                   host ns starting launches, starting flushes, retiring, polls; ingests, ingest
                                   gpu ns, host ns starting ingests, the largest launch */
   long     merge_idle_ns;      /* a launch on an idle GPU once the oldest request has waited this long */
-  int      lpf;                /* lanes per frag of the gather and flush kernels (64 or 16) */
   int      running;
 };
 
@@ -370,8 +364,6 @@ fd_verify_svc_boot( void * seg_mem, int device, ulong batch_max, ulong inflight 
   fd_verify_svc_t * s = (fd_verify_svc_t *)calloc( 1, sizeof(fd_verify_svc_t) );
   s->seg = seg; s->dev = device; s->batch_max = batch_max; s->inflight = inflight;
   s->merge_min = batch_max / 2ul; s->merge_wait_ns = 2000000L; s->merge_idle_ns = 20000L;
-  char const * lpf = getenv( "FD_VERIFY_SVC_LPF" );                /* tuning knob: 64 (default) or 16 */
-  s->lpf = lpf && atoi( lpf ) == 16 ? 16 : 64;
   SV_CHECK( hipMalloc( &s->d_stage, stage_sz + 4096ul ) );
   SV_CHECK( hipMalloc( &s->d_ing, 64ul * SVC_INGEST_CHUNKS * ing_cnt + 4096ul ) );
   SV_CHECK( hipMalloc( &s->d_ing_sz, 2ul * ing_cnt ) ); SV_CHECK( hipMalloc( &s->d_ing_kind, ing_cnt ) );
@@ -454,15 +446,11 @@ fd_verify_svc_run( fd_verify_svc_t * s ) {
                         L.d_cnt, L.d_tcode, L.d_fdesc, L.d_tso );
     SV_CHECK( hipGetLastError() );
   }
-  hipLaunchKernelGGL( k_svc_gather<64>, dim3( 1 ), dim3( 256 ), 0, s->st_ing, s->ING[0].d_desc, 0u, 0ul, s->d_ing, s->d_ing_sz,
-                      s->d_ing_kind, s->d_ing_tso, s->d_stage );
-  hipLaunchKernelGGL( k_svc_gather<16>, dim3( 1 ), dim3( 256 ), 0, s->st_ing, s->ING[0].d_desc, 0u, 0ul, s->d_ing, s->d_ing_sz,
+  hipLaunchKernelGGL( k_svc_gather, dim3( 1 ), dim3( 256 ), 0, s->st_ing, s->ING[0].d_desc, 0u, 0ul, s->d_ing, s->d_ing_sz,
                       s->d_ing_kind, s->d_ing_tso, s->d_stage );
   SV_CHECK( hipGetLastError() );
   for( ulong t = 0; t < s->seg->tile_cnt; t++ ) {
-    hipLaunchKernelGGL( k_svc_compact<64>, dim3( 1 ), dim3( 256 ), 0, s->tile[t].st, (fd_verify_svc_out_t const *)0, 0ul,
-                        (u8 const *)s->d_stage, 0ul, s->tile[t].d_out, 0L, 0ul, s->tile[t].d_err );
-    hipLaunchKernelGGL( k_svc_compact<16>, dim3( 1 ), dim3( 256 ), 0, s->tile[t].st, (fd_verify_svc_out_t const *)0, 0ul,
+    hipLaunchKernelGGL( k_svc_compact, dim3( 1 ), dim3( 256 ), 0, s->tile[t].st, (fd_verify_svc_out_t const *)0, 0ul,
                         (u8 const *)s->d_stage, 0ul, s->tile[t].d_out, 0L, 0ul, s->tile[t].d_err );
     SV_CHECK( hipGetLastError() );
   }
@@ -545,12 +533,8 @@ static void
 svc_ingest_start( fd_verify_svc_t * s, svc_ingest & I ) {
   svc_device( s->dev );
   SV_CHECK( hipEventRecord( I.ev0, s->st_ing ) );
-  if( s->lpf == 16 )
-    hipLaunchKernelGGL( k_svc_gather<16>, dim3( (unsigned)((I.n + 15ul) / 16ul) ), dim3( 256 ), 0, s->st_ing, I.d_desc,
-                        (u32)I.nreq, I.n, s->d_ing, s->d_ing_sz, s->d_ing_kind, s->d_ing_tso, s->d_stage );
-  else
-    hipLaunchKernelGGL( k_svc_gather<64>, dim3( (unsigned)((I.n + 3ul) / 4ul) ), dim3( 256 ), 0, s->st_ing, I.d_desc,
-                        (u32)I.nreq, I.n, s->d_ing, s->d_ing_sz, s->d_ing_kind, s->d_ing_tso, s->d_stage );
+  hipLaunchKernelGGL( k_svc_gather, dim3( (unsigned)((I.n + 3ul) / 4ul) ), dim3( 256 ), 0, s->st_ing, I.d_desc,
+                      (u32)I.nreq, I.n, s->d_ing, s->d_ing_sz, s->d_ing_kind, s->d_ing_tso, s->d_stage );
   SV_CHECK( hipGetLastError() );
   SV_CHECK( hipEventRecord( I.ev1, s->st_ing ) );
   I.busy = 1;
@@ -571,13 +555,9 @@ svc_flush_start( fd_verify_svc_t * s, ulong t, fd_verify_svc_flush_t const * f )
   if( m ) {
     /* the kernel checks every entry's chunks against the out dcache (the
        host does not walk the entries: the service thread drives every tile) */
-    fd_verify_svc_out_t const * d_out = (fd_verify_svc_out_t const *)svc_dev( s, out, m * sizeof(fd_verify_svc_out_t) );
-    if( s->lpf == 16 )
-      hipLaunchKernelGGL( k_svc_compact<16>, dim3( (unsigned)((m + 15ul) / 16ul) ), dim3( 256 ), 0, T.st, d_out, m,
-                          (u8 const *)s->d_stage, svc_stage0( s, t, f->slot ), T.d_out, delta, T.out_sz, T.d_err );
-    else
-      hipLaunchKernelGGL( k_svc_compact<64>, dim3( (unsigned)((m + 3ul) / 4ul) ), dim3( 256 ), 0, T.st, d_out, m,
-                          (u8 const *)s->d_stage, svc_stage0( s, t, f->slot ), T.d_out, delta, T.out_sz, T.d_err );
+    hipLaunchKernelGGL( k_svc_compact, dim3( (unsigned)((m + 3ul) / 4ul) ), dim3( 256 ), 0, T.st,
+                        (fd_verify_svc_out_t const *)svc_dev( s, out, m * sizeof(fd_verify_svc_out_t) ), m,
+                        (u8 const *)s->d_stage, svc_stage0( s, t, f->slot ), T.d_out, delta, T.out_sz, T.d_err );
     SV_CHECK( hipGetLastError() );
     s->stat[6]++;
   }
