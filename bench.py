@@ -61,7 +61,7 @@ PEAK_SLOTS = SIMDS * MAX_CLOCK / 4        # VALU issue slots/s: one quad-cycle p
 PMC_SUMMARY = "r04p_pmc_summary.json"    # rocprofv3 PMC passes of this kernel build (tools/run_profile.sh)
 ISSUE_SUMMARY = "r04p_valu_issue_calibration.json"   # VALU issue-slot pass of this build (tools/run_valu_calib.sh)
 ISSUE_SUMMARY_C4 = "r04p_c4_valu_issue.json"          # the same pass over C4's timing-leg batch (tools/run_c4_issue.sh)
-PMC_SUMMARY_C4 = "r04ab_c4_pmc_summary.json"            # FETCH/WRITE passes over the C4 bench (tools/txnm_pmc_summary.py)
+PMC_SUMMARY_C4 = "r05s_c4_pmc_summary.json"            # FETCH/WRITE passes over the C4 bench (tools/txnm_pmc_summary.py)
 
 
 def w_total(msg_sz):
