@@ -251,7 +251,6 @@ struct svc_tile {
   ulong        out_sz;
   u8 const *   chunk_base;     /* host address of out chunk 0 */
   u8 *         d_out;          /* the out dcache's device address (registered) */
-  u8 *         d_mirror;       /* DMA flushes: an HBM copy of the out dcache's layout (0: kernel flushes) */
   u32 *        h_err;          /* mapped pinned: a flush found an entry outside the out dcache */
   u32 *        d_err;
   hipStream_t  st;
@@ -294,8 +293,6 @@ struct fd_verify_svc {
                                   host ns starting launches, starting flushes, retiring, polls; ingests, ingest
                                   gpu ns, host ns starting ingests, the largest launch */
   long     merge_idle_ns;      /* a launch on an idle GPU once the oldest request has waited this long */
-  int      flush_dma;          /* flushes: compact into an HBM mirror, then the copy engine (1), or the
-                                  flush kernel writes the host out dcache itself (0) */
   int      running;
 };
 
@@ -367,8 +364,6 @@ fd_verify_svc_boot( void * seg_mem, int device, ulong batch_max, ulong inflight 
   fd_verify_svc_t * s = (fd_verify_svc_t *)calloc( 1, sizeof(fd_verify_svc_t) );
   s->seg = seg; s->dev = device; s->batch_max = batch_max; s->inflight = inflight;
   s->merge_min = batch_max / 2ul; s->merge_wait_ns = 2000000L; s->merge_idle_ns = 20000L;
-  char const * dma = getenv( "FD_VERIFY_SVC_FLUSH_DMA" );           /* tuning knob for the A/B */
-  s->flush_dma = dma && atoi( dma ) ? 1 : 0;
   SV_CHECK( hipMalloc( &s->d_stage, stage_sz + 4096ul ) );
   SV_CHECK( hipMalloc( &s->d_ing, 64ul * SVC_INGEST_CHUNKS * ing_cnt + 4096ul ) );
   SV_CHECK( hipMalloc( &s->d_ing_sz, 2ul * ing_cnt ) ); SV_CHECK( hipMalloc( &s->d_ing_kind, ing_cnt ) );
@@ -420,7 +415,6 @@ fd_verify_svc_set_tile( fd_verify_svc_t * s, ulong t, void * out_dcache, ulong o
   if( !s || t >= s->seg->tile_cnt || !out_dcache || !out_sz || s->tile[t].set ) return -1;
   svc_tile & T = s->tile[t];
   T.d_out = svc_dev( s, out_dcache, out_sz );               /* mapped: the flush kernel writes it */
-  if( s->flush_dma ) SV_CHECK( hipMalloc( &T.d_mirror, out_sz + 4096ul ) );
   SV_CHECK( hipHostMalloc( &T.h_err, 64, hipHostMallocMapped ) );
   SV_CHECK( hipHostGetDevicePointer( (void **)&T.d_err, T.h_err, 0 ) );
   *T.h_err = 0u;
@@ -558,38 +552,14 @@ svc_flush_start( fd_verify_svc_t * s, ulong t, fd_verify_svc_flush_t const * f )
   ulong const m = f->hi - f->lo;
   fd_verify_svc_out_t const * out = fd_verify_svc_out( g, t, f->slot ) + f->lo;
   long const delta = (long)(T.chunk_base - T.h_out);              /* dcache offset of chunk c: 64 c + delta */
-  /* DMA form: only for flushes whose entries are all the GPU's (a
-     host-written frag's bytes are in the host dcache, not in the mirror) */
-  bool const dma = T.d_mirror && !(f->flags & FD_VERIFY_SVC_FLUSH_HOSTWRITTEN);
   if( m ) {
     /* the kernel checks every entry's chunks against the out dcache (the
        host does not walk the entries: the service thread drives every tile) */
     hipLaunchKernelGGL( k_svc_compact, dim3( (unsigned)((m + 3ul) / 4ul) ), dim3( 256 ), 0, T.st,
                         (fd_verify_svc_out_t const *)svc_dev( s, out, m * sizeof(fd_verify_svc_out_t) ), m,
-                        (u8 const *)s->d_stage, svc_stage0( s, t, f->slot ), dma ? T.d_mirror : T.d_out, delta, T.out_sz,
-                        T.d_err );
+                        (u8 const *)s->d_stage, svc_stage0( s, t, f->slot ), T.d_out, delta, T.out_sz, T.d_err );
     SV_CHECK( hipGetLastError() );
     s->stat[6]++;
-  }
-  if( dma && m ) {
-    /* the flush's chunks run in assignment order (fd_dcache_compact_next by
-       chunk pairs): one span, or two if the ring wrapped inside the flush
-       (the wrap found by bisection over the entries, a few reads) */
-    ulong const c0 = out[0].chunk, cl = out[m - 1].chunk;
-    auto end_of = [&]( ulong e ) { return (long)(64ul * (ulong)out[e].chunk) + delta + (long)(((ulong)out[e].sz + 127ul) & ~127ul); };
-    long a0 = (long)(64ul * c0) + delta, b0, a1 = -1, b1 = -1;
-    if( cl >= c0 ) b0 = end_of( m - 1 );
-    else {
-      ulong lo = 0, hi = m - 1;                                   /* out[lo].chunk >= c0, out[hi].chunk < c0 */
-      while( hi - lo > 1 ) { ulong mid = (lo + hi) / 2; if( out[mid].chunk >= c0 ) lo = mid; else hi = mid; }
-      b0 = end_of( lo ); a1 = (long)(64ul * (ulong)out[hi].chunk) + delta; b1 = end_of( m - 1 );
-    }
-    if( a0 < 0 || b0 > (long)T.out_sz || b0 <= a0 || ( a1 >= 0 && ( b1 > (long)T.out_sz || b1 <= a1 ) ) ) {
-      fprintf( stderr, "fd_verify_svc: tile %lu: flush spans outside the out dcache\n", t );
-      abort();
-    }
-    SV_CHECK( hipMemcpyAsync( T.h_out + a0, T.d_mirror + a0, (ulong)(b0 - a0), hipMemcpyDeviceToHost, T.st ) );
-    if( a1 >= 0 ) SV_CHECK( hipMemcpyAsync( T.h_out + a1, T.d_mirror + a1, (ulong)(b1 - a1), hipMemcpyDeviceToHost, T.st ) );
   }
   SV_CHECK( hipEventRecord( T.ev[T.flush_take % SVC_FLUSH_Q], T.st ) );
   s->stat[3]++; s->stat[4] += m;
@@ -736,7 +706,6 @@ fd_verify_svc_delete( fd_verify_svc_t * s ) {
     if( !T.set ) continue;
     (void)hipStreamDestroy( T.st );
     (void)hipHostFree( T.h_err );
-    if( T.d_mirror ) (void)hipFree( T.d_mirror );
     for( ulong k = 0; k < SVC_FLUSH_Q; k++ ) (void)hipEventDestroy( T.ev[k] );
   }
   (void)hipFree( s->d_stage );

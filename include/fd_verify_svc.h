@@ -164,8 +164,7 @@ typedef struct {
   ulong rsv[ 3 ];
 } fd_verify_svc_req_t;
 
-#define FD_VERIFY_SVC_FLUSH_HOSTWRITTEN (1UL)   /* an entry of the flush's slot may be host-written */
-typedef struct { ulong slot, lo, hi, flags; } fd_verify_svc_flush_t;
+typedef struct { ulong slot, lo, hi, rsv; } fd_verify_svc_flush_t;
 
 /* A tile's block (followed by its slots and their arrays). */
 typedef struct {
@@ -330,12 +329,12 @@ fd_verify_svc_post_frags( fd_verify_svc_seg_t * s, ulong t, ulong id, ulong n, u
 
 /* Out entries [lo, hi) of slot to be written; -1 if the ring is full. */
 static inline int
-fd_verify_svc_post_flush( fd_verify_svc_seg_t * s, ulong t, ulong slot, ulong lo, ulong hi, ulong flags ) {
+fd_verify_svc_post_flush( fd_verify_svc_seg_t * s, ulong t, ulong slot, ulong lo, ulong hi ) {
   fd_verify_svc_tile_t * b = fd_verify_svc_tile( s, t );
   ulong post = b->flush_post;                                   /* only this tile writes it */
   if( post - fd_verify_svc_ld( &b->flush_done )>=FD_VERIFY_SVC_FLUSH_DEPTH ) return -1;
   fd_verify_svc_flush_t * f = &b->flush[ post & ( FD_VERIFY_SVC_FLUSH_DEPTH-1UL ) ];
-  f->slot = slot; f->lo = lo; f->hi = hi; f->flags = flags;
+  f->slot = slot; f->lo = lo; f->hi = hi;
   fd_verify_svc_st( &b->flush_post, post+1UL );
   return 0;
 }

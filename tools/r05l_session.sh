@@ -12,4 +12,7 @@ run w2i2 2,3,4 "SVC_RUN_REQ_DEPTH=8" "SVC_MERGE_WAIT_NS=2000000,SVC_INFLIGHT=2" 
 run w2i2d16 2,3 "SVC_RUN_REQ_DEPTH=16" "SVC_MERGE_WAIT_NS=2000000,SVC_INFLIGHT=2" || exit $?
 run v1 2,3 "SVC_RUN_REQ_DEPTH=16" "SVC_INFLIGHT=2,SVC_MERGE_WAIT_NS=2000000,SVC_MERGE_IDLE_NS=2000000,SVC_MERGE_MIN=262144,SVC_BATCH_MAX=524288" || exit $?
 SVC_BENCH_HIP_TRACE=1 timeout -k 10 240 python -u tools/svc_bench.py --frags 4194304 --tiles 3 --prelay --env SVC_RUN_REQ_DEPTH=8 \
-  --svc-env SVC_MERGE_WAIT_NS=2000000,SVC_INFLIGHT=2 --rocprof $out/prof --timeout 200 --logdir $out/logsp > $out/prof.jsonl 2> $out/prof.err
+  --svc-env SVC_MERGE_WAIT_NS=2000000,SVC_INFLIGHT=2 --rocprof $out/prof --timeout 200 --logdir $out/logsp > $out/prof.jsonl 2> $out/prof.err;
+# keep only the summaries: the API trace of a polling loop is hundreds of MiB
+find $out/prof -name "*trace*.csv" -delete
+du -sh $out
