@@ -125,43 +125,45 @@ void k_svc_gather( svc_desc const * __restrict__ desc, u32 nreq, ulong n, u8 * _
   __shared__ u64 sbase[SVC_REQ_MAX];
   for( u32 i = threadIdx.x; i < nreq; i += blockDim.x ) sbase[i] = desc[i].base;
   __syncthreads();
-  ulong const j = (ulong)blockIdx.x * 4ul + (threadIdx.x >> 6);
   u32 const lane = threadIdx.x & 63u;
-  if( j >= n ) return;
-  u32 lo = 0u, hi = nreq;                                   /* sbase[lo] <= j < sbase[hi] */
-  while( hi - lo > 1u ) { u32 mid = (lo + hi) >> 1; if( sbase[mid] <= j ) lo = mid; else hi = mid; }
-  svc_desc const * d = desc + lo;
-  ulong const i = j - d->base;
-  u32 sz = 0u, kind = FD_VERIFY_HIP_IN_QUIC, tsv = 0u;
-  bool ok;
-  u8 const * src;
-  if( d->kind == FD_VERIFY_SVC_REQ_RANGE ) {
-    ulong const seq = d->first + i * d->stride;
-    u8 const * line = (u8 const *)d->src + 32ul * (seq & d->line_mask);
-    /* lanes 0 and 1 read the line's two halves (seq, sig | chunk, sz,
-       ctl, tsorig, tspub) with vector loads, every lane takes them */
-    uint4 v = make_uint4( 0u, 0u, 0u, 0u );
-    if( lane < 2u ) v = *(uint4 const *)(line + 16u * lane);
-    u64 const found = (u64)(u32)__shfl( (int)v.x, 0 ) | ((u64)(u32)__shfl( (int)v.y, 0 ) << 32);
-    u32 const chunk = (u32)__shfl( (int)v.x, 1 );
-    sz  = (u32)__shfl( (int)v.y, 1 ) & 0xffffu;
-    tsv = (u32)__shfl( (int)v.z, 1 );
-    ok  = found == seq && (ulong)chunk >= d->chunk0 && (ulong)chunk <= d->wmark && sz <= FD_VERIFY_HIP_TPU_RAW_MTU;
-    src = (u8 const *)d->aux0 + 64ul * chunk;
-  } else {
-    src  = (u8 const *)d->src + FD_VERIFY_SVC_FRAG_STRIDE * i;
-    sz   = ((u16 const *)d->aux0)[i];
-    kind = ((u8 const *)d->aux1)[i];
-    ok   = sz <= FD_VERIFY_SVC_FRAG_STRIDE;
+  /* one wave per frag, grid-stride: a grid of n/4 workgroups takes each frag
+     once; a capped grid (gather_wgs) loops */
+  for( ulong j = (ulong)blockIdx.x * 4ul + (threadIdx.x >> 6); j < n; j += 4ul * gridDim.x ) {
+    u32 lo = 0u, hi = nreq;                                 /* sbase[lo] <= j < sbase[hi] */
+    while( hi - lo > 1u ) { u32 mid = (lo + hi) >> 1; if( sbase[mid] <= j ) lo = mid; else hi = mid; }
+    svc_desc const * d = desc + lo;
+    ulong const i = j - d->base;
+    u32 sz = 0u, kind = FD_VERIFY_HIP_IN_QUIC, tsv = 0u;
+    bool ok;
+    u8 const * src;
+    if( d->kind == FD_VERIFY_SVC_REQ_RANGE ) {
+      ulong const seq = d->first + i * d->stride;
+      u8 const * line = (u8 const *)d->src + 32ul * (seq & d->line_mask);
+      /* lanes 0 and 1 read the line's two halves (seq, sig | chunk, sz,
+         ctl, tsorig, tspub) with vector loads, every lane takes them */
+      uint4 v = make_uint4( 0u, 0u, 0u, 0u );
+      if( lane < 2u ) v = *(uint4 const *)(line + 16u * lane);
+      u64 const found = (u64)(u32)__shfl( (int)v.x, 0 ) | ((u64)(u32)__shfl( (int)v.y, 0 ) << 32);
+      u32 const chunk = (u32)__shfl( (int)v.x, 1 );
+      sz  = (u32)__shfl( (int)v.y, 1 ) & 0xffffu;
+      tsv = (u32)__shfl( (int)v.z, 1 );
+      ok  = found == seq && (ulong)chunk >= d->chunk0 && (ulong)chunk <= d->wmark && sz <= FD_VERIFY_HIP_TPU_RAW_MTU;
+      src = (u8 const *)d->aux0 + 64ul * chunk;
+    } else {
+      src  = (u8 const *)d->src + FD_VERIFY_SVC_FRAG_STRIDE * i;
+      sz   = ((u16 const *)d->aux0)[i];
+      kind = ((u8 const *)d->aux1)[i];
+      ok   = sz <= FD_VERIFY_SVC_FRAG_STRIDE;
+    }
+    ulong const f = d->ibase + i;
+    u8 * dst = ing + 64ul * SVC_INGEST_CHUNKS * f;
+    if( ok ) for( u32 p = 16u * lane; p < sz; p += 1024u ) *(uint4 *)(dst + p) = *(uint4 const *)(src + p);
+    /* a gossip vote's out header: the reference writes four fields into the
+       out chunk's stale header (fd_verify_tile.c:90-93); here the rest is 0 */
+    if( kind == FD_VERIFY_HIP_IN_GOSSIP && lane < 5u )
+      *(uint4 *)(stage + 64ul * (d->stage0 + FD_TXN_HIP_STAGE_CHUNKS * i) + 16u * lane) = make_uint4( 0u, 0u, 0u, 0u );
+    if( lane == 0u ) { ing_sz[f] = ok ? (u16)sz : (u16)0xffffu; ing_kind[f] = (u8)kind; ing_tso[f] = tsv; }
   }
-  ulong const f = d->ibase + i;
-  u8 * dst = ing + 64ul * SVC_INGEST_CHUNKS * f;
-  if( ok ) for( u32 p = 16u * lane; p < sz; p += 1024u ) *(uint4 *)(dst + p) = *(uint4 const *)(src + p);
-  /* a gossip vote's out header: the reference writes four fields into the
-     out chunk's stale header (fd_verify_tile.c:90-93); here the rest is 0 */
-  if( kind == FD_VERIFY_HIP_IN_GOSSIP && lane < 5u )
-    *(uint4 *)(stage + 64ul * (d->stage0 + FD_TXN_HIP_STAGE_CHUNKS * i) + 16u * lane) = make_uint4( 0u, 0u, 0u, 0u );
-  if( lane == 0u ) { ing_sz[f] = ok ? (u16)sz : (u16)0xffffu; ing_kind[f] = (u8)kind; ing_tso[f] = tsv; }
 }
 
 /* a verify launch's per-frag arrays (launch frag j = frag i of request d)
@@ -276,6 +278,7 @@ struct fd_verify_svc {
   int      dev;
   ulong    batch_max, inflight;
   ulong    merge_min; long merge_wait_ns;
+  ulong    gather_wgs;   /* the gather's grid cap (0: one wave per frag); FD_VERIFY_SVC_GATHER_WGS */
   struct { u8 * h; ulong sz; u8 * d; } reg[SVC_REGION_MAX];
   ulong    nreg;
   struct { int set; u8 const * d_mcache; ulong depth; u8 const * d_base; ulong chunk0, wmark; } link[FD_VERIFY_SVC_LINK_MAX];
@@ -363,6 +366,7 @@ fd_verify_svc_boot( void * seg_mem, int device, ulong batch_max, ulong inflight 
   SV_CHECK( hipSetDevice( device ) );
   fd_verify_svc_t * s = (fd_verify_svc_t *)calloc( 1, sizeof(fd_verify_svc_t) );
   s->seg = seg; s->dev = device; s->batch_max = batch_max; s->inflight = inflight;
+  { char const * e = getenv( "FD_VERIFY_SVC_GATHER_WGS" ); s->gather_wgs = e ? strtoul( e, 0, 0 ) : 0ul; }
   s->merge_min = batch_max / 2ul; s->merge_wait_ns = 2000000L; s->merge_idle_ns = 20000L;
   SV_CHECK( hipMalloc( &s->d_stage, stage_sz + 4096ul ) );
   SV_CHECK( hipMalloc( &s->d_ing, 64ul * SVC_INGEST_CHUNKS * ing_cnt + 4096ul ) );
@@ -533,7 +537,9 @@ static void
 svc_ingest_start( fd_verify_svc_t * s, svc_ingest & I ) {
   svc_device( s->dev );
   SV_CHECK( hipEventRecord( I.ev0, s->st_ing ) );
-  hipLaunchKernelGGL( k_svc_gather, dim3( (unsigned)((I.n + 3ul) / 4ul) ), dim3( 256 ), 0, s->st_ing, I.d_desc,
+  ulong wgs = (I.n + 3ul) / 4ul;
+  if( s->gather_wgs && wgs > s->gather_wgs ) wgs = s->gather_wgs;
+  hipLaunchKernelGGL( k_svc_gather, dim3( (unsigned)wgs ), dim3( 256 ), 0, s->st_ing, I.d_desc,
                       (u32)I.nreq, I.n, s->d_ing, s->d_ing_sz, s->d_ing_kind, s->d_ing_tso, s->d_stage );
   SV_CHECK( hipGetLastError() );
   SV_CHECK( hipEventRecord( I.ev1, s->st_ing ) );
