@@ -216,19 +216,20 @@ void k_svc_results( svc_desc const * __restrict__ desc, u32 nreq, ulong n, u16 c
 __global__ __launch_bounds__(256)
 void k_svc_compact( fd_verify_svc_out_t const * __restrict__ out, ulong m, u8 const * __restrict__ stage,
                     ulong stage0, u8 * __restrict__ dcache, long delta, ulong out_sz, u32 * __restrict__ err ) {
-  ulong const e = (ulong)blockIdx.x * 4ul + (threadIdx.x >> 6);
   u32 const lane = threadIdx.x & 63u;
-  if( e >= m ) return;
-  fd_verify_svc_out_t const o = out[e];
-  if( o.flags & FD_VERIFY_SVC_OUT_HOSTWRITTEN ) return;
-  u32 const len = ((u32)o.sz + 63u) & ~63u;
-  long const at = (long)(64ul * (ulong)o.chunk) + delta;
-  /* the tile's chunk must lie inside its out dcache: a bad entry is
-     reported (the service aborts at the flush's retirement), never written */
-  if( at < 0 || at + (long)len > (long)out_sz ) { if( lane == 0u ) *(volatile u32 *)err = 1u; return; }
-  u8 const * src = stage + 64ul * (stage0 + FD_TXN_HIP_STAGE_CHUNKS * (ulong)o.idx);
-  u8 *       dst = dcache + at;
-  for( u32 p = 16u * lane; p < len; p += 1024u ) *(uint4 *)(dst + p) = *(uint4 const *)(src + p);
+  /* one wave per entry, grid-stride (a capped grid, flush_wgs, loops) */
+  for( ulong e = (ulong)blockIdx.x * 4ul + (threadIdx.x >> 6); e < m; e += 4ul * gridDim.x ) {
+    fd_verify_svc_out_t const o = out[e];
+    if( o.flags & FD_VERIFY_SVC_OUT_HOSTWRITTEN ) continue;
+    u32 const len = ((u32)o.sz + 63u) & ~63u;
+    long const at = (long)(64ul * (ulong)o.chunk) + delta;
+    /* the tile's chunk must lie inside its out dcache: a bad entry is
+       reported (the service aborts at the flush's retirement), never written */
+    if( at < 0 || at + (long)len > (long)out_sz ) { if( lane == 0u ) *(volatile u32 *)err = 1u; continue; }
+    u8 const * src = stage + 64ul * (stage0 + FD_TXN_HIP_STAGE_CHUNKS * (ulong)o.idx);
+    u8 *       dst = dcache + at;
+    for( u32 p = 16u * lane; p < len; p += 1024u ) *(uint4 *)(dst + p) = *(uint4 const *)(src + p);
+  }
 }
 
 /**********************************************************************/
@@ -279,6 +280,7 @@ struct fd_verify_svc {
   ulong    batch_max, inflight;
   ulong    merge_min; long merge_wait_ns;
   ulong    gather_wgs;   /* the gather's grid cap (0: one wave per frag); FD_VERIFY_SVC_GATHER_WGS */
+  ulong    flush_wgs;    /* the flush kernel's grid cap (0: one wave per entry); FD_VERIFY_SVC_FLUSH_WGS */
   struct { u8 * h; ulong sz; u8 * d; } reg[SVC_REGION_MAX];
   ulong    nreg;
   struct { int set; u8 const * d_mcache; ulong depth; u8 const * d_base; ulong chunk0, wmark; } link[FD_VERIFY_SVC_LINK_MAX];
@@ -367,6 +369,7 @@ fd_verify_svc_boot( void * seg_mem, int device, ulong batch_max, ulong inflight 
   fd_verify_svc_t * s = (fd_verify_svc_t *)calloc( 1, sizeof(fd_verify_svc_t) );
   s->seg = seg; s->dev = device; s->batch_max = batch_max; s->inflight = inflight;
   { char const * e = getenv( "FD_VERIFY_SVC_GATHER_WGS" ); s->gather_wgs = e ? strtoul( e, 0, 0 ) : 0ul; }
+  { char const * e = getenv( "FD_VERIFY_SVC_FLUSH_WGS" );  s->flush_wgs  = e ? strtoul( e, 0, 0 ) : 0ul; }
   s->merge_min = batch_max / 2ul; s->merge_wait_ns = 2000000L; s->merge_idle_ns = 20000L;
   SV_CHECK( hipMalloc( &s->d_stage, stage_sz + 4096ul ) );
   SV_CHECK( hipMalloc( &s->d_ing, 64ul * SVC_INGEST_CHUNKS * ing_cnt + 4096ul ) );
@@ -561,7 +564,9 @@ svc_flush_start( fd_verify_svc_t * s, ulong t, fd_verify_svc_flush_t const * f )
   if( m ) {
     /* the kernel checks every entry's chunks against the out dcache (the
        host does not walk the entries: the service thread drives every tile) */
-    hipLaunchKernelGGL( k_svc_compact, dim3( (unsigned)((m + 3ul) / 4ul) ), dim3( 256 ), 0, T.st,
+    ulong wgs = (m + 3ul) / 4ul;
+    if( s->flush_wgs && wgs > s->flush_wgs ) wgs = s->flush_wgs;
+    hipLaunchKernelGGL( k_svc_compact, dim3( (unsigned)wgs ), dim3( 256 ), 0, T.st,
                         (fd_verify_svc_out_t const *)svc_dev( s, out, m * sizeof(fd_verify_svc_out_t) ), m,
                         (u8 const *)s->d_stage, svc_stage0( s, t, f->slot ), T.d_out, delta, T.out_sz, T.d_err );
     SV_CHECK( hipGetLastError() );
