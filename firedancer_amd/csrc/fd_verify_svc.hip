@@ -78,6 +78,7 @@ typedef uint64_t u64;
 #define SVC_INGEST_CHUNKS 32ul   /* an ingest frag: 2048 B (a gossip message's bound, the RAW_MTU's 1312 below it) */
 #define SVC_REQ_MAX       64u    /* requests per launch */
 #define SVC_LAUNCH_MAX    8ul
+#define SVC_GATHER_WGS    256ul  /* the gather's default grid: 1024 waves, enough to keep PCIe busy (64: 2x slower) */
 #define SVC_FLUSH_Q       64ul   /* flushes in flight per tile */
 #define SVC_REGION_MAX    64ul
 #define SVC_ING_MAX       8ul    /* ingest batches in flight */
@@ -279,7 +280,9 @@ struct fd_verify_svc {
   int      dev;
   ulong    batch_max, inflight;
   ulong    merge_min; long merge_wait_ns;
-  ulong    gather_wgs;   /* the gather's grid cap (0: one wave per frag); FD_VERIFY_SVC_GATHER_WGS */
+  ulong    gather_wgs;   /* the gather's grid cap (0: one wave per frag); FD_VERIFY_SVC_GATHER_WGS, default
+                            SVC_GATHER_WGS: a grid of one wave per frag fills the GPU with waves that wait on
+                            PCIe reads, and the verify launches beside it ran ~12% slower (profiles/r05u,v) */
   ulong    flush_wgs;    /* the flush kernel's grid cap (0: one wave per entry); FD_VERIFY_SVC_FLUSH_WGS */
   struct { u8 * h; ulong sz; u8 * d; } reg[SVC_REGION_MAX];
   ulong    nreg;
@@ -294,6 +297,9 @@ struct fd_verify_svc {
   svc_desc * sdesc;            /* per (tile, slot): the request's descriptor, made at ingest */
   svc_launch L[SVC_LAUNCH_MAX];
   svc_pend * pend; ulong pend_cap, pend_head, pend_tail, pend_frags;
+  ulong    occ[6];             /* every 64th poll: samples, then the summed slot counts posted (not yet
+                                  ingested), ingested and waiting for a launch, in a launch, results (the
+                                  tile's ordered pass, flushes, publish), free */
   ulong    stat[16];           /* launches, frags, requests, flushes, flushed frags, flushed bytes, flush kernels, gpu ns;
                                   host ns starting launches, starting flushes, retiring, polls; ingests, ingest
                                   gpu ns, host ns starting ingests, the largest launch */
@@ -368,7 +374,7 @@ fd_verify_svc_boot( void * seg_mem, int device, ulong batch_max, ulong inflight 
   SV_CHECK( hipSetDevice( device ) );
   fd_verify_svc_t * s = (fd_verify_svc_t *)calloc( 1, sizeof(fd_verify_svc_t) );
   s->seg = seg; s->dev = device; s->batch_max = batch_max; s->inflight = inflight;
-  { char const * e = getenv( "FD_VERIFY_SVC_GATHER_WGS" ); s->gather_wgs = e ? strtoul( e, 0, 0 ) : 0ul; }
+  { char const * e = getenv( "FD_VERIFY_SVC_GATHER_WGS" ); s->gather_wgs = e ? strtoul( e, 0, 0 ) : SVC_GATHER_WGS; }
   { char const * e = getenv( "FD_VERIFY_SVC_FLUSH_WGS" );  s->flush_wgs  = e ? strtoul( e, 0, 0 ) : 0ul; }
   s->merge_min = batch_max / 2ul; s->merge_wait_ns = 2000000L; s->merge_idle_ns = 20000L;
   SV_CHECK( hipMalloc( &s->d_stage, stage_sz + 4096ul ) );
@@ -584,6 +590,18 @@ fd_verify_svc_poll( fd_verify_svc_t * s ) {
   svc_device( s->dev );
   g->svc_heartbeat++;
   s->stat[11]++;
+  if( !(s->stat[11] & 63ul) ) {
+    ulong c[4] = { 0ul, 0ul, 0ul, 0ul };
+    for( ulong t = 0; t < g->tile_cnt; t++ )
+      for( ulong k = 0; k < g->req_depth; k++ ) {
+        ulong st = fd_verify_svc_ld( &fd_verify_svc_req( g, t, k )->state );
+        c[st == FD_VERIFY_SVC_POSTED ? 0 : st == FD_VERIFY_SVC_INGESTED ? 1 : st == FD_VERIFY_SVC_RESULTS ? 2 : 3]++;
+      }
+    ulong launched = 0;
+    for( ulong k = 0; k < s->inflight; k++ ) if( s->L[k].busy ) launched += s->L[k].nreq;
+    s->occ[0]++; s->occ[1] += c[0]; s->occ[2] += c[1] - launched; s->occ[3] += launched; s->occ[4] += c[2];
+    s->occ[5] += c[3];
+  }
   /* 1. finished verify launches: their slots' results are in the segment */
   ulong busy = 0;
   for( ulong k = 0; k < s->inflight; k++ ) {
@@ -704,6 +722,11 @@ fd_verify_svc_poll( fd_verify_svc_t * s ) {
 extern "C" void
 fd_verify_svc_stats( fd_verify_svc_t const * s, ulong out[16] ) {
   for( int k = 0; k < 16; k++ ) out[k] = s->stat[k];
+}
+
+extern "C" void
+fd_verify_svc_occupancy( fd_verify_svc_t const * s, ulong out[6] ) {
+  for( int k = 0; k < 6; k++ ) out[k] = s->occ[k];
 }
 
 extern "C" void

@@ -86,6 +86,9 @@ main( int argc, char ** argv ) {
   ulong st[ 16 ];
   fd_verify_svc_stats( svc, st );
   for( ulong k=0UL; k<16UL; k++ ) hdr->svc_stats[ k ] = st[ k ];
+  ulong occ[ 6 ];
+  fd_verify_svc_occupancy( svc, occ );
+  for( ulong k=0UL; k<6UL; k++ ) hdr->svc_occ[ k ] = occ[ k ];
   fd_verify_svc_delete( svc );
   FD_COMPILER_MFENCE();
   hdr->svc_done = 1UL;

@@ -52,6 +52,7 @@ typedef struct {
   volatile ulong tiles_ready, cons_ready, svc_ready, start, shutdown, svc_done;
   volatile long  t0, t_pub;
   volatile ulong svc_stats[ 16 ];
+  volatile ulong svc_occ[ 6 ];                 /* fd_verify_svc_occupancy */
   svc_run_tile_res_t tile[ SVC_RUN_TILE_MAX ];
   svc_run_cons_res_t cons[ SVC_RUN_TILE_MAX ];
 } svc_run_hdr_t;

@@ -337,14 +337,18 @@ produce( char const * path, char const * stream, ulong tile_cnt, ulong in_depth 
           (double)( reg[0]+reg[3]+reg[6] )/rt, (double)( reg[1]+reg[4]+reg[7] )/rt, (double)( reg[2]+reg[5] )/rt );
   print_lat( "latency", lat ); printf( ", " );
   print_lat( "latency_to_consumer", latq ); printf( ", " );
+  double occ_n = (double)hdr->svc_occ[0] + 1e-9;
   printf( "\"svc\": {\"launches\": %lu, \"frags\": %lu, \"requests\": %lu, \"flushes\": %lu, \"flushed_frags\": %lu, "
           "\"flushed_bytes\": %lu, \"spans\": %lu, \"gpu_s\": %.6f, \"host_launch_s\": %.6f, \"host_flush_s\": %.6f, "
           "\"host_poll_s\": %.6f, \"polls\": %lu, \"ingests\": %lu, \"ingest_gpu_s\": %.6f, \"host_ingest_s\": %.6f, "
-          "\"launch_max\": %lu}, ",
+          "\"launch_max\": %lu, \"slots\": {\"posted\": %.3f, \"waiting\": %.3f, \"launched\": %.3f, \"results\": %.3f, "
+          "\"free\": %.3f}}, ",
           hdr->svc_stats[0], hdr->svc_stats[1], hdr->svc_stats[2], hdr->svc_stats[3], hdr->svc_stats[4],
           hdr->svc_stats[5], hdr->svc_stats[6], (double)hdr->svc_stats[7]*1e-9, (double)hdr->svc_stats[8]*1e-9,
           (double)hdr->svc_stats[9]*1e-9, (double)hdr->svc_stats[10]*1e-9, hdr->svc_stats[11], hdr->svc_stats[12],
-          (double)hdr->svc_stats[13]*1e-9, (double)hdr->svc_stats[14]*1e-9, hdr->svc_stats[15] );
+          (double)hdr->svc_stats[13]*1e-9, (double)hdr->svc_stats[14]*1e-9, hdr->svc_stats[15],
+          (double)hdr->svc_occ[1]/occ_n, (double)hdr->svc_occ[2]/occ_n, (double)hdr->svc_occ[3]/occ_n,
+          (double)hdr->svc_occ[4]/occ_n, (double)hdr->svc_occ[5]/occ_n );
   printf( "\"frags\": %lu, \"sigs\": %lu, \"published\": %lu, \"parse_fail\": %lu, \"verify_fail\": %lu, "
           "\"dedup\": %lu, \"bundle_peer_fail\": %lu, \"overrun\": %lu, \"lapped\": %lu, \"host_redone\": %lu, "
           "\"consumed\": %lu, \"consumer_bad\": %lu, \"digest_on\": %d, \"metrics_ok\": %lu, \"tile_threads_max\": %lu, \"tile_dev_fds\": %lu, "
