@@ -79,6 +79,7 @@ typedef uint64_t u64;
 #define SVC_REQ_MAX       64u    /* requests per launch */
 #define SVC_LAUNCH_MAX    8ul
 #define SVC_GATHER_WGS    256ul  /* the gather's default grid: 1024 waves, enough to keep PCIe busy (64: 2x slower) */
+#define SVC_FLUSH_WGS     256ul  /* the flush kernel's default grid */
 #define SVC_FLUSH_Q       64ul   /* flushes in flight per tile */
 #define SVC_REGION_MAX    64ul
 #define SVC_ING_MAX       8ul    /* ingest batches in flight */
@@ -283,7 +284,8 @@ struct fd_verify_svc {
   ulong    gather_wgs;   /* the gather's grid cap (0: one wave per frag); FD_VERIFY_SVC_GATHER_WGS, default
                             SVC_GATHER_WGS: a grid of one wave per frag fills the GPU with waves that wait on
                             PCIe reads, and the verify launches beside it ran ~12% slower (profiles/r05u,v) */
-  ulong    flush_wgs;    /* the flush kernel's grid cap (0: one wave per entry); FD_VERIFY_SVC_FLUSH_WGS */
+  ulong    flush_wgs;    /* the flush kernel's grid cap (0: one wave per entry); FD_VERIFY_SVC_FLUSH_WGS, default
+                            SVC_FLUSH_WGS (profiles/r05w: 3 tiles 65-68 vs 61-64 M uncapped) */
   struct { u8 * h; ulong sz; u8 * d; } reg[SVC_REGION_MAX];
   ulong    nreg;
   struct { int set; u8 const * d_mcache; ulong depth; u8 const * d_base; ulong chunk0, wmark; } link[FD_VERIFY_SVC_LINK_MAX];
@@ -297,7 +299,7 @@ struct fd_verify_svc {
   svc_desc * sdesc;            /* per (tile, slot): the request's descriptor, made at ingest */
   svc_launch L[SVC_LAUNCH_MAX];
   svc_pend * pend; ulong pend_cap, pend_head, pend_tail, pend_frags;
-  ulong    occ[6];             /* every 64th poll: samples, then the summed slot counts posted (not yet
+  ulong    occ[6];             /* every 64th poll with a slot in use: samples, then the summed slot counts posted (not yet
                                   ingested), ingested and waiting for a launch, in a launch, results (the
                                   tile's ordered pass, flushes, publish), free */
   ulong    stat[16];           /* launches, frags, requests, flushes, flushed frags, flushed bytes, flush kernels, gpu ns;
@@ -375,7 +377,7 @@ fd_verify_svc_boot( void * seg_mem, int device, ulong batch_max, ulong inflight 
   fd_verify_svc_t * s = (fd_verify_svc_t *)calloc( 1, sizeof(fd_verify_svc_t) );
   s->seg = seg; s->dev = device; s->batch_max = batch_max; s->inflight = inflight;
   { char const * e = getenv( "FD_VERIFY_SVC_GATHER_WGS" ); s->gather_wgs = e ? strtoul( e, 0, 0 ) : SVC_GATHER_WGS; }
-  { char const * e = getenv( "FD_VERIFY_SVC_FLUSH_WGS" );  s->flush_wgs  = e ? strtoul( e, 0, 0 ) : 0ul; }
+  { char const * e = getenv( "FD_VERIFY_SVC_FLUSH_WGS" );  s->flush_wgs  = e ? strtoul( e, 0, 0 ) : SVC_FLUSH_WGS; }
   s->merge_min = batch_max / 2ul; s->merge_wait_ns = 2000000L; s->merge_idle_ns = 20000L;
   SV_CHECK( hipMalloc( &s->d_stage, stage_sz + 4096ul ) );
   SV_CHECK( hipMalloc( &s->d_ing, 64ul * SVC_INGEST_CHUNKS * ing_cnt + 4096ul ) );
@@ -599,8 +601,10 @@ fd_verify_svc_poll( fd_verify_svc_t * s ) {
       }
     ulong launched = 0;
     for( ulong k = 0; k < s->inflight; k++ ) if( s->L[k].busy ) launched += s->L[k].nreq;
-    s->occ[0]++; s->occ[1] += c[0]; s->occ[2] += c[1] - launched; s->occ[3] += launched; s->occ[4] += c[2];
-    s->occ[5] += c[3];
+    if( c[3] < g->tile_cnt * g->req_depth ) {                  /* only while some slot is in use */
+      s->occ[0]++; s->occ[1] += c[0]; s->occ[2] += c[1] - launched; s->occ[3] += launched; s->occ[4] += c[2];
+      s->occ[5] += c[3];
+    }
   }
   /* 1. finished verify launches: their slots' results are in the segment */
   ulong busy = 0;

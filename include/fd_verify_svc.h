@@ -400,10 +400,11 @@ void              fd_verify_svc_set_merge( fd_verify_svc_t * svc, ulong min_frag
 int               fd_verify_svc_run     ( fd_verify_svc_t * svc );
 int               fd_verify_svc_poll    ( fd_verify_svc_t * svc );
 void              fd_verify_svc_stats   ( fd_verify_svc_t const * svc, ulong out[ 16 ] );
-/* where the slots are, sampled every 64th poll: out[0] samples, then the
-   summed slot counts posted (not yet ingested), ingested and waiting for a
-   launch, in a launch, results (the tile's ordered pass, flushes and
-   publish), free.  Divide by out[0] for the mean occupancy of each state. */
+/* where the slots are, sampled every 64th poll while any slot is in use:
+   out[0] samples, then the summed slot counts posted (not yet ingested),
+   ingested and waiting for a launch, in a launch, results (the tile's
+   ordered pass, flushes and publish), free.  Divide by out[0] for the mean
+   occupancy of each state. */
 void              fd_verify_svc_occupancy( fd_verify_svc_t const * svc, ulong out[ 6 ] );
 void              fd_verify_svc_delete  ( fd_verify_svc_t * svc );
 

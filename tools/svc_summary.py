@@ -13,4 +13,5 @@ for path in sys.argv[1:]:
         print(f"T{r['tile_cnt']} {r['verifies_per_s']/1e6:6.1f} M/s {r['frags_per_s']/1e6:5.1f} Mfr/s {r['seconds']:.3f}s "
               f"launch {sv['launches']} ({sv['frags']/max(sv['launches'],1)/1e3:.0f}K fr) gpu {sv['gpu_s']:.3f}s "
               f"flush {sv['flushes']} ({sv['flushed_frags']/max(sv['flushes'],1):.0f} fr) spans {sv['spans']} "
-              f"reg {r['regime']} tile-busy {b} ovr {r['overrun']}/{r['lapped']} lat {r['latency']['p50_us']}/{r['latency']['p99_us']}")
+              f"reg {r['regime']} tile-busy {b} ovr {r['overrun']}/{r['lapped']} lat {r['latency']['p50_us']}/{r['latency']['p99_us']}"
+              + (f" slots {sv['slots']}" if "slots" in sv else ""))
