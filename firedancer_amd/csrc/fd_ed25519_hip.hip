@@ -1265,6 +1265,11 @@ fd_ed25519_hip_ctx_new( int device, ulong chunk_sigs ) {
     /* A/B: every context's DSM grid 1/share of the resident slots (contexts sharing the GPU;
        fd_ed25519_hip_set_dsm_share sets it per context) */
     { char const * ds = getenv( "FD_ED25519_HIP_DSM_SHARE" ); if( ds && atoi( ds ) > 0 ) ctx->dsm_share = (ulong)atoi( ds ); }
+    /* A/B: leave this many resident DSM workgroup slots free (room on some
+       CUs for kernels of other streams while a DSM runs) */
+    { char const * dr = getenv( "FD_ED25519_HIP_DSM_RESERVE" );
+      ulong r = dr ? strtoul( dr, 0, 0 ) : 0ul;
+      ctx->dsm_wgs = r < ctx->dsm_wgs ? ctx->dsm_wgs - r : 1ul; }
     ctx->ncu = (ulong)(ncu_ > 0 ? ncu_ : 1);
     FD_CHECK( hipMalloc( (void **)&ctx->d_lat_done, LAT_MAX_N * sizeof(ulong) ) );
     FD_CHECK( hipMemsetAsync( ctx->d_lat_done, 0, LAT_MAX_N * sizeof(ulong), ctx->stream ) );
