@@ -33,7 +33,7 @@ sys.path.insert(0, REPO)
 sys.path.insert(0, os.path.join(REPO, "tests"))
 sys.path.insert(0, os.path.join(REPO, "tools"))
 BUILD = os.path.join(REPO, "integration", "_build")
-EXE = os.path.join(BUILD, "svc_tile_run")
+EXE = os.environ.get("SVC_BENCH_TILE_EXE", os.path.join(BUILD, "svc_tile_run"))   # a build variant for an A/B
 SVC = os.path.join(BUILD, "svc_run")
 
 
