@@ -388,15 +388,17 @@ fd_verify_svc_boot( void * seg_mem, int device, ulong batch_max, ulong inflight 
   s->seg = seg; s->dev = device; s->batch_max = batch_max; s->inflight = inflight;
   { char const * e = getenv( "FD_VERIFY_SVC_GATHER_WGS" ); s->gather_wgs = e ? strtoul( e, 0, 0 ) : SVC_GATHER_WGS; }
   { char const * e = getenv( "FD_VERIFY_SVC_FLUSH_WGS" );  s->flush_wgs  = e ? strtoul( e, 0, 0 ) : SVC_FLUSH_WGS; }
-  { char const * e = getenv( "FD_VERIFY_SVC_MIRROR" );     s->mirror     = e ? atoi( e ) : 1; }
+  { char const * e = getenv( "FD_VERIFY_SVC_MIRROR" );     s->mirror     = e ? atoi( e ) : 0; }
   s->merge_min = batch_max / 2ul; s->merge_wait_ns = 2000000L; s->merge_idle_ns = 20000L;
   SV_CHECK( hipMalloc( &s->d_stage, stage_sz + 4096ul ) );
   SV_CHECK( hipMalloc( &s->d_ing, 64ul * SVC_INGEST_CHUNKS * ing_cnt + 4096ul ) );
   SV_CHECK( hipMalloc( &s->d_ing_sz, 2ul * ing_cnt ) ); SV_CHECK( hipMalloc( &s->d_ing_kind, ing_cnt ) );
   SV_CHECK( hipMalloc( &s->d_ing_tso, 4ul * ing_cnt ) );
   SV_CHECK( hipStreamCreateWithFlags( &s->st_ing, hipStreamNonBlocking ) );
-  SV_CHECK( hipStreamCreateWithFlags( &s->st_dma, hipStreamNonBlocking ) );
-  SV_CHECK( hipEventCreateWithFlags( &s->ev_dma, hipEventDisableTiming ) );
+  if( s->mirror ) {
+    SV_CHECK( hipStreamCreateWithFlags( &s->st_dma, hipStreamNonBlocking ) );
+    SV_CHECK( hipEventCreateWithFlags( &s->ev_dma, hipEventDisableTiming ) );
+  }
   for( ulong k = 0; k < SVC_ING_MAX; k++ ) {
     svc_ingest & I = s->ING[k];
     SV_CHECK( hipHostMalloc( &I.h_desc, sizeof(svc_desc) * SVC_REQ_MAX, hipHostMallocMapped ) );
