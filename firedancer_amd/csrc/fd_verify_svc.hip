@@ -295,9 +295,9 @@ struct fd_verify_svc {
     u8 *       d_mirror;                        /* HBM copy of the data region (chunk c at 64 (c - chunk0)), or 0 */
     ulong      m_lo, m_hi;                      /* seqs [m_lo, m_hi) copied after their publication (m_hi 0: none yet) */
   } link[FD_VERIFY_SVC_LINK_MAX];
-  int        mirror;           /* range links' frags reach HBM by DMA of the link's data region (FD_VERIFY_SVC_MIRROR) */
-  hipStream_t st_dma;          /* the mirror's copies (copy engines) */
-  hipEvent_t  ev_dma;
+  int        mirror;           /* range links' frags reach HBM by DMA of the link's data region (FD_VERIFY_SVC_MIRROR);
+                                  the copies go on the ingest stream ahead of the gather: one more stream in this
+                                  process, even idle, cost every configuration ~30% (profiles/r05ab-ae) */
   ulong      mirror_bytes, mirror_copies, mirror_misses;
   svc_tile tile[FD_VERIFY_SVC_TILE_MAX];
   u8 *     d_stage;            /* staging: tile x slot x slot_cap frags of FD_TXN_HIP_STAGE_CHUNKS */
@@ -395,10 +395,6 @@ fd_verify_svc_boot( void * seg_mem, int device, ulong batch_max, ulong inflight 
   SV_CHECK( hipMalloc( &s->d_ing_sz, 2ul * ing_cnt ) ); SV_CHECK( hipMalloc( &s->d_ing_kind, ing_cnt ) );
   SV_CHECK( hipMalloc( &s->d_ing_tso, 4ul * ing_cnt ) );
   SV_CHECK( hipStreamCreateWithFlags( &s->st_ing, hipStreamNonBlocking ) );
-  if( s->mirror ) {
-    SV_CHECK( hipStreamCreateWithFlags( &s->st_dma, hipStreamNonBlocking ) );
-    SV_CHECK( hipEventCreateWithFlags( &s->ev_dma, hipEventDisableTiming ) );
-  }
   for( ulong k = 0; k < SVC_ING_MAX; k++ ) {
     svc_ingest & I = s->ING[k];
     SV_CHECK( hipHostMalloc( &I.h_desc, sizeof(svc_desc) * SVC_REQ_MAX, hipHostMallocMapped ) );
@@ -508,7 +504,7 @@ fd_verify_svc_run( fd_verify_svc_t * s ) {
    mirror bytes the check passes are the frag's.  Returns 1 if the request
    [seq0, seq_hi) can read the mirror; issues the copies that extend it. */
 static int
-svc_mirror( fd_verify_svc_t * s, ulong link, ulong seq0, ulong seq_hi, int * copied ) {
+svc_mirror( fd_verify_svc_t * s, ulong link, ulong seq0, ulong seq_hi ) {
   auto & L = s->link[link];
   if( !L.d_mirror || seq_hi <= seq0 ) return 0;
   if( !L.m_hi ) L.m_lo = L.m_hi = seq0;                          /* the first request starts the window */
@@ -534,19 +530,18 @@ svc_mirror( fd_verify_svc_t * s, ulong link, ulong seq0, ulong seq_hi, int * cop
   auto copy = [&]( ulong c0, ulong c1 ) {
     if( c1 <= c0 ) return;
     SV_CHECK( hipMemcpyAsync( L.d_mirror + 64ul * (c0 - L.chunk0), L.h_base + 64ul * c0, 64ul * (c1 - c0),
-                              hipMemcpyHostToDevice, s->st_dma ) );
+                              hipMemcpyHostToDevice, s->st_ing ) );
     s->mirror_bytes += 64ul * (c1 - c0); s->mirror_copies++;
   };
   if( cb >= ca ) copy( ca, ce );
   else { copy( ca, rend ); copy( L.chunk0, ce ); }               /* the span wraps */
   L.m_hi = seq_hi;
-  *copied = 1;
   return 1;
 }
 
 /* validate a posted request and write its launch descriptor */
 static void
-svc_desc_of( fd_verify_svc_t * s, ulong t, ulong slot, ulong base, svc_desc & d, int * copied ) {
+svc_desc_of( fd_verify_svc_t * s, ulong t, ulong slot, ulong base, svc_desc & d ) {
   fd_verify_svc_seg_t * g = s->seg;
   fd_verify_svc_req_t const * r = fd_verify_svc_req( g, t, slot );
   memset( &d, 0, sizeof(d) );
@@ -561,7 +556,7 @@ svc_desc_of( fd_verify_svc_t * s, ulong t, ulong slot, ulong base, svc_desc & d,
       abort();
     }
     d.src = (u64)s->link[r->link].d_mcache; d.aux0 = (u64)s->link[r->link].d_base;
-    if( svc_mirror( s, r->link, r->seq0, r->seq0 + r->seq_cnt, copied ) )
+    if( svc_mirror( s, r->link, r->seq0, r->seq0 + r->seq_cnt ) )
       d.aux0 = (u64)(s->link[r->link].d_mirror - 64ul * s->link[r->link].chunk0);
     d.first = fd_verify_svc_range_first( r->seq0, r->rr_cnt, r->rr_idx ); d.stride = r->rr_cnt;
     d.line_mask = s->link[r->link].depth - 1ul; d.chunk0 = s->link[r->link].chunk0; d.wmark = s->link[r->link].wmark;
@@ -748,7 +743,6 @@ fd_verify_svc_poll( fd_verify_svc_t * s ) {
   if( s->ing_take - s->ing_fin < SVC_ING_MAX ) {
     svc_ingest & I = s->ING[s->ing_take % SVC_ING_MAX];
     I.nreq = 0; I.n = 0;
-    int copied = 0;
     for( ulong t = 0; t < g->tile_cnt && I.nreq < SVC_REQ_MAX; t++ ) {
       svc_tile & T = s->tile[t];
       while( I.nreq < SVC_REQ_MAX ) {
@@ -766,15 +760,11 @@ fd_verify_svc_poll( fd_verify_svc_t * s ) {
           continue;
         }
         svc_desc & d = s->sdesc[t * g->req_depth + slot];
-        svc_desc_of( s, t, slot, I.n, d, &copied );
+        svc_desc_of( s, t, slot, I.n, d );
         I.h_desc[I.nreq] = d;
         I.req[I.nreq].t = t; I.req[I.nreq].slot = slot;
         I.nreq++; I.n += q->n;
       }
-    }
-    if( copied ) {                                           /* the gather after the mirror's new copies */
-      SV_CHECK( hipEventRecord( s->ev_dma, s->st_dma ) );
-      SV_CHECK( hipStreamWaitEvent( s->st_ing, s->ev_dma, 0 ) );
     }
     if( I.nreq ) { svc_ingest_start( s, I ); s->ing_take++; }
   }
@@ -831,8 +821,6 @@ fd_verify_svc_delete( fd_verify_svc_t * s ) {
     (void)hipHostFree( I.h_desc ); (void)hipEventDestroy( I.ev0 ); (void)hipEventDestroy( I.ev1 );
   }
   if( s->st_ing ) (void)hipStreamDestroy( s->st_ing );
-  if( s->st_dma ) (void)hipStreamDestroy( s->st_dma );
-  if( s->ev_dma ) (void)hipEventDestroy( s->ev_dma );
   for( ulong k = 0; k < FD_VERIFY_SVC_LINK_MAX; k++ ) if( s->link[k].d_mirror ) (void)hipFree( s->link[k].d_mirror );
   free( s->sdesc );
   for( ulong k = 0; k < s->nreg; k++ ) (void)hipHostUnregister( s->reg[k].h );
