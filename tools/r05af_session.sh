@@ -3,7 +3,7 @@
 # the service tests with it on
 out=gpurun_out/r05af; mkdir -p $out
 export TMPDIR=/tmp
-lscpu | grep "Model name" > $out/host.txt
+lscpu | grep "Model name" > $out/host.txt; echo "GPU_MAX_HW_QUEUES=${GPU_MAX_HW_QUEUES-unset}" >> $out/host.txt
 FD_VERIFY_SVC_MIRROR=1 timeout -k 10 500 python -u -m pytest -x -v --timeout 200 --timeout-method thread tests/test_gpu_svc_run.py > $out/pytest_m1.txt 2>&1 || exit $?
 run() { # name tiles env svc-env
   timeout -k 10 150 python -u tools/svc_bench.py --frags 4194304 --tiles $2 --repeat 2 --prelay \
