@@ -25,6 +25,7 @@
      obj.<id>.{tile_cnt,req_depth,slot_cap,frag_cap}   the segment's shape
      verify_svc.batch_max, verify_svc.inflight         launch size and count
      verify_svc.merge_min, .merge_wait_ns, .merge_idle_ns   the merge policy (fd_verify_svc_set_merge)
+     verify_svc.hw_queues          GPU_MAX_HW_QUEUES for this process
    Defaults: the measured best on one MI355X, the
    same as integration/svc_run.c's. */
 
@@ -32,7 +33,9 @@
 #define SVC_INFLIGHT_DEFAULT      (2UL)
 #define SVC_MERGE_WAIT_NS_DEFAULT (2000000UL)
 #define SVC_MERGE_IDLE_NS_DEFAULT (20000UL)
+#define SVC_HW_QUEUES_DEFAULT     (16UL)
 
+#include <stdio.h>                            /* snprintf */
 #include <stdlib.h>                           /* setenv */
 #include "../topo/fd_topo.h"
 #include "../../util/pod/fd_pod_format.h"
@@ -103,8 +106,14 @@ privileged_init( fd_topo_t * topo, fd_topo_tile_t * tile ) {
   if( FD_UNLIKELY( !gpu_cnt || gpu>=gpu_cnt || obj_id==ULONG_MAX ) ) FD_LOG_ERR(( "no verify_svc object for GPU %lu", gpu ));
   /* before the first HIP call: hardware queues for the ingest, flush and
      launch streams (HIP's default 4 makes the ingest and flush streams wait
-     behind verify launches in shared queues) */
-  setenv( "GPU_MAX_HW_QUEUES", "16", 0 );
+     behind verify launches in shared queues); set
+     over the environment's value, which is HIP's default on hosts that
+     export it (verify_svc.hw_queues, default 16) */
+  {
+    char q[ 24 ];
+    snprintf( q, sizeof(q), "%lu", fd_pod_query_ulong( topo->props, "verify_svc.hw_queues", SVC_HW_QUEUES_DEFAULT ) );
+    setenv( "GPU_MAX_HW_QUEUES", q, 1 );
+  }
   ulong batch_max = fd_pod_query_ulong( topo->props, "verify_svc.batch_max", SVC_BATCH_MAX_DEFAULT );
   ulong inflight  = fd_pod_query_ulong( topo->props, "verify_svc.inflight",  SVC_INFLIGHT_DEFAULT  );
   ctx->svc = fd_verify_svc_boot( fd_topo_obj_laddr( topo, obj_id ), (int)gpu, batch_max, inflight );
