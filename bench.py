@@ -313,8 +313,10 @@ def main():
         # process, so give that process a queue per tile (HIP default 4).
         # Resident C4 is unchanged, the PCIe-inclusive leg +6% (profiles/r03u:
         # 113.8/113.6 vs 113.8/114.5 M resident, 100.6/100.9 vs 106.4/106.5 M).
-        # Set before the runtime initialises (the torch import below).
-        os.environ.setdefault("GPU_MAX_HW_QUEUES", str(max(4, min(args.tiles + 2, 8))))
+        # Set before the runtime initialises (the torch import below), over
+        # the environment's value: the GPU boxes export HIP's default of 4
+        # (profiles/r05af/host.txt), which a setdefault left in place.
+        os.environ["GPU_MAX_HW_QUEUES"] = str(max(4, min(args.tiles + 2, 8)))
 
     import torch
     rank = int(os.environ.get("RANK", "0"))

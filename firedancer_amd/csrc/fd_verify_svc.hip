@@ -288,17 +288,7 @@ struct fd_verify_svc {
                             SVC_FLUSH_WGS (profiles/r05w: 3 tiles 65-68 vs 61-64 M uncapped) */
   struct { u8 * h; ulong sz; u8 * d; } reg[SVC_REGION_MAX];
   ulong    nreg;
-  struct {
-    int        set;
-    u8 const * d_mcache; ulong depth; u8 const * d_base; ulong chunk0, wmark;
-    u8 const * h_mcache; u8 const * h_base;     /* host: the mcache, chunk 0 */
-    u8 *       d_mirror;                        /* HBM copy of the data region (chunk c at 64 (c - chunk0)), or 0 */
-    ulong      m_lo, m_hi;                      /* seqs [m_lo, m_hi) copied after their publication (m_hi 0: none yet) */
-  } link[FD_VERIFY_SVC_LINK_MAX];
-  int        mirror;           /* range links' frags reach HBM by DMA of the link's data region (FD_VERIFY_SVC_MIRROR);
-                                  the copies go on the ingest stream ahead of the gather: one more stream in this
-                                  process, even idle, cost every configuration ~30% (profiles/r05ab-ae) */
-  ulong      mirror_bytes, mirror_copies, mirror_misses;
+  struct { int set; u8 const * d_mcache; ulong depth; u8 const * d_base; ulong chunk0, wmark; } link[FD_VERIFY_SVC_LINK_MAX];
   svc_tile tile[FD_VERIFY_SVC_TILE_MAX];
   u8 *     d_stage;            /* staging: tile x slot x slot_cap frags of FD_TXN_HIP_STAGE_CHUNKS */
   u8 *     d_ing;              /* ingest: tile x slot x slot_cap frags of SVC_INGEST_CHUNKS */
@@ -312,7 +302,7 @@ struct fd_verify_svc {
   ulong    occ[6];             /* every 64th poll with a slot in use: samples, then the summed slot counts posted (not yet
                                   ingested), ingested and waiting for a launch, in a launch, results (the
                                   tile's ordered pass, flushes, publish), free */
-  ulong    stat[16];           /* launches, frags, requests, flushes, flushed frags, (mirror bytes), flush kernels, gpu ns;
+  ulong    stat[16];           /* launches, frags, requests, flushes, flushed frags, flushed bytes, flush kernels, gpu ns;
                                   host ns starting launches, starting flushes, retiring, polls; ingests, ingest
                                   gpu ns, host ns starting ingests, the largest launch */
   long     merge_idle_ns;      /* a launch on an idle GPU once the oldest request has waited this long */
@@ -388,7 +378,6 @@ fd_verify_svc_boot( void * seg_mem, int device, ulong batch_max, ulong inflight 
   s->seg = seg; s->dev = device; s->batch_max = batch_max; s->inflight = inflight;
   { char const * e = getenv( "FD_VERIFY_SVC_GATHER_WGS" ); s->gather_wgs = e ? strtoul( e, 0, 0 ) : SVC_GATHER_WGS; }
   { char const * e = getenv( "FD_VERIFY_SVC_FLUSH_WGS" );  s->flush_wgs  = e ? strtoul( e, 0, 0 ) : SVC_FLUSH_WGS; }
-  { char const * e = getenv( "FD_VERIFY_SVC_MIRROR" );     s->mirror     = e ? atoi( e ) : 0; }
   s->merge_min = batch_max / 2ul; s->merge_wait_ns = 2000000L; s->merge_idle_ns = 20000L;
   SV_CHECK( hipMalloc( &s->d_stage, stage_sz + 4096ul ) );
   SV_CHECK( hipMalloc( &s->d_ing, 64ul * SVC_INGEST_CHUNKS * ing_cnt + 4096ul ) );
@@ -432,13 +421,6 @@ fd_verify_svc_set_link( fd_verify_svc_t * s, ulong link, void const * mcache, ul
   s->link[link].d_base   = svc_dev( s, (u8 const *)chunk_base + 64ul * chunk0, 64ul * (wmark - chunk0) + 2048ul ) -
                            64ul * chunk0;
   s->link[link].chunk0   = chunk0; s->link[link].wmark = wmark;
-  s->link[link].h_mcache = (u8 const *)mcache;
-  s->link[link].h_base   = (u8 const *)chunk_base;
-  s->link[link].m_lo     = s->link[link].m_hi = 0ul;
-  if( s->mirror && !s->link[link].d_mirror ) {
-    SV_CHECK( hipSetDevice( s->dev ) );
-    SV_CHECK( hipMalloc( &s->link[link].d_mirror, 64ul * (wmark - chunk0) + 4096ul ) );
-  }
   s->link[link].set      = 1;
   return 0;
 }
@@ -493,52 +475,6 @@ fd_verify_svc_run( fd_verify_svc_t * s ) {
   return 0;
 }
 
-/* the link mirror: a range request's frags reach HBM by DMA of the span of
-   the link's data region they lie in (one copy per span for every tile on
-   the link, at the copy engines' rate), instead of the gather reading each
-   frag over PCIe.  Seqs [m_lo, m_hi) were copied after their publication.
-   A request whose seqs lie in that window takes its bytes from the mirror:
-   the producer writes a frag's chunk before it publishes the frag and
-   reuses the chunk only after its mcache line is overwritten (the dcache's
-   sizing), and the tile's overrun check at INGESTED sees that line -- so
-   mirror bytes the check passes are the frag's.  Returns 1 if the request
-   [seq0, seq_hi) can read the mirror; issues the copies that extend it. */
-static int
-svc_mirror( fd_verify_svc_t * s, ulong link, ulong seq0, ulong seq_hi ) {
-  auto & L = s->link[link];
-  if( !L.d_mirror || seq_hi <= seq0 ) return 0;
-  if( !L.m_hi ) L.m_lo = L.m_hi = seq0;                          /* the first request starts the window */
-  if( seq0 < L.m_lo ) return 0;
-  if( seq_hi <= L.m_hi ) return 1;
-  if( seq0 > L.m_hi ) L.m_lo = L.m_hi = seq0;                    /* a gap: restart the window here */
-  /* the chunks of seqs m_hi and seq_hi-1: the span between them holds the
-     frags of every seq in [m_hi, seq_hi) (one producer, chunks in order) */
-  ulong const sa = L.m_hi, sb = seq_hi - 1ul;
-  u8 const * la = L.h_mcache + 32ul * (sa & (L.depth - 1ul));
-  u8 const * lb = L.h_mcache + 32ul * (sb & (L.depth - 1ul));
-  ulong const qa = __atomic_load_n( (ulong const *)la, __ATOMIC_ACQUIRE );
-  ulong const qb = __atomic_load_n( (ulong const *)lb, __ATOMIC_ACQUIRE );
-  ulong const ca = *(u32 const volatile *)(la + 16);
-  ulong const cb = *(u32 const volatile *)(lb + 16), zb = *(u16 const volatile *)(lb + 20);
-  __atomic_thread_fence( __ATOMIC_ACQUIRE );
-  bool ok = qa == sa && qb == sb && __atomic_load_n( (ulong const *)la, __ATOMIC_ACQUIRE ) == sa &&
-            __atomic_load_n( (ulong const *)lb, __ATOMIC_ACQUIRE ) == sb &&
-            ca >= L.chunk0 && ca <= L.wmark && cb >= L.chunk0 && cb <= L.wmark && zb <= FD_VERIFY_HIP_TPU_RAW_MTU;
-  if( !ok ) { L.m_lo = L.m_hi = seq_hi; s->mirror_misses++; return 0; }   /* overrun: the gather reads the link */
-  ulong const ce = cb + (zb + 63ul) / 64ul;                      /* end of the last frag, chunks */
-  ulong const rend = L.wmark + (FD_VERIFY_HIP_TPU_RAW_MTU + 63ul) / 64ul;   /* the region's end */
-  auto copy = [&]( ulong c0, ulong c1 ) {
-    if( c1 <= c0 ) return;
-    SV_CHECK( hipMemcpyAsync( L.d_mirror + 64ul * (c0 - L.chunk0), L.h_base + 64ul * c0, 64ul * (c1 - c0),
-                              hipMemcpyHostToDevice, s->st_ing ) );
-    s->mirror_bytes += 64ul * (c1 - c0); s->mirror_copies++;
-  };
-  if( cb >= ca ) copy( ca, ce );
-  else { copy( ca, rend ); copy( L.chunk0, ce ); }               /* the span wraps */
-  L.m_hi = seq_hi;
-  return 1;
-}
-
 /* validate a posted request and write its launch descriptor */
 static void
 svc_desc_of( fd_verify_svc_t * s, ulong t, ulong slot, ulong base, svc_desc & d ) {
@@ -556,8 +492,6 @@ svc_desc_of( fd_verify_svc_t * s, ulong t, ulong slot, ulong base, svc_desc & d 
       abort();
     }
     d.src = (u64)s->link[r->link].d_mcache; d.aux0 = (u64)s->link[r->link].d_base;
-    if( svc_mirror( s, r->link, r->seq0, r->seq0 + r->seq_cnt ) )
-      d.aux0 = (u64)(s->link[r->link].d_mirror - 64ul * s->link[r->link].chunk0);
     d.first = fd_verify_svc_range_first( r->seq0, r->rr_cnt, r->rr_idx ); d.stride = r->rr_cnt;
     d.line_mask = s->link[r->link].depth - 1ul; d.chunk0 = s->link[r->link].chunk0; d.wmark = s->link[r->link].wmark;
   } else if( r->kind == FD_VERIFY_SVC_REQ_FRAGS ) {
@@ -792,7 +726,6 @@ fd_verify_svc_poll( fd_verify_svc_t * s ) {
 extern "C" void
 fd_verify_svc_stats( fd_verify_svc_t const * s, ulong out[16] ) {
   for( int k = 0; k < 16; k++ ) out[k] = s->stat[k];
-  out[5] = s->mirror_bytes;
 }
 
 extern "C" void
@@ -821,7 +754,6 @@ fd_verify_svc_delete( fd_verify_svc_t * s ) {
     (void)hipHostFree( I.h_desc ); (void)hipEventDestroy( I.ev0 ); (void)hipEventDestroy( I.ev1 );
   }
   if( s->st_ing ) (void)hipStreamDestroy( s->st_ing );
-  for( ulong k = 0; k < FD_VERIFY_SVC_LINK_MAX; k++ ) if( s->link[k].d_mirror ) (void)hipFree( s->link[k].d_mirror );
   free( s->sdesc );
   for( ulong k = 0; k < s->nreg; k++ ) (void)hipHostUnregister( s->reg[k].h );
   fd_verify_svc_st( &s->seg->svc_state, FD_VERIFY_SVC_SVC_STOPPED );

@@ -382,10 +382,10 @@ static inline ulong fd_verify_svc_tiles_on( ulong gpu, ulong verify_cnt, ulong g
      (defaults batch_max / 2, 2 ms, 20 us; two launches in flight measure
      best on one MI355X).
    fd_verify_svc_stats( svc, out[ 16 ] ): launches, frags, requests,
-     flushes, flushed frags, bytes the link mirror copied, flush kernels,
-     GPU ns (summed over verify launches), host ns starting launches, host
-     ns starting flushes, host ns polling events, polls, ingests, ingest GPU
-     ns, host ns starting ingests, the largest launch's frags.
+     flushes, flushed frags, 0 (unused), flush kernels, GPU ns (summed over
+     verify launches), host ns starting launches, host ns starting flushes,
+     host ns polling events, polls, ingests, ingest GPU ns, host ns starting
+     ingests, the largest launch's frags.
    fd_verify_svc_delete( svc ): waits for the GPU and frees everything. */
 
 typedef struct fd_verify_svc fd_verify_svc_t;

@@ -339,7 +339,7 @@ produce( char const * path, char const * stream, ulong tile_cnt, ulong in_depth 
   print_lat( "latency_to_consumer", latq ); printf( ", " );
   double occ_n = (double)hdr->svc_occ[0] + 1e-9;
   printf( "\"svc\": {\"launches\": %lu, \"frags\": %lu, \"requests\": %lu, \"flushes\": %lu, \"flushed_frags\": %lu, "
-          "\"mirror_bytes\": %lu, \"spans\": %lu, \"gpu_s\": %.6f, \"host_launch_s\": %.6f, \"host_flush_s\": %.6f, "
+          "\"flushed_bytes\": %lu, \"spans\": %lu, \"gpu_s\": %.6f, \"host_launch_s\": %.6f, \"host_flush_s\": %.6f, "
           "\"host_poll_s\": %.6f, \"polls\": %lu, \"ingests\": %lu, \"ingest_gpu_s\": %.6f, \"host_ingest_s\": %.6f, "
           "\"launch_max\": %lu, \"slots\": {\"posted\": %.3f, \"waiting\": %.3f, \"launched\": %.3f, \"results\": %.3f, "
           "\"free\": %.3f}}, ",
