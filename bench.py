@@ -313,10 +313,12 @@ def main():
         # process, so give that process a queue per tile (HIP default 4).
         # Resident C4 is unchanged, the PCIe-inclusive leg +6% (profiles/r03u:
         # 113.8/113.6 vs 113.8/114.5 M resident, 100.6/100.9 vs 106.4/106.5 M).
-        # Set before the runtime initialises (the torch import below), over
-        # the environment's value: the GPU boxes export HIP's default of 4
-        # (profiles/r05af/host.txt), which a setdefault left in place.
-        os.environ["GPU_MAX_HW_QUEUES"] = str(max(4, min(args.tiles + 2, 8)))
+        # Set before the runtime initialises (the torch import below).  The
+        # GPU boxes export HIP's default of 4 (profiles/r05af/host.txt), and
+        # it is left in place: this process keeps its queues while the tile
+        # leg's GPU tile runs beside it, and 8 here plus 16 there made the
+        # paced tile runs lose most frags (profiles/r05ah; alone, r05ai: none).
+        os.environ.setdefault("GPU_MAX_HW_QUEUES", str(max(4, min(args.tiles + 2, 8))))
 
     import torch
     rank = int(os.environ.get("RANK", "0"))

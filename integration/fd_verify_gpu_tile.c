@@ -33,7 +33,7 @@
 #define SVC_INFLIGHT_DEFAULT      (2UL)
 #define SVC_MERGE_WAIT_NS_DEFAULT (2000000UL)
 #define SVC_MERGE_IDLE_NS_DEFAULT (20000UL)
-#define SVC_HW_QUEUES_DEFAULT     (16UL)
+#define SVC_HW_QUEUES_DEFAULT     (8UL)
 
 #include <stdio.h>                            /* snprintf */
 #include <stdlib.h>                           /* setenv */
@@ -108,7 +108,7 @@ privileged_init( fd_topo_t * topo, fd_topo_tile_t * tile ) {
      launch streams (HIP's default 4 makes the ingest and flush streams wait
      behind verify launches in shared queues); set
      over the environment's value, which is HIP's default on hosts that
-     export it (verify_svc.hw_queues, default 16) */
+     export it (verify_svc.hw_queues, default 8) */
   {
     char q[ 24 ];
     snprintf( q, sizeof(q), "%lu", fd_pod_query_ulong( topo->props, "verify_svc.hw_queues", SVC_HW_QUEUES_DEFAULT ) );

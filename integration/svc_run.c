@@ -14,7 +14,7 @@
    start a launch at once, default batch_max / 2), SVC_MERGE_WAIT_NS
    (default 2000000), SVC_MERGE_IDLE_NS (the wait with no launch in flight,
    default 20000), SVC_HW_QUEUES (GPU_MAX_HW_QUEUES for this process,
-   default 16, set over the environment's).
+   default 8, set over the environment's).
 
    The integration's GPU tile (integration/fd_verify_gpu_tile.c) does the
    same from the topology's objects. */
@@ -53,10 +53,12 @@ main( int argc, char ** argv ) {
 
   /* hardware queues for this process's streams: the ingest and flush
      streams must not wait behind a verify launch in a shared queue
-     (DESIGN.md section 10).  SVC_HW_QUEUES (default 16) replaces the
-     environment's GPU_MAX_HW_QUEUES: the GPU boxes export HIP's default
-     of 4 for every process (profiles/r05af/host.txt) */
-  { char q[ 24 ]; snprintf( q, sizeof(q), "%lu", env_ulong( "SVC_HW_QUEUES", 16UL ) ); setenv( "GPU_MAX_HW_QUEUES", q, 1 ); }
+     (DESIGN.md section 10).  SVC_HW_QUEUES (default 8: the launch, ingest
+     and tile streams of up to 5 tiles, while leaving the device's queue
+     slots to other processes) replaces the environment's
+     GPU_MAX_HW_QUEUES: the GPU boxes export HIP's default of 4 for every
+     process (profiles/r05af/host.txt) */
+  { char q[ 24 ]; snprintf( q, sizeof(q), "%lu", env_ulong( "SVC_HW_QUEUES", 8UL ) ); setenv( "GPU_MAX_HW_QUEUES", q, 1 ); }
   ulong batch_max = env_ulong( "SVC_BATCH_MAX", 262144UL );
   ulong inflight  = env_ulong( "SVC_INFLIGHT", 2UL );
   fd_verify_svc_t * svc = fd_verify_svc_boot( base + hdr->svc_off, (int)strtol( argv[2], NULL, 0 ), batch_max, inflight );
