@@ -114,6 +114,9 @@ privileged_init( fd_topo_t * topo, fd_topo_tile_t * tile ) {
     snprintf( q, sizeof(q), "%lu", fd_pod_query_ulong( topo->props, "verify_svc.hw_queues", SVC_HW_QUEUES_DEFAULT ) );
     setenv( "GPU_MAX_HW_QUEUES", q, 1 );
   }
+  /* the verify contexts' DSM grids leave 128 workgroup slots free for the
+     ingest and flush kernels (profiles/r05an) */
+  setenv( "FD_ED25519_HIP_DSM_RESERVE", "128", 0 );
   ulong batch_max = fd_pod_query_ulong( topo->props, "verify_svc.batch_max", SVC_BATCH_MAX_DEFAULT );
   ulong inflight  = fd_pod_query_ulong( topo->props, "verify_svc.inflight",  SVC_INFLIGHT_DEFAULT  );
   ctx->svc = fd_verify_svc_boot( fd_topo_obj_laddr( topo, obj_id ), (int)gpu, batch_max, inflight );

@@ -59,6 +59,11 @@ main( int argc, char ** argv ) {
      GPU_MAX_HW_QUEUES: the GPU boxes export HIP's default of 4 for every
      process (profiles/r05af/host.txt) */
   { char q[ 24 ]; snprintf( q, sizeof(q), "%lu", env_ulong( "SVC_HW_QUEUES", 8UL ) ); setenv( "GPU_MAX_HW_QUEUES", q, 1 ); }
+  /* the verify contexts' DSM grids leave 128 workgroup slots free, room for
+     the ingest and flush kernels beside a DSM pass (3 tiles 72.1 vs 69.0 M,
+     2 tiles 67.6 vs 66.9 M, 6 runs each on one box, profiles/r05an); the
+     environment's value wins */
+  setenv( "FD_ED25519_HIP_DSM_RESERVE", "128", 0 );
   ulong batch_max = env_ulong( "SVC_BATCH_MAX", 262144UL );
   ulong inflight  = env_ulong( "SVC_INFLIGHT", 2UL );
   fd_verify_svc_t * svc = fd_verify_svc_boot( base + hdr->svc_off, (int)strtol( argv[2], NULL, 0 ), batch_max, inflight );
