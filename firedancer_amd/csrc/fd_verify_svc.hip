@@ -76,7 +76,7 @@ typedef uint32_t u32;
 typedef uint64_t u64;
 
 #define SVC_INGEST_CHUNKS 32ul   /* an ingest frag: 2048 B (a gossip message's bound, the RAW_MTU's 1312 below it) */
-#define SVC_REQ_MAX       64u    /* requests per launch */
+#define SVC_REQ_MAX       512u   /* requests per launch (small requests at shallow link depths: 512 x 1 K frags) */
 #define SVC_LAUNCH_MAX    8ul
 #define SVC_GATHER_WGS    256ul  /* the gather's default grid: 1024 waves, enough to keep PCIe busy (64: 2x slower) */
 #define SVC_FLUSH_WGS     256ul  /* the flush kernel's default grid */
@@ -217,7 +217,8 @@ void k_svc_results( svc_desc const * __restrict__ desc, u32 nreq, ulong n, u16 c
    entry's chunk; one wave per entry, 16-B stores, a frag's bytes contiguous */
 __global__ __launch_bounds__(256)
 void k_svc_compact( fd_verify_svc_out_t const * __restrict__ out, ulong m, u8 const * __restrict__ stage,
-                    ulong stage0, u8 * __restrict__ dcache, long delta, ulong out_sz, u32 * __restrict__ err ) {
+                    ulong stage0, u8 * __restrict__ dcache, long delta, ulong out_sz, ulong slot_cap,
+                    u32 * __restrict__ err ) {
   u32 const lane = threadIdx.x & 63u;
   /* one wave per entry, grid-stride (a capped grid, flush_wgs, loops) */
   for( ulong e = (ulong)blockIdx.x * 4ul + (threadIdx.x >> 6); e < m; e += 4ul * gridDim.x ) {
@@ -225,13 +226,472 @@ void k_svc_compact( fd_verify_svc_out_t const * __restrict__ out, ulong m, u8 co
     if( o.flags & FD_VERIFY_SVC_OUT_HOSTWRITTEN ) continue;
     u32 const len = ((u32)o.sz + 63u) & ~63u;
     long const at = (long)(64ul * (ulong)o.chunk) + delta;
-    /* the tile's chunk must lie inside its out dcache: a bad entry is
-       reported (the service aborts at the flush's retirement), never written */
-    if( at < 0 || at + (long)len > (long)out_sz ) { if( lane == 0u ) *(volatile u32 *)err = 1u; continue; }
+    /* the entry comes from the tile, an untrusted peer: its frag must be one
+       of the slot's staging frags (idx below slot_cap, at most a staging
+       frag's bytes) and its chunk must lie inside its out dcache.  A bad
+       entry is reported (the service aborts at the flush's retirement),
+       never read or written (an idx past the slot read other
+       tiles' staging or past the allocation) */
+    if( (ulong)o.idx >= slot_cap || len > 64u * (u32)FD_TXN_HIP_STAGE_CHUNKS || at < 0 || at + (long)len > (long)out_sz ) {
+      if( lane == 0u ) *(volatile u32 *)err = 1u;
+      continue;
+    }
     u8 const * src = stage + 64ul * (stage0 + FD_TXN_HIP_STAGE_CHUNKS * (ulong)o.idx);
     u8 *       dst = dcache + at;
     for( u32 p = 16u * lane; p < len; p += 1024u ) *(uint4 *)(dst + p) = *(uint4 const *)(src + p);
   }
+}
+
+/**********************************************************************/
+/* The IO engine: one persistent kernel (k_svc_io) that does the ingest
+   and the flushes on the GPU, with no host call between a tile's post and
+   the GPU's copy.
+
+   Why.  A range request holds its quic_verify link until the GPU has read
+   its frags.  With a kernel launched per ingest, the time from a tile's
+   post to INGESTED was the service thread's turn, a launch and the kernel's
+   dispatch beside 2-5 ms verify launches: ~0.5 ms on average at the
+   reference's depth of 16384 (the flow-controlled stage ran 29.7 M frags/s
+   there, one link lap per ~550 us), and a paced producer lapped the tiles
+   above 6-12 M frags/s.  Here a leader wave polls
+   the tiles' request and flush rings in the segment (mapped host memory,
+   system-coherent loads) and splits each new request or flush into jobs of
+   IO_JOB frags on a ring in HBM; the other waves take jobs, copy, and the
+   wave that finishes a request's last job stores INGESTED into the segment
+   itself.  The service thread only merges ingested requests into verify
+   launches.
+
+   Memory ordering (MI355X_MICROARCH.md, inter-workgroup visibility: the
+   XCDs' L2s are not coherent and a CU's L1 is never refreshed by other
+   CUs' stores):
+   - host memory (the segment, the links, the out dcaches) is read with
+     sc0 sc1 (system-coherent) loads and written with sc0 sc1 stores;
+   - HBM shared between waves of this kernel (descriptors, job ring,
+     counters) is written with sc1 stores or agent-scope atomics and read
+     with sc1 loads, a flag or counter written only after the writing wave's
+     s_waitcnt vmcnt(0);
+   - the ingest frags (HBM) are stored sc1 and read by later verify kernel
+     launches; the staging frags a flush reads were written by a verify
+     kernel that ended before the tile saw RESULTS, and are read sc1.
+   Every wave leaves when the host sets stop: the worker's job wait and
+   the leader's loop both poll it, so the grid drains (teardown waits on an
+   event recorded behind the kernel, with a deadline). */
+
+#define IO_RING   16384ul   /* job ring entries (power of 2) */
+#define IO_JOB    32ul      /* ingest frags per job */
+#define IO_FJOB   64ul      /* flush entries per job */
+#define IO_F      4u        /* frags a wave moves per step (their loads in flight together) */
+#define IO_FQ     64ul      /* flushes taken and not retired, per tile */
+#define IO_WGS    32ul      /* default grid: 127 worker waves, 4 workgroups per XCD */
+#define IO_CONS   (1ull << 63)
+
+typedef u32 io_v4 __attribute__((ext_vector_type(4)));
+
+struct svc_io_link { u64 mcache, mask, base, chunk0, wmark, set; };
+struct svc_io_tile { u64 out, out_sz; long delta; u64 rsv; };
+struct svc_io_cfg {
+  u64 seg, tile_cnt, req_depth, slot_cap, frag_cap, tile_sz, slot_sz, req_off, out_off, frag_off;
+  u64 ing, ing_sz, ing_kind, ing_tso, stage;
+  u64 ring, idesc, iremain, fdesc, fremain, fdone, dctl, hctl, hvd;
+  svc_io_link link[FD_VERIFY_SVC_LINK_MAX];
+  svc_io_tile tile[FD_VERIFY_SVC_TILE_MAX];
+};
+
+/* host-mapped control block (coherent pinned memory) */
+struct svc_io_hctl {
+  u64 stop;                   /* host: 1 = every wave leaves */
+  u64 err, err_a, err_b, err_c;   /* GPU: the first error (IO_ERR_*) and its details */
+  u64 beat;                   /* leader loops / 256 */
+  u64 st[8];                  /* the device counters (IO_ST_*), copied by the leader */
+  u64 rsv[18];
+};
+/* device control block (HBM) */
+struct svc_io_dctl {
+  u64 claim; u64 rsv0[15];    /* job ring positions claimed by workers */
+  u64 stop;  u64 rsv1[15];
+  u64 err;   u64 rsv2[15];
+  u64 st[8]; u64 rsv3[8];
+};
+struct svc_io_job { u64 tag; u64 pay; };            /* tag pos+1 when written, IO_CONS|pos once taken */
+struct svc_io_fdesc { u64 out, m, stage0, tile, seq, rsv[3]; };
+
+#define IO_ERR_RANGE  1ul   /* a: tile, b: slot, c: link */
+#define IO_ERR_FRAGS  2ul   /* a: tile, b: slot, c: n */
+#define IO_ERR_KIND   3ul   /* a: tile, b: slot, c: kind */
+#define IO_ERR_ID     4ul   /* a: tile, b: slot, c: id */
+#define IO_ERR_FLUSH  5ul   /* a: tile, b: flush, c: slot */
+#define IO_ERR_ENTRY  6ul   /* a: tile, b: flush, c: entry */
+
+#define IO_ST_REQS    0     /* requests ingested */
+#define IO_ST_FRAGS   1     /* frags ingested */
+#define IO_ST_FLUSHES 2     /* flushes done */
+#define IO_ST_FLFRAGS 3     /* frags flushed */
+#define IO_ST_JOBS    4     /* jobs done */
+#define IO_ST_EXITED  5     /* waves that left */
+
+/* global (not flat) accesses: the sc bits and the counters the visibility
+   rules are stated for (MI355X_MICROARCH.md: never flat_ for these) */
+typedef __attribute__((address_space(1))) u64 io_gu64;
+#define IO_G( p ) ((io_gu64 *)(u64)(p))
+static __device__ __forceinline__ u64 io_lds( u64 const * p ) { return __hip_atomic_load( IO_G( p ), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM ); }
+static __device__ __forceinline__ void io_sts( u64 * p, u64 v ) { __hip_atomic_store( IO_G( p ), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM ); }
+static __device__ __forceinline__ u64 io_lda( u64 const * p ) { return __hip_atomic_load( IO_G( p ), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT ); }
+static __device__ __forceinline__ void io_sta( u64 * p, u64 v ) { __hip_atomic_store( IO_G( p ), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT ); }
+static __device__ __forceinline__ u64 io_adda( u64 * p, u64 v ) { return __hip_atomic_fetch_add( IO_G( p ), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT ); }
+static __device__ __forceinline__ void io_drain( void ) { asm volatile( "s_waitcnt vmcnt(0)" ::: "memory" ); }
+/* a raw buffer over [p, p+n): accesses past n read 0 and write nothing */
+static __device__ __forceinline__ __amdgpu_buffer_rsrc_t io_rsrc( u64 p, u32 n ) {
+  p = ((u64)__builtin_amdgcn_readfirstlane( (u32)(p >> 32) ) << 32) | (u64)__builtin_amdgcn_readfirstlane( (u32)p );
+  return __builtin_amdgcn_make_buffer_rsrc( (void *)p, (short)0, (int)__builtin_amdgcn_readfirstlane( n ), 0x00020000 );
+}
+#define IO_SYS 17   /* sc0 sc1: system coherent (host memory) */
+#define IO_SC1 16   /* sc1: past this CU's L1 (HBM shared with other CUs) */
+static __device__ __forceinline__ u64 io_shfl64( u64 v, u32 l ) {
+  return (u64)(u32)__shfl( (int)(u32)v, (int)l ) | ((u64)(u32)__shfl( (int)(u32)(v >> 32), (int)l ) << 32);
+}
+static __device__ __forceinline__ u64 io_uni( u64 v ) {   /* lane 0's value, in SGPRs */
+  return ((u64)__builtin_amdgcn_readfirstlane( (u32)(v >> 32) ) << 32) | (u64)__builtin_amdgcn_readfirstlane( (u32)v );
+}
+
+/* the first error wins; the host aborts on it (the reference ends a tile
+   with FD_LOG_ERR on a corrupt frag or a bad request) */
+static __device__ void
+io_err( svc_io_cfg const & C, u64 code, u64 a, u64 b, u64 c ) {
+  if( (threadIdx.x & 63u) != __builtin_ctzll( __ballot( 1 ) ) ) return;
+  svc_io_dctl * dc = (svc_io_dctl *)C.dctl;
+  svc_io_hctl * hc = (svc_io_hctl *)C.hctl;
+  u64 zero = 0;
+  if( __hip_atomic_compare_exchange_strong( IO_G( &dc->err ), &zero, code, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                            __HIP_MEMORY_SCOPE_AGENT ) ) {
+    io_sts( &hc->err_a, a ); io_sts( &hc->err_b, b ); io_sts( &hc->err_c, c );
+    io_drain();
+    io_sts( &hc->err, code );
+  }
+}
+
+/* ingest job: frags [start, start+IO_JOB) of request r (its descriptor made
+   by the leader): k_svc_gather's checks and copy, IO_F frags per step with
+   their loads in flight together */
+static __device__ void
+io_ingest( svc_io_cfg const & C, u32 r, u64 start ) {
+  u32 const lane = threadIdx.x & 63u;
+  u64 const dw = lane < 16u ? io_lda( (u64 const *)(C.idesc + 128ul * r) + lane ) : 0ul;
+  u64 const n = io_uni( io_shfl64( dw, 1 ) ), kind = io_uni( io_shfl64( dw, 2 ) ), src = io_uni( io_shfl64( dw, 3 ) );
+  u64 const aux0 = io_uni( io_shfl64( dw, 4 ) ), aux1 = io_uni( io_shfl64( dw, 5 ) );
+  u64 const first = io_uni( io_shfl64( dw, 6 ) ), stride = io_uni( io_shfl64( dw, 7 ) );
+  u64 const lmask = io_uni( io_shfl64( dw, 8 ) ), chunk0 = io_uni( io_shfl64( dw, 9 ) ), wmark = io_uni( io_shfl64( dw, 10 ) );
+  u64 const stage0 = io_uni( io_shfl64( dw, 12 ) ), ibase = io_uni( io_shfl64( dw, 13 ) ), rq = io_uni( io_shfl64( dw, 15 ) );
+  bool const range = kind == FD_VERIFY_SVC_REQ_RANGE;
+  u64 const end = start + IO_JOB < n ? start + IO_JOB : n;
+  for( u64 i = start; i < end; i += IO_F ) {
+    u32 const nf = (u32)(end - i < IO_F ? end - i : IO_F);
+    /* lane f < nf: frag i+f's size, kind, tsorig, source, and whether it
+       passes the stem's and during_frag's checks */
+    u32 msz = 0u, mkind = FD_VERIFY_HIP_IN_QUIC, mtso = 0u; u64 msrc = 0ul; bool mok = false;
+    if( range ) {
+      /* lanes 2f, 2f+1 read frag f's mcache line halves (seq, sig | chunk,
+         sz, ctl, tsorig, tspub) */
+      __amdgpu_buffer_rsrc_t rm = io_rsrc( src, (u32)(32ul * (lmask + 1ul)) );
+      u64 const lseq = first + (i + (lane >> 1)) * stride;
+      io_v4 v = { 0u, 0u, 0u, 0u };
+      if( lane < 2u * nf ) v = __builtin_amdgcn_raw_buffer_load_b128( rm, (u32)(32ul * (lseq & lmask)) + 16u * (lane & 1u), 0, IO_SYS );
+      u32 const s0 = (u32)__shfl( (int)v.x, (int)(2u * lane) ), s1 = (u32)__shfl( (int)v.y, (int)(2u * lane) );
+      u32 const ch = (u32)__shfl( (int)v.x, (int)(2u * lane + 1u) ), szc = (u32)__shfl( (int)v.y, (int)(2u * lane + 1u) );
+      mtso = (u32)__shfl( (int)v.z, (int)(2u * lane + 1u) );
+      u64 const seq = first + (i + lane) * stride;
+      msz  = szc & 0xffffu;
+      mok  = lane < nf && ((u64)s0 | ((u64)s1 << 32)) == seq && (u64)ch >= chunk0 && (u64)ch <= wmark &&
+             msz <= FD_VERIFY_HIP_TPU_RAW_MTU;
+      msrc = aux0 + 64ul * ch;
+    } else {
+      __amdgpu_buffer_rsrc_t rs = io_rsrc( aux0 + 2ul * i, 2u * nf );
+      __amdgpu_buffer_rsrc_t rk = io_rsrc( aux1 + i, nf );
+      msz   = __builtin_amdgcn_raw_buffer_load_b16( rs, 2u * lane, 0, IO_SYS );
+      mkind = __builtin_amdgcn_raw_buffer_load_b8( rk, lane, 0, IO_SYS );
+      mok   = lane < nf && msz <= FD_VERIFY_SVC_FRAG_STRIDE;
+      msrc  = src + FD_VERIFY_SVC_FRAG_STRIDE * (i + lane);
+    }
+    u32 const mnb = mok ? (msz + 15u) & ~15u : 0u;
+    io_v4 a[IO_F], b[IO_F];
+#pragma unroll
+    for( u32 f = 0; f < IO_F; f++ ) {
+      __amdgpu_buffer_rsrc_t rs = io_rsrc( io_shfl64( msrc, f ), (u32)__shfl( (int)mnb, (int)f ) );
+      a[f] = __builtin_amdgcn_raw_buffer_load_b128( rs, 16u * lane, 0, IO_SYS );
+      b[f] = __builtin_amdgcn_raw_buffer_load_b128( rs, 16u * lane + 1024u, 0, IO_SYS );
+    }
+#pragma unroll
+    for( u32 f = 0; f < IO_F; f++ ) {
+      __amdgpu_buffer_rsrc_t rd = io_rsrc( C.ing + 64ul * SVC_INGEST_CHUNKS * (ibase + i + f), (u32)__shfl( (int)mnb, (int)f ) );
+      __builtin_amdgcn_raw_buffer_store_b128( a[f], rd, 16u * lane, 0, IO_SC1 );
+      __builtin_amdgcn_raw_buffer_store_b128( b[f], rd, 16u * lane + 1024u, 0, IO_SC1 );
+      /* a gossip vote's out header: the reference writes four fields into
+         the out chunk's stale header (fd_verify_tile.c:90-93); here the rest is 0 */
+      if( f < nf && (u32)__shfl( (int)mkind, (int)f ) == FD_VERIFY_HIP_IN_GOSSIP ) {
+        __amdgpu_buffer_rsrc_t rg = io_rsrc( C.stage + 64ul * (stage0 + FD_TXN_HIP_STAGE_CHUNKS * (i + f)), 80u );
+        __builtin_amdgcn_raw_buffer_store_b128( io_v4{ 0u, 0u, 0u, 0u }, rg, 16u * lane, 0, IO_SC1 );
+      }
+    }
+    __amdgpu_buffer_rsrc_t rz = io_rsrc( C.ing_sz + 2ul * (ibase + i), 2u * nf );
+    __amdgpu_buffer_rsrc_t rk = io_rsrc( C.ing_kind + (ibase + i), nf );
+    __amdgpu_buffer_rsrc_t rt = io_rsrc( C.ing_tso + 4ul * (ibase + i), 4u * nf );
+    __builtin_amdgcn_raw_buffer_store_b16( (u16)(mok ? msz : 0xffffu), rz, 2u * lane, 0, IO_SC1 );
+    __builtin_amdgcn_raw_buffer_store_b8( (u8)mkind, rk, lane, 0, IO_SC1 );
+    __builtin_amdgcn_raw_buffer_store_b32( range ? mtso : 0u, rt, 4u * lane, 0, IO_SC1 );
+  }
+  io_drain();
+  u64 const cnt = end - start;
+  svc_io_dctl * dc = (svc_io_dctl *)C.dctl;
+  if( lane == 0u ) {
+    u64 const left = io_adda( (u64 *)C.iremain + r, (u64)0 - cnt );
+    io_adda( &dc->st[IO_ST_FRAGS], cnt ); io_adda( &dc->st[IO_ST_JOBS], 1ul );
+    if( left == cnt ) {                                   /* the request's last job: its frags are in HBM */
+      io_adda( &dc->st[IO_ST_REQS], 1ul );
+      io_sts( (u64 *)rq, FD_VERIFY_SVC_INGESTED );
+    }
+  }
+}
+
+/* flush job: out entries [start, start+IO_FJOB) of flush fi, k_svc_compact's
+   checks and copy (staging HBM -> the tile's out dcache in host memory) */
+static __device__ void
+io_flush( svc_io_cfg const & C, u32 fi, u64 start ) {
+  u32 const lane = threadIdx.x & 63u;
+  u64 const fw = lane < 5u ? io_lda( (u64 const *)(C.fdesc + sizeof(svc_io_fdesc) * fi) + lane ) : 0ul;
+  u64 const out = io_uni( io_shfl64( fw, 0 ) ), m = io_uni( io_shfl64( fw, 1 ) ), stage0 = io_uni( io_shfl64( fw, 2 ) );
+  u64 const t = io_uni( io_shfl64( fw, 3 ) ), seq = io_uni( io_shfl64( fw, 4 ) );
+  u64 const dc_out = C.tile[t].out, out_sz = C.tile[t].out_sz;
+  long const delta = C.tile[t].delta;
+  u64 const end = start + IO_FJOB < m ? start + IO_FJOB : m;
+  for( u64 e = start; e < end; e += IO_F ) {
+    u32 const nf = (u32)(end - e < IO_F ? end - e : IO_F);
+    __amdgpu_buffer_rsrc_t ro = io_rsrc( out + 16ul * e, 16u * nf );
+    io_v4 const o = __builtin_amdgcn_raw_buffer_load_b128( ro, 16u * lane, 0, IO_SYS );
+    u32 const idx = o.x, len = ((o.z & 0xffffu) + 63u) & ~63u;
+    bool const hw = ((o.z >> 16) & FD_VERIFY_SVC_OUT_HOSTWRITTEN) != 0u;
+    long const at = (long)(64ul * (u64)o.y) + delta;
+    bool const bad = lane < nf && !hw && ((u64)idx >= C.slot_cap || len > 64u * (u32)FD_TXN_HIP_STAGE_CHUNKS ||
+                                          at < 0 || at + (long)len > (long)out_sz);
+    u64 const bm = __ballot( bad );
+    if( bm ) io_err( C, IO_ERR_ENTRY, t, seq, e + __builtin_ctzll( bm ) );
+    u32 const mnb = lane < nf && !hw && !bad ? len : 0u;
+    u64 const msrc = C.stage + 64ul * (stage0 + FD_TXN_HIP_STAGE_CHUNKS * (u64)idx);
+    u64 const mdst = dc_out + (u64)at;
+    io_v4 a[IO_F], b[IO_F], c[IO_F];
+#pragma unroll
+    for( u32 f = 0; f < IO_F; f++ ) {
+      __amdgpu_buffer_rsrc_t rs = io_rsrc( io_shfl64( msrc, f ), (u32)__shfl( (int)mnb, (int)f ) );
+      a[f] = __builtin_amdgcn_raw_buffer_load_b128( rs, 16u * lane, 0, IO_SC1 );
+      b[f] = __builtin_amdgcn_raw_buffer_load_b128( rs, 16u * lane + 1024u, 0, IO_SC1 );
+      c[f] = __builtin_amdgcn_raw_buffer_load_b128( rs, 16u * lane + 2048u, 0, IO_SC1 );
+    }
+#pragma unroll
+    for( u32 f = 0; f < IO_F; f++ ) {
+      __amdgpu_buffer_rsrc_t rd = io_rsrc( io_shfl64( mdst, f ), (u32)__shfl( (int)mnb, (int)f ) );
+      __builtin_amdgcn_raw_buffer_store_b128( a[f], rd, 16u * lane, 0, IO_SYS );
+      __builtin_amdgcn_raw_buffer_store_b128( b[f], rd, 16u * lane + 1024u, 0, IO_SYS );
+      __builtin_amdgcn_raw_buffer_store_b128( c[f], rd, 16u * lane + 2048u, 0, IO_SYS );
+    }
+  }
+  io_drain();
+  u64 const cnt = end - start;
+  svc_io_dctl * dc = (svc_io_dctl *)C.dctl;
+  if( lane == 0u ) {
+    u64 const left = io_adda( (u64 *)C.fremain + fi, (u64)0 - cnt );
+    io_adda( &dc->st[IO_ST_FLFRAGS], cnt ); io_adda( &dc->st[IO_ST_JOBS], 1ul );
+    if( left == cnt ) io_sta( (u64 *)C.fdone + fi, seq + 1ul );   /* the leader retires flushes in order */
+  }
+}
+
+/* push jobs [0, J) of descriptor idx (bit 31: a flush) at ring positions
+   tail.. (each position's previous occupant must have been taken) */
+static __device__ bool
+io_push( svc_io_cfg const & C, u64 & tail, u32 idx, u64 J, u64 step ) {
+  u32 const lane = threadIdx.x & 63u;
+  svc_io_job * ring = (svc_io_job *)C.ring;
+  svc_io_hctl * hc = (svc_io_hctl *)C.hctl;
+  for( u64 k0 = 0; k0 < J; k0 += 64ul ) {
+    u64 const k = k0 + lane, pos = tail + k;
+    svc_io_job * j = ring + (pos & (IO_RING - 1ul));
+    if( k < J ) {
+      for( ;; ) {
+        u64 const tg = io_lda( &j->tag );
+        if( !tg || tg == (IO_CONS | (pos - IO_RING)) ) break;
+        if( io_lds( &hc->stop ) ) break;
+        __builtin_amdgcn_s_sleep( 4 );
+      }
+      io_sta( &j->pay, ((k * step) << 32) | (u64)idx );
+    }
+    io_drain();
+    if( k < J ) io_sta( &j->tag, pos + 1ul );
+  }
+  tail += J;
+  return true;
+}
+
+static __device__ void
+io_leader( svc_io_cfg const & C ) {
+  u32 const lane = threadIdx.x & 63u;
+  svc_io_dctl * dc = (svc_io_dctl *)C.dctl;
+  svc_io_hctl * hc = (svc_io_hctl *)C.hctl;
+  u64 const T = C.tile_cnt, D = C.req_depth;
+  bool const tl = lane < T;
+  u64 const tb = C.seg + FD_VERIFY_SVC_ALIGN + (u64)lane * C.tile_sz;   /* this lane's tile block */
+  u64 take = 0, ftake = 0, ffin = 0, tail = 0, beat = 0;
+  bool dead = false;
+  for( ;; ) {
+    if( !(++beat & 255ul) ) {                               /* counters for the host, every 256th loop */
+      if( lane < 8u ) io_sts( &hc->st[lane], io_lda( &dc->st[lane] ) );
+      if( lane == 0u ) io_sts( &hc->beat, beat >> 8 );
+    }
+    if( io_lds( &hc->stop ) ) { if( lane == 0u ) io_sta( &dc->stop, 1ul ); break; }
+    bool active = false;
+
+    /* 1. requests: each tile's next slot in ring order */
+    u64 const slot = take & (D - 1ul);
+    u64 const rq   = tb + sizeof(fd_verify_svc_tile_t) + slot * sizeof(fd_verify_svc_req_t);
+    u64 const state = tl && !dead ? io_lds( (u64 const *)rq ) : 0ul;
+    bool const posted = state == FD_VERIFY_SVC_POSTED;
+    u64 const id = posted ? io_lds( (u64 const *)(rq + offsetof( fd_verify_svc_req_t, id )) ) : 0ul;
+    bool const fresh = posted && id == take;
+    bool const wrong = posted && id != take && id + D != take;
+    if( __ballot( wrong ) ) {
+      u64 const w = __ballot( wrong );
+      u32 const t = __builtin_ctzll( w );
+      io_err( C, IO_ERR_ID, t, io_shfl64( slot, t ), io_shfl64( id, t ) );
+      if( wrong ) dead = true;
+    }
+    for( u64 fm = __ballot( fresh ); fm; fm &= fm - 1ul ) {
+      u32 const t  = __builtin_ctzll( fm );
+      u64 const rt = io_uni( io_shfl64( rq, t ) ), st = io_uni( io_shfl64( slot, t ) );
+      u64 const w  = lane < 9u ? io_lds( (u64 const *)rt + lane ) : 0ul;      /* state kind link seq0 seq_cnt rr_cnt rr_idx n seed */
+      u64 const kind = io_uni( io_shfl64( w, 1 ) ), link = io_uni( io_shfl64( w, 2 ) ), seq0 = io_uni( io_shfl64( w, 3 ) );
+      u64 const seq_cnt = io_uni( io_shfl64( w, 4 ) ), rr_cnt = io_uni( io_shfl64( w, 5 ) ), rr_idx = io_uni( io_shfl64( w, 6 ) );
+      u64 const n = io_uni( io_shfl64( w, 7 ) ), seed = io_uni( io_shfl64( w, 8 ) );
+      u64 const r = (u64)t * D + st;
+      u64 d[16] = { 0ul };                                 /* svc_desc */
+      d[1] = n; d[2] = kind; d[11] = seed; d[12] = r * C.slot_cap * FD_TXN_HIP_STAGE_CHUNKS; d[13] = r * C.slot_cap;
+      d[15] = rt;                                          /* the request (its state word) */
+      u64 err = 0ul, ec = 0ul;
+      if( kind == FD_VERIFY_SVC_REQ_RANGE ) {
+        svc_io_link const * L = link < FD_VERIFY_SVC_LINK_MAX ? &C.link[link] : (svc_io_link const *)0;
+        u64 cnt = 0ul, fst = 0ul;
+        if( rr_cnt && rr_idx < rr_cnt && seq_cnt ) {
+          fst = seq0 + (rr_idx + rr_cnt - seq0 % rr_cnt) % rr_cnt;
+          cnt = fst < seq0 + seq_cnt ? (seq0 + seq_cnt - 1ul - fst) / rr_cnt + 1ul : 0ul;
+        }
+        if( !L || !L->set || !rr_cnt || rr_idx >= rr_cnt || seq_cnt > L->mask + 1ul || n != cnt || n > C.slot_cap ) {
+          err = IO_ERR_RANGE; ec = link;
+        } else {
+          d[3] = L->mcache; d[4] = L->base; d[6] = fst; d[7] = rr_cnt; d[8] = L->mask; d[9] = L->chunk0; d[10] = L->wmark;
+        }
+      } else if( kind == FD_VERIFY_SVC_REQ_FRAGS ) {
+        if( n > C.frag_cap ) { err = IO_ERR_FRAGS; ec = n; }
+        u64 const fa = tb - (u64)lane * C.tile_sz + (u64)t * C.tile_sz + C.req_off + st * C.slot_sz + C.frag_off;
+        d[3] = fa; d[4] = fa + C.frag_cap * FD_VERIFY_SVC_FRAG_STRIDE; d[5] = d[4] + 2ul * C.frag_cap;
+      } else {
+        err = IO_ERR_KIND; ec = kind;
+      }
+      if( err ) {
+        io_err( C, err, t, st, ec );
+        if( lane == t ) { dead = true; take++; }
+        continue;
+      }
+      /* the descriptor (HBM, the workers') and the validated size and seed
+         (host, the service thread's verify launch), then the jobs */
+      u64 dv = 0ul;
+#pragma unroll
+      for( u32 k = 0; k < 16u; k++ ) if( lane == k ) dv = d[k];
+      if( lane < 16u ) io_sta( (u64 *)(C.idesc + 128ul * r) + lane, dv );
+      if( lane < 2u ) io_sts( (u64 *)C.hvd + 2ul * r + lane, lane ? seed : n );
+      if( lane == 0u ) io_sta( (u64 *)C.iremain + r, n );
+      io_drain();
+      if( !n ) { if( lane == 0u ) io_sts( (u64 *)rt, FD_VERIFY_SVC_INGESTED ); }
+      else io_push( C, tail, (u32)r, (n + IO_JOB - 1ul) / IO_JOB, IO_JOB );
+      if( lane == t ) take++;
+      active = true;
+    }
+
+    /* 2. flushes: each tile's newly posted flush ring entries */
+    u64 const fpost = tl && !dead ? io_lds( (u64 const *)(tb + offsetof( fd_verify_svc_tile_t, flush_post )) ) : 0ul;
+    bool const fnew = tl && !dead && ftake < fpost && ftake - ffin < IO_FQ;
+    for( u64 fm = __ballot( fnew ); fm; fm &= fm - 1ul ) {
+      u32 const t = __builtin_ctzll( fm );
+      u64 const k = io_uni( io_shfl64( ftake, t ) );
+      u64 const tbt = C.seg + FD_VERIFY_SVC_ALIGN + (u64)t * C.tile_sz;
+      u64 const fe = tbt + offsetof( fd_verify_svc_tile_t, flush ) + (k & (FD_VERIFY_SVC_FLUSH_DEPTH - 1ul)) * sizeof(fd_verify_svc_flush_t);
+      u64 const w = lane < 3u ? io_lds( (u64 const *)fe + lane ) : 0ul;
+      u64 const fslot = io_uni( io_shfl64( w, 0 ) ), lo = io_uni( io_shfl64( w, 1 ) ), hi = io_uni( io_shfl64( w, 2 ) );
+      if( fslot >= D || lo > hi || hi > C.slot_cap ) {
+        io_err( C, IO_ERR_FLUSH, t, k, fslot );
+        if( lane == t ) dead = true;
+        continue;
+      }
+      u64 const fi = (u64)t * IO_FQ + (k & (IO_FQ - 1ul));
+      u64 const r  = (u64)t * D + fslot;
+      u64 fv = 0ul;
+      if( lane == 0u ) fv = tbt + C.req_off + fslot * C.slot_sz + C.out_off + 16ul * lo;
+      if( lane == 1u ) fv = hi - lo;
+      if( lane == 2u ) fv = r * C.slot_cap * FD_TXN_HIP_STAGE_CHUNKS;
+      if( lane == 3u ) fv = t;
+      if( lane == 4u ) fv = k;
+      if( lane < 5u ) io_sta( (u64 *)(C.fdesc + sizeof(svc_io_fdesc) * fi) + lane, fv );
+      if( lane == 0u ) io_sta( (u64 *)C.fremain + fi, hi - lo );
+      io_drain();
+      if( hi == lo ) { if( lane == 0u ) io_sta( (u64 *)C.fdone + fi, k + 1ul ); }
+      else io_push( C, tail, (u32)fi | 0x80000000u, (hi - lo + IO_FJOB - 1ul) / IO_FJOB, IO_FJOB );
+      if( lane == t ) ftake++;
+      active = true;
+    }
+
+    /* 3. finished flushes, in order per tile: flush_done */
+    bool adv = false;
+    for( ;; ) {
+      bool const can = tl && ffin < ftake && io_lda( (u64 const *)C.fdone + (u64)lane * IO_FQ + (ffin & (IO_FQ - 1ul)) ) == ffin + 1ul;
+      if( !__ballot( can ) ) break;
+      if( can ) { ffin++; adv = true; }
+    }
+    if( __ballot( adv ) ) {
+      __builtin_amdgcn_fence( __ATOMIC_RELEASE, "" );
+      if( adv ) io_sts( (u64 *)(tb + offsetof( fd_verify_svc_tile_t, flush_done )), ffin );
+      active = true;
+    }
+    if( !active ) __builtin_amdgcn_s_sleep( 8 );
+  }
+  if( lane == 0u ) io_adda( &dc->st[IO_ST_EXITED], 1ul );
+}
+
+static __device__ void
+io_worker( svc_io_cfg const & C ) {
+  u32 const lane = threadIdx.x & 63u;
+  svc_io_dctl * dc = (svc_io_dctl *)C.dctl;
+  svc_io_job * ring = (svc_io_job *)C.ring;
+  for( ;; ) {
+    u64 p = 0ul;
+    if( lane == 0u ) p = io_adda( &dc->claim, 1ul );
+    p = io_uni( io_shfl64( p, 0 ) );
+    svc_io_job * j = ring + (p & (IO_RING - 1ul));
+    u32 nap = 1u;
+    bool stop = false;
+    for( ;; ) {
+      if( io_lda( &j->tag ) == p + 1ul ) break;
+      if( io_lda( &dc->stop ) ) { stop = true; break; }
+      for( u32 q = 0; q < nap; q++ ) __builtin_amdgcn_s_sleep( 8 );
+      nap = nap < 16u ? 2u * nap : 16u;
+    }
+    if( stop ) break;
+    u64 const pay = io_uni( io_lda( &j->pay ) );
+    if( lane == 0u ) io_sta( &j->tag, IO_CONS | p );
+    u32 const idx = (u32)pay;
+    if( idx & 0x80000000u ) io_flush( C, idx & 0x7fffffffu, pay >> 32 );
+    else                    io_ingest( C, idx, pay >> 32 );
+  }
+  if( lane == 0u ) io_adda( &dc->st[IO_ST_EXITED], 1ul );
+}
+
+__global__ __launch_bounds__(256)
+void k_svc_io( svc_io_cfg C ) {
+  if( blockIdx.x == 0u && threadIdx.x < 64u ) io_leader( C );
+  else                                        io_worker( C );
 }
 
 /**********************************************************************/
@@ -307,6 +767,18 @@ struct fd_verify_svc {
                                   gpu ns, host ns starting ingests, the largest launch */
   long     merge_idle_ns;      /* a launch on an idle GPU once the oldest request has waited this long */
   int      running;
+  /* the IO engine (k_svc_io): FD_VERIFY_SVC_IO=launch selects the per-ingest
+     and per-flush kernel launches instead */
+  int      io;
+  ulong    io_wgs;
+  u8 *     d_io;               /* job ring, descriptors, counters (HBM) */
+  void *   h_ctl;              /* svc_io_hctl (coherent mapped pinned memory) */
+  u8 *     d_ctl;
+  u64 *    h_vd;               /* per request slot: the validated n and seed (coherent mapped pinned) */
+  u8 *     d_vd;
+  hipEvent_t io_ev;            /* recorded behind k_svc_io: the grid has drained */
+  ulong    pend_take[FD_VERIFY_SVC_TILE_MAX];   /* next request id of each tile to merge */
+  long     launch_t0[SVC_LAUNCH_MAX];           /* a verify launch's start (the stuck-launch watchdog) */
 };
 
 static u8 * svc_dev( fd_verify_svc_t * s, void const * h, ulong sz ) {
@@ -359,20 +831,22 @@ static void launch_free( svc_launch & L ) {
 extern "C" fd_verify_svc_t *
 fd_verify_svc_boot( void * seg_mem, int device, ulong batch_max, ulong inflight ) {
   fd_verify_svc_seg_t * seg = fd_verify_svc_join( seg_mem );
-  if( !seg || inflight < 1ul || inflight > SVC_LAUNCH_MAX || batch_max < seg->slot_cap ) return 0;
-  /* staging messages are addressed by 32-bit byte offsets (the verify's
-     msg_off): the whole staging area stays below 4 GiB */
-  ulong stage_sz = seg->tile_cnt * seg->req_depth * seg->slot_cap * FD_TXN_HIP_STAGE_CHUNKS * 64ul;
-  if( stage_sz + 4096ul >= (1ul << 32) ) {
-    fprintf( stderr, "fd_verify_svc: staging %lu B over 4 GiB (tiles x req_depth x slot_cap too large)\n", stage_sz );
+  static_assert( FD_TXN_HIP_STAGE_CHUNKS * 64ul == FD_VERIFY_SVC_STAGE_FRAG_SZ, "staging frag size" );
+  static_assert( SVC_INGEST_CHUNKS == FD_VERIFY_SVC_INGEST_CHUNKS && SVC_LAUNCH_MAX == FD_VERIFY_SVC_INFLIGHT_MAX, "limits" );
+  /* the shape checks (include/fd_verify_svc.h, the same function the
+     topologies' sizing is tested against): staging messages are addressed
+     by 32-bit byte offsets (the verify's msg_off), ingest frags by 32-bit
+     chunk indices (the parse's in_chunk) */
+  if( !seg ) return 0;
+  if( !fd_verify_svc_boot_ok( seg->tile_cnt, seg->req_depth, seg->slot_cap, seg->frag_cap, batch_max, inflight ) ) {
+    fprintf( stderr, "fd_verify_svc: segment shape %lu tiles x %lu slots x %lu frags (frag area %lu), batch_max %lu, "
+             "%lu in flight: outside the service's limits (staging %lu B, 4 GiB at most)\n", seg->tile_cnt, seg->req_depth,
+             seg->slot_cap, seg->frag_cap, batch_max, inflight,
+             seg->tile_cnt * seg->req_depth * seg->slot_cap * FD_VERIFY_SVC_STAGE_FRAG_SZ );
     return 0;
   }
-  /* ingest frags are addressed by 32-bit chunk indices (the parse's in_chunk) */
-  ulong const ing_cnt = seg->tile_cnt * seg->req_depth * seg->slot_cap;
-  if( SVC_INGEST_CHUNKS * ing_cnt >= (1ul << 32) ) {
-    fprintf( stderr, "fd_verify_svc: %lu ingest frags over the 32-bit chunk index\n", ing_cnt );
-    return 0;
-  }
+  ulong const stage_sz = seg->tile_cnt * seg->req_depth * seg->slot_cap * FD_TXN_HIP_STAGE_CHUNKS * 64ul;
+  ulong const ing_cnt  = seg->tile_cnt * seg->req_depth * seg->slot_cap;
   SV_CHECK( hipSetDevice( device ) );
   fd_verify_svc_t * s = (fd_verify_svc_t *)calloc( 1, sizeof(fd_verify_svc_t) );
   s->seg = seg; s->dev = device; s->batch_max = batch_max; s->inflight = inflight;
@@ -394,6 +868,23 @@ fd_verify_svc_boot( void * seg_mem, int device, ulong batch_max, ulong inflight 
   for( ulong k = 0; k < inflight; k++ ) launch_alloc( s->L[k], device, batch_max );
   s->pend_cap = seg->tile_cnt * seg->req_depth;
   s->pend = (svc_pend *)calloc( s->pend_cap, sizeof(svc_pend) );
+  { char const * e = getenv( "FD_VERIFY_SVC_IO" ); s->io = !( e && !strcmp( e, "launch" ) ); }
+  { char const * e = getenv( "FD_VERIFY_SVC_IO_WGS" ); s->io_wgs = e ? strtoul( e, 0, 0 ) : IO_WGS; }
+  if( s->io_wgs < 2ul || s->io_wgs > 1024ul ) s->io_wgs = IO_WGS;
+  if( s->io ) {
+    ulong const nreq = seg->tile_cnt * seg->req_depth, nfl = seg->tile_cnt * IO_FQ;
+    ulong const io_sz = IO_RING * sizeof(svc_io_job) + nreq * (128ul + 8ul) + nfl * (sizeof(svc_io_fdesc) + 16ul) +
+                        sizeof(svc_io_dctl);
+    SV_CHECK( hipMalloc( &s->d_io, io_sz ) );
+    SV_CHECK( hipMemset( s->d_io, 0, io_sz ) );
+    SV_CHECK( hipHostMalloc( &s->h_ctl, 4096, hipHostMallocMapped | hipHostMallocCoherent ) );
+    memset( s->h_ctl, 0, 4096 );
+    SV_CHECK( hipHostGetDevicePointer( (void **)&s->d_ctl, s->h_ctl, 0 ) );
+    SV_CHECK( hipHostMalloc( (void **)&s->h_vd, 16ul * nreq, hipHostMallocMapped | hipHostMallocCoherent ) );
+    memset( s->h_vd, 0, 16ul * nreq );
+    SV_CHECK( hipHostGetDevicePointer( (void **)&s->d_vd, s->h_vd, 0 ) );
+    SV_CHECK( hipEventCreate( &s->io_ev ) );
+  }
   SV_CHECK( hipDeviceSynchronize() );
   return s;
 }
@@ -436,8 +927,13 @@ fd_verify_svc_set_tile( fd_verify_svc_t * s, ulong t, void * out_dcache, ulong o
   (void)svc_dev( s, fd_verify_svc_tile( s->seg, t ), s->seg->tile_sz );   /* the tile's part of the segment */
   SV_CHECK( hipSetDevice( s->dev ) );
   T.h_out = (u8 *)out_dcache; T.out_sz = out_sz; T.chunk_base = (u8 const *)chunk_base;
-  SV_CHECK( hipStreamCreateWithFlags( &T.st, hipStreamNonBlocking ) );
-  for( ulong k = 0; k < SVC_FLUSH_Q; k++ ) SV_CHECK( hipEventCreateWithFlags( &T.ev[k], hipEventDisableTiming ) );
+  /* the IO engine flushes on its own grid: no stream per tile (one stream
+     fewer per tile also keeps the process's streams within its hardware
+     queues, so no stream ever shares a queue with the persistent kernel) */
+  if( !s->io ) {
+    SV_CHECK( hipStreamCreateWithFlags( &T.st, hipStreamNonBlocking ) );
+    for( ulong k = 0; k < SVC_FLUSH_Q; k++ ) SV_CHECK( hipEventCreateWithFlags( &T.ev[k], hipEventDisableTiming ) );
+  }
   T.set = 1;
   return 0;
 }
@@ -464,12 +960,50 @@ fd_verify_svc_run( fd_verify_svc_t * s ) {
   hipLaunchKernelGGL( k_svc_gather, dim3( 1 ), dim3( 256 ), 0, s->st_ing, s->ING[0].d_desc, 0u, 0ul, s->d_ing, s->d_ing_sz,
                       s->d_ing_kind, s->d_ing_tso, s->d_stage );
   SV_CHECK( hipGetLastError() );
-  for( ulong t = 0; t < s->seg->tile_cnt; t++ ) {
+  for( ulong t = 0; t < s->seg->tile_cnt && !s->io; t++ ) {
     hipLaunchKernelGGL( k_svc_compact, dim3( 1 ), dim3( 256 ), 0, s->tile[t].st, (fd_verify_svc_out_t const *)0, 0ul,
-                        (u8 const *)s->d_stage, 0ul, s->tile[t].d_out, 0L, 0ul, s->tile[t].d_err );
+                        (u8 const *)s->d_stage, 0ul, s->tile[t].d_out, 0L, 0ul, s->seg->slot_cap, s->tile[t].d_err );
     SV_CHECK( hipGetLastError() );
   }
   SV_CHECK( hipDeviceSynchronize() );
+  if( s->io ) {
+    /* the IO engine: from here on nothing in this process may wait for the
+       whole device (hipDeviceSynchronize, hipFree) until teardown has
+       stopped it */
+    fd_verify_svc_seg_t * g = s->seg;
+    svc_io_cfg C;
+    memset( &C, 0, sizeof(C) );
+    C.seg = (u64)svc_dev( s, g, fd_verify_svc_footprint( g->tile_cnt, g->req_depth, g->slot_cap, g->frag_cap ) );
+    C.tile_cnt = g->tile_cnt; C.req_depth = g->req_depth; C.slot_cap = g->slot_cap; C.frag_cap = g->frag_cap;
+    C.tile_sz = g->tile_sz; C.slot_sz = g->slot_sz;
+    C.req_off  = fd_verify_svc_align_up( sizeof(fd_verify_svc_tile_t) + g->req_depth * sizeof(fd_verify_svc_req_t), 4096ul );
+    C.out_off  = fd_verify_svc_align_up( g->slot_cap * sizeof(fd_verify_svc_res_t), 4096ul );
+    C.frag_off = C.out_off + fd_verify_svc_align_up( g->slot_cap * sizeof(fd_verify_svc_out_t), 4096ul );
+    C.ing = (u64)s->d_ing; C.ing_sz = (u64)s->d_ing_sz; C.ing_kind = (u64)s->d_ing_kind; C.ing_tso = (u64)s->d_ing_tso;
+    C.stage = (u64)s->d_stage;
+    ulong const nreq = g->tile_cnt * g->req_depth, nfl = g->tile_cnt * IO_FQ;
+    u8 * q = s->d_io;
+    C.ring    = (u64)q; q += IO_RING * sizeof(svc_io_job);
+    C.idesc   = (u64)q; q += nreq * 128ul;
+    C.iremain = (u64)q; q += nreq * 8ul;
+    C.fdesc   = (u64)q; q += nfl * sizeof(svc_io_fdesc);
+    C.fremain = (u64)q; q += nfl * 8ul;
+    C.fdone   = (u64)q; q += nfl * 8ul;
+    C.dctl    = (u64)q;
+    C.hctl = (u64)s->d_ctl; C.hvd = (u64)s->d_vd;
+    for( ulong l = 0; l < FD_VERIFY_SVC_LINK_MAX; l++ ) {
+      if( !s->link[l].set ) continue;
+      C.link[l].mcache = (u64)s->link[l].d_mcache; C.link[l].mask = s->link[l].depth - 1ul; C.link[l].base = (u64)s->link[l].d_base;
+      C.link[l].chunk0 = s->link[l].chunk0; C.link[l].wmark = s->link[l].wmark; C.link[l].set = 1ul;
+    }
+    for( ulong t = 0; t < g->tile_cnt; t++ ) {
+      C.tile[t].out = (u64)s->tile[t].d_out; C.tile[t].out_sz = s->tile[t].out_sz;
+      C.tile[t].delta = (long)(s->tile[t].chunk_base - s->tile[t].h_out);
+    }
+    hipLaunchKernelGGL( k_svc_io, dim3( (unsigned)s->io_wgs ), dim3( 256 ), 0, s->st_ing, C );
+    SV_CHECK( hipGetLastError() );
+    SV_CHECK( hipEventRecord( s->io_ev, s->st_ing ) );
+  }
   s->running = 1;
   fd_verify_svc_st( &s->seg->svc_state, FD_VERIFY_SVC_SVC_RUNNING );
   return 0;
@@ -576,7 +1110,8 @@ svc_flush_start( fd_verify_svc_t * s, ulong t, fd_verify_svc_flush_t const * f )
     if( s->flush_wgs && wgs > s->flush_wgs ) wgs = s->flush_wgs;
     hipLaunchKernelGGL( k_svc_compact, dim3( (unsigned)wgs ), dim3( 256 ), 0, T.st,
                         (fd_verify_svc_out_t const *)svc_dev( s, out, m * sizeof(fd_verify_svc_out_t) ), m,
-                        (u8 const *)s->d_stage, svc_stage0( s, t, f->slot ), T.d_out, delta, T.out_sz, T.d_err );
+                        (u8 const *)s->d_stage, svc_stage0( s, t, f->slot ), T.d_out, delta, T.out_sz, g->slot_cap,
+                        T.d_err );
     SV_CHECK( hipGetLastError() );
     s->stat[6]++;
   }
@@ -606,13 +1141,33 @@ fd_verify_svc_poll( fd_verify_svc_t * s ) {
       s->occ[5] += c[3];
     }
   }
+  if( s->io ) {
+    svc_io_hctl const * hc = (svc_io_hctl const *)s->h_ctl;
+    ulong const err = __atomic_load_n( &hc->err, __ATOMIC_ACQUIRE );
+    if( err ) {
+      static char const * const what[] = { "", "bad range request", "frag request over the frag area", "bad request kind",
+                                           "request id out of ring order", "bad flush (slot / range)",
+                                           "flush entry outside the slot's staging or the out dcache" };
+      fprintf( stderr, "fd_verify_svc: IO engine: %s (tile %lu, %lu, %lu)\n", err < 7ul ? what[err] : "?", hc->err_a,
+               hc->err_b, hc->err_c );
+      abort();
+    }
+  }
   /* 1. finished verify launches: their slots' results are in the segment */
   ulong busy = 0;
   for( ulong k = 0; k < s->inflight; k++ ) {
     svc_launch & L = s->L[k];
     if( !L.busy ) continue;
     hipError_t e = hipEventQuery( L.ev1 );
-    if( e == hipErrorNotReady ) { busy++; continue; }
+    if( e == hipErrorNotReady ) {
+      /* a launch that never ends (a stream sharing a hardware queue behind
+         the IO engine would) ends the service loudly, not silently */
+      if( p0 - s->launch_t0[k] > 20000000000L ) {
+        fprintf( stderr, "fd_verify_svc: verify launch %lu (%lu frags) not done after 20 s\n", k, L.n );
+        abort();
+      }
+      busy++; continue;
+    }
     SV_CHECK( e );
     float ms = 0.f;
     SV_CHECK( hipEventElapsedTime( &ms, L.ev0, L.ev1 ) );
@@ -624,10 +1179,31 @@ fd_verify_svc_poll( fd_verify_svc_t * s ) {
     }
     L.busy = 0; did = 1;
   }
+  long const now0 = svc_now_ns();
+  if( s->io ) {
+    /* the IO engine ingests and flushes on the GPU: the requests it has
+       ingested, in each tile's ring order, wait for a verify launch */
+    for( ulong t = 0; t < g->tile_cnt; t++ ) {
+      for( ;; ) {
+        ulong const slot = s->pend_take[t] & (g->req_depth - 1ul);
+        fd_verify_svc_req_t * q = fd_verify_svc_req( g, t, slot );
+        if( fd_verify_svc_ld( &q->state ) != FD_VERIFY_SVC_INGESTED ) break;
+        ulong const r = t * g->req_depth + slot;
+        ulong const n = __atomic_load_n( &s->h_vd[2ul * r], __ATOMIC_ACQUIRE ), seed = s->h_vd[2ul * r + 1ul];
+        s->pend_take[t]++; did = 1;
+        if( !n ) { q->batch_frags = 0; fd_verify_svc_st( &q->state, FD_VERIFY_SVC_RESULTS ); continue; }
+        svc_desc & d = s->sdesc[r];
+        memset( &d, 0, sizeof(d) );
+        d.n = n; d.seed = seed; d.stage0 = svc_stage0( s, t, slot ); d.ibase = r * g->slot_cap;
+        svc_pend & p = s->pend[s->pend_tail % s->pend_cap];
+        p.t = t; p.slot = slot; p.n = n; p.seen = now0;
+        s->pend_tail++; s->pend_frags += n;
+      }
+    }
+  }
   /* 1b. finished ingests, in order: their requests' frags are in HBM (the
      tiles may reuse the link space) and wait for a verify launch */
-  long const now0 = svc_now_ns();
-  while( s->ing_fin < s->ing_take ) {
+  while( !s->io && s->ing_fin < s->ing_take ) {
     svc_ingest & I = s->ING[s->ing_fin % SVC_ING_MAX];
     hipError_t e = hipEventQuery( I.ev1 );
     if( e == hipErrorNotReady ) break;
@@ -644,7 +1220,7 @@ fd_verify_svc_poll( fd_verify_svc_t * s ) {
     I.busy = 0; s->ing_fin++; did = 1;
   }
   /* 2. flushes: retire in order, start the newly posted */
-  for( ulong t = 0; t < g->tile_cnt; t++ ) {
+  for( ulong t = 0; t < g->tile_cnt && !s->io; t++ ) {
     svc_tile & T = s->tile[t];
     fd_verify_svc_tile_t * b = fd_verify_svc_tile( g, t );
     while( T.flush_fin < T.flush_take ) {
@@ -661,7 +1237,7 @@ fd_verify_svc_poll( fd_verify_svc_t * s ) {
   }
   long const p1 = svc_now_ns();
   s->stat[10] += (ulong)(p1 - p0);
-  for( ulong t = 0; t < g->tile_cnt; t++ ) {
+  for( ulong t = 0; t < g->tile_cnt && !s->io; t++ ) {
     svc_tile & T = s->tile[t];
     fd_verify_svc_tile_t * b = fd_verify_svc_tile( g, t );
     ulong post = fd_verify_svc_ld( &b->flush_post );
@@ -674,7 +1250,7 @@ fd_verify_svc_poll( fd_verify_svc_t * s ) {
   s->stat[9] += (ulong)(p2 - p1);
   /* 3. posted requests, in each tile's ring order, into one ingest batch
      (a request waits while every ingest slot is busy) */
-  if( s->ing_take - s->ing_fin < SVC_ING_MAX ) {
+  if( !s->io && s->ing_take - s->ing_fin < SVC_ING_MAX ) {
     svc_ingest & I = s->ING[s->ing_take % SVC_ING_MAX];
     I.nreq = 0; I.n = 0;
     for( ulong t = 0; t < g->tile_cnt && I.nreq < SVC_REQ_MAX; t++ ) {
@@ -716,6 +1292,7 @@ fd_verify_svc_poll( fd_verify_svc_t * s ) {
     ulong k = 0;
     while( s->L[k].busy ) k++;
     long const l0 = svc_now_ns();
+    s->launch_t0[k] = l0;
     svc_launch_start( s, s->L[k] );
     s->stat[8] += (ulong)(svc_now_ns() - l0);
     busy++; did = 1;
@@ -726,6 +1303,10 @@ fd_verify_svc_poll( fd_verify_svc_t * s ) {
 extern "C" void
 fd_verify_svc_stats( fd_verify_svc_t const * s, ulong out[16] ) {
   for( int k = 0; k < 16; k++ ) out[k] = s->stat[k];
+  if( s->io ) {                               /* the IO engine's counters (copied by its leader every 256 loops) */
+    svc_io_hctl const * hc = (svc_io_hctl const *)s->h_ctl;
+    out[12] = hc->st[IO_ST_REQS]; out[3] = hc->st[IO_ST_FLUSHES]; out[4] = hc->st[IO_ST_FLFRAGS]; out[6] = hc->st[IO_ST_JOBS];
+  }
 }
 
 extern "C" void
@@ -733,18 +1314,75 @@ fd_verify_svc_occupancy( fd_verify_svc_t const * s, ulong out[6] ) {
   for( int k = 0; k < 6; k++ ) out[k] = s->occ[k];
 }
 
+/* Teardown waits for each stream's work with a deadline, stage by stage,
+   so that a stuck shutdown says where it is stuck (a run's
+   service did not finish its shutdown in 60 s and left no trace of where;
+   hipDeviceSynchronize blocks without one).  A stage still running after
+   2 s is named on stderr, after 30 s the process aborts naming it. */
+static void
+svc_drain( hipStream_t st, hipEvent_t ev, char const * what, ulong idx, fd_verify_svc_t const * s ) {
+  int own = 0;
+  if( !ev ) {
+    SV_CHECK( hipEventCreateWithFlags( &ev, hipEventDisableTiming ) );
+    SV_CHECK( hipEventRecord( ev, st ) );
+    own = 1;
+  }
+  long const t0 = svc_now_ns();
+  int warned = 0;
+  for( ;; ) {
+    hipError_t e = hipEventQuery( ev );
+    if( e == hipSuccess ) break;
+    if( e != hipErrorNotReady ) {
+      fprintf( stderr, "fd_verify_svc: teardown: %s %lu: %s\n", what, idx, hipGetErrorString( e ) );
+      abort();
+    }
+    long const dt = svc_now_ns() - t0;
+    if( dt > 2000000000L && !warned ) {
+      warned = 1;
+      fprintf( stderr, "fd_verify_svc: teardown: %s %lu still running after 2 s\n", what, idx );
+      if( s->io ) {
+        svc_io_hctl const * hc = (svc_io_hctl const *)s->h_ctl;
+        fprintf( stderr, "fd_verify_svc: teardown: IO engine: %lu waves of %lu left, leader beat %lu\n",
+                 hc->st[IO_ST_EXITED], 4ul * s->io_wgs, hc->beat );
+      }
+    }
+    if( dt > 30000000000L ) {
+      fprintf( stderr, "fd_verify_svc: teardown: %s %lu not done after 30 s\n", what, idx );
+      abort();
+    }
+    struct timespec ts = { 0, 100000L };
+    nanosleep( &ts, 0 );
+  }
+  if( warned ) fprintf( stderr, "fd_verify_svc: teardown: %s %lu done after %.1f s\n", what, idx, 1e-9 * (double)(svc_now_ns() - t0) );
+  if( own ) (void)hipEventDestroy( ev );
+}
+
 extern "C" void
 fd_verify_svc_delete( fd_verify_svc_t * s ) {
   if( !s ) return;
   (void)hipSetDevice( s->dev );
+  svc_cur_dev = s->dev;
+  if( s->io && s->running ) {
+    __atomic_store_n( &((svc_io_hctl *)s->h_ctl)->stop, 1ul, __ATOMIC_SEQ_CST );
+    svc_drain( s->st_ing, s->io_ev, "the IO engine (k_svc_io)", 0ul, s );
+  }
+  for( ulong k = 0; k < s->inflight; k++ ) if( s->L[k].ctx ) svc_drain( s->L[k].st, 0, "verify launch stream", k, s );
+  for( ulong t = 0; t < FD_VERIFY_SVC_TILE_MAX && !s->io; t++ )
+    if( s->tile[t].set ) svc_drain( s->tile[t].st, 0, "flush stream of tile", t, s );
+  if( s->st_ing && !s->io ) svc_drain( s->st_ing, 0, "ingest stream", 0ul, s );
   (void)hipDeviceSynchronize();
   for( ulong k = 0; k < SVC_LAUNCH_MAX; k++ ) launch_free( s->L[k] );
   for( ulong t = 0; t < FD_VERIFY_SVC_TILE_MAX; t++ ) {
     svc_tile & T = s->tile[t];
     if( !T.set ) continue;
-    (void)hipStreamDestroy( T.st );
+    if( !s->io ) {
+      (void)hipStreamDestroy( T.st );
+      for( ulong k = 0; k < SVC_FLUSH_Q; k++ ) (void)hipEventDestroy( T.ev[k] );
+    }
     (void)hipHostFree( T.h_err );
-    for( ulong k = 0; k < SVC_FLUSH_Q; k++ ) (void)hipEventDestroy( T.ev[k] );
+  }
+  if( s->io ) {
+    (void)hipFree( s->d_io ); (void)hipHostFree( s->h_ctl ); (void)hipHostFree( s->h_vd ); (void)hipEventDestroy( s->io_ev );
   }
   (void)hipFree( s->d_stage );
   (void)hipFree( s->d_ing ); (void)hipFree( s->d_ing_sz ); (void)hipFree( s->d_ing_kind ); (void)hipFree( s->d_ing_tso );

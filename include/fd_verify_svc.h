@@ -339,6 +339,63 @@ fd_verify_svc_post_flush( fd_verify_svc_seg_t * s, ulong t, ulong slot, ulong lo
   return 0;
 }
 
+/* ---- sizing ----------------------------------------------------------------
+
+   The service keeps every slot's out frags in HBM staging, tile_cnt x
+   req_depth x slot_cap frags of FD_VERIFY_SVC_STAGE_FRAG_SZ bytes, and the
+   verify addresses their messages with 32-bit byte offsets: the staging of
+   one GPU stays below 4 GiB (fd_verify_svc_boot refuses a shape that does
+   not fit).  fd_verify_svc_stage_ok checks a shape.
+
+   fd_verify_svc_topo_shape is the shape the topologies give a GPU that
+   serves tile_cnt verify tiles (integration/fd_verify_topo_hip.patch):
+     req_depth  FD_VERIFY_SVC_TOPO_REQ_DEPTH: at the reference's quic_verify
+                depth (16384, default.toml:1153) a range request spans
+                depth / FD_VERIFY_SVC_RANGE_DIV seqs, and a tile holds a slot
+                from its post to the publish of its frags (~2-5 ms): 128 slots
+                keep up with > 50 M seqs/s
+     slot_cap   the largest power of 2 up to FD_VERIFY_SVC_TOPO_SLOT_CAP whose
+                staging fits (2 tiles: 4096; 6 tiles, the reference's default
+                verify_tile_count: 2048; 16 tiles: 512)
+     frag_cap   FD_VERIFY_SVC_TOPO_FRAG_CAP frags of the polled links (gossip
+                votes, send, bundles) per request
+   out[0..3] = tile_cnt, req_depth, slot_cap, frag_cap; returns 0, or -1 if
+   tile_cnt is not in [1, FD_VERIFY_SVC_TILE_MAX]. */
+
+#define FD_VERIFY_SVC_STAGE_FRAG_SZ   (2176UL)    /* FD_TXN_HIP_STAGE_CHUNKS (34) x 64 B: an out frag at its largest */
+#define FD_VERIFY_SVC_TOPO_REQ_DEPTH  (128UL)
+#define FD_VERIFY_SVC_TOPO_SLOT_CAP   (32768UL)
+#define FD_VERIFY_SVC_TOPO_FRAG_CAP   (256UL)
+
+static inline int
+fd_verify_svc_stage_ok( ulong tile_cnt, ulong req_depth, ulong slot_cap ) {
+  if( !tile_cnt || tile_cnt>FD_VERIFY_SVC_TILE_MAX || !req_depth || req_depth>256UL || !slot_cap || slot_cap>(1UL<<20) ) return 0;
+  return tile_cnt*req_depth*slot_cap*FD_VERIFY_SVC_STAGE_FRAG_SZ + 4096UL < (1UL<<32);
+}
+
+/* every shape check fd_verify_svc_boot makes before it allocates: a
+   segment footprint, 1..8 launches in flight of at least a slot each, the
+   staging within 4 GiB, the ingest frags (FD_VERIFY_SVC_INGEST_CHUNKS
+   64-B chunks each) addressed by 32-bit chunk indices */
+#define FD_VERIFY_SVC_INGEST_CHUNKS   (32UL)
+#define FD_VERIFY_SVC_INFLIGHT_MAX    (8UL)
+static inline int
+fd_verify_svc_boot_ok( ulong tile_cnt, ulong req_depth, ulong slot_cap, ulong frag_cap, ulong batch_max, ulong inflight ) {
+  return fd_verify_svc_footprint( tile_cnt, req_depth, slot_cap, frag_cap )!=0UL &&
+         inflight>=1UL && inflight<=FD_VERIFY_SVC_INFLIGHT_MAX && batch_max>=slot_cap &&
+         fd_verify_svc_stage_ok( tile_cnt, req_depth, slot_cap ) &&
+         FD_VERIFY_SVC_INGEST_CHUNKS*tile_cnt*req_depth*slot_cap < (1UL<<32);
+}
+
+static inline int
+fd_verify_svc_topo_shape( ulong tile_cnt, ulong out[ 4 ] ) {
+  if( !tile_cnt || tile_cnt>FD_VERIFY_SVC_TILE_MAX ) return -1;
+  ulong cap = FD_VERIFY_SVC_TOPO_SLOT_CAP;
+  while( cap>FD_VERIFY_SVC_TOPO_FRAG_CAP && !fd_verify_svc_stage_ok( tile_cnt, FD_VERIFY_SVC_TOPO_REQ_DEPTH, cap ) ) cap >>= 1;
+  out[ 0 ] = tile_cnt; out[ 1 ] = FD_VERIFY_SVC_TOPO_REQ_DEPTH; out[ 2 ] = cap; out[ 3 ] = FD_VERIFY_SVC_TOPO_FRAG_CAP;
+  return 0;
+}
+
 /* ---- multi-GPU assignment ---------------------------
 
    Verify tile kind_id is served by the GPU tile on device kind_id %

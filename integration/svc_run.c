@@ -14,7 +14,14 @@
    start a launch at once, default batch_max / 2), SVC_MERGE_WAIT_NS
    (default 2000000), SVC_MERGE_IDLE_NS (the wait with no launch in flight,
    default 20000), SVC_HW_QUEUES (GPU_MAX_HW_QUEUES for this process,
-   default 8, set over the environment's).
+   default 8, set over the environment's), SVC_SANDBOX (kill, the default:
+   after the service is running the process enters
+   fd_hip_tile_sandbox_process -- fd allow-list, rlimits, no capabilities,
+   no new privileges, a seccomp filter over every thread with
+   SECCOMP_RET_KILL_PROCESS; trap: the same filter with SECCOMP_RET_TRAP, a
+   refused call is recorded and fails with ENOSYS; 0: none),
+   SVC_SANDBOX_PROBE=1 (a refused call right after entering: the process
+   must die of SIGSYS).
 
    The integration's GPU tile (integration/fd_verify_gpu_tile.c) does the
    same from the topology's objects. */
@@ -23,8 +30,11 @@
 #include "../../tango/dcache/fd_dcache.h"
 #include "../quic/fd_tpu.h"
 #include "fd_verify_svc.h"
+#include "fd_hip_tile_sandbox.h"
 #include "svc_run.h"
 #include <errno.h>
+#include <signal.h>
+#include <ucontext.h>
 #include <fcntl.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -37,6 +47,22 @@ void fd_halt( void ) {}
 #endif
 
 static ulong env_ulong( char const * k, ulong def ) { char const * v = getenv( k ); return v ? strtoul( v, NULL, 0 ) : def; }
+
+/* SVC_SANDBOX=trap: a refused call is recorded (its number, once) and
+   returns -ENOSYS to the caller, so one run lists every call the filter is
+   missing */
+static svc_run_hdr_t * svc_hdr;
+static void
+svc_sigsys( int sig, siginfo_t * si, void * uc_ ) {
+  (void)sig;
+  ucontext_t * uc = (ucontext_t *)uc_;
+  uc->uc_mcontext.gregs[ REG_RAX ] = -ENOSYS;
+  ulong nr = (ulong)si->si_syscall;
+  ulong k  = __atomic_fetch_add( &svc_hdr->svc_traps, 1UL, __ATOMIC_RELAXED );
+  if( k<16UL ) svc_hdr->svc_trap_nr[ k ] = nr;
+  char m[ 48 ]; int n = snprintf( m, sizeof(m), "svc_run: seccomp trap, syscall %lu\n", nr );
+  if( n>0 ) (void)!write( 2, m, (ulong)n );
+}
 
 int
 main( int argc, char ** argv ) {
@@ -86,6 +112,31 @@ main( int argc, char ** argv ) {
       FD_LOG_ERR(( "fd_verify_svc_set_tile %lu failed", t ));
   }
   if( fd_verify_svc_run( svc ) ) FD_LOG_ERR(( "fd_verify_svc_run failed" ));
+
+  /* the GPU tile's sandbox: everything HIP needs is set up, so from here on
+     the process opens nothing, starts no thread and makes only the calls of
+     fd_hip_tile_seccomp_process (include/fd_hip_tile_sandbox.h) */
+  hdr->svc_pid = (ulong)getpid();
+  char const * sb = getenv( "SVC_SANDBOX" );
+  if( !sb || strcmp( sb, "0" ) ) {
+    int trap = sb && !strcmp( sb, "trap" );
+    svc_hdr = hdr;
+    if( trap ) {
+      struct sigaction sa;
+      memset( &sa, 0, sizeof(sa) );
+      sa.sa_sigaction = svc_sigsys; sa.sa_flags = SA_SIGINFO;
+      if( sigaction( SIGSYS, &sa, NULL ) ) FD_LOG_ERR(( "sigaction(SIGSYS) failed" ));
+    }
+    close( 0 ); close( 1 );                                     /* the driver's stdin and stdout (/dev/null) */
+    int dev[ FD_HIP_TILE_FD_MAX ];
+    long nd = fd_hip_tile_device_fds( dev, FD_HIP_TILE_FD_MAX );
+    if( nd<0L ) FD_LOG_ERR(( "the HIP device fds could not be listed" ));
+    char why[ 160 ];
+    if( fd_hip_tile_sandbox_process( -1, dev, (ulong)nd, 1, trap ? SECCOMP_RET_TRAP : SECCOMP_RET_KILL_PROCESS, why, sizeof(why) ) )
+      FD_LOG_ERR(( "sandbox: %s", why ));
+    hdr->svc_sandboxed = 1UL;
+    if( getenv( "SVC_SANDBOX_PROBE" ) ) (void)syscall( SYS_getppid );   /* refused: the process dies here */
+  }
   FD_COMPILER_MFENCE();
   hdr->svc_ready = 1UL;
   long deadline = fd_log_wallclock() + 1200L*1000000000L;

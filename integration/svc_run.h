@@ -53,6 +53,9 @@ typedef struct {
   volatile long  t0, t_pub;
   volatile ulong svc_stats[ 16 ];
   volatile ulong svc_occ[ 6 ];                 /* fd_verify_svc_occupancy */
+  volatile ulong svc_pid;                      /* the GPU tile's process (its /proc task census, svc_tile_run produce) */
+  volatile ulong svc_sandboxed;                /* the GPU tile entered fd_hip_tile_sandbox_process */
+  volatile ulong svc_traps, svc_trap_nr[ 16 ]; /* SVC_SANDBOX=trap: syscalls the filter refused (their numbers) */
   svc_run_tile_res_t tile[ SVC_RUN_TILE_MAX ];
   svc_run_cons_res_t cons[ SVC_RUN_TILE_MAX ];
 } svc_run_hdr_t;

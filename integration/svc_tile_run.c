@@ -300,6 +300,28 @@ produce( char const * path, char const * stream, ulong tile_cnt, ulong in_depth 
     if( fd_log_wallclock()-t0 > 900L*1000000000L ) FD_LOG_ERR(( "tiles / consumers not done after 900 s" ));
     FD_SPIN_PAUSE();
   }
+  /* the GPU tile's threads while it still runs: each one's seccomp mode
+     (2: filtered) and no_new_privs, from /proc (its sandbox, svc_run.c) */
+  ulong svc_threads = 0UL, svc_filtered = 0UL, svc_nnp = 0UL;
+  if( hdr->svc_pid ) {
+    char dpath[ 64 ];
+    snprintf( dpath, sizeof(dpath), "/proc/%lu/task", hdr->svc_pid );
+    DIR * d = opendir( dpath );
+    for( struct dirent * e; d && (e = readdir( d )); ) {
+      if( e->d_name[0]=='.' ) continue;
+      char spath[ 384 ], line[ 256 ];
+      snprintf( spath, sizeof(spath), "%s/%s/status", dpath, e->d_name );
+      FILE * f = fopen( spath, "r" );
+      if( !f ) continue;
+      svc_threads++;
+      while( fgets( line, sizeof(line), f ) ) {
+        if( !strncmp( line, "Seccomp:", 8 ) && strtoul( line+8, NULL, 10 )==2UL ) svc_filtered++;
+        if( !strncmp( line, "NoNewPrivs:", 11 ) && strtoul( line+11, NULL, 10 )==1UL ) svc_nnp++;
+      }
+      fclose( f );
+    }
+    if( d ) closedir( d );
+  }
   hdr->shutdown = 1UL;
   for( long tw=fd_log_wallclock(); !hdr->svc_done; FD_SPIN_PAUSE() )
     if( fd_log_wallclock()-tw > 60L*1000000000L ) FD_LOG_ERR(( "service not done 60 s after shutdown" ));
@@ -349,6 +371,10 @@ produce( char const * path, char const * stream, ulong tile_cnt, ulong in_depth 
           (double)hdr->svc_stats[13]*1e-9, (double)hdr->svc_stats[14]*1e-9, hdr->svc_stats[15],
           (double)hdr->svc_occ[1]/occ_n, (double)hdr->svc_occ[2]/occ_n, (double)hdr->svc_occ[3]/occ_n,
           (double)hdr->svc_occ[4]/occ_n, (double)hdr->svc_occ[5]/occ_n );
+  printf( "\"svc_sandbox\": {\"sandboxed\": %lu, \"threads\": %lu, \"seccomp_threads\": %lu, \"nnp_threads\": %lu, "
+          "\"traps\": %lu, \"trap_nr\": [", hdr->svc_sandboxed, svc_threads, svc_filtered, svc_nnp, hdr->svc_traps );
+  for( ulong k=0UL; k<fd_ulong_min( hdr->svc_traps, 16UL ); k++ ) printf( "%s%lu", k ? ", " : "", hdr->svc_trap_nr[ k ] );
+  printf( "]}, " );
   printf( "\"frags\": %lu, \"sigs\": %lu, \"published\": %lu, \"parse_fail\": %lu, \"verify_fail\": %lu, "
           "\"dedup\": %lu, \"bundle_peer_fail\": %lu, \"overrun\": %lu, \"lapped\": %lu, \"host_redone\": %lu, "
           "\"consumed\": %lu, \"consumer_bad\": %lu, \"digest_on\": %d, \"metrics_ok\": %lu, \"tile_threads_max\": %lu, \"tile_dev_fds\": %lu, "

@@ -162,3 +162,19 @@ def test_frags_shorter_than_their_payload_are_redone_on_the_tile(stream, tmp_pat
     _check(r, stream["s"].n)
     assert r["host_redone"] == len(range(96, stream["s"].n, 97))
 
+
+
+def test_six_tiles_reference_default_topology(stream, tmp_path):
+    """the reference's default verify_tile_count = 6 (default.toml:776) on one
+    GPU, in the segment shape the topology gives it (fd_verify_svc_topo_shape:
+    128 slots of 2048 frags, frag area 256; tests/test_svc_shape.py): each
+    tile's published sequence equals the reference tile's over its share"""
+    env = {"SVC_RUN_REQ_DEPTH": "128", "SVC_RUN_SLOT_CAP": "2048", "SVC_RUN_FRAG_CAP": "256"}
+    r = S.run(stream["path"], 6, 1 << 14, str(tmp_path / "run"), env=env)
+    _check(r, stream["s"].n)
+    assert r["tile_cnt"] == 6 and r["req_depth"] == 128 and r["slot_cap"] == 2048
+    for t in range(6):
+        p = str(tmp_path / f"share{t}.bin")
+        S.share_stream(p, stream["s"], stream["bid"], t, 6, SEED, DEPTH)
+        run_driver("ref", p, str(tmp_path / f"ref{t}.bin"))
+        assert S.tile_counts(r["tiles"][t]) == S.reference_digest(read_fdo1(str(tmp_path / f"ref{t}.bin"), DEPTH)), t

@@ -100,11 +100,11 @@ def test_topology_patch_applies_and_only_unpolls_quic_verify(tmp_path):
     links unpolled with FD_HAS_HIP or FD_HAS_HIP_SVC; everything else it
     adds sits in FD_HAS_HIP_SVC blocks (the GPU tiles, their verify_svc
     objects and registrations, the GPU tile's sandbox opt-out), and the
-    patched fdctl files compile with FD_HAS_HIP_SVC against the reference's
-    headers."""
+    patched files of both apps compile with FD_HAS_HIP_SVC against the
+    reference's headers."""
     import shutil
     topos = ["src/app/fdctl/topology.c", "src/app/firedancer/topology.c"]
-    others = ["src/app/fdctl/main.c", "src/disco/topo/fd_topo_run.c"]
+    others = ["src/app/fdctl/main.c", "src/app/firedancer/main.c", "src/disco/topo/fd_topo_run.c"]
     for f in topos + others:
         os.makedirs(tmp_path / os.path.dirname(f), exist_ok=True)
         shutil.copy(os.path.join(REF, f), tmp_path / f)
@@ -126,9 +126,16 @@ def test_topology_patch_applies_and_only_unpolls_quic_verify(tmp_path):
                    for x in extra), extra
     for f in others:
         assert _strip_svc(open(tmp_path / f).read().splitlines()) == open(os.path.join(REF, f)).read().splitlines(), f
-    fd = open(tmp_path / "src/app/fdctl/topology.c").read()
-    assert '"vgpu"' in fd and "fd_verify_svc_tiles_on" in fd and "verify_svc.gpu_cnt" in fd
-    for f in ["src/app/fdctl/topology.c", "src/app/fdctl/main.c", "src/disco/topo/fd_topo_run.c"]:
+    # both topologies get the GPU tiles and their verify_svc objects, shaped by fd_verify_svc_topo_shape
+    # (tests/test_svc_shape.py: every verify tile count boots), and both mains register them
+    for f in topos:
+        fd = open(tmp_path / f).read()
+        assert '"vgpu"' in fd and "fd_verify_svc_tiles_on" in fd and "verify_svc.gpu_cnt" in fd, f
+        assert "fd_verify_svc_topo_shape" in fd and "obj.%lu.slot_cap" in fd and "32768UL,  \"obj" not in fd, f
+    for f in ["src/app/fdctl/main.c", "src/app/firedancer/main.c"]:
+        fd = open(tmp_path / f).read()
+        assert "&fd_obj_cb_verify_svc" in fd and "&fd_tile_verify_gpu" in fd, f
+    for f in topos + others:
         subprocess.check_call(["gcc", "-std=c17", "-DFD_HAS_HOSTED=1", "-DFD_HAS_INT128=1", "-DFD_HAS_DOUBLE=1",
                                "-DFD_HAS_ALLOCA=1", "-DFD_HAS_X86=1", "-DFD_HAS_ATOMIC=1", "-DFD_HAS_THREADS=1",
                                "-DFD_HAS_HIP_SVC=1", "-fsyntax-only", "-Wall", "-Werror"] +

@@ -23,6 +23,13 @@
 #                      then the c4pmc and c4stats steps; summarise with tools/pmc_summary.py,
 #                      valu_calib_summary.py, c4_issue_summary.py, txnm_pmc_summary.py
 #   smoke              __graft_entry__.smoke()
+#   svc[:args]         python tools/svc_bench.py <args>         -> svc_<n>.jsonl (the service-mode stage)
+#   sweep[:args]       python tools/svc_link_sweep.py <args>    -> sweep_<n>.jsonl, table in sweep_<n>.err
+#   env:K=V,...        export K=V for the steps after it (e.g. SVC_BENCH_TILE_EXE=integration/_build/svc_tile_run_d2)
+# Round-5 service sessions, as steps (their one-off scripts tools/r05*_session.sh are in git history):
+#   the DSM reserve A/B (r05aq): svc:--frags,4194304,--tiles,2+3,--repeat,2,--prelay,--env,SVC_RUN_REQ_DEPTH=8
+#                                svc:...,--svc-env,FD_ED25519_HIP_DSM_RESERVE=192
+#   the link sweep (r05al):      sweep:--tiles,2,--depths,16384+65536+262144,--env,SVC_RUN_REQ_DEPTH=64+SVC_RUN_SLOT_CAP=8192
 # Round-4 sessions, as steps: replay/tile tests + tile sweep (r04n) =
 #   tests:tests/test_gpu_replay_block.py,tests/test_gpu_replay.py,tests/test_gpu_txn_batch.py,tests/test_gpu_tile_hip.py
 #   replay:--txns,16384+98039,--sched  tile:--frags,2097152,--tiles,1+2+4,--configs,b8192i4+b8192i4h
@@ -109,6 +116,22 @@ for step in "$@"; do
           python3 bench.py --config c4 --tiles 1 --no-cpu-baseline --steps 3 --warmup 1 --c4-pcie-steps 1 \
           > $O/c4stats_$n.json 2> $O/c4stats_$n.err || fail c4stats $? $O/c4stats_$n.err
       echo "profile set ok" ;;
+    svc)
+      timeout -k 10 900 python3 -u tools/svc_bench.py --logdir $O/svc_logs_$n $a > $O/svc_$n.jsonl 2> $O/svc_$n.err \
+          || fail svc $? $O/svc_$n.err
+      python3 -c "
+import json
+for l in open('$O/svc_$n.jsonl'):
+    d = json.loads(l)
+    if 'tiles' in d and isinstance(d['tiles'], list):
+        print('svc', d['tile_cnt'], round(d['verifies_per_s']/1e6, 2), 'M v/s', round(d['frags_per_s']/1e6, 2), 'M f/s lost', d['overrun'] + d['lapped'], 'p99', d['latency']['p99_us'])
+" ;;
+    sweep)
+      timeout -k 10 1100 python3 -u tools/svc_link_sweep.py --logdir $O/sweep_logs_$n $a > $O/sweep_$n.jsonl \
+          2> $O/sweep_$n.err || fail sweep $? $O/sweep_$n.err
+      grep depth_summary $O/sweep_$n.jsonl | cut -c1-400 ;;
+    env)
+      for kv in $a; do export "$kv"; done; echo "env $a" ;;
     smoke)
       timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.txt 2>&1 || fail smoke $? $O/smoke.txt
       tail -2 $O/smoke.txt ;;
