@@ -125,6 +125,7 @@ struct fd_ed25519_hip_ctx {
   u32 *        d_idx;       /* chunk: compacted survivor indices */
   u32 *        d_count;     /* [0] survivor count; [16..47] k_msg_order's histogram and cursors */
   ulong        dsm_wgs;     /* resident k_verify_dsm workgroups (its persistent grid) */
+  ulong        dsm_wgs_all; /* the same with no slots reserved */
   ulong        dsm_share;   /* the grid is dsm_wgs / dsm_share (contexts sharing the GPU) */
   u32 *        d_order;     /* chunk: k_verify_prep's record order (variable-size message paths) */
   int          errmode;
@@ -1209,6 +1210,27 @@ void k_sign( ulong n, uchar const * __restrict__ prvs, uchar const * __restrict_
 
 extern "C" {
 
+/* A reserve of at most half the resident slots: more would starve the
+   DSM it is meant to share the GPU with (a reserve at or above
+   the grid silently left one workgroup).  A clamped value is said once. */
+int
+fd_ed25519_hip_ctx_set_dsm_reserve( fd_ed25519_hip_ctx_t * ctx, ulong reserve ) {
+  if( !ctx ) return -1;
+  ulong const cap = ctx->dsm_wgs_all / 2ul;
+  int clamped = reserve > cap;
+  if( clamped ) {
+    static int warned;
+    if( !warned ) {
+      warned = 1;
+      fprintf( stderr, "fd_ed25519_hip: DSM reserve %lu clamped to %lu (half of %lu resident workgroup slots)\n", reserve,
+               cap, ctx->dsm_wgs_all );
+    }
+    reserve = cap;
+  }
+  ctx->dsm_wgs = ctx->dsm_wgs_all - reserve > 0ul ? ctx->dsm_wgs_all - reserve : 1ul;
+  return clamped;
+}
+
 fd_ed25519_hip_ctx_t *
 fd_ed25519_hip_ctx_new( int device, ulong chunk_sigs ) {
   if( !chunk_sigs ) chunk_sigs = 1UL << 20;
@@ -1265,11 +1287,13 @@ fd_ed25519_hip_ctx_new( int device, ulong chunk_sigs ) {
     /* A/B: every context's DSM grid 1/share of the resident slots (contexts sharing the GPU;
        fd_ed25519_hip_set_dsm_share sets it per context) */
     { char const * ds = getenv( "FD_ED25519_HIP_DSM_SHARE" ); if( ds && atoi( ds ) > 0 ) ctx->dsm_share = (ulong)atoi( ds ); }
-    /* A/B: leave this many resident DSM workgroup slots free (room on some
-       CUs for kernels of other streams while a DSM runs) */
+    /* leave this many resident DSM workgroup slots free (room on some CUs
+       for kernels of other streams while a DSM runs): per context with
+       fd_ed25519_hip_ctx_set_dsm_reserve; FD_ED25519_HIP_DSM_RESERVE sets it
+       for every context of the process (A/Bs) */
+    ctx->dsm_wgs_all = ctx->dsm_wgs;
     { char const * dr = getenv( "FD_ED25519_HIP_DSM_RESERVE" );
-      ulong r = dr ? strtoul( dr, 0, 0 ) : 0ul;
-      ctx->dsm_wgs = r < ctx->dsm_wgs ? ctx->dsm_wgs - r : 1ul; }
+      if( dr ) fd_ed25519_hip_ctx_set_dsm_reserve( ctx, strtoul( dr, 0, 0 ) ); }
     ctx->ncu = (ulong)(ncu_ > 0 ? ncu_ : 1);
     FD_CHECK( hipMalloc( (void **)&ctx->d_lat_done, LAT_MAX_N * sizeof(ulong) ) );
     FD_CHECK( hipMemsetAsync( ctx->d_lat_done, 0, LAT_MAX_N * sizeof(ulong), ctx->stream ) );

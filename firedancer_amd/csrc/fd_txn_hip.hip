@@ -1840,12 +1840,16 @@ fd_verify_hip_tile_set_cu_mask( fd_verify_hip_tile_t * t, uint const * mask, uin
     bool seen = false;                                       /* slots sharing the tile's context: once */
     for( ulong k = 0; k < j; k++ ) seen |= t->slot[k].ctx == c;
     if( !seen && fd_ed25519_hip_ctx_set_cu_mask( c, mask, words ) ) return -1;
-    /* the slot's out-flush stream runs on the same CUs */
+    /* the slot's out-flush stream runs on the same CUs: the new stream is
+       made first and the old one destroyed only then, so a refused mask
+       leaves the slot its working stream */
     tile_slot & s = t->slot[j];
+    hipStream_t ns = 0;
+    if( words ) { if( hipExtStreamCreateWithCUMask( &ns, words, mask ) != hipSuccess ) return -1; }
+    else        TX_CHECK( hipStreamCreateWithFlags( &ns, hipStreamNonBlocking ) );
     TX_CHECK( hipStreamSynchronize( s.st_flush ) );
     TX_CHECK( hipStreamDestroy( s.st_flush ) );
-    if( words ) { if( hipExtStreamCreateWithCUMask( &s.st_flush, words, mask ) != hipSuccess ) return -1; }
-    else        TX_CHECK( hipStreamCreateWithFlags( &s.st_flush, hipStreamNonBlocking ) );
+    s.st_flush = ns;
   }
   return 0;
 }

@@ -83,6 +83,7 @@ typedef uint64_t u64;
 #define SVC_FLUSH_Q       64ul   /* flushes in flight per tile */
 #define SVC_REGION_MAX    64ul
 #define SVC_ING_MAX       8ul    /* ingest batches in flight */
+#define SVC_DSM_RESERVE   128ul  /* DSM workgroup slots left free in the service's verify contexts */
 
 /* the device current on the calling thread (the service runs on one
    thread; hipSetDevice only when it changes) */
@@ -798,6 +799,11 @@ static void launch_alloc( svc_launch & L, int dev, ulong nmax ) {
   L.rcap = fd_txn_hip_record_cap( nmax );
   L.ctx  = fd_ed25519_hip_ctx_new( dev, L.rcap );
   if( !L.ctx ) { fprintf( stderr, "fd_verify_svc: context creation failed\n" ); abort(); }
+  /* the verify contexts' DSM grids leave SVC_DSM_RESERVE workgroup slots
+     free for the IO kernels beside a DSM pass (profiles/r05an: 3 tiles
+     72.1 vs 69.0 M, 2 tiles 67.6 vs 66.9 M); per context, so that no other
+     context of the process inherits it; the environment's value wins */
+  if( !getenv( "FD_ED25519_HIP_DSM_RESERVE" ) ) (void)fd_ed25519_hip_ctx_set_dsm_reserve( L.ctx, SVC_DSM_RESERVE );
   L.st = (hipStream_t)fd_ed25519_hip_ctx_stream( L.ctx );
   SV_CHECK( hipMalloc( &L.d_in_chunk, 4ul * nmax ) ); SV_CHECK( hipMalloc( &L.d_in_sz, 2ul * nmax ) );
   SV_CHECK( hipMalloc( &L.d_in_kind, nmax ) );        SV_CHECK( hipMalloc( &L.d_tso, 4ul * nmax ) );

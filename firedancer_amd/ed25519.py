@@ -37,7 +37,7 @@ EXPORTS = (
     "fd_ed25519_hip_stage_async", "fd_ed25519_hip_test_prim", "fd_ed25519_hip_set_small_batch",
     "fd_ed25519_hip_dropin_init", "fd_ed25519_hip_dropin_stats", "fd_ed25519_hip_host_register",
     "fd_ed25519_hip_host_unregister", "fd_ed25519_hip_device_cnt", "fd_ed25519_hip_set_dsm_share",
-    "fd_ed25519_hip_set_lat_cus", "fd_ed25519_hip_ctx_set_cu_mask",
+    "fd_ed25519_hip_set_lat_cus", "fd_ed25519_hip_ctx_set_cu_mask", "fd_ed25519_hip_ctx_set_dsm_reserve",
 )
 
 _lib = None
@@ -86,6 +86,8 @@ def lib():
         L.fd_ed25519_hip_set_small_batch.argtypes = [vp, u64]
         L.fd_ed25519_hip_set_dsm_share.argtypes = [vp, u64]
         L.fd_ed25519_hip_set_lat_cus.argtypes = [vp, u64]
+        L.fd_ed25519_hip_ctx_set_dsm_reserve.restype = c.c_int
+        L.fd_ed25519_hip_ctx_set_dsm_reserve.argtypes = [vp, u64]
         L.fd_ed25519_hip_ctx_set_cu_mask.restype = c.c_int
         L.fd_ed25519_hip_ctx_set_cu_mask.argtypes = [vp, vp, c.c_uint]
         L.fd_ed25519_hip_test_halfsize.argtypes = [vp, c.c_ulong, vp, vp, vp]

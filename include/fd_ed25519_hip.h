@@ -182,6 +182,14 @@ int                    fd_ed25519_hip_ctx_set_cu_mask( fd_ed25519_hip_ctx_t * ct
    Default 1; same verdicts. */
 void                   fd_ed25519_hip_set_dsm_share( fd_ed25519_hip_ctx_t * ctx, ulong share );
 
+/* Leave `reserve` of the GPU's resident k_verify_dsm workgroup slots free
+   while this context's DSM runs (room for other streams' kernels beside
+   it: the verify service's IO kernels).  At most half
+   the slots are reserved; a larger value is clamped, said once on stderr,
+   and 1 is returned (0 otherwise, -1 for a NULL ctx).  The environment's
+   FD_ED25519_HIP_DSM_RESERVE, if set, is applied to every new context. */
+int                    fd_ed25519_hip_ctx_set_dsm_reserve( fd_ed25519_hip_ctx_t * ctx, ulong reserve );
+
 /* Test hook: the device half-size reduction of n scalars k < L (d_k: 8 LE
    u32 words each) into d_out (18 words each: |k1| (8), k2 (8), k1 < 0 ? ~0 :
    0, max bit length).  Asynchronous on stream. */

@@ -210,8 +210,8 @@ fd_hip_tile_seccomp_process( unsigned long        out_cnt,
    process, fd_sandbox.c:649) and the HIP runtime has started its own; the
    rest applies to the whole process:
      1. the descriptors: every open fd is stderr, the logfile (logfile_fd,
-        -1: none), a HIP device fd (/dev/kfd, /dev/dri/...) or an anonymous
-        inode of the runtime's; any other is an error, as
+        -1: none), a HIP device fd (/dev/kfd, /dev/dri/...), an anonymous
+        inode of the runtime's or the launcher's pipe; any other is an error, as
         fd_sandbox_private_check_exact_file_descriptors makes it
      2. rlimits (fd_sandbox_private_set_rlimits): NOFILE at the highest open
         fd + 1, NPROC 0 (no new process or thread), CORE, NICE, MSGQUEUE,
@@ -259,9 +259,11 @@ fd_hip_tile_sandbox_process( int            logfile_fd,
       long len = (long)readlink( path, target, sizeof(target)-1UL );
       if( len<=0L ) continue;
       target[ len ] = '\0';
-      int ok = d==2 || d==logfile_fd || !strncmp( target, "anon_inode:", 11UL );
+      /* anonymous inodes are the runtime's (events, dma-bufs); a pipe is the
+         launcher's (fd_topo_run's allow_fd, the parent's death watch) */
+      int ok = d==2 || d==logfile_fd || !strncmp( target, "anon_inode:", 11UL ) || !strncmp( target, "pipe:", 5UL );
       for( unsigned long k=0UL; k<dev_cnt; k++ ) ok |= d==dev_fd[ k ];
-      if( !ok && bad<0 ) { bad = d; strncpy( bad_target, target, sizeof(bad_target)-1UL ); }
+      if( !ok && bad<0 ) { bad = d; snprintf( bad_target, sizeof(bad_target), "%s", target ); }
       if( d>hi ) hi = d;
     }
     closedir( dir );

@@ -5,10 +5,14 @@
    the tiles, the verify_svc objects and the registrations).
 
    One "vgpu" tile per GPU (kind_id = the HIP device).  It owns the GPU's
-   HIP context -- the only multithreaded tile, so the only one the sandbox
-   cannot take (fd_sandbox_enter's unshare( CLONE_NEWUSER ) refuses a
+   HIP context -- the only multithreaded tile, so the only one
+   fd_sandbox_enter cannot take (its unshare( CLONE_NEWUSER ) refuses a
    threaded process, src/util/sandbox/fd_sandbox.c:649; the topology patch
-   runs it unsandboxed, as Frankendancer runs Agave) -- and serves the verify
+   skips that call for it) -- and enters everything of the sandbox a
+   threaded process can take in unprivileged_init
+   (fd_hip_tile_sandbox_process, include/fd_hip_tile_sandbox.h): the fd
+   allow-list, rlimits, no capabilities, no_new_privs and a seccomp filter
+   over every thread of the process (SECCOMP_FILTER_FLAG_TSYNC).  It serves the verify
    tiles with kind_id % gpu_cnt == kind_id through its verify_svc object
    (include/fd_verify_svc.h): every quic_verify link's mcache and dcache and
    its tiles' verify_dedup dcaches are registered for the GPU in
@@ -25,7 +29,7 @@
      obj.<id>.{tile_cnt,req_depth,slot_cap,frag_cap}   the segment's shape
      verify_svc.batch_max, verify_svc.inflight         launch size and count
      verify_svc.merge_min, .merge_wait_ns, .merge_idle_ns   the merge policy (fd_verify_svc_set_merge)
-     verify_svc.hw_queues          GPU_MAX_HW_QUEUES for this process
+     verify_svc.hw_queues          GPU_MAX_HW_QUEUES for this process (1..32)
    Defaults: the measured best on one MI355X, the
    same as integration/svc_run.c's. */
 
@@ -42,6 +46,7 @@
 #include "../../tango/mcache/fd_mcache.h"
 #include "../../tango/dcache/fd_dcache.h"
 #include "fd_verify_svc.h"
+#include "fd_hip_tile_sandbox.h"
 
 #define VAL(name) (__extension__({                                                             \
   ulong __x = fd_pod_queryf_ulong( topo->props, ULONG_MAX, "obj.%lu.%s", obj->id, name );      \
@@ -110,13 +115,12 @@ privileged_init( fd_topo_t * topo, fd_topo_tile_t * tile ) {
      over the environment's value, which is HIP's default on hosts that
      export it (verify_svc.hw_queues, default 8) */
   {
+    ulong hwq = fd_pod_query_ulong( topo->props, "verify_svc.hw_queues", SVC_HW_QUEUES_DEFAULT );
+    if( FD_UNLIKELY( hwq<1UL || hwq>32UL ) ) FD_LOG_ERR(( "verify_svc.hw_queues %lu not in [1,32]", hwq ));
     char q[ 24 ];
-    snprintf( q, sizeof(q), "%lu", fd_pod_query_ulong( topo->props, "verify_svc.hw_queues", SVC_HW_QUEUES_DEFAULT ) );
+    snprintf( q, sizeof(q), "%lu", hwq );
     setenv( "GPU_MAX_HW_QUEUES", q, 1 );
   }
-  /* the verify contexts' DSM grids leave 128 workgroup slots free for the
-     ingest and flush kernels (profiles/r05an) */
-  setenv( "FD_ED25519_HIP_DSM_RESERVE", "128", 0 );
   ulong batch_max = fd_pod_query_ulong( topo->props, "verify_svc.batch_max", SVC_BATCH_MAX_DEFAULT );
   ulong inflight  = fd_pod_query_ulong( topo->props, "verify_svc.inflight",  SVC_INFLIGHT_DEFAULT  );
   ctx->svc = fd_verify_svc_boot( fd_topo_obj_laddr( topo, obj_id ), (int)gpu, batch_max, inflight );
@@ -153,6 +157,22 @@ privileged_init( fd_topo_t * topo, fd_topo_tile_t * tile ) {
   if( FD_UNLIKELY( fd_verify_svc_run( ctx->svc ) ) ) FD_LOG_ERR(( "fd_verify_svc_run failed (a verify tile not set?)" ));
 }
 
+/* after fd_topo_run_tile's uid / gid switch: the sandbox of a threaded
+   process (the HIP runtime's threads included), every HIP resource already
+   set up in privileged_init.  A call outside the filter kills the process,
+   as fd_sandbox's SECCOMP_RET_KILL_PROCESS policies do. */
+static void
+unprivileged_init( fd_topo_t * topo, fd_topo_tile_t * tile ) {
+  (void)topo; (void)tile;
+  int  dev[ FD_HIP_TILE_FD_MAX ];
+  long nd = fd_hip_tile_device_fds( dev, FD_HIP_TILE_FD_MAX );
+  if( FD_UNLIKELY( nd<0L ) ) FD_LOG_ERR(( "the HIP device fds could not be listed" ));
+  char why[ 160 ];
+  if( FD_UNLIKELY( fd_hip_tile_sandbox_process( fd_log_private_logfile_fd(), dev, (ulong)nd, 0, SECCOMP_RET_KILL_PROCESS,
+                                                why, sizeof(why) ) ) )
+    FD_LOG_ERR(( "vgpu sandbox: %s", why ));
+}
+
 static inline void
 after_credit( fd_vgpu_ctx_t *     ctx,
               fd_stem_context_t * stem,
@@ -174,5 +194,6 @@ fd_topo_run_tile_t fd_tile_verify_gpu = {
   .scratch_align            = scratch_align,
   .scratch_footprint        = scratch_footprint,
   .privileged_init          = privileged_init,
+  .unprivileged_init        = unprivileged_init,
   .run                      = stem_run,
 };

@@ -33,6 +33,7 @@
 #include "fd_hip_tile_sandbox.h"
 #include "svc_run.h"
 #include <errno.h>
+#include <execinfo.h>
 #include <signal.h>
 #include <ucontext.h>
 #include <fcntl.h>
@@ -60,8 +61,13 @@ svc_sigsys( int sig, siginfo_t * si, void * uc_ ) {
   ulong nr = (ulong)si->si_syscall;
   ulong k  = __atomic_fetch_add( &svc_hdr->svc_traps, 1UL, __ATOMIC_RELAXED );
   if( k<16UL ) svc_hdr->svc_trap_nr[ k ] = nr;
-  char m[ 48 ]; int n = snprintf( m, sizeof(m), "svc_run: seccomp trap, syscall %lu\n", nr );
+  char m[ 64 ]; int n = snprintf( m, sizeof(m), "svc_run: seccomp trap, syscall %lu, thread %ld\n", nr, (long)syscall( SYS_gettid ) );
   if( n>0 ) (void)!write( 2, m, (ulong)n );
+  if( k<4UL ) {                                                 /* where it came from (backtrace() was loaded before the filter) */
+    void * bt[ 32 ];
+    int    bn = backtrace( bt, 32 );
+    backtrace_symbols_fd( bt, bn, 2 );
+  }
 }
 
 int
@@ -84,12 +90,11 @@ main( int argc, char ** argv ) {
      slots to other processes) replaces the environment's
      GPU_MAX_HW_QUEUES: the GPU boxes export HIP's default of 4 for every
      process (profiles/r05af/host.txt) */
-  { char q[ 24 ]; snprintf( q, sizeof(q), "%lu", env_ulong( "SVC_HW_QUEUES", 8UL ) ); setenv( "GPU_MAX_HW_QUEUES", q, 1 ); }
-  /* the verify contexts' DSM grids leave 128 workgroup slots free, room for
-     the ingest and flush kernels beside a DSM pass (3 tiles 72.1 vs 69.0 M,
-     2 tiles 67.6 vs 66.9 M, 6 runs each on one box, profiles/r05an); the
-     environment's value wins */
-  setenv( "FD_ED25519_HIP_DSM_RESERVE", "128", 0 );
+  {
+    ulong hwq = env_ulong( "SVC_HW_QUEUES", 8UL );
+    if( hwq<1UL || hwq>32UL ) FD_LOG_ERR(( "SVC_HW_QUEUES %lu not in [1,32]", hwq ));
+    char q[ 24 ]; snprintf( q, sizeof(q), "%lu", hwq ); setenv( "GPU_MAX_HW_QUEUES", q, 1 );
+  }
   ulong batch_max = env_ulong( "SVC_BATCH_MAX", 262144UL );
   ulong inflight  = env_ulong( "SVC_INFLIGHT", 2UL );
   fd_verify_svc_t * svc = fd_verify_svc_boot( base + hdr->svc_off, (int)strtol( argv[2], NULL, 0 ), batch_max, inflight );
@@ -126,6 +131,7 @@ main( int argc, char ** argv ) {
       memset( &sa, 0, sizeof(sa) );
       sa.sa_sigaction = svc_sigsys; sa.sa_flags = SA_SIGINFO;
       if( sigaction( SIGSYS, &sa, NULL ) ) FD_LOG_ERR(( "sigaction(SIGSYS) failed" ));
+      void * bt[ 4 ]; (void)backtrace( bt, 4 );                  /* loads the unwinder now, not inside the handler */
     }
     close( 0 ); close( 1 );                                     /* the driver's stdin and stdout (/dev/null) */
     int dev[ FD_HIP_TILE_FD_MAX ];

@@ -118,3 +118,27 @@ def test_cu_masked_context_stream():
         assert np.array_equal(codes.cpu().numpy(), exp)
     finally:
         v.close()
+
+
+def test_dsm_reserve_per_context_and_clamped():
+    """fd_ed25519_hip_ctx_set_dsm_reserve: a reserve above half the resident
+    DSM slots is clamped (returns 1) instead of leaving a one-workgroup grid
+    (ADVICE r05), it applies to its context only, and the verdicts of a
+    reserved context are the unreserved one's"""
+    from firedancer_amd import Verifier
+    from firedancer_amd.ed25519 import lib
+    dev = torch.device("cuda", 0)
+    a, b = Verifier(device=0, chunk_sigs=1 << 16), Verifier(device=0, chunk_sigs=1 << 16)
+    try:
+        assert lib().fd_ed25519_hip_ctx_set_dsm_reserve(a.ctx, 1 << 30) == 1
+        assert lib().fd_ed25519_hip_ctx_set_dsm_reserve(a.ctx, 128) == 0
+        n = 1 << 16
+        x = W.make_batch_gpu(b, n, msg_sz=64, seed=0xd5a, mix="c2")
+        ca = torch.zeros(n, dtype=torch.int8, device=dev)
+        cb = torch.zeros(n, dtype=torch.int8, device=dev)
+        a.verify_dev(n, x.sigs, x.pubs, x.pool, x.msg_off, x.msg_sz, ca)
+        b.verify_dev(n, x.sigs, x.pubs, x.pool, x.msg_off, x.msg_sz, cb)
+        torch.cuda.synchronize()
+        assert torch.equal(ca, cb) and 0 < int((cb == 0).sum()) < n
+    finally:
+        a.close(); b.close()
