@@ -304,7 +304,9 @@ struct svc_io_hctl {
   u64 err, err_a, err_b, err_c;   /* GPU: the first error (IO_ERR_*) and its details */
   u64 beat;                   /* leader loops / 256 */
   u64 st[8];                  /* the device counters (IO_ST_*), copied by the leader */
-  u64 rsv[18];
+  u64 dbg[8];                 /* the leader's state, every 256 loops: ring tail, workers' claims, tile 0..3 takes,
+                                 tile 0 flush takes, tile 0 flushes retired */
+  u64 rsv[10];
 };
 /* device control block (HBM) */
 struct svc_io_dctl {
@@ -322,6 +324,8 @@ struct svc_io_fdesc { u64 out, m, stage0, tile, seq, rsv[3]; };
 #define IO_ERR_ID     4ul   /* a: tile, b: slot, c: id */
 #define IO_ERR_FLUSH  5ul   /* a: tile, b: flush, c: slot */
 #define IO_ERR_ENTRY  6ul   /* a: tile, b: flush, c: entry */
+#define IO_ERR_DESC   7ul   /* a: descriptor, b: job start, c: kind or frag count (a job whose descriptor was not
+                               the leader's: never followed to memory) */
 
 #define IO_ST_REQS    0     /* requests ingested */
 #define IO_ST_FRAGS   1     /* frags ingested */
@@ -336,8 +340,12 @@ typedef __attribute__((address_space(1))) u64 io_gu64;
 #define IO_G( p ) ((io_gu64 *)(u64)(p))
 static __device__ __forceinline__ u64 io_lds( u64 const * p ) { return __hip_atomic_load( IO_G( p ), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM ); }
 static __device__ __forceinline__ void io_sts( u64 * p, u64 v ) { __hip_atomic_store( IO_G( p ), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM ); }
-static __device__ __forceinline__ u64 io_lda( u64 const * p ) { return __hip_atomic_load( IO_G( p ), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT ); }
-static __device__ __forceinline__ void io_sta( u64 * p, u64 v ) { __hip_atomic_store( IO_G( p ), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT ); }
+/* the engine's own HBM words (job ring, descriptors, counters) are read and
+   written by atomics, which execute at the memory side and are never
+   served from an XCD's L2 (MI355X_MICROARCH.md): a word written by a wave
+   on one XCD is what a wave on another reads, whatever either L2 held */
+static __device__ __forceinline__ u64 io_lda( u64 const * p ) { return __hip_atomic_fetch_add( IO_G( p ), 0ul, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT ); }
+static __device__ __forceinline__ void io_sta( u64 * p, u64 v ) { (void)__hip_atomic_exchange( IO_G( p ), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT ); }
 static __device__ __forceinline__ u64 io_adda( u64 * p, u64 v ) { return __hip_atomic_fetch_add( IO_G( p ), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT ); }
 static __device__ __forceinline__ void io_drain( void ) { asm volatile( "s_waitcnt vmcnt(0)" ::: "memory" ); }
 /* a raw buffer over [p, p+n): accesses past n read 0 and write nothing */
@@ -383,6 +391,12 @@ io_ingest( svc_io_cfg const & C, u32 r, u64 start ) {
   u64 const lmask = io_uni( io_shfl64( dw, 8 ) ), chunk0 = io_uni( io_shfl64( dw, 9 ) ), wmark = io_uni( io_shfl64( dw, 10 ) );
   u64 const stage0 = io_uni( io_shfl64( dw, 12 ) ), ibase = io_uni( io_shfl64( dw, 13 ) ), rq = io_uni( io_shfl64( dw, 15 ) );
   bool const range = kind == FD_VERIFY_SVC_REQ_RANGE;
+  /* the descriptor is the leader's (written, drained, then the job's tag):
+     one that is not -- a stale line -- is reported, never followed */
+  bool const ok = start < n && ibase == (u64)r * C.slot_cap && rq && src &&
+                  ( range ? ( n <= C.slot_cap && aux0 && lmask && stride ) : ( kind == FD_VERIFY_SVC_REQ_FRAGS &&
+                                                                              n <= C.frag_cap && aux0 && aux1 ) );
+  if( !ok ) { io_err( C, IO_ERR_DESC, r, start, range ? n : kind ); return; }
   u64 const end = start + IO_JOB < n ? start + IO_JOB : n;
   for( u64 i = start; i < end; i += IO_F ) {
     u32 const nf = (u32)(end - i < IO_F ? end - i : IO_F);
@@ -460,9 +474,17 @@ io_flush( svc_io_cfg const & C, u32 fi, u64 start ) {
   u64 const fw = lane < 5u ? io_lda( (u64 const *)(C.fdesc + sizeof(svc_io_fdesc) * fi) + lane ) : 0ul;
   u64 const out = io_uni( io_shfl64( fw, 0 ) ), m = io_uni( io_shfl64( fw, 1 ) ), stage0 = io_uni( io_shfl64( fw, 2 ) );
   u64 const t = io_uni( io_shfl64( fw, 3 ) ), seq = io_uni( io_shfl64( fw, 4 ) );
+  if( t >= C.tile_cnt || !out || start >= m || m > C.slot_cap || fi != t * IO_FQ + (seq & (IO_FQ - 1ul)) ) {
+    io_err( C, IO_ERR_DESC, fi | (1ull << 31), start, m );
+    return;
+  }
   u64 const dc_out = C.tile[t].out, out_sz = C.tile[t].out_sz;
   long const delta = C.tile[t].delta;
   u64 const end = start + IO_FJOB < m ? start + IO_FJOB : m;
+  /* the staging frags were written by a verify launch that ended before the
+     tile saw RESULTS; this CU's L1 (and an XCD's L2 lines of the memory
+     types it does not keep coherent) may hold the slot's previous frags */
+  __builtin_amdgcn_fence( __ATOMIC_ACQUIRE, "agent" );
   for( u64 e = start; e < end; e += IO_F ) {
     u32 const nf = (u32)(end - e < IO_F ? end - e : IO_F);
     __amdgpu_buffer_rsrc_t ro = io_rsrc( out + 16ul * e, 16u * nf );
@@ -542,6 +564,13 @@ io_leader( svc_io_cfg const & C ) {
   for( ;; ) {
     if( !(++beat & 255ul) ) {                               /* counters for the host, every 256th loop */
       if( lane < 8u ) io_sts( &hc->st[lane], io_lda( &dc->st[lane] ) );
+      u64 dv = lane == 0u ? tail : lane == 1u ? io_lda( &dc->claim ) : 0ul;
+      u64 const tk = io_shfl64( take, lane - 2u );
+      if( lane >= 2u && lane < 6u ) dv = tk;
+      u64 const f0 = io_shfl64( ftake, 0 ), r0 = io_shfl64( ffin, 0 );
+      if( lane == 6u ) dv = f0;
+      if( lane == 7u ) dv = r0;
+      if( lane < 8u ) io_sts( &hc->dbg[lane], dv );
       if( lane == 0u ) io_sts( &hc->beat, beat >> 8 );
     }
     if( io_lds( &hc->stop ) ) { if( lane == 0u ) io_sta( &dc->stop, 1ul ); break; }
@@ -883,10 +912,12 @@ fd_verify_svc_boot( void * seg_mem, int device, ulong batch_max, ulong inflight 
                         sizeof(svc_io_dctl);
     SV_CHECK( hipMalloc( &s->d_io, io_sz ) );
     SV_CHECK( hipMemset( s->d_io, 0, io_sz ) );
-    SV_CHECK( hipHostMalloc( &s->h_ctl, 4096, hipHostMallocMapped | hipHostMallocCoherent ) );
+    /* the control block and the validated sizes: uncached (MTYPE_UC) host
+       memory, which the engine's polls always read from memory */
+    SV_CHECK( hipHostMalloc( &s->h_ctl, 4096, hipHostMallocMapped | hipHostMallocUncached ) );
     memset( s->h_ctl, 0, 4096 );
     SV_CHECK( hipHostGetDevicePointer( (void **)&s->d_ctl, s->h_ctl, 0 ) );
-    SV_CHECK( hipHostMalloc( (void **)&s->h_vd, 16ul * nreq, hipHostMallocMapped | hipHostMallocCoherent ) );
+    SV_CHECK( hipHostMalloc( (void **)&s->h_vd, 16ul * nreq, hipHostMallocMapped | hipHostMallocUncached ) );
     memset( s->h_vd, 0, 16ul * nreq );
     SV_CHECK( hipHostGetDevicePointer( (void **)&s->d_vd, s->h_vd, 0 ) );
     SV_CHECK( hipEventCreate( &s->io_ev ) );
@@ -900,7 +931,11 @@ fd_verify_svc_map( fd_verify_svc_t * s, void * host, ulong sz ) {
   if( !s || !host || !sz || s->nreg >= SVC_REGION_MAX ) return -1;
   ulong a = (ulong)host & ~4095ul, e = ((ulong)host + sz + 4095ul) & ~4095ul;
   SV_CHECK( hipSetDevice( s->dev ) );
-  if( hipHostRegister( (void *)a, e - a, hipHostRegisterMapped | hipHostRegisterPortable ) != hipSuccess ) return -1;
+  /* with the IO engine the GPU polls this memory from a running kernel (the
+     request and flush rings) and copies from it: mapped uncached
+     (MTYPE_UC), so no GPU cache level can serve a stale line */
+  unsigned flags = hipHostRegisterMapped | hipHostRegisterPortable | (s->io ? hipExtHostRegisterUncached : 0u);
+  if( hipHostRegister( (void *)a, e - a, flags ) != hipSuccess ) return -1;
   void * d = 0;
   SV_CHECK( hipHostGetDevicePointer( &d, (void *)a, 0 ) );
   s->reg[s->nreg].h = (u8 *)a; s->reg[s->nreg].sz = e - a; s->reg[s->nreg].d = (u8 *)d;
@@ -1153,10 +1188,19 @@ fd_verify_svc_poll( fd_verify_svc_t * s ) {
     if( err ) {
       static char const * const what[] = { "", "bad range request", "frag request over the frag area", "bad request kind",
                                            "request id out of ring order", "bad flush (slot / range)",
-                                           "flush entry outside the slot's staging or the out dcache" };
-      fprintf( stderr, "fd_verify_svc: IO engine: %s (tile %lu, %lu, %lu)\n", err < 7ul ? what[err] : "?", hc->err_a,
+                                           "flush entry outside the slot's staging or the out dcache",
+                                           "a job's descriptor is not the leader's" };
+      fprintf( stderr, "fd_verify_svc: IO engine: %s (%lu, %lu, %lu)\n", err < 8ul ? what[err] : "?", hc->err_a,
                hc->err_b, hc->err_c );
       abort();
+    }
+    /* the engine never ends while the service runs: an end is a fault */
+    if( !(s->stat[11] & 1023ul) ) {
+      hipError_t e = hipEventQuery( s->io_ev );
+      if( e != hipErrorNotReady ) {
+        fprintf( stderr, "fd_verify_svc: IO engine ended while running (%s)\n", hipGetErrorString( e ) );
+        abort();
+      }
     }
   }
   /* 1. finished verify launches: their slots' results are in the segment */
@@ -1313,6 +1357,30 @@ fd_verify_svc_stats( fd_verify_svc_t const * s, ulong out[16] ) {
     svc_io_hctl const * hc = (svc_io_hctl const *)s->h_ctl;
     out[12] = hc->st[IO_ST_REQS]; out[3] = hc->st[IO_ST_FLUSHES]; out[4] = hc->st[IO_ST_FLFRAGS]; out[6] = hc->st[IO_ST_JOBS];
   }
+}
+
+/* one line of the service's state, for a stalled run's log (svc_run.c
+   SVC_DEBUG_S) */
+extern "C" int
+fd_verify_svc_debug( fd_verify_svc_t const * s, char * buf, ulong sz ) {
+  fd_verify_svc_seg_t const * g = s->seg;
+  int n = snprintf( buf, sz, "polls %lu launches %lu frags %lu pend %lu/%lu", s->stat[11], s->stat[0], s->stat[1],
+                    s->pend_tail - s->pend_head, s->pend_frags );
+  for( ulong k = 0; k < s->inflight && n > 0 && (ulong)n < sz; k++ )
+    n += snprintf( buf + n, sz - (ulong)n, " L%lu:%d/%lu", k, s->L[k].busy, s->L[k].n );
+  for( ulong t = 0; t < g->tile_cnt && t < 4ul && n > 0 && (ulong)n < sz; t++ ) {
+    ulong st[4] = { 0, 0, 0, 0 };
+    for( ulong k = 0; k < g->req_depth; k++ ) st[__atomic_load_n( &fd_verify_svc_req( (fd_verify_svc_seg_t *)g, t, k )->state, __ATOMIC_ACQUIRE ) & 3ul]++;
+    n += snprintf( buf + n, sz - (ulong)n, " t%lu[take %lu free %lu posted %lu results %lu ingested %lu]", t, s->pend_take[t], st[0],
+                   st[1], st[2], st[3] );
+  }
+  if( s->io && n > 0 && (ulong)n < sz ) {
+    svc_io_hctl const * hc = (svc_io_hctl const *)s->h_ctl;
+    n += snprintf( buf + n, sz - (ulong)n, " io[beat %lu reqs %lu frags %lu flushes %lu jobs %lu exited %lu tail %lu claim %lu "
+                   "take %lu %lu ftake %lu ffin %lu err %lu]", hc->beat, hc->st[0], hc->st[1], hc->st[2], hc->st[4], hc->st[5],
+                   hc->dbg[0], hc->dbg[1], hc->dbg[2], hc->dbg[3], hc->dbg[6], hc->dbg[7], hc->err );
+  }
+  return n;
 }
 
 extern "C" void

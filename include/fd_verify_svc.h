@@ -463,6 +463,9 @@ void              fd_verify_svc_stats   ( fd_verify_svc_t const * svc, ulong out
    ordered pass, flushes and publish), free.  Divide by out[0] for the mean
    occupancy of each state. */
 void              fd_verify_svc_occupancy( fd_verify_svc_t const * svc, ulong out[ 6 ] );
+/* one line of the service's state (launches, request slots per tile, the
+   IO engine's counters and leader state) into buf; the length written */
+int               fd_verify_svc_debug   ( fd_verify_svc_t const * svc, char * buf, ulong sz );
 void              fd_verify_svc_delete  ( fd_verify_svc_t * svc );
 
 #ifdef __cplusplus

@@ -53,6 +53,12 @@ static ulong env_ulong( char const * k, ulong def ) { char const * v = getenv( k
    returns -ENOSYS to the caller, so one run lists every call the filter is
    missing */
 static svc_run_hdr_t * svc_hdr;
+
+/* SIGTERM (the driver's timeout): leave the poll loop and tear the service
+   down -- the IO engine stopped and drained -- rather than die with a
+   kernel running on the GPU */
+static volatile int svc_term;
+static void svc_sigterm( int sig ) { (void)sig; svc_term = 1; }
 static void
 svc_sigsys( int sig, siginfo_t * si, void * uc_ ) {
   (void)sig;
@@ -145,10 +151,31 @@ main( int argc, char ** argv ) {
   }
   FD_COMPILER_MFENCE();
   hdr->svc_ready = 1UL;
+  {
+    struct sigaction sa;
+    memset( &sa, 0, sizeof(sa) );
+    sa.sa_handler = svc_sigterm;
+    if( sigaction( SIGTERM, &sa, NULL ) ) FD_LOG_ERR(( "sigaction(SIGTERM) failed" ));
+  }
   long deadline = fd_log_wallclock() + 1200L*1000000000L;
-  for( ulong it=0UL; !hdr->shutdown; it++ ) {
+  /* SVC_DEBUG_S=s: the service's state on stderr every s seconds (a stalled
+     run's log names where it stalled) */
+  long dbg_ns = (long)env_ulong( "SVC_DEBUG_S", 0UL )*1000000000L, dbg_next = fd_log_wallclock() + dbg_ns;
+  for( ulong it=0UL; !hdr->shutdown && !svc_term; it++ ) {
     if( !fd_verify_svc_poll( svc ) ) FD_SPIN_PAUSE();
-    if( !( it & 0xffffUL ) && fd_log_wallclock()>deadline ) FD_LOG_ERR(( "service: no shutdown after 1200 s" ));
+    if( !( it & 0xffffUL ) ) {
+      long now = fd_log_wallclock();
+      if( now>deadline ) { fprintf( stderr, "svc_run: no shutdown after 1200 s\n" ); break; }
+      if( dbg_ns && now>dbg_next ) {
+        char b[ 1024 ]; int n = fd_verify_svc_debug( svc, b, sizeof(b) );
+        if( n>0 ) { b[ sizeof(b)-2 ] = '\0'; fprintf( stderr, "svc_run: %s\n", b ); }
+        dbg_next = now + dbg_ns;
+      }
+    }
+  }
+  if( svc_term || !hdr->shutdown ) {
+    char b[ 1024 ]; int n = fd_verify_svc_debug( svc, b, sizeof(b) );
+    if( n>0 ) { b[ sizeof(b)-2 ] = '\0'; fprintf( stderr, "svc_run: stopped before shutdown: %s\n", b ); }
   }
   ulong st[ 16 ];
   fd_verify_svc_stats( svc, st );

@@ -162,6 +162,15 @@ def run_one(stream, tiles, in_depth, timeout, logdir, env=None, svc_env=None, sv
         res["pinned"] = {k: sorted(v) for k, v in cpu_of.items()} or None
         return res
     finally:
+        # the GPU tile first, with SIGTERM: it stops its IO engine and drains the GPU before it
+        # exits (integration/svc_run.c); a process killed with a kernel on the card can leave it faulted
+        for n, p in procs:
+            if n == "svc" and p.poll() is None:
+                p.terminate()
+                try:
+                    p.wait(timeout=40)
+                except subprocess.TimeoutExpired:
+                    pass
         for _, p in procs + [("producer", prod)]:
             if p.poll() is None:
                 p.kill()
