@@ -31,6 +31,8 @@ typedef struct {
   volatile ulong threads, dev_fds;             /* after privileged_init: /proc/self/task entries, /dev/kfd|dri fds */
   volatile ulong sandboxed;                    /* the tile ran inside fd_sandbox_enter (SVC_RUN_SANDBOX) */
   volatile double sec_pub, sec_pass, sec_flush, sec_post;   /* the tile's time in before_credit's steps */
+  volatile ulong m_sigs, m_host;               /* the VERIFY_GPU_SIGNATURES / _HOST_REDONE metric slots */
+  volatile ulong m_ing_n, m_ing_sum, m_batch_n, m_batch_sum;   /* the two GPU latency histograms' samples and sums (ns) */
 } svc_run_tile_res_t;
 
 typedef struct {

@@ -347,11 +347,15 @@ produce( char const * path, char const * stream, ulong tile_cnt, ulong in_depth 
             "\"consumed\": %lu, \"digest\": \"%016lx\", \"threads\": %lu, \"dev_fds\": %lu, \"metrics_ok\": %lu, \"sandboxed\": %lu, "
             "\"link\": {\"consumed\": %lu, \"filtered\": %lu, \"overrun_polling\": %lu, \"overrun_polling_frags\": %lu, "
             "\"overrun_reading\": %lu, \"overrun_reading_frags\": %lu}, "
-            "\"busy_s\": {\"publish\": %.4f, \"pass\": %.4f, \"flush\": %.4f, \"post\": %.4f}, \"early_credits\": %lu}",
+            "\"busy_s\": {\"publish\": %.4f, \"pass\": %.4f, \"flush\": %.4f, \"post\": %.4f}, \"early_credits\": %lu, "
+            "\"gpu_metrics\": {\"signatures\": %lu, \"host_redone\": %lu, \"ingest_n\": %lu, \"ingest_mean_us\": %.1f, "
+            "\"batch_n\": %lu, \"batch_mean_us\": %.1f}}",
             t ? ", " : "", r->frags, r->sigs, r->pub, r->parse, r->verify, r->dedup, r->bundle, r->overrun, r->lapped,
             (double)( r->t_end - t0 )*1e-9, c->frags, c->digest, r->threads, r->dev_fds, r->metrics_ok, r->sandboxed,
             r->link_consumed, r->link_filtered, r->link_ovr_poll, r->link_ovr_poll_frags, r->link_ovr_read,
-            r->link_ovr_read_frags, r->sec_pub, r->sec_pass, r->sec_flush, r->sec_post, r->early );
+            r->link_ovr_read_frags, r->sec_pub, r->sec_pass, r->sec_flush, r->sec_post, r->early,
+            r->m_sigs, r->m_host, r->m_ing_n, r->m_ing_n ? 1e-3*(double)r->m_ing_sum/(double)r->m_ing_n : 0.0,
+            r->m_batch_n, r->m_batch_n ? 1e-3*(double)r->m_batch_sum/(double)r->m_batch_n : 0.0 );
   }
   double s  = (double)( t_end - t0 )*1e-9;
   double rt = (double)( reg[0]+reg[1]+reg[2]+reg[3]+reg[4]+reg[5]+reg[6]+reg[7] ) + 1e-9;
@@ -361,12 +365,12 @@ produce( char const * path, char const * stream, ulong tile_cnt, ulong in_depth 
   print_lat( "latency_to_consumer", latq ); printf( ", " );
   double occ_n = (double)hdr->svc_occ[0] + 1e-9;
   printf( "\"svc\": {\"launches\": %lu, \"frags\": %lu, \"requests\": %lu, \"flushes\": %lu, \"flushed_frags\": %lu, "
-          "\"flushed_bytes\": %lu, \"spans\": %lu, \"gpu_s\": %.6f, \"host_launch_s\": %.6f, \"host_flush_s\": %.6f, "
+          "\"spans\": %lu, \"gpu_s\": %.6f, \"host_launch_s\": %.6f, \"host_flush_s\": %.6f, "
           "\"host_poll_s\": %.6f, \"polls\": %lu, \"ingests\": %lu, \"ingest_gpu_s\": %.6f, \"host_ingest_s\": %.6f, "
           "\"launch_max\": %lu, \"slots\": {\"posted\": %.3f, \"waiting\": %.3f, \"launched\": %.3f, \"results\": %.3f, "
           "\"free\": %.3f}}, ",
           hdr->svc_stats[0], hdr->svc_stats[1], hdr->svc_stats[2], hdr->svc_stats[3], hdr->svc_stats[4],
-          hdr->svc_stats[5], hdr->svc_stats[6], (double)hdr->svc_stats[7]*1e-9, (double)hdr->svc_stats[8]*1e-9,
+          hdr->svc_stats[6], (double)hdr->svc_stats[7]*1e-9, (double)hdr->svc_stats[8]*1e-9,
           (double)hdr->svc_stats[9]*1e-9, (double)hdr->svc_stats[10]*1e-9, hdr->svc_stats[11], hdr->svc_stats[12],
           (double)hdr->svc_stats[13]*1e-9, (double)hdr->svc_stats[14]*1e-9, hdr->svc_stats[15],
           (double)hdr->svc_occ[1]/occ_n, (double)hdr->svc_occ[2]/occ_n, (double)hdr->svc_occ[3]/occ_n,
@@ -597,6 +601,18 @@ tile( char const * path, ulong t ) {
           m[ FD_METRICS_COUNTER_LINK_OVERRUN_POLLING_FRAG_COUNT_OFF ]==rl->overrun_polling_frag_cnt &&
           m[ FD_METRICS_COUNTER_LINK_OVERRUN_READING_FRAG_COUNT_OFF ]==rl->overrun_reading_frag_cnt;
   }
+  /* the GPU service's metrics (fd_verify_metrics_hip.patch), as metrics_write left them */
+  r->m_sigs = fd_metrics_tl[ MIDX( COUNTER, VERIFY, GPU_SIGNATURES ) ];
+  r->m_host = fd_metrics_tl[ MIDX( COUNTER, VERIFY, GPU_HOST_REDONE ) ];
+  ulong in_ = 0UL, bn = 0UL;
+  for( ulong k=0UL; k<FD_HISTF_BUCKET_CNT; k++ ) {
+    in_ += fd_metrics_tl[ MIDX( HISTOGRAM, VERIFY, GPU_INGEST_LATENCY_NANOS ) + k ];
+    bn  += fd_metrics_tl[ MIDX( HISTOGRAM, VERIFY, GPU_BATCH_LATENCY_NANOS  ) + k ];
+  }
+  r->m_ing_n = in_; r->m_batch_n = bn;
+  r->m_ing_sum   = FD_MHIST_SUM( VERIFY, GPU_INGEST_LATENCY_NANOS );
+  r->m_batch_sum = FD_MHIST_SUM( VERIFY, GPU_BATCH_LATENCY_NANOS );
+  ok &= r->m_sigs==ctx->svc_sig_cnt && r->m_host==ctx->svc_host_cnt;
   r->metrics_ok = ok;
   double tpn = fd_tempo_tick_per_ns( NULL );
   r->sec_pub  = (double)ctx->svc_ticks[ 0 ]/tpn*1e-9; r->sec_pass = (double)ctx->svc_ticks[ 1 ]/tpn*1e-9;

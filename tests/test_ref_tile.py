@@ -179,3 +179,40 @@ def test_patched_tile_compiles_warning_free():
     for s_ in ("fd_verify_hip_tile_submit_range", "fd_verify_hip_tile_complete_range",
                "fd_verify_hip_tile_set_staging", "fd_verify_hip_tile_submit_frags"):
         assert s_ in syms, s_                  # the range, staging and stem paths are compiled in
+
+
+@pytest.mark.skipif(not os.path.isdir(REF), reason="needs /root/reference")
+def test_metrics_patch_extends_the_verify_schema(tmp_path):
+    """integration/fd_verify_metrics_hip.patch: the verify tile's GPU metrics
+    in metrics.xml and in its generated header and table, laid out as
+    gen_metrics.py lays them out (src/disco/metrics/generate/types.py: each
+    counter one slot, each histogram FD_HISTF_BUCKET_CNT + 1 = 17 slots, after
+    the tile's existing ones), inside the tile's metric area"""
+    import re
+    import shutil
+    import xml.etree.ElementTree as ET
+    files = ["src/disco/metrics/metrics.xml", "src/disco/metrics/generated/fd_metrics_verify.h",
+             "src/disco/metrics/generated/fd_metrics_verify.c"]
+    for f in files:
+        os.makedirs(tmp_path / os.path.dirname(f), exist_ok=True)
+        shutil.copy(os.path.join(REF, f), tmp_path / f)
+    patch = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "integration",
+                         "fd_verify_metrics_hip.patch")
+    subprocess.check_call(["patch", "-s", "-p1", "-i", patch], cwd=tmp_path)
+    root = ET.parse(tmp_path / files[0]).getroot()
+    verify = [t for t in root.findall("tile") if t.attrib["name"] == "verify"][0]
+    names = [m.attrib["name"] for m in verify]
+    assert names[-4:] == ["GpuSignatures", "GpuHostRedone", "GpuIngestLatencyNanos", "GpuBatchLatencyNanos"]
+    h = open(tmp_path / files[1]).read()
+    off = {m.group(1): int(m.group(2)) for m in re.finditer(r"#define FD_METRICS_\w+?_VERIFY_(\w+)_OFF\s+\((\d+)UL\)", h)}
+    slots, at = {"counter": 1, "histogram": 17}, 16
+    for m in verify:
+        key = re.sub(r"(?<!^)(?=[A-Z])", "_", m.attrib["name"]).upper()
+        assert off[key] == at, (key, off[key], at)
+        at += slots[m.tag]
+    all_h = open(os.path.join(REF, "src/disco/metrics/generated/fd_metrics_all.h")).read()
+    total = 8 * 254
+    assert f"#define FD_METRICS_TOTAL_SZ (8UL*254UL)" in all_h and 8 * at <= total
+    assert "#define FD_METRICS_VERIFY_TOTAL (9UL)" in h
+    c = open(tmp_path / files[2]).read()
+    assert c.count("DECLARE_METRIC") == 9 and "DECLARE_METRIC_HISTOGRAM_NONE( VERIFY_GPU_BATCH_LATENCY_NANOS )" in c

@@ -129,6 +129,13 @@ def test_link_metrics_written(stream, tmp_path):
         assert x["link"]["consumed"] == share
         assert x["link"]["consumed"] + x["link"]["filtered"] == stream["s"].n
         assert x["link"]["overrun_polling"] == 0 and x["link"]["overrun_reading"] == 0
+        # the GPU service's metrics in the verify tile's schema (integration/fd_verify_metrics_hip.patch:
+        # metrics.xml's GpuSignatures, GpuHostRedone, GpuIngestLatencyNanos, GpuBatchLatencyNanos), written by
+        # metrics_write: the counters equal the tile's own, each request with frags is one sample of each
+        # histogram, and a request's results come after its ingest
+        m = x["gpu_metrics"]
+        assert m["signatures"] == x["sigs"] > 0 and m["host_redone"] == 0
+        assert m["ingest_n"] == m["batch_n"] > 0 and 0 < m["ingest_mean_us"] <= m["batch_mean_us"]
 
 
 def test_tile_to_gpu_assignment(tmp_path):
@@ -230,4 +237,5 @@ def test_frags_shorter_than_their_payload_are_redone_on_the_tile(stream, tmp_pat
     r = S.run(stream["path"], 1, 1 << 14, str(tmp_path / "run"), env=env, mock=True)
     _check_run(r, stream["s"].n)
     assert r["host_redone"] == len(range(96, stream["s"].n, 97))
+    assert r["tiles"][0]["gpu_metrics"]["host_redone"] == r["host_redone"] and r["metrics_ok"] == 1
 
