@@ -338,7 +338,11 @@ struct svc_io_fdesc { u64 out, m, stage0, tile, seq, rsv[3]; };
    rules are stated for (MI355X_MICROARCH.md: never flat_ for these) */
 typedef __attribute__((address_space(1))) u64 io_gu64;
 #define IO_G( p ) ((io_gu64 *)(u64)(p))
-static __device__ __forceinline__ u64 io_lds( u64 const * p ) { return __hip_atomic_load( IO_G( p ), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM ); }
+/* a host-memory word the host writes while the engine runs (the rings, the
+   stop flag): a system-scope atomic, which crosses PCIe to the host's memory
+   every time (an L2 line of host memory is not kept coherent with the CPU's
+   writes; a plain load polled a FREE state forever, profiles/r06c) */
+static __device__ __forceinline__ u64 io_lds( u64 const * p ) { return __hip_atomic_fetch_add( IO_G( p ), 0ul, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM ); }
 static __device__ __forceinline__ void io_sts( u64 * p, u64 v ) { __hip_atomic_store( IO_G( p ), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM ); }
 /* the engine's own HBM words (job ring, descriptors, counters) are read and
    written by atomics, which execute at the memory side and are never
@@ -398,6 +402,11 @@ io_ingest( svc_io_cfg const & C, u32 r, u64 start ) {
                                                                               n <= C.frag_cap && aux0 && aux1 ) );
   if( !ok ) { io_err( C, IO_ERR_DESC, r, start, range ? n : kind ); return; }
   u64 const end = start + IO_JOB < n ? start + IO_JOB : n;
+  /* the request's lines and bytes were written by host cores before the
+     tile posted it: a system-scope acquire drops any copy this CU's L1 or
+     its XCD's L2 holds from an earlier lap, so the loads below read the
+     host's memory */
+  __builtin_amdgcn_fence( __ATOMIC_ACQUIRE, "" );
   for( u64 i = start; i < end; i += IO_F ) {
     u32 const nf = (u32)(end - i < IO_F ? end - i : IO_F);
     /* lane f < nf: frag i+f's size, kind, tsorig, source, and whether it
@@ -481,10 +490,11 @@ io_flush( svc_io_cfg const & C, u32 fi, u64 start ) {
   u64 const dc_out = C.tile[t].out, out_sz = C.tile[t].out_sz;
   long const delta = C.tile[t].delta;
   u64 const end = start + IO_FJOB < m ? start + IO_FJOB : m;
-  /* the staging frags were written by a verify launch that ended before the
-     tile saw RESULTS; this CU's L1 (and an XCD's L2 lines of the memory
-     types it does not keep coherent) may hold the slot's previous frags */
-  __builtin_amdgcn_fence( __ATOMIC_ACQUIRE, "agent" );
+  /* the out entries (host memory, the tile's) and the staging frags (HBM,
+     written by a verify launch that ended before the tile saw RESULTS): a
+     system-scope acquire drops stale copies of either from this CU's L1 and
+     its XCD's L2 */
+  __builtin_amdgcn_fence( __ATOMIC_ACQUIRE, "" );
   for( u64 e = start; e < end; e += IO_F ) {
     u32 const nf = (u32)(end - e < IO_F ? end - e : IO_F);
     __amdgpu_buffer_rsrc_t ro = io_rsrc( out + 16ul * e, 16u * nf );
@@ -912,12 +922,12 @@ fd_verify_svc_boot( void * seg_mem, int device, ulong batch_max, ulong inflight 
                         sizeof(svc_io_dctl);
     SV_CHECK( hipMalloc( &s->d_io, io_sz ) );
     SV_CHECK( hipMemset( s->d_io, 0, io_sz ) );
-    /* the control block and the validated sizes: uncached (MTYPE_UC) host
-       memory, which the engine's polls always read from memory */
-    SV_CHECK( hipHostMalloc( &s->h_ctl, 4096, hipHostMallocMapped | hipHostMallocUncached ) );
+    /* the control block and the validated sizes: coherent (fine-grained)
+       host memory; the engine polls the stop flag with system atomics */
+    SV_CHECK( hipHostMalloc( &s->h_ctl, 4096, hipHostMallocMapped | hipHostMallocCoherent ) );
     memset( s->h_ctl, 0, 4096 );
     SV_CHECK( hipHostGetDevicePointer( (void **)&s->d_ctl, s->h_ctl, 0 ) );
-    SV_CHECK( hipHostMalloc( (void **)&s->h_vd, 16ul * nreq, hipHostMallocMapped | hipHostMallocUncached ) );
+    SV_CHECK( hipHostMalloc( (void **)&s->h_vd, 16ul * nreq, hipHostMallocMapped | hipHostMallocCoherent ) );
     memset( s->h_vd, 0, 16ul * nreq );
     SV_CHECK( hipHostGetDevicePointer( (void **)&s->d_vd, s->h_vd, 0 ) );
     SV_CHECK( hipEventCreate( &s->io_ev ) );
@@ -931,11 +941,11 @@ fd_verify_svc_map( fd_verify_svc_t * s, void * host, ulong sz ) {
   if( !s || !host || !sz || s->nreg >= SVC_REGION_MAX ) return -1;
   ulong a = (ulong)host & ~4095ul, e = ((ulong)host + sz + 4095ul) & ~4095ul;
   SV_CHECK( hipSetDevice( s->dev ) );
-  /* with the IO engine the GPU polls this memory from a running kernel (the
-     request and flush rings) and copies from it: mapped uncached
-     (MTYPE_UC), so no GPU cache level can serve a stale line */
-  unsigned flags = hipHostRegisterMapped | hipHostRegisterPortable | (s->io ? hipExtHostRegisterUncached : 0u);
-  if( hipHostRegister( (void *)a, e - a, flags ) != hipSuccess ) return -1;
+  /* (with hipExtHostRegisterUncached the IO engine's first access to the
+     segment faulted, profiles/r06d: registered as before; the engine reads
+     what the host writes while it runs with system atomics and after
+     system-scope acquires) */
+  if( hipHostRegister( (void *)a, e - a, hipHostRegisterMapped | hipHostRegisterPortable ) != hipSuccess ) return -1;
   void * d = 0;
   SV_CHECK( hipHostGetDevicePointer( &d, (void *)a, 0 ) );
   s->reg[s->nreg].h = (u8 *)a; s->reg[s->nreg].sz = e - a; s->reg[s->nreg].d = (u8 *)d;
