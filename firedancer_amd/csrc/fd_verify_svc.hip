@@ -342,13 +342,24 @@ typedef __attribute__((address_space(1))) u64 io_gu64;
    stop flag): a system-scope atomic, which crosses PCIe to the host's memory
    every time (an L2 line of host memory is not kept coherent with the CPU's
    writes; a plain load polled a FREE state forever, profiles/r06c) */
-static __device__ __forceinline__ u64 io_lds( u64 const * p ) { return __hip_atomic_fetch_add( IO_G( p ), 0ul, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM ); }
+/* the read is an add of zero written out as the instruction: LLVM turns a
+   relaxed RMW it can prove idempotent into a plain load (seen in the ISA),
+   which an L2 may serve */
+static __device__ __forceinline__ u64 io_lds( u64 const * p ) {
+  u64 r, z = 0ul;
+  asm volatile( "global_atomic_add_x2 %0, %1, %2, off sc0 sc1\n\ts_waitcnt vmcnt(0)" : "=v"( r ) : "v"( p ), "v"( z ) : "memory" );
+  return r;
+}
 static __device__ __forceinline__ void io_sts( u64 * p, u64 v ) { __hip_atomic_store( IO_G( p ), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM ); }
 /* the engine's own HBM words (job ring, descriptors, counters) are read and
    written by atomics, which execute at the memory side and are never
    served from an XCD's L2 (MI355X_MICROARCH.md): a word written by a wave
    on one XCD is what a wave on another reads, whatever either L2 held */
-static __device__ __forceinline__ u64 io_lda( u64 const * p ) { return __hip_atomic_fetch_add( IO_G( p ), 0ul, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT ); }
+static __device__ __forceinline__ u64 io_lda( u64 const * p ) {
+  u64 r, z = 0ul;
+  asm volatile( "global_atomic_add_x2 %0, %1, %2, off sc0\n\ts_waitcnt vmcnt(0)" : "=v"( r ) : "v"( p ), "v"( z ) : "memory" );
+  return r;
+}
 static __device__ __forceinline__ void io_sta( u64 * p, u64 v ) { (void)__hip_atomic_exchange( IO_G( p ), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT ); }
 static __device__ __forceinline__ u64 io_adda( u64 * p, u64 v ) { return __hip_atomic_fetch_add( IO_G( p ), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT ); }
 static __device__ __forceinline__ void io_drain( void ) { asm volatile( "s_waitcnt vmcnt(0)" ::: "memory" ); }
@@ -1170,6 +1181,8 @@ svc_flush_start( fd_verify_svc_t * s, ulong t, fd_verify_svc_flush_t const * f )
   s->stat[3]++; s->stat[4] += m;
 }
 
+extern "C" int fd_verify_svc_debug( fd_verify_svc_t const * s, char * buf, ulong sz );
+
 extern "C" int
 fd_verify_svc_poll( fd_verify_svc_t * s ) {
   fd_verify_svc_seg_t * g = s->seg;
@@ -1208,6 +1221,8 @@ fd_verify_svc_poll( fd_verify_svc_t * s ) {
     if( !(s->stat[11] & 1023ul) ) {
       hipError_t e = hipEventQuery( s->io_ev );
       if( e != hipErrorNotReady ) {
+        char b[ 1024 ];
+        if( fd_verify_svc_debug( s, b, sizeof(b) ) > 0 ) { b[ sizeof(b)-2 ] = '\0'; fprintf( stderr, "fd_verify_svc: %s\n", b ); }
         fprintf( stderr, "fd_verify_svc: IO engine ended while running (%s)\n", hipGetErrorString( e ) );
         abort();
       }
