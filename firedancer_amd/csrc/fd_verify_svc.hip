@@ -294,6 +294,7 @@ struct svc_io_cfg {
   u64 seg, tile_cnt, req_depth, slot_cap, frag_cap, tile_sz, slot_sz, req_off, out_off, frag_off;
   u64 ing, ing_sz, ing_kind, ing_tso, stage;
   u64 ring, idesc, iremain, fdesc, fremain, fdone, dctl, hctl, hvd;
+  u64 dbg;                    /* FD_VERIFY_SVC_IO_DBG: steps of the leader to leave out (diagnostics) */
   svc_io_link link[FD_VERIFY_SVC_LINK_MAX];
   svc_io_tile tile[FD_VERIFY_SVC_TILE_MAX];
 };
@@ -339,17 +340,10 @@ struct svc_io_fdesc { u64 out, m, stage0, tile, seq, rsv[3]; };
 typedef __attribute__((address_space(1))) u64 io_gu64;
 #define IO_G( p ) ((io_gu64 *)(u64)(p))
 /* a host-memory word the host writes while the engine runs (the rings, the
-   stop flag): a system-scope atomic, which crosses PCIe to the host's memory
-   every time (an L2 line of host memory is not kept coherent with the CPU's
-   writes; a plain load polled a FREE state forever, profiles/r06c) */
-/* the read is an add of zero written out as the instruction: LLVM turns a
-   relaxed RMW it can prove idempotent into a plain load (seen in the ISA),
-   which an L2 may serve */
-static __device__ __forceinline__ u64 io_lds( u64 const * p ) {
-  u64 r, z = 0ul;
-  asm volatile( "global_atomic_add_x2 %0, %1, %2, off sc0 sc1\n\ts_waitcnt vmcnt(0)" : "=v"( r ) : "v"( p ), "v"( z ) : "memory" );
-  return r;
-}
+   stop flag): a system-scope load (sc0 sc1), which fine-grained host memory
+   serves from the host's memory (the memory model's system coherence; an
+   atomic add of zero over PCIe took ~50 us a read, profiles/r06g) */
+static __device__ __forceinline__ u64 io_lds( u64 const * p ) { return __hip_atomic_load( IO_G( p ), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM ); }
 static __device__ __forceinline__ void io_sts( u64 * p, u64 v ) { __hip_atomic_store( IO_G( p ), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM ); }
 /* the engine's own HBM words (job ring, descriptors, counters) are read and
    written by atomics, which execute at the memory side and are never
@@ -365,7 +359,7 @@ static __device__ __forceinline__ u64 io_adda( u64 * p, u64 v ) { return __hip_a
 static __device__ __forceinline__ void io_drain( void ) { asm volatile( "s_waitcnt vmcnt(0)" ::: "memory" ); }
 /* a raw buffer over [p, p+n): accesses past n read 0 and write nothing */
 static __device__ __forceinline__ __amdgpu_buffer_rsrc_t io_rsrc( u64 p, u32 n ) {
-  p = ((u64)__builtin_amdgcn_readfirstlane( (u32)(p >> 32) ) << 32) | (u64)__builtin_amdgcn_readfirstlane( (u32)p );
+  p = ((u64)(u32)__builtin_amdgcn_readfirstlane( (u32)(p >> 32) ) << 32) | (u64)(u32)__builtin_amdgcn_readfirstlane( (u32)p );
   return __builtin_amdgcn_make_buffer_rsrc( (void *)p, (short)0, (int)__builtin_amdgcn_readfirstlane( n ), 0x00020000 );
 }
 #define IO_SYS 17   /* sc0 sc1: system coherent (host memory) */
@@ -373,8 +367,12 @@ static __device__ __forceinline__ __amdgpu_buffer_rsrc_t io_rsrc( u64 p, u32 n )
 static __device__ __forceinline__ u64 io_shfl64( u64 v, u32 l ) {
   return (u64)(u32)__shfl( (int)(u32)v, (int)l ) | ((u64)(u32)__shfl( (int)(u32)(v >> 32), (int)l ) << 32);
 }
-static __device__ __forceinline__ u64 io_uni( u64 v ) {   /* lane 0's value, in SGPRs */
-  return ((u64)__builtin_amdgcn_readfirstlane( (u32)(v >> 32) ) << 32) | (u64)__builtin_amdgcn_readfirstlane( (u32)v );
+/* the first active lane's value, in SGPRs (readfirstlane returns an int:
+   each half goes through u32 before it widens, or a low half with bit 31
+   set would sign-extend over the high half -- a pointer so corrupted was
+   the engine's first fault, profiles/r06h) */
+static __device__ __forceinline__ u64 io_uni( u64 v ) {
+  return ((u64)(u32)__builtin_amdgcn_readfirstlane( (u32)(v >> 32) ) << 32) | (u64)(u32)__builtin_amdgcn_readfirstlane( (u32)v );
 }
 
 /* the first error wins; the host aborts on it (the reference ends a tile
@@ -652,11 +650,11 @@ io_leader( svc_io_cfg const & C ) {
       u64 dv = 0ul;
 #pragma unroll
       for( u32 k = 0; k < 16u; k++ ) if( lane == k ) dv = d[k];
-      if( lane < 16u ) io_sta( (u64 *)(C.idesc + 128ul * r) + lane, dv );
-      if( lane < 2u ) io_sts( (u64 *)C.hvd + 2ul * r + lane, lane ? seed : n );
-      if( lane == 0u ) io_sta( (u64 *)C.iremain + r, n );
+      if( !(C.dbg & 1ul) && lane < 16u ) io_sta( (u64 *)(C.idesc + 128ul * r) + lane, dv );
+      if( !(C.dbg & 2ul) && lane < 2u ) io_sts( (u64 *)C.hvd + 2ul * r + lane, lane ? seed : n );
+      if( !(C.dbg & 4ul) && lane == 0u ) io_sta( (u64 *)C.iremain + r, n );
       io_drain();
-      if( !n ) { if( lane == 0u ) io_sts( (u64 *)rt, FD_VERIFY_SVC_INGESTED ); }
+      if( !n ) { if( !(C.dbg & 8ul) && lane == 0u ) io_sts( (u64 *)rt, FD_VERIFY_SVC_INGESTED ); }
       else io_push( C, tail, (u32)r, (n + IO_JOB - 1ul) / IO_JOB, IO_JOB );
       if( lane == t ) take++;
       active = true;
@@ -1053,6 +1051,10 @@ fd_verify_svc_run( fd_verify_svc_t * s ) {
     C.fdone   = (u64)q; q += nfl * 8ul;
     C.dctl    = (u64)q;
     C.hctl = (u64)s->d_ctl; C.hvd = (u64)s->d_vd;
+    { char const * e = getenv( "FD_VERIFY_SVC_IO_DBG" ); C.dbg = e ? strtoul( e, 0, 0 ) : 0ul; }
+    if( getenv( "FD_VERIFY_SVC_IO_DBG" ) )
+      fprintf( stderr, "fd_verify_svc: IO engine cfg seg %lx ring %lx idesc %lx iremain %lx dctl %lx hctl %lx hvd %lx dbg %lx\n",
+               C.seg, C.ring, C.idesc, C.iremain, C.dctl, C.hctl, C.hvd, C.dbg );
     for( ulong l = 0; l < FD_VERIFY_SVC_LINK_MAX; l++ ) {
       if( !s->link[l].set ) continue;
       C.link[l].mcache = (u64)s->link[l].d_mcache; C.link[l].mask = s->link[l].depth - 1ul; C.link[l].base = (u64)s->link[l].d_base;
