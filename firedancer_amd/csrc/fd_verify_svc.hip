@@ -354,6 +354,10 @@ static __device__ __forceinline__ u64 io_lda( u64 const * p ) {
   asm volatile( "global_atomic_add_x2 %0, %1, %2, off sc0\n\ts_waitcnt vmcnt(0)" : "=v"( r ) : "v"( p ), "v"( z ) : "memory" );
   return r;
 }
+/* a poll's cheap form: an sc1 load (past this CU's L1, served by the XCD's
+   L2); the worker's job wait polls with it and falls back to io_lda every
+   16th read, so a copy its L2 may keep is never trusted for long */
+static __device__ __forceinline__ u64 io_ldc( u64 const * p ) { return __hip_atomic_load( IO_G( p ), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT ); }
 static __device__ __forceinline__ void io_sta( u64 * p, u64 v ) { (void)__hip_atomic_exchange( IO_G( p ), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT ); }
 static __device__ __forceinline__ u64 io_adda( u64 * p, u64 v ) { return __hip_atomic_fetch_add( IO_G( p ), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT ); }
 static __device__ __forceinline__ void io_drain( void ) { asm volatile( "s_waitcnt vmcnt(0)" ::: "memory" ); }
@@ -411,11 +415,11 @@ io_ingest( svc_io_cfg const & C, u32 r, u64 start ) {
                                                                               n <= C.frag_cap && aux0 && aux1 ) );
   if( !ok ) { io_err( C, IO_ERR_DESC, r, start, range ? n : kind ); return; }
   u64 const end = start + IO_JOB < n ? start + IO_JOB : n;
-  /* the request's lines and bytes were written by host cores before the
-     tile posted it: a system-scope acquire drops any copy this CU's L1 or
-     its XCD's L2 holds from an earlier lap, so the loads below read the
-     host's memory */
-  __builtin_amdgcn_fence( __ATOMIC_ACQUIRE, "" );
+  /* the request's lines and bytes (host memory, written by host cores
+     before the tile posted it) are read with system-scope loads, which the
+     host's memory serves; FD_VERIFY_SVC_IO_DBG bit 16 adds a system-scope
+     acquire here (an A/B: it invalidates the XCD's L2) */
+  if( C.dbg & 16ul ) __builtin_amdgcn_fence( __ATOMIC_ACQUIRE, "" );
   for( u64 i = start; i < end; i += IO_F ) {
     u32 const nf = (u32)(end - i < IO_F ? end - i : IO_F);
     /* lane f < nf: frag i+f's size, kind, tsorig, source, and whether it
@@ -499,11 +503,11 @@ io_flush( svc_io_cfg const & C, u32 fi, u64 start ) {
   u64 const dc_out = C.tile[t].out, out_sz = C.tile[t].out_sz;
   long const delta = C.tile[t].delta;
   u64 const end = start + IO_FJOB < m ? start + IO_FJOB : m;
-  /* the out entries (host memory, the tile's) and the staging frags (HBM,
-     written by a verify launch that ended before the tile saw RESULTS): a
-     system-scope acquire drops stale copies of either from this CU's L1 and
-     its XCD's L2 */
-  __builtin_amdgcn_fence( __ATOMIC_ACQUIRE, "" );
+  /* the staging frags (HBM, written by a verify launch that ended before
+     the tile saw RESULTS): an agent-scope acquire drops this CU's L1 copies
+     of the slot's previous frags (the out entries are host memory, read with
+     system-scope loads) */
+  __builtin_amdgcn_fence( __ATOMIC_ACQUIRE, "agent" );
   for( u64 e = start; e < end; e += IO_F ) {
     u32 const nf = (u32)(end - e < IO_F ? end - e : IO_F);
     __amdgpu_buffer_rsrc_t ro = io_rsrc( out + 16ul * e, 16u * nf );
@@ -721,11 +725,16 @@ io_worker( svc_io_cfg const & C ) {
     svc_io_job * j = ring + (p & (IO_RING - 1ul));
     u32 nap = 1u;
     bool stop = false;
-    for( ;; ) {
-      if( io_lda( &j->tag ) == p + 1ul ) break;
-      if( io_lda( &dc->stop ) ) { stop = true; break; }
+    for( u32 it = 1u;; it++ ) {
+      /* sc1 polls, an atomic read every 16th (and for the stop flag, every
+         32nd): 127 waves' atomics on shared lines serialized at the memory
+         side and slowed every atomic of the engine (the leader's loop ran
+         ~90 us, profiles/r06i) */
+      u64 const tg = (it & 15u) ? io_ldc( &j->tag ) : io_lda( &j->tag );
+      if( tg == p + 1ul ) break;
+      if( !(it & 31u) && io_lda( &dc->stop ) ) { stop = true; break; }
       for( u32 q = 0; q < nap; q++ ) __builtin_amdgcn_s_sleep( 8 );
-      nap = nap < 16u ? 2u * nap : 16u;
+      nap = nap < 8u ? 2u * nap : 8u;
     }
     if( stop ) break;
     u64 const pay = io_uni( io_lda( &j->pay ) );

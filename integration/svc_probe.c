@@ -129,6 +129,31 @@ main( int argc, char ** argv ) {
   say( "flush", "ok" );
   fd_verify_svc_st( &r1->state, FD_VERIFY_SVC_FREE );
 
+  /* latency: 32 more frag requests one at a time, post -> INGESTED */
+  step_now = "latency";
+  double lat[ 32 ]; ulong nl = 0UL;
+  for( ulong k=2UL; k<34UL; k++ ) {
+    ulong slot = k & ( D-1UL );
+    fd_verify_svc_req_t * rq = fd_verify_svc_req( seg, 0UL, slot );
+    uchar * fb = fd_verify_svc_frag( seg, 0UL, slot );
+    ushort * fs = fd_verify_svc_frag_sz( seg, 0UL, slot );
+    uchar * fkk = fd_verify_svc_frag_kind( seg, 0UL, slot );
+    for( ulong j=0UL; j<nfr; j++ ) { memset( fb + j*FD_VERIFY_SVC_FRAG_STRIDE, 0, 128UL ); fs[ j ] = 96; fkk[ j ] = 0; }
+    if( fd_verify_svc_post_frags( seg, 0UL, k, nfr, 1UL, 0L ) ) { printf( "post %lu refused\n", k ); return 1; }
+    long a = now_ns();
+    while( !fd_verify_svc_state_ingested( fd_verify_svc_ld( &rq->state ) ) ) {
+      fd_verify_svc_poll( svc );
+      if( now_ns()-a>2000000000L ) { say( "latency", "TIMEOUT before INGESTED" ); return 1; }
+    }
+    lat[ nl++ ] = 1e-3*(double)( now_ns()-a );
+    if( wait_state( "latency", &rq->state, FD_VERIFY_SVC_RESULTS, 5000L ) ) return 1;
+    fd_verify_svc_st( &rq->state, FD_VERIFY_SVC_FREE );
+  }
+  for( ulong i=1UL; i<nl; i++ ) for( ulong j=i; j>0UL && lat[ j-1UL ]>lat[ j ]; j-- ) { double x = lat[ j ]; lat[ j ] = lat[ j-1UL ]; lat[ j-1UL ] = x; }
+  snprintf( m, sizeof(m), "post -> INGESTED over %lu requests of %lu frags: min %.1f, median %.1f, max %.1f us", nl, nfr,
+            lat[ 0 ], lat[ nl/2UL ], lat[ nl-1UL ] );
+  say( "latency", m );
+
   step_now = "delete";
   fd_verify_svc_delete( svc );
   svc = NULL;
