@@ -334,6 +334,8 @@ struct svc_io_fdesc { u64 out, m, stage0, tile, seq, rsv[3]; };
 #define IO_ST_FLFRAGS 3     /* frags flushed */
 #define IO_ST_JOBS    4     /* jobs done */
 #define IO_ST_EXITED  5     /* waves that left */
+#define IO_ST_TAKEN   6     /* jobs taken off the ring */
+#define IO_ST_LOADED  7     /* ingest jobs past their loads and stores */
 
 /* global (not flat) accesses: the sc bits and the counters the visibility
    rules are stated for (MI355X_MICROARCH.md: never flat_ for these) */
@@ -360,6 +362,13 @@ static __device__ __forceinline__ u64 io_lda( u64 const * p ) {
 static __device__ __forceinline__ u64 io_ldc( u64 const * p ) { return __hip_atomic_load( IO_G( p ), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT ); }
 static __device__ __forceinline__ void io_sta( u64 * p, u64 v ) { (void)__hip_atomic_exchange( IO_G( p ), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT ); }
 static __device__ __forceinline__ u64 io_adda( u64 * p, u64 v ) { return __hip_atomic_fetch_add( IO_G( p ), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT ); }
+/* FD_VERIFY_SVC_IO_DBG bit 64: the leader's host polls as system atomics (an A/B) */
+static __device__ __forceinline__ u64 io_ldx( u64 const * p ) {
+  u64 r, z = 0ul;
+  asm volatile( "global_atomic_add_x2 %0, %1, %2, off sc0 sc1\n\ts_waitcnt vmcnt(0)" : "=v"( r ) : "v"( p ), "v"( z ) : "memory" );
+  return r;
+}
+#define IO_LDS( p ) ( (C.dbg & 64ul) ? io_ldx( p ) : io_lds( p ) )
 static __device__ __forceinline__ void io_drain( void ) { asm volatile( "s_waitcnt vmcnt(0)" ::: "memory" ); }
 /* a raw buffer over [p, p+n): accesses past n read 0 and write nothing */
 static __device__ __forceinline__ __amdgpu_buffer_rsrc_t io_rsrc( u64 p, u32 n ) {
@@ -383,11 +392,11 @@ static __device__ __forceinline__ u64 io_uni( u64 v ) {
    with FD_LOG_ERR on a corrupt frag or a bad request) */
 static __device__ void
 io_err( svc_io_cfg const & C, u64 code, u64 a, u64 b, u64 c ) {
-  if( (threadIdx.x & 63u) != __builtin_ctzll( __ballot( 1 ) ) ) return;
   svc_io_dctl * dc = (svc_io_dctl *)C.dctl;
   svc_io_hctl * hc = (svc_io_hctl *)C.hctl;
   u64 zero = 0;
-  if( __hip_atomic_compare_exchange_strong( IO_G( &dc->err ), &zero, code, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+  if( (threadIdx.x & 63u) == (u32)__builtin_ctzll( __ballot( 1 ) ) &&
+      __hip_atomic_compare_exchange_strong( IO_G( &dc->err ), &zero, code, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
                                             __HIP_MEMORY_SCOPE_AGENT ) ) {
     io_sts( &hc->err_a, a ); io_sts( &hc->err_b, b ); io_sts( &hc->err_c, c );
     io_drain();
@@ -398,7 +407,7 @@ io_err( svc_io_cfg const & C, u64 code, u64 a, u64 b, u64 c ) {
 /* ingest job: frags [start, start+IO_JOB) of request r (its descriptor made
    by the leader): k_svc_gather's checks and copy, IO_F frags per step with
    their loads in flight together */
-static __device__ void
+static __device__ __attribute__((noinline)) void
 io_ingest( svc_io_cfg const & C, u32 r, u64 start ) {
   u32 const lane = threadIdx.x & 63u;
   u64 const dw = lane < 16u ? io_lda( (u64 const *)(C.idesc + 128ul * r) + lane ) : 0ul;
@@ -475,9 +484,10 @@ io_ingest( svc_io_cfg const & C, u32 r, u64 start ) {
     __builtin_amdgcn_raw_buffer_store_b8( (u8)mkind, rk, lane, 0, IO_SC1 );
     __builtin_amdgcn_raw_buffer_store_b32( range ? mtso : 0u, rt, 4u * lane, 0, IO_SC1 );
   }
-  io_drain();
-  u64 const cnt = end - start;
   svc_io_dctl * dc = (svc_io_dctl *)C.dctl;
+  io_drain();
+  if( lane == 0u ) io_adda( &dc->st[IO_ST_LOADED], 1ul );
+  u64 const cnt = end - start;
   if( lane == 0u ) {
     u64 const left = io_adda( (u64 *)C.iremain + r, (u64)0 - cnt );
     io_adda( &dc->st[IO_ST_FRAGS], cnt ); io_adda( &dc->st[IO_ST_JOBS], 1ul );
@@ -490,7 +500,7 @@ io_ingest( svc_io_cfg const & C, u32 r, u64 start ) {
 
 /* flush job: out entries [start, start+IO_FJOB) of flush fi, k_svc_compact's
    checks and copy (staging HBM -> the tile's out dcache in host memory) */
-static __device__ void
+static __device__ __attribute__((noinline)) void
 io_flush( svc_io_cfg const & C, u32 fi, u64 start ) {
   u32 const lane = threadIdx.x & 63u;
   u64 const fw = lane < 5u ? io_lda( (u64 const *)(C.fdesc + sizeof(svc_io_fdesc) * fi) + lane ) : 0ul;
@@ -538,9 +548,10 @@ io_flush( svc_io_cfg const & C, u32 fi, u64 start ) {
       __builtin_amdgcn_raw_buffer_store_b128( c[f], rd, 16u * lane + 2048u, 0, IO_SYS );
     }
   }
-  io_drain();
-  u64 const cnt = end - start;
   svc_io_dctl * dc = (svc_io_dctl *)C.dctl;
+  io_drain();
+  if( lane == 0u ) io_adda( &dc->st[IO_ST_LOADED], 1ul );
+  u64 const cnt = end - start;
   if( lane == 0u ) {
     u64 const left = io_adda( (u64 *)C.fremain + fi, (u64)0 - cnt );
     io_adda( &dc->st[IO_ST_FLFRAGS], cnt ); io_adda( &dc->st[IO_ST_JOBS], 1ul );
@@ -562,7 +573,7 @@ io_push( svc_io_cfg const & C, u64 & tail, u32 idx, u64 J, u64 step ) {
       for( ;; ) {
         u64 const tg = io_lda( &j->tag );
         if( !tg || tg == (IO_CONS | (pos - IO_RING)) ) break;
-        if( io_lds( &hc->stop ) ) break;
+        if( IO_LDS( &hc->stop ) ) break;
         __builtin_amdgcn_s_sleep( 4 );
       }
       io_sta( &j->pay, ((k * step) << 32) | (u64)idx );
@@ -596,15 +607,15 @@ io_leader( svc_io_cfg const & C ) {
       if( lane < 8u ) io_sts( &hc->dbg[lane], dv );
       if( lane == 0u ) io_sts( &hc->beat, beat >> 8 );
     }
-    if( io_lds( &hc->stop ) ) { if( lane == 0u ) io_sta( &dc->stop, 1ul ); break; }
+    if( IO_LDS( &hc->stop ) ) { if( lane == 0u ) io_sta( &dc->stop, 1ul ); break; }
     bool active = false;
 
     /* 1. requests: each tile's next slot in ring order */
     u64 const slot = take & (D - 1ul);
     u64 const rq   = tb + sizeof(fd_verify_svc_tile_t) + slot * sizeof(fd_verify_svc_req_t);
-    u64 const state = tl && !dead ? io_lds( (u64 const *)rq ) : 0ul;
+    u64 const state = tl && !dead ? IO_LDS( (u64 const *)rq ) : 0ul;
     bool const posted = state == FD_VERIFY_SVC_POSTED;
-    u64 const id = posted ? io_lds( (u64 const *)(rq + offsetof( fd_verify_svc_req_t, id )) ) : 0ul;
+    u64 const id = posted ? IO_LDS( (u64 const *)(rq + offsetof( fd_verify_svc_req_t, id )) ) : 0ul;
     bool const fresh = posted && id == take;
     bool const wrong = posted && id != take && id + D != take;
     if( __ballot( wrong ) ) {
@@ -616,7 +627,7 @@ io_leader( svc_io_cfg const & C ) {
     for( u64 fm = __ballot( fresh ); fm; fm &= fm - 1ul ) {
       u32 const t  = __builtin_ctzll( fm );
       u64 const rt = io_uni( io_shfl64( rq, t ) ), st = io_uni( io_shfl64( slot, t ) );
-      u64 const w  = lane < 9u ? io_lds( (u64 const *)rt + lane ) : 0ul;      /* state kind link seq0 seq_cnt rr_cnt rr_idx n seed */
+      u64 const w  = lane < 9u ? IO_LDS( (u64 const *)rt + lane ) : 0ul;      /* state kind link seq0 seq_cnt rr_cnt rr_idx n seed */
       u64 const kind = io_uni( io_shfl64( w, 1 ) ), link = io_uni( io_shfl64( w, 2 ) ), seq0 = io_uni( io_shfl64( w, 3 ) );
       u64 const seq_cnt = io_uni( io_shfl64( w, 4 ) ), rr_cnt = io_uni( io_shfl64( w, 5 ) ), rr_idx = io_uni( io_shfl64( w, 6 ) );
       u64 const n = io_uni( io_shfl64( w, 7 ) ), seed = io_uni( io_shfl64( w, 8 ) );
@@ -665,14 +676,14 @@ io_leader( svc_io_cfg const & C ) {
     }
 
     /* 2. flushes: each tile's newly posted flush ring entries */
-    u64 const fpost = tl && !dead ? io_lds( (u64 const *)(tb + offsetof( fd_verify_svc_tile_t, flush_post )) ) : 0ul;
+    u64 const fpost = tl && !dead ? IO_LDS( (u64 const *)(tb + offsetof( fd_verify_svc_tile_t, flush_post )) ) : 0ul;
     bool const fnew = tl && !dead && ftake < fpost && ftake - ffin < IO_FQ;
     for( u64 fm = __ballot( fnew ); fm; fm &= fm - 1ul ) {
       u32 const t = __builtin_ctzll( fm );
       u64 const k = io_uni( io_shfl64( ftake, t ) );
       u64 const tbt = C.seg + FD_VERIFY_SVC_ALIGN + (u64)t * C.tile_sz;
       u64 const fe = tbt + offsetof( fd_verify_svc_tile_t, flush ) + (k & (FD_VERIFY_SVC_FLUSH_DEPTH - 1ul)) * sizeof(fd_verify_svc_flush_t);
-      u64 const w = lane < 3u ? io_lds( (u64 const *)fe + lane ) : 0ul;
+      u64 const w = lane < 3u ? IO_LDS( (u64 const *)fe + lane ) : 0ul;
       u64 const fslot = io_uni( io_shfl64( w, 0 ) ), lo = io_uni( io_shfl64( w, 1 ) ), hi = io_uni( io_shfl64( w, 2 ) );
       if( fslot >= D || lo > hi || hi > C.slot_cap ) {
         io_err( C, IO_ERR_FLUSH, t, k, fslot );
@@ -730,15 +741,18 @@ io_worker( svc_io_cfg const & C ) {
          32nd): 127 waves' atomics on shared lines serialized at the memory
          side and slowed every atomic of the engine (the leader's loop ran
          ~90 us, profiles/r06i) */
-      u64 const tg = (it & 15u) ? io_ldc( &j->tag ) : io_lda( &j->tag );
+      /* io_uni: every lane read the same word; the branches are the wave's
+         (a compare on a VGPR value made the loop divergent to the compiler,
+         and its per-lane loop exits left the engine's waves stuck) */
+      u64 const tg = io_uni( (it & 15u) && !(C.dbg & 32ul) ? io_ldc( &j->tag ) : io_lda( &j->tag ) );
       if( tg == p + 1ul ) break;
-      if( !(it & 31u) && io_lda( &dc->stop ) ) { stop = true; break; }
+      if( !(it & 31u) && io_uni( io_lda( &dc->stop ) ) ) { stop = true; break; }
       for( u32 q = 0; q < nap; q++ ) __builtin_amdgcn_s_sleep( 8 );
       nap = nap < 8u ? 2u * nap : 8u;
     }
     if( stop ) break;
     u64 const pay = io_uni( io_lda( &j->pay ) );
-    if( lane == 0u ) io_sta( &j->tag, IO_CONS | p );
+    if( lane == 0u ) { io_sta( &j->tag, IO_CONS | p ); io_adda( &dc->st[IO_ST_TAKEN], 1ul ); }
     u32 const idx = (u32)pay;
     if( idx & 0x80000000u ) io_flush( C, idx & 0x7fffffffu, pay >> 32 );
     else                    io_ingest( C, idx, pay >> 32 );
@@ -1413,8 +1427,8 @@ fd_verify_svc_debug( fd_verify_svc_t const * s, char * buf, ulong sz ) {
   if( s->io && n > 0 && (ulong)n < sz ) {
     svc_io_hctl const * hc = (svc_io_hctl const *)s->h_ctl;
     n += snprintf( buf + n, sz - (ulong)n, " io[beat %lu reqs %lu frags %lu flushes %lu jobs %lu exited %lu tail %lu claim %lu "
-                   "take %lu %lu ftake %lu ffin %lu err %lu]", hc->beat, hc->st[0], hc->st[1], hc->st[2], hc->st[4], hc->st[5],
-                   hc->dbg[0], hc->dbg[1], hc->dbg[2], hc->dbg[3], hc->dbg[6], hc->dbg[7], hc->err );
+                   "take %lu %lu ftake %lu ffin %lu err %lu taken %lu loaded %lu]", hc->beat, hc->st[0], hc->st[1], hc->st[2], hc->st[4], hc->st[5],
+                   hc->dbg[0], hc->dbg[1], hc->dbg[2], hc->dbg[3], hc->dbg[6], hc->dbg[7], hc->err, hc->st[6], hc->st[7] );
   }
   return n;
 }

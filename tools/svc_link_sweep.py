@@ -37,6 +37,31 @@ def lost(r):
     return r["overrun"] + r["lapped"]
 
 
+def drop_free_search(run, hi, lo, steps):
+    """The highest offered rate in [lo, hi] at which run(rate) loses no frag:
+    hi first, then a geometric bisection (the rates span a decade).  Returns
+    (best run or None, every run as (rate, run))."""
+    tried = []
+    r = run(hi)
+    tried.append((hi, r))
+    if not lost(r):
+        return r, tried
+    best = None
+    for _ in range(steps):
+        mid = (lo * hi) ** 0.5
+        r = run(mid)
+        tried.append((mid, r))
+        if lost(r):
+            hi = mid
+        else:
+            lo, best = mid, r
+    if best is None:
+        r = run(lo)
+        tried.append((lo, r))
+        best = None if lost(r) else r
+    return best, tried
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--frags", type=int, default=1 << 22)
@@ -87,20 +112,9 @@ def main():
         print(f"stream: {s.n} frags, {time.time() - t:.1f} s", file=sys.stderr, flush=True)
         for depth in (int(x) for x in args.depths.split(",")):
             fc = run(stream, depth, 0)                       # flow-controlled: the stage's own rate
-            hi, lo, best = fc["frags_per_s"], args.lo, None
-            r = run(stream, depth, hi)
-            if not lost(r):
-                best = r
-            else:
-                for _ in range(args.steps):
-                    mid = (lo * hi) ** 0.5                    # geometric: the rates span a decade
-                    r = run(stream, depth, mid)
-                    if lost(r):
-                        hi = mid
-                    else:
-                        lo, best = mid, r
-                if best is None:
-                    best = run(stream, depth, lo)
+            best, _ = drop_free_search(lambda rate: run(stream, depth, rate), fc["frags_per_s"], args.lo, args.steps)
+            if best is None:
+                best = run(stream, depth, args.lo)
             over = run(stream, depth, 1.2 * best["offered_rate"])
             row = {"depth": depth, "tiles": args.tiles, "flow_controlled_frags_per_s": fc["frags_per_s"],
                    "drop_free_rate": best["offered_rate"], "drop_free_lost": lost(best),
