@@ -602,8 +602,8 @@ def run_tile_leg(args):
         tiles = int(os.environ.get("FD_BENCH_TILE_TILES", "3"))
         DEPTH = 16384
         # request slots for a shallow link: many small ranges
-        paced_env = {"SVC_RUN_PRELAY": "1", "SVC_RUN_REQ_DEPTH": os.environ.get("FD_BENCH_TILE_REQ_DEPTH", "64"),
-                     "SVC_RUN_SLOT_CAP": os.environ.get("FD_BENCH_TILE_SLOT_CAP", "8192")}
+        paced_env = {"SVC_RUN_PRELAY": "1", "SVC_RUN_REQ_DEPTH": os.environ.get("FD_BENCH_TILE_REQ_DEPTH", "128"),
+                     "SVC_RUN_SLOT_CAP": os.environ.get("FD_BENCH_TILE_SLOT_CAP", "2048")}
         with tempfile.TemporaryDirectory() as td:
             stream = os.path.join(td, "stream.bin")
             s = TB.make_stream(args.tile_frags, stream)

@@ -839,8 +839,11 @@ struct fd_verify_svc {
                                   gpu ns, host ns starting ingests, the largest launch */
   long     merge_idle_ns;      /* a launch on an idle GPU once the oldest request has waited this long */
   int      running;
-  /* the IO engine (k_svc_io): FD_VERIFY_SVC_IO=launch selects the per-ingest
-     and per-flush kernel launches instead */
+  /* the IO engine (k_svc_io), opt-in with FD_VERIFY_SVC_IO=io: a resident
+     kernel that polls the tiles' rings itself.  The default is the
+     per-ingest and per-flush kernel launches: post -> INGESTED 19.8 us
+     median for 64 frags against the engine's 86.9 us (profiles/r06/probe_*),
+     and the engine stalls svc_run under range traffic */
   int      io;
   ulong    io_wgs;
   u8 *     d_io;               /* job ring, descriptors, counters (HBM) */
@@ -945,7 +948,7 @@ fd_verify_svc_boot( void * seg_mem, int device, ulong batch_max, ulong inflight 
   for( ulong k = 0; k < inflight; k++ ) launch_alloc( s->L[k], device, batch_max );
   s->pend_cap = seg->tile_cnt * seg->req_depth;
   s->pend = (svc_pend *)calloc( s->pend_cap, sizeof(svc_pend) );
-  { char const * e = getenv( "FD_VERIFY_SVC_IO" ); s->io = !( e && !strcmp( e, "launch" ) ); }
+  { char const * e = getenv( "FD_VERIFY_SVC_IO" ); s->io = e && !strcmp( e, "io" ); }
   { char const * e = getenv( "FD_VERIFY_SVC_IO_WGS" ); s->io_wgs = e ? strtoul( e, 0, 0 ) : IO_WGS; }
   if( s->io_wgs < 2ul || s->io_wgs > 1024ul ) s->io_wgs = IO_WGS;
   if( s->io ) {

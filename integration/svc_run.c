@@ -33,7 +33,7 @@
 #include "fd_hip_tile_sandbox.h"
 #include "svc_run.h"
 #include <errno.h>
-#include <execinfo.h>
+#include <dlfcn.h>
 #include <signal.h>
 #include <ucontext.h>
 #include <fcntl.h>
@@ -67,12 +67,27 @@ svc_sigsys( int sig, siginfo_t * si, void * uc_ ) {
   ulong nr = (ulong)si->si_syscall;
   ulong k  = __atomic_fetch_add( &svc_hdr->svc_traps, 1UL, __ATOMIC_RELAXED );
   if( k<16UL ) svc_hdr->svc_trap_nr[ k ] = nr;
-  char m[ 64 ]; int n = snprintf( m, sizeof(m), "svc_run: seccomp trap, syscall %lu, thread %ld\n", nr, (long)syscall( SYS_gettid ) );
+  char m[ 192 ]; int n = snprintf( m, sizeof(m), "svc_run: seccomp trap, syscall %lu, thread %ld\n", nr, (long)syscall( SYS_gettid ) );
   if( n>0 ) (void)!write( 2, m, (ulong)n );
-  if( k<4UL ) {                                                 /* where it came from (backtrace() was loaded before the filter) */
-    void * bt[ 32 ];
-    int    bn = backtrace( bt, 32 );
-    backtrace_symbols_fd( bt, bn, 2 );
+  /* where from: the faulting pc and the words on the stack that fall in a
+     loaded object's code, named by dladdr (no unwinder: its first use in a
+     thread makes calls the filter refuses, and a refused call inside this
+     handler -- SIGSYS blocked -- kills the process) */
+  if( k<4UL ) {
+    ulong const * sp = (ulong const *)uc->uc_mcontext.gregs[ REG_RSP ];
+    ulong pcs[ 9 ]; ulong np = 0UL;
+    pcs[ np++ ] = (ulong)uc->uc_mcontext.gregs[ REG_RIP ];
+    for( ulong w=0UL; w<256UL && np<9UL; w++ ) {
+      Dl_info di;
+      if( sp[ w ]>4096UL && dladdr( (void *)sp[ w ], &di ) && di.dli_fname && di.dli_sname ) pcs[ np++ ] = sp[ w ];
+    }
+    for( ulong i=0UL; i<np; i++ ) {
+      Dl_info di; memset( &di, 0, sizeof(di) );
+      (void)dladdr( (void *)pcs[ i ], &di );
+      n = snprintf( m, sizeof(m), "  %s %s+0x%lx\n", di.dli_fname ? strrchr( di.dli_fname, '/' ) ? strrchr( di.dli_fname, '/' )+1 : di.dli_fname : "?",
+                    di.dli_sname ? di.dli_sname : "?", di.dli_saddr ? pcs[ i ]-(ulong)di.dli_saddr : 0UL );
+      if( n>0 ) (void)!write( 2, m, fd_ulong_min( (ulong)n, sizeof(m)-1UL ) );
+    }
   }
 }
 
@@ -124,6 +139,12 @@ main( int argc, char ** argv ) {
   }
   if( fd_verify_svc_run( svc ) ) FD_LOG_ERR(( "fd_verify_svc_run failed" ));
 
+  {                                                             /* before the sandbox: rt_sigaction is not in its filter */
+    struct sigaction sa;
+    memset( &sa, 0, sizeof(sa) );
+    sa.sa_handler = svc_sigterm;
+    if( sigaction( SIGTERM, &sa, NULL ) ) FD_LOG_ERR(( "sigaction(SIGTERM) failed" ));
+  }
   /* the GPU tile's sandbox: everything HIP needs is set up, so from here on
      the process opens nothing, starts no thread and makes only the calls of
      fd_hip_tile_seccomp_process (include/fd_hip_tile_sandbox.h) */
@@ -137,7 +158,6 @@ main( int argc, char ** argv ) {
       memset( &sa, 0, sizeof(sa) );
       sa.sa_sigaction = svc_sigsys; sa.sa_flags = SA_SIGINFO;
       if( sigaction( SIGSYS, &sa, NULL ) ) FD_LOG_ERR(( "sigaction(SIGSYS) failed" ));
-      void * bt[ 4 ]; (void)backtrace( bt, 4 );                  /* loads the unwinder now, not inside the handler */
     }
     close( 0 ); close( 1 );                                     /* the driver's stdin and stdout (/dev/null) */
     int dev[ FD_HIP_TILE_FD_MAX ];
@@ -151,12 +171,6 @@ main( int argc, char ** argv ) {
   }
   FD_COMPILER_MFENCE();
   hdr->svc_ready = 1UL;
-  {
-    struct sigaction sa;
-    memset( &sa, 0, sizeof(sa) );
-    sa.sa_handler = svc_sigterm;
-    if( sigaction( SIGTERM, &sa, NULL ) ) FD_LOG_ERR(( "sigaction(SIGTERM) failed" ));
-  }
   long deadline = fd_log_wallclock() + 1200L*1000000000L;
   /* SVC_DEBUG_S=s: the service's state on stderr every s seconds (a stalled
      run's log names where it stalled) */
@@ -177,6 +191,7 @@ main( int argc, char ** argv ) {
     char b[ 1024 ]; int n = fd_verify_svc_debug( svc, b, sizeof(b) );
     if( n>0 ) { b[ sizeof(b)-2 ] = '\0'; fprintf( stderr, "svc_run: stopped before shutdown: %s\n", b ); }
   }
+  (void)!write( 2, "svc_run: teardown\n", 18UL );
   ulong st[ 16 ];
   fd_verify_svc_stats( svc, st );
   for( ulong k=0UL; k<16UL; k++ ) hdr->svc_stats[ k ] = st[ k ];
@@ -184,6 +199,7 @@ main( int argc, char ** argv ) {
   fd_verify_svc_occupancy( svc, occ );
   for( ulong k=0UL; k<6UL; k++ ) hdr->svc_occ[ k ] = occ[ k ];
   fd_verify_svc_delete( svc );
+  (void)!write( 2, "svc_run: deleted\n", 17UL );
   FD_COMPILER_MFENCE();
   hdr->svc_done = 1UL;
   munmap( base, h.map_sz );
