@@ -31,6 +31,7 @@
    disabled. */
 
 #include <dirent.h>
+#include <errno.h>
 #include <stddef.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -141,7 +142,11 @@ fd_hip_tile_seccomp( unsigned long        out_cnt,
      clocks; the signal-mask calls and rt_sigreturn; poll / ppoll and read
      (the runtime's event waits); getpid, gettid; exit, exit_group; write to
      stderr or the logfile, fsync the logfile.
-   Not in it: open / openat, socket, connect, clone / clone3 / fork /
+   open / openat fail with EACCES rather than end the process: the HSA
+   runtime reads /proc/self/maps and std::random_device opens /dev/random
+   lazily after the sandbox is entered (measured: profiles/r06/sandbox.md)
+   and both take a failed open.
+   Not in it: socket, connect, clone / clone3 / fork /
    execve, ptrace, kill / tgkill (other processes), prctl, seccomp, mount,
    unshare -- the process cannot start a thread or program, reach a file,
    the network or another process. */
@@ -160,10 +165,11 @@ fd_hip_tile_seccomp_process( unsigned long        out_cnt,
   unsigned long const nany = sizeof(any)/sizeof(any[0]);
   unsigned long const i_fds   = 6UL;
   unsigned long const i_nr    = i_fds + fd_cnt + 1UL;
-  unsigned long const i_prot  = i_nr + 1UL + 2UL + nany + 2UL + 1UL;
+  unsigned long const i_prot  = i_nr + 1UL + 2UL + nany + 4UL + 1UL;
   unsigned long const i_write = i_prot + 4UL;
   unsigned long const i_fsync = i_write + 4UL;
-  unsigned long const i_allow = i_fsync + 3UL;
+  unsigned long const i_deny  = i_fsync + 3UL;
+  unsigned long const i_allow = i_deny + 1UL;
   unsigned long const cnt     = i_allow + 1UL;
   if( out_cnt<cnt || fd_cnt>FD_HIP_TILE_FD_MAX ) return 0UL;
   unsigned long i = 0UL;
@@ -184,6 +190,8 @@ fd_hip_tile_seccomp_process( unsigned long        out_cnt,
   for( unsigned long k=0UL; k<nany; k++ ) JUMP( BPF_JMP | BPF_JEQ | BPF_K, (unsigned int)any[ k ], TO( i_allow ), 0 );
   JUMP( BPF_JMP | BPF_JEQ | BPF_K, SYS_write, TO( i_write ), 0 );
   JUMP( BPF_JMP | BPF_JEQ | BPF_K, SYS_fsync, TO( i_fsync ), 0 );
+  JUMP( BPF_JMP | BPF_JEQ | BPF_K, SYS_open,   TO( i_deny ), 0 );
+  JUMP( BPF_JMP | BPF_JEQ | BPF_K, SYS_openat, TO( i_deny ), 0 );
   STMT( BPF_RET | BPF_K, fail_action );
   STMT( BPF_LD | BPF_W | BPF_ABS, offsetof( struct seccomp_data, args[2] ) );
   JUMP( BPF_JMP | BPF_JSET | BPF_K, PROT_EXEC, 0, 1 );
@@ -196,6 +204,7 @@ fd_hip_tile_seccomp_process( unsigned long        out_cnt,
   STMT( BPF_LD | BPF_W | BPF_ABS, offsetof( struct seccomp_data, args[0] ) );
   JUMP( BPF_JMP | BPF_JEQ | BPF_K, logfile_fd, TO( i_allow ), 0 );
   STMT( BPF_RET | BPF_K, fail_action );
+  STMT( BPF_RET | BPF_K, SECCOMP_RET_ERRNO | (EACCES & SECCOMP_RET_DATA) );
   STMT( BPF_RET | BPF_K, SECCOMP_RET_ALLOW );
 #undef JUMP
 #undef STMT

@@ -53,6 +53,7 @@ static ulong env_ulong( char const * k, ulong def ) { char const * v = getenv( k
    returns -ENOSYS to the caller, so one run lists every call the filter is
    missing */
 static svc_run_hdr_t * svc_hdr;
+static int             hdr_sandboxed;
 
 /* SIGTERM (the driver's timeout): leave the poll loop and tear the service
    down -- the IO engine stopped and drained -- rather than die with a
@@ -65,9 +66,17 @@ svc_sigsys( int sig, siginfo_t * si, void * uc_ ) {
   ucontext_t * uc = (ucontext_t *)uc_;
   uc->uc_mcontext.gregs[ REG_RAX ] = -ENOSYS;
   ulong nr = (ulong)si->si_syscall;
-  ulong k  = __atomic_fetch_add( &svc_hdr->svc_traps, 1UL, __ATOMIC_RELAXED );
-  if( k<16UL ) svc_hdr->svc_trap_nr[ k ] = nr;
-  char m[ 192 ]; int n = snprintf( m, sizeof(m), "svc_run: seccomp trap, syscall %lu, thread %ld\n", nr, (long)syscall( SYS_gettid ) );
+  static ulong traps;
+  ulong k = traps++;
+  if( svc_hdr ) {                                               /* NULL once the segment is unmapped */
+    __atomic_fetch_add( &svc_hdr->svc_traps, 1UL, __ATOMIC_RELAXED );
+    if( k<16UL ) svc_hdr->svc_trap_nr[ k ] = nr;
+  }
+  /* a path argument, when the call has one (openat, newfstatat: rsi; open, stat, access: rdi) */
+  char const * path = nr==257UL || nr==262UL ? (char const *)uc->uc_mcontext.gregs[ REG_RSI ] :
+                      nr==2UL || nr==4UL || nr==21UL ? (char const *)uc->uc_mcontext.gregs[ REG_RDI ] : NULL;
+  char m[ 192 ]; int n = snprintf( m, sizeof(m), "svc_run: seccomp trap, syscall %lu, thread %ld%s%.100s\n", nr,
+                                   (long)syscall( SYS_gettid ), path ? ", path " : "", path ? path : "" );
   if( n>0 ) (void)!write( 2, m, (ulong)n );
   /* where from: the faulting pc and the words on the stack that fall in a
      loaded object's code, named by dladdr (no unwinder: its first use in a
@@ -166,7 +175,7 @@ main( int argc, char ** argv ) {
     char why[ 160 ];
     if( fd_hip_tile_sandbox_process( -1, dev, (ulong)nd, 1, trap ? SECCOMP_RET_TRAP : SECCOMP_RET_KILL_PROCESS, why, sizeof(why) ) )
       FD_LOG_ERR(( "sandbox: %s", why ));
-    hdr->svc_sandboxed = 1UL;
+    hdr->svc_sandboxed = 1UL; hdr_sandboxed = 1;
     if( getenv( "SVC_SANDBOX_PROBE" ) ) (void)syscall( SYS_getppid );   /* refused: the process dies here */
   }
   FD_COMPILER_MFENCE();
@@ -202,6 +211,12 @@ main( int argc, char ** argv ) {
   (void)!write( 2, "svc_run: deleted\n", 17UL );
   FD_COMPILER_MFENCE();
   hdr->svc_done = 1UL;
+  svc_hdr = NULL;
   munmap( base, h.map_sz );
+  /* a sandboxed process leaves with exit_group: the HIP runtime's exit-time
+     destructors close descriptors and free what the kernel frees anyway,
+     calls the filter refuses (the GPU's work was drained by
+     fd_verify_svc_delete above) */
+  if( hdr_sandboxed ) { fflush( stderr ); _exit( 0 ); }
   return 0;
 }

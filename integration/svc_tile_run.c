@@ -384,11 +384,14 @@ produce( char const * path, char const * stream, ulong tile_cnt, ulong in_depth 
           "\"consumed\": %lu, \"consumer_bad\": %lu, \"digest_on\": %d, \"metrics_ok\": %lu, \"tile_threads_max\": %lu, \"tile_dev_fds\": %lu, "
           "\"seconds\": %.6f, \"publish_s\": %.6f, \"consumer_s\": %.6f, \"verifies_per_s\": %.1f, \"frags_per_s\": %.1f, "
           "\"offered_rate\": %lu, \"in_depth\": %lu, \"out_depth\": %lu, \"tile_cnt\": %lu, \"links\": %lu, \"prelay\": %d, "
-          "\"polled\": %d, \"req_depth\": %lu, \"slot_cap\": %lu, \"range_max\": %lu, \"stream_frags\": %lu}\n",
+          "\"polled\": %d, \"req_depth\": %lu, \"slot_cap\": %lu, \"range_max\": %lu, \"stream_frags\": %lu, \"unseen\": %lu}\n",
           frags, sigs, pub, parse, verify, dedup, bundle, ovr, lapped, host, cons_frags, cons_bad, !!getenv( "SVC_RUN_DIGEST" ), metrics_ok, threads_max,
           dev_fds, s, (double)( t_pub - t0 )*1e-9, (double)( t_last - t0 )*1e-9, (double)sigs/s, (double)frags/s, rate,
           in_depth, out_depth, tile_cnt, L, prelay, !!getenv( "SVC_RUN_POLLED" ), req_depth, slot_cap,
-          (ulong)FD_VERIFY_SVC_RANGE_MAX, n );
+          (ulong)FD_VERIFY_SVC_RANGE_MAX, n,
+          /* unseen: published frags no tile counted, processed or overrun -- a polled link's overruns
+             are the stem's own (its link metrics), so a polled run's losses show here */
+          n>frags+ovr+lapped ? n-frags-ovr-lapped : 0UL );
   fflush( stdout );
   munmap( base, map_sz );
   unlink( path );

@@ -124,7 +124,7 @@ import json
 for l in open('$O/svc_$n.jsonl'):
     d = json.loads(l)
     if 'tiles' in d and isinstance(d['tiles'], list):
-        print('svc', d['tile_cnt'], round(d['verifies_per_s']/1e6, 2), 'M v/s', round(d['frags_per_s']/1e6, 2), 'M f/s lost', d['overrun'] + d['lapped'], 'p99', d['latency']['p99_us'])
+        print('svc', d['tile_cnt'], round(d['verifies_per_s']/1e6, 2), 'M v/s', round(d['frags_per_s']/1e6, 2), 'M f/s lost', d['overrun'] + d['lapped'] + d.get('unseen', 0), 'p99', d['latency']['p99_us'])
 " ;;
     sweep)
       timeout -k 10 1100 python3 -u tools/svc_link_sweep.py --logdir $O/sweep_logs_$n $a > $O/sweep_$n.jsonl \

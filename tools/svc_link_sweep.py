@@ -34,7 +34,9 @@ import svc_bench as SB  # noqa: E402
 
 
 def lost(r):
-    return r["overrun"] + r["lapped"]
+    """frags the stage lost: overrun or lapped on a range link, or never seen by a tile (a polled
+    link's overruns are counted by the stem, not the tile: integration/svc_tile_run.c "unseen")"""
+    return r["overrun"] + r["lapped"] + r.get("unseen", 0)
 
 
 def drop_free_search(run, hi, lo, steps):
