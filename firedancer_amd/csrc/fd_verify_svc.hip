@@ -155,8 +155,9 @@ void k_svc_gather( svc_desc const * __restrict__ desc, u32 nreq, ulong n, u8 * _
     } else {
       src  = (u8 const *)d->src + FD_VERIFY_SVC_FRAG_STRIDE * i;
       sz   = ((u16 const *)d->aux0)[i];
-      kind = ((u8 const *)d->aux1)[i];
-      ok   = sz <= FD_VERIFY_SVC_FRAG_STRIDE;
+      bool const sigs = d->kind == FD_VERIFY_SVC_REQ_SIGS;   /* a client's signature records: no frag kind */
+      kind = sigs ? FD_VERIFY_HIP_IN_QUIC : ((u8 const *)d->aux1)[i];
+      ok   = sz <= FD_VERIFY_SVC_FRAG_STRIDE && ( !sigs || sz >= FD_VERIFY_SVC_SIG_HDR_SZ );
     }
     ulong const f = d->ibase + i;
     u8 * dst = ing + 64ul * SVC_INGEST_CHUNKS * f;
@@ -211,6 +212,62 @@ void k_svc_results( svc_desc const * __restrict__ desc, u32 nreq, ulong n, u16 c
   /* straight into the slot's result array in the (registered) segment: a
      wave writes 2 KB contiguous */
   ((fd_verify_svc_res_t *)desc[lo].res)[j - sbase[lo]] = r;
+}
+
+/* a signature launch (FD_VERIFY_SVC_REQ_SIGS, include/fd_verify_svc.h
+   "clients"): record j of the launch (record i of request d) from its
+   ingest frag -- signature, public key, message -- into the verify's
+   inputs: the signature and key into the launch's record arrays, the
+   message into the request slot's staging frag i (a client's slots are
+   never flushed; staging offsets fit the verify's 32-bit msg_off).  One
+   wave per record, grid-stride. */
+__global__ __launch_bounds__(256)
+void k_svc_sigrec( svc_desc const * __restrict__ desc, u32 nreq, ulong n, u8 const * __restrict__ ing,
+                   u16 const * __restrict__ ing_sz, u8 * __restrict__ stage, u8 * __restrict__ rsig,
+                   u8 * __restrict__ rpub, u32 * __restrict__ rmoff, u32 * __restrict__ rmsz ) {
+  __shared__ u64 sbase[SVC_REQ_MAX];
+  for( u32 i = threadIdx.x; i < nreq; i += blockDim.x ) sbase[i] = desc[i].base;
+  __syncthreads();
+  u32 const lane = threadIdx.x & 63u;
+  for( ulong j = (ulong)blockIdx.x * 4ul + (threadIdx.x >> 6); j < n; j += 4ul * gridDim.x ) {
+    u32 lo = 0u, hi = nreq;
+    while( hi - lo > 1u ) { u32 mid = (lo + hi) >> 1; if( sbase[mid] <= j ) lo = mid; else hi = mid; }
+    svc_desc const * d = desc + lo;
+    ulong const i = j - d->base, f = d->ibase + i;
+    u32 const sz = ing_sz[f];
+    bool const ok = sz != 0xffffu;                             /* the gather checked 96 <= sz <= the stride */
+    u32 const msz = ok ? sz - (u32)FD_VERIFY_SVC_SIG_HDR_SZ : 0u;
+    u8 const * src = ing + 64ul * SVC_INGEST_CHUNKS * f;
+    ulong const moff = 64ul * (d->stage0 + FD_TXN_HIP_STAGE_CHUNKS * i);
+    if( lane < 4u )      *(uint4 *)(rsig + 64ul * j + 16u * lane) = ok ? *(uint4 const *)(src + 16u * lane) : make_uint4( 0u, 0u, 0u, 0u );
+    else if( lane < 6u ) *(uint4 *)(rpub + 32ul * j + 16u * (lane - 4u)) = ok ? *(uint4 const *)(src + 16u * lane) : make_uint4( 0u, 0u, 0u, 0u );
+    /* the message: 16-B pieces from ingest byte 96 on (both 16-B aligned) */
+    for( u32 p = 16u * lane; p < msz; p += 1024u )
+      *(uint4 *)(stage + moff + p) = *(uint4 const *)(src + FD_VERIFY_SVC_SIG_HDR_SZ + p);
+    if( lane == 0u ) { rmoff[j] = (u32)moff; rmsz[j] = msz; }
+  }
+}
+
+/* a signature launch's results into the requests' result arrays */
+__global__ __launch_bounds__(256)
+void k_svc_sigres( svc_desc const * __restrict__ desc, u32 nreq, ulong n, u16 const * __restrict__ ing_sz,
+                   signed char const * __restrict__ rcode ) {
+  __shared__ u64 sbase[SVC_REQ_MAX];
+  for( u32 i = threadIdx.x; i < nreq; i += blockDim.x ) sbase[i] = desc[i].base;
+  __syncthreads();
+  ulong const j = (ulong)blockIdx.x * blockDim.x + threadIdx.x;
+  if( j >= n ) return;
+  u32 lo = 0u, hi = nreq;
+  while( hi - lo > 1u ) { u32 mid = (lo + hi) >> 1; if( sbase[mid] <= j ) lo = mid; else hi = mid; }
+  svc_desc const * d = desc + lo;
+  u32 const sz = ing_sz[d->ibase + (j - sbase[lo])];
+  bool const ok = sz != 0xffffu;
+  fd_verify_svc_res_t r;
+  r.tag = 0ul; r.bundle_id = 0ul; r.txn_t_sz = 0u; r.payload_sz = ok ? (u16)(sz - FD_VERIFY_SVC_SIG_HDR_SZ) : (u16)0;
+  r.code = ok ? rcode[j] : (signed char)-1;                     /* FD_ED25519_ERR_SIG */
+  r.flags = ok ? (u8)0 : (u8)FD_VERIFY_SVC_RES_BAD;
+  r.sig_cnt = ok ? (u8)1 : (u8)0; r.rsv0 = 0u; r.tsorig = 0u; r.rsv1 = 0u;
+  ((fd_verify_svc_res_t *)d->res)[j - sbase[lo]] = r;
 }
 
 /* a flush: out entry e's staging frag (its realized bytes, in whole 64-B
@@ -771,6 +828,7 @@ void k_svc_io( svc_io_cfg C ) {
 
 struct svc_launch {
   int                    busy;
+  int                    sig;            /* a signature launch (FD_VERIFY_SVC_REQ_SIGS requests) */
   fd_ed25519_hip_ctx_t * ctx;
   hipStream_t            st;
   hipEvent_t             ev0, ev1;
@@ -784,6 +842,7 @@ struct svc_launch {
 
 struct svc_tile {
   int          set;
+  int          client;         /* FD_VERIFY_SVC_REQ_SIGS only, no out dcache (fd_verify_svc_set_client) */
   u8 *         h_out;          /* the out dcache (host) */
   ulong        out_sz;
   u8 const *   chunk_base;     /* host address of out chunk 0 */
@@ -831,6 +890,8 @@ struct fd_verify_svc {
   svc_desc * sdesc;            /* per (tile, slot): the request's descriptor, made at ingest */
   svc_launch L[SVC_LAUNCH_MAX];
   svc_pend * pend; ulong pend_cap, pend_head, pend_tail, pend_frags;
+  svc_pend * spend; ulong spend_head, spend_tail;   /* ingested signature requests (clients), their own queue:
+                                                       they ride signature launches, not the merge of txn frags */
   ulong    occ[6];             /* every 64th poll with a slot in use: samples, then the summed slot counts posted (not yet
                                   ingested), ingested and waiting for a launch, in a launch, results (the
                                   tile's ordered pass, flushes, publish), free */
@@ -948,6 +1009,7 @@ fd_verify_svc_boot( void * seg_mem, int device, ulong batch_max, ulong inflight 
   for( ulong k = 0; k < inflight; k++ ) launch_alloc( s->L[k], device, batch_max );
   s->pend_cap = seg->tile_cnt * seg->req_depth;
   s->pend = (svc_pend *)calloc( s->pend_cap, sizeof(svc_pend) );
+  s->spend = (svc_pend *)calloc( s->pend_cap, sizeof(svc_pend) );
   { char const * e = getenv( "FD_VERIFY_SVC_IO" ); s->io = e && !strcmp( e, "io" ); }
   { char const * e = getenv( "FD_VERIFY_SVC_IO_WGS" ); s->io_wgs = e ? strtoul( e, 0, 0 ) : IO_WGS; }
   if( s->io_wgs < 2ul || s->io_wgs > 1024ul ) s->io_wgs = IO_WGS;
@@ -1024,6 +1086,15 @@ fd_verify_svc_set_tile( fd_verify_svc_t * s, ulong t, void * out_dcache, ulong o
   return 0;
 }
 
+extern "C" int
+fd_verify_svc_set_client( fd_verify_svc_t * s, ulong t ) {
+  if( !s || t >= s->seg->tile_cnt || s->tile[t].set ) return -1;
+  (void)svc_dev( s, fd_verify_svc_tile( s->seg, t ), s->seg->tile_sz );   /* the client's part of the segment is mapped */
+  s->tile[t].client = 1;
+  s->tile[t].set    = 1;
+  return 0;
+}
+
 extern "C" void
 fd_verify_svc_set_merge( fd_verify_svc_t * s, ulong min_frags, ulong wait_ns, ulong idle_ns ) {
   s->merge_min = min_frags; s->merge_wait_ns = (long)wait_ns; s->merge_idle_ns = (long)idle_ns;
@@ -1032,7 +1103,30 @@ fd_verify_svc_set_merge( fd_verify_svc_t * s, ulong min_frags, ulong wait_ns, ul
 extern "C" int
 fd_verify_svc_run( fd_verify_svc_t * s ) {
   for( ulong t = 0; t < s->seg->tile_cnt; t++ ) if( !s->tile[t].set ) return -1;
+  for( ulong t = 0; t < s->seg->tile_cnt && s->io; t++ )
+    if( s->tile[t].client ) {
+      fprintf( stderr, "fd_verify_svc: tile %lu is a client: the IO engine (FD_VERIFY_SVC_IO=io) serves verify tiles only\n", t );
+      return -1;
+    }
   svc_device( s->dev );
+  /* the signature path (k_svc_sigrec, the verify's latency and bulk
+     kernels, k_svc_sigres) once on zeroed records: its code objects load
+     here, before the GPU tile's sandbox */
+  for( ulong k = 0; k < s->inflight; k++ ) {
+    svc_launch & L = s->L[k];
+    SV_CHECK( hipMemsetAsync( L.d_rsig, 0, 64ul * 256ul, L.st ) ); SV_CHECK( hipMemsetAsync( L.d_rpub, 0, 32ul * 256ul, L.st ) );
+    SV_CHECK( hipMemsetAsync( L.d_rmoff, 0, 4ul * 256ul, L.st ) ); SV_CHECK( hipMemsetAsync( L.d_rmsz, 0, 4ul * 256ul, L.st ) );
+    hipLaunchKernelGGL( k_svc_sigrec, dim3( 1 ), dim3( 256 ), 0, L.st, L.d_desc, 0u, 0ul, (u8 const *)s->d_ing,
+                        (u16 const *)s->d_ing_sz, s->d_stage, L.d_rsig, L.d_rpub, L.d_rmoff, L.d_rmsz );
+    hipLaunchKernelGGL( k_svc_sigres, dim3( 1 ), dim3( 256 ), 0, L.st, L.d_desc, 0u, 0ul, (u16 const *)s->d_ing_sz,
+                        (signed char const *)L.d_rcode );
+    SV_CHECK( hipGetLastError() );
+    if( fd_ed25519_hip_verify_dev( L.ctx, 1ul, L.d_rsig, L.d_rpub, s->d_stage, L.d_rmoff, L.d_rmsz, L.d_rcode, 0, L.st ) ||
+        fd_ed25519_hip_verify_dev( L.ctx, 256ul, L.d_rsig, L.d_rpub, s->d_stage, L.d_rmoff, L.d_rmsz, L.d_rcode, 0, L.st ) ) {
+      fprintf( stderr, "fd_verify_svc: signature path warm-up failed\n" );
+      return -1;
+    }
+  }
   /* the kernels' code objects loaded and every buffer touched once before
      the first request (the steady state loads nothing) */
   for( ulong k = 0; k < s->inflight; k++ ) {
@@ -1047,6 +1141,7 @@ fd_verify_svc_run( fd_verify_svc_t * s ) {
                       s->d_ing_kind, s->d_ing_tso, s->d_stage );
   SV_CHECK( hipGetLastError() );
   for( ulong t = 0; t < s->seg->tile_cnt && !s->io; t++ ) {
+    if( s->tile[t].client ) continue;
     hipLaunchKernelGGL( k_svc_compact, dim3( 1 ), dim3( 256 ), 0, s->tile[t].st, (fd_verify_svc_out_t const *)0, 0ul,
                         (u8 const *)s->d_stage, 0ul, s->tile[t].d_out, 0L, 0ul, s->seg->slot_cap, s->tile[t].d_err );
     SV_CHECK( hipGetLastError() );
@@ -1107,6 +1202,12 @@ svc_desc_of( fd_verify_svc_t * s, ulong t, ulong slot, ulong base, svc_desc & d 
   memset( &d, 0, sizeof(d) );
   d.base = base; d.n = r->n; d.kind = r->kind; d.seed = r->seed; d.stage0 = svc_stage0( s, t, slot );
   d.ibase = (t * g->req_depth + slot) * g->slot_cap;
+  if( s->tile[t].client != ( r->kind == FD_VERIFY_SVC_REQ_SIGS ) ) {
+    /* a client posts signature records only, a verify tile never does */
+    fprintf( stderr, "fd_verify_svc: tile %lu slot %lu: request kind %lu from a %s\n", t, slot, r->kind,
+             s->tile[t].client ? "client" : "verify tile" );
+    abort();
+  }
   if( r->kind == FD_VERIFY_SVC_REQ_RANGE ) {
     if( r->link >= FD_VERIFY_SVC_LINK_MAX || !s->link[r->link].set || !r->rr_cnt || r->rr_idx >= r->rr_cnt ||
         r->seq_cnt > s->link[r->link].depth ||
@@ -1118,7 +1219,7 @@ svc_desc_of( fd_verify_svc_t * s, ulong t, ulong slot, ulong base, svc_desc & d 
     d.src = (u64)s->link[r->link].d_mcache; d.aux0 = (u64)s->link[r->link].d_base;
     d.first = fd_verify_svc_range_first( r->seq0, r->rr_cnt, r->rr_idx ); d.stride = r->rr_cnt;
     d.line_mask = s->link[r->link].depth - 1ul; d.chunk0 = s->link[r->link].chunk0; d.wmark = s->link[r->link].wmark;
-  } else if( r->kind == FD_VERIFY_SVC_REQ_FRAGS ) {
+  } else if( r->kind == FD_VERIFY_SVC_REQ_FRAGS || r->kind == FD_VERIFY_SVC_REQ_SIGS ) {
     if( r->n > g->frag_cap ) {
       fprintf( stderr, "fd_verify_svc: tile %lu slot %lu: %lu frags over the frag area's %lu\n", t, slot, r->n, g->frag_cap );
       abort();
@@ -1148,7 +1249,7 @@ svc_launch_start( fd_verify_svc_t * s, svc_launch & L ) {
     L.nreq++; n += p.n;
     s->pend_frags -= p.n; s->pend_head++;
   }
-  L.n = n; L.busy = 1;
+  L.n = n; L.busy = 1; L.sig = 0;
   svc_device( s->dev );
   SV_CHECK( hipEventRecord( L.ev0, L.st ) );
   hipLaunchKernelGGL( k_svc_assemble, dim3( (unsigned)((n + 255ul) / 256ul) ), dim3( 256 ), 0, L.st, L.d_desc, (u32)L.nreq,
@@ -1164,6 +1265,43 @@ svc_launch_start( fd_verify_svc_t * s, svc_launch & L ) {
   SV_CHECK( hipEventRecord( L.ev1, L.st ) );
   s->stat[0]++; s->stat[1] += n; s->stat[2] += L.nreq;
   if( n > s->stat[15] ) s->stat[15] = n;
+}
+
+/* a signature launch over ingested client requests: records -> the
+   verify's inputs (k_svc_sigrec), fd_ed25519_verify per record on the
+   launch's context, codes -> the slots' result arrays (k_svc_sigres) */
+static void
+svc_sig_launch_start( fd_verify_svc_t * s, svc_launch & L ) {
+  fd_verify_svc_seg_t * g = s->seg;
+  ulong n = 0;
+  L.nreq = 0;
+  while( s->spend_head != s->spend_tail && L.nreq < SVC_REQ_MAX ) {
+    svc_pend const & p = s->spend[s->spend_head % s->pend_cap];
+    if( n + p.n > s->batch_max ) break;
+    L.h_desc[L.nreq] = s->sdesc[p.t * g->req_depth + p.slot];
+    L.h_desc[L.nreq].base = n;
+    L.h_desc[L.nreq].res  = (u64)svc_dev( s, fd_verify_svc_res( g, p.t, p.slot ), sizeof(fd_verify_svc_res_t) * p.n );
+    L.req[L.nreq].t = p.t; L.req[L.nreq].slot = p.slot;
+    L.nreq++; n += p.n;
+    s->spend_head++;
+  }
+  L.n = n; L.busy = 1; L.sig = 1;
+  svc_device( s->dev );
+  SV_CHECK( hipEventRecord( L.ev0, L.st ) );
+  ulong wgs = (n + 3ul) / 4ul;
+  if( wgs > 2048ul ) wgs = 2048ul;
+  hipLaunchKernelGGL( k_svc_sigrec, dim3( (unsigned)wgs ), dim3( 256 ), 0, L.st, L.d_desc, (u32)L.nreq, n,
+                      (u8 const *)s->d_ing, (u16 const *)s->d_ing_sz, s->d_stage, L.d_rsig, L.d_rpub, L.d_rmoff, L.d_rmsz );
+  SV_CHECK( hipGetLastError() );
+  if( fd_ed25519_hip_verify_dev( L.ctx, n, L.d_rsig, L.d_rpub, s->d_stage, L.d_rmoff, L.d_rmsz, L.d_rcode, 0, L.st ) ) {
+    fprintf( stderr, "fd_verify_svc: signature launch of %lu records failed\n", n );
+    abort();
+  }
+  hipLaunchKernelGGL( k_svc_sigres, dim3( (unsigned)((n + 255ul) / 256ul) ), dim3( 256 ), 0, L.st, L.d_desc, (u32)L.nreq, n,
+                      (u16 const *)s->d_ing_sz, (signed char const *)L.d_rcode );
+  SV_CHECK( hipGetLastError() );
+  SV_CHECK( hipEventRecord( L.ev1, L.st ) );
+  s->stat[0]++; s->stat[1] += n; s->stat[2] += L.nreq;
 }
 
 /* the gather of the newly posted requests in I (their frags into the slots'
@@ -1316,6 +1454,12 @@ fd_verify_svc_poll( fd_verify_svc_t * s ) {
     s->stat[13] += (ulong)((double)ms * 1e6);
     for( ulong r = 0; r < I.nreq; r++ ) {
       fd_verify_svc_st( &fd_verify_svc_req( g, I.req[r].t, I.req[r].slot )->state, FD_VERIFY_SVC_INGESTED );
+      if( I.h_desc[r].kind == FD_VERIFY_SVC_REQ_SIGS ) {
+        svc_pend & p = s->spend[s->spend_tail % s->pend_cap];
+        p.t = I.req[r].t; p.slot = I.req[r].slot; p.n = I.h_desc[r].n; p.seen = now0;
+        s->spend_tail++;
+        continue;
+      }
       svc_pend & p = s->pend[s->pend_tail % s->pend_cap];
       p.t = I.req[r].t; p.slot = I.req[r].slot; p.n = I.h_desc[r].n; p.seen = now0;
       s->pend_tail++; s->pend_frags += p.n;
@@ -1325,6 +1469,7 @@ fd_verify_svc_poll( fd_verify_svc_t * s ) {
   /* 2. flushes: retire in order, start the newly posted */
   for( ulong t = 0; t < g->tile_cnt && !s->io; t++ ) {
     svc_tile & T = s->tile[t];
+    if( T.client ) continue;
     fd_verify_svc_tile_t * b = fd_verify_svc_tile( g, t );
     while( T.flush_fin < T.flush_take ) {
       hipError_t e = hipEventQuery( T.ev[T.flush_fin % SVC_FLUSH_Q] );
@@ -1344,6 +1489,10 @@ fd_verify_svc_poll( fd_verify_svc_t * s ) {
     svc_tile & T = s->tile[t];
     fd_verify_svc_tile_t * b = fd_verify_svc_tile( g, t );
     ulong post = fd_verify_svc_ld( &b->flush_post );
+    if( T.client ) {
+      if( post ) { fprintf( stderr, "fd_verify_svc: tile %lu is a client and posted a flush\n", t ); abort(); }
+      continue;
+    }
     while( T.flush_take < post && T.flush_take - T.flush_fin < SVC_FLUSH_Q ) {
       svc_flush_start( s, t, &b->flush[T.flush_take % FD_VERIFY_SVC_FLUSH_DEPTH] );
       T.flush_take++; did = 1;
@@ -1388,6 +1537,18 @@ fd_verify_svc_poll( fd_verify_svc_t * s ) {
      large launches while the GPU is busy (a 55 K-signature launch runs ~one
      wave per SIMD and costs 3x per signature), little added
      latency while it is not */
+  /* 4a. signature requests (clients: a FEC set's root, a replay batch)
+     launch as soon as a launch slot is free: they are few and wait on
+     their caller, so no merge target */
+  while( s->spend_head != s->spend_tail && busy < s->inflight ) {
+    ulong k = 0;
+    while( s->L[k].busy ) k++;
+    long const l0 = svc_now_ns();
+    s->launch_t0[k] = l0;
+    svc_sig_launch_start( s, s->L[k] );
+    s->stat[8] += (ulong)(svc_now_ns() - l0);
+    busy++; did = 1;
+  }
   while( s->pend_head != s->pend_tail && busy < s->inflight ) {
     long waited = now - s->pend[s->pend_head % s->pend_cap].seen;
     bool ready = s->pend_frags >= s->merge_min || waited >= s->merge_wait_ns || ( !busy && waited >= s->merge_idle_ns );
@@ -1495,18 +1656,18 @@ fd_verify_svc_delete( fd_verify_svc_t * s ) {
   }
   for( ulong k = 0; k < s->inflight; k++ ) if( s->L[k].ctx ) svc_drain( s->L[k].st, 0, "verify launch stream", k, s );
   for( ulong t = 0; t < FD_VERIFY_SVC_TILE_MAX && !s->io; t++ )
-    if( s->tile[t].set ) svc_drain( s->tile[t].st, 0, "flush stream of tile", t, s );
+    if( s->tile[t].set && !s->tile[t].client ) svc_drain( s->tile[t].st, 0, "flush stream of tile", t, s );
   if( s->st_ing && !s->io ) svc_drain( s->st_ing, 0, "ingest stream", 0ul, s );
   (void)hipDeviceSynchronize();
   for( ulong k = 0; k < SVC_LAUNCH_MAX; k++ ) launch_free( s->L[k] );
   for( ulong t = 0; t < FD_VERIFY_SVC_TILE_MAX; t++ ) {
     svc_tile & T = s->tile[t];
     if( !T.set ) continue;
-    if( !s->io ) {
+    if( !s->io && !T.client ) {
       (void)hipStreamDestroy( T.st );
       for( ulong k = 0; k < SVC_FLUSH_Q; k++ ) (void)hipEventDestroy( T.ev[k] );
     }
-    (void)hipHostFree( T.h_err );
+    if( T.h_err ) (void)hipHostFree( T.h_err );
   }
   if( s->io ) {
     (void)hipFree( s->d_io ); (void)hipHostFree( s->h_ctl ); (void)hipHostFree( s->h_vd ); (void)hipEventDestroy( s->io_ev );
@@ -1522,6 +1683,6 @@ fd_verify_svc_delete( fd_verify_svc_t * s ) {
   free( s->sdesc );
   for( ulong k = 0; k < s->nreg; k++ ) (void)hipHostUnregister( s->reg[k].h );
   fd_verify_svc_st( &s->seg->svc_state, FD_VERIFY_SVC_SVC_STOPPED );
-  free( s->pend );
+  free( s->pend ); free( s->spend );
   free( s );
 }

@@ -86,7 +86,7 @@ typedef unsigned int   uint;
 typedef unsigned long  ulong;
 
 #define FD_VERIFY_SVC_MAGIC        (0xfd7e51f5e1c0de02UL)
-#define FD_VERIFY_SVC_TILE_MAX     (16UL)
+#define FD_VERIFY_SVC_TILE_MAX     (32UL)      /* verify tiles and clients per GPU */
 #define FD_VERIFY_SVC_LINK_MAX     (16UL)
 #define FD_VERIFY_SVC_FLUSH_DEPTH  (256UL)     /* flush ring entries per tile (power of 2) */
 #define FD_VERIFY_SVC_FRAG_STRIDE  (2048UL)    /* a polled frag's bytes in the frag area: <= 2048 (gossip, fd_verify_tile.c:89) */
@@ -95,6 +95,10 @@ typedef unsigned long  ulong;
 /* request kinds */
 #define FD_VERIFY_SVC_REQ_RANGE    (1UL)   /* seq range of an unpolled quic_verify link (range mode) */
 #define FD_VERIFY_SVC_REQ_FRAGS    (2UL)   /* frags the tile copied into the slot's frag area (polled links) */
+#define FD_VERIFY_SVC_REQ_SIGS     (3UL)   /* signature records a client wrote into the slot's frag area: one
+                                              fd_ed25519_verify each (the shred tile's FEC-set roots,
+                                              fd_fec_resolver.c:476; the replay tile's transactions,
+                                              fd_executor.c:1607-1623); see "clients" below */
 
 /* slot states */
 #define FD_VERIFY_SVC_FREE         (0UL)
@@ -339,6 +343,118 @@ fd_verify_svc_post_flush( fd_verify_svc_seg_t * s, ulong t, ulong slot, ulong lo
   return 0;
 }
 
+/* ---- clients ----------------------------------------------------------------
+
+   A client is a segment tile that posts FD_VERIFY_SVC_REQ_SIGS requests
+   only: the shred tile (FEC-set roots) and the replay tile (its block's
+   transaction signatures) stay single-threaded and without a device fd,
+   as the verify tiles do, and their verifies ride the GPU tile's launches
+   (fd_verify_svc_set_client on the service side; a client has no out
+   dcache and posts no flush).  Record i of a request is frag i of the
+   slot's frag area: the signature (64 B), the public key (32 B), then the
+   message; frag_sz[ i ] = 96 + the message's size.  The service writes
+   res[ i ].code = fd_ed25519_verify( msg, msg_sz, sig, pub ) (FD_ED25519_*
+   in the service contexts' error mode), sig_cnt 1 and payload_sz the
+   message size; a record shorter than 96 B or over the frag stride gets
+   FD_VERIFY_SVC_RES_BAD and code FD_ED25519_ERR_SIG.  The slot goes from
+   POSTED to RESULTS; the client reads the codes and stores FREE.
+
+   fd_verify_svc_client_t keeps one client's request ring: records are
+   added into the open request (the next slot, when FREE), a request is
+   posted when full or on flush, and poll hands every finished record's
+   code back with the caller's 32-bit tag (kept in the slot's out array,
+   which a client does not otherwise use), oldest request first.  No
+   syscall, no allocation: it runs inside the reference's seccomp
+   policies. */
+
+#define FD_VERIFY_SVC_SIG_HDR_SZ   (96UL)
+#define FD_VERIFY_SVC_SIG_MSG_MAX  (FD_VERIFY_SVC_FRAG_STRIDE - FD_VERIFY_SVC_SIG_HDR_SZ)
+
+typedef struct {
+  fd_verify_svc_seg_t * seg;
+  ulong t;                 /* the client's tile index in the segment */
+  ulong id_post;           /* next request id to post (the open request, if open_n) */
+  ulong id_done;           /* oldest posted request not yet collected */
+  ulong open_n;            /* records in the open request */
+  ulong recs_posted, recs_done, reqs_posted;
+} fd_verify_svc_client_t;
+
+static inline fd_verify_svc_client_t *
+fd_verify_svc_client_join( fd_verify_svc_client_t * c, fd_verify_svc_seg_t * seg, ulong t ) {
+  if( !c || !seg || t>=seg->tile_cnt || !seg->frag_cap ) return (fd_verify_svc_client_t *)0;
+  c->seg = seg; c->t = t; c->id_post = 0UL; c->id_done = 0UL; c->open_n = 0UL;
+  c->recs_posted = 0UL; c->recs_done = 0UL; c->reqs_posted = 0UL;
+  return c;
+}
+
+/* requests posted and not yet collected */
+static inline ulong fd_verify_svc_client_busy( fd_verify_svc_client_t const * c ) { return c->id_post - c->id_done; }
+
+/* post the open request (nothing if it is empty); 0, or -1 on a protocol error */
+static inline int
+fd_verify_svc_client_flush( fd_verify_svc_client_t * c, long now ) {
+  if( !c->open_n ) return 0;
+  fd_verify_svc_seg_t * s = c->seg;
+  fd_verify_svc_req_t * r = fd_verify_svc_req( s, c->t, c->id_post & ( s->req_depth-1UL ) );
+  r->kind = FD_VERIFY_SVC_REQ_SIGS; r->link = 0UL; r->seq0 = 0UL; r->seq_cnt = 0UL; r->rr_cnt = 1UL; r->rr_idx = 0UL;
+  r->n = c->open_n; r->seed = 0UL; r->id = c->id_post; r->t_post = now; r->sig_cnt = 0UL; r->batch_frags = 0UL;
+  fd_verify_svc_st( &r->state, FD_VERIFY_SVC_POSTED );
+  c->recs_posted += c->open_n; c->reqs_posted++;
+  c->id_post++; c->open_n = 0UL;
+  return 0;
+}
+
+/* add one record (tag: the caller's, handed back by poll).  Returns 1 if
+   added, 0 if no slot is free (poll, then retry), -1 if msg_sz is over
+   FD_VERIFY_SVC_SIG_MSG_MAX.  A full request is posted at once. */
+static inline int
+fd_verify_svc_client_add( fd_verify_svc_client_t * c, uchar const * sig, uchar const * pub, uchar const * msg,
+                          ulong msg_sz, uint tag, long now ) {
+  if( msg_sz>FD_VERIFY_SVC_SIG_MSG_MAX ) return -1;
+  fd_verify_svc_seg_t * s = c->seg;
+  ulong slot = c->id_post & ( s->req_depth-1UL );
+  if( !c->open_n ) {                                            /* opening a request: its slot must be free */
+    if( c->id_post - c->id_done>=s->req_depth ||
+        fd_verify_svc_ld( &fd_verify_svc_req( s, c->t, slot )->state )!=FD_VERIFY_SVC_FREE ) return 0;
+  }
+  ulong i = c->open_n;
+  uchar * f = fd_verify_svc_frag( s, c->t, slot ) + i*FD_VERIFY_SVC_FRAG_STRIDE;
+  for( ulong k=0UL; k<64UL; k++ ) f[ k ] = sig[ k ];
+  for( ulong k=0UL; k<32UL; k++ ) f[ 64UL+k ] = pub[ k ];
+  for( ulong k=0UL; k<msg_sz; k++ ) f[ 96UL+k ] = msg[ k ];
+  fd_verify_svc_frag_sz  ( s, c->t, slot )[ i ] = (ushort)( FD_VERIFY_SVC_SIG_HDR_SZ + msg_sz );
+  fd_verify_svc_frag_kind( s, c->t, slot )[ i ] = 0;
+  fd_verify_svc_out( s, c->t, slot )[ i ].idx = tag;
+  c->open_n = i+1UL;
+  if( c->open_n==s->frag_cap ) (void)fd_verify_svc_client_flush( c, now );
+  return 1;
+}
+
+/* collect finished requests, oldest first: cb( ctx, tag, code ) per record
+   (code FD_ED25519_*, or FD_ED25519_ERR_SIG for a record the service
+   found malformed); stops at the first request still on the GPU.  Returns
+   the records collected. */
+typedef void (*fd_verify_svc_client_cb_t)( void * ctx, uint tag, int code );
+
+static inline ulong
+fd_verify_svc_client_poll( fd_verify_svc_client_t * c, fd_verify_svc_client_cb_t cb, void * ctx ) {
+  fd_verify_svc_seg_t * s = c->seg;
+  ulong got = 0UL;
+  while( c->id_done!=c->id_post ) {
+    ulong slot = c->id_done & ( s->req_depth-1UL );
+    fd_verify_svc_req_t * r = fd_verify_svc_req( s, c->t, slot );
+    if( fd_verify_svc_ld( &r->state )!=FD_VERIFY_SVC_RESULTS ) break;
+    fd_verify_svc_res_t const * res = fd_verify_svc_res( s, c->t, slot );
+    fd_verify_svc_out_t const * out = fd_verify_svc_out( s, c->t, slot );
+    ulong n = r->n;
+    for( ulong i=0UL; i<n; i++ ) cb( ctx, out[ i ].idx, ( res[ i ].flags & FD_VERIFY_SVC_RES_BAD ) ? -1 : (int)res[ i ].code );
+    fd_verify_svc_st( &r->state, FD_VERIFY_SVC_FREE );
+    c->id_done++; got += n;
+  }
+  c->recs_done += got;
+  return got;
+}
+
 /* ---- sizing ----------------------------------------------------------------
 
    The service keeps every slot's out frags in HBM staging, tile_cnt x
@@ -428,6 +544,8 @@ static inline ulong fd_verify_svc_tiles_on( ulong gpu, ulong verify_cnt, ulong g
      _wmark).
    fd_verify_svc_set_tile( svc, t, out_dcache, out_dcache_sz, out_chunk_base ):
      tile t's verify_dedup dcache (flush target) and its chunk base.
+   fd_verify_svc_set_client( svc, t ): tile t is a client (see "clients");
+     every tile of the segment is set one way or the other before run.
    fd_verify_svc_run( svc ): marks the service running; then
    fd_verify_svc_poll( svc ): one iteration of the service loop (retire
      finished launches, ingests and flushes, start flushes, copy newly
@@ -453,6 +571,10 @@ int               fd_verify_svc_set_link( fd_verify_svc_t * svc, ulong link, voi
                                           void const * chunk_base, ulong chunk0, ulong wmark );
 int               fd_verify_svc_set_tile( fd_verify_svc_t * svc, ulong t, void * out_dcache, ulong out_dcache_sz,
                                           void const * out_chunk_base );
+/* tile t is a client (FD_VERIFY_SVC_REQ_SIGS requests only, no out dcache:
+   a flush or a verify-tile request from it ends the service).  -1 on bad
+   arguments or a tile already set. */
+int               fd_verify_svc_set_client( fd_verify_svc_t * svc, ulong t );
 void              fd_verify_svc_set_merge( fd_verify_svc_t * svc, ulong min_frags, ulong wait_ns, ulong idle_ns );
 int               fd_verify_svc_run     ( fd_verify_svc_t * svc );
 int               fd_verify_svc_poll    ( fd_verify_svc_t * svc );

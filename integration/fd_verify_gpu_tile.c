@@ -154,6 +154,15 @@ privileged_init( fd_topo_t * topo, fd_topo_tile_t * tile ) {
                                              fd_dcache_data_sz( out->dcache ), topo->workspaces[ dw ].wksp ) ) )
       FD_LOG_ERR(( "verify tile %lu: fd_verify_svc_set_tile failed", v->kind_id ));
   }
+  /* GPU 0's clients (the shred tiles' FEC-set roots, the replay tile's
+     block sigverify; include/fd_verify_svc.h "clients"): segment tiles
+     [verify_svc.client_base, +verify_svc.client_cnt), after its verify tiles */
+  if( gpu==0UL ) {
+    ulong cb = fd_pod_query_ulong( topo->props, "verify_svc.client_base", 0UL );
+    ulong cc = fd_pod_query_ulong( topo->props, "verify_svc.client_cnt",  0UL );
+    for( ulong c=0UL; c<cc; c++ )
+      if( FD_UNLIKELY( fd_verify_svc_set_client( ctx->svc, cb+c ) ) ) FD_LOG_ERR(( "client tile %lu: fd_verify_svc_set_client failed", cb+c ));
+  }
   if( FD_UNLIKELY( fd_verify_svc_run( ctx->svc ) ) ) FD_LOG_ERR(( "fd_verify_svc_run failed (a verify tile not set?)" ));
 }
 

@@ -27,7 +27,17 @@
    The FD_HAS_HIP build also checks every root the GPU verified against the
    reference's own fd_ed25519_verify on the same three inputs (codes must be
    equal), and reports the resolver's table hits (add_shred took the GPU's
-   code) and core verifies. */
+   code) and core verifies.
+
+     _build/fec_run_svc   FD_HAS_HIP_SVC: no HIP in the process; the resolver
+                          is a client of the GPU tile's service
+                          (fd_fec_resolver_hip_attach_svc, integration/svc_client.h:
+                          SVC_CLIENT_SHM names the run, svc_tile_run host or
+                          produce with SVC_RUN_CLIENTS); the same checks, the
+                          codes compared by verdict (the service's contexts
+                          give the AVX-512 build's error codes, this
+                          process's reference verify the portable build's),
+                          and the process's threads and device fds. */
 
 #include "../../util/fd_util.h"
 #include "../../ballet/shred/fd_shred.h"
@@ -37,6 +47,9 @@
 #include FEC_SRC
 #include <stdio.h>
 #include <stdlib.h>
+#if FD_HAS_HIP_SVC
+#include "svc_client.h"
+#endif
 
 #if defined(fd_boot)
 void fd_boot( int * pargc, char *** pargv ) { (void)pargc; (void)pargv; }
@@ -153,6 +166,13 @@ main( int argc, char ** argv ) {
   FD_TEST( !fd_fec_resolver_hip_attach( r, hip ) );
   FD_TEST( window<=FD_FEC_RESOLVER_HIP_BATCH_MAX );               /* one launch per window: its roots are checked below */
   ulong checked = 0UL, code_bad = 0UL;
+#elif FD_HAS_HIP_SVC
+  ulong svc_t;
+  fd_verify_svc_seg_t * svc_seg = svc_client_attach( &svc_t );
+  void * svc_mem = aligned_alloc( 128UL, fd_ulong_align_up( fd_fec_resolver_hip_svc_footprint(), 128UL ) );
+  FD_TEST( svc_mem && !fd_fec_resolver_hip_attach_svc( r, svc_seg, svc_t, svc_mem ) );
+  FD_TEST( window<=FD_FEC_RESOLVER_HIP_BATCH_MAX );
+  ulong checked = 0UL, code_bad = 0UL, code_diff = 0UL;
 #endif
 
   FILE * out = fopen( argv[1], "wb" );
@@ -178,6 +198,16 @@ main( int argc, char ** argv ) {
     for( ulong j=0UL; j<m; j++ ) {                                 /* the GPU's codes against the reference's verify */
       int ref = fd_ed25519_verify( r->hip_roots + 32UL*j, 32UL, r->hip_sigs + 64UL*j, r->hip_pubs + 32UL*j, sha );
       code_bad += ref!=(int)r->hip_codes[ j ];
+    }
+    checked += m;
+    t0 = fd_log_wallclock();
+#elif FD_HAS_HIP_SVC
+    ulong m = fd_fec_resolver_hip_preverify( r, parsed, psz, ppub, n );
+    t_add += fd_log_wallclock() - t0;
+    for( ulong j=0UL; j<m; j++ ) {                                 /* the service's verdicts against the reference's verify */
+      int ref = fd_ed25519_verify( r->hip_roots + 32UL*j, 32UL, r->hip_sigs + 64UL*j, r->hip_pubs + 32UL*j, sha );
+      code_bad  += ( ref==FD_ED25519_SUCCESS )!=( (int)r->hip_codes[ j ]==FD_ED25519_SUCCESS );
+      code_diff += ref!=(int)r->hip_codes[ j ];
     }
     checked += m;
     t0 = fd_log_wallclock();
@@ -207,6 +237,14 @@ main( int argc, char ** argv ) {
   ulong st[ 4 ]; fd_fec_resolver_hip_stats( r, st );
   printf( ", \"hip\": 1, \"roots_verified\": %lu, \"launches\": %lu, \"table_hits\": %lu, \"core_verifies\": %lu, "
           "\"roots_checked\": %lu, \"code_mismatch\": %lu", st[ 0 ], st[ 1 ], st[ 2 ], st[ 3 ], checked, code_bad );
+#elif FD_HAS_HIP_SVC
+  ulong st[ 4 ]; fd_fec_resolver_hip_stats( r, st );
+  ulong threads, dev_fds; svc_client_census( &threads, &dev_fds );
+  printf( ", \"hip\": 2, \"roots_verified\": %lu, \"launches\": %lu, \"table_hits\": %lu, \"core_verifies\": %lu, "
+          "\"roots_checked\": %lu, \"code_mismatch\": %lu, \"code_diff\": %lu, \"threads\": %lu, \"dev_fds\": %lu, "
+          "\"svc_requests\": %lu", st[ 0 ], st[ 1 ], st[ 2 ], st[ 3 ], checked, code_bad, code_diff, threads, dev_fds,
+          r->hip_svc->reqs_posted );
+  svc_client_done();
 #else
   printf( ", \"hip\": 0" );
 #endif

@@ -17,6 +17,11 @@
             (replay_hip_sigverify in fd_replay_tile.c): claimed batches
             packed into pinned buffers and verified by
             fd_replay_hip_txn_verify_host on the GPU, polled without blocking
+     svc    the bulk path as the replay tile runs it in service mode
+            (FD_HAS_HIP_SVC, _build/sched_run_svc): claimed batches become
+            the GPU tile's signature records (include/fd_replay_svc.h) --
+            no HIP in this process; a client of the run named by
+            SVC_CLIENT_SHM (integration/svc_client.h)
 
    Exec tiles are emulated: a dispatched task completes one loop iteration
    later (tasks on several tiles overlap).  Banks are emulated by a refcnt
@@ -25,7 +30,7 @@
    abandon) unless the run is in record mode, which keeps verifying so that
    every transaction's result can be compared.
 
-   usage: sched_run <fecs.bin> <exec|claim|skip|hip> <exec_cnt> <record 0|1> <out.bin> [batch_max] [batch_min]
+   usage: sched_run <fecs.bin> <exec|claim|skip|hip|svc> <exec_cnt> <record 0|1> <out.bin> [batch_max] [batch_min]
    fecs.bin : "FDB1" u64 fec_cnt, then per FEC set: u32 data_sz, u8 last_in_batch, data
               (one block, bank 1 on the snapshot root bank 0; the last FEC
               set is the block's last)
@@ -38,6 +43,10 @@
 #include "../../flamenco/runtime/fd_runtime_err.h"
 #if FD_HAS_HIP
 #include "fd_replay_hip.h"
+#endif
+#if FD_HAS_HIP_SVC
+#include "fd_replay_svc.h"
+#include "svc_client.h"
 #endif
 #include <stdio.h>
 #include <stdlib.h>
@@ -56,6 +65,7 @@ void fd_halt( void ) {}
 #define MODE_CLAIM 1
 #define MODE_HIP   2
 #define MODE_SKIP  3
+#define MODE_SVC   4
 
 typedef struct { uchar sig0[ 64 ]; int result; uchar source; uchar pad[ 3 ]; } rec_t;
 FD_STATIC_ASSERT( sizeof(rec_t)==72UL, rec_layout );
@@ -115,6 +125,10 @@ typedef struct {
   uchar *             pool;
   fd_txn_hip_desc_t * desc;
 #endif
+#if FD_HAS_HIP_SVC
+  fd_replay_svc_t *     svc;
+  fd_replay_svc_txn_t * stx;
+#endif
 } bulk_t;
 
 static int
@@ -126,6 +140,9 @@ bulk_sigverify( fd_sched_t * sched, bulk_t * b, int mode, ulong batch_min, ulong
       if( !done ) return 0;
       FD_TEST( done==1 );
     }
+#endif
+#if FD_HAS_HIP_SVC
+    if( mode==MODE_SVC && !fd_replay_svc_step( b->svc, fd_tickcount() ) ) return 0;
 #endif
     for( ulong j=0UL; j<b->cnt; j++ ) {
       bank_refcnt[ b->bank_idx ]--;
@@ -165,8 +182,21 @@ bulk_sigverify( fd_sched_t * sched, bulk_t * b, int mode, ulong batch_min, ulong
       pool_sz += txn_p->payload_sz;
     }
     FD_TEST( !fd_replay_hip_txn_verify_host( b->replay, cnt, b->pool, pool_sz, b->desc, b->result, NULL ) );
+#elif FD_HAS_HIP_SVC
+    for( ulong j=0UL; j<cnt; j++ ) {
+      fd_txn_p_t const * txn_p = fd_sched_get_txn( sched, b->txn_idx[ j ] );
+      fd_txn_t const *   txn   = TXN( txn_p );
+      b->stx[ j ] = (fd_replay_svc_txn_t){ .payload       = txn_p->payload,
+                                           .payload_sz    = (ushort)txn_p->payload_sz,
+                                           .signature_off = txn->signature_off,
+                                           .message_off   = txn->message_off,
+                                           .acct_addr_off = txn->acct_addr_off,
+                                           .signature_cnt = txn->signature_cnt };
+    }
+    fd_replay_svc_start( b->svc, cnt, b->stx, b->result );
+    (void)fd_replay_svc_step( b->svc, fd_tickcount() );
 #else
-    FD_LOG_ERR(( "hip mode needs a FD_HAS_HIP build" ));
+    FD_LOG_ERR(( "hip / svc mode needs a FD_HAS_HIP / FD_HAS_HIP_SVC build" ));
 #endif
   }
   b->cnt = cnt;
@@ -181,9 +211,10 @@ static void * sched_mem;
 
 static int
 run_job( char ** argv, int argc ) {
-  if( argc<5 ) { fprintf( stderr, "job: fecs.bin exec|claim|skip|hip exec_cnt record out.bin [batch_max] [batch_min]\n" ); return 2; }
+  if( argc<5 ) { fprintf( stderr, "job: fecs.bin exec|claim|skip|hip|svc exec_cnt record out.bin [batch_max] [batch_min]\n" ); return 2; }
   int mode = !strcmp( argv[1], "exec" ) ? MODE_EXEC : !strcmp( argv[1], "claim" ) ? MODE_CLAIM :
-             !strcmp( argv[1], "hip" ) ? MODE_HIP : !strcmp( argv[1], "skip" ) ? MODE_SKIP : -1;
+             !strcmp( argv[1], "hip" ) ? MODE_HIP : !strcmp( argv[1], "skip" ) ? MODE_SKIP :
+             !strcmp( argv[1], "svc" ) ? MODE_SVC : -1;
   FD_TEST( mode>=0 );
   ulong exec_cnt  = strtoul( argv[2], NULL, 0 );
   record_mode     = atoi( argv[3] );
@@ -237,6 +268,21 @@ run_job( char ** argv, int argc ) {
     FD_TEST( bulk->replay && bulk->pool && bulk->desc && res );
     free( bulk->result );
     bulk->result = res;
+  }
+#endif
+#if FD_HAS_HIP_SVC
+  if( mode==MODE_SVC ) {
+    /* one client per process: its request ring continues across jobs */
+    static fd_replay_svc_t svc[1]; static int joined;
+    if( !joined ) {
+      ulong seg_t;
+      fd_verify_svc_seg_t * seg = svc_client_attach( &seg_t );
+      FD_TEST( fd_replay_svc_join( svc, seg, seg_t ) );
+      joined = 1;
+    }
+    bulk->svc = svc;
+    bulk->stx = malloc( batch_max*sizeof(fd_replay_svc_txn_t) );
+    FD_TEST( bulk->stx );
   }
 #endif
 
@@ -335,14 +381,22 @@ run_job( char ** argv, int argc ) {
   FD_TEST( fwrite( "FDR1", 1, 4, o )==4 && fwrite( &rec_cnt, 8, 1, o )==1 &&
            fwrite( recs, sizeof(rec_t), rec_cnt, o )==rec_cnt );
   fclose( o );
+  char svc_extra[ 160 ] = "";
+#if FD_HAS_HIP_SVC
+  if( mode==MODE_SVC ) {
+    ulong threads, dev_fds; svc_client_census( &threads, &dev_fds );
+    snprintf( svc_extra, sizeof(svc_extra), ", \"threads\": %lu, \"dev_fds\": %lu, \"svc_requests\": %lu, \"svc_sigs\": %lu",
+              threads, dev_fds, bulk->svc->c->reqs_posted, bulk->svc->sigs );
+  }
+#endif
   printf( "{\"mode\": \"%s\", \"record\": %d, \"exec_cnt\": %lu, \"fec_cnt\": %lu, \"fec_ingested\": %lu, "
           "\"sigverified\": %lu, \"tasks_exec\": %lu, \"tasks_sigverify\": %lu, \"bulk_batches\": %lu, "
           "\"bulk_max\": %lu, \"sigs_exec\": %lu, \"sigs_bulk\": %lu, \"block_started\": %d, \"block_ended\": %d, "
           "\"dead\": %d, \"refcnt\": %lu, \"seconds\": %.6f, \"batch_max\": %lu, \"batch_min\": %lu, "
-          "\"ingest_s\": %.6f, \"bulk_s\": %.6f, \"sigverify_done_s\": %.6f}\n",
+          "\"ingest_s\": %.6f, \"bulk_s\": %.6f, \"sigverify_done_s\": %.6f%s}\n",
           argv[1], record_mode, exec_cnt, fec_cnt, fec_i, rec_cnt, tasks_exec, tasks_sigverify, batches_bulk, bulk_max,
           sigs_exec, sigs_bulk, block_started, block_ended, bank_dead[ 1 ], bank_refcnt[ 1 ], dt, batch_max, batch_min,
-          t_ingest, t_bulk, t_sv_last );
+          t_ingest, t_bulk, t_sv_last, svc_extra );
   fflush( stdout );
 #if FD_HAS_HIP
   if( hip ) {
@@ -359,7 +413,7 @@ int
 main( int argc, char ** argv ) {
   fd_boot( &argc, &argv );
   if( argc!=2 && argc<6 ) {
-    fprintf( stderr, "usage: %s fecs.bin exec|claim|skip|hip exec_cnt record out.bin [batch_max] [batch_min]\n"
+    fprintf( stderr, "usage: %s fecs.bin exec|claim|skip|hip|svc exec_cnt record out.bin [batch_max] [batch_min]\n"
                      "       %s jobs.txt   (one job per line, same fields)\n", argv[0], argv[0] );
     return 2;
   }
@@ -373,7 +427,13 @@ main( int argc, char ** argv ) {
   static uchar sha_mem[ FD_TXN_ACTUAL_SIG_MAX ][ sizeof(fd_sha512_t) ] __attribute__((aligned(FD_SHA512_ALIGN)));
   for( ulong k=0UL; k<FD_TXN_ACTUAL_SIG_MAX; k++ ) shas[ k ] = fd_sha512_join( fd_sha512_new( sha_mem[ k ] ) );
 
-  if( argc>=6 ) return run_job( argv+1, argc-1 );
+  if( argc>=6 ) {
+    int rc = run_job( argv+1, argc-1 );
+#if FD_HAS_HIP_SVC
+    svc_client_done();
+#endif
+    return rc;
+  }
   FILE * jf = fopen( argv[1], "r" ); FD_TEST( jf );
   char line[ 4096 ];
   while( fgets( line, sizeof(line), jf ) ) {
@@ -384,5 +444,8 @@ main( int argc, char ** argv ) {
     if( rc ) return rc;
   }
   fclose( jf );
+#if FD_HAS_HIP_SVC
+  svc_client_done();
+#endif
   return 0;
 }

@@ -8,7 +8,8 @@
    Maps the run's shared file, registers it for the GPU once (every link's
    mcache and dcache, the tiles' verify_dedup dcaches and the segment lie
    in it), names the quic_verify links (service link l = link kind_id l)
-   and the tiles' out dcaches, then polls until the producer sets shutdown.
+   and the tiles' out dcaches (the segment's client tiles, after them, get
+   fd_verify_svc_set_client), then polls until the producer sets shutdown.
    Environment: SVC_BATCH_MAX (frags per merged launch, default 262144),
    SVC_INFLIGHT (launches at once, default 2), SVC_MERGE_MIN (frags that
    start a launch at once, default batch_max / 2), SVC_MERGE_WAIT_NS
@@ -146,6 +147,8 @@ main( int argc, char ** argv ) {
     if( !dcache || fd_verify_svc_set_tile( svc, t, dcache, fd_dcache_data_sz( dcache ), base ) )
       FD_LOG_ERR(( "fd_verify_svc_set_tile %lu failed", t ));
   }
+  for( ulong c=0UL; c<hdr->client_cnt; c++ )
+    if( fd_verify_svc_set_client( svc, hdr->tile_cnt+c ) ) FD_LOG_ERR(( "fd_verify_svc_set_client %lu failed", hdr->tile_cnt+c ));
   if( fd_verify_svc_run( svc ) ) FD_LOG_ERR(( "fd_verify_svc_run failed" ));
 
   {                                                             /* before the sandbox: rt_sigaction is not in its filter */

@@ -50,6 +50,9 @@ typedef struct {
   ulong out_mcache_off[ SVC_RUN_TILE_MAX ], out_dcache_off[ SVC_RUN_TILE_MAX ], cons_fseq_off[ SVC_RUN_TILE_MAX ];
   ulong out_data_sz;
   ulong svc_off, svc_sz, req_depth, slot_cap, frag_cap;
+  ulong client_cnt;                            /* the segment's last client_cnt tiles are clients (FD_VERIFY_SVC_REQ_SIGS:
+                                                  integration/svc_client.h), after the tile_cnt verify tiles */
+  volatile ulong clients_ready, clients_done;
   ulong map_sz;
   volatile ulong tiles_ready, cons_ready, svc_ready, start, shutdown, svc_done;
   volatile long  t0, t_pub;

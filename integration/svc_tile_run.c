@@ -57,6 +57,12 @@
          same digest the reference tile's run gives, oracle/ref_txn_drv.c)
          and histograms tspub - tsorig and consume time - tsorig.
          SVC_RUN_CONS_STALL_MS=m: it sleeps m ms before reading anything.
+     svc_tile_run host <shm> <clients> <req_depth> <slot_cap> <frag_cap>
+         A run of client tiles only (see host() below).
+   produce with SVC_RUN_CLIENTS=k adds k client tiles to the segment after
+   the verify tiles (a replay or shred tile beside them,
+   integration/svc_client.h) and ends the run only once each has set
+   clients_done.
 
    Stream file: "FDT1" u64 n, u64 seed, u64 tcache_depth, per frag u64
    bundle_id, u16 payload_sz, payload bytes (oracle/tile_drv.c's format). */
@@ -166,11 +172,17 @@ produce( char const * path, char const * stream, ulong tile_cnt, ulong in_depth 
   ulong const out_depth = env_ulong( "SVC_RUN_OUT_DEPTH", 16384UL );
   ulong const req_depth = env_ulong( "SVC_RUN_REQ_DEPTH", 16UL );
   ulong const slot_cap  = env_ulong( "SVC_RUN_SLOT_CAP", 32768UL );
-  ulong const frag_cap  = env_ulong( "SVC_RUN_FRAG_CAP", getenv( "SVC_RUN_POLLED" ) ? 4096UL : 0UL );
+  /* a polled link's frag area: 4096 frags per request, at most the slot's capacity (a frag area over
+     slot_cap is no segment: the shallow-link shape's 2048-frag slots made every polled run fail) */
+  ulong const frag_cap  = env_ulong( "SVC_RUN_FRAG_CAP", getenv( "SVC_RUN_POLLED" ) ? fd_ulong_min( 4096UL, slot_cap ) : 0UL );
   if( FD_UNLIKELY( L<1UL || L>SVC_RUN_LINK_MAX ) ) FD_LOG_ERR(( "SVC_RUN_LINKS %lu not in [1,%lu]", L, SVC_RUN_LINK_MAX ));
   if( FD_UNLIKELY( !fd_ulong_is_pow2( out_depth ) ) ) FD_LOG_ERR(( "SVC_RUN_OUT_DEPTH %lu not a power of 2", out_depth ));
-  ulong svc_sz = fd_verify_svc_footprint( tile_cnt, req_depth, slot_cap, frag_cap );
-  if( FD_UNLIKELY( !svc_sz ) ) FD_LOG_ERR(( "bad service segment parameters" ));
+  /* clients (integration/svc_client.h: a replay or shred tile beside the verify tiles): frag areas for their records */
+  ulong const clients   = env_ulong( "SVC_RUN_CLIENTS", 0UL );
+  ulong const frag_capc = clients ? fd_ulong_max( frag_cap, fd_ulong_min( 256UL, slot_cap ) ) : frag_cap;
+  ulong svc_sz = fd_verify_svc_footprint( tile_cnt+clients, req_depth, slot_cap, frag_capc );
+  if( FD_UNLIKELY( !svc_sz ) ) FD_LOG_ERR(( "bad service segment parameters (%lu tiles, %lu clients, %lu slots x %lu frags, frag area %lu)",
+                                          tile_cnt, clients, req_depth, slot_cap, frag_capc ));
 
   ulong data_sz = fd_dcache_req_data_sz( FD_TPU_RAW_MTU, in_depth, 1UL, 1 );
   if( prelay ) {
@@ -222,11 +234,12 @@ produce( char const * path, char const * stream, ulong tile_cnt, ulong in_depth 
     FD_TEST( fd_fseq_join( fd_fseq_new( base + cfs_off[ t ], 0UL ) ) );
     hdr->out_mcache_off[ t ] = omc_off[ t ]; hdr->out_dcache_off[ t ] = odc_off[ t ]; hdr->cons_fseq_off[ t ] = cfs_off[ t ];
   }
-  FD_TEST( fd_verify_svc_new( base + svc_off, tile_cnt, req_depth, slot_cap, frag_cap ) );
+  FD_TEST( fd_verify_svc_new( base + svc_off, tile_cnt+clients, req_depth, slot_cap, frag_capc ) );
+  hdr->client_cnt = clients;
   hdr->n = n; hdr->tile_cnt = tile_cnt; hdr->seed = seed; hdr->tcache_depth = depth; hdr->in_depth = in_depth;
   hdr->link_cnt = L; hdr->out_depth = out_depth; hdr->fseq_stride = fs_strd; hdr->dcache_data_sz = data_sz;
   hdr->out_data_sz = out_data; hdr->svc_off = svc_off; hdr->svc_sz = svc_sz; hdr->req_depth = req_depth;
-  hdr->slot_cap = slot_cap; hdr->frag_cap = frag_cap; hdr->map_sz = map_sz;
+  hdr->slot_cap = slot_cap; hdr->frag_cap = frag_capc; hdr->map_sz = map_sz;
   ulong * pchunk = NULL;
   if( prelay ) {
     pchunk = malloc( n*sizeof(ulong) ); FD_TEST( pchunk );
@@ -296,8 +309,8 @@ produce( char const * path, char const * stream, ulong tile_cnt, ulong in_depth 
   for( ;; ) {
     ulong done = 0UL;
     for( ulong t=0UL; t<tile_cnt; t++ ) done += hdr->tile[ t ].done + hdr->cons[ t ].done;
-    if( done==2UL*tile_cnt ) break;
-    if( fd_log_wallclock()-t0 > 900L*1000000000L ) FD_LOG_ERR(( "tiles / consumers not done after 900 s" ));
+    if( done==2UL*tile_cnt && hdr->clients_done>=clients ) break;
+    if( fd_log_wallclock()-t0 > 900L*1000000000L ) FD_LOG_ERR(( "tiles / consumers / clients not done after 900 s" ));
     FD_SPIN_PAUSE();
   }
   /* the GPU tile's threads while it still runs: each one's seccomp mode
@@ -696,6 +709,54 @@ consume( char const * path, ulong t ) {
   return 0;
 }
 
+/* svc_tile_run host <shm> <clients> <req_depth> <slot_cap> <frag_cap>: a
+   run of clients only (no link, no verify tile): creates <shm> with a
+   segment of <clients> client tiles, prints READY, waits for the GPU tile
+   (svc_run or oracle/svc_mock on the same file) and for every client
+   process (integration/svc_client.h: each sets clients_done when done),
+   then shuts the service down and prints the service's counters */
+static int
+host( char const * path, ulong clients, ulong req_depth, ulong slot_cap, ulong frag_cap ) {
+  FD_TEST( clients>=1UL && clients<=FD_VERIFY_SVC_TILE_MAX );
+  ulong svc_sz = fd_verify_svc_footprint( clients, req_depth, slot_cap, frag_cap );
+  if( FD_UNLIKELY( !svc_sz ) ) FD_LOG_ERR(( "bad segment parameters (%lu clients, %lu slots x %lu, frag area %lu)",
+                                          clients, req_depth, slot_cap, frag_cap ));
+  ulong svc_off = fd_ulong_align_up( sizeof(svc_run_hdr_t), 4096UL );
+  ulong map_sz  = fd_ulong_align_up( svc_off + svc_sz, 4096UL );
+  uchar * base = drv_map( path, map_sz, 1 );
+  svc_run_hdr_t * hdr = (svc_run_hdr_t *)base;
+  memset( hdr, 0, sizeof(svc_run_hdr_t) );
+  FD_TEST( fd_verify_svc_new( base + svc_off, clients, req_depth, slot_cap, frag_cap ) );
+  hdr->tile_cnt = 0UL; hdr->client_cnt = clients; hdr->link_cnt = 0UL;
+  hdr->svc_off = svc_off; hdr->svc_sz = svc_sz; hdr->req_depth = req_depth; hdr->slot_cap = slot_cap;
+  hdr->frag_cap = frag_cap; hdr->map_sz = map_sz;
+  FD_COMPILER_MFENCE();
+  hdr->magic = SVC_RUN_MAGIC;
+  FD_COMPILER_MFENCE();
+  printf( "READY\n" ); fflush( stdout );
+  long t0 = fd_log_wallclock();
+  while( hdr->svc_ready<1UL ) {
+    if( fd_log_wallclock()-t0 > 180L*1000000000L ) FD_LOG_ERR(( "GPU tile not ready after 180 s" ));
+    FD_SPIN_PAUSE();
+  }
+  hdr->start = 1UL;
+  while( hdr->clients_done<clients ) {
+    if( fd_log_wallclock()-t0 > 900L*1000000000L ) FD_LOG_ERR(( "clients not done after 900 s (%lu of %lu)", hdr->clients_done, clients ));
+    FD_SPIN_PAUSE();
+  }
+  long t1 = fd_log_wallclock();
+  hdr->shutdown = 1UL;
+  while( !hdr->svc_done ) {
+    if( fd_log_wallclock()-t1 > 120L*1000000000L ) FD_LOG_ERR(( "GPU tile not done 120 s after shutdown" ));
+    FD_SPIN_PAUSE();
+  }
+  printf( "{\"clients\": %lu, \"seconds\": %.6f, \"svc\": {\"launches\": %lu, \"records\": %lu, \"requests\": %lu, "
+          "\"gpu_ns\": %lu, \"largest_launch\": %lu}, \"svc_sandboxed\": %lu, \"svc_traps\": %lu}\n", clients,
+          (double)( t1-t0 )*1e-9, hdr->svc_stats[ 0 ], hdr->svc_stats[ 1 ], hdr->svc_stats[ 2 ], hdr->svc_stats[ 7 ],
+          hdr->svc_stats[ 15 ], hdr->svc_sandboxed, hdr->svc_traps );
+  return 0;
+}
+
 int
 main( int argc, char ** argv ) {
   fd_boot( &argc, &argv );
@@ -703,6 +764,10 @@ main( int argc, char ** argv ) {
     return produce( argv[2], argv[3], strtoul( argv[4], NULL, 0 ), strtoul( argv[5], NULL, 0 ) );
   if( argc>=4 && !strcmp( argv[1], "tile" ) )    return tile( argv[2], strtoul( argv[3], NULL, 0 ) );
   if( argc>=4 && !strcmp( argv[1], "consume" ) ) return consume( argv[2], strtoul( argv[3], NULL, 0 ) );
-  fprintf( stderr, "usage: %s produce <shm> <stream.bin> <tile_cnt> <in_depth> | tile <shm> <t> | consume <shm> <t>\n", argv[0] );
+  if( argc>=7 && !strcmp( argv[1], "host" ) )
+    return host( argv[2], strtoul( argv[3], NULL, 0 ), strtoul( argv[4], NULL, 0 ), strtoul( argv[5], NULL, 0 ),
+                 strtoul( argv[6], NULL, 0 ) );
+  fprintf( stderr, "usage: %s produce <shm> <stream.bin> <tile_cnt> <in_depth> | tile <shm> <t> | consume <shm> <t> | "
+                   "host <shm> <clients> <req_depth> <slot_cap> <frag_cap>\n", argv[0] );
   return 2;
 }

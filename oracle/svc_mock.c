@@ -18,7 +18,11 @@
    posted request's frags (the link's bytes) into staging and mark it
    INGESTED, then, at least `us` microseconds later, parse and verify from
    staging only and mark it RESULTS (the tile returns the link's credits in
-   between); default: both at once, straight to RESULTS. */
+   between); default: both at once, straight to RESULTS.
+
+   Client tiles (the segment's tiles after the run's tile_cnt verify tiles,
+   integration/svc_client.h) post FD_VERIFY_SVC_REQ_SIGS records: each is
+   answered with the reference's fd_ed25519_verify. */
 
 #include "../../tango/mcache/fd_mcache.h"
 #include "../../tango/dcache/fd_dcache.h"
@@ -45,7 +49,7 @@ void fd_halt( void ) {}
 
 static uchar * stage;                          /* tile x slot x slot_cap staging frags */
 static fd_sha512_t * shas[ 16 ];
-typedef struct { uchar flags; uchar kind; uint tsorig; } meta_t;
+typedef struct { uchar flags; uchar kind; ushort sz; uint tsorig; } meta_t;
 static meta_t * meta;                          /* per staging frag: what the ingest saw */
 
 static uchar *
@@ -64,7 +68,15 @@ ingest( svc_run_hdr_t * hdr, uchar * base, fd_verify_svc_seg_t * s, ulong t, ulo
     ulong sz = 0UL, kind = 0UL;                                  /* FD_VERIFY_HIP_IN_QUIC */
     int   ok = 1;
     uchar const * src = NULL;
-    m->flags = 0; m->tsorig = 0U;
+    m->flags = 0; m->tsorig = 0U; m->sz = 0;
+    if( q->kind==FD_VERIFY_SVC_REQ_SIGS ) {                     /* a client's signature record, as it stands */
+      sz = fd_verify_svc_frag_sz( s, t, slot )[ j ];
+      m->kind = 0xff;
+      if( sz<FD_VERIFY_SVC_SIG_HDR_SZ || sz>FD_VERIFY_SVC_FRAG_STRIDE ) { m->flags = FD_VERIFY_SVC_RES_BAD; continue; }
+      memcpy( dst, fd_verify_svc_frag( s, t, slot ) + j*FD_VERIFY_SVC_FRAG_STRIDE, sz );
+      m->sz = (ushort)sz;
+      continue;
+    }
     if( q->kind==FD_VERIFY_SVC_REQ_RANGE ) {
       ulong first = fd_verify_svc_range_first( q->seq0, q->rr_cnt, q->rr_idx ), seq = first + j*q->rr_cnt;
       fd_frag_meta_t const * mc   = fd_mcache_join( base + hdr->mcache_off[ q->link ] );
@@ -110,6 +122,15 @@ answer( fd_verify_svc_seg_t * s, ulong t, ulong slot ) {
     meta_t const * m = &meta[ ( t*s->req_depth + slot )*s->slot_cap + j ];
     fd_verify_svc_res_t r; memset( &r, 0, sizeof(r) );
     r.flags = m->flags; r.tsorig = m->tsorig;
+    if( q->kind==FD_VERIFY_SVC_REQ_SIGS ) {                     /* fd_ed25519_verify of the record (the reference's) */
+      if( m->flags & FD_VERIFY_SVC_RES_BAD ) { r.code = (schar)FD_ED25519_ERR_SIG; res[ j ] = r; continue; }
+      uchar const * rec = stage_of( s, t, slot, j );
+      ulong msz = (ulong)m->sz - FD_VERIFY_SVC_SIG_HDR_SZ;
+      r.code = (schar)fd_ed25519_verify( rec + FD_VERIFY_SVC_SIG_HDR_SZ, msz, rec, rec + 64UL, shas[ 0 ] );
+      r.sig_cnt = 1; r.payload_sz = (ushort)msz;
+      res[ j ] = r;
+      continue;
+    }
     if( m->flags & FD_VERIFY_SVC_RES_BAD ) { res[ j ] = r; continue; }
     fd_txn_m_t * txnm = (fd_txn_m_t *)stage_of( s, t, slot, j );
     fd_txn_t * txnt = fd_txn_m_txn_t( txnm );
@@ -164,6 +185,7 @@ main( int argc, char ** argv ) {
         if( fd_verify_svc_ld( &q->state )!=FD_VERIFY_SVC_POSTED ) break;
         if( q->id+s->req_depth==take[ t ] ) break;               /* the slot's previous request, not yet verified */
         FD_TEST( q->id==take[ t ] );
+        FD_TEST( ( t>=hdr->tile_cnt )==( q->kind==FD_VERIFY_SVC_REQ_SIGS ) );   /* clients post signature records only */
         ingest( hdr, base, s, t, slot );
         if( ing_ns<0L ) { answer( s, t, slot ); vtake[ t ]++; }
         else { fd_verify_svc_st( &q->state, FD_VERIFY_SVC_INGESTED ); ing_at[ t ][ slot ] = fd_log_wallclock(); }
@@ -178,6 +200,7 @@ main( int argc, char ** argv ) {
       }
       fd_verify_svc_tile_t * b = fd_verify_svc_tile( s, t );
       ulong post = fd_verify_svc_ld( &b->flush_post );
+      if( t>=hdr->tile_cnt ) { FD_TEST( !post ); continue; }     /* a client: no out dcache, no flush */
       uchar * odc = fd_dcache_join( base + hdr->out_dcache_off[ t ] );
       ulong   osz = fd_dcache_data_sz( odc );
       while( ftake[ t ]<post ) {

@@ -106,3 +106,36 @@ def results_by_sig0(recs):
     d = {bytes(r["sig0"]): int(r["result"]) for r in recs}
     assert len(d) == len(recs), "duplicate sig0 in the records"
     return d
+
+
+def sched_jobs_file(jobs, tmp_dir):
+    """jobs.txt for sched_run (one job per line) and the records' paths"""
+    lines, outs = [], []
+    for k, j in enumerate(jobs):
+        out = os.path.join(str(tmp_dir), f"job{k}.bin")
+        outs.append(out)
+        lines.append(" ".join(str(x) for x in (j["block"], j["mode"], j.get("exec_cnt", 4), int(j.get("record", 0)), out,
+                                               j.get("batch_max", 16384), j.get("batch_min", 256))))
+    jf = os.path.join(str(tmp_dir), "jobs.txt")
+    with open(jf, "w") as f:
+        f.write("\n".join(lines) + "\n")
+    return jf, outs
+
+
+def run_sched_svc(jobs, tmp_dir, mock=False, timeout=600, svc_env=None):
+    """The svc-mode jobs (mode "svc") in ONE sched_run_svc process, a client
+    of the GPU tile (integration/svc_run.c, or oracle/_ref/svc_mock with
+    mock) in a clients-only run (svc_tile_run host, tools/svc_bench.py
+    run_host).  Returns ([(JSON summary, records)] in job order, the host's
+    line)."""
+    import json
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(BUILD), "..", "tools"))
+    import svc_bench as SB
+    import svc_io as SI
+    jf, outs = sched_jobs_file(jobs, tmp_dir)
+    res = SB.run_host([("replay", [os.path.join(BUILD, "sched_run_svc"), jf])], os.path.join(str(tmp_dir), "logs"),
+                      timeout=timeout, svc_exe=SI.MOCK if mock else None, svc_env=svc_env)
+    infos = [json.loads(x) for x in res["clients_lines"]["replay"] if x.startswith("{")]
+    assert len(infos) == len(jobs), res["clients_lines"]["replay"][-5:]
+    return [(i, read_records(o)) for i, o in zip(infos, outs)], res

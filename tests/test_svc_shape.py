@@ -9,7 +9,9 @@ checks of fd_verify_svc_boot_ok (the same header function: staging below
 default verify_tile_count = 6 on one GPU (6.85 GB of staging; VERDICT r05,
 missing #2).
 
-Here every verify_tile_count in 1..16 on 1..8 GPUs: each GPU's shape boots
+Here every verify_tile_count in 1..16 on 1..8 GPUs, with 0..5 client tiles
+(shred tiles, the replay tile: include/fd_verify_svc.h "clients") on GPU 0:
+each GPU's shape boots
 with the GPU tile's defaults (batch_max 262144, 2 launches in flight,
 integration/fd_verify_gpu_tile.c), the shapes cover every verify tile once,
 and the staging bound is recomputed here independently of the header."""
@@ -27,15 +29,17 @@ PROG = r"""
 int main( void ) {
   printf( "{\"rows\": [" );
   int first = 1;
-  for( ulong v=1UL; v<=16UL; v++ ) for( ulong gpus=1UL; gpus<=8UL; gpus++ ) {
+  /* clients on GPU 0 (the topology patch): shred tiles (1..4), plus the
+     replay tile in the Firedancer topology */
+  for( ulong v=1UL; v<=16UL; v++ ) for( ulong gpus=1UL; gpus<=8UL; gpus++ ) for( ulong cl=0UL; cl<=5UL; cl++ ) {
     ulong gc = gpus<v ? gpus : v;                       /* vgpu_cnt = min( FD_VERIFY_SVC_GPU_CNT, verify_tile_cnt ) */
     for( ulong g=0UL; g<gc; g++ ) {
       ulong sh[ 4 ] = { 0UL, 0UL, 0UL, 0UL };
-      int rc = fd_verify_svc_topo_shape( fd_verify_svc_tiles_on( g, v, gc ), sh );
+      int rc = fd_verify_svc_topo_shape( fd_verify_svc_tiles_on( g, v, gc ) + ( g ? 0UL : cl ), sh );
       int ok = !rc && fd_verify_svc_boot_ok( sh[0], sh[1], sh[2], sh[3], 262144UL, 2UL );
-      printf( "%s{\"verify\": %lu, \"gpus\": %lu, \"g\": %lu, \"rc\": %d, \"boot_ok\": %d, \"shape\": [%lu, %lu, %lu, %lu], "
-              "\"footprint\": %lu}", first ? "" : ", ", v, gc, g, rc, ok, sh[0], sh[1], sh[2], sh[3],
-              fd_verify_svc_footprint( sh[0], sh[1], sh[2], sh[3] ) );
+      printf( "%s{\"verify\": %lu, \"gpus\": %lu, \"g\": %lu, \"clients\": %lu, \"rc\": %d, \"boot_ok\": %d, "
+              "\"shape\": [%lu, %lu, %lu, %lu], \"footprint\": %lu}", first ? "" : ", ", v, gc, g, g ? 0UL : cl, rc, ok,
+              sh[0], sh[1], sh[2], sh[3], fd_verify_svc_footprint( sh[0], sh[1], sh[2], sh[3] ) );
       first = 0;
     }
   }
@@ -61,7 +65,7 @@ def shapes(tmp_path_factory):
 
 def test_every_topology_shape_boots(shapes):
     rows, _ = shapes
-    assert len(rows) == sum(min(g, v) for v in range(1, 17) for g in range(1, 9))
+    assert len(rows) == 6 * sum(min(g, v) for v in range(1, 17) for g in range(1, 9))
     for r in rows:
         t, depth, cap, frag = r["shape"]
         assert r["rc"] == 0 and r["boot_ok"] == 1, r
@@ -75,8 +79,13 @@ def test_shapes_cover_every_tile(shapes):
     rows, _ = shapes
     for v in range(1, 17):
         for gpus in range(1, 9):
-            served = list({r["g"]: r["shape"][0] for r in rows if r["verify"] == v and r["gpus"] == min(gpus, v)}.values())
-            assert len(served) == min(gpus, v) and sum(served) == v and max(served) - min(served) <= 1, (v, gpus, served)
+            for cl in range(6):
+                sel = [r for r in rows if r["verify"] == v and r["gpus"] == min(gpus, v) and
+                       (r["g"] > 0 or r["clients"] == cl)]
+                by_g = {r["g"]: r["shape"][0] - r["clients"] for r in sel}
+                served = list(by_g.values())
+                assert len(served) == min(gpus, v) and sum(served) == v and max(served) - min(served) <= 1, (v, gpus, served)
+                assert {r["shape"][0] for r in sel if r["g"] == 0} == {by_g[0] + cl}
 
 
 def test_reference_default_six_tiles_on_one_gpu(shapes):
@@ -84,6 +93,9 @@ def test_reference_default_six_tiles_on_one_gpu(shapes):
     128 slots of 2048 frags (3.4 GB of staging); round 5's 16 x 32768 does not
     boot, and twice the slot capacity is over the bound"""
     rows, extra = shapes
-    six = [r for r in rows if r["verify"] == 6 and r["gpus"] == 1]
+    six = [r for r in rows if r["verify"] == 6 and r["gpus"] == 1 and r["clients"] == 0]
     assert six and six[0]["shape"] == [6, 128, 2048, 256]
+    # with the Firedancer topology's clients on GPU 0 (one shred tile, the replay tile): 8 tiles, 1024-frag slots
+    eight = [r for r in rows if r["verify"] == 6 and r["gpus"] == 1 and r["clients"] == 2]
+    assert eight and eight[0]["shape"] == [8, 128, 1024, 256] and eight[0]["boot_ok"] == 1
     assert extra["r05_6"] == 0 and extra["over"] == 0

@@ -74,20 +74,27 @@ def pick_cpus(count, node=-1):
 
 
 def run_one(stream, tiles, in_depth, timeout, logdir, env=None, svc_env=None, svc_exe=None, gpu=0, pin=None,
-            rocprof=None):
+            rocprof=None, clients=None):
     """One producer, the GPU tile, `tiles` tile processes and `tiles`
     consumers.  env: the SVC_RUN_* settings (every process); svc_env: the
     GPU tile's (SVC_BATCH_MAX, SVC_INFLIGHT, ...).  Liveness is checked every
     0.2 s: a process that dies ends the run at once.  rocprof: a directory;
     the GPU tile runs under rocprofv3 --kernel-trace --memory-copy-trace
     --stats there (the program itself after --); SVC_BENCH_HIP_TRACE=1 adds
-    --hip-trace (the HIP API calls' host durations)."""
+    --hip-trace (the HIP API calls' host durations).  clients: [(name,
+    argv)], client processes of the GPU tile beside the verify tiles
+    (integration/svc_client.h: a replay or shred harness built with
+    FD_HAS_HIP_SVC), client i on the segment's tile tiles + i; each one's
+    last stdout line (JSON) lands in res["clients"][name]."""
     shm = f"/dev/shm/fd_svc_bench_{os.getpid()}"
     if os.path.exists(shm):
         os.unlink(shm)
     os.makedirs(logdir, exist_ok=True)
     e = dict(os.environ)
     e.update(env or {})
+    clients = list(clients or [])
+    if clients:
+        e["SVC_RUN_CLIENTS"] = str(len(clients))
     errs, procs = [], []
     # pin: one core each for the producer, the GPU tile, the tiles and the consumers, on the GPU's NUMA node
     # (the reference pins every tile to a core, [layout.affinity]); "auto" picks them, or a list of CPUs
@@ -134,6 +141,14 @@ def run_one(stream, tiles, in_depth, timeout, logdir, env=None, svc_env=None, sv
         for t in range(tiles):
             spawn([EXE, "consume", shm, str(t)], f"cons{t}")
             spawn([EXE, "tile", shm, str(t)], f"tile{t}")
+        cout = {}
+        for i, (cname, argv) in enumerate(clients):
+            cout[cname] = open(os.path.join(logdir, cname + ".out"), "w+")
+            errs.append(cout[cname])
+            f = open(os.path.join(logdir, cname + ".err"), "w")
+            errs.append(f)
+            procs.append((cname, subprocess.Popen(argv, stdout=cout[cname], stderr=f,
+                                                  env=dict(e, SVC_CLIENT_SHM=shm, SVC_CLIENT_IDX=str(i)))))
         # a sandboxed tile (SVC_RUN_SANDBOX) dies of SIGSYS after reporting: exit is not in the
         # reference tile's seccomp policy (a reference tile never returns)
         ok_rc = {0, -signal.SIGSYS} if e.get("SVC_RUN_SANDBOX") else {0}
@@ -160,6 +175,13 @@ def run_one(stream, tiles, in_depth, timeout, logdir, env=None, svc_env=None, sv
                 raise RuntimeError(f"{n} rc {p.returncode} (see {logdir}/{n}.err)")
         res = json.loads(out.strip().splitlines()[-1])
         res["pinned"] = {k: sorted(v) for k, v in cpu_of.items()} or None
+        if clients:
+            res["clients"], res["clients_lines"] = {}, {}
+            for cname, f in cout.items():
+                f.seek(0)
+                lines = [x for x in f.read().splitlines() if x.strip()]
+                res["clients"][cname] = json.loads(lines[-1]) if lines else None
+                res["clients_lines"][cname] = lines
         return res
     finally:
         # the GPU tile first, with SIGTERM: it stops its IO engine and drains the GPU before it
@@ -176,6 +198,79 @@ def run_one(stream, tiles, in_depth, timeout, logdir, env=None, svc_env=None, sv
                 p.kill()
                 p.wait()
         for f in errs:
+            f.close()
+        if os.path.exists(shm):
+            os.unlink(shm)
+
+
+def run_host(clients, logdir, timeout=300, svc_env=None, svc_exe=None, gpu=0, req_depth=128, slot_cap=2048,
+             frag_cap=256, env=None):
+    """A run of client processes only (svc_tile_run host): the GPU tile (or
+    oracle/_ref/svc_mock with svc_exe) and clients [(name, argv)], client i
+    on segment tile i.  Returns the host's JSON line with "clients": each
+    client's last stdout line (JSON)."""
+    shm = f"/dev/shm/fd_svc_host_{os.getpid()}"
+    if os.path.exists(shm):
+        os.unlink(shm)
+    os.makedirs(logdir, exist_ok=True)
+    e = dict(os.environ)
+    e.update(env or {})
+    files, procs = [], []
+    herr = open(os.path.join(logdir, "host.err"), "w")
+    files.append(herr)
+    host = subprocess.Popen([EXE, "host", shm, str(len(clients)), str(req_depth), str(slot_cap), str(frag_cap)],
+                            stdout=subprocess.PIPE, stderr=herr, text=True, env=e)
+    t0 = time.time()
+    try:
+        line = host.stdout.readline()
+        if line.strip() != "READY":
+            raise RuntimeError(f"host: {line!r} (see {logdir}/host.err)")
+        f = open(os.path.join(logdir, "svc.err"), "w")
+        files.append(f)
+        procs.append(("svc", subprocess.Popen([svc_exe or SVC, shm, str(gpu)], stdout=subprocess.DEVNULL, stderr=f,
+                                              env=dict(e, **(svc_env or {})))))
+        outs = {}
+        for i, (cname, argv) in enumerate(clients):
+            outs[cname] = open(os.path.join(logdir, cname + ".out"), "w+")
+            f = open(os.path.join(logdir, cname + ".err"), "w")
+            files += [outs[cname], f]
+            procs.append((cname, subprocess.Popen(argv, stdout=outs[cname], stderr=f,
+                                                  env=dict(e, SVC_CLIENT_SHM=shm, SVC_CLIENT_IDX=str(i)))))
+        while host.poll() is None:
+            dead = [(n, p.returncode) for n, p in procs if p.poll() is not None and p.returncode != 0]
+            if dead:
+                raise RuntimeError(f"died: {dead} (see {logdir}/*.err)")
+            if time.time() - t0 > timeout:
+                raise RuntimeError(f"timeout after {timeout} s")
+            time.sleep(0.1)
+        out = host.stdout.read()
+        if host.returncode:
+            raise RuntimeError(f"host rc {host.returncode} (see {logdir}/host.err)")
+        for n, p in procs:
+            p.wait(timeout=60)
+            if p.returncode:
+                raise RuntimeError(f"{n} rc {p.returncode} (see {logdir}/{n}.err)")
+        res = json.loads(out.strip().splitlines()[-1])
+        res["clients"], res["clients_lines"] = {}, {}
+        for cname, f in outs.items():
+            f.seek(0)
+            lines = [x for x in f.read().splitlines() if x.strip()]
+            res["clients"][cname] = json.loads(lines[-1]) if lines else None
+            res["clients_lines"][cname] = lines
+        return res
+    finally:
+        for n, p in procs:
+            if n == "svc" and p.poll() is None:
+                p.terminate()
+                try:
+                    p.wait(timeout=40)
+                except subprocess.TimeoutExpired:
+                    pass
+        for _, p in procs + [("host", host)]:
+            if p.poll() is None:
+                p.kill()
+                p.wait()
+        for f in files:
             f.close()
         if os.path.exists(shm):
             os.unlink(shm)
