@@ -607,13 +607,26 @@ def run_tile_leg(args):
         with tempfile.TemporaryDirectory() as td:
             stream = os.path.join(td, "stream.bin")
             s = TB.make_stream(args.tile_frags, stream)
-            logdir = os.path.join(td, "logs")
+            # FD_BENCH_TILE_LOGDIR: keep every run's process logs (a GPU box's gpurun_out/...)
+            logdir = os.environ.get("FD_BENCH_TILE_LOGDIR") or os.path.join(td, "logs")
             nrun = [0]
 
             def run(depth, env, rate=0):
                 nrun[0] += 1
                 e = dict(env, SVC_RUN_RATE=str(int(rate))) if rate else dict(env)
-                return SB.run_one(stream, tiles, depth, 180, os.path.join(logdir, f"run{nrun[0]}"), env=e, pin="auto")
+                rd = os.path.join(logdir, f"run{nrun[0]}")
+                try:
+                    return SB.run_one(stream, tiles, depth, 180, rd, env=e, pin="auto",
+                                      svc_env={"SVC_DEBUG_S": "10"})
+                except Exception as x:          # name the run and what its processes said last
+                    tails = {}
+                    for f in sorted(os.listdir(rd)) if os.path.isdir(rd) else []:
+                        with open(os.path.join(rd, f), errors="replace") as fh:
+                            t = fh.read()[-600:]
+                        if t.strip():
+                            tails[f] = t
+                    raise RuntimeError(f"run {nrun[0]} (depth {depth}, rate {int(rate)}, "
+                                       f"{ {k: v for k, v in env.items() if k != 'SVC_RUN_PRELAY'} }): {x}; logs: {tails}")
 
             def lat(r):
                 return {"offered_frags_per_s": int(r["offered_rate"]), "achieved_verifies_per_s": r["verifies_per_s"],

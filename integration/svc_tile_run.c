@@ -426,6 +426,16 @@ drv_malloc( ulong align, ulong sz ) {
 }
 
 static ulong           drv_share;           /* seqs of the stream this tile takes */
+/* the polled links: the stem's fseq for each (its consumed seq, written at
+   housekeeping) and the seq one past the link's last frag.  A polled
+   link's overruns are the stem's own (its link-in metrics count every
+   lapped frag, whichever tile's share it held), so a lapped tile cannot
+   count its share to the end: it is done once the stem has passed every
+   polled link's last seq (each frag processed, filtered or skipped) */
+static ulong           drv_polled_cnt;
+static ulong *         drv_polled_fseq[ SVC_RUN_LINK_MAX ];
+static ulong           drv_polled_end [ SVC_RUN_LINK_MAX ];
+static svc_run_hdr_t * drv_hdr;
 static long            drv_deadline;
 static svc_run_tile_res_t * drv_res;
 
@@ -448,7 +458,9 @@ drv_should_shutdown( void * _ctx ) {
   fd_verify_ctx_t * ctx = (fd_verify_ctx_t *)_ctx;
   ulong seen = drv_seen( ctx );
   if( FD_UNLIKELY( fd_log_wallclock()>drv_deadline ) ) FD_LOG_ERR(( "tile: %lu of %lu frags after the deadline", seen, drv_share ));
-  return seen>=drv_share && FD_VERIFY_SVC_IDLE( ctx );
+  int drained = drv_polled_cnt && drv_hdr->t_pub;             /* the producer is done publishing */
+  for( ulong k=0UL; drained && k<drv_polled_cnt; k++ ) drained = fd_fseq_query( drv_polled_fseq[ k ] )>=drv_polled_end[ k ];
+  return ( seen>=drv_share || drained ) && FD_VERIFY_SVC_IDLE( ctx );
 }
 
 /* threads of this process and its open device fds (the GPU test's check
@@ -536,7 +548,13 @@ tile( char const * path, ulong t ) {
   fd_frag_meta_t const * in_mcache[ SVC_RUN_LINK_MAX ];
   ulong *                in_fseqs [ SVC_RUN_LINK_MAX ];
   for( ulong l=0UL; l<L; l++ )                                  /* the stem's ins: the polled links, in link order */
-    if( ( polled_mask>>l )&1UL ) { in_mcache[ polled_cnt ] = quic[ l ]->mcache; in_fseqs[ polled_cnt ] = in_fseq[ l ]; polled_cnt++; }
+    if( ( polled_mask>>l )&1UL ) {
+      in_mcache[ polled_cnt ] = quic[ l ]->mcache; in_fseqs[ polled_cnt ] = in_fseq[ l ];
+      drv_polled_fseq[ polled_cnt ] = in_fseq[ l ];
+      drv_polled_end [ polled_cnt ] = ( hdr->n + L - 1UL - l )/L;   /* frags j = l mod L: seqs 0 .. end-1 */
+      polled_cnt++;
+    }
+  drv_polled_cnt = polled_cnt; drv_hdr = hdr;
   void * stem_scratch = aligned_alloc( FD_STEM_SCRATCH_ALIGN,
                                        fd_ulong_align_up( stem_scratch_footprint( polled_cnt, 1UL, 1UL ), FD_STEM_SCRATCH_ALIGN ) );
   fd_rng_t rng_mem[ 1 ];

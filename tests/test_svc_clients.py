@@ -111,3 +111,45 @@ def test_replay_tile_service_mode_has_no_hip():
     und = subprocess.run(["nm", "-u", o], capture_output=True, text=True, check=True).stdout
     assert "fd_sched_sigverify_claim" in und and "fd_sched_sigverify_claim_done" in und
     assert "hip" not in und.replace("fd_sched", ""), [x for x in und.split() if "hip" in x]
+
+
+REF = "/root/reference"
+
+
+@pytest.mark.skipif(not os.path.isdir(REF), reason="needs /root/reference")
+def test_shred_tile_patch_wires_the_burst(tmp_path):
+    """integration/fd_shred_tile_hip.patch on src/disco/shred/fd_shred_tile.c
+    (with the resolver patch): every line it adds sits in an FD_HAS_HIP_SVC
+    block (without it the tile is the reference's, line for line); with it,
+    the tile compiles -Wall -Wextra -Werror against the reference's headers,
+    attaches its resolver to the GPU 0 service as a client
+    (fd_fec_resolver_hip_attach_svc, memory from its scratch: the tile is
+    sandboxed when it makes its resolver), and before add_shred on a shred
+    of an unknown set (fd_fec_resolver_hip_needed) preverifies that shred
+    with the frags already published after it on its net link
+    (fd_fec_resolver_hip_preverify) -- and references nothing of the engine"""
+    import shutil
+    import subprocess
+    from test_ref_tile import _strip_svc
+    d = tmp_path / "src" / "disco" / "shred"
+    os.makedirs(d)
+    for f in ("fd_shred_tile.c", "fd_fec_resolver.c", "fd_fec_resolver.h"):
+        shutil.copy(os.path.join(REF, "src/disco/shred", f), d / f)
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    for p in ("fd_shred_tile_hip.patch", "fd_fec_resolver_hip.patch"):
+        subprocess.check_call(["patch", "-s", "-p1", "-i", os.path.join(repo, "integration", p)], cwd=tmp_path)
+    got = open(d / "fd_shred_tile.c").read().splitlines()
+    assert _strip_svc(got) == open(os.path.join(REF, "src/disco/shred/fd_shred_tile.c")).read().splitlines()
+    body = "\n".join(got)
+    for s_ in ("fd_fec_resolver_hip_attach_svc", "fd_fec_resolver_hip_needed", "fd_fec_resolver_hip_preverify",
+               "fd_fec_resolver_hip_svc_footprint", "verify_svc.shred_client_base"):
+        assert s_ in body, s_
+    flags = ["gcc", "-std=c17", "-O1", "-DFD_HAS_HOSTED=1", "-DFD_HAS_INT128=1", "-DFD_HAS_DOUBLE=1", "-DFD_HAS_ALLOCA=1",
+             "-DFD_HAS_X86=1", "-DFD_HAS_ATOMIC=1", "-DFD_HAS_THREADS=1", "-D_GNU_SOURCE", "-Wall", "-Wextra", "-Werror",
+             "-I" + str(d), "-I" + os.path.join(REF, "src/disco/shred"), "-I" + os.path.join(repo, "include")]
+    for svc in (0, 1):
+        o = str(tmp_path / f"shred{svc}.o")
+        subprocess.check_call(flags + ([f"-DFD_HAS_HIP_SVC=1"] if svc else []) + ["-c", str(d / "fd_shred_tile.c"), "-o", o])
+        und = subprocess.run(["nm", "-u", o], capture_output=True, text=True, check=True).stdout
+        assert ("fd_fec_resolver_hip_preverify" in und) == bool(svc) and ("fd_fec_resolver_hip_attach_svc" in und) == bool(svc)
+        assert "fd_ed25519_hip" not in und

@@ -239,3 +239,20 @@ def test_frags_shorter_than_their_payload_are_redone_on_the_tile(stream, tmp_pat
     assert r["host_redone"] == len(range(96, stream["s"].n, 97))
     assert r["tiles"][0]["gpu_metrics"]["host_redone"] == r["host_redone"] and r["metrics_ok"] == 1
 
+
+
+def test_lapped_polled_link_ends_the_run(tmp_path):
+    """an unreliable producer far ahead of a shallow polled link: the stem
+    skips the lapped frags itself (its link-in metrics count them, every
+    tile's share alike), so a tile cannot count its share to the end -- it
+    ends once the stem has passed the link's last seq, and the frags no tile
+    saw are reported as unseen (the bench's lost count).  Before round 6 such
+    a tile waited for its deadline: the paced polled bench runs timed out."""
+    from firedancer_amd.txn_workload import make_txn_stream
+    s = make_txn_stream(20000, T.oracle_signer, seed=0x7e6a)
+    p = str(tmp_path / "s.bin")
+    write_fdt1(p, s.pool, s.off, s.sz, np.zeros(s.n, np.uint64), SEED, DEPTH)
+    r = S.run(p, 2, 256, str(tmp_path / "run"), mock=True, timeout=120,
+              env={"SVC_RUN_POLLED": "1", "SVC_RUN_RATE": "50000000", "SVC_RUN_REQ_DEPTH": "16", "SVC_RUN_SLOT_CAP": "1024"})
+    assert r["unseen"] > 0 and r["frags"] + r["overrun"] + r["lapped"] + r["unseen"] == s.n, r
+    assert r["consumer_bad"] == 0 and r["consumed"] == r["published"]
