@@ -83,6 +83,8 @@ typedef uint64_t u64;
 #define SVC_FLUSH_Q       64ul   /* flushes in flight per tile */
 #define SVC_REGION_MAX    64ul
 #define SVC_ING_MAX       8ul    /* ingest batches in flight */
+#define SVC_FB_MAX        8ul    /* flush batches in flight */
+#define SVC_FB_FLUSH_MAX  512u   /* flushes per flush batch */
 #define SVC_DSM_RESERVE   128ul  /* DSM workgroup slots left free in the service's verify contexts */
 
 /* the device current on the calling thread (the service runs on one
@@ -296,6 +298,48 @@ void k_svc_compact( fd_verify_svc_out_t const * __restrict__ out, ulong m, u8 co
     }
     u8 const * src = stage + 64ul * (stage0 + FD_TXN_HIP_STAGE_CHUNKS * (ulong)o.idx);
     u8 *       dst = dcache + at;
+    for( u32 p = 16u * lane; p < len; p += 1024u ) *(uint4 *)(dst + p) = *(uint4 const *)(src + p);
+  }
+}
+
+/* one flush of a flush batch (64 B): k_svc_compact's arguments */
+struct __attribute__((aligned(16))) svc_fdesc {
+  u64 base;        /* the flush's first entry in the batch */
+  u64 out;         /* its out entries (device address) */
+  u64 stage0;
+  u64 dcache;      /* the tile's out dcache (device address) */
+  long delta;
+  u64 out_sz;
+  u64 err;         /* the tile's error flag (device address) */
+  u64 rsv;
+};
+static_assert( sizeof(svc_fdesc) == 64, "svc_fdesc layout" );
+
+/* a flush batch: the newly posted flushes of every tile in one launch
+   (one wave per out entry, as k_svc_compact; entry j of the batch is entry
+   j - base of the flush whose range holds it) */
+__global__ __launch_bounds__(256)
+void k_svc_compact_batch( svc_fdesc const * __restrict__ fd, u32 nf, ulong n, u8 const * __restrict__ stage,
+                          ulong slot_cap ) {
+  __shared__ u64 sbase[SVC_FB_FLUSH_MAX];
+  for( u32 i = threadIdx.x; i < nf; i += blockDim.x ) sbase[i] = fd[i].base;
+  __syncthreads();
+  u32 const lane = threadIdx.x & 63u;
+  for( ulong j = (ulong)blockIdx.x * 4ul + (threadIdx.x >> 6); j < n; j += 4ul * gridDim.x ) {
+    u32 lo = 0u, hi = nf;
+    while( hi - lo > 1u ) { u32 mid = (lo + hi) >> 1; if( sbase[mid] <= j ) lo = mid; else hi = mid; }
+    svc_fdesc const * d = fd + lo;
+    fd_verify_svc_out_t const o = ((fd_verify_svc_out_t const *)d->out)[j - sbase[lo]];
+    if( o.flags & FD_VERIFY_SVC_OUT_HOSTWRITTEN ) continue;
+    u32 const len = ((u32)o.sz + 63u) & ~63u;
+    long const at = (long)(64ul * (ulong)o.chunk) + d->delta;
+    /* the tile is an untrusted peer: k_svc_compact's checks */
+    if( (ulong)o.idx >= slot_cap || len > 64u * (u32)FD_TXN_HIP_STAGE_CHUNKS || at < 0 || at + (long)len > (long)d->out_sz ) {
+      if( lane == 0u ) *(volatile u32 *)d->err = 1u;
+      continue;
+    }
+    u8 const * src = stage + 64ul * (d->stage0 + FD_TXN_HIP_STAGE_CHUNKS * (ulong)o.idx);
+    u8 *       dst = (u8 *)d->dcache + at;
     for( u32 p = 16u * lane; p < len; p += 1024u ) *(uint4 *)(dst + p) = *(uint4 const *)(src + p);
   }
 }
@@ -858,6 +902,18 @@ struct svc_tile {
 
 struct svc_pend { ulong t, slot, n; long seen; };
 
+/* a flush batch: every tile's newly posted flushes (up to
+   SVC_FB_FLUSH_MAX) in one k_svc_compact_batch launch on the flush
+   stream; retired in order, each flush's tile advancing flush_done */
+struct svc_fbatch {
+  int         busy;
+  hipEvent_t  ev;
+  svc_fdesc * h_desc; svc_fdesc * d_desc;   /* mapped pinned memory */
+  u32         nf;
+  ulong       n;
+  u8          t[SVC_FB_FLUSH_MAX];          /* each flush's tile */
+};
+
 /* an ingest batch: the gather of newly posted requests, on the ingest stream */
 struct svc_ingest {
   int         busy;
@@ -887,6 +943,13 @@ struct fd_verify_svc {
   hipStream_t st_ing;
   svc_ingest ING[SVC_ING_MAX];
   ulong    ing_take, ing_fin;  /* ingest batches started / retired (ring order) */
+  /* flushes: batched over tiles on one stream (default), or one launch per
+     flush on each tile's stream (FD_VERIFY_SVC_FLUSH=tile, the round-5
+     form, for an A/B) */
+  int      flush_batch;
+  hipStream_t st_flush;
+  svc_fbatch FB[SVC_FB_MAX];
+  ulong    fb_take, fb_fin;
   svc_desc * sdesc;            /* per (tile, slot): the request's descriptor, made at ingest */
   svc_launch L[SVC_LAUNCH_MAX];
   svc_pend * pend; ulong pend_cap, pend_head, pend_tail, pend_frags;
@@ -1005,6 +1068,20 @@ fd_verify_svc_boot( void * seg_mem, int device, ulong batch_max, ulong inflight 
     SV_CHECK( hipHostGetDevicePointer( (void **)&I.d_desc, I.h_desc, 0 ) );
     SV_CHECK( hipEventCreate( &I.ev0 ) ); SV_CHECK( hipEventCreate( &I.ev1 ) );
   }
+  {
+    char const * e  = getenv( "FD_VERIFY_SVC_FLUSH" );
+    char const * io = getenv( "FD_VERIFY_SVC_IO" );          /* the IO engine flushes on its own grid */
+    s->flush_batch = !( e && !strcmp( e, "tile" ) ) && !( io && !strcmp( io, "io" ) );
+  }
+  if( s->flush_batch ) {
+    SV_CHECK( hipStreamCreateWithFlags( &s->st_flush, hipStreamNonBlocking ) );
+    for( ulong k = 0; k < SVC_FB_MAX; k++ ) {
+      svc_fbatch & F = s->FB[k];
+      SV_CHECK( hipHostMalloc( &F.h_desc, sizeof(svc_fdesc) * SVC_FB_FLUSH_MAX, hipHostMallocMapped ) );
+      SV_CHECK( hipHostGetDevicePointer( (void **)&F.d_desc, F.h_desc, 0 ) );
+      SV_CHECK( hipEventCreateWithFlags( &F.ev, hipEventDisableTiming ) );
+    }
+  }
   s->sdesc = (svc_desc *)calloc( seg->tile_cnt * seg->req_depth, sizeof(svc_desc) );
   for( ulong k = 0; k < inflight; k++ ) launch_alloc( s->L[k], device, batch_max );
   s->pend_cap = seg->tile_cnt * seg->req_depth;
@@ -1078,7 +1155,7 @@ fd_verify_svc_set_tile( fd_verify_svc_t * s, ulong t, void * out_dcache, ulong o
   /* the IO engine flushes on its own grid: no stream per tile (one stream
      fewer per tile also keeps the process's streams within its hardware
      queues, so no stream ever shares a queue with the persistent kernel) */
-  if( !s->io ) {
+  if( !s->io && !s->flush_batch ) {
     SV_CHECK( hipStreamCreateWithFlags( &T.st, hipStreamNonBlocking ) );
     for( ulong k = 0; k < SVC_FLUSH_Q; k++ ) SV_CHECK( hipEventCreateWithFlags( &T.ev[k], hipEventDisableTiming ) );
   }
@@ -1140,7 +1217,12 @@ fd_verify_svc_run( fd_verify_svc_t * s ) {
   hipLaunchKernelGGL( k_svc_gather, dim3( 1 ), dim3( 256 ), 0, s->st_ing, s->ING[0].d_desc, 0u, 0ul, s->d_ing, s->d_ing_sz,
                       s->d_ing_kind, s->d_ing_tso, s->d_stage );
   SV_CHECK( hipGetLastError() );
-  for( ulong t = 0; t < s->seg->tile_cnt && !s->io; t++ ) {
+  if( s->flush_batch ) {
+    hipLaunchKernelGGL( k_svc_compact_batch, dim3( 1 ), dim3( 256 ), 0, s->st_flush, s->FB[0].d_desc, 0u, 0ul,
+                        (u8 const *)s->d_stage, s->seg->slot_cap );
+    SV_CHECK( hipGetLastError() );
+  }
+  for( ulong t = 0; t < s->seg->tile_cnt && !s->io && !s->flush_batch; t++ ) {
     if( s->tile[t].client ) continue;
     hipLaunchKernelGGL( k_svc_compact, dim3( 1 ), dim3( 256 ), 0, s->tile[t].st, (fd_verify_svc_out_t const *)0, 0ul,
                         (u8 const *)s->d_stage, 0ul, s->tile[t].d_out, 0L, 0ul, s->seg->slot_cap, s->tile[t].d_err );
@@ -1347,6 +1429,50 @@ svc_flush_start( fd_verify_svc_t * s, ulong t, fd_verify_svc_flush_t const * f )
   s->stat[3]++; s->stat[4] += m;
 }
 
+/* the newly posted flushes of every tile (each tile's in order) into one
+   k_svc_compact_batch launch; 1 if it started one */
+static int
+svc_flush_batch_start( fd_verify_svc_t * s, svc_fbatch & F ) {
+  fd_verify_svc_seg_t * g = s->seg;
+  F.nf = 0; F.n = 0;
+  for( ulong t = 0; t < g->tile_cnt && F.nf < SVC_FB_FLUSH_MAX; t++ ) {
+    svc_tile & T = s->tile[t];
+    if( T.client ) continue;
+    fd_verify_svc_tile_t * b = fd_verify_svc_tile( g, t );
+    ulong const post = fd_verify_svc_ld( &b->flush_post );
+    while( T.flush_take < post && F.nf < SVC_FB_FLUSH_MAX ) {
+      fd_verify_svc_flush_t const * f = &b->flush[T.flush_take % FD_VERIFY_SVC_FLUSH_DEPTH];
+      if( f->slot >= g->req_depth || f->lo > f->hi || f->hi > g->slot_cap ) {
+        fprintf( stderr, "fd_verify_svc: tile %lu: bad flush (slot %lu [%lu,%lu))\n", t, f->slot, f->lo, f->hi );
+        abort();
+      }
+      ulong const m = f->hi - f->lo;
+      svc_fdesc & d = F.h_desc[F.nf];
+      d.base = F.n;
+      d.out = m ? (u64)svc_dev( s, fd_verify_svc_out( g, t, f->slot ) + f->lo, m * sizeof(fd_verify_svc_out_t) ) : 0ul;
+      d.stage0 = svc_stage0( s, t, f->slot ); d.dcache = (u64)T.d_out; d.delta = (long)(T.chunk_base - T.h_out);
+      d.out_sz = T.out_sz; d.err = (u64)T.d_err; d.rsv = 0;
+      F.t[F.nf] = (u8)t;
+      F.nf++; F.n += m;
+      T.flush_take++;
+      s->stat[3]++; s->stat[4] += m;
+    }
+  }
+  if( !F.nf ) return 0;
+  svc_device( s->dev );
+  if( F.n ) {
+    ulong wgs = (F.n + 3ul) / 4ul;
+    if( s->flush_wgs && wgs > s->flush_wgs ) wgs = s->flush_wgs;
+    hipLaunchKernelGGL( k_svc_compact_batch, dim3( (unsigned)wgs ), dim3( 256 ), 0, s->st_flush, F.d_desc, F.nf, F.n,
+                        (u8 const *)s->d_stage, g->slot_cap );
+    SV_CHECK( hipGetLastError() );
+    s->stat[6]++;
+  }
+  SV_CHECK( hipEventRecord( F.ev, s->st_flush ) );
+  F.busy = 1;
+  return 1;
+}
+
 extern "C" int fd_verify_svc_debug( fd_verify_svc_t const * s, char * buf, ulong sz );
 
 extern "C" int
@@ -1467,7 +1593,24 @@ fd_verify_svc_poll( fd_verify_svc_t * s ) {
     I.busy = 0; s->ing_fin++; did = 1;
   }
   /* 2. flushes: retire in order, start the newly posted */
-  for( ulong t = 0; t < g->tile_cnt && !s->io; t++ ) {
+  while( s->flush_batch && s->fb_fin < s->fb_take ) {
+    svc_fbatch & F = s->FB[s->fb_fin % SVC_FB_MAX];
+    hipError_t e = hipEventQuery( F.ev );
+    if( e == hipErrorNotReady ) break;
+    SV_CHECK( e );
+    for( u32 i = 0; i < F.nf; i++ ) {
+      ulong const t = F.t[i];
+      svc_tile & T = s->tile[t];
+      if( *(volatile u32 *)T.h_err ) {
+        fprintf( stderr, "fd_verify_svc: tile %lu: a flush entry's chunks lie outside the out dcache\n", t );
+        abort();
+      }
+      T.flush_fin++;
+      fd_verify_svc_st( &fd_verify_svc_tile( g, t )->flush_done, T.flush_fin );
+    }
+    F.busy = 0; s->fb_fin++; did = 1;
+  }
+  for( ulong t = 0; t < g->tile_cnt && !s->io && !s->flush_batch; t++ ) {
     svc_tile & T = s->tile[t];
     if( T.client ) continue;
     fd_verify_svc_tile_t * b = fd_verify_svc_tile( g, t );
@@ -1493,10 +1636,14 @@ fd_verify_svc_poll( fd_verify_svc_t * s ) {
       if( post ) { fprintf( stderr, "fd_verify_svc: tile %lu is a client and posted a flush\n", t ); abort(); }
       continue;
     }
+    if( s->flush_batch ) continue;
     while( T.flush_take < post && T.flush_take - T.flush_fin < SVC_FLUSH_Q ) {
       svc_flush_start( s, t, &b->flush[T.flush_take % FD_VERIFY_SVC_FLUSH_DEPTH] );
       T.flush_take++; did = 1;
     }
+  }
+  if( s->flush_batch && !s->io && s->fb_take - s->fb_fin < SVC_FB_MAX ) {
+    if( svc_flush_batch_start( s, s->FB[s->fb_take % SVC_FB_MAX] ) ) { s->fb_take++; did = 1; }
   }
   long const p2 = svc_now_ns();
   s->stat[9] += (ulong)(p2 - p1);
@@ -1655,15 +1802,16 @@ fd_verify_svc_delete( fd_verify_svc_t * s ) {
     svc_drain( s->st_ing, s->io_ev, "the IO engine (k_svc_io)", 0ul, s );
   }
   for( ulong k = 0; k < s->inflight; k++ ) if( s->L[k].ctx ) svc_drain( s->L[k].st, 0, "verify launch stream", k, s );
-  for( ulong t = 0; t < FD_VERIFY_SVC_TILE_MAX && !s->io; t++ )
+  for( ulong t = 0; t < FD_VERIFY_SVC_TILE_MAX && !s->io && !s->flush_batch; t++ )
     if( s->tile[t].set && !s->tile[t].client ) svc_drain( s->tile[t].st, 0, "flush stream of tile", t, s );
+  if( s->flush_batch ) svc_drain( s->st_flush, 0, "flush stream", 0ul, s );
   if( s->st_ing && !s->io ) svc_drain( s->st_ing, 0, "ingest stream", 0ul, s );
   (void)hipDeviceSynchronize();
   for( ulong k = 0; k < SVC_LAUNCH_MAX; k++ ) launch_free( s->L[k] );
   for( ulong t = 0; t < FD_VERIFY_SVC_TILE_MAX; t++ ) {
     svc_tile & T = s->tile[t];
     if( !T.set ) continue;
-    if( !s->io && !T.client ) {
+    if( !s->io && !T.client && !s->flush_batch ) {
       (void)hipStreamDestroy( T.st );
       for( ulong k = 0; k < SVC_FLUSH_Q; k++ ) (void)hipEventDestroy( T.ev[k] );
     }
@@ -1680,6 +1828,13 @@ fd_verify_svc_delete( fd_verify_svc_t * s ) {
     (void)hipHostFree( I.h_desc ); (void)hipEventDestroy( I.ev0 ); (void)hipEventDestroy( I.ev1 );
   }
   if( s->st_ing ) (void)hipStreamDestroy( s->st_ing );
+  if( s->flush_batch ) {
+    for( ulong k = 0; k < SVC_FB_MAX; k++ ) {
+      if( !s->FB[k].h_desc ) continue;
+      (void)hipHostFree( s->FB[k].h_desc ); (void)hipEventDestroy( s->FB[k].ev );
+    }
+    (void)hipStreamDestroy( s->st_flush );
+  }
   free( s->sdesc );
   for( ulong k = 0; k < s->nreg; k++ ) (void)hipHostUnregister( s->reg[k].h );
   fd_verify_svc_st( &s->seg->svc_state, FD_VERIFY_SVC_SVC_STOPPED );
