@@ -116,7 +116,8 @@ struct __attribute__((aligned(16))) svc_desc {
   u64 stage0;      /* staging chunk of the request's frag 0 */
   u64 ibase;       /* ingest frag of the request's frag 0 (slot (t, s): (t x req_depth + s) x slot_cap) */
   u64 res;         /* the slot's result array in the segment (device address; verify launches) */
-  u64 rsv[1];
+  u64 state;       /* the request slot's state word in the segment (device address; ingests: the kernel's last
+                      workgroup stores INGESTED there itself) */
 };
 static_assert( sizeof(svc_desc) == 128, "svc_desc layout" );
 
@@ -126,7 +127,7 @@ static_assert( sizeof(svc_desc) == 128, "svc_desc layout" );
 __global__ __launch_bounds__(256)
 void k_svc_gather( svc_desc const * __restrict__ desc, u32 nreq, ulong n, u8 * __restrict__ ing,
                    u16 * __restrict__ ing_sz, u8 * __restrict__ ing_kind, u32 * __restrict__ ing_tso,
-                   u8 * __restrict__ stage ) {
+                   u8 * __restrict__ stage, u32 * __restrict__ done_ctr ) {
   __shared__ u64 sbase[SVC_REQ_MAX];
   for( u32 i = threadIdx.x; i < nreq; i += blockDim.x ) sbase[i] = desc[i].base;
   __syncthreads();
@@ -170,6 +171,28 @@ void k_svc_gather( svc_desc const * __restrict__ desc, u32 nreq, ulong n, u8 * _
       *(uint4 *)(stage + 64ul * (d->stage0 + FD_TXN_HIP_STAGE_CHUNKS * i) + 16u * lane) = make_uint4( 0u, 0u, 0u, 0u );
     if( lane == 0u ) { ing_sz[f] = ok ? (u16)sz : (u16)0xffffu; ing_kind[f] = (u8)kind; ing_tso[f] = tsv; }
   }
+  /* INGESTED from the GPU: once every workgroup has passed its loop (all of
+     its loads from the links have returned), the last one stores INGESTED
+     into each request's slot in the segment, so a tile may reuse its link
+     without waiting for the service thread's turn (the service still
+     retires the batch by its event before a verify launch reads the HBM
+     frags).  done_ctr: this batch's counter, zero at launch; the last
+     workgroup puts it back to zero for the next batch on the ingest stream */
+  /* Only the links' reads must be over (their values were stored, so they
+     have returned): no fence, and relaxed stores -- a system-scope release
+     here would write the whole L2 back (the verify kernels' dirty lines
+     included) once per request, which measured slower than the host's
+     turn it saves */
+  if( !done_ctr ) return;
+  __syncthreads();
+  __shared__ u32 last;
+  if( threadIdx.x == 0u ) last = atomicAdd( done_ctr, 1u ) == gridDim.x - 1u;
+  __syncthreads();
+  if( !last ) return;
+  for( u32 i = threadIdx.x; i < nreq; i += blockDim.x )
+    if( desc[i].state )
+      __hip_atomic_store( (u64 *)desc[i].state, (u64)FD_VERIFY_SVC_INGESTED, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM );
+  if( threadIdx.x == 0u ) *done_ctr = 0u;
 }
 
 /* a verify launch's per-frag arrays (launch frag j = frag i of request d)
@@ -943,6 +966,7 @@ struct fd_verify_svc {
   hipStream_t st_ing;
   svc_ingest ING[SVC_ING_MAX];
   ulong    ing_take, ing_fin;  /* ingest batches started / retired (ring order) */
+  u32 *    d_ing_ctr;          /* per ingest batch slot: k_svc_gather's workgroups done (HBM, zero between batches) */
   /* flushes: batched over tiles on one stream (default), or one launch per
      flush on each tile's stream (FD_VERIFY_SVC_FLUSH=tile, the round-5
      form, for an A/B) */
@@ -1002,6 +1026,31 @@ static void launch_alloc( svc_launch & L, int dev, ulong nmax ) {
      72.1 vs 69.0 M, 2 tiles 67.6 vs 66.9 M); per context, so that no other
      context of the process inherits it; the environment's value wins */
   if( !getenv( "FD_ED25519_HIP_DSM_RESERVE" ) ) (void)fd_ed25519_hip_ctx_set_dsm_reserve( L.ctx, SVC_DSM_RESERVE );
+  /* FD_VERIFY_SVC_FREE_CUS=k: the verify launches' stream on all CUs but
+     k (every (cus/k)-th), so that the ingest and flush kernels always find
+     CUs no verify kernel holds -- a link's frags wait for the gather, and a
+     one-shot verify kernel (prep, parse) fills every CU it may use for up to
+     ~1 ms */
+  {
+    char const * e = getenv( "FD_VERIFY_SVC_FREE_CUS" );
+    ulong k = e ? strtoul( e, 0, 0 ) : 0ul;
+    if( k ) {
+      hipDeviceProp_t prop;
+      SV_CHECK( hipGetDeviceProperties( &prop, dev ) );
+      ulong const cus = (ulong)prop.multiProcessorCount, step = k < cus ? cus / k : 1ul;
+      uint mask[16]; memset( mask, 0, sizeof(mask) );
+      ulong freed = 0;
+      for( ulong c = 0; c < cus && c < 512ul; c++ ) {
+        bool const keep = !( (c % step) == step - 1ul && freed < k );
+        if( !keep ) freed++;
+        if( keep ) mask[c >> 5] |= 1u << (c & 31ul);
+      }
+      if( fd_ed25519_hip_ctx_set_cu_mask( L.ctx, mask, (uint)((cus + 31ul) / 32ul) ) ) {
+        fprintf( stderr, "fd_verify_svc: the verify stream's CU mask (%lu of %lu CUs free) failed\n", k, cus );
+        abort();
+      }
+    }
+  }
   L.st = (hipStream_t)fd_ed25519_hip_ctx_stream( L.ctx );
   SV_CHECK( hipMalloc( &L.d_in_chunk, 4ul * nmax ) ); SV_CHECK( hipMalloc( &L.d_in_sz, 2ul * nmax ) );
   SV_CHECK( hipMalloc( &L.d_in_kind, nmax ) );        SV_CHECK( hipMalloc( &L.d_tso, 4ul * nmax ) );
@@ -1061,6 +1110,7 @@ fd_verify_svc_boot( void * seg_mem, int device, ulong batch_max, ulong inflight 
   SV_CHECK( hipMalloc( &s->d_ing, 64ul * SVC_INGEST_CHUNKS * ing_cnt + 4096ul ) );
   SV_CHECK( hipMalloc( &s->d_ing_sz, 2ul * ing_cnt ) ); SV_CHECK( hipMalloc( &s->d_ing_kind, ing_cnt ) );
   SV_CHECK( hipMalloc( &s->d_ing_tso, 4ul * ing_cnt ) );
+  SV_CHECK( hipMalloc( &s->d_ing_ctr, 4ul * SVC_ING_MAX ) ); SV_CHECK( hipMemset( s->d_ing_ctr, 0, 4ul * SVC_ING_MAX ) );
   SV_CHECK( hipStreamCreateWithFlags( &s->st_ing, hipStreamNonBlocking ) );
   for( ulong k = 0; k < SVC_ING_MAX; k++ ) {
     svc_ingest & I = s->ING[k];
@@ -1215,7 +1265,7 @@ fd_verify_svc_run( fd_verify_svc_t * s ) {
     SV_CHECK( hipGetLastError() );
   }
   hipLaunchKernelGGL( k_svc_gather, dim3( 1 ), dim3( 256 ), 0, s->st_ing, s->ING[0].d_desc, 0u, 0ul, s->d_ing, s->d_ing_sz,
-                      s->d_ing_kind, s->d_ing_tso, s->d_stage );
+                      s->d_ing_kind, s->d_ing_tso, s->d_stage, (u32 *)0 );
   SV_CHECK( hipGetLastError() );
   if( s->flush_batch ) {
     hipLaunchKernelGGL( k_svc_compact_batch, dim3( 1 ), dim3( 256 ), 0, s->st_flush, s->FB[0].d_desc, 0u, 0ul,
@@ -1284,6 +1334,7 @@ svc_desc_of( fd_verify_svc_t * s, ulong t, ulong slot, ulong base, svc_desc & d 
   memset( &d, 0, sizeof(d) );
   d.base = base; d.n = r->n; d.kind = r->kind; d.seed = r->seed; d.stage0 = svc_stage0( s, t, slot );
   d.ibase = (t * g->req_depth + slot) * g->slot_cap;
+  d.state = (u64)svc_dev( s, &r->state, sizeof(ulong) );
   if( s->tile[t].client != ( r->kind == FD_VERIFY_SVC_REQ_SIGS ) ) {
     /* a client posts signature records only, a verify tile never does */
     fprintf( stderr, "fd_verify_svc: tile %lu slot %lu: request kind %lu from a %s\n", t, slot, r->kind,
@@ -1395,7 +1446,8 @@ svc_ingest_start( fd_verify_svc_t * s, svc_ingest & I ) {
   ulong wgs = (I.n + 3ul) / 4ul;
   if( s->gather_wgs && wgs > s->gather_wgs ) wgs = s->gather_wgs;
   hipLaunchKernelGGL( k_svc_gather, dim3( (unsigned)wgs ), dim3( 256 ), 0, s->st_ing, I.d_desc,
-                      (u32)I.nreq, I.n, s->d_ing, s->d_ing_sz, s->d_ing_kind, s->d_ing_tso, s->d_stage );
+                      (u32)I.nreq, I.n, s->d_ing, s->d_ing_sz, s->d_ing_kind, s->d_ing_tso, s->d_stage,
+                      s->d_ing_ctr + (s->ing_take % SVC_ING_MAX) );
   SV_CHECK( hipGetLastError() );
   SV_CHECK( hipEventRecord( I.ev1, s->st_ing ) );
   I.busy = 1;
@@ -1578,8 +1630,10 @@ fd_verify_svc_poll( fd_verify_svc_t * s ) {
     float ms = 0.f;
     SV_CHECK( hipEventElapsedTime( &ms, I.ev0, I.ev1 ) );
     s->stat[13] += (ulong)((double)ms * 1e6);
+    /* the gather's last workgroup has stored INGESTED into each slot (the
+       tiles learn it from the GPU, not from this turn); here they join the
+       launch queues */
     for( ulong r = 0; r < I.nreq; r++ ) {
-      fd_verify_svc_st( &fd_verify_svc_req( g, I.req[r].t, I.req[r].slot )->state, FD_VERIFY_SVC_INGESTED );
       if( I.h_desc[r].kind == FD_VERIFY_SVC_REQ_SIGS ) {
         svc_pend & p = s->spend[s->spend_tail % s->pend_cap];
         p.t = I.req[r].t; p.slot = I.req[r].slot; p.n = I.h_desc[r].n; p.seen = now0;
@@ -1592,7 +1646,42 @@ fd_verify_svc_poll( fd_verify_svc_t * s ) {
     }
     I.busy = 0; s->ing_fin++; did = 1;
   }
-  /* 2. flushes: retire in order, start the newly posted */
+  long const p1 = svc_now_ns();
+  s->stat[10] += (ulong)(p1 - p0);
+  /* 2. posted requests, in each tile's ring order, into one ingest batch
+     (a request waits while every ingest slot is busy) -- before the
+     flushes: a range request holds its link until its gather has read it */
+  if( !s->io && s->ing_take - s->ing_fin < SVC_ING_MAX ) {
+    svc_ingest & I = s->ING[s->ing_take % SVC_ING_MAX];
+    I.nreq = 0; I.n = 0;
+    for( ulong t = 0; t < g->tile_cnt && I.nreq < SVC_REQ_MAX; t++ ) {
+      svc_tile & T = s->tile[t];
+      while( I.nreq < SVC_REQ_MAX ) {
+        ulong slot = T.take & (g->req_depth - 1ul);
+        fd_verify_svc_req_t * q = fd_verify_svc_req( g, t, slot );
+        if( fd_verify_svc_ld( &q->state ) != FD_VERIFY_SVC_POSTED ) break;
+        if( q->id + g->req_depth == T.take ) break;          /* the slot's previous request, still on the GPU */
+        if( q->id != T.take ) {
+          fprintf( stderr, "fd_verify_svc: tile %lu posted request %lu in slot %lu, expected %lu\n", t, q->id, slot, T.take );
+          abort();
+        }
+        T.take++; did = 1;
+        if( !q->n ) {                                        /* nothing to verify: results at once */
+          q->batch_frags = 0; fd_verify_svc_st( &q->state, FD_VERIFY_SVC_RESULTS );
+          continue;
+        }
+        svc_desc & d = s->sdesc[t * g->req_depth + slot];
+        svc_desc_of( s, t, slot, I.n, d );
+        I.h_desc[I.nreq] = d;
+        I.req[I.nreq].t = t; I.req[I.nreq].slot = slot;
+        I.nreq++; I.n += q->n;
+      }
+    }
+    if( I.nreq ) { svc_ingest_start( s, I ); s->ing_take++; }
+  }
+  long const p2 = svc_now_ns();
+  s->stat[14] += (ulong)(p2 - p1);
+  /* 3. flushes: retire in order, start the newly posted */
   while( s->flush_batch && s->fb_fin < s->fb_take ) {
     svc_fbatch & F = s->FB[s->fb_fin % SVC_FB_MAX];
     hipError_t e = hipEventQuery( F.ev );
@@ -1626,8 +1715,7 @@ fd_verify_svc_poll( fd_verify_svc_t * s ) {
       fd_verify_svc_st( &b->flush_done, T.flush_fin );
     }
   }
-  long const p1 = svc_now_ns();
-  s->stat[10] += (ulong)(p1 - p0);
+
   for( ulong t = 0; t < g->tile_cnt && !s->io; t++ ) {
     svc_tile & T = s->tile[t];
     fd_verify_svc_tile_t * b = fd_verify_svc_tile( g, t );
@@ -1645,40 +1733,8 @@ fd_verify_svc_poll( fd_verify_svc_t * s ) {
   if( s->flush_batch && !s->io && s->fb_take - s->fb_fin < SVC_FB_MAX ) {
     if( svc_flush_batch_start( s, s->FB[s->fb_take % SVC_FB_MAX] ) ) { s->fb_take++; did = 1; }
   }
-  long const p2 = svc_now_ns();
-  s->stat[9] += (ulong)(p2 - p1);
-  /* 3. posted requests, in each tile's ring order, into one ingest batch
-     (a request waits while every ingest slot is busy) */
-  if( !s->io && s->ing_take - s->ing_fin < SVC_ING_MAX ) {
-    svc_ingest & I = s->ING[s->ing_take % SVC_ING_MAX];
-    I.nreq = 0; I.n = 0;
-    for( ulong t = 0; t < g->tile_cnt && I.nreq < SVC_REQ_MAX; t++ ) {
-      svc_tile & T = s->tile[t];
-      while( I.nreq < SVC_REQ_MAX ) {
-        ulong slot = T.take & (g->req_depth - 1ul);
-        fd_verify_svc_req_t * q = fd_verify_svc_req( g, t, slot );
-        if( fd_verify_svc_ld( &q->state ) != FD_VERIFY_SVC_POSTED ) break;
-        if( q->id + g->req_depth == T.take ) break;          /* the slot's previous request, still on the GPU */
-        if( q->id != T.take ) {
-          fprintf( stderr, "fd_verify_svc: tile %lu posted request %lu in slot %lu, expected %lu\n", t, q->id, slot, T.take );
-          abort();
-        }
-        T.take++; did = 1;
-        if( !q->n ) {                                        /* nothing to verify: results at once */
-          q->batch_frags = 0; fd_verify_svc_st( &q->state, FD_VERIFY_SVC_RESULTS );
-          continue;
-        }
-        svc_desc & d = s->sdesc[t * g->req_depth + slot];
-        svc_desc_of( s, t, slot, I.n, d );
-        I.h_desc[I.nreq] = d;
-        I.req[I.nreq].t = t; I.req[I.nreq].slot = slot;
-        I.nreq++; I.n += q->n;
-      }
-    }
-    if( I.nreq ) { svc_ingest_start( s, I ); s->ing_take++; }
-  }
   long const now = svc_now_ns();
-  s->stat[14] += (ulong)(now - p2);
+  s->stat[9] += (ulong)(now - p2);
   /* 4. a verify launch: when the ingested frags fill its merge target, or
      the oldest has waited merge_wait_ns, or (the GPU idle) merge_idle_ns --
      large launches while the GPU is busy (a 55 K-signature launch runs ~one
@@ -1822,6 +1878,7 @@ fd_verify_svc_delete( fd_verify_svc_t * s ) {
   }
   (void)hipFree( s->d_stage );
   (void)hipFree( s->d_ing ); (void)hipFree( s->d_ing_sz ); (void)hipFree( s->d_ing_kind ); (void)hipFree( s->d_ing_tso );
+  (void)hipFree( s->d_ing_ctr );
   for( ulong k = 0; k < SVC_ING_MAX; k++ ) {
     svc_ingest & I = s->ING[k];
     if( !I.h_desc ) continue;

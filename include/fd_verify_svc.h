@@ -76,6 +76,8 @@
    Plain C (gcc and hipcc), no HIP types.  Library (service side only):
    firedancer_amd/libfd_ed25519_hip.so. */
 
+#include <string.h>
+
 #ifdef __cplusplus
 extern "C" {
 #endif
@@ -419,9 +421,7 @@ fd_verify_svc_client_add( fd_verify_svc_client_t * c, uchar const * sig, uchar c
   }
   ulong i = c->open_n;
   uchar * f = fd_verify_svc_frag( s, c->t, slot ) + i*FD_VERIFY_SVC_FRAG_STRIDE;
-  for( ulong k=0UL; k<64UL; k++ ) f[ k ] = sig[ k ];
-  for( ulong k=0UL; k<32UL; k++ ) f[ 64UL+k ] = pub[ k ];
-  for( ulong k=0UL; k<msg_sz; k++ ) f[ 96UL+k ] = msg[ k ];
+  memcpy( f, sig, 64UL ); memcpy( f+64UL, pub, 32UL ); memcpy( f+96UL, msg, msg_sz );
   fd_verify_svc_frag_sz  ( s, c->t, slot )[ i ] = (ushort)( FD_VERIFY_SVC_SIG_HDR_SZ + msg_sz );
   fd_verify_svc_frag_kind( s, c->t, slot )[ i ] = 0;
   fd_verify_svc_out( s, c->t, slot )[ i ].idx = tag;

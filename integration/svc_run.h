@@ -33,6 +33,8 @@ typedef struct {
   volatile double sec_pub, sec_pass, sec_flush, sec_post;   /* the tile's time in before_credit's steps */
   volatile ulong m_sigs, m_host;               /* the VERIFY_GPU_SIGNATURES / _HOST_REDONE metric slots */
   volatile ulong m_ing_n, m_ing_sum, m_batch_n, m_batch_sum;   /* the two GPU latency histograms' samples and sums (ns) */
+  volatile ulong ing_p50, ing_p99, ing_max;    /* post -> INGESTED as the tile saw it (ns; bucket right edges; max: the
+                                                  highest nonempty bucket's) */
 } svc_run_tile_res_t;
 
 typedef struct {

@@ -362,13 +362,15 @@ produce( char const * path, char const * stream, ulong tile_cnt, ulong in_depth 
             "\"overrun_reading\": %lu, \"overrun_reading_frags\": %lu}, "
             "\"busy_s\": {\"publish\": %.4f, \"pass\": %.4f, \"flush\": %.4f, \"post\": %.4f}, \"early_credits\": %lu, "
             "\"gpu_metrics\": {\"signatures\": %lu, \"host_redone\": %lu, \"ingest_n\": %lu, \"ingest_mean_us\": %.1f, "
-            "\"batch_n\": %lu, \"batch_mean_us\": %.1f}}",
+            "\"batch_n\": %lu, \"batch_mean_us\": %.1f, \"ingest_p50_us\": %.1f, \"ingest_p99_us\": %.1f, "
+            "\"ingest_max_us\": %.1f}}",
             t ? ", " : "", r->frags, r->sigs, r->pub, r->parse, r->verify, r->dedup, r->bundle, r->overrun, r->lapped,
             (double)( r->t_end - t0 )*1e-9, c->frags, c->digest, r->threads, r->dev_fds, r->metrics_ok, r->sandboxed,
             r->link_consumed, r->link_filtered, r->link_ovr_poll, r->link_ovr_poll_frags, r->link_ovr_read,
             r->link_ovr_read_frags, r->sec_pub, r->sec_pass, r->sec_flush, r->sec_post, r->early,
             r->m_sigs, r->m_host, r->m_ing_n, r->m_ing_n ? 1e-3*(double)r->m_ing_sum/(double)r->m_ing_n : 0.0,
-            r->m_batch_n, r->m_batch_n ? 1e-3*(double)r->m_batch_sum/(double)r->m_batch_n : 0.0 );
+            r->m_batch_n, r->m_batch_n ? 1e-3*(double)r->m_batch_sum/(double)r->m_batch_n : 0.0,
+            1e-3*(double)r->ing_p50, 1e-3*(double)r->ing_p99, 1e-3*(double)r->ing_max );
   }
   double s  = (double)( t_end - t0 )*1e-9;
   double rt = (double)( reg[0]+reg[1]+reg[2]+reg[3]+reg[4]+reg[5]+reg[6]+reg[7] ) + 1e-9;
@@ -644,6 +646,11 @@ tile( char const * path, ulong t ) {
     bn  += fd_metrics_tl[ MIDX( HISTOGRAM, VERIFY, GPU_BATCH_LATENCY_NANOS  ) + k ];
   }
   r->m_ing_n = in_; r->m_batch_n = bn;
+  r->ing_p50 = fd_histf_percentile( ctx->svc_ing_hist, 50, 0UL );
+  r->ing_p99 = fd_histf_percentile( ctx->svc_ing_hist, 99, 0UL );
+  r->ing_max = 0UL;
+  for( ulong k=0UL; k<fd_histf_bucket_cnt( ctx->svc_ing_hist ); k++ )
+    if( fd_histf_cnt( ctx->svc_ing_hist, k ) ) r->ing_max = fd_histf_right( ctx->svc_ing_hist, k );
   r->m_ing_sum   = FD_MHIST_SUM( VERIFY, GPU_INGEST_LATENCY_NANOS );
   r->m_batch_sum = FD_MHIST_SUM( VERIFY, GPU_BATCH_LATENCY_NANOS );
   ok &= r->m_sigs==ctx->svc_sig_cnt && r->m_host==ctx->svc_host_cnt;
