@@ -60,6 +60,8 @@
 #include <stdlib.h>
 #include <string.h>
 #include <time.h>
+#include <pthread.h>
+#include <sched.h>
 
 #define SV_CHECK( x ) do {                                                            \
     hipError_t e_ = (x);                                                               \
@@ -923,7 +925,7 @@ struct svc_tile {
   ulong        flush_fin;      /* flushes retired */
 };
 
-struct svc_pend { ulong t, slot, n; long seen; };
+struct svc_pend { ulong t, slot, n; long seen; ulong sig; };
 
 /* a flush batch: every tile's newly posted flushes (up to
    SVC_FB_FLUSH_MAX) in one k_svc_compact_batch launch on the flush
@@ -1001,6 +1003,20 @@ struct fd_verify_svc {
   u8 *     d_vd;
   hipEvent_t io_ev;            /* recorded behind k_svc_io: the grid has drained */
   ulong    pend_take[FD_VERIFY_SVC_TILE_MAX];   /* next request id of each tile to merge */
+  /* the ingest side (steps 1b and 2 of the poll: retire finished gathers,
+     gather newly posted requests) on a thread of its own when the process
+     may run on two or more CPUs (FD_VERIFY_SVC_INGEST_THREAD=0 keeps it on
+     the service thread): a range request holds its link until its gather
+     has read it, and on one thread a new request waited behind the flush
+     and launch work of every other tile (profiles/r06/gpu_ingested: the
+     service thread's ingest and flush turns filled the run).  Ingested
+     requests reach the launch queues through ih, a single-producer
+     single-consumer ring (ih_tail: stored by the ingest side with release;
+     sdesc is written before it) */
+  int      ithread;            /* the ingest thread runs */
+  pthread_t ith;
+  int      istop;
+  svc_pend * ih; ulong ih_cap; ulong ih_tail, ih_head;
   long     launch_t0[SVC_LAUNCH_MAX];           /* a verify launch's start (the stuck-launch watchdog) */
 };
 
@@ -1137,6 +1153,8 @@ fd_verify_svc_boot( void * seg_mem, int device, ulong batch_max, ulong inflight 
   s->pend_cap = seg->tile_cnt * seg->req_depth;
   s->pend = (svc_pend *)calloc( s->pend_cap, sizeof(svc_pend) );
   s->spend = (svc_pend *)calloc( s->pend_cap, sizeof(svc_pend) );
+  s->ih_cap = s->pend_cap;                          /* a slot's request is in the handoff ring at most once */
+  s->ih = (svc_pend *)calloc( s->ih_cap, sizeof(svc_pend) );
   { char const * e = getenv( "FD_VERIFY_SVC_IO" ); s->io = e && !strcmp( e, "io" ); }
   { char const * e = getenv( "FD_VERIFY_SVC_IO_WGS" ); s->io_wgs = e ? strtoul( e, 0, 0 ) : IO_WGS; }
   if( s->io_wgs < 2ul || s->io_wgs > 1024ul ) s->io_wgs = IO_WGS;
@@ -1226,6 +1244,8 @@ extern "C" void
 fd_verify_svc_set_merge( fd_verify_svc_t * s, ulong min_frags, ulong wait_ns, ulong idle_ns ) {
   s->merge_min = min_frags; s->merge_wait_ns = (long)wait_ns; s->merge_idle_ns = (long)idle_ns;
 }
+
+static void * svc_ingest_main( void * arg );
 
 extern "C" int
 fd_verify_svc_run( fd_verify_svc_t * s ) {
@@ -1322,6 +1342,23 @@ fd_verify_svc_run( fd_verify_svc_t * s ) {
     SV_CHECK( hipEventRecord( s->io_ev, s->st_ing ) );
   }
   s->running = 1;
+  /* the ingest thread: started here, before the GPU tile's sandbox, and
+     only when the process may run on two CPUs or more (a thread sharing the
+     service thread's one CPU would take turns with it, the opposite of the
+     point); it inherits the process's CPU set */
+  if( !s->io ) {
+    char const * e = getenv( "FD_VERIFY_SVC_INGEST_THREAD" );
+    cpu_set_t cs;
+    CPU_ZERO( &cs );
+    int const cpus = sched_getaffinity( 0, sizeof(cs), &cs ) ? 1 : CPU_COUNT( &cs );
+    if( !( e && !strcmp( e, "0" ) ) && cpus >= 2 ) {
+      if( pthread_create( &s->ith, 0, svc_ingest_main, s ) ) {
+        fprintf( stderr, "fd_verify_svc: the ingest thread could not start\n" );
+        return -1;
+      }
+      s->ithread = 1;
+    }
+  }
   fd_verify_svc_st( &s->seg->svc_state, FD_VERIFY_SVC_SVC_RUNNING );
   return 0;
 }
@@ -1525,6 +1562,81 @@ svc_flush_batch_start( fd_verify_svc_t * s, svc_fbatch & F ) {
   return 1;
 }
 
+/* the ingest side of a poll: 1b. finished gathers, in order (their
+   requests' frags are in HBM, the tiles may reuse the link space) into the
+   handoff ring; 2. newly posted requests, in each tile's ring order, into
+   one gather batch (a request waits while every batch is busy).  Runs on
+   the ingest thread, or inside fd_verify_svc_poll without one; it alone
+   touches the ING ring, the tiles' take counters, sdesc and stat[12..14] */
+static int
+svc_ingest_step( fd_verify_svc_t * s ) {
+  fd_verify_svc_seg_t * g = s->seg;
+  int did = 0;
+  long const now0 = svc_now_ns();
+  ulong tail = s->ih_tail;
+  while( s->ing_fin < s->ing_take ) {
+    svc_ingest & I = s->ING[s->ing_fin % SVC_ING_MAX];
+    hipError_t e = hipEventQuery( I.ev1 );
+    if( e == hipErrorNotReady ) break;
+    SV_CHECK( e );
+    float ms = 0.f;
+    SV_CHECK( hipEventElapsedTime( &ms, I.ev0, I.ev1 ) );
+    s->stat[13] += (ulong)((double)ms * 1e6);
+    /* the gather's last workgroup has stored INGESTED into each slot (the
+       tiles learn it from the GPU, not from this turn); here they go to the
+       launch queues */
+    for( ulong r = 0; r < I.nreq; r++ ) {
+      svc_pend & p = s->ih[tail % s->ih_cap];
+      p.t = I.req[r].t; p.slot = I.req[r].slot; p.n = I.h_desc[r].n; p.seen = now0;
+      p.sig = I.h_desc[r].kind == FD_VERIFY_SVC_REQ_SIGS;
+      tail++;
+    }
+    I.busy = 0; s->ing_fin++; did = 1;
+  }
+  __atomic_store_n( &s->ih_tail, tail, __ATOMIC_RELEASE );
+  long const p1 = svc_now_ns();
+  /* a range request holds its link until its gather has read it */
+  if( s->ing_take - s->ing_fin < SVC_ING_MAX ) {
+    svc_ingest & I = s->ING[s->ing_take % SVC_ING_MAX];
+    I.nreq = 0; I.n = 0;
+    for( ulong t = 0; t < g->tile_cnt && I.nreq < SVC_REQ_MAX; t++ ) {
+      svc_tile & T = s->tile[t];
+      while( I.nreq < SVC_REQ_MAX ) {
+        ulong slot = T.take & (g->req_depth - 1ul);
+        fd_verify_svc_req_t * q = fd_verify_svc_req( g, t, slot );
+        if( fd_verify_svc_ld( &q->state ) != FD_VERIFY_SVC_POSTED ) break;
+        if( q->id + g->req_depth == T.take ) break;          /* the slot's previous request, still on the GPU */
+        if( q->id != T.take ) {
+          fprintf( stderr, "fd_verify_svc: tile %lu posted request %lu in slot %lu, expected %lu\n", t, q->id, slot, T.take );
+          abort();
+        }
+        T.take++; did = 1;
+        if( !q->n ) {                                        /* nothing to verify: results at once */
+          q->batch_frags = 0; fd_verify_svc_st( &q->state, FD_VERIFY_SVC_RESULTS );
+          continue;
+        }
+        svc_desc & d = s->sdesc[t * g->req_depth + slot];
+        svc_desc_of( s, t, slot, I.n, d );
+        I.h_desc[I.nreq] = d;
+        I.req[I.nreq].t = t; I.req[I.nreq].slot = slot;
+        I.nreq++; I.n += q->n;
+      }
+    }
+    if( I.nreq ) { svc_ingest_start( s, I ); s->ing_take++; }
+  }
+  s->stat[14] += (ulong)(svc_now_ns() - p1);
+  return did;
+}
+
+static void *
+svc_ingest_main( void * arg ) {
+  fd_verify_svc_t * s = (fd_verify_svc_t *)arg;
+  svc_device( s->dev );
+  while( !__atomic_load_n( &s->istop, __ATOMIC_ACQUIRE ) )
+    if( !svc_ingest_step( s ) ) __builtin_ia32_pause();
+  return 0;
+}
+
 extern "C" int fd_verify_svc_debug( fd_verify_svc_t const * s, char * buf, ulong sz );
 
 extern "C" int
@@ -1615,72 +1727,27 @@ fd_verify_svc_poll( fd_verify_svc_t * s ) {
         memset( &d, 0, sizeof(d) );
         d.n = n; d.seed = seed; d.stage0 = svc_stage0( s, t, slot ); d.ibase = r * g->slot_cap;
         svc_pend & p = s->pend[s->pend_tail % s->pend_cap];
-        p.t = t; p.slot = slot; p.n = n; p.seen = now0;
+        p.t = t; p.slot = slot; p.n = n; p.seen = now0; p.sig = 0ul;
         s->pend_tail++; s->pend_frags += n;
       }
     }
   }
-  /* 1b. finished ingests, in order: their requests' frags are in HBM (the
-     tiles may reuse the link space) and wait for a verify launch */
-  while( !s->io && s->ing_fin < s->ing_take ) {
-    svc_ingest & I = s->ING[s->ing_fin % SVC_ING_MAX];
-    hipError_t e = hipEventQuery( I.ev1 );
-    if( e == hipErrorNotReady ) break;
-    SV_CHECK( e );
-    float ms = 0.f;
-    SV_CHECK( hipEventElapsedTime( &ms, I.ev0, I.ev1 ) );
-    s->stat[13] += (ulong)((double)ms * 1e6);
-    /* the gather's last workgroup has stored INGESTED into each slot (the
-       tiles learn it from the GPU, not from this turn); here they join the
-       launch queues */
-    for( ulong r = 0; r < I.nreq; r++ ) {
-      if( I.h_desc[r].kind == FD_VERIFY_SVC_REQ_SIGS ) {
-        svc_pend & p = s->spend[s->spend_tail % s->pend_cap];
-        p.t = I.req[r].t; p.slot = I.req[r].slot; p.n = I.h_desc[r].n; p.seen = now0;
-        s->spend_tail++;
-        continue;
-      }
-      svc_pend & p = s->pend[s->pend_tail % s->pend_cap];
-      p.t = I.req[r].t; p.slot = I.req[r].slot; p.n = I.h_desc[r].n; p.seen = now0;
-      s->pend_tail++; s->pend_frags += p.n;
-    }
-    I.busy = 0; s->ing_fin++; did = 1;
-  }
   long const p1 = svc_now_ns();
   s->stat[10] += (ulong)(p1 - p0);
-  /* 2. posted requests, in each tile's ring order, into one ingest batch
-     (a request waits while every ingest slot is busy) -- before the
-     flushes: a range request holds its link until its gather has read it */
-  if( !s->io && s->ing_take - s->ing_fin < SVC_ING_MAX ) {
-    svc_ingest & I = s->ING[s->ing_take % SVC_ING_MAX];
-    I.nreq = 0; I.n = 0;
-    for( ulong t = 0; t < g->tile_cnt && I.nreq < SVC_REQ_MAX; t++ ) {
-      svc_tile & T = s->tile[t];
-      while( I.nreq < SVC_REQ_MAX ) {
-        ulong slot = T.take & (g->req_depth - 1ul);
-        fd_verify_svc_req_t * q = fd_verify_svc_req( g, t, slot );
-        if( fd_verify_svc_ld( &q->state ) != FD_VERIFY_SVC_POSTED ) break;
-        if( q->id + g->req_depth == T.take ) break;          /* the slot's previous request, still on the GPU */
-        if( q->id != T.take ) {
-          fprintf( stderr, "fd_verify_svc: tile %lu posted request %lu in slot %lu, expected %lu\n", t, q->id, slot, T.take );
-          abort();
-        }
-        T.take++; did = 1;
-        if( !q->n ) {                                        /* nothing to verify: results at once */
-          q->batch_frags = 0; fd_verify_svc_st( &q->state, FD_VERIFY_SVC_RESULTS );
-          continue;
-        }
-        svc_desc & d = s->sdesc[t * g->req_depth + slot];
-        svc_desc_of( s, t, slot, I.n, d );
-        I.h_desc[I.nreq] = d;
-        I.req[I.nreq].t = t; I.req[I.nreq].slot = slot;
-        I.nreq++; I.n += q->n;
-      }
+  /* 1b, 2: the ingest side, here when it has no thread of its own */
+  if( !s->io && !s->ithread ) did |= svc_ingest_step( s );
+  /* ingested requests join the launch queues (txn frags merge; signature
+     requests ride their own launches) */
+  {
+    ulong const tail = __atomic_load_n( &s->ih_tail, __ATOMIC_ACQUIRE );
+    for( ; s->ih_head < tail; s->ih_head++ ) {
+      svc_pend const & h = s->ih[s->ih_head % s->ih_cap];
+      if( h.sig ) { s->spend[s->spend_tail % s->pend_cap] = h; s->spend_tail++; }
+      else        { s->pend[s->pend_tail % s->pend_cap] = h; s->pend_tail++; s->pend_frags += h.n; }
+      did = 1;
     }
-    if( I.nreq ) { svc_ingest_start( s, I ); s->ing_take++; }
   }
   long const p2 = svc_now_ns();
-  s->stat[14] += (ulong)(p2 - p1);
   /* 3. flushes: retire in order, start the newly posted */
   while( s->flush_batch && s->fb_fin < s->fb_take ) {
     svc_fbatch & F = s->FB[s->fb_fin % SVC_FB_MAX];
@@ -1853,6 +1920,11 @@ fd_verify_svc_delete( fd_verify_svc_t * s ) {
   if( !s ) return;
   (void)hipSetDevice( s->dev );
   svc_cur_dev = s->dev;
+  if( s->ithread ) {                          /* no new gathers from here on (the stream drains below) */
+    __atomic_store_n( &s->istop, 1, __ATOMIC_RELEASE );
+    (void)pthread_join( s->ith, 0 );
+    s->ithread = 0;
+  }
   if( s->io && s->running ) {
     __atomic_store_n( &((svc_io_hctl *)s->h_ctl)->stop, 1ul, __ATOMIC_SEQ_CST );
     svc_drain( s->st_ing, s->io_ev, "the IO engine (k_svc_io)", 0ul, s );
@@ -1895,6 +1967,6 @@ fd_verify_svc_delete( fd_verify_svc_t * s ) {
   free( s->sdesc );
   for( ulong k = 0; k < s->nreg; k++ ) (void)hipHostUnregister( s->reg[k].h );
   fd_verify_svc_st( &s->seg->svc_state, FD_VERIFY_SVC_SVC_STOPPED );
-  free( s->pend ); free( s->spend );
+  free( s->pend ); free( s->spend ); free( s->ih );
   free( s );
 }
