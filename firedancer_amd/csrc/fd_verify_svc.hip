@@ -1016,6 +1016,7 @@ struct fd_verify_svc {
   int      ithread;            /* the ingest thread runs */
   pthread_t ith;
   int      istop;
+  int      iready;             /* the ingest thread has made its first HIP calls */
   svc_pend * ih; ulong ih_cap; ulong ih_tail, ih_head;
   long     launch_t0[SVC_LAUNCH_MAX];           /* a verify launch's start (the stuck-launch watchdog) */
 };
@@ -1357,6 +1358,7 @@ fd_verify_svc_run( fd_verify_svc_t * s ) {
         return -1;
       }
       s->ithread = 1;
+      while( !__atomic_load_n( &s->iready, __ATOMIC_ACQUIRE ) ) __builtin_ia32_pause();
     }
   }
   fd_verify_svc_st( &s->seg->svc_state, FD_VERIFY_SVC_SVC_RUNNING );
@@ -1631,7 +1633,23 @@ svc_ingest_step( fd_verify_svc_t * s ) {
 static void *
 svc_ingest_main( void * arg ) {
   fd_verify_svc_t * s = (fd_verify_svc_t *)arg;
+  /* the thread's first HIP calls (the runtime's per-thread setup), an empty
+     gather, an event and its query, and its first malloc (its arena) happen
+     here, before fd_verify_svc_run returns and the GPU tile enters its
+     sandbox: made after it, the setup's calls met the seccomp filter (one
+     bench run of r06l ended in SIGSYS) */
   svc_device( s->dev );
+  free( malloc( 4096 ) );
+  hipLaunchKernelGGL( k_svc_gather, dim3( 1 ), dim3( 256 ), 0, s->st_ing, s->ING[0].d_desc, 0u, 0ul, s->d_ing, s->d_ing_sz,
+                      s->d_ing_kind, s->d_ing_tso, s->d_stage, (u32 *)0 );
+  SV_CHECK( hipGetLastError() );
+  SV_CHECK( hipEventRecord( s->ING[0].ev0, s->st_ing ) );
+  SV_CHECK( hipEventRecord( s->ING[0].ev1, s->st_ing ) );
+  SV_CHECK( hipStreamSynchronize( s->st_ing ) );
+  SV_CHECK( hipEventQuery( s->ING[0].ev1 ) );
+  float ms = 0.f;
+  SV_CHECK( hipEventElapsedTime( &ms, s->ING[0].ev0, s->ING[0].ev1 ) );
+  __atomic_store_n( &s->iready, 1, __ATOMIC_RELEASE );
   while( !__atomic_load_n( &s->istop, __ATOMIC_ACQUIRE ) )
     if( !svc_ingest_step( s ) ) __builtin_ia32_pause();
   return 0;
