@@ -126,20 +126,33 @@ static_assert( sizeof(svc_desc) == 128, "svc_desc layout" );
 /**********************************************************************/
 /* kernels                                                             */
 
+typedef u32 v4u __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(1))) v4u gv4u;     /* global memory: global_load / global_store, not flat */
+
 __global__ __launch_bounds__(256)
 void k_svc_gather( svc_desc const * __restrict__ desc, u32 nreq, ulong n, u8 * __restrict__ ing,
                    u16 * __restrict__ ing_sz, u8 * __restrict__ ing_kind, u32 * __restrict__ ing_tso,
                    u8 * __restrict__ stage, u32 * __restrict__ done_ctr ) {
-  __shared__ u64 sbase[SVC_REQ_MAX];
-  for( u32 i = threadIdx.x; i < nreq; i += blockDim.x ) sbase[i] = desc[i].base;
+  /* the requests' descriptors into LDS first (dynamic, nreq x 128 B): they
+     live in mapped host memory, and read in place every frag paid a chain of
+     dependent PCIe round trips for its descriptor's fields */
+  extern __shared__ uint4 sd4[];
+  svc_desc const * sd = (svc_desc const *)sd4;
+  for( u32 k = threadIdx.x; k < 8u * nreq; k += blockDim.x ) sd4[k] = ((uint4 const *)desc)[k];
   __syncthreads();
-  u32 const lane = threadIdx.x & 63u;
-  /* one wave per frag, grid-stride: a grid of n/4 workgroups takes each frag
-     once; a capped grid (gather_wgs) loops */
-  for( ulong j = (ulong)blockIdx.x * 4ul + (threadIdx.x >> 6); j < n; j += 4ul * gridDim.x ) {
-    u32 lo = 0u, hi = nreq;                                 /* sbase[lo] <= j < sbase[hi] */
-    while( hi - lo > 1u ) { u32 mid = (lo + hi) >> 1; if( sbase[mid] <= j ) lo = mid; else hi = mid; }
-    svc_desc const * d = desc + lo;
+  /* a quarter wave (16 lanes) per frag, 16 frags per workgroup per trip,
+     grid-stride: a grid of n/16 workgroups takes each frag once, a capped
+     grid (gather_wgs) loops.  The loads are PCIe reads of host memory; a
+     quarter issues its frag's line read, then every 256-B piece of the frag
+     at once (up to 8, before any store), so a wave has 4 frags and all of
+     their pieces in flight (one wave per frag, one piece per round trip
+     after the line: 16 GB/s, 25 ns per frag at 3 tiles, profiles/r06/
+     gather_mlp) */
+  u32 const ql = threadIdx.x & 15u;
+  for( ulong j = (ulong)blockIdx.x * 16ul + (threadIdx.x >> 4); j < n; j += 16ul * gridDim.x ) {
+    u32 lo = 0u, hi = nreq;                                 /* sd[lo].base <= j < sd[hi].base */
+    while( hi - lo > 1u ) { u32 mid = (lo + hi) >> 1; if( sd[mid].base <= j ) lo = mid; else hi = mid; }
+    svc_desc const * d = sd + lo;
     ulong const i = j - d->base;
     u32 sz = 0u, kind = FD_VERIFY_HIP_IN_QUIC, tsv = 0u;
     bool ok;
@@ -147,14 +160,14 @@ void k_svc_gather( svc_desc const * __restrict__ desc, u32 nreq, ulong n, u8 * _
     if( d->kind == FD_VERIFY_SVC_REQ_RANGE ) {
       ulong const seq = d->first + i * d->stride;
       u8 const * line = (u8 const *)d->src + 32ul * (seq & d->line_mask);
-      /* lanes 0 and 1 read the line's two halves (seq, sig | chunk, sz,
-         ctl, tsorig, tspub) with vector loads, every lane takes them */
+      /* the quarter's lanes 0 and 1 read the line's two halves (seq, sig |
+         chunk, sz, ctl, tsorig, tspub), every lane of the quarter takes them */
       uint4 v = make_uint4( 0u, 0u, 0u, 0u );
-      if( lane < 2u ) v = *(uint4 const *)(line + 16u * lane);
-      u64 const found = (u64)(u32)__shfl( (int)v.x, 0 ) | ((u64)(u32)__shfl( (int)v.y, 0 ) << 32);
-      u32 const chunk = (u32)__shfl( (int)v.x, 1 );
-      sz  = (u32)__shfl( (int)v.y, 1 ) & 0xffffu;
-      tsv = (u32)__shfl( (int)v.z, 1 );
+      if( ql < 2u ) v = *(uint4 const *)(line + 16u * ql);
+      u64 const found = (u64)(u32)__shfl( (int)v.x, 0, 16 ) | ((u64)(u32)__shfl( (int)v.y, 0, 16 ) << 32);
+      u32 const chunk = (u32)__shfl( (int)v.x, 1, 16 );
+      sz  = (u32)__shfl( (int)v.y, 1, 16 ) & 0xffffu;
+      tsv = (u32)__shfl( (int)v.z, 1, 16 );
       ok  = found == seq && (ulong)chunk >= d->chunk0 && (ulong)chunk <= d->wmark && sz <= FD_VERIFY_HIP_TPU_RAW_MTU;
       src = (u8 const *)d->aux0 + 64ul * chunk;
     } else {
@@ -166,12 +179,25 @@ void k_svc_gather( svc_desc const * __restrict__ desc, u32 nreq, ulong n, u8 * _
     }
     ulong const f = d->ibase + i;
     u8 * dst = ing + 64ul * SVC_INGEST_CHUNKS * f;
-    if( ok ) for( u32 p = 16u * lane; p < sz; p += 1024u ) *(uint4 *)(dst + p) = *(uint4 const *)(src + p);
+    u32 const m = ok ? sz : 0u;                             /* sz <= 2048: 8 pieces of 256 B */
+    /* every piece load is made (a piece past the frag reads the destination,
+       device memory, and is not stored), as global loads into named
+       registers: predicated loads into an array went through scratch with a
+       wait each */
+    u32 const p0 = 16u * ql;
+#define SVC_PIECE_LD( k ) v4u const v##k = *(gv4u const *)( p0 + 256u * k < m ? src + p0 + 256u * k : dst + p0 + 256u * k )
+    SVC_PIECE_LD( 0 ); SVC_PIECE_LD( 1 ); SVC_PIECE_LD( 2 ); SVC_PIECE_LD( 3 );
+    SVC_PIECE_LD( 4 ); SVC_PIECE_LD( 5 ); SVC_PIECE_LD( 6 ); SVC_PIECE_LD( 7 );
+#undef SVC_PIECE_LD
+#define SVC_PIECE_ST( k ) if( p0 + 256u * k < m ) *(gv4u *)( dst + p0 + 256u * k ) = v##k
+    SVC_PIECE_ST( 0 ); SVC_PIECE_ST( 1 ); SVC_PIECE_ST( 2 ); SVC_PIECE_ST( 3 );
+    SVC_PIECE_ST( 4 ); SVC_PIECE_ST( 5 ); SVC_PIECE_ST( 6 ); SVC_PIECE_ST( 7 );
+#undef SVC_PIECE_ST
     /* a gossip vote's out header: the reference writes four fields into the
        out chunk's stale header (fd_verify_tile.c:90-93); here the rest is 0 */
-    if( kind == FD_VERIFY_HIP_IN_GOSSIP && lane < 5u )
-      *(uint4 *)(stage + 64ul * (d->stage0 + FD_TXN_HIP_STAGE_CHUNKS * i) + 16u * lane) = make_uint4( 0u, 0u, 0u, 0u );
-    if( lane == 0u ) { ing_sz[f] = ok ? (u16)sz : (u16)0xffffu; ing_kind[f] = (u8)kind; ing_tso[f] = tsv; }
+    if( kind == FD_VERIFY_HIP_IN_GOSSIP && ql < 5u )
+      *(uint4 *)(stage + 64ul * (d->stage0 + FD_TXN_HIP_STAGE_CHUNKS * i) + 16u * ql) = make_uint4( 0u, 0u, 0u, 0u );
+    if( ql == 0u ) { ing_sz[f] = ok ? (u16)sz : (u16)0xffffu; ing_kind[f] = (u8)kind; ing_tso[f] = tsv; }
   }
   /* INGESTED from the GPU: once every workgroup has passed its loop (all of
      its loads from the links have returned), the last one stores INGESTED
@@ -192,8 +218,8 @@ void k_svc_gather( svc_desc const * __restrict__ desc, u32 nreq, ulong n, u8 * _
   __syncthreads();
   if( !last ) return;
   for( u32 i = threadIdx.x; i < nreq; i += blockDim.x )
-    if( desc[i].state )
-      __hip_atomic_store( (u64 *)desc[i].state, (u64)FD_VERIFY_SVC_INGESTED, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM );
+    if( sd[i].state )
+      __hip_atomic_store( (u64 *)sd[i].state, (u64)FD_VERIFY_SVC_INGESTED, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM );
   if( threadIdx.x == 0u ) *done_ctr = 0u;
 }
 
@@ -1017,6 +1043,8 @@ struct fd_verify_svc {
   pthread_t ith;
   int      istop;
   int      iready;             /* the ingest thread has made its first HIP calls */
+  int      iexited;            /* the ingest thread has left its loop */
+  int      io_prio;            /* the ingest and flush streams' priority */
   svc_pend * ih; ulong ih_cap; ulong ih_tail, ih_head;
   long     launch_t0[SVC_LAUNCH_MAX];           /* a verify launch's start (the stuck-launch watchdog) */
 };
@@ -1128,7 +1156,17 @@ fd_verify_svc_boot( void * seg_mem, int device, ulong batch_max, ulong inflight 
   SV_CHECK( hipMalloc( &s->d_ing_sz, 2ul * ing_cnt ) ); SV_CHECK( hipMalloc( &s->d_ing_kind, ing_cnt ) );
   SV_CHECK( hipMalloc( &s->d_ing_tso, 4ul * ing_cnt ) );
   SV_CHECK( hipMalloc( &s->d_ing_ctr, 4ul * SVC_ING_MAX ) ); SV_CHECK( hipMemset( s->d_ing_ctr, 0, 4ul * SVC_ING_MAX ) );
-  SV_CHECK( hipStreamCreateWithFlags( &s->st_ing, hipStreamNonBlocking ) );
+  /* FD_VERIFY_SVC_IO_PRIO=1: the ingest and flush streams at the device's
+     greatest stream priority.  Opt-in: it lost its A/B (profiles/r06/
+     io_prio, depth 16384, 3 tiles: 24 M frags/s runs lost 140-220 K frags
+     with it, 0.5-2.4 K without) */
+  {
+    char const * e = getenv( "FD_VERIFY_SVC_IO_PRIO" );
+    int lo = 0, hi = 0;
+    SV_CHECK( hipDeviceGetStreamPriorityRange( &lo, &hi ) );
+    s->io_prio = ( e && !strcmp( e, "1" ) ) ? hi : 0;
+  }
+  SV_CHECK( hipStreamCreateWithPriority( &s->st_ing, hipStreamNonBlocking, s->io_prio ) );
   for( ulong k = 0; k < SVC_ING_MAX; k++ ) {
     svc_ingest & I = s->ING[k];
     SV_CHECK( hipHostMalloc( &I.h_desc, sizeof(svc_desc) * SVC_REQ_MAX, hipHostMallocMapped ) );
@@ -1141,7 +1179,7 @@ fd_verify_svc_boot( void * seg_mem, int device, ulong batch_max, ulong inflight 
     s->flush_batch = !( e && !strcmp( e, "tile" ) ) && !( io && !strcmp( io, "io" ) );
   }
   if( s->flush_batch ) {
-    SV_CHECK( hipStreamCreateWithFlags( &s->st_flush, hipStreamNonBlocking ) );
+    SV_CHECK( hipStreamCreateWithPriority( &s->st_flush, hipStreamNonBlocking, s->io_prio ) );
     for( ulong k = 0; k < SVC_FB_MAX; k++ ) {
       svc_fbatch & F = s->FB[k];
       SV_CHECK( hipHostMalloc( &F.h_desc, sizeof(svc_fdesc) * SVC_FB_FLUSH_MAX, hipHostMallocMapped ) );
@@ -1482,9 +1520,9 @@ static void
 svc_ingest_start( fd_verify_svc_t * s, svc_ingest & I ) {
   svc_device( s->dev );
   SV_CHECK( hipEventRecord( I.ev0, s->st_ing ) );
-  ulong wgs = (I.n + 3ul) / 4ul;
+  ulong wgs = (I.n + 15ul) / 16ul;                          /* 16 frags per workgroup per trip */
   if( s->gather_wgs && wgs > s->gather_wgs ) wgs = s->gather_wgs;
-  hipLaunchKernelGGL( k_svc_gather, dim3( (unsigned)wgs ), dim3( 256 ), 0, s->st_ing, I.d_desc,
+  hipLaunchKernelGGL( k_svc_gather, dim3( (unsigned)wgs ), dim3( 256 ), sizeof(svc_desc) * I.nreq, s->st_ing, I.d_desc,
                       (u32)I.nreq, I.n, s->d_ing, s->d_ing_sz, s->d_ing_kind, s->d_ing_tso, s->d_stage,
                       s->d_ing_ctr + (s->ing_take % SVC_ING_MAX) );
   SV_CHECK( hipGetLastError() );
@@ -1652,6 +1690,7 @@ svc_ingest_main( void * arg ) {
   __atomic_store_n( &s->iready, 1, __ATOMIC_RELEASE );
   while( !__atomic_load_n( &s->istop, __ATOMIC_ACQUIRE ) )
     if( !svc_ingest_step( s ) ) __builtin_ia32_pause();
+  __atomic_store_n( &s->iexited, 1, __ATOMIC_RELEASE );
   return 0;
 }
 
@@ -1940,6 +1979,21 @@ fd_verify_svc_delete( fd_verify_svc_t * s ) {
   svc_cur_dev = s->dev;
   if( s->ithread ) {                          /* no new gathers from here on (the stream drains below) */
     __atomic_store_n( &s->istop, 1, __ATOMIC_RELEASE );
+    /* a thread held inside a HIP call would hold pthread_join silently: the
+       wait is staged as the streams' are (named after 2 s, abort after 30 s) */
+    long const t0 = svc_now_ns();
+    int warned = 0;
+    while( !__atomic_load_n( &s->iexited, __ATOMIC_ACQUIRE ) ) {
+      long const dt = svc_now_ns() - t0;
+      if( dt > 2000000000L && !warned ) {
+        warned = 1;
+        fprintf( stderr, "fd_verify_svc: teardown: the ingest thread still in a HIP call after 2 s (gathers %lu started, "
+                 "%lu retired)\n", s->ing_take, s->ing_fin );
+      }
+      if( dt > 30000000000L ) { fprintf( stderr, "fd_verify_svc: teardown: the ingest thread not done after 30 s\n" ); abort(); }
+      struct timespec ts = { 0, 100000L };
+      nanosleep( &ts, 0 );
+    }
     (void)pthread_join( s->ith, 0 );
     s->ithread = 0;
   }

@@ -308,7 +308,8 @@ def main():
                 env = kv(args.env)
                 if args.prelay:
                     env["SVC_RUN_PRELAY"] = "1"
-                    depth = max(depth, 1 << (s.n - 1).bit_length())
+                    if not args.in_depth:     # prelaid frags with no depth given: a link that holds the stream
+                        depth = max(depth, 1 << (s.n - 1).bit_length())
                 if rate:
                     env["SVC_RUN_RATE"] = str(rate)
                 for r in range(args.repeat):
