@@ -992,6 +992,13 @@ struct fd_verify_svc {
   u8 *     d_ing;              /* ingest: tile x slot x slot_cap frags of SVC_INGEST_CHUNKS */
   u16 *    d_ing_sz; u8 * d_ing_kind; u32 * d_ing_tso;   /* per ingest frag */
   hipStream_t st_ing;
+  /* FD_VERIFY_SVC_ING_STREAMS=2: gathers alternate over two streams
+     (st_ing, st_ing2).  One gather runs at ~24 GB/s of PCIe reads beside the
+     verify kernels and gathers queue behind each other on one stream, but
+     two did not win their A/B (profiles/r06/ing_streams: 24 M frags/s lost
+     less, 28 M more, on the same box): default one */
+  hipStream_t st_ing2;
+  ulong    ing_nst;
   svc_ingest ING[SVC_ING_MAX];
   ulong    ing_take, ing_fin;  /* ingest batches started / retired (ring order) */
   u32 *    d_ing_ctr;          /* per ingest batch slot: k_svc_gather's workgroups done (HBM, zero between batches) */
@@ -1167,6 +1174,11 @@ fd_verify_svc_boot( void * seg_mem, int device, ulong batch_max, ulong inflight 
     s->io_prio = ( e && !strcmp( e, "1" ) ) ? hi : 0;
   }
   SV_CHECK( hipStreamCreateWithPriority( &s->st_ing, hipStreamNonBlocking, s->io_prio ) );
+  {
+    char const * e = getenv( "FD_VERIFY_SVC_ING_STREAMS" );
+    s->ing_nst = ( e && !strcmp( e, "2" ) ) ? 2ul : 1ul;
+    if( s->ing_nst == 2ul ) SV_CHECK( hipStreamCreateWithPriority( &s->st_ing2, hipStreamNonBlocking, s->io_prio ) );
+  }
   for( ulong k = 0; k < SVC_ING_MAX; k++ ) {
     svc_ingest & I = s->ING[k];
     SV_CHECK( hipHostMalloc( &I.h_desc, sizeof(svc_desc) * SVC_REQ_MAX, hipHostMallocMapped ) );
@@ -1519,14 +1531,15 @@ svc_sig_launch_start( fd_verify_svc_t * s, svc_launch & L ) {
 static void
 svc_ingest_start( fd_verify_svc_t * s, svc_ingest & I ) {
   svc_device( s->dev );
-  SV_CHECK( hipEventRecord( I.ev0, s->st_ing ) );
+  hipStream_t const st = ( s->ing_nst == 2ul && ( s->ing_take & 1ul ) ) ? s->st_ing2 : s->st_ing;
+  SV_CHECK( hipEventRecord( I.ev0, st ) );
   ulong wgs = (I.n + 15ul) / 16ul;                          /* 16 frags per workgroup per trip */
   if( s->gather_wgs && wgs > s->gather_wgs ) wgs = s->gather_wgs;
-  hipLaunchKernelGGL( k_svc_gather, dim3( (unsigned)wgs ), dim3( 256 ), sizeof(svc_desc) * I.nreq, s->st_ing, I.d_desc,
+  hipLaunchKernelGGL( k_svc_gather, dim3( (unsigned)wgs ), dim3( 256 ), sizeof(svc_desc) * I.nreq, st, I.d_desc,
                       (u32)I.nreq, I.n, s->d_ing, s->d_ing_sz, s->d_ing_kind, s->d_ing_tso, s->d_stage,
                       s->d_ing_ctr + (s->ing_take % SVC_ING_MAX) );
   SV_CHECK( hipGetLastError() );
-  SV_CHECK( hipEventRecord( I.ev1, s->st_ing ) );
+  SV_CHECK( hipEventRecord( I.ev1, st ) );
   I.busy = 1;
   s->stat[12]++;
 }
@@ -1684,6 +1697,12 @@ svc_ingest_main( void * arg ) {
   SV_CHECK( hipEventRecord( s->ING[0].ev0, s->st_ing ) );
   SV_CHECK( hipEventRecord( s->ING[0].ev1, s->st_ing ) );
   SV_CHECK( hipStreamSynchronize( s->st_ing ) );
+  if( s->st_ing2 ) {
+    hipLaunchKernelGGL( k_svc_gather, dim3( 1 ), dim3( 256 ), 0, s->st_ing2, s->ING[1].d_desc, 0u, 0ul, s->d_ing, s->d_ing_sz,
+                        s->d_ing_kind, s->d_ing_tso, s->d_stage, (u32 *)0 );
+    SV_CHECK( hipGetLastError() );
+    SV_CHECK( hipStreamSynchronize( s->st_ing2 ) );
+  }
   SV_CHECK( hipEventQuery( s->ING[0].ev1 ) );
   float ms = 0.f;
   SV_CHECK( hipEventElapsedTime( &ms, s->ING[0].ev0, s->ING[0].ev1 ) );
@@ -2006,6 +2025,7 @@ fd_verify_svc_delete( fd_verify_svc_t * s ) {
     if( s->tile[t].set && !s->tile[t].client ) svc_drain( s->tile[t].st, 0, "flush stream of tile", t, s );
   if( s->flush_batch ) svc_drain( s->st_flush, 0, "flush stream", 0ul, s );
   if( s->st_ing && !s->io ) svc_drain( s->st_ing, 0, "ingest stream", 0ul, s );
+  if( s->st_ing2 ) svc_drain( s->st_ing2, 0, "ingest stream", 1ul, s );
   (void)hipDeviceSynchronize();
   for( ulong k = 0; k < SVC_LAUNCH_MAX; k++ ) launch_free( s->L[k] );
   for( ulong t = 0; t < FD_VERIFY_SVC_TILE_MAX; t++ ) {
@@ -2029,6 +2049,7 @@ fd_verify_svc_delete( fd_verify_svc_t * s ) {
     (void)hipHostFree( I.h_desc ); (void)hipEventDestroy( I.ev0 ); (void)hipEventDestroy( I.ev1 );
   }
   if( s->st_ing ) (void)hipStreamDestroy( s->st_ing );
+  if( s->st_ing2 ) (void)hipStreamDestroy( s->st_ing2 );
   if( s->flush_batch ) {
     for( ulong k = 0; k < SVC_FB_MAX; k++ ) {
       if( !s->FB[k].h_desc ) continue;
