@@ -223,6 +223,80 @@ void k_svc_gather( svc_desc const * __restrict__ desc, u32 nreq, ulong n, u8 * _
   if( threadIdx.x == 0u ) *done_ctr = 0u;
 }
 
+/* the round-5 gather (the default; FD_VERIFY_SVC_GATHER=quarter selects
+   k_svc_gather above): one wave per frag, descriptors read in place from
+   mapped host memory */
+__global__ __launch_bounds__(256)
+void k_svc_gather_wave( svc_desc const * __restrict__ desc, u32 nreq, ulong n, u8 * __restrict__ ing,
+                   u16 * __restrict__ ing_sz, u8 * __restrict__ ing_kind, u32 * __restrict__ ing_tso,
+                   u8 * __restrict__ stage, u32 * __restrict__ done_ctr ) {
+  __shared__ u64 sbase[SVC_REQ_MAX];
+  for( u32 i = threadIdx.x; i < nreq; i += blockDim.x ) sbase[i] = desc[i].base;
+  __syncthreads();
+  u32 const lane = threadIdx.x & 63u;
+  /* one wave per frag, grid-stride: a grid of n/4 workgroups takes each frag
+     once; a capped grid (gather_wgs) loops */
+  for( ulong j = (ulong)blockIdx.x * 4ul + (threadIdx.x >> 6); j < n; j += 4ul * gridDim.x ) {
+    u32 lo = 0u, hi = nreq;                                 /* sbase[lo] <= j < sbase[hi] */
+    while( hi - lo > 1u ) { u32 mid = (lo + hi) >> 1; if( sbase[mid] <= j ) lo = mid; else hi = mid; }
+    svc_desc const * d = desc + lo;
+    ulong const i = j - d->base;
+    u32 sz = 0u, kind = FD_VERIFY_HIP_IN_QUIC, tsv = 0u;
+    bool ok;
+    u8 const * src;
+    if( d->kind == FD_VERIFY_SVC_REQ_RANGE ) {
+      ulong const seq = d->first + i * d->stride;
+      u8 const * line = (u8 const *)d->src + 32ul * (seq & d->line_mask);
+      /* lanes 0 and 1 read the line's two halves (seq, sig | chunk, sz,
+         ctl, tsorig, tspub) with vector loads, every lane takes them */
+      uint4 v = make_uint4( 0u, 0u, 0u, 0u );
+      if( lane < 2u ) v = *(uint4 const *)(line + 16u * lane);
+      u64 const found = (u64)(u32)__shfl( (int)v.x, 0 ) | ((u64)(u32)__shfl( (int)v.y, 0 ) << 32);
+      u32 const chunk = (u32)__shfl( (int)v.x, 1 );
+      sz  = (u32)__shfl( (int)v.y, 1 ) & 0xffffu;
+      tsv = (u32)__shfl( (int)v.z, 1 );
+      ok  = found == seq && (ulong)chunk >= d->chunk0 && (ulong)chunk <= d->wmark && sz <= FD_VERIFY_HIP_TPU_RAW_MTU;
+      src = (u8 const *)d->aux0 + 64ul * chunk;
+    } else {
+      src  = (u8 const *)d->src + FD_VERIFY_SVC_FRAG_STRIDE * i;
+      sz   = ((u16 const *)d->aux0)[i];
+      bool const sigs = d->kind == FD_VERIFY_SVC_REQ_SIGS;   /* a client's signature records: no frag kind */
+      kind = sigs ? FD_VERIFY_HIP_IN_QUIC : ((u8 const *)d->aux1)[i];
+      ok   = sz <= FD_VERIFY_SVC_FRAG_STRIDE && ( !sigs || sz >= FD_VERIFY_SVC_SIG_HDR_SZ );
+    }
+    ulong const f = d->ibase + i;
+    u8 * dst = ing + 64ul * SVC_INGEST_CHUNKS * f;
+    if( ok ) for( u32 p = 16u * lane; p < sz; p += 1024u ) *(uint4 *)(dst + p) = *(uint4 const *)(src + p);
+    /* a gossip vote's out header: the reference writes four fields into the
+       out chunk's stale header (fd_verify_tile.c:90-93); here the rest is 0 */
+    if( kind == FD_VERIFY_HIP_IN_GOSSIP && lane < 5u )
+      *(uint4 *)(stage + 64ul * (d->stage0 + FD_TXN_HIP_STAGE_CHUNKS * i) + 16u * lane) = make_uint4( 0u, 0u, 0u, 0u );
+    if( lane == 0u ) { ing_sz[f] = ok ? (u16)sz : (u16)0xffffu; ing_kind[f] = (u8)kind; ing_tso[f] = tsv; }
+  }
+  /* INGESTED from the GPU: once every workgroup has passed its loop (all of
+     its loads from the links have returned), the last one stores INGESTED
+     into each request's slot in the segment, so a tile may reuse its link
+     without waiting for the service thread's turn (the service still
+     retires the batch by its event before a verify launch reads the HBM
+     frags).  done_ctr: this batch's counter, zero at launch; the last
+     workgroup puts it back to zero for the next batch on the ingest stream */
+  /* Only the links' reads must be over (their values were stored, so they
+     have returned): no fence, and relaxed stores -- a system-scope release
+     here would write the whole L2 back (the verify kernels' dirty lines
+     included) once per request, which measured slower than the host's
+     turn it saves */
+  if( !done_ctr ) return;
+  __syncthreads();
+  __shared__ u32 last;
+  if( threadIdx.x == 0u ) last = atomicAdd( done_ctr, 1u ) == gridDim.x - 1u;
+  __syncthreads();
+  if( !last ) return;
+  for( u32 i = threadIdx.x; i < nreq; i += blockDim.x )
+    if( desc[i].state )
+      __hip_atomic_store( (u64 *)desc[i].state, (u64)FD_VERIFY_SVC_INGESTED, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM );
+  if( threadIdx.x == 0u ) *done_ctr = 0u;
+}
+
 /* a verify launch's per-frag arrays (launch frag j = frag i of request d)
    from the requests' ingest frags: one thread per frag */
 __global__ __launch_bounds__(256)
@@ -999,6 +1073,13 @@ struct fd_verify_svc {
      less, 28 M more, on the same box): default one */
   hipStream_t st_ing2;
   ulong    ing_nst;
+  int      gather_wave;        /* k_svc_gather_wave (the round-5 kernel), the default; FD_VERIFY_SVC_GATHER=quarter:
+                                  k_svc_gather (descriptors in LDS, a quarter wave per frag).  Same box, depth 16384,
+                                  3 tiles, 9 paced runs each (profiles/r06/gather_ab): equal loss at 16-24 M except
+                                  one run of the quarter form that collapsed (1.2 M frags lost, p99 16.8 ms; r06p
+                                  had another at 32 M) -- its LDS grows with the requests in a gather (up to 64 KB),
+                                  so a backlog makes its workgroups harder to place beside the DSM, a suspected
+                                  feedback not yet proven */
   svc_ingest ING[SVC_ING_MAX];
   ulong    ing_take, ing_fin;  /* ingest batches started / retired (ring order) */
   u32 *    d_ing_ctr;          /* per ingest batch slot: k_svc_gather's workgroups done (HBM, zero between batches) */
@@ -1179,6 +1260,7 @@ fd_verify_svc_boot( void * seg_mem, int device, ulong batch_max, ulong inflight 
     s->ing_nst = ( e && !strcmp( e, "2" ) ) ? 2ul : 1ul;
     if( s->ing_nst == 2ul ) SV_CHECK( hipStreamCreateWithPriority( &s->st_ing2, hipStreamNonBlocking, s->io_prio ) );
   }
+  { char const * e = getenv( "FD_VERIFY_SVC_GATHER" ); s->gather_wave = !( e && !strcmp( e, "quarter" ) ); }
   for( ulong k = 0; k < SVC_ING_MAX; k++ ) {
     svc_ingest & I = s->ING[k];
     SV_CHECK( hipHostMalloc( &I.h_desc, sizeof(svc_desc) * SVC_REQ_MAX, hipHostMallocMapped ) );
@@ -1533,8 +1615,13 @@ svc_ingest_start( fd_verify_svc_t * s, svc_ingest & I ) {
   svc_device( s->dev );
   hipStream_t const st = ( s->ing_nst == 2ul && ( s->ing_take & 1ul ) ) ? s->st_ing2 : s->st_ing;
   SV_CHECK( hipEventRecord( I.ev0, st ) );
-  ulong wgs = (I.n + 15ul) / 16ul;                          /* 16 frags per workgroup per trip */
+  ulong wgs = s->gather_wave ? (I.n + 3ul) / 4ul : (I.n + 15ul) / 16ul;   /* frags per workgroup per trip: 4 / 16 */
   if( s->gather_wgs && wgs > s->gather_wgs ) wgs = s->gather_wgs;
+  if( s->gather_wave ) {
+    hipLaunchKernelGGL( k_svc_gather_wave, dim3( (unsigned)wgs ), dim3( 256 ), 0, st, I.d_desc,
+                        (u32)I.nreq, I.n, s->d_ing, s->d_ing_sz, s->d_ing_kind, s->d_ing_tso, s->d_stage,
+                        s->d_ing_ctr + (s->ing_take % SVC_ING_MAX) );
+  } else
   hipLaunchKernelGGL( k_svc_gather, dim3( (unsigned)wgs ), dim3( 256 ), sizeof(svc_desc) * I.nreq, st, I.d_desc,
                       (u32)I.nreq, I.n, s->d_ing, s->d_ing_sz, s->d_ing_kind, s->d_ing_tso, s->d_stage,
                       s->d_ing_ctr + (s->ing_take % SVC_ING_MAX) );
@@ -1694,6 +1781,11 @@ svc_ingest_main( void * arg ) {
   hipLaunchKernelGGL( k_svc_gather, dim3( 1 ), dim3( 256 ), 0, s->st_ing, s->ING[0].d_desc, 0u, 0ul, s->d_ing, s->d_ing_sz,
                       s->d_ing_kind, s->d_ing_tso, s->d_stage, (u32 *)0 );
   SV_CHECK( hipGetLastError() );
+  if( s->gather_wave ) {
+    hipLaunchKernelGGL( k_svc_gather_wave, dim3( 1 ), dim3( 256 ), 0, s->st_ing, s->ING[0].d_desc, 0u, 0ul, s->d_ing,
+                        s->d_ing_sz, s->d_ing_kind, s->d_ing_tso, s->d_stage, (u32 *)0 );
+    SV_CHECK( hipGetLastError() );
+  }
   SV_CHECK( hipEventRecord( s->ING[0].ev0, s->st_ing ) );
   SV_CHECK( hipEventRecord( s->ING[0].ev1, s->st_ing ) );
   SV_CHECK( hipStreamSynchronize( s->st_ing ) );
