@@ -2048,9 +2048,15 @@ fd_verify_svc_occupancy( fd_verify_svc_t const * s, ulong out[6] ) {
 static void
 svc_drain( hipStream_t st, hipEvent_t ev, char const * what, ulong idx, fd_verify_svc_t const * s ) {
   int own = 0;
+  /* each stage is named before its first HIP call: with CU-masked verify
+     streams (FD_VERIFY_SVC_FREE_CUS) teardown hung with nothing said after
+     "teardown" (profiles/r06/teardown) */
+  if( getenv( "FD_VERIFY_SVC_TEARDOWN_LOG" ) ) fprintf( stderr, "fd_verify_svc: teardown: %s %lu\n", what, idx );
   if( !ev ) {
     SV_CHECK( hipEventCreateWithFlags( &ev, hipEventDisableTiming ) );
+    if( getenv( "FD_VERIFY_SVC_TEARDOWN_LOG" ) ) fprintf( stderr, "fd_verify_svc: teardown: %s %lu: event created\n", what, idx );
     SV_CHECK( hipEventRecord( ev, st ) );
+    if( getenv( "FD_VERIFY_SVC_TEARDOWN_LOG" ) ) fprintf( stderr, "fd_verify_svc: teardown: %s %lu: event recorded\n", what, idx );
     own = 1;
   }
   long const t0 = svc_now_ns();
@@ -2086,8 +2092,11 @@ svc_drain( hipStream_t st, hipEvent_t ev, char const * what, ulong idx, fd_verif
 extern "C" void
 fd_verify_svc_delete( fd_verify_svc_t * s ) {
   if( !s ) return;
-  (void)hipSetDevice( s->dev );
-  svc_cur_dev = s->dev;
+  /* no HIP call before the ingest thread has stopped: a call that takes a
+     runtime lock the thread holds inside a blocked HIP call would hang here
+     with nothing said (profiles/r06/teardown: with CU-masked verify streams
+     nothing came after "teardown" for 60 s) */
+  if( getenv( "FD_VERIFY_SVC_TEARDOWN_LOG" ) ) fprintf( stderr, "fd_verify_svc: teardown: begin (ingest thread %d)\n", s->ithread );
   if( s->ithread ) {                          /* no new gathers from here on (the stream drains below) */
     __atomic_store_n( &s->istop, 1, __ATOMIC_RELEASE );
     /* a thread held inside a HIP call would hold pthread_join silently: the
@@ -2108,6 +2117,7 @@ fd_verify_svc_delete( fd_verify_svc_t * s ) {
     (void)pthread_join( s->ith, 0 );
     s->ithread = 0;
   }
+  svc_device( s->dev );                       /* the service thread's device (set by its polls already) */
   if( s->io && s->running ) {
     __atomic_store_n( &((svc_io_hctl *)s->h_ctl)->stop, 1ul, __ATOMIC_SEQ_CST );
     svc_drain( s->st_ing, s->io_ev, "the IO engine (k_svc_io)", 0ul, s );
@@ -2118,7 +2128,12 @@ fd_verify_svc_delete( fd_verify_svc_t * s ) {
   if( s->flush_batch ) svc_drain( s->st_flush, 0, "flush stream", 0ul, s );
   if( s->st_ing && !s->io ) svc_drain( s->st_ing, 0, "ingest stream", 0ul, s );
   if( s->st_ing2 ) svc_drain( s->st_ing2, 0, "ingest stream", 1ul, s );
-  (void)hipDeviceSynchronize();
+  /* the null stream (the runtime's memsets) the same way, not
+     hipDeviceSynchronize: with a CU-masked stream in the process
+     (FD_VERIFY_SVC_FREE_CUS) hipDeviceSynchronize never returned although
+     every stream above had drained -- the r05m and r06o shutdown hangs
+     (profiles/r06/teardown) */
+  svc_drain( 0, 0, "null stream", 0ul, s );
   for( ulong k = 0; k < SVC_LAUNCH_MAX; k++ ) launch_free( s->L[k] );
   for( ulong t = 0; t < FD_VERIFY_SVC_TILE_MAX; t++ ) {
     svc_tile & T = s->tile[t];
