@@ -574,8 +574,10 @@ def run_tile_leg(args):
     src/app/fdctl/topology.c:173) on an mcache of the reference's default
     depth (16384, default.toml:1153), the rate bisected between the
     flow-controlled rate of the same shape and 2 M frags/s
-    (tools/svc_link_sweep.py: drop_free_search); value = the signatures per
-    second that run verified, with its tspub - tsorig p50/p99 and the frags
+    (tools/svc_link_sweep.py: drop_free_search), each probed rate judged
+    by the majority of up to 3 runs (judge_rate: one run's collapse does not
+    decide a step; every run is listed in tried); value = the signatures per
+    second of a drop-free run at the highest passing rate, with its tspub - tsorig p50/p99 and the frags
     lost at 1.2x.  The frags are prelaid in the dcache (one producer core's
     copy caps near 15-20 M frags/s); the mcache still laps a slow tile.  Both
     request forms are searched: range (the tile posts mcache ranges, the GPU
@@ -638,7 +640,8 @@ def run_tile_leg(args):
             for form, extra in (("range", {}), ("polled", {"SVC_RUN_POLLED": "1"})):
                 env = dict(paced_env, **extra)
                 fc = run(DEPTH, env)                       # flow-controlled: the shape's own rate
-                best, tried = SL.drop_free_search(lambda rate: run(DEPTH, env, rate), fc["frags_per_s"], 2e6, 4)
+                best, tried = SL.drop_free_search(lambda rate: run(DEPTH, env, rate), fc["frags_per_s"], 2e6, 4,
+                                                  votes=3)
                 over = run(DEPTH, env, 1.2 * best["offered_rate"]) if best else None
                 forms[form] = {"flow_controlled_frags_per_s": fc["frags_per_s"],
                                "drop_free": lat(best) if best else None,

@@ -7,12 +7,15 @@
    (oracle_verify, fd_ed25519_oracle.c).  The checker for
    fd_precompile_hip_ed25519_verify_dev (include/fd_replay_hip.h).
 
-   Pinning: the reference's precompile cannot be built here (it needs the
-   flamenco runtime: fd_exec_instr_ctx_t, banks, the secp256k1/r1 backends),
-   and the reference holds no fixtures for it, so this file is pinned only
-   through oracle_verify (itself pinned by Wycheproof, CCTV and the
-   reference's own builds) plus the hand-derived cases of
-   tests/test_precompile_oracle.py.  The offset / size rules below are
+   Pinning (round 6): the reference's fd_precompiles.c compiles here from
+   the file where it lies (headers only; the secp256k1/r1 verifiers it also
+   holds are never referenced and are garbage-collected), and
+   oracle/ref_precompile_drv.c drives its fd_precompile_ed25519_verify
+   through a minimal instruction context (_ref/libfdref_precompile.so).
+   tests/test_precompile_ref.py checks this restatement against it, return
+   value and custom error, on boundary offsets, random blocks and mutated
+   instructions, and against the committed reference answers
+   (tests/golden/precompile_ref.npz).  The offset / size rules below are
    restated line by line from the reference's source text. */
 
 #include "fd_ed25519_oracle.h"

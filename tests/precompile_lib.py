@@ -9,6 +9,7 @@ sig_instr_idx, pubkey_offset, pubkey_instr_idx, msg_offset, msg_data_sz,
 msg_instr_idx.  Index 0xFFFF names the instruction itself.
 """
 import ctypes
+import os
 import struct
 
 import numpy as np
@@ -160,4 +161,51 @@ def oracle_many(pool, desc, tab):
     olib().oracle_precompile_ed25519_verify_many(n, pool.ctypes.data, doff.ctypes.data, dsz.ctypes.data,
                                                  icnt.ctypes.data, ibase.ctypes.data, toff.ctypes.data,
                                                  tsz.ctypes.data, err.ctypes.data, ce.ctypes.data)
+    return err, ce
+
+
+_rlib = None
+
+
+def ref_path():
+    return os.path.join(O.ORACLE_DIR, "_ref", "libfdref_precompile.so")
+
+
+def rlib():
+    """The reference's own fd_precompile_ed25519_verify (fd_precompiles.c:120-222),
+    compiled from its source by oracle/Makefile behind ref_precompile_drv.c."""
+    global _rlib
+    if _rlib is None:
+        c = ctypes
+        L = c.CDLL(ref_path())
+        L.ref_precompile_ed25519_verify.restype = c.c_int
+        L.ref_precompile_ed25519_verify.argtypes = [c.c_char_p, c.c_ulong, c.c_void_p, c.c_void_p, c.c_ulong,
+                                                    c.POINTER(c.c_uint32)]
+        _rlib = L
+    return _rlib
+
+
+def ref_verify(data, instrs):
+    """(err, custom_err) from the reference itself, same arguments as oracle_verify."""
+    bufs = [ctypes.create_string_buffer(bytes(d), max(len(d), 1)) for d in instrs]
+    ptrs = (ctypes.c_void_p * max(len(bufs), 1))(*[ctypes.addressof(b) for b in bufs])
+    szs = (ctypes.c_ulong * max(len(bufs), 1))(*[len(d) for d in instrs])
+    cur = ctypes.create_string_buffer(bytes(data), max(len(data), 1))
+    ce = ctypes.c_uint32(0)
+    err = rlib().ref_precompile_ed25519_verify(ctypes.cast(cur, ctypes.c_char_p), len(data), ptrs, szs,
+                                               len(instrs), ctypes.byref(ce))
+    assert err != -1000, "driver refused the instruction (size or count past the context's arrays)"
+    return err, ce.value
+
+
+def ref_many(pool, desc, tab):
+    """The reference over random_block's layout: (err, custom_err) arrays."""
+    n = desc.size
+    err = np.zeros(n, np.int32)
+    ce = np.zeros(n, np.uint32)
+    for j in range(n):
+        b, k = int(desc[j]["instr_base"]), int(desc[j]["instr_cnt"])
+        instrs = [pool[int(t["data_off"]):int(t["data_off"]) + int(t["data_sz"])].tobytes() for t in tab[b:b + k]]
+        o, s = int(desc[j]["data_off"]), int(desc[j]["data_sz"])
+        err[j], ce[j] = ref_verify(pool[o:o + s].tobytes(), instrs)
     return err, ce

@@ -1,6 +1,7 @@
 """GPU: ed25519 program instructions (fd_precompile_hip_ed25519_verify_dev)
 against the oracle's restatement of fd_precompile_ed25519_verify
-(oracle/fd_precompile_oracle.c; fd_precompiles.c:76-211), bit-exact in both
+(oracle/fd_precompile_oracle.c; fd_precompiles.c:76-211) and against the
+reference itself (compiled from its source, tests/test_precompile_ref.py), bit-exact in both
 the return value and the custom error, on a synthetic block holding every
 outcome class."""
 import numpy as np
@@ -54,3 +55,22 @@ def test_batch_larger_than_max_instr_raises(verifier):
     with pytest.raises(ValueError):
         pv.ed25519_verify_dev(5, z, z, z, z, z)
     pv.close()
+
+
+def test_reference_fixture(verifier):
+    """The GPU path against the reference's own fd_precompile_ed25519_verify
+    (fd_precompiles.c:120-222, compiled from its source), through the committed
+    answers of tests/golden/gen_precompile_ref.py; and against the compiled
+    reference directly when oracle/_ref travelled with the tree."""
+    import os
+    g = np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "precompile_ref.npz"))
+    pool, desc, tab = g["pool"], g["desc"].view(P.PC_DESC).reshape(-1), g["tab"].view(P.PC_INSTR).reshape(-1)
+    err, ce = _run(verifier, pool, desc, tab)
+    bad = np.nonzero((err != g["err"]) | (ce != g["custom_err"]))[0]
+    assert bad.size == 0, [(int(j), int(err[j]), int(ce[j]), int(g["err"][j]), int(g["custom_err"][j]))
+                           for j in bad[:10]]
+    if os.path.exists(P.ref_path()):
+        pool, desc, tab = P.random_block(31337, 1500)
+        err, ce = _run(verifier, pool, desc, tab)
+        rerr, rce = P.ref_many(pool, desc, tab)
+        assert np.array_equal(err, rerr) and np.array_equal(ce, rce)

@@ -1,10 +1,9 @@
 """CPU: the oracle's restatement of fd_precompile_ed25519_verify
 (oracle/fd_precompile_oracle.c) on cases whose outcome follows directly from
 the reference's source text (src/flamenco/runtime/program/fd_precompiles.c:
-76-107 fetch rules, 114-211 instruction rules).  The reference's precompile
-cannot be built here and it holds no fixtures for it: this restatement is
-"parity unpinned" beyond these cases and its signature verify (the pinned
-oracle_verify)."""
+76-107 fetch rules, 114-211 instruction rules).  The same restatement is
+pinned to the reference's own precompile, compiled from its source, in
+tests/test_precompile_ref.py."""
 import struct
 
 import numpy as np
