@@ -93,6 +93,7 @@ def main():
     ap.add_argument("--svc-env", default="", help="KEY=VAL,... for the GPU tile only")
     ap.add_argument("--pin", default="auto")
     ap.add_argument("--timeout", type=float, default=120)
+    ap.add_argument("--votes", type=int, default=3, help="runs per probed rate, majority decides (judge_rate)")
     ap.add_argument("--mock", action="store_true", help="the CPU stand-in for the GPU tile (oracle/_ref/svc_mock)")
     ap.add_argument("--logdir", default=os.path.join(SB.REPO, "gpurun_out", "svc_link_sweep_logs"))
     args = ap.parse_args()
@@ -132,7 +133,8 @@ def main():
         print(f"stream: {s.n} frags, {time.time() - t:.1f} s", file=sys.stderr, flush=True)
         for depth in (int(x) for x in args.depths.split(",")):
             fc = run(stream, depth, 0)                       # flow-controlled: the stage's own rate
-            best, _ = drop_free_search(lambda rate: run(stream, depth, rate), fc["frags_per_s"], args.lo, args.steps)
+            best, _ = drop_free_search(lambda rate: run(stream, depth, rate), fc["frags_per_s"], args.lo, args.steps,
+                                       votes=args.votes)
             if best is None:
                 best = run(stream, depth, args.lo)
             over = run(stream, depth, 1.2 * best["offered_rate"])
