@@ -601,7 +601,9 @@ def run_tile_leg(args):
         import tile_bench as TB
         if not (os.path.exists(SB.EXE) and os.path.exists(SB.SVC)):
             return {"value": None, "error": "integration/_build/svc_tile_run or svc_run missing (build() with /root/reference)"}
-        tiles = int(os.environ.get("FD_BENCH_TILE_TILES", "3"))
+        # the reference's default verify_tile_count (default.toml:776); FD_BENCH_TILE_TILES=3 is round 6's
+        # earlier shape (profiles/r06/final)
+        tiles = int(os.environ.get("FD_BENCH_TILE_TILES", "6"))
         DEPTH = 16384
         # request slots for a shallow link: many small ranges
         paced_env = {"SVC_RUN_PRELAY": "1", "SVC_RUN_REQ_DEPTH": os.environ.get("FD_BENCH_TILE_REQ_DEPTH", "128"),
@@ -652,7 +654,12 @@ def run_tile_leg(args):
             hd = forms[head]["drop_free"] if head else None
             # parity against the reference's code, per tile (flow-controlled, every frag digested)
             depth_all = 1 << (s.n - 1).bit_length()
-            pre = {"SVC_RUN_PRELAY": "1"}
+            # deep-link shape: 32768-frag slots, as many as the service's 4 GiB staging holds (16 at 3 tiles,
+            # 8 at 6: fd_verify_svc_boot_ok, 2176 B of staging per frag)
+            req_deep = 16
+            while tiles * req_deep * 32768 * 2176 >= 1 << 32:
+                req_deep //= 2
+            pre = {"SVC_RUN_PRELAY": "1", "SVC_RUN_REQ_DEPTH": str(req_deep), "SVC_RUN_SLOT_CAP": "32768"}
             d = run(depth_all, dict(pre, SVC_RUN_DIGEST="1"))
             ref = SI.ref_share_digests(s.pool, s.off, s.sz, None, tiles, 0x7f4a11, 4194302, threads=16)
             got = [SI.tile_counts(x) for x in d["tiles"]]
@@ -671,6 +678,7 @@ def run_tile_leg(args):
                 "prelaid": {"value": wmed["verifies_per_s"], "frags_per_s": wmed["frags_per_s"], "in_depth": depth_all,
                             "windows": [round(x["verifies_per_s"], 1) for x in wins],
                             "overrun": sum(x["overrun"] + x["lapped"] for x in wins),
+                            "req_depth": req_deep, "slot_cap": 32768,
                             "what": "flow-controlled, a link that holds the whole stream (round 5's headline)"},
                 "svc": wmed["svc"], "regime": wmed["regime"],
                 "tile_process": {"threads_max": wmed["tile_threads_max"], "dev_fds": wmed["tile_dev_fds"]},
