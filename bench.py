@@ -58,10 +58,10 @@ N_M_DECODE, N_S_DECODE = 42.0, 510.0
 PEAK_OPS = 256 * 4 * 32 * 2.4e9          # 78.6e12 int32 lane-ops/s (32-wide SIMDs)
 SIMDS, MAX_CLOCK = 256 * 4, 2.4e9         # MI355X_MICROARCH.md: 256 CU x 4 SIMD, 2400 MHz max clock
 PEAK_SLOTS = SIMDS * MAX_CLOCK / 4        # VALU issue slots/s: one quad-cycle per SIMD at the max clock
-PMC_SUMMARY = "r04p_pmc_summary.json"    # rocprofv3 PMC passes of this kernel build (tools/run_profile.sh)
-ISSUE_SUMMARY = "r04p_valu_issue_calibration.json"   # VALU issue-slot pass of this build (tools/run_valu_calib.sh)
-ISSUE_SUMMARY_C4 = "r04p_c4_valu_issue.json"          # the same pass over C4's timing-leg batch (tools/run_c4_issue.sh)
-PMC_SUMMARY_C4 = "r05s_c4_pmc_summary.json"            # FETCH/WRITE passes over the C4 bench (tools/txnm_pmc_summary.py)
+PMC_SUMMARY = "r06af_pmc_summary.json"   # rocprofv3 PMC passes of this kernel build (tools/run_profile.sh)
+ISSUE_SUMMARY = "r06af_valu_issue_calibration.json"   # VALU issue-slot pass of this build (tools/run_valu_calib.sh)
+ISSUE_SUMMARY_C4 = "r06af_c4_valu_issue.json"         # the same pass over C4's timing-leg batch (tools/run_c4_issue.sh)
+PMC_SUMMARY_C4 = "r06af_c4_pmc_summary.json"           # FETCH/WRITE passes over the C4 bench (tools/txnm_pmc_summary.py)
 
 
 def w_total(msg_sz):

@@ -13,6 +13,6 @@ timeout -s KILL 120 rocprofv3 --pmc $G --kernel-trace --output-format csv -d $O/
     $R/tools/valu_rates2 > $O/micro.out 2> $O/micro.err
 rc=$?; echo "micro rc=$rc"; [ $rc -ne 0 ] && { tail -5 $O/micro.err; exit $rc; }
 timeout -s KILL 240 rocprofv3 --pmc $G --kernel-trace --output-format csv -d $O/engine -o run -- \
-    python3 bench.py --contexts 1 --no-c4 --no-cpu-baseline --steps 2 --warmup 1 > $O/engine.out 2> $O/engine.err
+    python3 bench.py --contexts 1 --no-c4 --no-tile --no-cpu-baseline --steps 2 --warmup 1 > $O/engine.out 2> $O/engine.err
 rc=$?; echo "engine rc=$rc"; [ $rc -ne 0 ] && { tail -5 $O/engine.err; exit $rc; }
 exit 0
